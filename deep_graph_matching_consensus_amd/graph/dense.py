@@ -1,0 +1,60 @@
+"""Packed ``[sum N, C]`` <-> padded ``[B, N_max, C]`` conversions.
+
+Replaces PyG's ``to_dense_batch`` (``/root/reference/dgmc/models/dgmc.py:4,
+154-155``) and the boolean-mask ``to_sparse``/``to_dense`` helpers
+(``dgmc.py:22-29``).  The reference versions index with boolean masks, which
+forces a device->host sync (``nonzero``) on *every* call - ten times per
+consensus step.  Here the flat dense index of every node is computed once on
+the host from :class:`~.meta.BatchInfo` and cached on the device, so packing
+and unpacking are single gather/scatter kernels with no synchronisation.
+"""
+import torch
+
+from .meta import batch_info
+
+
+class DenseLayout(object):
+    """Mapping between packed node rows and a padded ``[B, N_max]`` grid."""
+
+    def __init__(self, info, device, max_nodes=None):
+        self.info = info
+        self.B = info.num_graphs
+        self.N = info.max_nodes if max_nodes is None else max_nodes
+        self.device = device
+        self.index = info.dense_index(device, self.N)        # [sum N] int64
+        self.counts = info.device_tensor('counts', device, torch.int32)
+        self.num_nodes = info.num_nodes
+        self._mask = None
+
+    @property
+    def mask(self):
+        """``[B, N_max]`` bool validity mask."""
+        if self._mask is None:
+            m = torch.zeros(self.B * self.N, dtype=torch.bool,
+                            device=self.device)
+            m[self.index] = True
+            self._mask = m.view(self.B, self.N)
+        return self._mask
+
+    def to_dense(self, x, fill_value=0.):
+        """``[sum N, *]`` -> ``[B, N_max, *]`` (padding = ``fill_value``)."""
+        feat = x.shape[1:]
+        out = x.new_full((self.B * self.N, ) + tuple(feat), fill_value)
+        out = out.index_copy(0, self.index, x)
+        return out.view((self.B, self.N) + tuple(feat))
+
+    def to_sparse(self, x):
+        """``[B, N_max, *]`` -> ``[sum N, *]``."""
+        feat = x.shape[2:]
+        return x.reshape((self.B * self.N, ) + tuple(feat)).index_select(
+            0, self.index)
+
+
+def dense_layout(batch, num_nodes, device, max_nodes=None):
+    return DenseLayout(batch_info(batch, num_nodes), device, max_nodes)
+
+
+def to_dense_batch(x, batch=None, fill_value=0.):
+    r"""Drop-in for PyG's ``to_dense_batch``: returns ``(dense, mask)``."""
+    layout = dense_layout(batch, x.size(0), x.device)
+    return layout.to_dense(x, fill_value), layout.mask

@@ -1,0 +1,49 @@
+"""Shared skeleton of the stacked GNN encoders (GIN, SplineCNN, RelCNN).
+
+All three reference encoders (``/root/reference/dgmc/models/gin.py``,
+``spline.py``, ``rel.py``) share the same output rule
+(``gin.py:25-34``): features of all layers are optionally concatenated
+(``cat``, including the input) and optionally projected by a final
+``Linear`` (``lin``)::
+
+    out_channels = out            if lin
+                 = in + L * out   if cat and not lin
+                 = out            otherwise
+
+``pair_fusable`` tells :class:`~..models.dgmc.DGMC` that encoding the source
+and target graphs in ONE call on their disjoint union gives the same result as
+two calls (true unless BatchNorm runs in training mode), which halves the
+kernel launches and doubles GEMM sizes on the hot path.
+"""
+import torch
+from torch.nn import Linear
+
+
+class StackedEncoder(torch.nn.Module):
+    def _init_head(self, in_channels, out_channels, num_layers, cat, lin):
+        self.in_channels = in_channels
+        self.num_layers = num_layers
+        self.cat = cat
+        self.lin = lin
+        width = in_channels + num_layers * out_channels if cat \
+            else out_channels
+        if lin:
+            self.out_channels = out_channels
+            self.final = Linear(width, out_channels)
+        else:
+            self.out_channels = width
+
+    def _head(self, xs):
+        x = torch.cat(xs, dim=-1) if self.cat else xs[-1]
+        return x
+
+    def _project(self, x):
+        return self.final(x) if self.lin else x
+
+    @property
+    def pair_fusable(self):
+        for m in self.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and \
+                    m.training and getattr(self, 'batch_norm', False):
+                return False
+        return True

@@ -1,0 +1,85 @@
+"""Relational encoder (API of ``/root/reference/dgmc/models/rel.py``).
+
+``RelConv`` (``rel.py:7-38``) computes
+``root(x) + mean_{j->i} lin1(x)_j + mean_{i->j} lin2(x)_j`` by running
+message passing twice with a mutated ``flow``.  Here the three linear maps are
+stacked into ONE GEMM (``x @ [lin1 | lin2 | root]^T``) and both aggregation
+directions plus the root term are a single sparse operator
+(:func:`~..ops.plans.relational_plan`) evaluated by one gather-reduce kernel
+(ReLU fused when the encoder has no BatchNorm).  Checkpoint keys are kept
+(``lin1.weight``, ``lin2.weight``, ``root.weight``, ``root.bias``).
+"""
+import torch
+import torch.nn.functional as F
+from torch.nn import BatchNorm1d, Linear, ModuleList
+
+from ..ops.plans import relational_plan
+from ..ops.sparse import spmm
+from .encoder import StackedEncoder
+
+
+class RelConv(torch.nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super(RelConv, self).__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.lin1 = Linear(in_channels, out_channels, bias=False)
+        self.lin2 = Linear(in_channels, out_channels, bias=False)
+        self.root = Linear(in_channels, out_channels)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for lin in (self.lin1, self.lin2, self.root):
+            lin.reset_parameters()
+
+    def forward(self, x, edge_index, act=None):
+        weight = torch.cat(
+            [self.lin1.weight, self.lin2.weight, self.root.weight], dim=0)
+        bias = torch.cat([self.root.bias.new_zeros(2 * self.out_channels),
+                          self.root.bias])
+        y = F.linear(x, weight, bias).view(-1, self.out_channels)
+        plan = relational_plan(edge_index, x.size(0))
+        return spmm(plan, y, relu=(act == 'relu'))
+
+    def __repr__(self):
+        return '{}({}, {})'.format(type(self).__name__, self.in_channels,
+                                   self.out_channels)
+
+
+class RelCNN(StackedEncoder):
+    def __init__(self, in_channels, out_channels, num_layers,
+                 batch_norm=False, cat=True, lin=True, dropout=0.0):
+        super(RelCNN, self).__init__()
+        self.batch_norm = batch_norm
+        self.dropout = dropout
+        widths = [in_channels] + [out_channels] * num_layers
+        self.convs = ModuleList(
+            [RelConv(a, out_channels) for a in widths[:-1]])
+        self.batch_norms = ModuleList(
+            [BatchNorm1d(out_channels) for _ in range(num_layers)])
+        self._init_head(in_channels, out_channels, num_layers, cat, lin)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for conv, bn in zip(self.convs, self.batch_norms):
+            conv.reset_parameters()
+            bn.reset_parameters()
+        if self.lin:
+            self.final.reset_parameters()
+
+    def forward(self, x, edge_index, *args):
+        xs = [x]
+        for conv, bn in zip(self.convs, self.batch_norms):
+            if self.batch_norm:
+                h = bn(F.relu(conv(xs[-1], edge_index)))
+            else:
+                h = conv(xs[-1], edge_index, act='relu')
+            xs.append(F.dropout(h, p=self.dropout, training=self.training))
+        return self._project(self._head(xs))
+
+    def __repr__(self):
+        return ('{}({}, {}, num_layers={}, batch_norm={}, cat={}, lin={}, '
+                'dropout={})').format(type(self).__name__, self.in_channels,
+                                      self.out_channels, self.num_layers,
+                                      self.batch_norm, self.cat, self.lin,
+                                      self.dropout)

@@ -1,0 +1,47 @@
+"""SplineCNN encoder (API of ``/root/reference/dgmc/models/spline.py``).
+
+``num_layers`` x ``SplineConv(kernel_size=5)`` each followed by ReLU (fused
+into the aggregation kernel's epilogue here), optional concatenation,
+dropout applied ONCE to the (concatenated) features (``spline.py:52``), then
+the optional final ``Linear``.
+"""
+import torch.nn.functional as F
+from torch.nn import ModuleList
+
+from ..nn.conv import SplineConv
+from .encoder import StackedEncoder
+
+
+class SplineCNN(StackedEncoder):
+    def __init__(self, in_channels, out_channels, dim, num_layers, cat=True,
+                 lin=True, dropout=0.0):
+        super(SplineCNN, self).__init__()
+        self.dim = dim
+        self.dropout = dropout
+        widths = [in_channels] + [out_channels] * num_layers
+        self.convs = ModuleList([
+            SplineConv(a, out_channels, dim, kernel_size=5)
+            for a in widths[:-1]
+        ])
+        self._init_head(in_channels, out_channels, num_layers, cat, lin)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        for conv in self.convs:
+            conv.reset_parameters()
+        if self.lin:
+            self.final.reset_parameters()
+
+    def forward(self, x, edge_index, edge_attr, *args):
+        xs = [x]
+        for conv in self.convs:
+            xs.append(conv(xs[-1], edge_index, edge_attr, act='relu'))
+        h = F.dropout(self._head(xs), p=self.dropout, training=self.training)
+        return self._project(h)
+
+    def __repr__(self):
+        return ('{}({}, {}, dim={}, num_layers={}, cat={}, lin={}, '
+                'dropout={})').format(type(self).__name__, self.in_channels,
+                                      self.out_channels, self.dim,
+                                      self.num_layers, self.cat, self.lin,
+                                      self.dropout)
