@@ -1,0 +1,128 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// * wave64 reductions via __shfl_xor (CDNA wavefront = 64 lanes);
+// * bf16/f16/f32 <-> f32 vector load helpers (16-byte per lane loads);
+// * bijective XCD-aware block remap: consecutive *logical* blocks land on the
+//   same XCD so neighbouring rows (nodes of one graph) share that XCD's L2.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#define DGMC_CHECK_HIP(expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    TORCH_CHECK(_e == hipSuccess, "HIP error: ", hipGetErrorString(_e));       \
+  } while (0)
+
+#define DGMC_CHECK_LAUNCH() DGMC_CHECK_HIP(hipGetLastError())
+
+namespace dgmc {
+
+constexpr int kWave = 64;
+constexpr int kNumXcd = 8;
+
+inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+// Bijective remap of a linear block id so that blocks b and b+1 share an XCD
+// (hardware dispatches block ids round-robin over the 8 XCDs).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  if (nblocks <= kNumXcd) return bid;
+  const int q = nblocks / kNumXcd, r = nblocks % kNumXcd;
+  const int xcd = bid % kNumXcd, slot = bid / kNumXcd;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + slot;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Scalar conversions
+// ---------------------------------------------------------------------------
+template <typename T> struct Cvt;
+template <> struct Cvt<float> {
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+};
+template <> struct Cvt<__hip_bfloat16> {
+  __device__ __forceinline__ static float to_f(__hip_bfloat16 v) {
+    return __bfloat162float(v);
+  }
+  __device__ __forceinline__ static __hip_bfloat16 from_f(float v) {
+    return __float2bfloat16(v);
+  }
+};
+template <> struct Cvt<__half> {
+  __device__ __forceinline__ static float to_f(__half v) {
+    return __half2float(v);
+  }
+  __device__ __forceinline__ static __half from_f(float v) {
+    return __float2half(v);
+  }
+};
+
+// Elements per 16-byte vector access.
+template <typename T> struct Vec16 {
+  static constexpr int N = 16 / sizeof(T);
+};
+
+// Load N consecutive elements (16-byte aligned) into floats.
+template <typename T, int N>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, float* out) {
+  static_assert(N * sizeof(T) == 16 || N == 1, "vector width");
+  if constexpr (N == 1) {
+    out[0] = Cvt<T>::to_f(p[0]);
+  } else {
+    const uint4 raw = *reinterpret_cast<const uint4*>(p);
+    const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = Cvt<T>::to_f(e[k]);
+  }
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
+  static_assert(N * sizeof(T) == 16 || N == 1, "vector width");
+  if constexpr (N == 1) {
+    p[0] = Cvt<T>::from_f(v[0]);
+  } else {
+    uint4 raw;
+    T* e = reinterpret_cast<T*>(&raw);
+#pragma unroll
+    for (int k = 0; k < N; ++k) e[k] = Cvt<T>::from_f(v[k]);
+    *reinterpret_cast<uint4*>(p) = raw;
+  }
+}
+
+inline bool aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+}  // namespace dgmc
+
+// Dispatch over the floating types our kernels accept (f32, bf16, f16).
+#define DGMC_DISPATCH_FLOAT(ST, T, ...)                                        \
+  [&] {                                                                        \
+    switch (ST) {                                                              \
+      case at::kFloat: { using T = float; return __VA_ARGS__(); }              \
+      case at::kBFloat16: { using T = __hip_bfloat16; return __VA_ARGS__(); }  \
+      case at::kHalf: { using T = __half; return __VA_ARGS__(); }              \
+      default: TORCH_CHECK(false, "dgmc_amd: unsupported dtype ", ST);         \
+    }                                                                          \
+  }()

@@ -1,0 +1,83 @@
+// Operator schemas + CUDA(=HIP)-key registrations for the gfx950 kernels.
+// Loaded from Python with torch.ops.load_library (no pybind module), so the
+// ops are visible to the dispatcher, the profiler and hipGraph capture.
+#include <ATen/ATen.h>
+#include <torch/library.h>
+
+namespace dgmc {
+
+at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
+                    const at::Tensor& val, const at::Tensor& x,
+                    const c10::optional<at::Tensor>& self_x,
+                    const c10::optional<at::Tensor>& self_scale,
+                    const c10::optional<at::Tensor>& bias, bool relu,
+                    bool out_fp32);
+
+std::tuple<at::Tensor, at::Tensor> spline_basis(const at::Tensor& pseudo,
+                                                const at::Tensor& kernel_size,
+                                                const at::Tensor& is_open,
+                                                int64_t degree);
+
+at::Tensor dense_masked_softmax(const at::Tensor& S_hat, const at::Tensor& n_s,
+                                const at::Tensor& n_t);
+at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
+                                    const at::Tensor& n_s,
+                                    const at::Tensor& n_t);
+std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
+    const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& n_s,
+    const at::Tensor& n_t);
+at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
+                                       const at::Tensor& r_s,
+                                       const at::Tensor& g,
+                                       const at::Tensor& n_s,
+                                       const at::Tensor& n_t);
+at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
+                           const at::Tensor& Q, const at::Tensor& w2,
+                           const at::Tensor& b2, const at::Tensor& n_s,
+                           const at::Tensor& n_t);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
+    const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
+    const at::Tensor& w2, const at::Tensor& n_s, const at::Tensor& n_t);
+
+at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
+
+}  // namespace dgmc
+
+TORCH_LIBRARY(dgmc_amd, m) {
+  m.def(
+      "spmm_csr(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
+      "self_x, Tensor? self_scale, Tensor? bias, bool relu, bool out_fp32) -> "
+      "Tensor");
+  m.def(
+      "spline_basis(Tensor pseudo, Tensor kernel_size, Tensor is_open, int "
+      "degree) -> (Tensor, Tensor)");
+  m.def("dense_masked_softmax(Tensor S_hat, Tensor n_s, Tensor n_t) -> Tensor");
+  m.def(
+      "dense_masked_softmax_bwd(Tensor S, Tensor grad, Tensor n_s, Tensor n_t) "
+      "-> Tensor");
+  m.def(
+      "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor n_s, Tensor "
+      "n_t) -> (Tensor, Tensor)");
+  m.def(
+      "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
+      "n_s, Tensor n_t) -> Tensor");
+  m.def(
+      "dense_consensus(Tensor S_hat, Tensor P, Tensor Q, Tensor w2, Tensor b2, "
+      "Tensor n_s, Tensor n_t) -> Tensor");
+  m.def(
+      "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor w2, Tensor "
+      "n_s, Tensor n_t) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
+  m.impl("spmm_csr", &dgmc::spmm_csr);
+  m.impl("spline_basis", &dgmc::spline_basis);
+  m.impl("dense_masked_softmax", &dgmc::dense_masked_softmax);
+  m.impl("dense_masked_softmax_bwd", &dgmc::dense_masked_softmax_bwd);
+  m.impl("dense_softmax_transport", &dgmc::dense_softmax_transport);
+  m.impl("dense_softmax_transport_bwd", &dgmc::dense_softmax_transport_bwd);
+  m.impl("dense_consensus", &dgmc::dense_consensus);
+  m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
+  m.impl("topk_dot", &dgmc::topk_dot);
+}

@@ -1,0 +1,149 @@
+// Host-side pair collation (native data loader core).
+//
+// The reference collates graph pairs in Python (PyG Batch.from_data_list with
+// the PairData.__inc__ rule, /root/reference/dgmc/utils/data.py:9-16, and
+// follow_batch=['x_s', 'x_t'] in examples/pascal.py:42-43).  For the
+// MI355X pipeline the whole synthetic dataset stays resident in HBM; per step
+// the host only decides WHICH graphs form the batch and emits compact int64
+// index arrays (node/edge gather lists, offset edge_index, batch vectors,
+// per-graph counts, ground truth).  The device then gathers features with a
+// handful of index_select kernels.  OpenMP parallelises over pairs.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace dgmc_host {
+
+using at::Tensor;
+
+static void check_cpu_long(const Tensor& t, const char* name) {
+  TORCH_CHECK(!t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous(),
+              name, " must be a contiguous int64 CPU tensor");
+}
+
+// Returns (node_idx_s, node_idx_t, edge_idx_s, edge_idx_t, edge_index_s,
+//          edge_index_t, batch_s, batch_t, counts_s, counts_t, y)
+std::vector<Tensor> collate_pairs(const Tensor& node_ptr, const Tensor& edge_ptr,
+                                  const Tensor& edge_local,
+                                  const Tensor& node_class,
+                                  const Tensor& pos_of_class,
+                                  const Tensor& s_ids, const Tensor& t_ids) {
+  check_cpu_long(node_ptr, "node_ptr");
+  check_cpu_long(edge_ptr, "edge_ptr");
+  check_cpu_long(edge_local, "edge_local");
+  check_cpu_long(node_class, "node_class");
+  check_cpu_long(pos_of_class, "pos_of_class");
+  check_cpu_long(s_ids, "s_ids");
+  check_cpu_long(t_ids, "t_ids");
+  TORCH_CHECK(edge_local.dim() == 2 && edge_local.size(0) == 2, "edge_local");
+  const int64_t B = s_ids.numel();
+  TORCH_CHECK(t_ids.numel() == B, "s_ids / t_ids size mismatch");
+  const int64_t G = node_ptr.numel() - 1;
+  const int64_t C = pos_of_class.dim() == 2 ? pos_of_class.size(1) : 0;
+  const int64_t E_all = edge_local.size(1);
+  const int64_t* np_ = node_ptr.data_ptr<int64_t>();
+  const int64_t* ep_ = edge_ptr.data_ptr<int64_t>();
+  const int64_t* src_ = edge_local.data_ptr<int64_t>();
+  const int64_t* dst_ = src_ + E_all;
+  const int64_t* cls_ = node_class.data_ptr<int64_t>();
+  const int64_t* poc_ = pos_of_class.data_ptr<int64_t>();
+  const int64_t* sid = s_ids.data_ptr<int64_t>();
+  const int64_t* tid = t_ids.data_ptr<int64_t>();
+
+  // Exclusive scans of node / edge counts per pair (serial: B is small).
+  std::vector<int64_t> ns_off(B + 1, 0), nt_off(B + 1, 0), es_off(B + 1, 0),
+      et_off(B + 1, 0);
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t gs = sid[b], gt = tid[b];
+    TORCH_CHECK(gs >= 0 && gs < G && gt >= 0 && gt < G, "graph id out of range");
+    ns_off[b + 1] = ns_off[b] + (np_[gs + 1] - np_[gs]);
+    nt_off[b + 1] = nt_off[b] + (np_[gt + 1] - np_[gt]);
+    es_off[b + 1] = es_off[b] + (ep_[gs + 1] - ep_[gs]);
+    et_off[b + 1] = et_off[b] + (ep_[gt + 1] - ep_[gt]);
+  }
+  auto L = at::TensorOptions().dtype(at::kLong);
+  Tensor node_idx_s = at::empty({ns_off[B]}, L), node_idx_t = at::empty({nt_off[B]}, L);
+  Tensor edge_idx_s = at::empty({es_off[B]}, L), edge_idx_t = at::empty({et_off[B]}, L);
+  Tensor ei_s = at::empty({2, es_off[B]}, L), ei_t = at::empty({2, et_off[B]}, L);
+  Tensor batch_s = at::empty({ns_off[B]}, L), batch_t = at::empty({nt_off[B]}, L);
+  Tensor counts_s = at::empty({B}, L), counts_t = at::empty({B}, L);
+  Tensor y = at::empty({ns_off[B]}, L);
+  int64_t *nis = node_idx_s.data_ptr<int64_t>(), *nit = node_idx_t.data_ptr<int64_t>();
+  int64_t *eis = edge_idx_s.data_ptr<int64_t>(), *eit = edge_idx_t.data_ptr<int64_t>();
+  int64_t *eis0 = ei_s.data_ptr<int64_t>(), *eis1 = eis0 + es_off[B];
+  int64_t *eit0 = ei_t.data_ptr<int64_t>(), *eit1 = eit0 + et_off[B];
+  int64_t *bs = batch_s.data_ptr<int64_t>(), *bt = batch_t.data_ptr<int64_t>();
+  int64_t *cs = counts_s.data_ptr<int64_t>(), *ct = counts_t.data_ptr<int64_t>();
+  int64_t* yp = y.data_ptr<int64_t>();
+
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t gs = sid[b], gt = tid[b];
+    const int64_t n0s = np_[gs], nns = np_[gs + 1] - n0s;
+    const int64_t n0t = np_[gt], nnt = np_[gt + 1] - n0t;
+    cs[b] = nns;
+    ct[b] = nnt;
+    for (int64_t i = 0; i < nns; ++i) {
+      nis[ns_off[b] + i] = n0s + i;
+      bs[ns_off[b] + i] = b;
+      const int64_t c = cls_[n0s + i];
+      yp[ns_off[b] + i] = (c >= 0 && c < C) ? poc_[gt * C + c] : -1;
+    }
+    for (int64_t i = 0; i < nnt; ++i) {
+      nit[nt_off[b] + i] = n0t + i;
+      bt[nt_off[b] + i] = b;
+    }
+    const int64_t e0s = ep_[gs], nes = ep_[gs + 1] - e0s;
+    for (int64_t e = 0; e < nes; ++e) {
+      const int64_t o = es_off[b] + e;
+      eis[o] = e0s + e;
+      eis0[o] = src_[e0s + e] + ns_off[b];
+      eis1[o] = dst_[e0s + e] + ns_off[b];
+    }
+    const int64_t e0t = ep_[gt], net = ep_[gt + 1] - e0t;
+    for (int64_t e = 0; e < net; ++e) {
+      const int64_t o = et_off[b] + e;
+      eit[o] = e0t + e;
+      eit0[o] = src_[e0t + e] + nt_off[b];
+      eit1[o] = dst_[e0t + e] + nt_off[b];
+    }
+  }
+  return {node_idx_s, node_idx_t, edge_idx_s, edge_idx_t, ei_s, ei_t,
+          batch_s,    batch_t,    counts_s,   counts_t,   y};
+}
+
+// CSR (rowptr, perm) of an index vector over [0, n): stable counting sort.
+std::vector<Tensor> counting_sort(const Tensor& index, int64_t n) {
+  check_cpu_long(index, "index");
+  const int64_t m = index.numel();
+  const int64_t* ix = index.data_ptr<int64_t>();
+  Tensor rowptr = at::zeros({n + 1}, at::TensorOptions().dtype(at::kLong));
+  Tensor perm = at::empty({m}, at::TensorOptions().dtype(at::kLong));
+  int64_t* rp = rowptr.data_ptr<int64_t>();
+  for (int64_t i = 0; i < m; ++i) {
+    TORCH_CHECK(ix[i] >= 0 && ix[i] < n, "counting_sort: index out of range");
+    ++rp[ix[i] + 1];
+  }
+  for (int64_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+  std::vector<int64_t> cursor(rp, rp + n);
+  int64_t* pp = perm.data_ptr<int64_t>();
+  for (int64_t i = 0; i < m; ++i) pp[cursor[ix[i]]++] = i;
+  return {rowptr, perm};
+}
+
+}  // namespace dgmc_host
+
+TORCH_LIBRARY(dgmc_host, m) {
+  m.def(
+      "collate_pairs(Tensor node_ptr, Tensor edge_ptr, Tensor edge_local, "
+      "Tensor node_class, Tensor pos_of_class, Tensor s_ids, Tensor t_ids) -> "
+      "Tensor[]");
+  m.def("counting_sort(Tensor index, int n) -> Tensor[]");
+}
+
+TORCH_LIBRARY_IMPL(dgmc_host, CPU, m) {
+  m.impl("collate_pairs", &dgmc_host::collate_pairs);
+  m.impl("counting_sort", &dgmc_host::counting_sort);
+}

@@ -50,7 +50,41 @@ class DenseLayout(object):
             0, self.index)
 
 
+class MaskLayout(object):
+    """Reference-mode layout: sizes recovered from the device batch vector
+    (two host syncs, like PyG's ``to_dense_batch``) and boolean-mask packing
+    (``x[mask]``, one ``nonzero`` sync per call, like ``dgmc.py:22-29``)."""
+
+    def __init__(self, batch, num_nodes, device):
+        if batch is None:
+            batch = torch.zeros(num_nodes, dtype=torch.long, device=device)
+        self.B = int(batch[-1].item()) + 1 if num_nodes > 0 else 0
+        counts = torch.zeros(self.B, dtype=torch.long, device=device)
+        counts.scatter_add_(0, batch, torch.ones_like(batch))
+        self.N = int(counts.max().item()) if self.B > 0 else 0
+        self.counts = counts.to(torch.int32)
+        self.num_nodes = num_nodes
+        self.device = device
+        ar = torch.arange(self.N, device=device).view(1, -1)
+        self.mask = ar < counts.view(-1, 1)
+
+    @property
+    def index(self):
+        return self.mask.view(-1).nonzero().view(-1)
+
+    def to_dense(self, x, fill_value=0.):
+        out = x.new_full((self.B, self.N) + tuple(x.shape[1:]), fill_value)
+        out[self.mask] = x
+        return out
+
+    def to_sparse(self, x):
+        return x[self.mask]
+
+
 def dense_layout(batch, num_nodes, device, max_nodes=None):
+    from ..runtime.mode import is_reference_mode
+    if is_reference_mode():
+        return MaskLayout(batch, num_nodes, device)
     return DenseLayout(batch_info(batch, num_nodes), device, max_nodes)
 
 

@@ -18,6 +18,14 @@ import torch
 _REGISTRY = {}
 
 
+def _upload(t, device):
+    """Async H2D copy from pinned memory (never stalls the GPU queue)."""
+    device = torch.device(device)
+    if device.type == 'cuda':
+        return t.pin_memory().to(device, non_blocking=True)
+    return t.to(device)
+
+
 class BatchInfo(object):
     """Per-graph node counts of a sorted, contiguous batch vector."""
 
@@ -44,7 +52,7 @@ class BatchInfo(object):
             batch = torch.repeat_interleave(
                 torch.arange(self.num_graphs), self.counts)
             local = torch.arange(self.num_nodes) - self.ptr[:-1][batch]
-            out = (batch * n_max + local).to(device, non_blocking=True)
+            out = _upload(batch * n_max + local, device)
             self._device_cache[key] = out
         return out
 
@@ -53,7 +61,7 @@ class BatchInfo(object):
         out = self._device_cache.get(key)
         if out is None:
             src = getattr(self, name)
-            out = src.to(dtype).to(device, non_blocking=True)
+            out = _upload(src.to(dtype), device)
             self._device_cache[key] = out
         return out
 

@@ -30,6 +30,7 @@ from ..graph.dense import dense_layout
 from ..nn.inits import reset
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
+from ..runtime.mode import is_reference_mode
 
 EPS = 1e-8
 
@@ -88,6 +89,8 @@ class DGMC(torch.nn.Module):
     # ------------------------------------------------------------------
     @staticmethod
     def _fusable(psi):
+        if is_reference_mode():
+            return False
         return bool(getattr(psi, 'pair_fusable', False))
 
     def _encode(self, psi, pair, x_s, x_t, ei_s, ea_s, ei_t, ea_t):

@@ -66,6 +66,9 @@ def use_hip(*tensors):
     t = next((t for t in tensors if torch.is_tensor(t)), None)
     if t is None or not t.is_cuda:
         return False
+    from ..runtime.mode import is_reference_mode
+    if is_reference_mode():
+        return False
     if hip_available():
         return True
     if allow_fallback():

@@ -1,0 +1,89 @@
+"""Process-group setup for one-process-per-GPU training.
+
+The reference is single-process/single-device (``examples/pascal.py:45``);
+the north-star adds data parallelism across the 8 MI355X of a node.  We use
+``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm, over xGMI) for
+GPU ranks and ``gloo`` for CPU ranks (tests).  Rendezvous uses the standard
+``RANK``/``WORLD_SIZE``/``LOCAL_RANK``/``MASTER_ADDR``/``MASTER_PORT``
+environment (``torch.distributed.run``).
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return int(os.environ.get('RANK', '0'))
+
+
+def env_world_size():
+    return int(os.environ.get('WORLD_SIZE', '1'))
+
+
+def env_local_rank():
+    return int(os.environ.get('LOCAL_RANK', '0'))
+
+
+def is_distributed():
+    return dist.is_available() and dist.is_initialized()
+
+
+def rank():
+    return dist.get_rank() if is_distributed() else 0
+
+
+def world_size():
+    return dist.get_world_size() if is_distributed() else 1
+
+
+def init_distributed(backend=None, timeout_s=600):
+    """Initialise the default process group from the environment.
+
+    Returns the device this rank should use.  No-op for a single process.
+    """
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        device = torch.device('cuda', env_local_rank() %
+                              max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(device)
+    else:
+        device = torch.device('cpu')
+    if env_world_size() > 1 and not is_distributed():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        backend = backend or ('nccl' if use_cuda else 'gloo')
+        kwargs = dict(backend=backend,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == 'nccl':
+            kwargs['device_id'] = device
+        dist.init_process_group(**kwargs)
+    return device
+
+
+def barrier():
+    if is_distributed():
+        if dist.get_backend() == 'nccl':
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(value, device):
+    """Max of a Python float over ranks."""
+    if not is_distributed():
+        return value
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(tensor):
+    if is_distributed():
+        dist.all_reduce(tensor, op=dist.ReduceOp.SUM)
+    return tensor
+
+
+def shutdown():
+    if is_distributed():
+        dist.destroy_process_group()
