@@ -67,13 +67,13 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void softmax_transport_kernel(
     const float* __restrict__ S_hat, const float* __restrict__ r_s,
-    const int* __restrict__ n_s, const int* __restrict__ n_t,
+    const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     float* __restrict__ S, float* __restrict__ r_t, int Ns, int Nt, int R) {
   __shared__ float sS[kMaxN * kPitch];
   __shared__ float sR[kMaxN * kPitch];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = n_s[b], nt = n_t[b];
+  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
   const float* Sh = S_hat + (size_t)b * Ns * Nt;
   float* Sb = S + (size_t)b * Ns * Nt;
 
@@ -90,15 +90,15 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
     }
   }
 
-  const float* rs = r_s + (size_t)b * Ns * R;
-  float* rt = r_t + (size_t)b * Nt * R;
+  const float* rs = r_s + (size_t)ptr_s[b] * R;
+  float* rt = r_t + (size_t)ptr_t[b] * R;
   for (int c0 = 0; c0 < R; c0 += kCh) {
     const int c = c0 + lane;
     __syncthreads();
     for (int i = wave; i < ns; i += kWaves)
       sR[i * kPitch + lane] = c < R ? rs[(size_t)i * R + c] : 0.f;
     __syncthreads();
-    for (int j = wave; j < Nt; j += kWaves) {
+    for (int j = wave; j < nt; j += kWaves) {
       float acc = 0.f;
       for (int i = 0; i < ns; ++i)
         acc = fmaf(sS[i * kPitch + j], sR[i * kPitch + lane], acc);
@@ -110,14 +110,16 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
 // dS_hat = softmax_bwd(S, dS),  dS[i][j] = sum_c r_s[i][c] * g[j][c].
 __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
     const float* __restrict__ S, const float* __restrict__ r_s,
-    const float* __restrict__ g, float* __restrict__ dS_hat, int Ns, int Nt,
-    int R) {
+    const float* __restrict__ g, const int* __restrict__ ptr_s,
+    const int* __restrict__ ptr_t, float* __restrict__ dS_hat, int Ns,
+    int Nt, int R) {
   __shared__ float sR[kMaxN * kPitch];
   __shared__ float sG[kMaxN * kPitch];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const float* rs = r_s + (size_t)b * Ns * R;
-  const float* gb = g + (size_t)b * Nt * R;
+  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
+  const float* rs = r_s + (size_t)ptr_s[b] * R;
+  const float* gb = g + (size_t)ptr_t[b] * R;
 
   float acc[kRowsPerWave];
 #pragma unroll
@@ -126,17 +128,17 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
   for (int c0 = 0; c0 < R; c0 += kCh) {
     const int c = c0 + lane;
     __syncthreads();
-    for (int i = wave; i < Ns; i += kWaves)
+    for (int i = wave; i < ns; i += kWaves)
       sR[i * kPitch + lane] = c < R ? rs[(size_t)i * R + c] : 0.f;
-    for (int j = wave; j < Nt; j += kWaves)
+    for (int j = wave; j < nt; j += kWaves)
       sG[j * kPitch + lane] = c < R ? gb[(size_t)j * R + c] : 0.f;
     __syncthreads();
     const int cmax = min(kCh, R - c0);
-    if (lane < Nt) {
+    if (lane < nt) {
 #pragma unroll
       for (int q = 0; q < kRowsPerWave; ++q) {
         const int i = wave + q * kWaves;
-        if (i < Ns) {
+        if (i < ns) {
           float a = acc[q];
           for (int cc = 0; cc < cmax; ++cc)
             a = fmaf(sR[i * kPitch + cc], sG[lane * kPitch + cc], a);
@@ -161,20 +163,21 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
 // ---------------------------------------------------------------------------
 // Consensus update: out = S_hat + mask * (sum_c relu(P_ic - Q_jc) w2_c + b2)
 // ---------------------------------------------------------------------------
+template <typename TPQ>
 __global__ __launch_bounds__(256) void consensus_fwd_kernel(
-    const float* __restrict__ S_hat, const float* __restrict__ P,
-    const float* __restrict__ Q, const float* __restrict__ w2,
-    const float* __restrict__ b2, const int* __restrict__ n_s,
-    const int* __restrict__ n_t, float* __restrict__ out, int Ns, int Nt,
-    int R) {
+    const float* __restrict__ S_hat, const TPQ* __restrict__ P,
+    const TPQ* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2,
+    const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
+    float* __restrict__ out, int Ns, int Nt, int R) {
   __shared__ float sP[kMaxN * kPitch];
   __shared__ float sQ[kMaxN * kPitch];
   __shared__ float sW[kCh];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = n_s[b], nt = n_t[b];
-  const float* Pb = P + (size_t)b * Ns * R;
-  const float* Qb = Q + (size_t)b * Nt * R;
+  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
+  const TPQ* Pb = P + (size_t)ptr_s[b] * R;
+  const TPQ* Qb = Q + (size_t)ptr_t[b] * R;
 
   float acc[kRowsPerWave];
 #pragma unroll
@@ -183,10 +186,13 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
   for (int c0 = 0; c0 < R; c0 += kCh) {
     const int c = c0 + lane;
     __syncthreads();
+    const float bias1 = c < R ? b1[c] : 0.f;
     for (int i = wave; i < ns; i += kWaves)
-      sP[i * kPitch + lane] = c < R ? Pb[(size_t)i * R + c] : 0.f;
+      sP[i * kPitch + lane] =
+          c < R ? Cvt<TPQ>::to_f(Pb[(size_t)i * R + c]) + bias1 : 0.f;
     for (int j = wave; j < nt; j += kWaves)
-      sQ[j * kPitch + lane] = c < R ? Qb[(size_t)j * R + c] : 0.f;
+      sQ[j * kPitch + lane] =
+          c < R ? Cvt<TPQ>::to_f(Qb[(size_t)j * R + c]) : 0.f;
     if (wave == 0) sW[lane] = c < R ? w2[c] : 0.f;
     __syncthreads();
     const int cmax = min(kCh, R - c0);
@@ -218,25 +224,26 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
   }
 }
 
+template <typename TPQ>
 __global__ __launch_bounds__(256) void consensus_bwd_kernel(
-    const float* __restrict__ G, const float* __restrict__ P,
-    const float* __restrict__ Q, const float* __restrict__ w2,
-    const int* __restrict__ n_s, const int* __restrict__ n_t,
-    float* __restrict__ dP, float* __restrict__ dQ,
-    float* __restrict__ dw2_part, float* __restrict__ db2_part, int Ns,
-    int Nt, int R) {
+    const float* __restrict__ G, const TPQ* __restrict__ P,
+    const TPQ* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, const int* __restrict__ ptr_s,
+    const int* __restrict__ ptr_t, TPQ* __restrict__ dP,
+    TPQ* __restrict__ dQ, float* __restrict__ dw2_part,
+    float* __restrict__ db2_part, int Ns, int Nt, int R) {
   __shared__ float sG[kMaxN * kPitch];
   __shared__ float sP[kMaxN * kPitch];
   __shared__ float sQ[kMaxN * kPitch];
   __shared__ float sRed[kWaves * kCh];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = n_s[b], nt = n_t[b];
+  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
   const float* Gb = G + (size_t)b * Ns * Nt;
-  const float* Pb = P + (size_t)b * Ns * R;
-  const float* Qb = Q + (size_t)b * Nt * R;
-  float* dPb = dP + (size_t)b * Ns * R;
-  float* dQb = dQ + (size_t)b * Nt * R;
+  const TPQ* Pb = P + (size_t)ptr_s[b] * R;
+  const TPQ* Qb = Q + (size_t)ptr_t[b] * R;
+  TPQ* dPb = dP + (size_t)ptr_s[b] * R;
+  TPQ* dQb = dQ + (size_t)ptr_t[b] * R;
 
   // Masked upstream gradient tile + db2 partial.
   float gsum = 0.f;
@@ -255,18 +262,20 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     const int c = c0 + lane;
     const bool cv = c < R;
     __syncthreads();
+    const float bias1 = cv ? b1[c] : 0.f;
     for (int i = wave; i < ns; i += kWaves)
-      sP[i * kPitch + lane] = cv ? Pb[(size_t)i * R + c] : 0.f;
+      sP[i * kPitch + lane] =
+          cv ? Cvt<TPQ>::to_f(Pb[(size_t)i * R + c]) + bias1 : 0.f;
     for (int j = wave; j < nt; j += kWaves)
-      sQ[j * kPitch + lane] = cv ? Qb[(size_t)j * R + c] : 0.f;
+      sQ[j * kPitch + lane] = cv ? Cvt<TPQ>::to_f(Qb[(size_t)j * R + c]) : 0.f;
     __syncthreads();
     const float w = cv ? w2[c] : 0.f;
 
     // dP[i][c] and dw2 partial: rows owned by this wave, lane = channel.
     float dw = 0.f;
-    for (int i = wave; i < Ns; i += kWaves) {
+    for (int i = wave; i < ns; i += kWaves) {
       float dp = 0.f;
-      if (i < ns) {
+      {
         const float p = sP[i * kPitch + lane];
         for (int j = 0; j < nt; ++j) {
           const float z = p - sQ[j * kPitch + lane];
@@ -277,17 +286,15 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
           }
         }
       }
-      if (cv) dPb[(size_t)i * R + c] = dp * w;
+      if (cv) dPb[(size_t)i * R + c] = Cvt<TPQ>::from_f(dp * w);
     }
     // dQ[j][c] = -w * sum_i G[i][j] [P_ic > Q_jc]
-    for (int j = wave; j < Nt; j += kWaves) {
+    for (int j = wave; j < nt; j += kWaves) {
       float dq = 0.f;
-      if (j < nt) {
-        const float qv = sQ[j * kPitch + lane];
-        for (int i = 0; i < ns; ++i)
-          if (sP[i * kPitch + lane] > qv) dq += sG[i * kPitch + j];
-      }
-      if (cv) dQb[(size_t)j * R + c] = -dq * w;
+      const float qv = sQ[j * kPitch + lane];
+      for (int i = 0; i < ns; ++i)
+        if (sP[i * kPitch + lane] > qv) dq += sG[i * kPitch + j];
+      if (cv) dQb[(size_t)j * R + c] = Cvt<TPQ>::from_f(-dq * w);
     }
     // Reduce dw over the 4 waves.
     sRed[wave * kCh + lane] = dw;
@@ -313,6 +320,19 @@ static void check_counts(const at::Tensor& n_s, const at::Tensor& n_t,
   TORCH_CHECK(n_s.scalar_type() == at::kInt && n_t.scalar_type() == at::kInt &&
                   n_s.numel() == B && n_t.numel() == B,
               "node counts must be int32 [B]");
+}
+
+static void check_ptr(const at::Tensor& ptr_s, const at::Tensor& ptr_t,
+                      int64_t B) {
+  TORCH_CHECK(ptr_s.scalar_type() == at::kInt && ptr_t.scalar_type() == at::kInt &&
+                  ptr_s.numel() == B + 1 && ptr_t.numel() == B + 1 &&
+                  ptr_s.is_cuda() && ptr_t.is_cuda(),
+              "row offsets must be int32 [B + 1] GPU tensors");
+}
+
+static void check_packed(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous(), name,
+              " must be a contiguous [rows, R] GPU tensor");
 }
 
 at::Tensor dense_masked_softmax(const at::Tensor& S_hat, const at::Tensor& n_s,
@@ -349,23 +369,24 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
   return out;
 }
 
+// r_s: packed [sum N_s, R]; returns (S [B, Ns, Nt], r_t packed [rows_t, R]).
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
-    const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& n_s,
-    const at::Tensor& n_t) {
+    const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
+    const at::Tensor& ptr_t, int64_t rows_t) {
   check_pair_tensor(S_hat, "S_hat");
-  check_pair_tensor(r_s, "r_s");
+  check_packed(r_s, "r_s");
+  TORCH_CHECK(r_s.scalar_type() == at::kFloat, "r_s must be fp32");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
-  const int R = r_s.size(2);
+  const int R = r_s.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
-  TORCH_CHECK(r_s.size(0) == B && r_s.size(1) == Ns, "r_s shape");
-  check_counts(n_s, n_t, B);
+  check_ptr(ptr_s, ptr_t, B);
   at::Tensor S = at::empty_like(S_hat);
-  at::Tensor r_t = at::empty({B, Nt, R}, r_s.options());
+  at::Tensor r_t = at::empty({rows_t, R}, r_s.options());
   if (B == 0) return {S, r_t};
   hipLaunchKernelGGL(softmax_transport_kernel, dim3(B), dim3(256), 0, stream(),
                      S_hat.data_ptr<float>(), r_s.data_ptr<float>(),
-                     n_s.data_ptr<int>(), n_t.data_ptr<int>(),
+                     ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
                      S.data_ptr<float>(), r_t.data_ptr<float>(), Ns, Nt, R);
   DGMC_CHECK_LAUNCH();
   return {S, r_t};
@@ -374,78 +395,92 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
-                                       const at::Tensor& n_s,
-                                       const at::Tensor& n_t) {
+                                       const at::Tensor& ptr_s,
+                                       const at::Tensor& ptr_t) {
   check_pair_tensor(S, "S");
-  check_pair_tensor(r_s, "r_s");
-  check_pair_tensor(g, "grad r_t");
+  check_packed(r_s, "r_s");
+  check_packed(g, "grad r_t");
+  TORCH_CHECK(r_s.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat,
+              "fp32 expected");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
   const int B = S.size(0), Ns = S.size(1), Nt = S.size(2);
-  const int R = r_s.size(2);
+  const int R = r_s.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
-  TORCH_CHECK(g.size(0) == B && g.size(1) == Nt && g.size(2) == R, "grad shape");
-  check_counts(n_s, n_t, B);
+  TORCH_CHECK(g.size(1) == R, "grad shape");
+  check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S);
   if (B == 0) return out;
   hipLaunchKernelGGL(softmax_transport_bwd_kernel, dim3(B), dim3(256), 0,
                      stream(), S.data_ptr<float>(), r_s.data_ptr<float>(),
-                     g.data_ptr<float>(), out.data_ptr<float>(), Ns, Nt, R);
+                     g.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                     ptr_t.data_ptr<int>(), out.data_ptr<float>(), Ns, Nt, R);
   DGMC_CHECK_LAUNCH();
   return out;
 }
 
+// P: packed [sum N_s, R] (without bias), Q: packed [sum N_t, R]
 at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
-                           const at::Tensor& Q, const at::Tensor& w2,
-                           const at::Tensor& b2, const at::Tensor& n_s,
-                           const at::Tensor& n_t) {
+                           const at::Tensor& Q, const at::Tensor& b1,
+                           const at::Tensor& w2, const at::Tensor& b2,
+                           const at::Tensor& ptr_s, const at::Tensor& ptr_t) {
   check_pair_tensor(S_hat, "S_hat");
-  check_pair_tensor(P, "P");
-  check_pair_tensor(Q, "Q");
+  check_packed(P, "P");
+  check_packed(Q, "Q");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
-  const int R = P.size(2);
+  const int R = P.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
-  TORCH_CHECK(P.size(0) == B && P.size(1) == Ns && Q.size(0) == B &&
-                  Q.size(1) == Nt && Q.size(2) == R,
-              "P/Q shape");
-  TORCH_CHECK(w2.numel() == R && b2.numel() == 1 &&
+  TORCH_CHECK(Q.size(1) == R && Q.scalar_type() == P.scalar_type(), "P/Q");
+  TORCH_CHECK(b1.numel() == R && w2.numel() == R && b2.numel() == 1 &&
+                  b1.scalar_type() == at::kFloat &&
                   w2.scalar_type() == at::kFloat &&
                   b2.scalar_type() == at::kFloat,
-              "w2/b2");
-  check_counts(n_s, n_t, B);
+              "b1/w2/b2 must be fp32");
+  check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S_hat);
   if (B == 0) return out;
-  hipLaunchKernelGGL(consensus_fwd_kernel, dim3(B), dim3(256), 0, stream(),
-                     S_hat.data_ptr<float>(), P.data_ptr<float>(),
-                     Q.data_ptr<float>(), w2.data_ptr<float>(),
-                     b2.data_ptr<float>(), n_s.data_ptr<int>(),
-                     n_t.data_ptr<int>(), out.data_ptr<float>(), Ns, Nt, R);
+  DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
+    hipLaunchKernelGGL(consensus_fwd_kernel<T>, dim3(B), dim3(256), 0,
+                       stream(), S_hat.data_ptr<float>(),
+                       reinterpret_cast<const T*>(P.data_ptr()),
+                       reinterpret_cast<const T*>(Q.data_ptr()),
+                       b1.data_ptr<float>(), w2.data_ptr<float>(),
+                       b2.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                       ptr_t.data_ptr<int>(), out.data_ptr<float>(), Ns, Nt,
+                       R);
+  });
   DGMC_CHECK_LAUNCH();
   return out;
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
-    const at::Tensor& w2, const at::Tensor& n_s, const at::Tensor& n_t) {
+    const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
+    const at::Tensor& ptr_t) {
   check_pair_tensor(G, "grad");
-  check_pair_tensor(P, "P");
-  check_pair_tensor(Q, "Q");
+  check_packed(P, "P");
+  check_packed(Q, "Q");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(G.device());
   const int B = G.size(0), Ns = G.size(1), Nt = G.size(2);
-  const int R = P.size(2);
+  const int R = P.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
-  check_counts(n_s, n_t, B);
+  check_ptr(ptr_s, ptr_t, B);
   at::Tensor dP = at::empty_like(P);
   at::Tensor dQ = at::empty_like(Q);
-  at::Tensor dw2 = at::empty({B, R}, P.options());
-  at::Tensor db2 = at::empty({B}, P.options());
+  at::Tensor dw2 = at::empty({B, R}, G.options());
+  at::Tensor db2 = at::empty({B}, G.options());
   if (B == 0) return {dP, dQ, dw2.zero_(), db2.zero_()};
-  hipLaunchKernelGGL(consensus_bwd_kernel, dim3(B), dim3(256), 0, stream(),
-                     G.data_ptr<float>(), P.data_ptr<float>(),
-                     Q.data_ptr<float>(), w2.data_ptr<float>(),
-                     n_s.data_ptr<int>(), n_t.data_ptr<int>(),
-                     dP.data_ptr<float>(), dQ.data_ptr<float>(),
-                     dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R);
+  DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
+    hipLaunchKernelGGL(consensus_bwd_kernel<T>, dim3(B), dim3(256), 0,
+                       stream(), G.data_ptr<float>(),
+                       reinterpret_cast<const T*>(P.data_ptr()),
+                       reinterpret_cast<const T*>(Q.data_ptr()),
+                       b1.data_ptr<float>(), w2.data_ptr<float>(),
+                       ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
+                       reinterpret_cast<T*>(dP.data_ptr()),
+                       reinterpret_cast<T*>(dQ.data_ptr()),
+                       dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R);
+  });
   DGMC_CHECK_LAUNCH();
   return {dP, dQ, dw2, db2};
 }

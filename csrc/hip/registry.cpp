@@ -11,7 +11,7 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& self_x,
                     const c10::optional<at::Tensor>& self_scale,
                     const c10::optional<at::Tensor>& bias, bool relu,
-                    bool out_fp32);
+                    at::ScalarType out_dtype);
 
 std::tuple<at::Tensor, at::Tensor> spline_basis(const at::Tensor& pseudo,
                                                 const at::Tensor& kernel_size,
@@ -24,20 +24,21 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
                                     const at::Tensor& n_s,
                                     const at::Tensor& n_t);
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
-    const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& n_s,
-    const at::Tensor& n_t);
+    const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
+    const at::Tensor& ptr_t, int64_t rows_t);
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
-                                       const at::Tensor& n_s,
-                                       const at::Tensor& n_t);
+                                       const at::Tensor& ptr_s,
+                                       const at::Tensor& ptr_t);
 at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
-                           const at::Tensor& Q, const at::Tensor& w2,
-                           const at::Tensor& b2, const at::Tensor& n_s,
-                           const at::Tensor& n_t);
+                           const at::Tensor& Q, const at::Tensor& b1,
+                           const at::Tensor& w2, const at::Tensor& b2,
+                           const at::Tensor& ptr_s, const at::Tensor& ptr_t);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
-    const at::Tensor& w2, const at::Tensor& n_s, const at::Tensor& n_t);
+    const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
+    const at::Tensor& ptr_t);
 
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
 
@@ -46,7 +47,8 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
 TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "spmm_csr(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
-      "self_x, Tensor? self_scale, Tensor? bias, bool relu, bool out_fp32) -> "
+      "self_x, Tensor? self_scale, Tensor? bias, bool relu, ScalarType "
+      "out_dtype) -> "
       "Tensor");
   m.def(
       "spline_basis(Tensor pseudo, Tensor kernel_size, Tensor is_open, int "
@@ -56,17 +58,17 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "dense_masked_softmax_bwd(Tensor S, Tensor grad, Tensor n_s, Tensor n_t) "
       "-> Tensor");
   m.def(
-      "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor n_s, Tensor "
-      "n_t) -> (Tensor, Tensor)");
+      "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor ptr_s, Tensor "
+      "ptr_t, int rows_t) -> (Tensor, Tensor)");
   m.def(
       "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
-      "n_s, Tensor n_t) -> Tensor");
+      "ptr_s, Tensor ptr_t) -> Tensor");
   m.def(
-      "dense_consensus(Tensor S_hat, Tensor P, Tensor Q, Tensor w2, Tensor b2, "
-      "Tensor n_s, Tensor n_t) -> Tensor");
+      "dense_consensus(Tensor S_hat, Tensor P, Tensor Q, Tensor b1, Tensor w2, "
+      "Tensor b2, Tensor ptr_s, Tensor ptr_t) -> Tensor");
   m.def(
-      "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor w2, Tensor "
-      "n_s, Tensor n_t) -> (Tensor, Tensor, Tensor, Tensor)");
+      "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
+      "w2, Tensor ptr_s, Tensor ptr_t) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
 }
 

@@ -137,7 +137,7 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& self_x,
                     const c10::optional<at::Tensor>& self_scale,
                     const c10::optional<at::Tensor>& bias, bool relu,
-                    bool out_fp32) {
+                    at::ScalarType out_dtype) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous(), "spmm: x");
   TORCH_CHECK(rowptr.scalar_type() == at::kInt && col.scalar_type() == at::kInt,
               "spmm: int32 index expected");
@@ -147,7 +147,6 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
   const int64_t R = rowptr.numel() - 1;
   const int64_t C = x.size(1);
   TORCH_CHECK(R >= 0 && R < INT32_MAX && C < INT32_MAX, "spmm: size");
-  const auto out_dtype = out_fp32 ? at::kFloat : x.scalar_type();
   at::Tensor out = at::empty({R, C}, x.options().dtype(out_dtype));
   if (R == 0 || C == 0) return out;
 
@@ -176,17 +175,12 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
     const TIn* sp = sx ? reinterpret_cast<const TIn*>(sx->data_ptr()) : nullptr;
     const float* ssp = sx ? ss_c.data_ptr<float>() : nullptr;
     const float* bp = b_c.defined() ? b_c.data_ptr<float>() : nullptr;
-    if (out_fp32) {
-      spmm_dispatch<TIn, float>(rowptr.data_ptr<int>(), col.data_ptr<int>(),
-                                val.data_ptr<float>(), xp, sp, ssp, bp,
-                                out.data_ptr<float>(), (int)R, (int)C, relu,
-                                vec_ok);
-    } else {
-      spmm_dispatch<TIn, TIn>(rowptr.data_ptr<int>(), col.data_ptr<int>(),
-                              val.data_ptr<float>(), xp, sp, ssp, bp,
-                              reinterpret_cast<TIn*>(out.data_ptr()), (int)R,
-                              (int)C, relu, vec_ok);
-    }
+    DGMC_DISPATCH_FLOAT(out_dtype, TOut, [&] {
+      spmm_dispatch<TIn, TOut>(rowptr.data_ptr<int>(), col.data_ptr<int>(),
+                               val.data_ptr<float>(), xp, sp, ssp, bp,
+                               reinterpret_cast<TOut*>(out.data_ptr()), (int)R,
+                               (int)C, relu, vec_ok);
+    });
   });
   return out;
 }

@@ -23,6 +23,7 @@ class DenseLayout(object):
         self.device = device
         self.index = info.dense_index(device, self.N)        # [sum N] int64
         self.counts = info.device_tensor('counts', device, torch.int32)
+        self.ptr = info.device_tensor('ptr', device, torch.int32)
         self.num_nodes = info.num_nodes
         self._mask = None
 

@@ -30,6 +30,7 @@ from ..graph.dense import dense_layout
 from ..nn.inits import reset
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
+from ..runtime.cache import forward_cache
 from ..runtime.mode import is_reference_mode
 
 EPS = 1e-8
@@ -131,6 +132,12 @@ class DGMC(torch.nn.Module):
                 edge_index_t, edge_attr_t, batch_t, y=None):
         r"""Returns initial and refined correspondences ``(S_0, S_L)`` of
         shape ``[batch_size * num_nodes, num_nodes]`` (dense or sparse)."""
+        with forward_cache():
+            return self._forward(x_s, edge_index_s, edge_attr_s, batch_s, x_t,
+                                 edge_index_t, edge_attr_t, batch_t, y)
+
+    def _forward(self, x_s, edge_index_s, edge_attr_s, batch_s, x_t,
+                 edge_index_t, edge_attr_t, batch_t, y):
         device = x_s.device
         dev_type = _device_type(device)
         outer_autocast = torch.is_autocast_enabled(dev_type)
@@ -158,34 +165,38 @@ class DGMC(torch.nn.Module):
                 else torch.float32
             hs = lay_s.to_dense(h_s.to(f32))
             ht = lay_t.to_dense(h_t.to(f32))
+            # Random node indicators for all steps, packed [steps, sum N_s, R].
+            if steps > 0:
+                r_all = torch.randn((steps, lay_s.num_nodes, R_in), dtype=f32,
+                                    device=device)
 
             def refine(r_s, r_t):
-                # psi_2 runs under the caller's autocast policy.
+                """psi_2 on both graphs (packed in/out) under the caller's
+                autocast policy; returns (o_s, o_t, o_joint or None)."""
                 with torch.autocast(device_type=dev_type, dtype=outer_dtype,
                                     enabled=outer_autocast):
-                    o_s, o_t = self._encode(
-                        self.psi_2, pair, lay_s.to_sparse(r_s),
-                        lay_t.to_sparse(r_t), edge_index_s, edge_attr_s,
-                        edge_index_t, edge_attr_t)
-                return lay_s.to_dense(o_s.to(f32)), lay_t.to_dense(
-                    o_t.to(f32))
+                    if pair is not None and self._fusable(self.psi_2):
+                        o = self.psi_2(torch.cat([r_s, r_t], dim=0),
+                                       pair.edge_index, pair.edge_attr)
+                        return o[:pair.n_s], o[pair.n_s:], o
+                    o_s = self.psi_2(r_s, edge_index_s, edge_attr_s)
+                    o_t = self.psi_2(r_t, edge_index_t, edge_attr_t)
+                    return o_s, o_t, None
 
             if self.k < 1:
                 # ------------------ dense variant -------------------- #
                 S_hat = hs @ ht.transpose(-1, -2)            # [B, N_s, N_t]
                 S_0 = lay_s.to_sparse(
-                    dense_ops.masked_softmax(S_hat, n_s, n_t))
-                if steps > 0:
-                    r_all = torch.randn((steps, B, N_s, R_in), dtype=f32,
-                                        device=device)
+                    dense_ops.masked_softmax(S_hat, lay_s, lay_t))
                 for step in range(steps):
                     r_s = r_all[step]
-                    r_t = dense_ops.softmax_transport(S_hat, r_s, n_s, n_t)
-                    o_s, o_t = refine(r_s, r_t)
-                    S_hat = dense_ops.consensus_update(S_hat, o_s, o_t,
-                                                       self.mlp, n_s, n_t)
+                    r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,
+                                                      lay_t)
+                    o_s, o_t, o = refine(r_s, r_t)
+                    S_hat = dense_ops.consensus_update(
+                        S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o)
                 S_L = lay_s.to_sparse(dense_ops.masked_softmax(
-                    S_hat, n_s, n_t))
+                    S_hat, lay_s, lay_t))
                 return S_0, S_L
 
             # ------------------- sparse variant ---------------------- #
@@ -200,16 +211,15 @@ class DGMC(torch.nn.Module):
 
             S_hat = sparse_corr.gather_dot(hs, ht, S_idx)     # [B, N_s, k]
             S_0 = lay_s.to_sparse(S_hat.softmax(dim=-1))
-            if steps > 0:
-                r_all = torch.randn((steps, B, N_s, R_in), dtype=f32,
-                                    device=device)
             for step in range(steps):
                 S = S_hat.softmax(dim=-1)
                 r_s = r_all[step]
-                r_t = sparse_corr.sparse_transport(S, r_s, S_idx, N_t)
-                o_s, o_t = refine(r_s, r_t)
-                S_hat = sparse_corr.consensus_update(S_hat, o_s, o_t, S_idx,
-                                                     self.mlp)
+                r_t = sparse_corr.sparse_transport(
+                    S, lay_s.to_dense(r_s), S_idx, N_t)
+                o_s, o_t, _ = refine(r_s, lay_t.to_sparse(r_t))
+                S_hat = sparse_corr.consensus_update(
+                    S_hat, lay_s.to_dense(o_s.to(f32)),
+                    lay_t.to_dense(o_t.to(f32)), S_idx, self.mlp)
             S_L = lay_s.to_sparse(S_hat.softmax(dim=-1))
             S_idx = lay_s.to_sparse(S_idx)
 

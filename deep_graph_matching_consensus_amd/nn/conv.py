@@ -22,6 +22,7 @@ from torch.nn import Parameter
 
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.sparse import spmm
+from ..runtime.cache import cached
 from .inits import reset, uniform
 
 
@@ -95,12 +96,15 @@ class SplineConv(torch.nn.Module):
         self._open = tuple(int(v) for v in self.is_open_spline.tolist())
 
     def stacked_weight(self, dtype):
-        """``[in, (K + root) * out]`` GEMM operand (slot-major columns)."""
-        K, cin, cout = self.weight.shape
-        w = self.weight.permute(1, 0, 2).reshape(cin, K * cout)
-        if self.root is not None:
-            w = torch.cat([w, self.root], dim=1)
-        return w.to(dtype)
+        """``[in, (K + root) * out]`` GEMM operand (slot-major columns),
+        memoised per forward scope (:mod:`..runtime.cache`)."""
+        def build():
+            K, cin, cout = self.weight.shape
+            w = self.weight.permute(1, 0, 2).reshape(cin, K * cout)
+            if self.root is not None:
+                w = torch.cat([w, self.root], dim=1)
+            return w.to(dtype)
+        return cached(('spline_w', id(self), dtype), build)
 
     def forward(self, x, edge_index, pseudo, act=None):
         x = x.unsqueeze(-1) if x.dim() == 1 else x

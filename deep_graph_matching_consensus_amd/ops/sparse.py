@@ -91,7 +91,7 @@ def _spmm_raw(op, x, self_x, self_scale, bias, relu, out_dtype):
         return _backend.ops().spmm_csr(
             op.rowptr, op.col, op.val, x.contiguous(),
             self_x.contiguous() if self_x is not None else None,
-            self_scale, bias, relu, out_dtype == torch.float32)
+            self_scale, bias, relu, out_dtype)
     return ref.spmm(op.row, op.col, op.val, op.num_rows, x, self_x,
                     self_scale, bias, relu, out_dtype)
 
@@ -116,7 +116,6 @@ class _SpMM(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = _spmm_raw(ctx.op.t(), g, None, None, None, False,
                            ctx.x_dtype)
-            gx = gx.to(ctx.x_dtype)
         if self_x is not None:
             if ctx.needs_input_grad[1]:
                 gself = (g * self_scale.float()).to(self_x.dtype)

@@ -98,22 +98,27 @@ def test_spline_conv_matches_cpu():
     assert torch.allclose(out_cpu, out_gpu.cpu(), atol=1e-4)
 
 
-def _pair_inputs(B=7, Ns=13, Nt=17, R=40):
-    n_s = torch.randint(1, Ns + 1, (B, ), device=DEV, dtype=torch.int32)
-    n_t = torch.randint(1, Nt + 1, (B, ), device=DEV, dtype=torch.int32)
-    n_s[0], n_t[0] = Ns, Nt
-    S_hat = torch.randn(B, Ns, Nt, device=DEV)
-    return S_hat, n_s, n_t
+def _layouts(B, Ns, Nt):
+    from deep_graph_matching_consensus_amd.graph.dense import DenseLayout
+    from deep_graph_matching_consensus_amd.graph.meta import BatchInfo
+    c_s = torch.randint(1, Ns + 1, (B, ))
+    c_t = torch.randint(1, Nt + 1, (B, ))
+    c_s[0], c_t[0] = Ns, Nt
+    return (DenseLayout(BatchInfo(c_s), torch.device(DEV)),
+            DenseLayout(BatchInfo(c_t), torch.device(DEV)))
+
+
+def _mask(lay_s, lay_t):
+    return ref.count_mask(lay_s.counts, lay_t.counts, lay_s.N, lay_t.N)
 
 
 @pytest.mark.parametrize('shape', [(7, 13, 17), (3, 64, 64), (5, 1, 9)])
 def test_dense_masked_softmax(shape):
-    S_hat, n_s, n_t = _pair_inputs(*shape)
-    S_hat.requires_grad_()
-    out = dense_ops.masked_softmax(S_hat, n_s, n_t)
-    mask = ref.count_mask(n_s, n_t, shape[1], shape[2])
+    lay_s, lay_t = _layouts(*shape)
+    S_hat = torch.randn(shape, device=DEV, requires_grad=True)
+    out = dense_ops.masked_softmax(S_hat, lay_s, lay_t)
     S2 = S_hat.detach().clone().requires_grad_()
-    out2 = ref.masked_softmax(S2, mask)
+    out2 = ref.masked_softmax(S2, _mask(lay_s, lay_t))
     assert torch.allclose(out, out2, atol=1e-6)
     g = torch.randn_like(out)
     assert torch.allclose(torch.autograd.grad(out, S_hat, g)[0],
@@ -123,13 +128,15 @@ def test_dense_masked_softmax(shape):
 @pytest.mark.parametrize('R', [8, 64, 100, 128])
 def test_dense_softmax_transport(R):
     B, Ns, Nt = 6, 19, 23
-    S_hat, n_s, n_t = _pair_inputs(B, Ns, Nt)
-    S_hat.requires_grad_()
-    r_s = torch.randn(B, Ns, R, device=DEV)
-    r_t = dense_ops.softmax_transport(S_hat, r_s, n_s, n_t)
-    mask = ref.count_mask(n_s, n_t, Ns, Nt)
+    lay_s, lay_t = _layouts(B, Ns, Nt)
+    S_hat = torch.randn(B, Ns, Nt, device=DEV, requires_grad=True)
+    r_s = torch.randn(lay_s.num_nodes, R, device=DEV)
+    r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s, lay_t)
+    assert r_t.shape == (lay_t.num_nodes, R)
     S2 = S_hat.detach().clone().requires_grad_()
-    r_t2 = ref.masked_softmax(S2, mask).transpose(-1, -2) @ r_s
+    r_t2 = ref.masked_softmax(S2, _mask(lay_s, lay_t)).transpose(-1, -2) \
+        @ lay_s.to_dense(r_s)
+    r_t2 = lay_t.to_sparse(r_t2)
     assert torch.allclose(r_t, r_t2, atol=1e-5)
     g = torch.randn_like(r_t)
     assert torch.allclose(torch.autograd.grad(r_t, S_hat, g)[0],
@@ -137,20 +144,23 @@ def test_dense_softmax_transport(R):
 
 
 @pytest.mark.parametrize('R', [8, 32, 100, 128])
-def test_dense_consensus_update(R):
+@pytest.mark.parametrize('joint', [False, True])
+def test_dense_consensus_update(R, joint):
     B, Ns, Nt = 5, 21, 18
-    S_hat, n_s, n_t = _pair_inputs(B, Ns, Nt)
+    lay_s, lay_t = _layouts(B, Ns, Nt)
+    S_hat = torch.randn(B, Ns, Nt, device=DEV, requires_grad=True)
     mlp = torch.nn.Sequential(torch.nn.Linear(R, R), torch.nn.ReLU(),
                               torch.nn.Linear(R, 1)).to(DEV)
-    o_s = torch.randn(B, Ns, R, device=DEV, requires_grad=True)
-    o_t = torch.randn(B, Nt, R, device=DEV, requires_grad=True)
-    S_hat.requires_grad_()
-    out = dense_ops.consensus_update(S_hat, o_s, o_t, mlp, n_s, n_t)
+    o = torch.randn(lay_s.num_nodes + lay_t.num_nodes, R, device=DEV,
+                    requires_grad=True)
+    o_s, o_t = o[:lay_s.num_nodes], o[lay_s.num_nodes:]
+    out = dense_ops.consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t,
+                                     o_joint=o if joint else None)
     with reference_mode():
-        out2 = dense_ops.consensus_update(S_hat, o_s, o_t, mlp, n_s, n_t)
+        out2 = dense_ops.consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t)
     assert torch.allclose(out, out2, atol=1e-4)
     g = torch.randn_like(out)
-    inputs = (S_hat, o_s, o_t) + tuple(mlp.parameters())
+    inputs = (S_hat, o) + tuple(mlp.parameters())
     ga = torch.autograd.grad(out, inputs, g)
     gb = torch.autograd.grad(out2, inputs, g)
     for a, b in zip(ga, gb):
