@@ -18,6 +18,8 @@ kernel launches and doubles GEMM sizes on the hot path.
 import torch
 from torch.nn import Linear
 
+from ..ops.gemm import linear
+
 
 class StackedEncoder(torch.nn.Module):
     def _init_head(self, in_channels, out_channels, num_layers, cat, lin):
@@ -38,7 +40,9 @@ class StackedEncoder(torch.nn.Module):
         return x
 
     def _project(self, x):
-        return self.final(x) if self.lin else x
+        if not self.lin:
+            return x
+        return linear(x, self.final.weight, self.final.bias)
 
     @property
     def pair_fusable(self):

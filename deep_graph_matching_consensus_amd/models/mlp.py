@@ -9,6 +9,8 @@ import torch
 import torch.nn.functional as F
 from torch.nn import BatchNorm1d, Linear, ModuleList
 
+from ..ops.gemm import linear
+
 
 class MLP(torch.nn.Module):
     def __init__(self, in_channels, out_channels, num_layers,
@@ -34,11 +36,12 @@ class MLP(torch.nn.Module):
     def forward(self, x, *args):
         last = self.num_layers - 1
         for depth in range(self.num_layers):
+            lin = self.lins[depth]
             if depth == last:
                 x = F.dropout(x, p=self.dropout, training=self.training)
-                x = self.lins[depth](x)
+                x = linear(x, lin.weight, lin.bias)
                 break
-            x = F.relu(self.lins[depth](x))
+            x = F.relu(linear(x, lin.weight, lin.bias))
             if self.batch_norm:
                 x = self.batch_norms[depth](x)
         return x

@@ -13,6 +13,7 @@ import torch
 import torch.nn.functional as F
 from torch.nn import BatchNorm1d, Linear, ModuleList
 
+from ..ops.gemm import linear
 from ..ops.plans import relational_plan
 from ..ops.sparse import spmm
 from .encoder import StackedEncoder
@@ -37,7 +38,7 @@ class RelConv(torch.nn.Module):
             [self.lin1.weight, self.lin2.weight, self.root.weight], dim=0)
         bias = torch.cat([self.root.bias.new_zeros(2 * self.out_channels),
                           self.root.bias])
-        y = F.linear(x, weight, bias).view(-1, self.out_channels)
+        y = linear(x, weight, bias).view(-1, self.out_channels)
         plan = relational_plan(edge_index, x.size(0))
         return spmm(plan, y, relu=(act == 'relu'))
 

@@ -21,16 +21,10 @@ import torch
 from torch.nn import Parameter
 
 from ..ops.plans import spline_plan, adjacency_plan
+from ..ops.gemm import compute_dtype, mixed_matmul
 from ..ops.sparse import spmm
 from ..runtime.cache import cached
 from .inits import reset, uniform
-
-
-def matmul_dtype(x):
-    dev = 'cuda' if x.is_cuda else 'cpu'
-    if torch.is_autocast_enabled(dev):
-        return torch.get_autocast_dtype(dev)
-    return x.dtype
 
 
 def repeat(src, length):
@@ -95,16 +89,16 @@ class SplineConv(torch.nn.Module):
         self._ks = tuple(int(k) for k in self.kernel_size.tolist())
         self._open = tuple(int(v) for v in self.is_open_spline.tolist())
 
-    def stacked_weight(self, dtype):
-        """``[in, (K + root) * out]`` GEMM operand (slot-major columns),
+    def stacked_weight(self):
+        """``[in, (K + root) * out]`` fp32 GEMM operand (slot-major columns),
         memoised per forward scope (:mod:`..runtime.cache`)."""
         def build():
             K, cin, cout = self.weight.shape
             w = self.weight.permute(1, 0, 2).reshape(cin, K * cout)
             if self.root is not None:
                 w = torch.cat([w, self.root], dim=1)
-            return w.to(dtype)
-        return cached(('spline_w', id(self), dtype), build)
+            return w
+        return cached(('spline_w', id(self)), build)
 
     def forward(self, x, edge_index, pseudo, act=None):
         x = x.unsqueeze(-1) if x.dim() == 1 else x
@@ -112,9 +106,11 @@ class SplineConv(torch.nn.Module):
         N = x.size(0)
         plan = spline_plan(edge_index, pseudo, N, self._ks, self._open,
                            self.degree, root=self.root is not None)
-        dtype = matmul_dtype(x)
-        y = torch.matmul(x.to(dtype), self.stacked_weight(dtype))
-        y = y.view(-1, self.out_channels)
+        dtype = compute_dtype(x)
+        w = self.stacked_weight()
+        w_lp = cached(('spline_w_lp', id(self), dtype),
+                      lambda: w.detach().to(dtype))
+        y = mixed_matmul(x, w, w_lp).view(-1, self.out_channels)
         return spmm(plan, y, bias=self.bias, relu=(act == 'relu'))
 
     def __repr__(self):
@@ -151,4 +147,4 @@ class GINConv(torch.nn.Module):
         return '{}(nn={})'.format(self.__class__.__name__, self.nn)
 
 
-__all__ = ['SplineConv', 'GINConv', 'matmul_dtype']
+__all__ = ['SplineConv', 'GINConv']

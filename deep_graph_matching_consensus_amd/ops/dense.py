@@ -23,10 +23,10 @@ per step for PascalVOC shapes); the backward recomputes the ReLU from
 ``P``/``Q``.  Masks come from per-pair node counts.
 """
 import torch
-import torch.nn.functional as F
 
 from . import _backend
 from . import reference as ref
+from .gemm import mixed_matmul
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
@@ -136,12 +136,13 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None):
     lin1, lin2 = mlp[0], mlp[2]
     B, N_s, N_t = S_hat.shape
     if _hip_ok(S_hat, N_s, N_t):
+        w1t = lin1.weight.t()
         if o_joint is not None:
-            PQ = F.linear(o_joint, lin1.weight.to(o_joint.dtype))
+            PQ = mixed_matmul(o_joint, w1t, w1t.detach().to(o_joint.dtype))
             P, Q = PQ[:lay_s.num_nodes], PQ[lay_s.num_nodes:]
         else:
-            P = F.linear(o_s, lin1.weight.to(o_s.dtype))
-            Q = F.linear(o_t, lin1.weight.to(o_t.dtype))
+            P = mixed_matmul(o_s, w1t, w1t.detach().to(o_s.dtype))
+            Q = mixed_matmul(o_t, w1t, w1t.detach().to(o_t.dtype))
         return _ConsensusUpdate.apply(S_hat, P, Q, lin1.bias, lin2.weight,
                                       lin2.bias, lay_s.ptr, lay_t.ptr)
     o_s_d = lay_s.to_dense(o_s.to(S_hat.dtype))

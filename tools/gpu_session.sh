@@ -39,4 +39,5 @@ if want prof; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 5 --warmup 2
 fi
+want torchprof && run torchprof 600 python tools/profile_step.py --steps 2 --rows 60
 echo "=== done ($(date +%T))"
