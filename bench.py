@@ -37,6 +37,9 @@ from deep_graph_matching_consensus_amd import parallel  # noqa: E402
 from deep_graph_matching_consensus_amd.datasets import (  # noqa: E402
     PASCAL_VOC_CATEGORIES, WILLOW_CATEGORIES, DevicePairLoader, GraphStore,
     make_keypoint_datasets)
+from deep_graph_matching_consensus_amd.datasets.static_batch import (  # noqa
+    StaticPairBatcher)
+from deep_graph_matching_consensus_amd.runtime import GraphedStep  # noqa
 from deep_graph_matching_consensus_amd.models import (  # noqa: E402
     DGMC, SplineCNN)
 from deep_graph_matching_consensus_amd.runtime import reference_mode  # noqa
@@ -70,6 +73,8 @@ def parse_args(argv=None):
     p.add_argument('--num-steps', type=int, default=10)
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--no-overlap', action='store_true')
+    p.add_argument('--no-graph', action='store_true',
+                   help='disable hipGraph capture of the training step')
     p.add_argument('--json-out', default=None)
     return p.parse_args(argv)
 
@@ -97,38 +102,72 @@ def main(argv=None):
                        x_dtype=torch.bfloat16 if use_bf16 else torch.float32,
                        valid_pairs=True)
     shard = torch.arange(store.num_graphs)[rank::world].numpy()
-    loader = DevicePairLoader(store, args.batch_size, sources=shard,
-                              seed=args.seed + 1000 * rank)
-    batches = loader.forever()
+    use_graph = (device.type == 'cuda' and not reference and
+                 not args.no_graph)
 
     model = build_model(cfg, args, groups[0].num_node_features,
                         groups[0].num_edge_features, device)
     model.train()
-    reducer = parallel.GradBucketAllReducer(model,
-                                            overlap=not args.no_overlap)
+    reducer = parallel.GradBucketAllReducer(
+        model, overlap=not (args.no_overlap or use_graph))
     fused = device.type == 'cuda'
-    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3, fused=fused)
-
+    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3, fused=fused,
+                                 capturable=use_graph)
     stats = torch.zeros(3, dtype=torch.float64, device=device)
+    autocast = dict(device_type=device.type, dtype=torch.bfloat16,
+                    enabled=use_bf16, cache_enabled=False)
 
-    def train_step(batch):
-        reducer.zero_grad()
-        with torch.autocast(device_type=device.type, dtype=torch.bfloat16,
-                            enabled=use_bf16):
+    def forward_loss(batch, rows, mask):
+        with torch.autocast(**autocast):
             S_0, S_L = model(batch.x_s, batch.edge_index_s,
                              batch.edge_attr_s, batch.x_s_batch, batch.x_t,
                              batch.edge_index_t, batch.edge_attr_t,
                              batch.x_t_batch)
-        rows = torch.arange(batch.y.numel(), device=device)
         y = torch.stack([rows, batch.y], dim=0)
-        loss = model.loss(S_0, y)
-        loss = model.loss(S_L, y) + loss if model.num_steps > 0 else loss
+        loss = model.loss(S_0, y, mask=mask)
+        if model.num_steps > 0:
+            loss = model.loss(S_L, y, mask=mask) + loss
         loss.backward()
-        reducer.finish()
-        optimizer.step()
         stats[0] += loss.detach().double()
-        stats[1] += model.correct(S_L.detach(), y).double()
-        stats[2] += y.size(1)
+        stats[1] += model.correct(S_L.detach(), y, mask).double()
+        stats[2] += y.size(1) if mask is None else mask.sum().double()
+
+    overflows = 0
+    if use_graph:
+        # Static shapes + whole-step hipGraph (zero-grad, gather, forward,
+        # backward and - on one GPU - the optimizer update).
+        batcher = StaticPairBatcher(store, args.batch_size, sources=shard,
+                                    seed=args.seed + 1000 * rank)
+        rows = torch.arange(batcher.cap_s, device=device)
+
+        def body():
+            reducer.flat.zero_()
+            batch = batcher.materialize()
+            forward_loss(batch, rows, batch.y_mask)
+            if world == 1:
+                optimizer.step()
+
+        step_graph = GraphedStep(body, warmup=3)
+
+        def train_step():
+            while not batcher.load():
+                pass
+            step_graph()
+            if world > 1:
+                reducer.finish()
+                optimizer.step()
+    else:
+        loader = DevicePairLoader(store, args.batch_size, sources=shard,
+                                  seed=args.seed + 1000 * rank)
+        batches = loader.forever()
+
+        def train_step():
+            batch = next(batches)
+            reducer.zero_grad()
+            rows = torch.arange(batch.y.numel(), device=device)
+            forward_loss(batch, rows, None)
+            reducer.finish()
+            optimizer.step()
 
     def sync():
         if device.type == 'cuda':
@@ -136,16 +175,18 @@ def main(argv=None):
 
     with reference_mode(reference):
         for _ in range(args.warmup):
-            train_step(next(batches))
+            train_step()
         stats.zero_()
         parallel.barrier()
         sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            train_step(next(batches))
+            train_step()
         sync()
         parallel.barrier()
         elapsed = time.perf_counter() - t0
+    if use_graph:
+        overflows = batcher.overflows
 
     elapsed = parallel.all_reduce_max(elapsed, device)
     parallel.all_reduce_sum(stats)
@@ -188,9 +229,11 @@ def main(argv=None):
             'parallelism': 'dp{}'.format(world),
             'impl': args.impl,
             'consensus_steps': args.num_steps,
+            'hipgraph': bool(use_graph),
         },
         'hits@1_train': round(hits1, 4) if hits1 is not None else None,
         'loss': round(mean_loss, 4),
+        'capacity_overflows': overflows,
     }
     if rank == 0:
         line = json.dumps(out)

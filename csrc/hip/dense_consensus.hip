@@ -22,6 +22,16 @@ constexpr int kCh = 64;        // channel chunk staged per pass
 constexpr int kWaves = 4;      // waves per workgroup
 constexpr int kRowsPerWave = kMaxN / kWaves;
 
+// Zero rows [row0, rows) of a packed [rows, R] tensor (padding rows of static
+// batches; executed by the last workgroup of a launch).
+template <typename T>
+__device__ __forceinline__ void zero_tail(T* __restrict__ x, int row0,
+                                          int rows, int R) {
+  const size_t begin = (size_t)row0 * R, end = (size_t)rows * R;
+  for (size_t e = begin + threadIdx.x; e < end; e += blockDim.x)
+    x[e] = Cvt<T>::from_f(0.f);
+}
+
 // ---------------------------------------------------------------------------
 // Row-wise masked softmax (+ backward).  One wave per (b, i) row.
 // ---------------------------------------------------------------------------
@@ -68,10 +78,12 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
 __global__ __launch_bounds__(256) void softmax_transport_kernel(
     const float* __restrict__ S_hat, const float* __restrict__ r_s,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
-    float* __restrict__ S, float* __restrict__ r_t, int Ns, int Nt, int R) {
+    float* __restrict__ S, float* __restrict__ r_t, int Ns, int Nt, int R,
+    int rows_t) {
   __shared__ float sS[kMaxN * kPitch];
   __shared__ float sR[kMaxN * kPitch];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
+  if (blockIdx.x == gridDim.x - 1) zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
   const float* Sh = S_hat + (size_t)b * Ns * Nt;
@@ -231,12 +243,17 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     const float* __restrict__ w2, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, TPQ* __restrict__ dP,
     TPQ* __restrict__ dQ, float* __restrict__ dw2_part,
-    float* __restrict__ db2_part, int Ns, int Nt, int R) {
+    float* __restrict__ db2_part, int Ns, int Nt, int R, int rows_s,
+    int rows_t) {
   __shared__ float sG[kMaxN * kPitch];
   __shared__ float sP[kMaxN * kPitch];
   __shared__ float sQ[kMaxN * kPitch];
   __shared__ float sRed[kWaves * kCh];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
+  if (blockIdx.x == gridDim.x - 1) {
+    zero_tail(dP, ptr_s[gridDim.x], rows_s, R);
+    zero_tail(dQ, ptr_t[gridDim.x], rows_t, R);
+  }
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
   const float* Gb = G + (size_t)b * Ns * Nt;
@@ -387,7 +404,8 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   hipLaunchKernelGGL(softmax_transport_kernel, dim3(B), dim3(256), 0, stream(),
                      S_hat.data_ptr<float>(), r_s.data_ptr<float>(),
                      ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
-                     S.data_ptr<float>(), r_t.data_ptr<float>(), Ns, Nt, R);
+                     S.data_ptr<float>(), r_t.data_ptr<float>(), Ns, Nt, R,
+                     (int)rows_t);
   DGMC_CHECK_LAUNCH();
   return {S, r_t};
 }
@@ -479,7 +497,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
                        ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
                        reinterpret_cast<T*>(dP.data_ptr()),
                        reinterpret_cast<T*>(dQ.data_ptr()),
-                       dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R);
+                       dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R,
+                       (int)P.size(0), (int)Q.size(0));
   });
   DGMC_CHECK_LAUNCH();
   return {dP, dQ, dw2, db2};

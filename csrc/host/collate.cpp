@@ -114,6 +114,134 @@ std::vector<Tensor> collate_pairs(const Tensor& node_ptr, const Tensor& edge_ptr
           batch_s,    batch_t,    counts_s,   counts_t,   y};
 }
 
+// Static-shape variant for hipGraph replay: writes every index array of the
+// batch, padded to fixed capacities, into ONE preallocated (pinned) int64
+// buffer so a single H2D copy refreshes all inputs of a captured step.
+// Layout (int64 words):
+//   node_s[cs] node_t[ct] eattr_s[es] eattr_t[et] ei_s[2*es] ei_t[2*et]
+//   y[cs] ymask[cs] dense_s[cs] dense_t[ct] ptr_s[B+1] ptr_t[B+1]
+// Padding: node gather -> zero_node, edge-attr gather -> zero_edge, padded
+// edges connect the last padding node to itself, dense index -> B*n_max
+// (trash slot), y -> 0 with ymask 0.  Returns false (buffer untouched
+// semantics irrelevant) if the batch does not fit the capacities.
+bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
+                          const Tensor& edge_local, const Tensor& node_class,
+                          const Tensor& pos_of_class, const Tensor& s_ids,
+                          const Tensor& t_ids, Tensor out, int64_t cap_s,
+                          int64_t cap_t, int64_t ecap_s, int64_t ecap_t,
+                          int64_t n_max, int64_t zero_node, int64_t zero_edge) {
+  check_cpu_long(node_ptr, "node_ptr");
+  check_cpu_long(edge_ptr, "edge_ptr");
+  check_cpu_long(edge_local, "edge_local");
+  check_cpu_long(node_class, "node_class");
+  check_cpu_long(pos_of_class, "pos_of_class");
+  check_cpu_long(s_ids, "s_ids");
+  check_cpu_long(t_ids, "t_ids");
+  check_cpu_long(out, "out");
+  const int64_t B = s_ids.numel();
+  TORCH_CHECK(t_ids.numel() == B, "s_ids / t_ids size mismatch");
+  const int64_t need = cap_s * 4 + cap_t * 2 + ecap_s * 3 + ecap_t * 3 +
+                       2 * (B + 1);
+  TORCH_CHECK(out.numel() >= need, "collate_pairs_padded: buffer too small");
+  const int64_t G = node_ptr.numel() - 1;
+  const int64_t C = pos_of_class.size(1);
+  const int64_t E_all = edge_local.size(1);
+  const int64_t* np_ = node_ptr.data_ptr<int64_t>();
+  const int64_t* ep_ = edge_ptr.data_ptr<int64_t>();
+  const int64_t* src_ = edge_local.data_ptr<int64_t>();
+  const int64_t* dst_ = src_ + E_all;
+  const int64_t* cls_ = node_class.data_ptr<int64_t>();
+  const int64_t* poc_ = pos_of_class.data_ptr<int64_t>();
+  const int64_t* sid = s_ids.data_ptr<int64_t>();
+  const int64_t* tid = t_ids.data_ptr<int64_t>();
+
+  std::vector<int64_t> ns_off(B + 1, 0), nt_off(B + 1, 0), es_off(B + 1, 0),
+      et_off(B + 1, 0);
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t gs = sid[b], gt = tid[b];
+    TORCH_CHECK(gs >= 0 && gs < G && gt >= 0 && gt < G, "graph id out of range");
+    const int64_t cs = np_[gs + 1] - np_[gs], ct = np_[gt + 1] - np_[gt];
+    TORCH_CHECK(cs <= n_max && ct <= n_max, "graph larger than n_max");
+    ns_off[b + 1] = ns_off[b] + cs;
+    nt_off[b + 1] = nt_off[b] + ct;
+    es_off[b + 1] = es_off[b] + (ep_[gs + 1] - ep_[gs]);
+    et_off[b + 1] = et_off[b] + (ep_[gt + 1] - ep_[gt]);
+  }
+  // At least one padding node per side hosts the padded edges.
+  if (ns_off[B] >= cap_s || nt_off[B] >= cap_t || es_off[B] > ecap_s ||
+      et_off[B] > ecap_t)
+    return false;
+
+  int64_t* o = out.data_ptr<int64_t>();
+  int64_t* node_s = o;            o += cap_s;
+  int64_t* node_t = o;            o += cap_t;
+  int64_t* ea_s = o;              o += ecap_s;
+  int64_t* ea_t = o;              o += ecap_t;
+  int64_t* ei_s0 = o;             o += ecap_s;
+  int64_t* ei_s1 = o;             o += ecap_s;
+  int64_t* ei_t0 = o;             o += ecap_t;
+  int64_t* ei_t1 = o;             o += ecap_t;
+  int64_t* yv = o;                o += cap_s;
+  int64_t* ym = o;                o += cap_s;
+  int64_t* dn_s = o;              o += cap_s;
+  int64_t* dn_t = o;              o += cap_t;
+  int64_t* ptr_s = o;             o += B + 1;
+  int64_t* ptr_t = o;             o += B + 1;
+  const int64_t trash = B * n_max;
+
+#pragma omp parallel for schedule(static)
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t gs = sid[b], gt = tid[b];
+    const int64_t n0s = np_[gs], nns = np_[gs + 1] - n0s;
+    const int64_t n0t = np_[gt], nnt = np_[gt + 1] - n0t;
+    for (int64_t i = 0; i < nns; ++i) {
+      const int64_t r = ns_off[b] + i;
+      node_s[r] = n0s + i;
+      const int64_t c = cls_[n0s + i];
+      const int64_t yy = (c >= 0 && c < C) ? poc_[gt * C + c] : -1;
+      yv[r] = yy >= 0 ? yy : 0;
+      ym[r] = yy >= 0 ? 1 : 0;
+      dn_s[r] = b * n_max + i;
+    }
+    for (int64_t i = 0; i < nnt; ++i) {
+      const int64_t r = nt_off[b] + i;
+      node_t[r] = n0t + i;
+      dn_t[r] = b * n_max + i;
+    }
+    const int64_t e0s = ep_[gs], nes = ep_[gs + 1] - e0s;
+    for (int64_t e = 0; e < nes; ++e) {
+      const int64_t r = es_off[b] + e;
+      ea_s[r] = e0s + e;
+      ei_s0[r] = src_[e0s + e] + ns_off[b];
+      ei_s1[r] = dst_[e0s + e] + ns_off[b];
+    }
+    const int64_t e0t = ep_[gt], net = ep_[gt + 1] - e0t;
+    for (int64_t e = 0; e < net; ++e) {
+      const int64_t r = et_off[b] + e;
+      ea_t[r] = e0t + e;
+      ei_t0[r] = src_[e0t + e] + nt_off[b];
+      ei_t1[r] = dst_[e0t + e] + nt_off[b];
+    }
+  }
+  for (int64_t r = ns_off[B]; r < cap_s; ++r) {
+    node_s[r] = zero_node; yv[r] = 0; ym[r] = 0; dn_s[r] = trash;
+  }
+  for (int64_t r = nt_off[B]; r < cap_t; ++r) {
+    node_t[r] = zero_node; dn_t[r] = trash;
+  }
+  for (int64_t r = es_off[B]; r < ecap_s; ++r) {
+    ea_s[r] = zero_edge; ei_s0[r] = cap_s - 1; ei_s1[r] = cap_s - 1;
+  }
+  for (int64_t r = et_off[B]; r < ecap_t; ++r) {
+    ea_t[r] = zero_edge; ei_t0[r] = cap_t - 1; ei_t1[r] = cap_t - 1;
+  }
+  for (int64_t b = 0; b <= B; ++b) {
+    ptr_s[b] = ns_off[b];
+    ptr_t[b] = nt_off[b];
+  }
+  return true;
+}
+
 // CSR (rowptr, perm) of an index vector over [0, n): stable counting sort.
 std::vector<Tensor> counting_sort(const Tensor& index, int64_t n) {
   check_cpu_long(index, "index");
@@ -141,9 +269,15 @@ TORCH_LIBRARY(dgmc_host, m) {
       "Tensor node_class, Tensor pos_of_class, Tensor s_ids, Tensor t_ids) -> "
       "Tensor[]");
   m.def("counting_sort(Tensor index, int n) -> Tensor[]");
+  m.def(
+      "collate_pairs_padded(Tensor node_ptr, Tensor edge_ptr, Tensor "
+      "edge_local, Tensor node_class, Tensor pos_of_class, Tensor s_ids, "
+      "Tensor t_ids, Tensor(a!) out, int cap_s, int cap_t, int ecap_s, int "
+      "ecap_t, int n_max, int zero_node, int zero_edge) -> bool");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_host, CPU, m) {
   m.impl("collate_pairs", &dgmc_host::collate_pairs);
   m.impl("counting_sort", &dgmc_host::counting_sort);
+  m.impl("collate_pairs_padded", &dgmc_host::collate_pairs_padded);
 }

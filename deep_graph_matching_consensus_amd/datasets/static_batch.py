@@ -1,0 +1,184 @@
+"""Static-shape pair batches for hipGraph-captured training steps.
+
+A captured graph replays fixed kernels on fixed addresses, but every pair
+batch has a different number of nodes/edges.  :class:`StaticPairBatcher`
+pads each batch to capacities estimated once from the dataset (node/edge
+totals per side, plus the per-graph bound ``n_max``) and keeps ALL per-step
+inputs in one static int64 device buffer:
+
+* host: the native collator (``dgmc_host::collate_pairs_padded``) writes the
+  padded index arrays into a pinned staging buffer (double-buffered, guarded
+  by events so the host never overwrites a buffer an H2D copy still reads);
+* one ``non_blocking`` H2D copy refreshes the device buffer;
+* :meth:`materialize` (captured inside the graph) gathers node features and
+  edge attributes from the HBM-resident :class:`GraphStore` and exposes the
+  batch with the reference attribute names plus ``y_mask``.
+
+Padding is inert: padded nodes have zero features, belong to no pair (the
+per-pair kernels address rows through ``ptr``), are routed to a trash slot of
+the dense grid, carry only self-loop padded edges, and are masked out of the
+loss/metrics.  Batches that exceed a capacity (vanishingly rare with the 6
+sigma headroom) are reported so the caller can run that step eagerly.
+"""
+import numpy as np
+import torch
+
+from ..graph.data import Batch
+from ..graph.meta import StaticBatchInfo, register_batch_info
+
+
+def _round_up(x, m):
+    return int((int(x) + m - 1) // m * m)
+
+
+class StaticPairBatcher(object):
+    r"""Fixed-capacity pair batches drawn from a :class:`GraphStore`.
+
+    Args:
+        store (GraphStore): HBM-resident graphs.
+        batch_size (int): pairs per step.
+        sources (array, optional): source graph ids (e.g. a rank shard).
+        seed (int): host RNG seed.
+        probe_batches (int): batches sampled to size the capacities.
+        headroom (float): multiplicative slack on the probed maxima.
+    """
+
+    def __init__(self, store, batch_size, sources=None, seed=0,
+                 probe_batches=256, headroom=1.04, n_max=None):
+        self.store = store
+        self.B = int(batch_size)
+        self.rng = np.random.default_rng(seed)
+        self.sources = np.arange(store.num_graphs) if sources is None \
+            else np.asarray(sources, dtype=np.int64)
+        counts = store.node_ptr[1:] - store.node_ptr[:-1]
+        self.n_max = int(counts.max()) if n_max is None else int(n_max)
+        self._size_capacities(probe_batches, headroom)
+        self.device = store.device
+
+        # Zero feature row / zero edge-attr row appended once for padding.
+        self.zero_node = int(store.node_ptr[-1])
+        self.zero_edge = int(store.edge_ptr[-1])
+        self.x = torch.cat([store.x, store.x.new_zeros(1, store.x.size(1))])
+        self.edge_attr = None if store.edge_attr is None else torch.cat(
+            [store.edge_attr,
+             store.edge_attr.new_zeros(1, store.edge_attr.size(1))])
+
+        cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
+            self.B
+        self.words = cs * 4 + ct * 2 + es * 3 + et * 3 + 2 * (B + 1)
+        pin = self.device.type == 'cuda'
+        self._host = [torch.zeros(self.words, dtype=torch.long,
+                                  pin_memory=pin) for _ in range(2)]
+        self._events = [None, None]
+        self._slot = 0
+        self.buf = torch.zeros(self.words, dtype=torch.long,
+                               device=self.device)
+        self._views()
+        self.batch_s = torch.zeros(cs, dtype=torch.long, device=self.device)
+        self.batch_t = torch.zeros(ct, dtype=torch.long, device=self.device)
+        self._order = None
+        self._pos = 0
+        self.overflows = 0
+
+    # ------------------------------------------------------------------
+    def _size_capacities(self, probes, headroom):
+        st = self.store
+        n = st.node_ptr[1:] - st.node_ptr[:-1]
+        e = st.edge_ptr[1:] - st.edge_ptr[:-1]
+        rng = np.random.default_rng(12345)
+        mx = np.zeros(4)
+        for _ in range(probes):
+            s = rng.choice(self.sources, size=self.B,
+                           replace=len(self.sources) < self.B)
+            t = st.sample_partners(s, rng)
+            mx = np.maximum(mx, [n[s].sum(), n[t].sum(), e[s].sum(),
+                                 e[t].sum()])
+        self.cap_s = _round_up(mx[0] * headroom + 1, 64)
+        self.cap_t = _round_up(mx[1] * headroom + 1, 64)
+        self.ecap_s = _round_up(mx[2] * headroom, 256)
+        self.ecap_t = _round_up(mx[3] * headroom, 256)
+
+    def _views(self):
+        cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
+            self.B
+        o = 0
+        v = {}
+        for name, n in [('node_s', cs), ('node_t', ct), ('ea_s', es),
+                        ('ea_t', et), ('ei_s', 2 * es), ('ei_t', 2 * et),
+                        ('y', cs), ('ymask', cs), ('dense_s', cs),
+                        ('dense_t', ct), ('ptr_s', B + 1), ('ptr_t', B + 1)]:
+            v[name] = self.buf[o:o + n]
+            o += n
+        v['ei_s'] = v['ei_s'].view(2, es)
+        v['ei_t'] = v['ei_t'].view(2, et)
+        self.v = v
+
+    # ------------------------------------------------------------------
+    def next_ids(self):
+        """Next sources (epoch permutation) and random valid partners."""
+        if self._order is None or self._pos + self.B > len(self._order):
+            self._order = self.rng.permutation(self.sources)
+            self._pos = 0
+        s = self._order[self._pos:self._pos + self.B]
+        self._pos += self.B
+        return s, self.store.sample_partners(s, self.rng)
+
+    def load(self, s_ids=None, t_ids=None):
+        """Stage the next batch into the static device buffer.
+
+        Returns False (buffer unchanged) if the batch exceeds a capacity.
+        """
+        if s_ids is None:
+            s_ids, t_ids = self.next_ids()
+        slot = self._slot
+        self._slot ^= 1
+        if self._events[slot] is not None:
+            self._events[slot].synchronize()
+        host = self._host[slot]
+        st = self.store
+        ok = torch.ops.dgmc_host.collate_pairs_padded(
+            st._node_ptr_t, st._edge_ptr_t, st.edge_local, st.node_class,
+            st.pos_of_class,
+            torch.from_numpy(np.ascontiguousarray(s_ids, dtype=np.int64)),
+            torch.from_numpy(np.ascontiguousarray(t_ids, dtype=np.int64)),
+            host, self.cap_s, self.cap_t, self.ecap_s, self.ecap_t,
+            self.n_max, self.zero_node, self.zero_edge)
+        if not ok:
+            self.overflows += 1
+            return False
+        self.buf.copy_(host, non_blocking=True)
+        if self.device.type == 'cuda':
+            ev = torch.cuda.Event()
+            ev.record()
+            self._events[slot] = ev
+        return True
+
+    def materialize(self):
+        """Device-side batch from the static buffer (graph-capturable)."""
+        v = self.v
+        batch = Batch()
+        batch.x_s = self.x.index_select(0, v['node_s'])
+        batch.x_t = self.x.index_select(0, v['node_t'])
+        batch.edge_index_s, batch.edge_index_t = v['ei_s'], v['ei_t']
+        if self.edge_attr is not None:
+            batch.edge_attr_s = self.edge_attr.index_select(0, v['ea_s'])
+            batch.edge_attr_t = self.edge_attr.index_select(0, v['ea_t'])
+        batch.y = v['y']
+        batch.y_mask = v['ymask'].to(torch.bool)
+        ptr_s = v['ptr_s'].to(torch.int32)
+        ptr_t = v['ptr_t'].to(torch.int32)
+        info_s = StaticBatchInfo(self.B, self.n_max, self.cap_s,
+                                 ptr_s[1:] - ptr_s[:-1], ptr_s, v['dense_s'])
+        info_t = StaticBatchInfo(self.B, self.n_max, self.cap_t,
+                                 ptr_t[1:] - ptr_t[:-1], ptr_t, v['dense_t'])
+        batch.x_s_batch, batch.x_t_batch = self.batch_s, self.batch_t
+        register_batch_info(self.batch_s, info_s)
+        register_batch_info(self.batch_t, info_t)
+        batch.__num_graphs__ = self.B
+        return batch
+
+    def __repr__(self):
+        return ('{}(B={}, n_max={}, cap_s={}, cap_t={}, ecap_s={}, '
+                'ecap_t={})').format(type(self).__name__, self.B, self.n_max,
+                                     self.cap_s, self.cap_t, self.ecap_s,
+                                     self.ecap_t)

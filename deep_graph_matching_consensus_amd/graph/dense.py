@@ -25,30 +25,37 @@ class DenseLayout(object):
         self.counts = info.device_tensor('counts', device, torch.int32)
         self.ptr = info.device_tensor('ptr', device, torch.int32)
         self.num_nodes = info.num_nodes
+        # Static (padded) batches route padding rows to a trash slot B*N.
+        self.trash = bool(getattr(info, 'has_trash', False))
         self._mask = None
 
     @property
     def mask(self):
         """``[B, N_max]`` bool validity mask."""
         if self._mask is None:
-            m = torch.zeros(self.B * self.N, dtype=torch.bool,
-                            device=self.device)
+            m = torch.zeros(self.B * self.N + int(self.trash),
+                            dtype=torch.bool, device=self.device)
             m[self.index] = True
-            self._mask = m.view(self.B, self.N)
+            self._mask = m[:self.B * self.N].view(self.B, self.N)
         return self._mask
 
     def to_dense(self, x, fill_value=0.):
         """``[sum N, *]`` -> ``[B, N_max, *]`` (padding = ``fill_value``)."""
-        feat = x.shape[1:]
-        out = x.new_full((self.B * self.N, ) + tuple(feat), fill_value)
+        feat = tuple(x.shape[1:])
+        rows = self.B * self.N
+        out = x.new_full((rows + int(self.trash), ) + feat, fill_value)
         out = out.index_copy(0, self.index, x)
-        return out.view((self.B, self.N) + tuple(feat))
+        if self.trash:
+            out = out[:rows]
+        return out.view((self.B, self.N) + feat)
 
     def to_sparse(self, x):
         """``[B, N_max, *]`` -> ``[sum N, *]``."""
-        feat = x.shape[2:]
-        return x.reshape((self.B * self.N, ) + tuple(feat)).index_select(
-            0, self.index)
+        feat = tuple(x.shape[2:])
+        flat = x.reshape((self.B * self.N, ) + feat)
+        if self.trash:
+            flat = torch.cat([flat, flat.new_zeros((1, ) + feat)], dim=0)
+        return flat.index_select(0, self.index)
 
 
 class MaskLayout(object):

@@ -32,6 +32,8 @@ class BatchInfo(object):
     __slots__ = ('counts', 'ptr', 'num_graphs', 'max_nodes', 'num_nodes',
                  '_device_cache', '__weakref__')
 
+    has_trash = False
+
     def __init__(self, counts):
         counts = torch.as_tensor(counts, dtype=torch.long).cpu()
         self.counts = counts
@@ -66,13 +68,43 @@ class BatchInfo(object):
         return out
 
 
+class StaticBatchInfo(object):
+    """Batch metadata living in *static device buffers* (hipGraph replay).
+
+    Shapes are fixed by capacities: ``num_nodes`` is the padded row count,
+    ``max_nodes`` the fixed per-graph bound; padded rows map to a trash slot
+    ``B * max_nodes`` of the dense grid (``has_trash``).  The buffers are
+    refreshed in place before every replay.
+    """
+
+    has_trash = True
+
+    def __init__(self, num_graphs, max_nodes, num_nodes, counts, ptr,
+                 dense_index):
+        self.num_graphs = int(num_graphs)
+        self.max_nodes = int(max_nodes)
+        self.num_nodes = int(num_nodes)
+        self._dev = {'counts': counts, 'ptr': ptr}
+        self._dense_index = dense_index
+
+    def dense_index(self, device, max_nodes=None):
+        assert max_nodes in (None, self.max_nodes)
+        return self._dense_index
+
+    def device_tensor(self, name, device, dtype=torch.int32):
+        t = self._dev[name]
+        assert t.dtype == dtype
+        return t
+
+
 def _drop(key):
     _REGISTRY.pop(key, None)
 
 
 def register_batch_info(batch, counts):
     """Associate host-side per-graph node ``counts`` with ``batch``."""
-    info = counts if isinstance(counts, BatchInfo) else BatchInfo(counts)
+    info = counts if isinstance(counts, (BatchInfo, StaticBatchInfo)) \
+        else BatchInfo(counts)
     key = id(batch)
     _REGISTRY[key] = (weakref.ref(batch, lambda _, k=key: _drop(k)), info)
     return info

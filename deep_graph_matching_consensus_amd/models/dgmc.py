@@ -247,10 +247,18 @@ class DGMC(torch.nn.Module):
         mask = S.__idx__[y[0]] == y[1].view(-1, 1)
         return S.__val__[y[0]][mask]
 
-    def loss(self, S, y, reduction='mean'):
-        r"""Negative log-likelihood of the ground-truth correspondences."""
+    def loss(self, S, y, reduction='mean', mask=None):
+        r"""Negative log-likelihood of the ground-truth correspondences.
+
+        ``mask`` (extension): boolean ``[num_gt]`` selecting the valid ground
+        truths of a padded static batch; ``'mean'`` then averages over them.
+        """
         assert reduction in ['none', 'mean', 'sum']
         nll = -torch.log(self._gt_values(S, y) + EPS)
+        if mask is not None:
+            nll = nll * mask
+            if reduction == 'mean':
+                return nll.sum() / mask.sum().clamp(min=1)
         if reduction == 'none':
             return nll
         return nll.mean() if reduction == 'mean' else nll.sum()
@@ -262,9 +270,12 @@ class DGMC(torch.nn.Module):
         assert S.__idx__ is not None and S.__val__ is not None
         return S.__idx__[rows, S.__val__[rows].argmax(dim=-1)]
 
-    def correct(self, S, y):
+    def correct(self, S, y, mask=None):
         """Device tensor with the number of correct top-1 predictions."""
-        return (self._predict(S, y[0]) == y[1]).sum()
+        hit = self._predict(S, y[0]) == y[1]
+        if mask is not None:
+            hit = hit & mask
+        return hit.sum()
 
     def acc(self, S, y, reduction='mean'):
         r"""Top-1 accuracy (Python number, like the reference)."""

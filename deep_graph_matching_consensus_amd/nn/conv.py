@@ -105,7 +105,9 @@ class SplineConv(torch.nn.Module):
         pseudo = pseudo.unsqueeze(-1) if pseudo.dim() == 1 else pseudo
         N = x.size(0)
         plan = spline_plan(edge_index, pseudo, N, self._ks, self._open,
-                           self.degree, root=self.root is not None)
+                           self.degree, root=self.root is not None,
+                           device_params=(self.kernel_size,
+                                          self.is_open_spline))
         dtype = compute_dtype(x)
         w = self.stacked_weight()
         w_lp = cached(('spline_w_lp', id(self), dtype),

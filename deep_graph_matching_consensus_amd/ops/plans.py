@@ -71,23 +71,33 @@ def _degree(index, num_nodes):
     return deg
 
 
-def compute_spline_basis(pseudo, kernel_size, is_open_spline, degree):
-    """``(basis [E,S] fp32, weight_index [E,S] int64)`` on pseudo's device."""
+def compute_spline_basis(pseudo, kernel_size, is_open_spline, degree,
+                         device_params=None):
+    """``(basis [E,S] fp32, weight_index [E,S] int64)`` on pseudo's device.
+
+    ``device_params`` = ``(kernel_size, is_open_spline)`` tensors already on
+    the device (module buffers) - avoids host->device copies, which are not
+    allowed while a hipGraph is being captured.
+    """
     if pseudo.dim() == 1:
         pseudo = pseudo.view(-1, 1)
     if _backend.use_hip(pseudo) and pseudo.numel() > 0:
-        ks = torch.tensor(list(kernel_size), dtype=torch.int32)
-        op = torch.tensor([int(v) for v in is_open_spline], dtype=torch.int32)
+        if device_params is not None:
+            ks, op = device_params
+        else:
+            ks = torch.tensor(list(kernel_size), dtype=torch.int32).to(
+                pseudo.device)
+            op = torch.tensor([int(v) for v in is_open_spline],
+                              dtype=torch.int32).to(pseudo.device)
         basis, wi = _backend.ops().spline_basis(
-            pseudo.float().contiguous(), ks.to(pseudo.device),
-            op.to(pseudo.device), int(degree))
-        return basis, wi.long()
+            pseudo.float().contiguous(), ks, op, int(degree))
+        return basis, wi
     return ref.spline_basis(pseudo.float(), kernel_size, is_open_spline,
                             degree)
 
 
 def spline_plan(edge_index, pseudo, num_nodes, kernel_size, is_open_spline,
-                degree=1, root=True):
+                degree=1, root=True, device_params=None):
     r"""Operator ``A [N, N * (K + root)]`` so that
     ``SplineConv(x) = A @ (x @ [W_0 | ... | W_{K-1} | root]).view(-1, C)``.
     Entry ``(i, src * (K+1) + wi)`` holds ``basis / deg_in(i)`` (mean
@@ -111,7 +121,7 @@ def spline_plan(edge_index, pseudo, num_nodes, kernel_size, is_open_spline,
     N = int(num_nodes)
     if edge_index.numel() > 0:
         basis, wi = compute_spline_basis(pseudo, kernel_size, is_open_spline,
-                                         degree)
+                                         degree, device_params)
         S = basis.size(1)
         inv_deg = 1.0 / _degree(dst, N).clamp_(min=1)
         row = dst.view(-1, 1).expand(-1, S).reshape(-1)

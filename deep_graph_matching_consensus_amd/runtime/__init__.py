@@ -1,4 +1,8 @@
-"""Runtime: execution modes, hipGraph capture, profiling hooks."""
+"""Runtime: execution modes, forward caches, hipGraph capture."""
 from .mode import reference_mode, is_reference_mode, set_reference_mode
+from .cache import forward_cache, cached
+from .graphs import GraphedStep, graph_capture_supported
 
-__all__ = ['reference_mode', 'is_reference_mode', 'set_reference_mode']
+__all__ = ['reference_mode', 'is_reference_mode', 'set_reference_mode',
+           'forward_cache', 'cached', 'GraphedStep',
+           'graph_capture_supported']

@@ -227,3 +227,51 @@ def test_dgmc_sparse_gpu_matches_dense():
     S2_0, S2_L = model(x, ei, None, None, x, ei, None, None)
     assert torch.allclose(S1_0, S2_0.to_dense(), atol=1e-5)
     assert torch.allclose(S1_L, S2_L.to_dense(), atol=1e-4)
+
+
+def test_graph_captured_step_matches_eager():
+    """hipGraph replay of a static-shape step == eager on the same batch."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.runtime import GraphedStep
+    groups = make_keypoint_datasets(graphs=8, feature_dim=32, seed=0)
+    store = GraphStore(groups, DEV)
+    batcher = StaticPairBatcher(store, 24, seed=0)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(32, 32, 2, 2, cat=False),
+                 SplineCNN(16, 16, 2, 2, cat=True), num_steps=0).to(DEV)
+    rows = torch.arange(batcher.cap_s, device=DEV)
+    out = {}
+
+    def body():
+        for p in model.parameters():
+            p.grad = None
+        b = batcher.materialize()
+        with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=False):
+            S_0, _ = model(b.x_s, b.edge_index_s, b.edge_attr_s, b.x_s_batch,
+                           b.x_t, b.edge_index_t, b.edge_attr_t, b.x_t_batch)
+        y = torch.stack([rows, b.y])
+        loss = model.loss(S_0, y, mask=b.y_mask)
+        out['loss'] = loss.detach()
+        out['g'] = torch.autograd.grad(loss, model.psi_1.convs[0].weight)[0]
+
+    ids = [batcher.next_ids() for _ in range(3)]
+    assert batcher.load(*ids[0])
+    step = GraphedStep(body, warmup=2).capture()
+    results = []
+    for s, t in ids[1:]:
+        assert batcher.load(s, t)
+        step()
+        torch.cuda.synchronize()
+        replay = (out['loss'].clone(), out['g'].clone())
+        body()   # eager on the same static inputs
+        torch.cuda.synchronize()
+        results.append((replay, (out['loss'], out['g'])))
+    for (la, ga), (lb, gb) in results:
+        assert torch.isfinite(la)
+        assert torch.allclose(la, lb, atol=1e-5)
+        assert torch.allclose(ga, gb, atol=1e-5, rtol=1e-4)
+    assert not torch.allclose(results[0][0][0], results[1][0][0])

@@ -1,0 +1,83 @@
+"""Padded static batches (hipGraph path) must match dynamic batches."""
+import numpy as np
+import pytest
+import torch
+
+from deep_graph_matching_consensus_amd.datasets import (
+    GraphStore, make_keypoint_datasets)
+from deep_graph_matching_consensus_amd.datasets.static_batch import \
+    StaticPairBatcher
+from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+from deep_graph_matching_consensus_amd.ops import _backend
+
+
+def _setup(device='cpu'):
+    groups = make_keypoint_datasets(graphs=8, feature_dim=16, seed=4)
+    store = GraphStore(groups, device)
+    batcher = StaticPairBatcher(store, 12, seed=0)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(16, 16, 2, 2, cat=False),
+                 SplineCNN(8, 8, 2, 2, cat=True), num_steps=0).to(device)
+    model.eval()
+    return store, batcher, model
+
+
+def _run(model, batch, rows, mask):
+    S_0, S_L = model(batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+                     batch.x_s_batch, batch.x_t, batch.edge_index_t,
+                     batch.edge_attr_t, batch.x_t_batch)
+    y = torch.stack([rows, batch.y])
+    return S_0, S_L, model.loss(S_0, y, mask=mask)
+
+
+@pytest.mark.skipif(not _backend.host_available(),
+                    reason='native host library not built')
+def test_static_equals_dynamic_cpu():
+    store, batcher, model = _setup()
+    s, t = batcher.next_ids()
+    dyn = store.collate(s, t)
+    assert batcher.load(s, t)
+    sta = batcher.materialize()
+    n_s = dyn.x_s.size(0)
+    assert sta.x_s.size(0) == batcher.cap_s > n_s
+    assert int(sta.y_mask.sum()) == n_s
+    assert torch.equal(sta.y[:n_s], dyn.y)
+
+    a0, _, la = _run(model, dyn, torch.arange(n_s), None)
+    grads_a = torch.autograd.grad(la, list(model.parameters()),
+                                  allow_unused=True)
+    b0, _, lb = _run(model, sta, torch.arange(batcher.cap_s), sta.y_mask)
+    grads_b = torch.autograd.grad(lb, list(model.parameters()),
+                                  allow_unused=True)
+    N_t = a0.size(1)
+    assert torch.allclose(a0, b0[:n_s, :N_t], atol=1e-6)
+    assert torch.allclose(la, lb, atol=1e-6)
+    for ga, gb in zip(grads_a, grads_b):
+        if ga is None:
+            assert gb is None or gb.abs().max() == 0
+        else:
+            assert torch.allclose(ga, gb, atol=1e-5)
+
+
+@pytest.mark.skipif(not _backend.host_available(),
+                    reason='native host library not built')
+def test_static_consensus_finite_cpu():
+    store, batcher, model = _setup()
+    model.num_steps = 2
+    model.train()
+    assert batcher.load()
+    sta = batcher.materialize()
+    _, S_L, loss = _run(model, sta, torch.arange(batcher.cap_s), sta.y_mask)
+    loss.backward()
+    assert torch.isfinite(loss)
+    for p in model.parameters():
+        assert p.grad is None or torch.isfinite(p.grad).all()
+
+
+def test_capacity_covers_probe():
+    store, batcher, _ = _setup()
+    n = store.node_ptr[1:] - store.node_ptr[:-1]
+    rng = np.random.default_rng(7)
+    for _ in range(20):
+        s, t = batcher.next_ids()
+        assert n[s].sum() < batcher.cap_s and n[t].sum() < batcher.cap_t
