@@ -25,6 +25,7 @@ import torch
 
 from ..graph.data import Batch
 from ..graph.meta import StaticBatchInfo, register_batch_info
+from ..ops import _backend
 
 
 def _round_up(x, m):
@@ -45,6 +46,9 @@ class StaticPairBatcher(object):
 
     def __init__(self, store, batch_size, sources=None, seed=0,
                  probe_batches=256, headroom=1.04, n_max=None):
+        if not _backend.host_available():
+            raise RuntimeError('StaticPairBatcher needs the native host '
+                               'library (_C_host.so); build it first')
         self.store = store
         self.B = int(batch_size)
         self.rng = np.random.default_rng(seed)

@@ -261,12 +261,13 @@ def test_graph_captured_step_matches_eager():
     ids = [batcher.next_ids() for _ in range(3)]
     assert batcher.load(*ids[0])
     step = GraphedStep(body, warmup=2).capture()
+    graph_out = dict(out)   # tensors owned by the captured graph
     results = []
     for s, t in ids[1:]:
         assert batcher.load(s, t)
         step()
         torch.cuda.synchronize()
-        replay = (out['loss'].clone(), out['g'].clone())
+        replay = (graph_out['loss'].clone(), graph_out['g'].clone())
         body()   # eager on the same static inputs
         torch.cuda.synchronize()
         results.append((replay, (out['loss'], out['g'])))
