@@ -121,7 +121,7 @@ std::vector<Tensor> collate_pairs(const Tensor& node_ptr, const Tensor& edge_ptr
 //   node_s[cs] node_t[ct] eattr_s[es] eattr_t[et] ei_s[2*es] ei_t[2*et]
 //   y[cs] ymask[cs] dense_s[cs] dense_t[ct] ptr_s[B+1] ptr_t[B+1]
 // Padding: node gather -> zero_node, edge-attr gather -> zero_edge, padded
-// edges connect the last padding node to itself, dense index -> B*n_max
+// edges are self-loops on the padding nodes, dense index -> B*n_max
 // (trash slot), y -> 0 with ymask 0.  Returns false (buffer untouched
 // semantics irrelevant) if the batch does not fit the capacities.
 bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
@@ -229,11 +229,17 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   for (int64_t r = nt_off[B]; r < cap_t; ++r) {
     node_t[r] = zero_node; dn_t[r] = trash;
   }
+  // Padded edges are self-loops spread round-robin over ALL padding nodes so
+  // no single row of the sparse operators becomes a hub (one hub row of
+  // ~1k entries serialised a whole SpMM launch).
+  const int64_t pad_s = cap_s - ns_off[B], pad_t = cap_t - nt_off[B];
   for (int64_t r = es_off[B]; r < ecap_s; ++r) {
-    ea_s[r] = zero_edge; ei_s0[r] = cap_s - 1; ei_s1[r] = cap_s - 1;
+    const int64_t node = ns_off[B] + (r - es_off[B]) % pad_s;
+    ea_s[r] = zero_edge; ei_s0[r] = node; ei_s1[r] = node;
   }
   for (int64_t r = et_off[B]; r < ecap_t; ++r) {
-    ea_t[r] = zero_edge; ei_t0[r] = cap_t - 1; ei_t1[r] = cap_t - 1;
+    const int64_t node = nt_off[B] + (r - et_off[B]) % pad_t;
+    ea_t[r] = zero_edge; ei_t0[r] = node; ei_t1[r] = node;
   }
   for (int64_t b = 0; b <= B; ++b) {
     ptr_s[b] = ns_off[b];
