@@ -37,9 +37,7 @@ from deep_graph_matching_consensus_amd import parallel  # noqa: E402
 from deep_graph_matching_consensus_amd.datasets import (  # noqa: E402
     PASCAL_VOC_CATEGORIES, WILLOW_CATEGORIES, DevicePairLoader, GraphStore,
     make_keypoint_datasets)
-from deep_graph_matching_consensus_amd.datasets.static_batch import (  # noqa
-    StaticPairBatcher)
-from deep_graph_matching_consensus_amd.runtime import GraphedStep  # noqa
+from deep_graph_matching_consensus_amd.train import PairTrainer  # noqa
 from deep_graph_matching_consensus_amd.models import (  # noqa: E402
     DGMC, SplineCNN)
 from deep_graph_matching_consensus_amd.runtime import reference_mode  # noqa
@@ -75,6 +73,11 @@ def parse_args(argv=None):
     p.add_argument('--no-overlap', action='store_true')
     p.add_argument('--no-graph', action='store_true',
                    help='disable hipGraph capture of the training step')
+    p.add_argument('--mode', default=None,
+                   choices=['graph', 'static', 'eager'],
+                   help='execution mode (default: graph on GPU, else eager)')
+    p.add_argument('--eval-pairs', type=int, default=0,
+                   help='evaluate test Hits@1/@10 on this many pairs')
     p.add_argument('--json-out', default=None)
     return p.parse_args(argv)
 
@@ -101,73 +104,17 @@ def main(argv=None):
     store = GraphStore(groups, device,
                        x_dtype=torch.bfloat16 if use_bf16 else torch.float32,
                        valid_pairs=True)
-    shard = torch.arange(store.num_graphs)[rank::world].numpy()
-    use_graph = (device.type == 'cuda' and not reference and
-                 not args.no_graph)
+    mode = args.mode
+    if mode is None:
+        mode = 'graph' if device.type == 'cuda' else 'eager'
+    if reference or args.no_graph and mode == 'graph':
+        mode = 'eager'
 
     model = build_model(cfg, args, groups[0].num_node_features,
                         groups[0].num_edge_features, device)
-    model.train()
-    reducer = parallel.GradBucketAllReducer(
-        model, overlap=not (args.no_overlap or use_graph))
-    fused = device.type == 'cuda'
-    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3, fused=fused,
-                                 capturable=use_graph)
-    stats = torch.zeros(3, dtype=torch.float64, device=device)
-    autocast = dict(device_type=device.type, dtype=torch.bfloat16,
-                    enabled=use_bf16, cache_enabled=False)
-
-    def forward_loss(batch, rows, mask):
-        with torch.autocast(**autocast):
-            S_0, S_L = model(batch.x_s, batch.edge_index_s,
-                             batch.edge_attr_s, batch.x_s_batch, batch.x_t,
-                             batch.edge_index_t, batch.edge_attr_t,
-                             batch.x_t_batch)
-        y = torch.stack([rows, batch.y], dim=0)
-        loss = model.loss(S_0, y, mask=mask)
-        if model.num_steps > 0:
-            loss = model.loss(S_L, y, mask=mask) + loss
-        loss.backward()
-        stats[0] += loss.detach().double()
-        stats[1] += model.correct(S_L.detach(), y, mask).double()
-        stats[2] += y.size(1) if mask is None else mask.sum().double()
-
-    overflows = 0
-    if use_graph:
-        # Static shapes + whole-step hipGraph (zero-grad, gather, forward,
-        # backward and - on one GPU - the optimizer update).
-        batcher = StaticPairBatcher(store, args.batch_size, sources=shard,
-                                    seed=args.seed + 1000 * rank)
-        rows = torch.arange(batcher.cap_s, device=device)
-
-        def body():
-            reducer.flat.zero_()
-            batch = batcher.materialize()
-            forward_loss(batch, rows, batch.y_mask)
-            if world == 1:
-                optimizer.step()
-
-        step_graph = GraphedStep(body, warmup=3)
-
-        def train_step():
-            while not batcher.load():
-                pass
-            step_graph()
-            if world > 1:
-                reducer.finish()
-                optimizer.step()
-    else:
-        loader = DevicePairLoader(store, args.batch_size, sources=shard,
-                                  seed=args.seed + 1000 * rank)
-        batches = loader.forever()
-
-        def train_step():
-            batch = next(batches)
-            reducer.zero_grad()
-            rows = torch.arange(batch.y.numel(), device=device)
-            forward_loss(batch, rows, None)
-            reducer.finish()
-            optimizer.step()
+    trainer = PairTrainer(model, store, args.batch_size, lr=1e-3, mode=mode,
+                          bf16=use_bf16, seed=args.seed,
+                          overlap=not args.no_overlap)
 
     def sync():
         if device.type == 'cuda':
@@ -175,21 +122,33 @@ def main(argv=None):
 
     with reference_mode(reference):
         for _ in range(args.warmup):
-            train_step()
-        stats.zero_()
+            trainer.step()
+        trainer.stats.zero_()
         parallel.barrier()
         sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            train_step()
+            trainer.step()
         sync()
         parallel.barrier()
         elapsed = time.perf_counter() - t0
-    if use_graph:
-        overflows = batcher.overflows
+        test_hits = None
+        if args.eval_pairs > 0:
+            test_groups = make_keypoint_datasets(
+                cfg['categories'], graphs=max(args.graphs_per_category // 4,
+                                              8),
+                visible_prob=cfg['visible_prob'], seed=args.seed,
+                split='test')
+            test_store = GraphStore(test_groups, device,
+                                    x_dtype=store.x.dtype)
+            test_hits = trainer.evaluate(test_store, args.eval_pairs)
+    use_graph = trainer.mode == 'graph'
+    overflows = trainer.batcher.overflows if trainer.mode != 'eager' else 0
+    run_stats = trainer.read_stats()
+    stats = torch.tensor([run_stats['loss_sum'], run_stats['correct'],
+                          run_stats['count']], dtype=torch.float64)
 
     elapsed = parallel.all_reduce_max(elapsed, device)
-    parallel.all_reduce_sum(stats)
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     pairs = args.batch_size * world * args.steps
     value = pairs / elapsed
@@ -230,11 +189,15 @@ def main(argv=None):
             'impl': args.impl,
             'consensus_steps': args.num_steps,
             'hipgraph': bool(use_graph),
+            'mode': trainer.mode,
         },
         'hits@1_train': round(hits1, 4) if hits1 is not None else None,
         'loss': round(mean_loss, 4),
         'capacity_overflows': overflows,
     }
+    if test_hits is not None:
+        out['hits@1_test'] = round(test_hits[1], 4)
+        out['hits@10_test'] = round(test_hits[10], 4)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -1,0 +1,235 @@
+"""Training/evaluation driver shared by ``bench.py`` and ``examples/``.
+
+The reference drivers (``/root/reference/examples/pascal.py:60-99``,
+``willow.py:60-140``) loop over a host DataLoader, call ``.item()`` twice per
+step and keep the model in a single process.  :class:`PairTrainer` runs the
+same objective (``NLL(S_0) + NLL(S_L)``, ``pascal.py:70-72``) in one of three
+execution modes:
+
+* ``'eager'``  - dynamic batches from :class:`DevicePairLoader`, gradient
+  all-reduce overlapped with backward;
+* ``'static'`` - fixed-capacity padded batches (:class:`StaticPairBatcher`),
+  eager execution (useful on CPU and for debugging the graph path);
+* ``'graph'``  - static batches + the whole step (gather, forward, backward,
+  optimizer) captured once into a hipGraph and replayed.
+
+Metrics are accumulated on the device and synchronised only when read.
+Checkpoints store the model in the reference state-dict schema plus
+optimizer state, step counter and RNG states (resume support).
+"""
+import json
+import os
+import random
+import time
+
+import numpy as np
+import torch
+
+from . import parallel
+from .datasets.device_loader import DevicePairLoader
+from .datasets.static_batch import StaticPairBatcher
+from .runtime.graphs import GraphedStep
+
+
+class PairTrainer(object):
+    r"""DGMC trainer over an HBM-resident :class:`GraphStore`.
+
+    Args:
+        model (DGMC): the matching model (already on ``device``).
+        store (GraphStore): training graphs.
+        batch_size (int): pairs per step and rank.
+        lr (float): Adam learning rate.
+        mode (str): ``'eager'``, ``'static'`` or ``'graph'``.
+        bf16 (bool): bf16 autocast for the encoder GEMMs.
+        seed (int): data-order seed (offset by rank).
+        overlap (bool): overlap gradient all-reduce with backward (eager).
+    """
+
+    def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
+                 bf16=True, seed=0, overlap=True, sources=None):
+        self.model = model
+        self.store = store
+        self.device = store.device
+        self.rank, self.world = parallel.rank(), parallel.world_size()
+        if mode == 'graph' and self.device.type != 'cuda':
+            mode = 'static'
+        self.mode = mode
+        self.bf16 = bf16 and self.device.type == 'cuda'
+        if sources is None:
+            sources = np.arange(store.num_graphs)[self.rank::self.world]
+        self.reducer = parallel.GradBucketAllReducer(
+            model, overlap=overlap and mode == 'eager')
+        cuda = self.device.type == 'cuda'
+        self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
+                                          fused=cuda,
+                                          capturable=mode == 'graph')
+        self.stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self.step_count = 0
+        data_seed = seed + 1000 * self.rank
+        if mode == 'eager':
+            self.loader = DevicePairLoader(store, batch_size, sources=sources,
+                                           seed=data_seed)
+            self._batches = self.loader.forever()
+        else:
+            self.batcher = StaticPairBatcher(store, batch_size,
+                                             sources=sources, seed=data_seed)
+            self._rows = torch.arange(self.batcher.cap_s, device=self.device)
+            self._graph = GraphedStep(self._static_body, warmup=2) \
+                if mode == 'graph' else None
+
+    # ------------------------------------------------------------------
+    def _autocast(self):
+        return torch.autocast(device_type=self.device.type,
+                              dtype=torch.bfloat16, enabled=self.bf16,
+                              cache_enabled=False)
+
+    def _forward_backward(self, batch, rows, mask):
+        model = self.model
+        with self._autocast():
+            S_0, S_L = model(batch.x_s, batch.edge_index_s,
+                             batch.edge_attr_s, batch.x_s_batch, batch.x_t,
+                             batch.edge_index_t, batch.edge_attr_t,
+                             batch.x_t_batch)
+        y = torch.stack([rows, batch.y], dim=0)
+        loss = model.loss(S_0, y, mask=mask)
+        if model.num_steps:
+            loss = model.loss(S_L, y, mask=mask) + loss
+        loss.backward()
+        self.stats[0] += loss.detach().double()
+        self.stats[1] += model.correct(S_L.detach(), y, mask).double()
+        self.stats[2] += y.size(1) if mask is None else mask.sum().double()
+
+    def _static_body(self):
+        self.reducer.flat.zero_()
+        batch = self.batcher.materialize()
+        self._forward_backward(batch, self._rows, batch.y_mask)
+        if self.world == 1:
+            self.optimizer.step()
+
+    def step(self):
+        """One training step (data, forward, backward, all-reduce, Adam)."""
+        self.model.train()
+        if self.mode == 'eager':
+            batch = next(self._batches)
+            self.reducer.zero_grad()
+            rows = torch.arange(batch.y.numel(), device=self.device)
+            self._forward_backward(batch, rows, None)
+            self.reducer.finish()
+            self.optimizer.step()
+        else:
+            while not self.batcher.load():
+                pass
+            if self._graph is not None:
+                self._graph()
+            else:
+                self._static_body()
+            if self.world > 1:
+                self.reducer.finish()
+                self.optimizer.step()
+        self.step_count += 1
+
+    def read_stats(self, reset=True):
+        """``(mean loss, Hits@1)`` over the steps since the last reset,
+        reduced over ranks (one host synchronisation)."""
+        s = self.stats.clone()
+        parallel.all_reduce_sum(s)
+        out = {'loss_sum': float(s[0]), 'correct': float(s[1]),
+               'count': float(s[2]),
+               'hits@1': float(s[1] / s[2]) if s[2] > 0 else None}
+        if reset:
+            self.stats.zero_()
+        return out
+
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def evaluate(self, store, num_pairs=1024, batch_size=None, seed=123,
+                 k=(1, 10)):
+        """Hits@k of ``S_L`` (fraction of ground-truth nodes) on
+        ``num_pairs`` random valid pairs of ``store``."""
+        model = self.model
+        was_training = model.training
+        model.eval()
+        bs = batch_size or min(num_pairs, 512)
+        loader = DevicePairLoader(store, bs, shuffle=True, drop_last=False,
+                                  seed=seed)
+        seen, gt, hits = 0, 0, {kk: 0 for kk in k}
+        while seen < num_pairs:
+            for batch in loader:
+                with self._autocast():
+                    _, S_L = model(batch.x_s, batch.edge_index_s,
+                                   batch.edge_attr_s, batch.x_s_batch,
+                                   batch.x_t, batch.edge_index_t,
+                                   batch.edge_attr_t, batch.x_t_batch)
+                y = torch.stack([torch.arange(batch.y.numel(),
+                                              device=self.device), batch.y])
+                for kk in k:
+                    hits[kk] += model.hits_at_k(kk, S_L, y, reduction='sum')
+                gt += y.size(1)
+                seen += batch.num_graphs
+                if seen >= num_pairs:
+                    break
+        model.train(was_training)
+        return {kk: v / max(gt, 1) for kk, v in hits.items()}
+
+    # ------------------------------------------------------------------
+    def state_dict(self):
+        """Checkpoint content; every leaf is a tensor or a Python primitive
+        so it loads with ``torch.load(..., weights_only=True)``."""
+        np_state = np.random.get_state()
+        state = {
+            'model': self.model.state_dict(),
+            'optimizer': self.optimizer.state_dict(),
+            'step': self.step_count,
+            'rng': {
+                'torch': torch.get_rng_state(),
+                'python': random.getstate(),
+                'numpy': (np_state[0], torch.from_numpy(np_state[1].copy()),
+                          int(np_state[2]), int(np_state[3]),
+                          float(np_state[4])),
+            },
+        }
+        if torch.cuda.is_available():
+            state['rng']['cuda'] = torch.cuda.get_rng_state_all()
+        return state
+
+    def save(self, path):
+        """Rank-0 checkpoint (model in the reference key schema)."""
+        if self.rank == 0:
+            tmp = path + '.tmp'
+            torch.save(self.state_dict(), tmp)
+            os.replace(tmp, path)
+        parallel.barrier()
+
+    def load(self, path):
+        state = torch.load(path, map_location=self.device,
+                           weights_only=True)
+        self.model.load_state_dict(state['model'])
+        self.optimizer.load_state_dict(state['optimizer'])
+        self.step_count = int(state.get('step', 0))
+        rng = state.get('rng', {})
+        if 'torch' in rng:
+            torch.set_rng_state(rng['torch'].cpu())
+        if 'python' in rng:
+            random.setstate(rng['python'])
+        if 'numpy' in rng:
+            name, keys, pos, has_gauss, cached = rng['numpy']
+            np.random.set_state((name, keys.cpu().numpy().astype(np.uint32),
+                                 pos, has_gauss, cached))
+        if 'cuda' in rng and torch.cuda.is_available():
+            torch.cuda.set_rng_state_all([t.cpu() for t in rng['cuda']])
+        return state
+
+
+class MetricsLogger(object):
+    """Append-only JSONL metrics (rank 0)."""
+
+    def __init__(self, path=None):
+        self.path = path
+        self.t0 = time.time()
+
+    def log(self, **fields):
+        if self.path is None or parallel.rank() != 0:
+            return
+        fields.setdefault('time', round(time.time() - self.t0, 3))
+        with open(self.path, 'a') as f:
+            f.write(json.dumps(fields) + '\n')

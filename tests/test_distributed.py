@@ -101,3 +101,38 @@ def test_grad_allreduce_matches_average(overlap):
     assert torch.allclose(g0, expected, atol=1e-6, rtol=1e-5)
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
+
+
+def _bench_worker(rank, world, port, mode, out_path):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import bench
+    bench.main(['--steps', '2', '--warmup', '1', '--batch-size', '16',
+                '--graphs-per-category', '8', '--dtype', 'fp32', '--mode',
+                mode, '--json-out', out_path])
+
+
+@pytest.mark.parametrize('mode', ['eager', 'static'])
+def test_bench_two_ranks_gloo(tmp_path, mode):
+    """The bench's distributed path (rank sharding, all-reduce, max-time
+    reduction, rank-0 JSON) runs end to end with two gloo ranks."""
+    import json
+    world = 2
+    out_path = str(tmp_path / 'bench.json')
+    ctx = mp.get_context('spawn')
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker,
+                         args=(r, world, port, mode, out_path))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    with open(out_path) as f:
+        result = json.loads(f.read())
+    assert result['n_gpus'] == 2
+    assert result['config']['global_batch'] == 32
+    assert result['config']['parallelism'] == 'dp2'
+    assert result['value'] > 0
