@@ -42,6 +42,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
 
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
 
+at::Tensor sddmm(const at::Tensor& rowptr, const at::Tensor& col,
+                 const at::Tensor& A, const at::Tensor& B);
+at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
+                                const at::Tensor& S_hat, const at::Tensor& P,
+                                const at::Tensor& Q, const at::Tensor& b1,
+                                const at::Tensor& w2, const at::Tensor& b2);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& colptr,
+    const at::Tensor& row_of, const at::Tensor& perm, const at::Tensor& G,
+    const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
+    const at::Tensor& w2);
+
 }  // namespace dgmc
 
 TORCH_LIBRARY(dgmc_amd, m) {
@@ -70,6 +82,14 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
       "w2, Tensor ptr_s, Tensor ptr_t) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
+  m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
+  m.def(
+      "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
+      "Tensor Q, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
+  m.def(
+      "sparse_consensus_bwd(Tensor rowptr, Tensor col, Tensor colptr, Tensor "
+      "row_of, Tensor perm, Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
+      "w2) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
@@ -82,4 +102,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_consensus", &dgmc::dense_consensus);
   m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
   m.impl("topk_dot", &dgmc::topk_dot);
+  m.impl("sddmm", &dgmc::sddmm);
+  m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
+  m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
 }

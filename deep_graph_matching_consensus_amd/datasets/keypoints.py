@@ -80,7 +80,7 @@ class KeypointGraphDataset(torch.utils.data.Dataset):
     """
 
     def __init__(self, category, num_graphs, visible_prob=0.75, min_nodes=3,
-                 feature_noise=1.0, pos_noise=0.05, transform=None, seed=0):
+                 feature_noise=6.0, pos_noise=0.05, transform=None, seed=0):
         self.category = category
         g = torch.Generator().manual_seed(seed)
         self.graphs = [
@@ -133,7 +133,7 @@ class KeypointGraphDataset(torch.utils.data.Dataset):
 
 def make_keypoint_datasets(categories=PASCAL_VOC_CATEGORIES, graphs=64,
                            feature_dim=1024, visible_prob=0.75, min_nodes=3,
-                           feature_noise=1.0, transform=None, seed=0,
+                           feature_noise=6.0, transform=None, seed=0,
                            split='train'):
     """One :class:`KeypointGraphDataset` per category.  Calls with the same
     ``seed`` share the latent categories; ``split`` selects independent

@@ -208,18 +208,21 @@ class DGMC(torch.nn.Module):
                 S_idx = torch.cat([S_idx, S_rnd_idx], dim=-1)
                 S_idx = self._include_gt(S_idx, lay_s.index, y)
             k = S_idx.size(-1)
+            # CSR/CSC of the candidate set, shared by every op of the loop.
+            cand = sparse_corr.CandidateGraph(S_idx, N_t) \
+                if device.type == 'cuda' and not is_reference_mode() else None
 
-            S_hat = sparse_corr.gather_dot(hs, ht, S_idx)     # [B, N_s, k]
+            S_hat = sparse_corr.gather_dot(hs, ht, S_idx, cand)  # [B,N_s,k]
             S_0 = lay_s.to_sparse(S_hat.softmax(dim=-1))
             for step in range(steps):
                 S = S_hat.softmax(dim=-1)
                 r_s = r_all[step]
                 r_t = sparse_corr.sparse_transport(
-                    S, lay_s.to_dense(r_s), S_idx, N_t)
+                    S, lay_s.to_dense(r_s), S_idx, N_t, cand)
                 o_s, o_t, _ = refine(r_s, lay_t.to_sparse(r_t))
                 S_hat = sparse_corr.consensus_update(
                     S_hat, lay_s.to_dense(o_s.to(f32)),
-                    lay_t.to_dense(o_t.to(f32)), S_idx, self.mlp)
+                    lay_t.to_dense(o_t.to(f32)), S_idx, self.mlp, cand)
             S_L = lay_s.to_sparse(S_hat.softmax(dim=-1))
             S_idx = lay_s.to_sparse(S_idx)
 

@@ -2,49 +2,136 @@
 
 * :func:`top_k`            - candidate search ``argtopk_j <h_s[b,i], h_t[b,j]>``
   (``dgmc.py:85-94``; KeOps ``argKmin`` in the reference).  On the GPU a fused
-  HIP kernel streams ``h_t`` tiles through LDS, computes dot tiles with MFMA
-  and keeps a per-row register top-k, so the ``N_s x N_t`` score matrix is
-  never materialised.
+  HIP kernel streams ``h_t`` tiles through LDS, computes the dot tiles with
+  exact-f32 MFMA and keeps a per-row register top-k, so the ``N_s x N_t``
+  score matrix is never materialised.
+* :class:`CandidateGraph`  - the candidate set ``S_idx [B, N_s, k]`` as a CSR
+  matrix over flattened source rows (global target columns ``b*N_t + idx``)
+  plus its transpose, built once per forward.
 * :func:`gather_dot`       - ``S_hat[b,i,c] = <h_s[b,i], h_t[b, S_idx[b,i,c]]>``
-  (``dgmc.py:197-201``).
+  (``dgmc.py:197-201``): an SDDMM kernel; backward = two SpMMs.
 * :func:`sparse_transport` - ``r_t = scatter_add(S * r_s, S_idx)``
-  (``dgmc.py:209-212``), deterministic (segment sums over a transposed index
-  built once per forward, no atomics).
+  (``dgmc.py:209-212``): SpMM over the transpose (deterministic, no atomics);
+  backward w.r.t. ``S`` = SDDMM.
 * :func:`consensus_update` - ``S_hat + MLP(o_s[:, :, None] - o_t[S_idx])``
-  (``dgmc.py:219-223``; factored ``relu(P_i - Q_idx) . w2 + b2`` on GPU).
+  (``dgmc.py:219-223``) in factored form ``relu(P_i + b1 - Q_idx) . w2 + b2``
+  with ``P = o_s W1^T``, ``Q = o_t W1^T`` computed per node.
+
+The reference quirks are kept: no masking of padded targets or rows in the
+sparse path (``dgmc.py:202,223``).
 """
 import torch
 import torch.nn.functional as F
 
 from . import _backend
 from . import reference as ref
+from .sparse import SparseOperator
 
 
 def top_k(h_s, h_t, k):
     """``[B, N_s, k]`` int64 indices of the k best targets per source row."""
     B, N_s, C = h_s.shape
-    N_t = h_t.size(1)
-    if _backend.use_hip(h_s) and k <= 64 and C % 4 == 0:
-        return _backend.ops().topk_dot(h_s.float().contiguous(),
-                                       h_t.float().contiguous(), int(k))
+    if _backend.use_hip(h_s) and k <= 64 and C % 4 == 0 and C <= 256 \
+            and h_s.dtype == torch.float32:
+        return _backend.ops().topk_dot(h_s.contiguous(), h_t.contiguous(),
+                                       int(k))
     return ref.top_k(h_s, h_t, k)
 
 
+class CandidateGraph(object):
+    """CSR/CSC view of ``S_idx [B, N_s, k]`` over targets ``[B * N_t]``."""
+
+    def __init__(self, S_idx, N_t):
+        B, N_s, k = S_idx.shape
+        dev = S_idx.device
+        self.B, self.N_s, self.N_t, self.k = B, N_s, N_t, k
+        self.rows, self.cols = B * N_s, B * N_t
+        offs = (torch.arange(B, device=dev) * N_t).view(B, 1, 1)
+        col = (S_idx + offs).reshape(-1)
+        self.rowptr = (torch.arange(self.rows + 1, device=dev) * k).to(
+            torch.int32)
+        self.col = col.to(torch.int32)
+        self.perm = torch.argsort(col, stable=True)
+        counts = torch.zeros(self.cols, dtype=torch.long, device=dev)
+        counts.index_add_(0, col, torch.ones_like(col))
+        colptr = torch.zeros(self.cols + 1, dtype=torch.long, device=dev)
+        torch.cumsum(counts, 0, out=colptr[1:])
+        self.colptr = colptr.to(torch.int32)
+        self.row_of = (self.perm // k).to(torch.int32)
+
+    def op(self, val):
+        """``[rows, cols]`` operator with per-entry values ``val``."""
+        return SparseOperator(self.rowptr, self.col, val, self.rows,
+                              self.cols)
+
+    def op_t(self, val):
+        """Transposed operator ``[cols, rows]``."""
+        return SparseOperator(self.colptr, self.row_of, val[self.perm],
+                              self.cols, self.rows)
+
+
+def _spmm(op, x):
+    return _backend.ops().spmm_csr(op.rowptr, op.col, op.val, x.contiguous(),
+                                   None, None, None, False, torch.float32)
+
+
 # ---------------------------------------------------------------------------
-def gather_dot(h_s, h_t, S_idx):
+class _GatherDot(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, A, Bm, cand):
+        ctx.cand = cand
+        ctx.save_for_backward(A, Bm)
+        return _backend.ops().sddmm(cand.rowptr, cand.col, A, Bm)
+
+    @staticmethod
+    def backward(ctx, g):
+        A, Bm = ctx.saved_tensors
+        cand = ctx.cand
+        g = g.contiguous().float()
+        dA = _spmm(cand.op(g), Bm) if ctx.needs_input_grad[0] else None
+        dB = _spmm(cand.op_t(g), A) if ctx.needs_input_grad[1] else None
+        return dA, dB, None
+
+
+def gather_dot(h_s, h_t, S_idx, cand=None):
     """``S_hat [B, N_s, k]`` (autograd through both embeddings)."""
     B, N_s, C = h_s.shape
     k = S_idx.size(-1)
+    if cand is not None and _backend.use_hip(h_s) and C <= 512:
+        out = _GatherDot.apply(h_s.reshape(-1, C).float().contiguous(),
+                               h_t.reshape(-1, C).float().contiguous(), cand)
+        return out.view(B, N_s, k)
     idx = S_idx.reshape(B, N_s * k, 1).expand(-1, -1, C)
     tmp_t = torch.gather(h_t, 1, idx).view(B, N_s, k, C)
     return (h_s.unsqueeze(2) * tmp_t).sum(dim=-1)
 
 
 # ---------------------------------------------------------------------------
-def sparse_transport(S, r_s, S_idx, N_t):
+class _SparseTransport(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, S, r_s, cand):
+        ctx.cand = cand
+        ctx.save_for_backward(r_s)
+        return _spmm(cand.op_t(S), r_s)
+
+    @staticmethod
+    def backward(ctx, g):
+        r_s, = ctx.saved_tensors
+        cand = ctx.cand
+        dS = _backend.ops().sddmm(cand.rowptr, cand.col, r_s,
+                                  g.contiguous().float())
+        return dS, None, None
+
+
+def sparse_transport(S, r_s, S_idx, N_t, cand=None):
     """``r_t[b, j] = sum_{(i,c): S_idx[b,i,c] = j} S[b,i,c] * r_s[b,i]``."""
     B, N_s, k = S.shape
     R = r_s.size(-1)
+    if cand is not None and _backend.use_hip(S) and R <= 512:
+        out = _SparseTransport.apply(S.reshape(-1).float().contiguous(),
+                                     r_s.reshape(-1, R).float().contiguous(),
+                                     cand)
+        return out.view(B, N_t, R)
     tmp = (r_s.unsqueeze(2) * S.unsqueeze(-1)).reshape(B, N_s * k, R)
     idx = S_idx.reshape(B, N_s * k, 1).expand(-1, -1, R)
     out = torch.zeros(B, N_t, R, dtype=tmp.dtype, device=tmp.device)
@@ -52,17 +139,46 @@ def sparse_transport(S, r_s, S_idx, N_t):
 
 
 # ---------------------------------------------------------------------------
-def consensus_update(S_hat, o_s, o_t, S_idx, mlp):
+class _SparseConsensus(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand):
+        ctx.cand = cand
+        ctx.save_for_backward(P, Q, b1, w2)
+        ctx.meta = (b1.dtype, w2.dtype, b2.dtype, b2.shape)
+        return _backend.ops().sparse_consensus_fwd(
+            cand.rowptr, cand.col, S_hat, P, Q, b1.float().contiguous(),
+            w2.float().contiguous().view(-1),
+            b2.float().contiguous().view(-1))
+
+    @staticmethod
+    def backward(ctx, g):
+        P, Q, b1, w2 = ctx.saved_tensors
+        cand = ctx.cand
+        g = g.contiguous().float()
+        dP, dQ, dw2_part = _backend.ops().sparse_consensus_bwd(
+            cand.rowptr, cand.col, cand.colptr, cand.row_of, cand.perm, g,
+            P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1))
+        b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
+        db1 = dP.sum(0).to(b1_dt)
+        dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
+        db2 = g.sum().view(b2_shape).to(b2_dt)
+        return g, dP, dQ, db1, dw2, db2, None
+
+
+def consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand=None):
+    """``S_hat + MLP(o_s[:, :, None] - o_t[S_idx])`` on dense ``o_s
+    [B, N_s, R]`` / ``o_t [B, N_t, R]``."""
     B, N_s, k = S_hat.shape
     R = o_s.size(-1)
     lin1, lin2 = mlp[0], mlp[2]
+    if cand is not None and _backend.use_hip(S_hat) and R <= 512:
+        P = F.linear(o_s.reshape(-1, R).float(), lin1.weight.float())
+        Q = F.linear(o_t.reshape(-1, R).float(), lin1.weight.float())
+        out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
+                                     P.contiguous(), Q.contiguous(),
+                                     lin1.bias, lin2.weight, lin2.bias, cand)
+        return out.view(B, N_s, k)
     idx = S_idx.reshape(B, N_s * k, 1).expand(-1, -1, R)
-    if _backend.use_hip(S_hat):
-        P = F.linear(o_s, lin1.weight, lin1.bias)            # [B, N_s, R]
-        Q = F.linear(o_t, lin1.weight)                        # [B, N_t, R]
-        Qg = torch.gather(Q, 1, idx).view(B, N_s, k, R)
-        h = torch.relu(P.unsqueeze(2) - Qg)
-        return S_hat + F.linear(h, lin2.weight, lin2.bias).squeeze(-1)
     o_t_g = torch.gather(o_t, 1, idx).view(B, N_s, k, R)
     return S_hat + ref.consensus_mlp_sparse(o_s, o_t_g, lin1.weight,
                                             lin1.bias, lin2.weight, lin2.bias)

@@ -276,3 +276,93 @@ def test_graph_captured_step_matches_eager():
         assert torch.allclose(la, lb, atol=1e-5)
         assert torch.allclose(ga, gb, atol=1e-5, rtol=1e-4)
     assert not torch.allclose(results[0][0][0], results[1][0][0])
+
+
+def _cand_inputs(B=3, Ns=37, Nt=41, k=7, C=48):
+    S_idx = torch.randint(Nt, (B, Ns, k), device=DEV)
+    return S_idx, sparse_corr.CandidateGraph(S_idx, Nt)
+
+
+@pytest.mark.parametrize('C', [16, 100, 256])
+def test_sparse_gather_dot(C):
+    B, Ns, Nt, k = 3, 37, 41, 7
+    S_idx, cand = _cand_inputs(B, Ns, Nt, k)
+    h_s = torch.randn(B, Ns, C, device=DEV, requires_grad=True)
+    h_t = torch.randn(B, Nt, C, device=DEV, requires_grad=True)
+    out = sparse_corr.gather_dot(h_s, h_t, S_idx, cand)
+    out2 = sparse_corr.gather_dot(h_s, h_t, S_idx, None)
+    assert torch.allclose(out, out2, atol=1e-4)
+    g = torch.randn_like(out)
+    ga = torch.autograd.grad(out, (h_s, h_t), g)
+    gb = torch.autograd.grad(out2, (h_s, h_t), g)
+    for a, b in zip(ga, gb):
+        assert torch.allclose(a, b, atol=1e-4)
+
+
+@pytest.mark.parametrize('R', [8, 32, 130])
+def test_sparse_transport(R):
+    B, Ns, Nt, k = 2, 29, 31, 6
+    S_idx, cand = _cand_inputs(B, Ns, Nt, k)
+    S = torch.rand(B, Ns, k, device=DEV, requires_grad=True)
+    r_s = torch.randn(B, Ns, R, device=DEV)
+    out = sparse_corr.sparse_transport(S, r_s, S_idx, Nt, cand)
+    out2 = sparse_corr.sparse_transport(S, r_s, S_idx, Nt, None)
+    assert torch.allclose(out, out2, atol=1e-5)
+    g = torch.randn_like(out)
+    assert torch.allclose(torch.autograd.grad(out, S, g)[0],
+                          torch.autograd.grad(out2, S, g)[0], atol=1e-4)
+
+
+@pytest.mark.parametrize('R', [8, 32, 70])
+def test_sparse_consensus(R):
+    B, Ns, Nt, k = 2, 23, 27, 5
+    S_idx, cand = _cand_inputs(B, Ns, Nt, k)
+    mlp = torch.nn.Sequential(torch.nn.Linear(R, R), torch.nn.ReLU(),
+                              torch.nn.Linear(R, 1)).to(DEV)
+    S_hat = torch.randn(B, Ns, k, device=DEV, requires_grad=True)
+    o_s = torch.randn(B, Ns, R, device=DEV, requires_grad=True)
+    o_t = torch.randn(B, Nt, R, device=DEV, requires_grad=True)
+    out = sparse_corr.consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand)
+    out2 = sparse_corr.consensus_update(S_hat, o_s, o_t, S_idx, mlp, None)
+    assert torch.allclose(out, out2, atol=1e-4)
+    g = torch.randn_like(out)
+    inputs = (S_hat, o_s, o_t) + tuple(mlp.parameters())
+    ga = torch.autograd.grad(out, inputs, g)
+    gb = torch.autograd.grad(out2, inputs, g)
+    for a, b in zip(ga, gb):
+        assert torch.allclose(a, b, atol=1e-3, rtol=1e-3)
+
+
+def test_dgmc_sparse_training_hip_vs_reference():
+    """RelCNN + top-k (DBP15K-style) forward/backward: HIP == oracle."""
+    from deep_graph_matching_consensus_amd.models import DGMC, RelCNN
+    torch.manual_seed(0)
+    N, E = 300, 1500
+    x1 = torch.randn(N, 24, device=DEV)
+    x2 = x1[torch.randperm(N, device=DEV)] + 0.1 * torch.randn(N, 24,
+                                                             device=DEV)
+    e1 = torch.randint(N, (2, E), device=DEV)
+    e2 = torch.randint(N, (2, E), device=DEV)
+    model = DGMC(RelCNN(24, 32, 2), RelCNN(8, 8, 2), num_steps=2,
+                 k=5).to(DEV)
+    y = torch.stack([torch.arange(50, device=DEV),
+                     torch.randint(N, (50, ), device=DEV)])
+    torch.manual_seed(1)
+    _, S_L = model(x1, e1, None, None, x2, e2, None, None, y)
+    loss = model.loss(S_L, y)
+    grads = torch.autograd.grad(loss, list(model.parameters()),
+                                allow_unused=True)
+    with reference_mode():
+        torch.manual_seed(1)
+        _, R_L = model(x1, e1, None, None, x2, e2, None, None, y)
+        loss2 = model.loss(R_L, y)
+        grads2 = torch.autograd.grad(loss2, list(model.parameters()),
+                                     allow_unused=True)
+    assert torch.equal(S_L.__idx__, R_L.__idx__)
+    assert torch.allclose(S_L.__val__, R_L.__val__, atol=1e-4)
+    assert torch.allclose(loss, loss2, atol=1e-4)
+    for a, b in zip(grads, grads2):
+        if a is None or b is None:
+            assert a is None and b is None
+        else:
+            assert torch.allclose(a, b, atol=1e-3, rtol=1e-2)
