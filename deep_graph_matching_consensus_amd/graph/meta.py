@@ -126,10 +126,17 @@ def transfer_batch_info(src, dst):
         register_batch_info(dst, info)
 
 
+_SINGLE = {}
+
+
 def batch_info(batch, num_nodes):
     """Return :class:`BatchInfo` for ``batch`` (``None`` = single graph)."""
     if batch is None:
-        return BatchInfo([num_nodes])
+        # Cached per size so device index maps upload once (graph-safe).
+        info = _SINGLE.get(int(num_nodes))
+        if info is None:
+            info = _SINGLE[int(num_nodes)] = BatchInfo([num_nodes])
+        return info
     info = lookup_batch_info(batch)
     if info is not None and info.num_nodes == num_nodes:
         return info

@@ -30,10 +30,12 @@ from ..graph.dense import dense_layout
 from ..nn.inits import reset
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
+from ..ops.plans import _IdentityCache
 from ..runtime.cache import forward_cache
 from ..runtime.mode import is_reference_mode
 
 EPS = 1e-8
+_PAIR_CACHE = _IdentityCache(max_entries=8)
 
 
 def _device_type(device):
@@ -144,8 +146,16 @@ class DGMC(torch.nn.Module):
         outer_dtype = torch.get_autocast_dtype(dev_type)
         pair = None
         if self._fusable(self.psi_1) or self._fusable(self.psi_2):
-            pair = _PairGraph(edge_index_s, edge_attr_s, x_s.size(0),
-                              edge_index_t, edge_attr_t)
+            # Memoised on tensor identity+version: a static graph (e.g. a
+            # KG trained full-batch) keeps its union graph and hence all its
+            # cached message-passing plans across steps.
+            key = (edge_index_s, edge_attr_s, edge_index_t, edge_attr_t)
+            params = ('pair', x_s.size(0))
+            pair = _PAIR_CACHE.get(key, params)
+            if pair is None:
+                pair = _PAIR_CACHE.put(key, params, _PairGraph(
+                    edge_index_s, edge_attr_s, x_s.size(0), edge_index_t,
+                    edge_attr_t))
 
         h_s, h_t = self._encode(self.psi_1, pair, x_s, x_t, edge_index_s,
                                 edge_attr_s, edge_index_t, edge_attr_t)
@@ -242,26 +252,34 @@ class DGMC(torch.nn.Module):
     # ------------------------------------------------------------------
     # Objectives and metrics (dgmc.py:246-311)
     # ------------------------------------------------------------------
-    @staticmethod
-    def _gt_values(S, y):
-        if not S.is_sparse:
-            return S[y[0], y[1]]
-        assert S.__idx__ is not None and S.__val__ is not None
-        mask = S.__idx__[y[0]] == y[1].view(-1, 1)
-        return S.__val__[y[0]][mask]
-
     def loss(self, S, y, reduction='mean', mask=None):
         r"""Negative log-likelihood of the ground-truth correspondences.
+
+        Dense: ``-log(S[y0, y1] + eps)``.  Sparse: every candidate slot of
+        row ``y0`` holding target ``y1`` contributes (ground truths missing
+        from the candidates are dropped, duplicates count twice - as in
+        ``dgmc.py:263-265``), evaluated without a host sync.
 
         ``mask`` (extension): boolean ``[num_gt]`` selecting the valid ground
         truths of a padded static batch; ``'mean'`` then averages over them.
         """
         assert reduction in ['none', 'mean', 'sum']
-        nll = -torch.log(self._gt_values(S, y) + EPS)
-        if mask is not None:
-            nll = nll * mask
+        if not S.is_sparse:
+            nll = -torch.log(S[y[0], y[1]] + EPS)
+            weight = mask
+        else:
+            assert S.__idx__ is not None and S.__val__ is not None
+            hit = S.__idx__[y[0]] == y[1].view(-1, 1)          # [G, k]
+            if mask is not None:
+                hit = hit & mask.view(-1, 1)
+            if reduction == 'none':
+                return -torch.log(S.__val__[y[0]][hit] + EPS)
+            nll = -torch.log(S.__val__[y[0]] + EPS)
+            weight = hit
+        if weight is not None:
+            nll = nll * weight
             if reduction == 'mean':
-                return nll.sum() / mask.sum().clamp(min=1)
+                return nll.sum() / weight.sum().clamp(min=1)
         if reduction == 'none':
             return nll
         return nll.mean() if reduction == 'mean' else nll.sum()

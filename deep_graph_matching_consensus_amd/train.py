@@ -233,3 +233,79 @@ class MetricsLogger(object):
         fields.setdefault('time', round(time.time() - self.t0, 3))
         with open(self.path, 'a') as f:
             f.write(json.dumps(fields) + '\n')
+
+
+class KGTrainer(object):
+    r"""Full-graph KG alignment trainer (DBP15K driver semantics,
+    ``/root/reference/examples/dbp15k.py:37-69``).
+
+    One step = forward on the whole pair with ``train_y`` (random negatives
+    + ground-truth injection in the sparse top-k path), ``NLL(S_L)``,
+    backward, Adam.  The graph is static, so with ``graph=True`` each phase
+    (``num_steps``/``detach`` setting) is captured once into a hipGraph.
+    """
+
+    def __init__(self, model, data, lr=1e-3, graph=True, bf16=False):
+        self.model = model
+        self.data = data
+        self.device = data.x1.device
+        cuda = self.device.type == 'cuda'
+        self.graph = graph and cuda
+        self.bf16 = bf16 and cuda
+        self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
+                                          fused=cuda, capturable=self.graph)
+        self.last_loss = torch.zeros((), device=self.device)
+        self._graphs = {}
+
+    def _autocast(self):
+        return torch.autocast(device_type=self.device.type,
+                              dtype=torch.bfloat16, enabled=self.bf16,
+                              cache_enabled=False)
+
+    def _body(self):
+        d, model = self.data, self.model
+        for p in model.parameters():
+            p.grad = None
+        with self._autocast():
+            _, S_L = model(d.x1, d.edge_index1, None, None, d.x2,
+                           d.edge_index2, None, None, d.train_y)
+        loss = model.loss(S_L, d.train_y)
+        loss.backward()
+        self.optimizer.step()
+        self.last_loss.copy_(loss.detach())
+
+    def step(self):
+        self.model.train()
+        if not self.graph:
+            return self._body()
+        key = (self.model.num_steps, self.model.detach, self.model.k)
+        g = self._graphs.get(key)
+        if g is None:
+            # Grads must exist (zero) as static tensors before capture.
+            g = self._graphs[key] = GraphedStep(self._body_static, warmup=2)
+        g()
+
+    def _body_static(self):
+        d, model = self.data, self.model
+        for p in model.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        with self._autocast():
+            _, S_L = model(d.x1, d.edge_index1, None, None, d.x2,
+                           d.edge_index2, None, None, d.train_y)
+        loss = model.loss(S_L, d.train_y)
+        loss.backward()
+        self.optimizer.step()
+        self.last_loss.copy_(loss.detach())
+
+    @torch.no_grad()
+    def evaluate(self, k=10):
+        d, model = self.data, self.model
+        model.eval()
+        with self._autocast():
+            _, S_L = model(d.x1, d.edge_index1, None, None, d.x2,
+                           d.edge_index2, None, None)
+        hits1 = model.acc(S_L, d.test_y)
+        hitsk = model.hits_at_k(k, S_L, d.test_y)
+        model.train()
+        return hits1, hitsk
