@@ -133,6 +133,10 @@ def bench_kg(args, cfg, device):
             times[phase] = (time.perf_counter() - t0) / max(args.steps, 1)
         hits1, hits10 = trainer.evaluate()
     ms2 = 1000.0 * times['phase2']
+    baseline = None
+    if osp.exists(BASELINE_FILE) and not reference:
+        with open(BASELINE_FILE) as f:
+            baseline = json.load(f).get(args.config, {}).get('value')
     out = {
         'metric': 'DBP15K-shaped KG alignment training steps/sec '
                   '(refinement phase, full graph)',
@@ -145,7 +149,8 @@ def bench_kg(args, cfg, device):
         'ms_per_step_phase1': round(1000.0 * times['phase1'], 3),
         'higher_is_better': True,
         'scaling': 'strong',
-        'vs_baseline': None,
+        'vs_baseline': round((1.0 / times['phase2']) / baseline, 3)
+        if baseline else None,
         'dtype': 'fp32',
         'data': 'synthetic DBP15K-shaped {} KG pair ({} / {} entities, {} / '
                 '{} triples, {} train / {} test alignments), random-init '
