@@ -75,10 +75,11 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
 // ---------------------------------------------------------------------------
 // Softmax + transport:  S = masked_softmax(S_hat[b]);  r_t[b] = S^T r_s[b].
 // ---------------------------------------------------------------------------
+template <typename TR>
 __global__ __launch_bounds__(256) void softmax_transport_kernel(
-    const float* __restrict__ S_hat, const float* __restrict__ r_s,
+    const float* __restrict__ S_hat, const TR* __restrict__ r_s,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
-    float* __restrict__ S, float* __restrict__ r_t, int Ns, int Nt, int R,
+    float* __restrict__ S, TR* __restrict__ r_t, int Ns, int Nt, int R,
     int rows_t) {
   __shared__ float sS[kMaxN * kPitch];
   __shared__ float sR[kMaxN * kPitch];
@@ -102,27 +103,28 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
     }
   }
 
-  const float* rs = r_s + (size_t)ptr_s[b] * R;
-  float* rt = r_t + (size_t)ptr_t[b] * R;
+  const TR* rs = r_s + (size_t)ptr_s[b] * R;
+  TR* rt = r_t + (size_t)ptr_t[b] * R;
   for (int c0 = 0; c0 < R; c0 += kCh) {
     const int c = c0 + lane;
     __syncthreads();
     for (int i = wave; i < ns; i += kWaves)
-      sR[i * kPitch + lane] = c < R ? rs[(size_t)i * R + c] : 0.f;
+      sR[i * kPitch + lane] = c < R ? Cvt<TR>::to_f(rs[(size_t)i * R + c]) : 0.f;
     __syncthreads();
     for (int j = wave; j < nt; j += kWaves) {
       float acc = 0.f;
       for (int i = 0; i < ns; ++i)
         acc = fmaf(sS[i * kPitch + j], sR[i * kPitch + lane], acc);
-      if (c < R) rt[(size_t)j * R + c] = acc;
+      if (c < R) rt[(size_t)j * R + c] = Cvt<TR>::from_f(acc);
     }
   }
 }
 
 // dS_hat = softmax_bwd(S, dS),  dS[i][j] = sum_c r_s[i][c] * g[j][c].
+template <typename TR>
 __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
-    const float* __restrict__ S, const float* __restrict__ r_s,
-    const float* __restrict__ g, const int* __restrict__ ptr_s,
+    const float* __restrict__ S, const TR* __restrict__ r_s,
+    const TR* __restrict__ g, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, float* __restrict__ dS_hat, int Ns,
     int Nt, int R) {
   __shared__ float sR[kMaxN * kPitch];
@@ -130,8 +132,8 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
   const int b = xcd_remap(blockIdx.x, gridDim.x);
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
-  const float* rs = r_s + (size_t)ptr_s[b] * R;
-  const float* gb = g + (size_t)ptr_t[b] * R;
+  const TR* rs = r_s + (size_t)ptr_s[b] * R;
+  const TR* gb = g + (size_t)ptr_t[b] * R;
 
   float acc[kRowsPerWave];
 #pragma unroll
@@ -141,9 +143,9 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
     const int c = c0 + lane;
     __syncthreads();
     for (int i = wave; i < ns; i += kWaves)
-      sR[i * kPitch + lane] = c < R ? rs[(size_t)i * R + c] : 0.f;
+      sR[i * kPitch + lane] = c < R ? Cvt<TR>::to_f(rs[(size_t)i * R + c]) : 0.f;
     for (int j = wave; j < nt; j += kWaves)
-      sG[j * kPitch + lane] = c < R ? gb[(size_t)j * R + c] : 0.f;
+      sG[j * kPitch + lane] = c < R ? Cvt<TR>::to_f(gb[(size_t)j * R + c]) : 0.f;
     __syncthreads();
     const int cmax = min(kCh, R - c0);
     if (lane < nt) {
@@ -392,7 +394,6 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& ptr_t, int64_t rows_t) {
   check_pair_tensor(S_hat, "S_hat");
   check_packed(r_s, "r_s");
-  TORCH_CHECK(r_s.scalar_type() == at::kFloat, "r_s must be fp32");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
   const int R = r_s.size(1);
@@ -401,11 +402,14 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   at::Tensor S = at::empty_like(S_hat);
   at::Tensor r_t = at::empty({rows_t, R}, r_s.options());
   if (B == 0) return {S, r_t};
-  hipLaunchKernelGGL(softmax_transport_kernel, dim3(B), dim3(256), 0, stream(),
-                     S_hat.data_ptr<float>(), r_s.data_ptr<float>(),
-                     ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
-                     S.data_ptr<float>(), r_t.data_ptr<float>(), Ns, Nt, R,
-                     (int)rows_t);
+  DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
+    hipLaunchKernelGGL(softmax_transport_kernel<T>, dim3(B), dim3(256), 0,
+                       stream(), S_hat.data_ptr<float>(),
+                       reinterpret_cast<const T*>(r_s.data_ptr()),
+                       ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
+                       S.data_ptr<float>(), reinterpret_cast<T*>(r_t.data_ptr()),
+                       Ns, Nt, R, (int)rows_t);
+  });
   DGMC_CHECK_LAUNCH();
   return {S, r_t};
 }
@@ -418,8 +422,7 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
   check_pair_tensor(S, "S");
   check_packed(r_s, "r_s");
   check_packed(g, "grad r_t");
-  TORCH_CHECK(r_s.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat,
-              "fp32 expected");
+  TORCH_CHECK(r_s.scalar_type() == g.scalar_type(), "r_s/grad dtype");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
   const int B = S.size(0), Ns = S.size(1), Nt = S.size(2);
   const int R = r_s.size(1);
@@ -428,10 +431,14 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S);
   if (B == 0) return out;
-  hipLaunchKernelGGL(softmax_transport_bwd_kernel, dim3(B), dim3(256), 0,
-                     stream(), S.data_ptr<float>(), r_s.data_ptr<float>(),
-                     g.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                     ptr_t.data_ptr<int>(), out.data_ptr<float>(), Ns, Nt, R);
+  DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
+    hipLaunchKernelGGL(softmax_transport_bwd_kernel<T>, dim3(B), dim3(256), 0,
+                       stream(), S.data_ptr<float>(),
+                       reinterpret_cast<const T*>(r_s.data_ptr()),
+                       reinterpret_cast<const T*>(g.data_ptr()),
+                       ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
+                       out.data_ptr<float>(), Ns, Nt, R);
+  });
   DGMC_CHECK_LAUNCH();
   return out;
 }

@@ -54,6 +54,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
     const at::Tensor& w2);
 
+std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
+                                                 const at::Tensor& out,
+                                                 bool relu,
+                                                 at::ScalarType g_dtype);
+void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
+
 }  // namespace dgmc
 
 TORCH_LIBRARY(dgmc_amd, m) {
@@ -84,6 +90,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
+      "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype) "
+      "-> (Tensor, Tensor)");
+  m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
+  m.def(
       "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
       "Tensor Q, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def(
@@ -103,6 +113,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
   m.impl("topk_dot", &dgmc::topk_dot);
   m.impl("sddmm", &dgmc::sddmm);
+  m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
+  m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
 }

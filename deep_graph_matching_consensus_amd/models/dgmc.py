@@ -175,10 +175,14 @@ class DGMC(torch.nn.Module):
                 else torch.float32
             hs = lay_s.to_dense(h_s.to(f32))
             ht = lay_t.to_dense(h_t.to(f32))
-            # Random node indicators for all steps, packed [steps, sum N_s, R].
+            # Random node indicators for all steps, packed [steps, sum N_s, R]
+            # (drawn directly in the encoder GEMM dtype under autocast).
+            r_dtype = outer_dtype if (outer_autocast and self.k < 1 and
+                                      device.type == 'cuda' and
+                                      not is_reference_mode()) else f32
             if steps > 0:
-                r_all = torch.randn((steps, lay_s.num_nodes, R_in), dtype=f32,
-                                    device=device)
+                r_all = torch.randn((steps, lay_s.num_nodes, R_in),
+                                    dtype=r_dtype, device=device)
 
             def refine(r_s, r_t):
                 """psi_2 on both graphs (packed in/out) under the caller's

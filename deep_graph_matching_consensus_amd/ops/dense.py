@@ -71,8 +71,8 @@ class _SoftmaxTransport(torch.autograd.Function):
     @staticmethod
     def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t):
         S, r_t = _backend.ops().dense_softmax_transport(
-            S_hat.float().contiguous(), r_s.float().contiguous(), ptr_s,
-            ptr_t, rows_t)
+            S_hat.float().contiguous(), r_s.contiguous(), ptr_s, ptr_t,
+            rows_t)
         ctx.save_for_backward(S, r_s, ptr_s, ptr_t)
         ctx.dtype = S_hat.dtype
         return r_t
@@ -81,15 +81,16 @@ class _SoftmaxTransport(torch.autograd.Function):
     def backward(ctx, grad):
         S, r_s, ptr_s, ptr_t = ctx.saved_tensors
         g = _backend.ops().dense_softmax_transport_bwd(
-            S, r_s.float().contiguous(), grad.float().contiguous(), ptr_s,
+            S, r_s.contiguous(), grad.to(r_s.dtype).contiguous(), ptr_s,
             ptr_t)
         return g.to(ctx.dtype), None, None, None, None
 
 
 def softmax_transport(S_hat, r_s, lay_s, lay_t):
     r"""``masked_softmax(S_hat)^T r_s`` with packed ``r_s [sum N_s, R]``;
-    returns packed ``r_t [sum N_t, R]``.  ``r_s`` is a non-differentiable
-    random indicator (as in the reference); gradients flow into ``S_hat``.
+    returns packed ``r_t [sum N_t, R]`` in ``r_s``'s dtype (fp32 or bf16;
+    accumulation in fp32).  ``r_s`` is a non-differentiable random indicator
+    (as in the reference); gradients flow into ``S_hat``.
     """
     B, N_s, N_t = S_hat.shape
     if _hip_ok(S_hat, N_s, N_t):

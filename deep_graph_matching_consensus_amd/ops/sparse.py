@@ -98,8 +98,8 @@ def _spmm_raw(op, x, self_x, self_scale, bias, relu, out_dtype):
 
 class _SpMM(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, self_x, self_scale, bias, op, relu):
-        out = _spmm_raw(op, x, self_x, self_scale, bias, relu, torch.float32)
+    def forward(ctx, x, self_x, self_scale, bias, op, relu, out_dtype):
+        out = _spmm_raw(op, x, self_x, self_scale, bias, relu, out_dtype)
         ctx.op, ctx.relu = op, relu
         ctx.x_dtype = x.dtype
         ctx.bias_dtype = bias.dtype if bias is not None else None
@@ -109,31 +109,49 @@ class _SpMM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         self_x, self_scale, out = ctx.saved_tensors
-        g = grad.contiguous().float()
-        if ctx.relu:
-            g = g * (out > 0)
-        gx = gself = gscale = gbias = None
+        grad = grad.contiguous()
+        gbias = None
+        need_bias = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
+        if _backend.use_hip(grad) and (ctx.relu or need_bias):
+            # Fused: g = grad * (out > 0) and per-block bias partials.
+            g, part = _backend.ops().relu_bias_bwd(
+                grad, out if ctx.relu else grad, ctx.relu, ctx.x_dtype)
+            if need_bias:
+                gbias = part.sum(0).to(ctx.bias_dtype)
+        else:
+            g = grad.float()
+            if ctx.relu:
+                g = g * (out > 0)
+            if need_bias:
+                gbias = g.sum(0).to(ctx.bias_dtype)
+        gx = gself = gscale = None
         if ctx.needs_input_grad[0]:
             gx = _spmm_raw(ctx.op.t(), g, None, None, None, False,
                            ctx.x_dtype)
         if self_x is not None:
+            gf = g.float()
             if ctx.needs_input_grad[1]:
-                gself = (g * self_scale.float()).to(self_x.dtype)
+                gself = (gf * self_scale.float()).to(self_x.dtype)
             if ctx.needs_input_grad[2]:
-                gscale = (g * self_x.float()).sum().view_as(self_scale)
+                gscale = (gf * self_x.float()).sum().view_as(self_scale)
                 gscale = gscale.to(self_scale.dtype)
-        if ctx.needs_input_grad[3]:
-            gbias = g.sum(0).to(ctx.bias_dtype)
-        return gx, gself, gscale, gbias, None, None
+        return gx, gself, gscale, gbias, None, None, None
 
 
-def spmm(op, x, self_x=None, self_scale=None, bias=None, relu=False):
+def spmm(op, x, self_x=None, self_scale=None, bias=None, relu=False,
+         out_dtype=None):
     r"""``act(op @ x + self_scale * self_x + bias)`` with fp32 accumulation.
 
-    ``x`` may be fp32 or bf16 (e.g. the output of a bf16 GEMM); the result is
-    fp32.  Gradients flow to ``x``, ``self_x``, ``self_scale`` and ``bias``.
+    ``x`` may be fp32 or bf16 (e.g. the output of a bf16 GEMM).  The result
+    keeps bf16/fp16 inputs in their dtype (so the next GEMM needs no cast and
+    the backward moves half the bytes) and is fp32 otherwise; override with
+    ``out_dtype``.  Gradients flow to ``x``, ``self_x``, ``self_scale`` and
+    ``bias``.
     """
     assert x.dim() == 2 and x.size(0) == op.num_cols, (x.shape, op)
     if self_x is not None:
         assert self_x.size(0) == op.num_rows and self_scale is not None
-    return _SpMM.apply(x, self_x, self_scale, bias, op, relu)
+    if out_dtype is None:
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) \
+            else torch.float32
+    return _SpMM.apply(x, self_x, self_scale, bias, op, relu, out_dtype)
