@@ -13,35 +13,62 @@
 
 namespace dgmc {
 
-constexpr int kRowsPerBlock = 64;
-
-template <typename TG, typename TO, typename TR>
+// LPR lanes own one row (VEC channels each per pass); a block holds
+// RPB = 256 / LPR row slots and walks rows grid-stride, keeping per-thread
+// channel partials in registers; the block's column partial is reduced
+// through LDS once at the end.
+template <typename TG, typename TO, typename TR, int VEC, int LPR>
 __global__ __launch_bounds__(256) void relu_bias_bwd_kernel(
     const TG* __restrict__ grad, const TO* __restrict__ out,
     TR* __restrict__ g_out, float* __restrict__ dbias_part, int rows, int C,
     int relu) {
-  extern __shared__ __attribute__((aligned(16))) float part[];  // [4][C]
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int r0 = blockIdx.x * kRowsPerBlock;
-  const int r1 = min(r0 + kRowsPerBlock, rows);
-  for (int c0 = 0; c0 < C; c0 += kWave) {
-    const int c = c0 + lane;
-    float acc = 0.f;
-    if (c < C) {
-      for (int r = r0 + wave; r < r1; r += 4) {
-        const size_t o = (size_t)r * C + c;
-        float g = Cvt<TG>::to_f(grad[o]);
-        if (relu && !(Cvt<TO>::to_f(out[o]) > 0.f)) g = 0.f;
-        g_out[o] = Cvt<TR>::from_f(g);
-        acc += g;
+  constexpr int RPB = 256 / LPR;
+  extern __shared__ __attribute__((aligned(16))) float part[];  // [RPB][C]
+  const int slot = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  for (int c0 = lane * VEC; c0 < C; c0 += LPR * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    for (int r = blockIdx.x * RPB + slot; r < rows; r += gridDim.x * RPB) {
+      const size_t o = (size_t)r * C + c0;
+      float g[VEC], m[VEC];
+      load_vec<TG, VEC>(grad + o, g);
+      if (relu) {
+        load_vec<TO, VEC>(out + o, m);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) g[k] = m[k] > 0.f ? g[k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += g[k];
+      if constexpr (VEC * sizeof(TR) == 16) {
+        store_vec<TR, VEC>(g_out + o, g);
+      } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) g_out[o + k] = Cvt<TR>::from_f(g[k]);
       }
     }
-    if (c < C) part[wave * C + c] = acc;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) part[slot * C + c0 + k] = acc[k];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x)
-    dbias_part[(size_t)blockIdx.x * C + c] =
-        part[c] + part[C + c] + part[2 * C + c] + part[3 * C + c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int q = 0; q < RPB; ++q) s += part[q * C + c];
+    dbias_part[(size_t)blockIdx.x * C + c] = s;
+  }
+}
+
+template <typename TG, typename TO, typename TR, int VEC, int LPR>
+void launch_relu_bias(const at::Tensor& grad, const at::Tensor& out,
+                      at::Tensor& g, at::Tensor& part, int blocks, int rows,
+                      int C, bool relu) {
+  constexpr int RPB = 256 / LPR;
+  hipLaunchKernelGGL((relu_bias_bwd_kernel<TG, TO, TR, VEC, LPR>),
+                     dim3(blocks), dim3(256), RPB * C * sizeof(float),
+                     stream(), reinterpret_cast<const TG*>(grad.data_ptr()),
+                     reinterpret_cast<const TO*>(out.data_ptr()),
+                     reinterpret_cast<TR*>(g.data_ptr()),
+                     part.data_ptr<float>(), rows, C, relu ? 1 : 0);
 }
 
 std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
@@ -51,24 +78,38 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
   TORCH_CHECK(grad.is_cuda() && grad.dim() == 2 && grad.is_contiguous() &&
                   out.is_contiguous() && out.sizes() == grad.sizes(),
               "relu_bias_bwd: grad/out must be contiguous [rows, C]");
+  TORCH_CHECK(grad.scalar_type() == out.scalar_type(),
+              "relu_bias_bwd: grad/out dtype mismatch");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
   const int rows = grad.size(0), C = grad.size(1);
+  TORCH_CHECK(C <= 2048, "relu_bias_bwd: C <= 2048");
   at::Tensor g = at::empty({rows, C}, grad.options().dtype(g_dtype));
-  const int blocks = std::max(1, (rows + kRowsPerBlock - 1) / kRowsPerBlock);
+  const int blocks = std::max(1, std::min((rows + 7) / 8, 1024));
   at::Tensor part = at::empty({blocks, C}, grad.options().dtype(at::kFloat));
   if (rows == 0 || C == 0) return {g, part.zero_()};
-  const size_t lds = 4 * (size_t)C * sizeof(float);
-  TORCH_CHECK(lds <= 64 * 1024, "relu_bias_bwd: C too large");
-  DGMC_DISPATCH_FLOAT(grad.scalar_type(), TG, [&] {
-    DGMC_DISPATCH_FLOAT(out.scalar_type(), TO, [&] {
-      DGMC_DISPATCH_FLOAT(g_dtype, TR, [&] {
-        hipLaunchKernelGGL((relu_bias_bwd_kernel<TG, TO, TR>), dim3(blocks),
-                           dim3(256), lds, stream(),
-                           reinterpret_cast<const TG*>(grad.data_ptr()),
-                           reinterpret_cast<const TO*>(out.data_ptr()),
-                           reinterpret_cast<TR*>(g.data_ptr()),
-                           part.data_ptr<float>(), rows, C, relu ? 1 : 0);
-      });
+  const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
+                   aligned16(g.data_ptr());
+  DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
+    DGMC_DISPATCH_FLOAT(g_dtype, TR, [&] {
+      constexpr int V = Vec16<T>::N;
+      if (vec && C % V == 0) {
+        const int lanes = C / V;
+        if (lanes <= 8)
+          launch_relu_bias<T, T, TR, V, 8>(grad, out, g, part, blocks, rows,
+                                           C, relu);
+        else if (lanes <= 16)
+          launch_relu_bias<T, T, TR, V, 16>(grad, out, g, part, blocks, rows,
+                                            C, relu);
+        else if (lanes <= 32)
+          launch_relu_bias<T, T, TR, V, 32>(grad, out, g, part, blocks, rows,
+                                            C, relu);
+        else
+          launch_relu_bias<T, T, TR, V, 64>(grad, out, g, part, blocks, rows,
+                                            C, relu);
+      } else {
+        launch_relu_bias<T, T, TR, 1, 64>(grad, out, g, part, blocks, rows, C,
+                                          relu);
+      }
     });
   });
   DGMC_CHECK_LAUNCH();

@@ -16,6 +16,8 @@ in ~33 us (s=16) and accumulates directly in fp32 for the fp32 master weight
 """
 import torch
 
+from . import _backend
+
 
 def _split_factor(m, n, k):
     elems = m * n
@@ -42,9 +44,14 @@ def matmul_tn_fp32(a, b):
     a3 = a[:main].view(s, k, M).transpose(1, 2)
     b3 = b[:main].view(s, k, N)
     if a.dtype == torch.float32:
-        out = torch.bmm(a3, b3).sum(0)
+        part = torch.bmm(a3, b3)
     else:
-        out = torch.bmm(a3, b3, out_dtype=torch.float32).sum(0)
+        part = torch.bmm(a3, b3, out_dtype=torch.float32)
+    if _backend.hip_available():
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+        _backend.ops().reduce_add_rows(part, out, False)
+    else:
+        out = part.sum(0)
     if main < K:
         tail = a[main:].t() @ b[main:]
         out = out + tail.float()
