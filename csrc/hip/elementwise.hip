@@ -1,11 +1,17 @@
-// Fused element-wise backward helpers.
+// Fused column reductions and backward helpers.
 //
 // relu_bias_bwd: for an aggregation output `out = relu(A x + bias)` the
 // backward needs g' = grad * (out > 0) for the transposed aggregation and
-// dbias = sum_rows g'.  Eager PyTorch spends three kernels (compare, mul,
-// column reduction); this kernel does both in one pass: each workgroup owns a
-// row range, writes g' (in the activation dtype) and one fp32 partial column
-// sum per block; the tiny [blocks, C] partial is summed by the caller.
+// dbias = sum_rows g'.  Eager PyTorch spends four kernels (compare, mul,
+// column reduction, cast) plus one gradient-accumulation add per reuse of
+// the bias; this kernel does everything in ONE launch: each workgroup owns a
+// row range, writes g' and one fp32 column partial; the last workgroup to
+// finish (ticket counter) folds the partials in fixed order into `dbias`,
+// optionally accumulating into an existing fp32 buffer (the consensus loop
+// reuses psi_2's biases ten times - see runtime/loopgrad.py).  Deterministic:
+// the fold order does not depend on which block finishes last.
+//
+// col_sum: the same machinery without the g' output (dst (+)= sum_rows src).
 //
 // reduce_add_rows: dst[n] (+)= sum_s src[s, n] - the split-K combine of the
 // weight-gradient GEMMs, accumulating straight into the fp32 gradient.
@@ -13,23 +19,69 @@
 
 namespace dgmc {
 
-// LPR lanes own one row (VEC channels each per pass); a block holds
-// RPB = 256 / LPR row slots and walks rows grid-stride, keeping per-thread
-// channel partials in registers; the block's column partial is reduced
-// through LDS once at the end.
-template <typename TG, typename TO, typename TR, int VEC, int LPR>
-__global__ __launch_bounds__(256) void relu_bias_bwd_kernel(
+namespace {
+// Self-resetting tickets (atomicInc wraps to 0 at the last block).  Zero
+// initialised at code-object load, so no allocation or memset is needed and
+// the kernels are hipGraph-capturable.  Launches rotate through the slots;
+// kernels sharing a slot would have to be in flight concurrently to collide.
+constexpr int kTickets = 256;
+__device__ unsigned int g_tickets[kTickets];
+int next_ticket() {
+  static int t = 0;
+  t = (t + 1) % kTickets;
+  return t;
+}
+constexpr int kMaxColBlocks = 128;
+}  // namespace
+
+// Last block: dst[c] (+)= sum_b part[b, c] in fixed b order (row groups then
+// an LDS fold).  256 threads.
+__device__ __forceinline__ void fold_partials(const float* __restrict__ part,
+                                              float* __restrict__ dst,
+                                              int nblocks, int C,
+                                              int accumulate, float* lds) {
+  const int tid = threadIdx.x;
+  if (C <= 256) {
+    const int groups = 256 / C;
+    const int c = tid % C, rg = tid / C;
+    float s = 0.f;
+    if (rg < groups)
+      for (int b = rg; b < nblocks; b += groups) s += part[(size_t)b * C + c];
+    if (rg < groups) lds[rg * C + c] = s;
+    __syncthreads();
+    if (tid < C) {
+      float t = accumulate ? dst[tid] : 0.f;
+      for (int g = 0; g < groups; ++g) t += lds[g * C + tid];
+      dst[tid] = t;
+    }
+  } else {
+    for (int c = tid; c < C; c += 256) {
+      float s = accumulate ? dst[c] : 0.f;
+      for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * C + c];
+      dst[c] = s;
+    }
+  }
+}
+
+// LPR lanes own one row (VEC channels per pass); a block holds RPB = 256/LPR
+// row slots and walks its row range, keeping channel partials in registers;
+// the block partial goes through LDS to `part[block]`.
+template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
+__global__ __launch_bounds__(256) void colsum_kernel(
     const TG* __restrict__ grad, const TO* __restrict__ out,
-    TR* __restrict__ g_out, float* __restrict__ dbias_part, int rows, int C,
-    int relu) {
+    TR* __restrict__ g_out, float* __restrict__ part, float* __restrict__ dst,
+    int rows, int C, int relu, int accumulate, int ticket) {
   constexpr int RPB = 256 / LPR;
-  extern __shared__ __attribute__((aligned(16))) float part[];  // [RPB][C]
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [RPB][C]
+  __shared__ bool is_last;
   const int slot = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  const int per = (rows + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
   for (int c0 = lane * VEC; c0 < C; c0 += LPR * VEC) {
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-    for (int r = blockIdx.x * RPB + slot; r < rows; r += gridDim.x * RPB) {
+    for (int r = r0 + slot; r < r1; r += RPB) {
       const size_t o = (size_t)r * C + c0;
       float g[VEC], m[VEC];
       load_vec<TG, VEC>(grad + o, g);
@@ -40,41 +92,94 @@ __global__ __launch_bounds__(256) void relu_bias_bwd_kernel(
       }
 #pragma unroll
       for (int k = 0; k < VEC; ++k) acc[k] += g[k];
-      if constexpr (VEC * sizeof(TR) == 16) {
-        store_vec<TR, VEC>(g_out + o, g);
-      } else {
+      if constexpr (WRITE_G) {
+        if constexpr (VEC * sizeof(TR) == 16) {
+          store_vec<TR, VEC>(g_out + o, g);
+        } else {
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) g_out[o + k] = Cvt<TR>::from_f(g[k]);
+          for (int k = 0; k < VEC; ++k) g_out[o + k] = Cvt<TR>::from_f(g[k]);
+        }
       }
     }
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) part[slot * C + c0 + k] = acc[k];
+    for (int k = 0; k < VEC; ++k) lds[slot * C + c0 + k] = acc[k];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float s = 0.f;
-    for (int q = 0; q < RPB; ++q) s += part[q * C + c];
-    dbias_part[(size_t)blockIdx.x * C + c] = s;
+    for (int q = 0; q < RPB; ++q) s += lds[q * C + c];
+    part[(size_t)blockIdx.x * C + c] = s;
+  }
+  // Publish the partial, take a ticket; the last block folds.
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    is_last = atomicInc(&g_tickets[ticket], gridDim.x - 1) == gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  fold_partials(part, dst, gridDim.x, C, accumulate, lds);
+}
+
+template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
+void launch_colsum(const at::Tensor& grad, const void* out, void* g,
+                   at::Tensor& part, float* dst, int blocks, int rows, int C,
+                   bool relu, bool accumulate) {
+  constexpr int RPB = 256 / LPR;
+  const size_t lds = std::max<size_t>(RPB * C, 256) * sizeof(float);
+  hipLaunchKernelGGL((colsum_kernel<TG, TO, TR, VEC, LPR, WRITE_G>),
+                     dim3(blocks), dim3(256), lds, stream(),
+                     reinterpret_cast<const TG*>(grad.data_ptr()),
+                     reinterpret_cast<const TO*>(out),
+                     reinterpret_cast<TR*>(g), part.data_ptr<float>(), dst,
+                     rows, C, relu ? 1 : 0, accumulate ? 1 : 0, next_ticket());
+}
+
+template <typename T, typename TR, bool WRITE_G>
+void dispatch_colsum(const at::Tensor& grad, const void* out, void* g,
+                     at::Tensor& part, float* dst, int blocks, int rows,
+                     int C, bool relu, bool accumulate, bool vec) {
+  constexpr int V = Vec16<T>::N;
+  if (vec && C % V == 0) {
+    const int lanes = C / V;
+    if (lanes <= 8)
+      launch_colsum<T, T, TR, V, 8, WRITE_G>(grad, out, g, part, dst, blocks,
+                                             rows, C, relu, accumulate);
+    else if (lanes <= 16)
+      launch_colsum<T, T, TR, V, 16, WRITE_G>(grad, out, g, part, dst, blocks,
+                                              rows, C, relu, accumulate);
+    else if (lanes <= 32)
+      launch_colsum<T, T, TR, V, 32, WRITE_G>(grad, out, g, part, dst, blocks,
+                                              rows, C, relu, accumulate);
+    else
+      launch_colsum<T, T, TR, V, 64, WRITE_G>(grad, out, g, part, dst, blocks,
+                                              rows, C, relu, accumulate);
+  } else {
+    launch_colsum<T, T, TR, 1, 64, WRITE_G>(grad, out, g, part, dst, blocks,
+                                            rows, C, relu, accumulate);
   }
 }
 
-template <typename TG, typename TO, typename TR, int VEC, int LPR>
-void launch_relu_bias(const at::Tensor& grad, const at::Tensor& out,
-                      at::Tensor& g, at::Tensor& part, int blocks, int rows,
-                      int C, bool relu) {
-  constexpr int RPB = 256 / LPR;
-  hipLaunchKernelGGL((relu_bias_bwd_kernel<TG, TO, TR, VEC, LPR>),
-                     dim3(blocks), dim3(256), RPB * C * sizeof(float),
-                     stream(), reinterpret_cast<const TG*>(grad.data_ptr()),
-                     reinterpret_cast<const TO*>(out.data_ptr()),
-                     reinterpret_cast<TR*>(g.data_ptr()),
-                     part.data_ptr<float>(), rows, C, relu ? 1 : 0);
+static int colsum_blocks(int rows) {
+  return std::max(1, std::min((rows + 63) / 64, kMaxColBlocks));
 }
 
-std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
-                                                 const at::Tensor& out,
-                                                 bool relu,
-                                                 at::ScalarType g_dtype) {
+static at::Tensor dst_or_new(const c10::optional<at::Tensor>& dst, int64_t C,
+                             const at::Tensor& like, bool& accumulate) {
+  if (dst.has_value() && dst->defined()) {
+    TORCH_CHECK(dst->scalar_type() == at::kFloat && dst->is_contiguous() &&
+                    dst->numel() == C && dst->device() == like.device(),
+                "colsum: dst must be a contiguous fp32 [C] tensor");
+    return *dst;
+  }
+  accumulate = false;
+  return at::empty({C}, like.options().dtype(at::kFloat));
+}
+
+std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
+    const at::Tensor& grad, const at::Tensor& out, bool relu,
+    at::ScalarType g_dtype, const c10::optional<at::Tensor>& dbias,
+    bool accumulate) {
   TORCH_CHECK(grad.is_cuda() && grad.dim() == 2 && grad.is_contiguous() &&
                   out.is_contiguous() && out.sizes() == grad.sizes(),
               "relu_bias_bwd: grad/out must be contiguous [rows, C]");
@@ -84,36 +189,50 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
   const int rows = grad.size(0), C = grad.size(1);
   TORCH_CHECK(C <= 2048, "relu_bias_bwd: C <= 2048");
   at::Tensor g = at::empty({rows, C}, grad.options().dtype(g_dtype));
-  const int blocks = std::max(1, std::min((rows + 7) / 8, 1024));
+  at::Tensor db = dst_or_new(dbias, C, grad, accumulate);
+  if (C == 0) return {g, db};
+  if (rows == 0) {
+    if (!accumulate) db.zero_();
+    return {g, db};
+  }
+  const int blocks = colsum_blocks(rows);
   at::Tensor part = at::empty({blocks, C}, grad.options().dtype(at::kFloat));
-  if (rows == 0 || C == 0) return {g, part.zero_()};
   const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
                    aligned16(g.data_ptr());
   DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
     DGMC_DISPATCH_FLOAT(g_dtype, TR, [&] {
-      constexpr int V = Vec16<T>::N;
-      if (vec && C % V == 0) {
-        const int lanes = C / V;
-        if (lanes <= 8)
-          launch_relu_bias<T, T, TR, V, 8>(grad, out, g, part, blocks, rows,
-                                           C, relu);
-        else if (lanes <= 16)
-          launch_relu_bias<T, T, TR, V, 16>(grad, out, g, part, blocks, rows,
-                                            C, relu);
-        else if (lanes <= 32)
-          launch_relu_bias<T, T, TR, V, 32>(grad, out, g, part, blocks, rows,
-                                            C, relu);
-        else
-          launch_relu_bias<T, T, TR, V, 64>(grad, out, g, part, blocks, rows,
-                                            C, relu);
-      } else {
-        launch_relu_bias<T, T, TR, 1, 64>(grad, out, g, part, blocks, rows, C,
-                                          relu);
-      }
+      dispatch_colsum<T, TR, true>(grad, out.data_ptr(), g.data_ptr(), part,
+                                   db.data_ptr<float>(), blocks, rows, C,
+                                   relu, accumulate, vec);
     });
   });
   DGMC_CHECK_LAUNCH();
-  return {g, part};
+  return {g, db};
+}
+
+at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
+                   bool accumulate) {
+  TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous(),
+              "col_sum: contiguous [rows, C] expected");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  const int rows = src.size(0), C = src.size(1);
+  TORCH_CHECK(C <= 2048, "col_sum: C <= 2048");
+  at::Tensor out = dst_or_new(dst, C, src, accumulate);
+  if (C == 0) return out;
+  if (rows == 0) {
+    if (!accumulate) out.zero_();
+    return out;
+  }
+  const int blocks = colsum_blocks(rows);
+  at::Tensor part = at::empty({blocks, C}, src.options().dtype(at::kFloat));
+  const bool vec = aligned16(src.data_ptr());
+  DGMC_DISPATCH_FLOAT(src.scalar_type(), T, [&] {
+    dispatch_colsum<T, float, false>(src, src.data_ptr(), nullptr, part,
+                                     out.data_ptr<float>(), blocks, rows, C,
+                                     false, accumulate, vec);
+  });
+  DGMC_CHECK_LAUNCH();
+  return out;
 }
 
 // dst (+)= sum over the leading dim of src [S, n] (fp32), float4 vectorised.

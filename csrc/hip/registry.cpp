@@ -12,6 +12,12 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& self_scale,
                     const c10::optional<at::Tensor>& bias, bool relu,
                     at::ScalarType out_dtype);
+void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
+                  const at::Tensor& val, const at::Tensor& x,
+                  const c10::optional<at::Tensor>& self_x,
+                  const c10::optional<at::Tensor>& self_scale,
+                  const c10::optional<at::Tensor>& bias, bool relu,
+                  at::Tensor out);
 
 std::tuple<at::Tensor, at::Tensor> spline_basis(const at::Tensor& pseudo,
                                                 const at::Tensor& kernel_size,
@@ -54,10 +60,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
     const at::Tensor& w2);
 
-std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(const at::Tensor& grad,
-                                                 const at::Tensor& out,
-                                                 bool relu,
-                                                 at::ScalarType g_dtype);
+std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
+    const at::Tensor& grad, const at::Tensor& out, bool relu,
+    at::ScalarType g_dtype, const c10::optional<at::Tensor>& dbias,
+    bool accumulate);
+at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
+                   bool accumulate);
 void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
 
 }  // namespace dgmc
@@ -68,6 +76,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "self_x, Tensor? self_scale, Tensor? bias, bool relu, ScalarType "
       "out_dtype) -> "
       "Tensor");
+  m.def(
+      "spmm_csr_out(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
+      "self_x, Tensor? self_scale, Tensor? bias, bool relu, Tensor(a!) out) "
+      "-> ()");
   m.def(
       "spline_basis(Tensor pseudo, Tensor kernel_size, Tensor is_open, int "
       "degree) -> (Tensor, Tensor)");
@@ -90,8 +102,11 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
-      "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype) "
-      "-> (Tensor, Tensor)");
+      "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype, "
+      "Tensor(a!)? dbias=None, bool accumulate=False) -> (Tensor, Tensor)");
+  m.def(
+      "col_sum(Tensor src, Tensor(a!)? dst=None, bool accumulate=False) -> "
+      "Tensor");
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
   m.def(
       "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
@@ -104,6 +119,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spmm_csr", &dgmc::spmm_csr);
+  m.impl("spmm_csr_out", &dgmc::spmm_csr_out);
   m.impl("spline_basis", &dgmc::spline_basis);
   m.impl("dense_masked_softmax", &dgmc::dense_masked_softmax);
   m.impl("dense_masked_softmax_bwd", &dgmc::dense_masked_softmax_bwd);
@@ -114,6 +130,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("topk_dot", &dgmc::topk_dot);
   m.impl("sddmm", &dgmc::sddmm);
   m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
+  m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);

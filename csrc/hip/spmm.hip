@@ -132,23 +132,25 @@ void spmm_dispatch(const int* rowptr, const int* col, const float* val,
                                 out, R, C, relu);
 }
 
-at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
-                    const at::Tensor& val, const at::Tensor& x,
-                    const c10::optional<at::Tensor>& self_x,
-                    const c10::optional<at::Tensor>& self_scale,
-                    const c10::optional<at::Tensor>& bias, bool relu,
-                    at::ScalarType out_dtype) {
+static void spmm_into(const at::Tensor& rowptr, const at::Tensor& col,
+                      const at::Tensor& val, const at::Tensor& x,
+                      const c10::optional<at::Tensor>& self_x,
+                      const c10::optional<at::Tensor>& self_scale,
+                      const c10::optional<at::Tensor>& bias, bool relu,
+                      at::Tensor& out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous(), "spmm: x");
   TORCH_CHECK(rowptr.scalar_type() == at::kInt && col.scalar_type() == at::kInt,
               "spmm: int32 index expected");
   TORCH_CHECK(val.scalar_type() == at::kFloat, "spmm: fp32 values expected");
   TORCH_CHECK(col.numel() == val.numel(), "spmm: col/val size mismatch");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int64_t R = rowptr.numel() - 1;
   const int64_t C = x.size(1);
   TORCH_CHECK(R >= 0 && R < INT32_MAX && C < INT32_MAX, "spmm: size");
-  at::Tensor out = at::empty({R, C}, x.options().dtype(out_dtype));
-  if (R == 0 || C == 0) return out;
+  TORCH_CHECK(out.is_contiguous() && out.numel() == R * C &&
+                  out.device() == x.device(),
+              "spmm: out must be a contiguous tensor with R*C elements");
+  const at::ScalarType out_dtype = out.scalar_type();
+  if (R == 0 || C == 0) return;
 
   const at::Tensor* sx = nullptr;
   at::Tensor sx_c, ss_c, b_c;
@@ -182,7 +184,32 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                                (int)C, relu, vec_ok);
     });
   });
+  DGMC_CHECK_LAUNCH();
+}
+
+at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
+                    const at::Tensor& val, const at::Tensor& x,
+                    const c10::optional<at::Tensor>& self_x,
+                    const c10::optional<at::Tensor>& self_scale,
+                    const c10::optional<at::Tensor>& bias, bool relu,
+                    at::ScalarType out_dtype) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  at::Tensor out =
+      at::empty({rowptr.numel() - 1, x.size(1)}, x.options().dtype(out_dtype));
+  spmm_into(rowptr, col, val, x, self_x, self_scale, bias, relu, out);
   return out;
+}
+
+// Writes into a caller-owned buffer (e.g. a slot of a loop-gradient stack,
+// runtime/loopgrad.py), so the consumer needs no copy.
+void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
+                  const at::Tensor& val, const at::Tensor& x,
+                  const c10::optional<at::Tensor>& self_x,
+                  const c10::optional<at::Tensor>& self_scale,
+                  const c10::optional<at::Tensor>& bias, bool relu,
+                  at::Tensor out) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  spmm_into(rowptr, col, val, x, self_x, self_scale, bias, relu, out);
 }
 
 }  // namespace dgmc

@@ -31,6 +31,7 @@ from ..nn.inits import reset
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
 from ..ops.plans import _IdentityCache
+from ..runtime import loopgrad
 from ..runtime.cache import forward_cache
 from ..runtime.mode import is_reference_mode
 
@@ -170,7 +171,10 @@ class DGMC(torch.nn.Module):
         R_in = self.psi_2.in_channels
         steps = self.num_steps or 0
 
-        with torch.autocast(device_type=dev_type, enabled=False):
+        # loop_scope: psi_2 / MLP weight gradients of the num_steps uses are
+        # accumulated in place (runtime/loopgrad.py) instead of per use.
+        with torch.autocast(device_type=dev_type, enabled=False), \
+                loopgrad.loop_scope(not is_reference_mode()):
             f32 = torch.float64 if h_s.dtype == torch.float64 \
                 else torch.float32
             hs = lay_s.to_dense(h_s.to(f32))

@@ -13,9 +13,10 @@ import torch
 import torch.nn.functional as F
 from torch.nn import BatchNorm1d, Linear, ModuleList
 
-from ..ops.gemm import linear
+from ..ops.gemm import compute_dtype
 from ..ops.plans import relational_plan
-from ..ops.sparse import spmm
+from ..ops.sparse import gemm_spmm
+from ..runtime.cache import cached
 from .encoder import StackedEncoder
 
 
@@ -33,14 +34,23 @@ class RelConv(torch.nn.Module):
         for lin in (self.lin1, self.lin2, self.root):
             lin.reset_parameters()
 
+    def stacked_weight(self):
+        """``[in, 3 * out]`` fp32 operand ``[lin1 | lin2 | root]^T``,
+        memoised per forward scope."""
+        return cached(('rel_w', id(self)), lambda: torch.cat(
+            [self.lin1.weight, self.lin2.weight, self.root.weight],
+            dim=0).t())
+
     def forward(self, x, edge_index, act=None):
-        weight = torch.cat(
-            [self.lin1.weight, self.lin2.weight, self.root.weight], dim=0)
-        bias = torch.cat([self.root.bias.new_zeros(2 * self.out_channels),
-                          self.root.bias])
-        y = linear(x, weight, bias).view(-1, self.out_channels)
         plan = relational_plan(edge_index, x.size(0))
-        return spmm(plan, y, relu=(act == 'relu'))
+        dtype = compute_dtype(x)
+        w = self.stacked_weight()
+        w_lp = cached(('rel_w_lp', id(self), dtype),
+                      lambda: w.detach().to(dtype))
+        # root.bias enters through the root slot (coefficient 1) = output bias.
+        return gemm_spmm(plan, x, w, w_lp, self.out_channels,
+                         bias=self.root.bias, relu=(act == 'relu'),
+                         loop_key=(id(self), x.size(0), plan.num_cols))
 
     def __repr__(self):
         return '{}({}, {})'.format(type(self).__name__, self.in_channels,

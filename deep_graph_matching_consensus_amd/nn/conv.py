@@ -21,8 +21,8 @@ import torch
 from torch.nn import Parameter
 
 from ..ops.plans import spline_plan, adjacency_plan
-from ..ops.gemm import compute_dtype, mixed_matmul
-from ..ops.sparse import spmm
+from ..ops.gemm import compute_dtype
+from ..ops.sparse import gemm_spmm, spmm
 from ..runtime.cache import cached
 from .inits import reset, uniform
 
@@ -112,8 +112,9 @@ class SplineConv(torch.nn.Module):
         w = self.stacked_weight()
         w_lp = cached(('spline_w_lp', id(self), dtype),
                       lambda: w.detach().to(dtype))
-        y = mixed_matmul(x, w, w_lp).view(-1, self.out_channels)
-        return spmm(plan, y, bias=self.bias, relu=(act == 'relu'))
+        return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
+                         relu=(act == 'relu'),
+                         loop_key=(id(self), N, plan.num_cols))
 
     def __repr__(self):
         return '{}({}, {}, dim={})'.format(self.__class__.__name__,

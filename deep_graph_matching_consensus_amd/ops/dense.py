@@ -26,7 +26,8 @@ import torch
 
 from . import _backend
 from . import reference as ref
-from .gemm import mixed_matmul
+from .gemm import _col_sum, lowp_weight_t, mixed_matmul
+from ..runtime import loopgrad
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
@@ -104,13 +105,16 @@ def softmax_transport(S_hat, r_s, lay_s, lay_t):
 # ---------------------------------------------------------------------------
 class _ConsensusUpdate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, S_hat, P, Q, b1, w2, b2, ptr_s, ptr_t):
+    def forward(ctx, S_hat, P, Q, b1, w2, b2, ptr_s, ptr_t, loop):
         out = _backend.ops().dense_consensus(
             S_hat.float().contiguous(), P.contiguous(), Q.contiguous(),
             b1.float().contiguous(), w2.float().contiguous().view(-1),
             b2.float().contiguous().view(-1), ptr_s, ptr_t)
         ctx.save_for_backward(P, Q, b1, w2, ptr_s, ptr_t)
         ctx.meta = (S_hat.dtype, b1.dtype, w2.dtype, b2.dtype, b2.shape)
+        ctx.loop = loop
+        if loop is not None:
+            loop.register()
         return out
 
     @staticmethod
@@ -121,10 +125,23 @@ class _ConsensusUpdate(torch.autograd.Function):
             b1.float().contiguous(), w2.float().contiguous().view(-1), ptr_s,
             ptr_t)
         s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
-        db1 = dP.float().sum(0).to(b1_dt)
-        dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
-        db2 = db2_part.sum().view(b2_shape).to(b2_dt)
-        return (grad.to(s_dt), dP, dQ, db1, dw2, db2, None, None)
+        loop = ctx.loop
+        parts = (('b1', dP), ('w2', dw2_part), ('b2', db2_part.view(-1, 1)))
+        if loop is None:
+            db1, dw2, db2 = [_col_sum(t) for _, t in parts]
+        else:
+            for name, t in parts:
+                buf, acc = loop.acc(name, (t.size(1), ), t.device)
+                _col_sum(t, buf, acc)
+            db1 = dw2 = db2 = None
+            if loop.arrive():
+                db1, dw2, db2 = [loop.get_acc(n) for n, _ in parts]
+                loop.release()
+        if db1 is not None:
+            db1 = db1.to(b1_dt)
+            dw2 = dw2.view_as(w2).to(w2_dt)
+            db2 = db2.view(b2_shape).to(b2_dt)
+        return (grad.to(s_dt), dP, dQ, db1, dw2, db2, None, None, None)
 
 
 def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None):
@@ -138,14 +155,20 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None):
     B, N_s, N_t = S_hat.shape
     if _hip_ok(S_hat, N_s, N_t):
         w1t = lin1.weight.t()
+        key = (id(lin1.weight), )
         if o_joint is not None:
-            PQ = mixed_matmul(o_joint, w1t, w1t.detach().to(o_joint.dtype))
+            PQ = mixed_matmul(o_joint, w1t,
+                              lowp_weight_t(lin1.weight, o_joint.dtype),
+                              loop_key=key + (o_joint.size(0), ))
             P, Q = PQ[:lay_s.num_nodes], PQ[lay_s.num_nodes:]
         else:
-            P = mixed_matmul(o_s, w1t, w1t.detach().to(o_s.dtype))
-            Q = mixed_matmul(o_t, w1t, w1t.detach().to(o_t.dtype))
+            P = mixed_matmul(o_s, w1t, lowp_weight_t(lin1.weight, o_s.dtype),
+                             loop_key=key + (o_s.size(0), ))
+            Q = mixed_matmul(o_t, w1t, lowp_weight_t(lin1.weight, o_t.dtype),
+                             loop_key=key + (o_t.size(0), ))
+        loop = loopgrad.group(('consensus', id(mlp)))
         return _ConsensusUpdate.apply(S_hat, P, Q, lin1.bias, lin2.weight,
-                                      lin2.bias, lay_s.ptr, lay_t.ptr)
+                                      lin2.bias, lay_s.ptr, lay_t.ptr, loop)
     o_s_d = lay_s.to_dense(o_s.to(S_hat.dtype))
     o_t_d = lay_t.to_dense(o_t.to(S_hat.dtype))
     upd = ref.consensus_mlp_dense(o_s_d, o_t_d, lin1.weight, lin1.bias,

@@ -12,11 +12,15 @@ in ~33 us (s=16) and accumulates directly in fp32 for the fp32 master weight
 
 ``mixed_matmul(x, w, w_lp)`` computes ``x @ w`` in the autocast dtype with
 ``w_lp`` an (optionally cached) low-precision copy of the fp32 parameter
-``w``; gradients flow to ``x`` and to the fp32 ``w``.
+``w``; gradients flow to ``x`` and to the fp32 ``w``.  Inside a
+:func:`~..runtime.loopgrad.loop_scope` the weight/bias gradients of repeated
+uses are accumulated in place by the split-K combine / column-sum kernels.
 """
 import torch
 
 from . import _backend
+from ..runtime import loopgrad
+from ..runtime.cache import cached
 
 
 def _split_factor(m, n, k):
@@ -29,38 +33,56 @@ def _split_factor(m, n, k):
     return s
 
 
-def matmul_tn_fp32(a, b):
-    """``a^T @ b`` (``a [K, M]``, ``b [K, N]``) with fp32 output, split-K."""
+def matmul_tn_fp32(a, b, out=None, accumulate=False):
+    """``a^T @ b`` (``a [K, M]``, ``b [K, N]``) with fp32 output, split-K.
+
+    With ``out`` (fp32 ``[M, N]``) the product is written (or added, when
+    ``accumulate``) there; on the GPU the split-K combine does the
+    accumulation, so it costs no extra kernel.
+    """
     K, M = a.shape
     N = b.shape[1]
-    s = _split_factor(M, N, K) if a.is_cuda else 1
     if not a.is_cuda:
-        return a.float().t() @ b.float()
-    if s == 1:
-        return torch.mm(a.t(), b, out_dtype=torch.float32) \
-            if a.dtype != torch.float32 else a.t() @ b
-    k = K // s
-    main = k * s
-    a3 = a[:main].view(s, k, M).transpose(1, 2)
-    b3 = b[:main].view(s, k, N)
-    if a.dtype == torch.float32:
-        part = torch.bmm(a3, b3)
+        res = a.float().t() @ b.float()
     else:
-        part = torch.bmm(a3, b3, out_dtype=torch.float32)
-    if _backend.hip_available():
-        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
-        _backend.ops().reduce_add_rows(part, out, False)
+        s = _split_factor(M, N, K)
+        if s == 1:
+            res = torch.mm(a.t(), b, out_dtype=torch.float32) \
+                if a.dtype != torch.float32 else a.t() @ b
+        else:
+            k = K // s
+            main = k * s
+            a3 = a[:main].view(s, k, M).transpose(1, 2)
+            b3 = b[:main].view(s, k, N)
+            if a.dtype == torch.float32:
+                part = torch.bmm(a3, b3)
+            else:
+                part = torch.bmm(a3, b3, out_dtype=torch.float32)
+            if main < K:   # fold the remainder rows into the first split
+                tail = torch.mm(a[main:].t(), b[main:],
+                                out_dtype=torch.float32) \
+                    if a.dtype != torch.float32 else a[main:].t() @ b[main:]
+                part[0].add_(tail)
+            if _backend.hip_available():
+                if out is None:
+                    out = torch.empty((M, N), dtype=torch.float32,
+                                      device=a.device)
+                    accumulate = False
+                _backend.ops().reduce_add_rows(part, out, accumulate)
+                return out
+            res = part.sum(0)
+    if out is None:
+        return res
+    if accumulate:
+        out.add_(res)
     else:
-        out = part.sum(0)
-    if main < K:
-        tail = a[main:].t() @ b[main:]
-        out = out + tail.float()
+        out.copy_(res)
     return out
 
 
 class _MixedMatmul(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, w_lp, bias):
+    def forward(ctx, x, w, w_lp, bias, loop):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
         out = xc @ w_lp
         if bias is not None:
@@ -69,6 +91,9 @@ class _MixedMatmul(torch.autograd.Function):
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.loop = loop
+        if loop is not None:
+            loop.register()
         return out
 
     @staticmethod
@@ -80,11 +105,42 @@ class _MixedMatmul(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = (g @ w_lp.t()).to(ctx.x_dtype)
-        if ctx.needs_input_grad[1]:
-            gw = matmul_tn_fp32(xc.contiguous(), g).to(ctx.w_dtype)
-        if ctx.has_bias and ctx.needs_input_grad[3]:
-            gb = g.float().sum(0).to(ctx.bias_dtype)
-        return gx, gw, None, gb
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[3]
+        loop = ctx.loop
+        if loop is None:
+            if need_w:
+                gw = matmul_tn_fp32(xc.contiguous(), g).to(ctx.w_dtype)
+            if need_b:
+                gb = _col_sum(g).to(ctx.bias_dtype)
+            return gx, gw, None, gb, None
+        if need_w:
+            buf, acc = loop.acc('w', w_lp.shape, g.device)
+            matmul_tn_fp32(xc.contiguous(), g, out=buf, accumulate=acc)
+        if need_b:
+            buf, acc = loop.acc('b', (g.size(1), ), g.device)
+            _col_sum(g, buf, acc)
+        if loop.arrive():
+            if need_w:
+                gw = loop.get_acc('w').to(ctx.w_dtype)
+            if need_b:
+                gb = loop.get_acc('b').to(ctx.bias_dtype)
+            loop.release()
+        return gx, gw, None, gb, None
+
+
+def _col_sum(src, out=None, accumulate=False):
+    """Column sum of a 2-D tensor in fp32 (optionally into ``out``)."""
+    if _backend.use_hip(src):
+        return _backend.ops().col_sum(src.contiguous(), out, accumulate)
+    res = src.float().sum(0)
+    if out is None:
+        return res
+    if accumulate:
+        out.add_(res)
+    else:
+        out.copy_(res)
+    return out
 
 
 def compute_dtype(x):
@@ -94,7 +150,7 @@ def compute_dtype(x):
     return x.dtype
 
 
-def mixed_matmul(x, w, w_lp=None, bias=None):
+def mixed_matmul(x, w, w_lp=None, bias=None, loop_key=None):
     r"""``x @ w (+ bias)`` in the autocast dtype; fp32 gradient for ``w``.
 
     Args:
@@ -102,15 +158,34 @@ def mixed_matmul(x, w, w_lp=None, bias=None):
         w: ``[K, M]`` fp32 weight (receives the gradient).
         w_lp: optional pre-cast copy of ``w`` in the compute dtype.
         bias: optional ``[M]``.
+        loop_key: identifies the op instance inside a
+            :func:`~..runtime.loopgrad.loop_scope` (gradient accumulation
+            across loop iterations).
     """
     dtype = compute_dtype(x)
     if w_lp is None:
         w_lp = w.detach().to(dtype)
+    loop = loopgrad.group(('mm', ) + loop_key) if loop_key is not None \
+        else None
     with torch.autocast(device_type='cuda' if x.is_cuda else 'cpu',
                         enabled=False):
-        return _MixedMatmul.apply(x, w, w_lp.detach(), bias)
+        return _MixedMatmul.apply(x, w, w_lp.detach(), bias, loop)
+
+
+def lowp_weight_t(weight, dtype):
+    """``weight.t()`` cast to ``dtype``, memoised per forward scope for
+    parameters (the cache entry keeps the parameter alive, so its ``id``
+    cannot be recycled within the scope)."""
+    if not isinstance(weight, torch.nn.Parameter):
+        return weight.detach().t().to(dtype)
+    return cached(('w_lp_t', id(weight), dtype),
+                  lambda: (weight, weight.detach().t().to(dtype)))[1]
 
 
 def linear(x, weight, bias=None):
-    """``F.linear`` with split-K fp32 weight gradients (``weight [out, in]``)."""
-    return mixed_matmul(x, weight.t(), None, bias)
+    """``F.linear`` with split-K fp32 weight gradients (``weight [out, in]``).
+    Parameters reused inside a loop scope accumulate their gradient in
+    place."""
+    w_lp = lowp_weight_t(weight, compute_dtype(x))
+    key = (id(weight), ) if isinstance(weight, torch.nn.Parameter) else None
+    return mixed_matmul(x, weight.t(), w_lp, bias, loop_key=key)

@@ -113,11 +113,11 @@ class _SpMM(torch.autograd.Function):
         gbias = None
         need_bias = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         if _backend.use_hip(grad) and (ctx.relu or need_bias):
-            # Fused: g = grad * (out > 0) and per-block bias partials.
-            g, part = _backend.ops().relu_bias_bwd(
+            # Fused: g = grad * (out > 0) and the bias gradient.
+            g, db = _backend.ops().relu_bias_bwd(
                 grad, out if ctx.relu else grad, ctx.relu, ctx.x_dtype)
             if need_bias:
-                gbias = part.sum(0).to(ctx.bias_dtype)
+                gbias = db.to(ctx.bias_dtype)
         else:
             g = grad.float()
             if ctx.relu:
@@ -155,3 +155,110 @@ def spmm(op, x, self_x=None, self_scale=None, bias=None, relu=False,
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) \
             else torch.float32
     return _SpMM.apply(x, self_x, self_scale, bias, op, relu, out_dtype)
+
+
+# ---------------------------------------------------------------------------
+# Fused "GEMM then aggregate" layer (SplineConv / RelConv shape)
+# ---------------------------------------------------------------------------
+class _GemmSpMM(torch.autograd.Function):
+    """``out = act(A @ view(x @ W, [-1, C]) + bias)`` as ONE autograd node.
+
+    Backward: ``g' = grad * relu'`` and ``dbias`` (one fused kernel),
+    ``dY = A^T g'`` (written straight into the loop stack when ``loop`` is
+    set), ``dx = dY W^T``, ``dW = x^T dY`` - deferred to one long-K GEMM over
+    all loop uses (see :mod:`..runtime.loopgrad`).
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, w_lp, bias, op, relu, C, loop):
+        xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
+        y = (xc @ w_lp).view(-1, C)
+        out_dtype = y.dtype if y.dtype in (torch.bfloat16, torch.float16) \
+            else torch.float32
+        out = _spmm_raw(op, y, None, None, bias, relu, out_dtype)
+        ctx.save_for_backward(xc, w_lp, out if relu else None)
+        ctx.op, ctx.relu, ctx.C, ctx.loop = op, relu, C, loop
+        ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.idx = loop.register() if loop is not None else None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        from .gemm import matmul_tn_fp32
+        xc, w_lp, out = ctx.saved_tensors
+        loop, idx, C = ctx.loop, ctx.idx, ctx.C
+        grad = grad.contiguous()
+        dev = grad.device
+        need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
+        hip = _backend.use_hip(grad)
+        # 1. g' = grad * relu'(out) and the bias gradient.
+        db = None
+        if hip:
+            dbuf, acc = loop.acc('b', (C, ), dev) if (loop and need_b) \
+                else (None, False)
+            g, db = _backend.ops().relu_bias_bwd(
+                grad, out if ctx.relu else grad, ctx.relu, w_lp.dtype, dbuf,
+                acc)
+        else:
+            g = grad.float()
+            if ctx.relu:
+                g = g * (out > 0)
+            if need_b:
+                db = g.sum(0)
+                if loop is not None:
+                    loop.add_to('b', db)
+            g = g.to(w_lp.dtype)
+        # 2. dY = A^T g'.
+        opt = ctx.op.t()
+        if loop is not None:
+            dy = loop.slot('dy', idx, (opt.num_rows, C), w_lp.dtype, dev)
+            if hip:
+                _backend.ops().spmm_csr_out(opt.rowptr, opt.col, opt.val, g,
+                                            None, None, None, False, dy)
+            else:
+                dy.copy_(_spmm_raw(opt, g, None, None, None, False,
+                                   w_lp.dtype))
+            loop.slot('x', idx, xc.shape, xc.dtype, dev).copy_(xc)
+        else:
+            dy = _spmm_raw(opt, g, None, None, None, False, w_lp.dtype)
+        dY = dy.view(xc.size(0), -1)
+        # 3. dx and dW.
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (dY @ w_lp.t()).to(ctx.x_dtype)
+        if loop is None:
+            if ctx.needs_input_grad[1]:
+                gw = matmul_tn_fp32(xc.contiguous(), dY).to(ctx.w_dtype)
+            if need_b:
+                gb = db.to(ctx.bias_dtype)
+        elif loop.arrive():
+            if ctx.needs_input_grad[1]:
+                X = loop.stack('x')
+                X = X.view(-1, X.size(-1))
+                gw = matmul_tn_fp32(X, loop.stack('dy').view(X.size(0), -1))
+                gw = gw.to(ctx.w_dtype)
+            if need_b:
+                gb = loop.get_acc('b').to(ctx.bias_dtype)
+            loop.release()
+        return gx, gw, None, gb, None, None, None, None
+
+
+def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,
+              loop_key=None):
+    r"""``act(op @ (x @ w).view(-1, out_channels) + bias)``.
+
+    ``w [in, S * out]`` is the fp32 stacked weight (receives the gradient),
+    ``w_lp`` its compute-dtype copy; ``op`` maps the ``S`` slot rows of
+    every node to the output rows.  ``loop_key`` enables loop-shared gradient
+    accumulation inside :func:`~..runtime.loopgrad.loop_scope`.
+    """
+    from ..runtime import loopgrad
+    assert x.dim() == 2 and x.size(0) * (w.size(1) // out_channels) == \
+        op.num_cols, (x.shape, w.shape, op)
+    loop = loopgrad.group(('gemm_spmm', ) + loop_key) \
+        if loop_key is not None else None
+    with torch.autocast(device_type='cuda' if x.is_cuda else 'cpu',
+                        enabled=False):
+        return _GemmSpMM.apply(x, w, w_lp.detach(), bias, op, relu,
+                               out_channels, loop)

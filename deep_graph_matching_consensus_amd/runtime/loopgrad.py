@@ -1,0 +1,129 @@
+"""Loop-shared parameter gradients.
+
+The consensus loop (``/root/reference/dgmc/models/dgmc.py:167-179``) applies
+``psi_2`` and the consensus MLP ``num_steps`` times with the same weights.
+Plain autograd computes one weight gradient per use and sums them with an
+``add`` per reuse: for PascalVOC that is ~20 small split-K GEMMs (52 output
+tiles each for 256 CUs), ~20 combine kernels and ~100 accumulation adds per
+training step.
+
+Inside :func:`loop_scope` every op that owns a reused weight registers a
+:class:`LoopGrad` collector (one per op instance and forward) and its backward
+deposits *contributions* instead of returning gradients:
+
+* **stacked** - operands ``(x_l, dy_l)`` of ``dW = sum_l x_l^T dy_l`` are
+  written into slot ``l`` of ``[uses, ...]`` buffers (``dy`` directly by the
+  producing kernel); the last arriving use computes ONE GEMM with a
+  ``uses``-times longer reduction dimension (fills the chip, one split-K
+  combine);
+* **accumulated** - small reductions (bias/vector gradients, small GEMMs)
+  are folded into a persistent fp32 buffer by the producing kernel itself
+  (``accumulate`` flags of ``col_sum``/``relu_bias_bwd``/``reduce_add_rows``)
+  - no separate add kernels.
+
+Only the use whose backward completes the set returns the gradients; the
+others return ``None``.  This is order-independent (the count, not the order,
+decides) and deterministic (fixed fold order per buffer).  Requirement: all
+registered uses take part in the same backward pass - true for the consensus
+loop, whose every step feeds ``S_L``.
+"""
+import contextlib
+import threading
+
+import torch
+
+_TLS = threading.local()
+# Global switch (tests compare against plain per-use autograd).
+ENABLED = True
+
+
+class LoopGrad(object):
+    """Collects the gradient contributions of one op reused in a loop."""
+
+    def __init__(self):
+        self.uses = 0
+        self.arrived = 0
+        self._stacks = {}
+        self._accs = {}
+
+    def register(self):
+        """Called by every forward use; returns the use index."""
+        idx = self.uses
+        self.uses += 1
+        return idx
+
+    def slot(self, name, idx, shape, dtype, device):
+        """Slot ``idx`` of the ``[uses, *shape]`` stack ``name``."""
+        buf = self._stacks.get(name)
+        shape = tuple(shape)
+        if buf is None:
+            buf = torch.empty((self.uses, ) + shape, dtype=dtype,
+                              device=device)
+            self._stacks[name] = buf
+        assert buf.shape[1:] == shape and buf.dtype == dtype, \
+            'loop uses must have identical shapes ({} vs {})'.format(
+                tuple(buf.shape[1:]), shape)
+        return buf[idx]
+
+    def stack(self, name):
+        return self._stacks[name]
+
+    def acc(self, name, shape, device):
+        """``(buffer, accumulate)``: fp32 accumulator ``name``; ``accumulate``
+        is False for the first contribution (the producer overwrites)."""
+        buf = self._accs.get(name)
+        if buf is None:
+            buf = torch.empty(tuple(shape), dtype=torch.float32,
+                              device=device)
+            self._accs[name] = buf
+            return buf, False
+        return buf, True
+
+    def add_to(self, name, value):
+        """Accumulate a tensor computed elsewhere (fallback paths)."""
+        buf, accumulate = self.acc(name, value.shape, value.device)
+        if accumulate:
+            buf.add_(value)
+        else:
+            buf.copy_(value)
+
+    def get_acc(self, name):
+        return self._accs.get(name)
+
+    def arrive(self):
+        """Called once per backward use; True for the use completing the set
+        (which then computes/returns the gradients and calls
+        :meth:`release`)."""
+        self.arrived += 1
+        return self.arrived == self.uses
+
+    def release(self):
+        self._stacks = {}
+        self._accs = {}
+        self.arrived = 0
+
+
+@contextlib.contextmanager
+def loop_scope(enabled=True):
+    """Ops called inside share one :class:`LoopGrad` per op instance."""
+    outer = getattr(_TLS, 'groups', None)
+    if outer is not None or not (enabled and ENABLED):
+        yield
+        return
+    _TLS.groups = {}
+    try:
+        yield
+    finally:
+        _TLS.groups = None
+
+
+def group(key):
+    """The collector for ``key`` in the active loop scope, or None (no scope
+    or no autograd recording)."""
+    groups = getattr(_TLS, 'groups', None)
+    if groups is None or not torch.is_grad_enabled():
+        return None
+    g = groups.get(key)
+    if g is None:
+        g = groups[key] = LoopGrad()
+    return g
