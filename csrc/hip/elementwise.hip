@@ -20,57 +20,63 @@
 namespace dgmc {
 
 namespace {
-// Self-resetting tickets (atomicInc wraps to 0 at the last block).  Zero
+// Self-resetting tickets (atomicInc wraps to 0 at the last arrival).  Zero
 // initialised at code-object load, so no allocation or memset is needed and
-// the kernels are hipGraph-capturable.  Launches rotate through the slots;
-// kernels sharing a slot would have to be in flight concurrently to collide.
-constexpr int kTickets = 256;
-__device__ unsigned int g_tickets[kTickets];
-int next_ticket() {
+// the kernels are hipGraph-capturable.  Each launch uses one set of
+// kChunksMax + 1 counters; launches rotate through kTicketSets sets, so two
+// launches sharing a set would have to be in flight concurrently to collide.
+constexpr int kChunk = 32;            // blocks folded by a chunk's last block
+constexpr int kMaxColBlocks = 1024;   // => at most 32 chunks
+constexpr int kChunksMax = kMaxColBlocks / kChunk;
+constexpr int kTicketSets = 64;
+__device__ unsigned int g_tickets[kTicketSets * (kChunksMax + 1)];
+int next_ticket_set() {
   static int t = 0;
-  t = (t + 1) % kTickets;
-  return t;
+  t = (t + 1) % kTicketSets;
+  return t * (kChunksMax + 1);
 }
-constexpr int kMaxColBlocks = 128;
 }  // namespace
 
-// Last block: dst[c] (+)= sum_b part[b, c] in fixed b order (row groups then
-// an LDS fold).  256 threads.
-__device__ __forceinline__ void fold_partials(const float* __restrict__ part,
-                                              float* __restrict__ dst,
-                                              int nblocks, int C,
-                                              int accumulate, float* lds) {
+// dst[c] (+)= sum_{r < nrows} src[r, c] by one 256-thread block: thread
+// (c, rg) sums rows rg, rg + RG, ... with many loads in flight, then an LDS
+// fold over the RG row groups (fixed order -> deterministic).
+__device__ __forceinline__ void fold_rows(const float* __restrict__ src,
+                                          int nrows, int C,
+                                          float* __restrict__ dst,
+                                          int accumulate, float* lds) {
   const int tid = threadIdx.x;
-  if (C <= 256) {
-    const int groups = 256 / C;
-    const int c = tid % C, rg = tid / C;
-    float s = 0.f;
-    if (rg < groups)
-      for (int b = rg; b < nblocks; b += groups) s += part[(size_t)b * C + c];
-    if (rg < groups) lds[rg * C + c] = s;
+  for (int cb = 0; cb < C; cb += 256) {
+    const int cw = min(256, C - cb);
+    const int RG = 256 / cw;
+    const int cl = tid % cw, rg = tid / cw;
+    if (rg < RG) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = rg; r < nrows; r += RG) s += src[(size_t)r * C + cb + cl];
+      lds[rg * cw + cl] = s;
+    }
     __syncthreads();
-    if (tid < C) {
-      float t = accumulate ? dst[tid] : 0.f;
-      for (int g = 0; g < groups; ++g) t += lds[g * C + tid];
-      dst[tid] = t;
+    if (tid < cw) {
+      float t = accumulate ? dst[cb + tid] : 0.f;
+      for (int g = 0; g < RG; ++g) t += lds[g * cw + tid];
+      dst[cb + tid] = t;
     }
-  } else {
-    for (int c = tid; c < C; c += 256) {
-      float s = accumulate ? dst[c] : 0.f;
-      for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * C + c];
-      dst[c] = s;
-    }
+    __syncthreads();
   }
 }
 
 // LPR lanes own one row (VEC channels per pass); a block holds RPB = 256/LPR
 // row slots and walks its row range, keeping channel partials in registers;
-// the block partial goes through LDS to `part[block]`.
+// the block partial goes through LDS to `part[block]`.  The last block of
+// every chunk of kChunk blocks folds the chunk into `part2[chunk]`; the last
+// chunk folder folds `part2` into `dst`.  Three short latency stages instead
+// of one long serial fold.
 template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
 __global__ __launch_bounds__(256) void colsum_kernel(
     const TG* __restrict__ grad, const TO* __restrict__ out,
-    TR* __restrict__ g_out, float* __restrict__ part, float* __restrict__ dst,
-    int rows, int C, int relu, int accumulate, int ticket) {
+    TR* __restrict__ g_out, float* __restrict__ part,
+    float* __restrict__ part2, float* __restrict__ dst, int rows, int C,
+    int relu, int accumulate, int tickets) {
   constexpr int RPB = 256 / LPR;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [RPB][C]
   __shared__ bool is_last;
@@ -105,20 +111,42 @@ __global__ __launch_bounds__(256) void colsum_kernel(
     for (int k = 0; k < VEC; ++k) lds[slot * C + c0 + k] = acc[k];
   }
   __syncthreads();
+  const int nblocks = gridDim.x;
+  float* my_dst = nblocks == 1 ? dst : part + (size_t)blockIdx.x * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f;
+    float s = nblocks == 1 && accumulate ? dst[c] : 0.f;
     for (int q = 0; q < RPB; ++q) s += lds[q * C + c];
-    part[(size_t)blockIdx.x * C + c] = s;
+    my_dst[c] = s;
   }
-  // Publish the partial, take a ticket; the last block folds.
+  if (nblocks == 1) return;
+  // Stage 2: last block of the chunk folds it.
+  const int chunk = blockIdx.x / kChunk;
+  const int chunk_blocks = min(kChunk, nblocks - chunk * kChunk);
+  const int nchunks = (nblocks + kChunk - 1) / kChunk;
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0)
-    is_last = atomicInc(&g_tickets[ticket], gridDim.x - 1) == gridDim.x - 1;
+    is_last = atomicInc(&g_tickets[tickets + chunk], chunk_blocks - 1) ==
+              (unsigned)(chunk_blocks - 1);
   __syncthreads();
   if (!is_last) return;
   __threadfence();
-  fold_partials(part, dst, gridDim.x, C, accumulate, lds);
+  if (nchunks == 1) {
+    fold_rows(part, nblocks, C, dst, accumulate, lds);
+    return;
+  }
+  fold_rows(part + (size_t)chunk * kChunk * C, chunk_blocks, C,
+            part2 + (size_t)chunk * C, 0, lds);
+  // Stage 3: last chunk folder folds the chunk partials.
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    is_last = atomicInc(&g_tickets[tickets + kChunksMax], nchunks - 1) ==
+              (unsigned)(nchunks - 1);
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  fold_rows(part2, nchunks, C, dst, accumulate, lds);
 }
 
 template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
@@ -127,12 +155,14 @@ void launch_colsum(const at::Tensor& grad, const void* out, void* g,
                    bool relu, bool accumulate) {
   constexpr int RPB = 256 / LPR;
   const size_t lds = std::max<size_t>(RPB * C, 256) * sizeof(float);
+  float* p = part.data_ptr<float>();
   hipLaunchKernelGGL((colsum_kernel<TG, TO, TR, VEC, LPR, WRITE_G>),
                      dim3(blocks), dim3(256), lds, stream(),
                      reinterpret_cast<const TG*>(grad.data_ptr()),
                      reinterpret_cast<const TO*>(out),
-                     reinterpret_cast<TR*>(g), part.data_ptr<float>(), dst,
-                     rows, C, relu ? 1 : 0, accumulate ? 1 : 0, next_ticket());
+                     reinterpret_cast<TR*>(g), p, p + (size_t)blocks * C, dst,
+                     rows, C, relu ? 1 : 0, accumulate ? 1 : 0,
+                     next_ticket_set());
 }
 
 template <typename T, typename TR, bool WRITE_G>
@@ -160,8 +190,14 @@ void dispatch_colsum(const at::Tensor& grad, const void* out, void* g,
   }
 }
 
+// ~16 rows per block: one row per row-slot for typical widths, so the main
+// pass is a single round trip of loads across >= 256 CUs.
 static int colsum_blocks(int rows) {
-  return std::max(1, std::min((rows + 63) / 64, kMaxColBlocks));
+  return std::max(1, std::min((rows + 15) / 16, kMaxColBlocks));
+}
+
+static int64_t colsum_part_rows(int blocks) {
+  return blocks + (blocks + kChunk - 1) / kChunk;
 }
 
 static at::Tensor dst_or_new(const c10::optional<at::Tensor>& dst, int64_t C,
@@ -196,7 +232,8 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     return {g, db};
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({blocks, C}, grad.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({colsum_part_rows(blocks), C},
+                              grad.options().dtype(at::kFloat));
   const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
                    aligned16(g.data_ptr());
   DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
@@ -224,7 +261,8 @@ at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
     return out;
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({blocks, C}, src.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({colsum_part_rows(blocks), C},
+                              src.options().dtype(at::kFloat));
   const bool vec = aligned16(src.data_ptr());
   DGMC_DISPATCH_FLOAT(src.scalar_type(), T, [&] {
     dispatch_colsum<T, float, false>(src, src.data_ptr(), nullptr, part,

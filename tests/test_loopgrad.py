@@ -43,7 +43,8 @@ def _compare(model, args, y, rtol, autocast=False):
     for n in g0:
         err = (g0[n] - g1[n]).abs().max().item()
         scale = g0[n].abs().max().item() + 1e-12
-        assert err <= rtol * scale, (n, err, scale)
+        # (psi_2.final.bias cancels in P_i - Q_j: its gradient is ~0.)
+        assert err <= rtol * scale + 1e-6, (n, err, scale)
     # Every psi_2 / MLP parameter actually received a gradient.
     assert any(n.startswith('psi_2.') for n in g1)
     assert 'mlp.0.weight' in g1
