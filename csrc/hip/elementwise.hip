@@ -4,12 +4,10 @@
 // backward needs g' = grad * (out > 0) for the transposed aggregation and
 // dbias = sum_rows g'.  Eager PyTorch spends four kernels (compare, mul,
 // column reduction, cast) plus one gradient-accumulation add per reuse of
-// the bias; this kernel does everything in ONE launch: each workgroup owns a
-// row range, writes g' and one fp32 column partial; the last workgroup to
-// finish (ticket counter) folds the partials in fixed order into `dbias`,
-// optionally accumulating into an existing fp32 buffer (the consensus loop
-// reuses psi_2's biases ten times - see runtime/loopgrad.py).  Deterministic:
-// the fold order does not depend on which block finishes last.
+// the bias; here: one pass writing g' and per-block fp32 column partials,
+// then a small fold kernel into `dbias`, optionally accumulating into an
+// existing fp32 buffer (the consensus loop reuses psi_2's biases ten times -
+// see runtime/loopgrad.py).  Deterministic (fixed fold order).
 //
 // col_sum: the same machinery without the g' output (dst (+)= sum_rows src).
 //
@@ -20,66 +18,25 @@
 namespace dgmc {
 
 namespace {
-// Self-resetting tickets (atomicInc wraps to 0 at the last arrival).  Zero
-// initialised at code-object load, so no allocation or memset is needed and
-// the kernels are hipGraph-capturable.  Each launch uses one set of
-// kChunksMax + 1 counters; launches rotate through kTicketSets sets, so two
-// launches sharing a set would have to be in flight concurrently to collide.
-constexpr int kChunk = 32;            // blocks folded by a chunk's last block
-constexpr int kMaxColBlocks = 1024;   // => at most 32 chunks
-constexpr int kChunksMax = kMaxColBlocks / kChunk;
-constexpr int kTicketSets = 64;
-__device__ unsigned int g_tickets[kTicketSets * (kChunksMax + 1)];
-int next_ticket_set() {
-  static int t = 0;
-  t = (t + 1) % kTicketSets;
-  return t * (kChunksMax + 1);
-}
+constexpr int kMaxColBlocks = 256;   // partial rows folded by the 2nd kernel
 }  // namespace
 
-// dst[c] (+)= sum_{r < nrows} src[r, c] by one 256-thread block: thread
-// (c, rg) sums rows rg, rg + RG, ... with many loads in flight, then an LDS
-// fold over the RG row groups (fixed order -> deterministic).
-__device__ __forceinline__ void fold_rows(const float* __restrict__ src,
-                                          int nrows, int C,
-                                          float* __restrict__ dst,
-                                          int accumulate, float* lds) {
-  const int tid = threadIdx.x;
-  for (int cb = 0; cb < C; cb += 256) {
-    const int cw = min(256, C - cb);
-    const int RG = 256 / cw;
-    const int cl = tid % cw, rg = tid / cw;
-    if (rg < RG) {
-      float s = 0.f;
-#pragma unroll 8
-      for (int r = rg; r < nrows; r += RG) s += src[(size_t)r * C + cb + cl];
-      lds[rg * cw + cl] = s;
-    }
-    __syncthreads();
-    if (tid < cw) {
-      float t = accumulate ? dst[cb + tid] : 0.f;
-      for (int g = 0; g < RG; ++g) t += lds[g * cw + tid];
-      dst[cb + tid] = t;
-    }
-    __syncthreads();
-  }
-}
+// NOTE (MI355X): a single-kernel "last block folds" reduction needs a
+// device-scope release fence per block, which gfx950 lowers to
+// `buffer_wbl2 sc1` - a write-back of the XCD's whole L2.  Measured: 76 us
+// for a [9216, 128] column sum.  Two launches (partials, then a fold) cost
+// ~2 us of extra launch latency inside a hipGraph instead.
 
-// LPR lanes own one row (VEC channels per pass); a block holds RPB = 256/LPR
-// row slots and walks its row range, keeping channel partials in registers;
-// the block partial goes through LDS to `part[block]`.  The last block of
-// every chunk of kChunk blocks folds the chunk into `part2[chunk]`; the last
-// chunk folder folds `part2` into `dst`.  Three short latency stages instead
-// of one long serial fold.
+// Stage 1.  LPR lanes own one row (VEC channels per pass); a block holds
+// RPB = 256/LPR row slots and walks its row range, keeping channel partials
+// in registers; the block partial goes through LDS to `part[block]`.
 template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
 __global__ __launch_bounds__(256) void colsum_kernel(
     const TG* __restrict__ grad, const TO* __restrict__ out,
-    TR* __restrict__ g_out, float* __restrict__ part,
-    float* __restrict__ part2, float* __restrict__ dst, int rows, int C,
-    int relu, int accumulate, int tickets) {
+    TR* __restrict__ g_out, float* __restrict__ part, int rows, int C,
+    int relu) {
   constexpr int RPB = 256 / LPR;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [RPB][C]
-  __shared__ bool is_last;
   const int slot = threadIdx.x / LPR, lane = threadIdx.x % LPR;
   const int per = (rows + gridDim.x - 1) / gridDim.x;
   const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
@@ -87,6 +44,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+#pragma unroll 2
     for (int r = r0 + slot; r < r1; r += RPB) {
       const size_t o = (size_t)r * C + c0;
       float g[VEC], m[VEC];
@@ -111,42 +69,35 @@ __global__ __launch_bounds__(256) void colsum_kernel(
     for (int k = 0; k < VEC; ++k) lds[slot * C + c0 + k] = acc[k];
   }
   __syncthreads();
-  const int nblocks = gridDim.x;
-  float* my_dst = nblocks == 1 ? dst : part + (size_t)blockIdx.x * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = nblocks == 1 && accumulate ? dst[c] : 0.f;
+    float s = 0.f;
     for (int q = 0; q < RPB; ++q) s += lds[q * C + c];
-    my_dst[c] = s;
+    part[(size_t)blockIdx.x * C + c] = s;
   }
-  if (nblocks == 1) return;
-  // Stage 2: last block of the chunk folds it.
-  const int chunk = blockIdx.x / kChunk;
-  const int chunk_blocks = min(kChunk, nblocks - chunk * kChunk);
-  const int nchunks = (nblocks + kChunk - 1) / kChunk;
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0)
-    is_last = atomicInc(&g_tickets[tickets + chunk], chunk_blocks - 1) ==
-              (unsigned)(chunk_blocks - 1);
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  if (nchunks == 1) {
-    fold_rows(part, nblocks, C, dst, accumulate, lds);
-    return;
+}
+
+// Stage 2.  dst[c] (+)= sum_r part[r, c]: block = 32 columns x 8 row groups,
+// each thread keeps 8 loads in flight; LDS fold in fixed order
+// (deterministic).
+__global__ __launch_bounds__(256) void fold_rows_kernel(
+    const float* __restrict__ part, float* __restrict__ dst, int nrows, int C,
+    int accumulate) {
+  __shared__ float lds[8][33];
+  const int cl = threadIdx.x % 32, rg = threadIdx.x / 32;
+  const int c = blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (c < C) {
+#pragma unroll 8
+    for (int r = rg; r < nrows; r += 8) s += part[(size_t)r * C + c];
   }
-  fold_rows(part + (size_t)chunk * kChunk * C, chunk_blocks, C,
-            part2 + (size_t)chunk * C, 0, lds);
-  // Stage 3: last chunk folder folds the chunk partials.
-  __threadfence();
+  lds[rg][cl] = s;
   __syncthreads();
-  if (threadIdx.x == 0)
-    is_last = atomicInc(&g_tickets[tickets + kChunksMax], nchunks - 1) ==
-              (unsigned)(nchunks - 1);
-  __syncthreads();
-  if (!is_last) return;
-  __threadfence();
-  fold_rows(part2, nchunks, C, dst, accumulate, lds);
+  if (rg == 0 && c < C) {
+    float t = accumulate ? dst[c] : 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += lds[g][cl];
+    dst[c] = t;
+  }
 }
 
 template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
@@ -154,15 +105,16 @@ void launch_colsum(const at::Tensor& grad, const void* out, void* g,
                    at::Tensor& part, float* dst, int blocks, int rows, int C,
                    bool relu, bool accumulate) {
   constexpr int RPB = 256 / LPR;
-  const size_t lds = std::max<size_t>(RPB * C, 256) * sizeof(float);
-  float* p = part.data_ptr<float>();
+  const size_t lds = (size_t)RPB * C * sizeof(float);
   hipLaunchKernelGGL((colsum_kernel<TG, TO, TR, VEC, LPR, WRITE_G>),
                      dim3(blocks), dim3(256), lds, stream(),
                      reinterpret_cast<const TG*>(grad.data_ptr()),
                      reinterpret_cast<const TO*>(out),
-                     reinterpret_cast<TR*>(g), p, p + (size_t)blocks * C, dst,
-                     rows, C, relu ? 1 : 0, accumulate ? 1 : 0,
-                     next_ticket_set());
+                     reinterpret_cast<TR*>(g), part.data_ptr<float>(), rows, C,
+                     relu ? 1 : 0);
+  hipLaunchKernelGGL(fold_rows_kernel, dim3((C + 31) / 32), dim3(256), 0,
+                     stream(), part.data_ptr<float>(), dst, blocks, C,
+                     accumulate ? 1 : 0);
 }
 
 template <typename T, typename TR, bool WRITE_G>
@@ -190,14 +142,8 @@ void dispatch_colsum(const at::Tensor& grad, const void* out, void* g,
   }
 }
 
-// ~16 rows per block: one row per row-slot for typical widths, so the main
-// pass is a single round trip of loads across >= 256 CUs.
 static int colsum_blocks(int rows) {
   return std::max(1, std::min((rows + 15) / 16, kMaxColBlocks));
-}
-
-static int64_t colsum_part_rows(int blocks) {
-  return blocks + (blocks + kChunk - 1) / kChunk;
 }
 
 static at::Tensor dst_or_new(const c10::optional<at::Tensor>& dst, int64_t C,
@@ -232,8 +178,7 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     return {g, db};
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({colsum_part_rows(blocks), C},
-                              grad.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({blocks, C}, grad.options().dtype(at::kFloat));
   const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
                    aligned16(g.data_ptr());
   DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
@@ -261,8 +206,7 @@ at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
     return out;
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({colsum_part_rows(blocks), C},
-                              src.options().dtype(at::kFloat));
+  at::Tensor part = at::empty({blocks, C}, src.options().dtype(at::kFloat));
   const bool vec = aligned16(src.data_ptr());
   DGMC_DISPATCH_FLOAT(src.scalar_type(), T, [&] {
     dispatch_colsum<T, float, false>(src, src.data_ptr(), nullptr, part,
