@@ -1,0 +1,298 @@
+// Fused gather + MFMA GEMM for slot-structured message passing.
+//
+//   out[i, :] = act( sum_k Z_k[i, :] @ W_k + bias ),
+//   Z_k[i, :] = sum_{e in (i, k)} a_e * X[j_e, :]
+//
+// is SplineConv (k = B-spline slot, 25 + root for psi_2) and RelConv (k in
+// {in-flow, out-flow, root}) - see /root/reference/dgmc/models/spline.py:49
+// and rel.py:26-31.  The unfused formulation (nn/conv.py) materialises
+// Y = X @ [W_0 | ... | W_{S-1}] ([N, S*C], 61 MB for psi_2 at PascalVOC
+// batch 512) and gathers it back; both passes ran at ~2.2 TB/s in hipBLASLt's
+// skinny-GEMM kernels and the SpMM (45 us per layer).  Here Z never leaves
+// the CU:
+//
+// * block = 64 destination rows x 64 output columns, 4 waves (2 x 2 tiles of
+//   32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in registers);
+// * the block's slot-CSR metadata (row pointers, source ids, coefficients)
+//   is staged in LDS once;
+// * per slot: the Z_k tile is gathered (16-byte bf16 loads of L2-resident X
+//   rows, fp32 FMA, one bf16 rounding) into one of two LDS buffers while the
+//   other buffer feeds the MFMAs - one barrier per slot; the W_k fragments of
+//   slot k+1 are loaded from L2 into registers during slot k;
+// * epilogue: + bias, ReLU, store (bf16/fp32).
+//
+// The backward of the same layer is the same kernel on the transposed
+// operator (slot-CSR of A^T has rows j*S + k) with W_k^T read in place, and
+// it can write the gathered tiles (= dY = A^T G) for the weight-gradient
+// GEMM (runtime/loopgrad.py stacks them across consensus steps).
+#include "common.h"
+
+namespace dgmc {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+constexpr int kGG_BM = 64;
+constexpr int kGG_BN = 64;
+constexpr int kGG_ECAP = 4096;  // staged (col, val) entries per block
+
+__device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
+  bf16x8_t r;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) r[c] = (__bf16)v[c];
+  return r;
+}
+
+template <int K, bool WRITE_Z, typename TOUT>
+__global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
+    const __hip_bfloat16* __restrict__ X, const int* __restrict__ srp,
+    const int* __restrict__ ecol, const float* __restrict__ eval,
+    const __hip_bfloat16* __restrict__ Wb, int64_t ss, int64_t sn,
+    const float* __restrict__ bias, int relu, TOUT* __restrict__ out,
+    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M) {
+  constexpr int BM = kGG_BM, BN = kGG_BN;
+  constexpr int KP = K + 8;          // padded LDS row (bf16 elements)
+  constexpr int LPR = K / 8;         // gather lanes per row (16 B each)
+  constexpr int RPP = 256 / LPR;     // rows per gather pass
+  constexpr int PASSES = BM / RPP;
+  constexpr int KS = K / 16;         // MFMA k-steps per slot
+  static_assert(BM % RPP == 0, "gather mapping");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* zbuf = reinterpret_cast<__bf16*>(smem);              // [2][BM][KP]
+  int* srp_l = reinterpret_cast<int*>(zbuf + 2 * BM * KP);     // [BM*S+1]
+  const int srp_n = BM * S + 1;
+  int* ecol_l = srp_l + ((srp_n + 3) & ~3);                     // [ECAP]
+  float* eval_l = reinterpret_cast<float*>(ecol_l + kGG_ECAP);  // [ECAP]
+
+  const int tid = threadIdx.x;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int i0 = tile * BM;
+  const int n0 = blockIdx.y * BN;
+  const int rows = min(BM, Ndst - i0);
+
+  // ---- stage the block's slot-CSR metadata ------------------------------
+  const int nsrp = rows * S + 1;
+  for (int t = tid; t < nsrp; t += 256) srp_l[t] = srp[(size_t)i0 * S + t];
+  __syncthreads();
+  const int ebase = srp_l[0];
+  const int ecount = srp_l[rows * S] - ebase;
+  const bool staged = ecount <= kGG_ECAP;
+  if (staged) {
+    for (int t = tid; t < ecount; t += 256) {
+      ecol_l[t] = ecol[ebase + t];
+      eval_l[t] = eval[ebase + t];
+    }
+  }
+  __syncthreads();
+
+  // ---- gather Z_k for the block into LDS buffer `buf` -------------------
+  const int q = tid % LPR, rg = tid / LPR;
+  auto gather = [&](int k, int buf) {
+    __bf16* zb = zbuf + buf * BM * KP;
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int r = p * RPP + rg;
+      float acc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+      if (r < rows) {
+        const int e0 = srp_l[r * S + k] - ebase;
+        const int e1 = srp_l[r * S + k + 1] - ebase;
+        for (int e = e0; e < e1; ++e) {
+          int j;
+          float a;
+          if (staged) {
+            j = ecol_l[e];
+            a = eval_l[e];
+          } else {
+            j = ecol[ebase + e];
+            a = eval[ebase + e];
+          }
+          float xv[8];
+          load_vec<__hip_bfloat16, 8>(X + (size_t)j * K + q * 8, xv);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc[c] = fmaf(a, xv[c], acc[c]);
+        }
+      }
+      const bf16x8_t v = pack_bf16x8(acc);
+      *reinterpret_cast<bf16x8_t*>(zb + r * KP + q * 8) = v;
+      if constexpr (WRITE_Z) {
+        if (blockIdx.y == 0 && r < rows)
+          *reinterpret_cast<bf16x8_t*>(
+              reinterpret_cast<__bf16*>(Z) +
+              ((size_t)(i0 + r) * S + k) * K + q * 8) = v;
+      }
+    }
+  };
+
+  // ---- MFMA tiles --------------------------------------------------------
+  const int wave = tid / 64, lane = tid % 64;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int col = n0 + wc * 32 + lr;
+  const bool wave_active = n0 + wc * 32 < M;   // wave-uniform
+  const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
+  bf16x8_t bcur[KS], bnext[KS];
+  auto load_b = [&](int k, bf16x8_t* b) {
+    const __bf16* base = W + (size_t)k * ss + (size_t)col * sn + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      b[s] = *reinterpret_cast<const bf16x8_t*>(base + 16 * s);
+  };
+  f32x16_t acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+
+  if (wave_active) load_b(0, bcur);
+  gather(0, 0);
+  __syncthreads();
+  for (int k = 0; k < S; ++k) {
+    const int buf = k & 1;
+    if (wave_active) {
+      if (k + 1 < S) load_b(k + 1, bnext);
+      const __bf16* za = zbuf + buf * BM * KP + (wr * 32 + lr) * KP + 8 * lh;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(za + 16 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bcur[s], acc, 0, 0,
+                                                       0);
+      }
+    }
+    if (k + 1 < S) gather(k + 1, buf ^ 1);
+    __syncthreads();
+    if (wave_active) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) bcur[s] = bnext[s];
+    }
+  }
+
+  // ---- epilogue ----------------------------------------------------------
+  if (!wave_active || col >= M) return;
+  const float b = bias ? bias[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    if (row < rows) {
+      float v = acc[r] + b;
+      if (relu) v = fmaxf(v, 0.f);
+      out[(size_t)(i0 + row) * M + col] = Cvt<TOUT>::from_f(v);
+    }
+  }
+}
+
+template <int K, bool WRITE_Z, typename TOUT>
+static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
+                      const at::Tensor& ecol, const at::Tensor& eval,
+                      const at::Tensor& W, int64_t ss, int64_t sn,
+                      const float* bias, bool relu, at::Tensor& out,
+                      __hip_bfloat16* Z, int Ndst, int S, int M) {
+  const size_t srp_n = (size_t)kGG_BM * S + 1;
+  const size_t lds = (size_t)2 * kGG_BM * (K + 8) * 2 +
+                     ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8;
+  TORCH_CHECK(lds <= 160 * 1024, "gather_gemm: LDS budget exceeded (S=", S,
+              ")");
+  auto kern = gather_gemm_kernel<K, WRITE_Z, TOUT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DGMC_CHECK_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kern),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  dim3 grid((Ndst + kGG_BM - 1) / kGG_BM, (M + kGG_BN - 1) / kGG_BN);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
+                     srp.data_ptr<int>(), ecol.data_ptr<int>(),
+                     eval.data_ptr<float>(),
+                     reinterpret_cast<const __hip_bfloat16*>(W.data_ptr()), ss,
+                     sn, bias, relu ? 1 : 0,
+                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst, S, M);
+}
+
+template <int K>
+static void dispatch_gg(const at::Tensor& X, const at::Tensor& srp,
+                        const at::Tensor& ecol, const at::Tensor& eval,
+                        const at::Tensor& W, int64_t ss, int64_t sn,
+                        const float* bias, bool relu, at::Tensor& out,
+                        __hip_bfloat16* Z, int Ndst, int S, int M) {
+  const bool f32 = out.scalar_type() == at::kFloat;
+  if (Z) {
+    if (f32)
+      launch_gg<K, true, float>(X, srp, ecol, eval, W, ss, sn, bias, relu,
+                                out, Z, Ndst, S, M);
+    else
+      launch_gg<K, true, __hip_bfloat16>(X, srp, ecol, eval, W, ss, sn, bias,
+                                         relu, out, Z, Ndst, S, M);
+  } else {
+    if (f32)
+      launch_gg<K, false, float>(X, srp, ecol, eval, W, ss, sn, bias, relu,
+                                 out, Z, Ndst, S, M);
+    else
+      launch_gg<K, false, __hip_bfloat16>(X, srp, ecol, eval, W, ss, sn, bias,
+                                          relu, out, Z, Ndst, S, M);
+  }
+}
+
+// X [Nsrc, K] bf16; srp [Ndst*S + 1] int32 slot-CSR (row i*S + k);
+// ecol/eval entries; W bf16 with element (slot k, out col n, in kk) at
+// W[k*ss + n*sn + kk]; optional bias [M]; optional Z [Ndst*S, K] bf16 output.
+at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
+                       const at::Tensor& ecol, const at::Tensor& eval,
+                       const at::Tensor& W, int64_t ss, int64_t sn,
+                       int64_t num_slots, int64_t M,
+                       const c10::optional<at::Tensor>& bias, bool relu,
+                       at::ScalarType out_dtype,
+                       const c10::optional<at::Tensor>& Z) {
+  TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.is_contiguous() &&
+                  X.scalar_type() == at::kBFloat16,
+              "gather_gemm: X must be contiguous bf16 [N, K]");
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 && W.is_cuda(),
+              "gather_gemm: W must be bf16");
+  TORCH_CHECK(srp.scalar_type() == at::kInt && ecol.scalar_type() == at::kInt &&
+                  eval.scalar_type() == at::kFloat,
+              "gather_gemm: int32 index / fp32 value expected");
+  TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kFloat,
+              "gather_gemm: bf16 or fp32 output");
+  const int K = X.size(1);
+  const int S = num_slots;
+  TORCH_CHECK(S >= 1 && (srp.numel() - 1) % S == 0,
+              "gather_gemm: srp size must be Ndst*S + 1");
+  const int Ndst = (srp.numel() - 1) / S;
+  TORCH_CHECK(M > 0 && M % 32 == 0, "gather_gemm: M % 32 == 0");
+  TORCH_CHECK(ss % 8 == 0 && sn % 8 == 0 && aligned16(W.data_ptr()) &&
+                  aligned16(X.data_ptr()),
+              "gather_gemm: 16-byte aligned operand rows required");
+  // Bounds of the strided W reads.
+  TORCH_CHECK((S - 1) * ss + (M - 1) * sn + K <= W.numel(),
+              "gather_gemm: W too small for (S, M, K, strides)");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  at::Tensor out = at::empty({Ndst, M}, X.options().dtype(out_dtype));
+  at::Tensor b_c;
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    b_c = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b_c.numel() == M, "gather_gemm: bias size");
+    bp = b_c.data_ptr<float>();
+  }
+  __hip_bfloat16* zp = nullptr;
+  if (Z.has_value() && Z->defined()) {
+    TORCH_CHECK(Z->scalar_type() == at::kBFloat16 && Z->is_contiguous() &&
+                    Z->numel() == (int64_t)Ndst * S * K &&
+                    aligned16(Z->data_ptr()),
+                "gather_gemm: Z must be contiguous bf16 [Ndst*S, K]");
+    zp = reinterpret_cast<__hip_bfloat16*>(Z->data_ptr());
+  }
+  if (Ndst == 0) return out;
+  switch (K) {
+    case 32: dispatch_gg<32>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
+    case 64: dispatch_gg<64>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
+    case 128: dispatch_gg<128>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
+    case 256: dispatch_gg<256>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
+    default: TORCH_CHECK(false, "gather_gemm: K must be 32, 64, 128 or 256");
+  }
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+}  // namespace dgmc

@@ -67,6 +67,13 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
 at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
                    bool accumulate);
 void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
+at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
+                       const at::Tensor& ecol, const at::Tensor& eval,
+                       const at::Tensor& W, int64_t ss, int64_t sn,
+                       int64_t num_slots, int64_t M,
+                       const c10::optional<at::Tensor>& bias, bool relu,
+                       at::ScalarType out_dtype,
+                       const c10::optional<at::Tensor>& Z);
 
 }  // namespace dgmc
 
@@ -109,6 +116,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor");
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
   m.def(
+      "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
+      "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
+      "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
+  m.def(
       "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
       "Tensor Q, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def(
@@ -132,6 +143,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
   m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
+  m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
 }

@@ -46,7 +46,8 @@ class RelConv(torch.nn.Module):
         dtype = compute_dtype(x)
         w = self.stacked_weight()
         w_lp = cached(('rel_w_lp', id(self), dtype),
-                      lambda: w.detach().to(dtype))
+                      lambda: w.detach().to(
+                          dtype, memory_format=torch.contiguous_format))
         # root.bias enters through the root slot (coefficient 1) = output bias.
         return gemm_spmm(plan, x, w, w_lp, self.out_channels,
                          bias=self.root.bias, relu=(act == 'relu'),

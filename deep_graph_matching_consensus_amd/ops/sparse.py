@@ -76,6 +76,22 @@ class SparseOperator(object):
             self._t._t = self
         return self._t
 
+    def slot_csr(self, num_slots):
+        """``[R * S, C / S]`` re-indexing of a slot-structured operator
+        (columns ``j * S + k``): row ``i * S + k`` lists the source nodes
+        ``j`` of slot ``k`` - the gather order of :func:`gemm_spmm`'s fused
+        kernel.  Cached."""
+        cache = self.__dict__.setdefault('_slot_csr', {})
+        sc = cache.get(num_slots)
+        if sc is None:
+            S = int(num_slots)
+            col = self.col.long()
+            sc = SparseOperator.from_coo(self.row * S + col % S, col // S,
+                                         self.val, self.num_rows * S,
+                                         self.num_cols // S)
+            cache[num_slots] = sc
+        return sc
+
     def to_dense(self):
         out = torch.zeros(self.num_rows, self.num_cols, device=self.device)
         out.index_put_((self.row, self.col.long()), self.val, accumulate=True)
@@ -172,10 +188,21 @@ class _GemmSpMM(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w_lp, bias, op, relu, C, loop):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
-        y = (xc @ w_lp).view(-1, C)
-        out_dtype = y.dtype if y.dtype in (torch.bfloat16, torch.float16) \
-            else torch.float32
-        out = _spmm_raw(op, y, None, None, bias, relu, out_dtype)
+        K = xc.size(1)
+        S = w_lp.size(1) // C
+        if _fused_ok(xc, K, C):
+            # Fused gather + MFMA: Y = x @ W is never materialised.
+            sc = op.slot_csr(S)
+            wt = _slot_major_t(w_lp)                    # [S * C, K]
+            out = _backend.ops().gather_gemm(
+                xc.contiguous(), sc.rowptr, sc.col, sc.val, wt, C * K, K, S,
+                C, bias, relu, xc.dtype, None)
+        else:
+            y = (xc @ w_lp).view(-1, C)
+            out_dtype = y.dtype if y.dtype in (torch.bfloat16,
+                                               torch.float16) \
+                else torch.float32
+            out = _spmm_raw(op, y, None, None, bias, relu, out_dtype)
         ctx.save_for_backward(xc, w_lp, out if relu else None)
         ctx.op, ctx.relu, ctx.C, ctx.loop = op, relu, C, loop
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
@@ -209,23 +236,37 @@ class _GemmSpMM(torch.autograd.Function):
                 if loop is not None:
                     loop.add_to('b', db)
             g = g.to(w_lp.dtype)
-        # 2. dY = A^T g'.
+        # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
         opt = ctx.op.t()
+        K = xc.size(1)
+        S = w_lp.size(1) // C
+        fused = ctx.needs_input_grad[0] and _fused_ok(g, C, K)
         if loop is not None:
             dy = loop.slot('dy', idx, (opt.num_rows, C), w_lp.dtype, dev)
-            if hip:
-                _backend.ops().spmm_csr_out(opt.rowptr, opt.col, opt.val, g,
-                                            None, None, None, False, dy)
-            else:
-                dy.copy_(_spmm_raw(opt, g, None, None, None, False,
-                                   w_lp.dtype))
             loop.slot('x', idx, xc.shape, xc.dtype, dev).copy_(xc)
+        elif fused:
+            dy = torch.empty((opt.num_rows, C), dtype=w_lp.dtype, device=dev)
+        else:
+            dy = None
+        gx = gw = gb = None
+        if fused:
+            # Gather over A^T (rows j*S + k) writes dY and contracts it with
+            # W_k^T read in place from w_lp [K, S*C] in one kernel.
+            gx = _backend.ops().gather_gemm(
+                g, opt.rowptr, opt.col, opt.val, _contig(w_lp), C, S * C, S,
+                K, None, False, g.dtype, dy)
+            if gx.dtype != ctx.x_dtype:
+                gx = gx.to(ctx.x_dtype)
+        elif dy is not None and hip:
+            _backend.ops().spmm_csr_out(opt.rowptr, opt.col, opt.val, g,
+                                        None, None, None, False, dy)
+        elif dy is not None:
+            dy.copy_(_spmm_raw(opt, g, None, None, None, False, w_lp.dtype))
         else:
             dy = _spmm_raw(opt, g, None, None, None, False, w_lp.dtype)
         dY = dy.view(xc.size(0), -1)
-        # 3. dx and dW.
-        gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
+        # 3. dx (unfused path) and dW.
+        if ctx.needs_input_grad[0] and gx is None:
             gx = (dY @ w_lp.t()).to(ctx.x_dtype)
         if loop is None:
             if ctx.needs_input_grad[1]:
@@ -242,6 +283,27 @@ class _GemmSpMM(torch.autograd.Function):
                 gb = loop.get_acc('b').to(ctx.bias_dtype)
             loop.release()
         return gx, gw, None, gb, None, None, None, None
+
+
+_FUSED_WIDTHS = (32, 64, 128, 256)
+
+
+def _fused_ok(x, K, M):
+    """Shapes/dtypes served by the fused gather-MFMA kernel."""
+    return (_backend.use_hip(x) and x.dtype == torch.bfloat16
+            and K in _FUSED_WIDTHS and M % 32 == 0)
+
+
+def _contig(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _slot_major_t(w_lp):
+    """``w_lp [K, S*C]`` -> ``[S*C, K]`` (B operand of the fused forward),
+    memoised per forward scope (``w_lp`` itself is cached there)."""
+    from ..runtime.cache import cached
+    return cached(('slot_major_t', id(w_lp)),
+                  lambda: (w_lp, w_lp.t().contiguous()))[1]
 
 
 def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,

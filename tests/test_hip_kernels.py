@@ -405,3 +405,45 @@ def test_split_k_accumulate():
     buf = torch.ones(128, 384, device=DEV)
     matmul_tn_fp32(a, b, out=buf, accumulate=True)
     assert torch.allclose(buf, ref_ + 1, atol=0.05, rtol=1e-3)
+
+
+def _slot_op(N, S, E, device):
+    """Random slot-structured operator [N, N*S] (SplineConv-like)."""
+    row = torch.randint(N, (E, ), device=device)
+    j = torch.randint(N, (E, ), device=device)
+    k = torch.randint(S - 1, (E, ), device=device)
+    val = torch.rand(E, device=device)
+    ar = torch.arange(N, device=device)
+    row = torch.cat([row, ar])
+    col = torch.cat([j * S + k, ar * S + (S - 1)])
+    val = torch.cat([val, torch.ones(N, device=device)])
+    return SparseOperator.from_coo(row, col, val, N, N * S)
+
+
+@pytest.mark.parametrize('K,C,S', [(128, 128, 26), (32, 32, 3), (64, 96, 5),
+                                   (256, 64, 26), (128, 256, 4)])
+def test_gather_gemm_fused_forward_backward(K, C, S):
+    from deep_graph_matching_consensus_amd.ops.sparse import gemm_spmm
+    N = 300
+    op = _slot_op(N, S, 2000, DEV)
+    x = torch.randn(N, K, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(K, S * C, device=DEV) / K ** 0.5).requires_grad_()
+    bias = torch.randn(C, device=DEV, requires_grad=True)
+    w_lp = w.detach().bfloat16()
+    out = gemm_spmm(op, x, w, w_lp, C, bias=bias, relu=True)
+    # fp32 oracle on the same bf16-rounded operands.
+    xf = x.detach().float().requires_grad_()
+    wf = w_lp.float().requires_grad_()
+    bf = bias.detach().clone().requires_grad_()
+    y = (xf @ wf).view(-1, C)
+    ref_out = torch.relu(op.to_dense() @ y + bf)
+    assert out.dtype == torch.bfloat16
+    assert torch.allclose(out.float(), ref_out, atol=3e-2, rtol=3e-2)
+    g = torch.randn(N, C, device=DEV)
+    gx, gw, gb = torch.autograd.grad(out, (x, w, bias), g.bfloat16())
+    rx, rw, rb = torch.autograd.grad(ref_out, (xf, wf, bf), g)
+    def close(a, b, tol):
+        return (a.float() - b).abs().max() <= tol * b.abs().max() + 1e-3
+    assert close(gx, rx, 3e-2)
+    assert close(gw, rw, 3e-2)
+    assert close(gb, rb, 1e-2)
