@@ -11,14 +11,16 @@
 // skinny-GEMM kernels and the SpMM (45 us per layer).  Here Z never leaves
 // the CU:
 //
-// * block = 64 destination rows x 64 output columns, 4 waves (2 x 2 tiles of
-//   32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in registers);
+// * block = 64 destination rows x 64 output columns; 4 MFMA waves (2 x 2
+//   tiles of 32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in
+//   registers) and 4 gather waves;
 // * the block's slot-CSR metadata (row pointers, source ids, coefficients)
-//   is staged in LDS once;
-// * per slot: the Z_k tile is gathered (16-byte bf16 loads of L2-resident X
-//   rows, fp32 FMA, one bf16 rounding) into one of two LDS buffers while the
-//   other buffer feeds the MFMAs - one barrier per slot; the W_k fragments of
-//   slot k+1 are loaded from L2 into registers during slot k;
+//   and, when the sources are local, the window of X rows they touch are
+//   staged in LDS once;
+// * per slot: the gather waves build the Z_k tile (16-byte bf16 reads, fp32
+//   FMA, one bf16 rounding) in one LDS buffer while the MFMA waves consume
+//   the other - one barrier per slot; the W_k fragments of slot k+1 are
+//   loaded from L2 into registers during slot k;
 // * epilogue: + bias, ReLU, store (bf16/fp32).
 //
 // The backward of the same layer is the same kernel on the transposed
@@ -27,6 +29,8 @@
 // GEMM (runtime/loopgrad.py stacks them across consensus steps).
 #include "common.h"
 
+#include <climits>
+
 namespace dgmc {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -34,7 +38,9 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 constexpr int kGG_BM = 64;
 constexpr int kGG_BN = 64;
-constexpr int kGG_ECAP = 4096;  // staged (col, val) entries per block
+constexpr int kGG_ECAP = 4096;          // staged (col, val) entries per block
+constexpr int kGG_LDS = 160 * 1024;     // gfx950 LDS per CU
+constexpr int kGG_THREADS = 512;        // 4 MFMA waves + 4 gather waves
 
 __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
   bf16x8_t r;
@@ -43,13 +49,25 @@ __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
   return r;
 }
 
+__device__ __forceinline__ void bf16x8_to_f32(const bf16x8_t& v, float* o) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) o[c] = (float)v[c];
+}
+
+// Warp-specialised: waves 0-3 run the MFMAs of slot k while waves 4-7 gather
+// slot k+1 into the other LDS buffer (one barrier per slot).  When the
+// block's source rows span a small window (graphs batched as disjoint unions
+// keep their edges local), the window of X is staged in LDS once and every
+// gather is an LDS read; otherwise gathers read L2 with all of a thread's
+// rows in flight together.
 template <int K, bool WRITE_Z, typename TOUT>
-__global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
+__global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
     const __hip_bfloat16* __restrict__ X, const int* __restrict__ srp,
     const int* __restrict__ ecol, const float* __restrict__ eval,
     const __hip_bfloat16* __restrict__ Wb, int64_t ss, int64_t sn,
     const float* __restrict__ bias, int relu, TOUT* __restrict__ out,
-    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M) {
+    __hip_bfloat16* __restrict__ Z, int Ndst, int Nsrc, int S, int M,
+    int wcap) {
   constexpr int BM = kGG_BM, BN = kGG_BN;
   constexpr int KP = K + 8;          // padded LDS row (bf16 elements)
   constexpr int LPR = K / 8;         // gather lanes per row (16 B each)
@@ -60,10 +78,12 @@ __global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* zbuf = reinterpret_cast<__bf16*>(smem);              // [2][BM][KP]
-  int* srp_l = reinterpret_cast<int*>(zbuf + 2 * BM * KP);     // [BM*S+1]
+  __bf16* xwin = zbuf + 2 * BM * KP;                           // [wcap][KP]
+  int* srp_l = reinterpret_cast<int*>(xwin + (size_t)wcap * KP);
   const int srp_n = BM * S + 1;
   int* ecol_l = srp_l + ((srp_n + 3) & ~3);                     // [ECAP]
   float* eval_l = reinterpret_cast<float*>(ecol_l + kGG_ECAP);  // [ECAP]
+  __shared__ int s_lo, s_hi;
 
   const int tid = threadIdx.x;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -71,35 +91,81 @@ __global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
   const int n0 = blockIdx.y * BN;
   const int rows = min(BM, Ndst - i0);
 
-  // ---- stage the block's slot-CSR metadata ------------------------------
+  // ---- stage the block's slot-CSR metadata (+ source window) -----------
   const int nsrp = rows * S + 1;
-  for (int t = tid; t < nsrp; t += 256) srp_l[t] = srp[(size_t)i0 * S + t];
+  for (int t = tid; t < nsrp; t += kGG_THREADS)
+    srp_l[t] = srp[(size_t)i0 * S + t];
+  if (tid == 0) {
+    s_lo = INT_MAX;
+    s_hi = -1;
+  }
   __syncthreads();
   const int ebase = srp_l[0];
   const int ecount = srp_l[rows * S] - ebase;
   const bool staged = ecount <= kGG_ECAP;
   if (staged) {
-    for (int t = tid; t < ecount; t += 256) {
-      ecol_l[t] = ecol[ebase + t];
+    int lo = INT_MAX, hi = -1;
+    for (int t = tid; t < ecount; t += kGG_THREADS) {
+      const int j = ecol[ebase + t];
+      ecol_l[t] = j;
       eval_l[t] = eval[ebase + t];
+      lo = min(lo, j);
+      hi = max(hi, j);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o));
+      hi = max(hi, __shfl_xor(hi, o));
+    }
+    if ((tid & 63) == 0 && hi >= 0) {
+      atomicMin(&s_lo, lo);
+      atomicMax(&s_hi, hi);
+    }
+  }
+  __syncthreads();
+  const int wlo = s_lo;
+  const bool windowed = staged && s_hi >= 0 && s_hi - wlo + 1 <= wcap;
+  if (windowed) {
+    const int wrows = s_hi - wlo + 1;
+    for (int t = tid; t < wrows * LPR; t += kGG_THREADS) {
+      const int r = t / LPR, c = t % LPR;
+      *reinterpret_cast<uint4*>(xwin + r * KP + c * 8) =
+          *reinterpret_cast<const uint4*>(X + (size_t)(wlo + r) * K + c * 8);
     }
   }
   __syncthreads();
 
-  // ---- gather Z_k for the block into LDS buffer `buf` -------------------
-  const int q = tid % LPR, rg = tid / LPR;
+  const int wave = tid / 64, lane = tid % 64;
+  const bool mfma_role = wave < 4;
+
+  // ---- gather Z_k for the block into LDS buffer `buf` (gather waves) ----
+  const int gt = tid - 256;
+  const int q = gt % LPR, rg = gt / LPR;
   auto gather = [&](int k, int buf) {
     __bf16* zb = zbuf + buf * BM * KP;
+    int eb[PASSES], cnt[PASSES];
+    int mx = 0;
 #pragma unroll
     for (int p = 0; p < PASSES; ++p) {
       const int r = p * RPP + rg;
-      float acc[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+      eb[p] = 0;
+      cnt[p] = 0;
       if (r < rows) {
-        const int e0 = srp_l[r * S + k] - ebase;
-        const int e1 = srp_l[r * S + k + 1] - ebase;
-        for (int e = e0; e < e1; ++e) {
+        eb[p] = srp_l[r * S + k] - ebase;
+        cnt[p] = srp_l[r * S + k + 1] - ebase - eb[p];
+      }
+      mx = max(mx, cnt[p]);
+    }
+    float acc[PASSES][8];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[p][c] = 0.f;
+    for (int t = 0; t < mx; ++t) {
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p) {
+        if (t < cnt[p]) {
+          const int e = eb[p] + t;
           int j;
           float a;
           if (staged) {
@@ -110,12 +176,21 @@ __global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
             a = eval[ebase + e];
           }
           float xv[8];
-          load_vec<__hip_bfloat16, 8>(X + (size_t)j * K + q * 8, xv);
+          if (windowed)
+            bf16x8_to_f32(*reinterpret_cast<const bf16x8_t*>(
+                              xwin + (j - wlo) * KP + q * 8),
+                          xv);
+          else
+            load_vec<__hip_bfloat16, 8>(X + (size_t)j * K + q * 8, xv);
 #pragma unroll
-          for (int c = 0; c < 8; ++c) acc[c] = fmaf(a, xv[c], acc[c]);
+          for (int c = 0; c < 8; ++c) acc[p][c] = fmaf(a, xv[c], acc[p][c]);
         }
       }
-      const bf16x8_t v = pack_bf16x8(acc);
+    }
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const int r = p * RPP + rg;
+      const bf16x8_t v = pack_bf16x8(acc[p]);
       *reinterpret_cast<bf16x8_t*>(zb + r * KP + q * 8) = v;
       if constexpr (WRITE_Z) {
         if (blockIdx.y == 0 && r < rows)
@@ -126,26 +201,25 @@ __global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
     }
   };
 
-  // ---- MFMA tiles --------------------------------------------------------
-  const int wave = tid / 64, lane = tid % 64;
-  const int wr = wave >> 1, wc = wave & 1;
+  // ---- MFMA tiles (MFMA waves) -------------------------------------------
+  const int wr = (wave >> 1) & 1, wc = wave & 1;
   const int lr = lane & 31, lh = lane >> 5;
   const int col = n0 + wc * 32 + lr;
-  const bool wave_active = n0 + wc * 32 < M;   // wave-uniform
+  const bool wave_active = mfma_role && n0 + wc * 32 < M;  // wave-uniform
   const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
   bf16x8_t bcur[KS], bnext[KS];
   auto load_b = [&](int k, bf16x8_t* b) {
     const __bf16* base = W + (size_t)k * ss + (size_t)col * sn + 8 * lh;
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-      b[s] = *reinterpret_cast<const bf16x8_t*>(base + 16 * s);
+    for (int s2 = 0; s2 < KS; ++s2)
+      b[s2] = *reinterpret_cast<const bf16x8_t*>(base + 16 * s2);
   };
   f32x16_t acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
   if (wave_active) load_b(0, bcur);
-  gather(0, 0);
+  if (!mfma_role) gather(0, 0);
   __syncthreads();
   for (int k = 0; k < S; ++k) {
     const int buf = k & 1;
@@ -153,18 +227,17 @@ __global__ __launch_bounds__(256, 2) void gather_gemm_kernel(
       if (k + 1 < S) load_b(k + 1, bnext);
       const __bf16* za = zbuf + buf * BM * KP + (wr * 32 + lr) * KP + 8 * lh;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(za + 16 * s);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bcur[s], acc, 0, 0,
+      for (int s2 = 0; s2 < KS; ++s2) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(za + 16 * s2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bcur[s2], acc, 0, 0,
                                                        0);
       }
-    }
-    if (k + 1 < S) gather(k + 1, buf ^ 1);
-    __syncthreads();
-    if (wave_active) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) bcur[s] = bnext[s];
+      for (int s2 = 0; s2 < KS; ++s2) bcur[s2] = bnext[s2];
+    } else if (!mfma_role && k + 1 < S) {
+      gather(k + 1, buf ^ 1);
     }
+    __syncthreads();
   }
 
   // ---- epilogue ----------------------------------------------------------
@@ -187,27 +260,32 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                       const at::Tensor& W, int64_t ss, int64_t sn,
                       const float* bias, bool relu, at::Tensor& out,
                       __hip_bfloat16* Z, int Ndst, int S, int M) {
+  const size_t row_bytes = (size_t)(K + 8) * 2;
   const size_t srp_n = (size_t)kGG_BM * S + 1;
-  const size_t lds = (size_t)2 * kGG_BM * (K + 8) * 2 +
-                     ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8;
-  TORCH_CHECK(lds <= 160 * 1024, "gather_gemm: LDS budget exceeded (S=", S,
-              ")");
+  const size_t fixed = (size_t)2 * kGG_BM * row_bytes +
+                       ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8 +
+                       64;
+  TORCH_CHECK(fixed <= (size_t)kGG_LDS, "gather_gemm: LDS budget exceeded (S=",
+              S, ")");
+  const int wcap = (int)std::min<size_t>((kGG_LDS - fixed) / row_bytes, 1024);
+  const size_t lds = fixed - 64 + (size_t)wcap * row_bytes;
   auto kern = gather_gemm_kernel<K, WRITE_Z, TOUT>;
   static bool attr_set = false;
   if (!attr_set) {
     DGMC_CHECK_HIP(hipFuncSetAttribute(
         reinterpret_cast<const void*>(kern),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        hipFuncAttributeMaxDynamicSharedMemorySize, kGG_LDS - 64));
     attr_set = true;
   }
   dim3 grid((Ndst + kGG_BM - 1) / kGG_BM, (M + kGG_BN - 1) / kGG_BN);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream(),
+  hipLaunchKernelGGL(kern, grid, dim3(kGG_THREADS), lds, stream(),
                      reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
                      srp.data_ptr<int>(), ecol.data_ptr<int>(),
                      eval.data_ptr<float>(),
                      reinterpret_cast<const __hip_bfloat16*>(W.data_ptr()), ss,
                      sn, bias, relu ? 1 : 0,
-                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst, S, M);
+                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst,
+                     (int)X.size(0), S, M, wcap);
 }
 
 template <int K>

@@ -436,12 +436,15 @@ def test_gather_gemm_fused_forward_backward(K, C, S):
     wf = w_lp.float().requires_grad_()
     bf = bias.detach().clone().requires_grad_()
     y = (xf @ wf).view(-1, C)
-    ref_out = torch.relu(op.to_dense() @ y + bf)
+    ref_pre = op.to_dense() @ y + bf
     assert out.dtype == torch.bfloat16
-    assert torch.allclose(out.float(), ref_out, atol=3e-2, rtol=3e-2)
-    g = torch.randn(N, C, device=DEV)
+    assert torch.allclose(out.float(), ref_pre.relu(), atol=3e-2, rtol=3e-2)
+    g = torch.randn(N, C, device=DEV).bfloat16().float()
     gx, gw, gb = torch.autograd.grad(out, (x, w, bias), g.bfloat16())
-    rx, rw, rb = torch.autograd.grad(ref_out, (xf, wf, bf), g)
+    # Reference backward through the kernel's own ReLU mask (outputs within
+    # bf16 rounding of 0 may legitimately flip).
+    mask = (out.detach().float() > 0).float()
+    rx, rw, rb = torch.autograd.grad(ref_pre, (xf, wf, bf), g * mask)
     def close(a, b, tol):
         return (a.float() - b).abs().max() <= tol * b.abs().max() + 1e-3
     assert close(gx, rx, 3e-2)
