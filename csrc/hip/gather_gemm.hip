@@ -11,16 +11,16 @@
 // skinny-GEMM kernels and the SpMM (45 us per layer).  Here Z never leaves
 // the CU:
 //
-// * block = 64 destination rows x 64 output columns; 4 MFMA waves (2 x 2
-//   tiles of 32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in
-//   registers) and 4 gather waves;
+// * block = 32 destination rows x 128 output columns; 4 MFMA waves (tiles
+//   of 32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in registers)
+//   and 4 gather waves; ~52 KB of LDS -> 3 blocks (24 waves) per CU;
 // * the block's slot-CSR metadata (row pointers, source ids, coefficients)
 //   and, when the sources are local, the window of X rows they touch are
 //   staged in LDS once;
 // * per slot: the gather waves build the Z_k tile (16-byte bf16 reads, fp32
 //   FMA, one bf16 rounding) in one LDS buffer while the MFMA waves consume
 //   the other - one barrier per slot; the W_k fragments of slot k+1 are
-//   loaded from L2 into registers during slot k;
+//   loaded from L2 into registers two slots ahead;
 // * epilogue: + bias, ReLU, store (bf16/fp32).
 //
 // The backward of the same layer is the same kernel on the transposed
@@ -36,10 +36,13 @@ namespace dgmc {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
-constexpr int kGG_BM = 64;
-constexpr int kGG_BN = 64;
-constexpr int kGG_ECAP = 4096;          // staged (col, val) entries per block
-constexpr int kGG_LDS = 160 * 1024;     // gfx950 LDS per CU
+#define DGMC_LDS __attribute__((address_space(3)))
+
+constexpr int kGG_BM = 32;              // destination rows per block
+constexpr int kGG_BN = 128;             // output columns per block
+constexpr int kGG_ECAP = 2048;          // staged (col, val) entries per block
+constexpr int kGG_LDS_TARGET = 52 * 1024;  // => 3 blocks (24 waves) per CU
+constexpr int kGG_LDS_MAX = 160 * 1024;
 constexpr int kGG_THREADS = 512;        // 4 MFMA waves + 4 gather waves
 
 __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
@@ -49,41 +52,131 @@ __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
   return r;
 }
 
-__device__ __forceinline__ void bf16x8_to_f32(const bf16x8_t& v, float* o) {
+// Block-shared state, all in the dynamic LDS region carved at 16-byte
+// multiples (a static __shared__ in front of it would misalign every
+// ds_*_b128 access) and typed address_space(3) so every access is a ds_*
+// instruction (generic pointers would become flat_* loads that wait on
+// vmcnt and lgkmcnt together).
+struct GGShared {
+  DGMC_LDS int* minmax;     // [2]
+  DGMC_LDS __bf16* zbuf;    // [2][BM][KP]
+  DGMC_LDS __bf16* xwin;    // [wcap][KP]
+  DGMC_LDS int* srp;        // [BM*S + 1]
+  DGMC_LDS int* ecol;       // [ECAP]
+  DGMC_LDS float* eval;     // [ECAP]
+};
+
+// Gather Z_k of the block's rows into `zb` (gather waves, 256 threads).
+// Branch-free in the entry loop: every row slot of a thread issues its load
+// each iteration (exhausted slots read a valid dummy with weight 0), so all
+// of a thread's loads are in flight together.
+template <int K, bool STAGED, bool WINDOWED, bool WRITE_Z>
+__device__ __forceinline__ void gg_gather(
+    const GGShared& sh, DGMC_LDS __bf16* zb, int k, int S, int rows,
+    int ebase, int wlo, const __hip_bfloat16* __restrict__ X,
+    const int* __restrict__ ecol, const float* __restrict__ eval,
+    __hip_bfloat16* __restrict__ Z, int i0, bool write_z, int gt) {
+  constexpr int BM = kGG_BM;
+  constexpr int KP = K + 8;
+  constexpr int LPR = K / 8;
+  constexpr int RPP = 256 / LPR;
+  constexpr int PASSES = BM >= RPP ? BM / RPP : 1;
+  const int q = gt % LPR, rg = gt / LPR;
+  int eb[PASSES], cnt[PASSES];
+  int mx = 0;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) o[c] = (float)v[c];
+  for (int p = 0; p < PASSES; ++p) {
+    const int r = p * RPP + rg;
+    eb[p] = 0;
+    cnt[p] = 0;
+    if (r < rows) {
+      eb[p] = sh.srp[r * S + k] - ebase;
+      cnt[p] = sh.srp[r * S + k + 1] - ebase - eb[p];
+    }
+    mx = max(mx, cnt[p]);
+  }
+  float acc[PASSES][8];
+#pragma unroll
+  for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[p][c] = 0.f;
+  for (int t = 0; t < mx; ++t) {
+    int j[PASSES];
+    float a[PASSES];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      const bool v = t < cnt[p];
+      const int e = v ? eb[p] + t : 0;
+      if constexpr (STAGED) {
+        j[p] = sh.ecol[e];
+        a[p] = sh.eval[e];
+      } else {
+        j[p] = ecol[ebase + e];
+        a[p] = eval[ebase + e];
+      }
+      if (!v) a[p] = 0.f;
+    }
+    bf16x8_t xv[PASSES];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      if constexpr (WINDOWED)
+        xv[p] = *reinterpret_cast<DGMC_LDS const bf16x8_t*>(
+            sh.xwin + (j[p] - wlo) * KP + q * 8);
+      else
+        xv[p] = *reinterpret_cast<const bf16x8_t*>(
+            reinterpret_cast<const __bf16*>(X) + (size_t)j[p] * K + q * 8);
+    }
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        acc[p][c] = fmaf(a[p], (float)xv[p][c], acc[p][c]);
+  }
+#pragma unroll
+  for (int p = 0; p < PASSES; ++p) {
+    const int r = p * RPP + rg;
+    if (r < BM) {
+      const bf16x8_t v = pack_bf16x8(acc[p]);
+      *reinterpret_cast<DGMC_LDS bf16x8_t*>(zb + r * KP + q * 8) = v;
+      if constexpr (WRITE_Z) {
+        if (write_z && r < rows)
+          *reinterpret_cast<bf16x8_t*>(reinterpret_cast<__bf16*>(Z) +
+                                       ((size_t)(i0 + r) * S + k) * K +
+                                       q * 8) = v;
+      }
+    }
+  }
 }
 
 // Warp-specialised: waves 0-3 run the MFMAs of slot k while waves 4-7 gather
 // slot k+1 into the other LDS buffer (one barrier per slot).  When the
 // block's source rows span a small window (graphs batched as disjoint unions
-// keep their edges local), the window of X is staged in LDS once and every
-// gather is an LDS read; otherwise gathers read L2 with all of a thread's
-// rows in flight together.
+// keep their edges local), that window of X is staged in LDS once and every
+// gather is an LDS read; otherwise gathers read L2.  W_k fragments are
+// prefetched two slots ahead into registers.
 template <int K, bool WRITE_Z, typename TOUT>
-__global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
+__global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
     const __hip_bfloat16* __restrict__ X, const int* __restrict__ srp,
     const int* __restrict__ ecol, const float* __restrict__ eval,
     const __hip_bfloat16* __restrict__ Wb, int64_t ss, int64_t sn,
     const float* __restrict__ bias, int relu, TOUT* __restrict__ out,
-    __hip_bfloat16* __restrict__ Z, int Ndst, int Nsrc, int S, int M,
-    int wcap) {
+    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M, int wcap,
+    int dbg) {
   constexpr int BM = kGG_BM, BN = kGG_BN;
   constexpr int KP = K + 8;          // padded LDS row (bf16 elements)
-  constexpr int LPR = K / 8;         // gather lanes per row (16 B each)
-  constexpr int RPP = 256 / LPR;     // rows per gather pass
-  constexpr int PASSES = BM / RPP;
+  constexpr int LPR = K / 8;
   constexpr int KS = K / 16;         // MFMA k-steps per slot
-  static_assert(BM % RPP == 0, "gather mapping");
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __bf16* zbuf = reinterpret_cast<__bf16*>(smem);              // [2][BM][KP]
-  __bf16* xwin = zbuf + 2 * BM * KP;                           // [wcap][KP]
-  int* srp_l = reinterpret_cast<int*>(xwin + (size_t)wcap * KP);
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS char* smem = (DGMC_LDS char*)smem_raw;
+  GGShared sh;
+  sh.minmax = (DGMC_LDS int*)smem;
+  sh.zbuf = (DGMC_LDS __bf16*)(smem + 16);
+  sh.xwin = sh.zbuf + 2 * BM * KP;
+  sh.srp = (DGMC_LDS int*)(sh.xwin + (size_t)wcap * KP);
   const int srp_n = BM * S + 1;
-  int* ecol_l = srp_l + ((srp_n + 3) & ~3);                     // [ECAP]
-  float* eval_l = reinterpret_cast<float*>(ecol_l + kGG_ECAP);  // [ECAP]
-  __shared__ int s_lo, s_hi;
+  sh.ecol = sh.srp + ((srp_n + 3) & ~3);
+  sh.eval = (DGMC_LDS float*)(sh.ecol + kGG_ECAP);
 
   const int tid = threadIdx.x;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -94,21 +187,21 @@ __global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
   // ---- stage the block's slot-CSR metadata (+ source window) -----------
   const int nsrp = rows * S + 1;
   for (int t = tid; t < nsrp; t += kGG_THREADS)
-    srp_l[t] = srp[(size_t)i0 * S + t];
+    sh.srp[t] = srp[(size_t)i0 * S + t];
   if (tid == 0) {
-    s_lo = INT_MAX;
-    s_hi = -1;
+    sh.minmax[0] = INT_MAX;
+    sh.minmax[1] = -1;
   }
   __syncthreads();
-  const int ebase = srp_l[0];
-  const int ecount = srp_l[rows * S] - ebase;
+  const int ebase = sh.srp[0];
+  const int ecount = sh.srp[rows * S] - ebase;
   const bool staged = ecount <= kGG_ECAP;
   if (staged) {
     int lo = INT_MAX, hi = -1;
     for (int t = tid; t < ecount; t += kGG_THREADS) {
       const int j = ecol[ebase + t];
-      ecol_l[t] = j;
-      eval_l[t] = eval[ebase + t];
+      sh.ecol[t] = j;
+      sh.eval[t] = eval[ebase + t];
       lo = min(lo, j);
       hi = max(hi, j);
     }
@@ -118,96 +211,49 @@ __global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
       hi = max(hi, __shfl_xor(hi, o));
     }
     if ((tid & 63) == 0 && hi >= 0) {
-      atomicMin(&s_lo, lo);
-      atomicMax(&s_hi, hi);
+      atomicMin((int*)&sh.minmax[0], lo);
+      atomicMax((int*)&sh.minmax[1], hi);
     }
   }
   __syncthreads();
-  const int wlo = s_lo;
-  const bool windowed = staged && s_hi >= 0 && s_hi - wlo + 1 <= wcap;
+  const int wlo = sh.minmax[0];
+  const int whi = sh.minmax[1];
+  const bool windowed = staged && whi >= 0 && whi - wlo + 1 <= wcap;
   if (windowed) {
-    const int wrows = s_hi - wlo + 1;
+    const int wrows = whi - wlo + 1;
     for (int t = tid; t < wrows * LPR; t += kGG_THREADS) {
       const int r = t / LPR, c = t % LPR;
-      *reinterpret_cast<uint4*>(xwin + r * KP + c * 8) =
-          *reinterpret_cast<const uint4*>(X + (size_t)(wlo + r) * K + c * 8);
+      *reinterpret_cast<DGMC_LDS bf16x8_t*>(sh.xwin + r * KP + c * 8) =
+          *reinterpret_cast<const bf16x8_t*>(
+              reinterpret_cast<const __bf16*>(X) + (size_t)(wlo + r) * K +
+              c * 8);
     }
   }
   __syncthreads();
 
   const int wave = tid / 64, lane = tid % 64;
   const bool mfma_role = wave < 4;
-
-  // ---- gather Z_k for the block into LDS buffer `buf` (gather waves) ----
+  const bool write_z = blockIdx.y == 0;
   const int gt = tid - 256;
-  const int q = gt % LPR, rg = gt / LPR;
   auto gather = [&](int k, int buf) {
-    __bf16* zb = zbuf + buf * BM * KP;
-    int eb[PASSES], cnt[PASSES];
-    int mx = 0;
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int r = p * RPP + rg;
-      eb[p] = 0;
-      cnt[p] = 0;
-      if (r < rows) {
-        eb[p] = srp_l[r * S + k] - ebase;
-        cnt[p] = srp_l[r * S + k + 1] - ebase - eb[p];
-      }
-      mx = max(mx, cnt[p]);
-    }
-    float acc[PASSES][8];
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p)
-#pragma unroll
-      for (int c = 0; c < 8; ++c) acc[p][c] = 0.f;
-    for (int t = 0; t < mx; ++t) {
-#pragma unroll
-      for (int p = 0; p < PASSES; ++p) {
-        if (t < cnt[p]) {
-          const int e = eb[p] + t;
-          int j;
-          float a;
-          if (staged) {
-            j = ecol_l[e];
-            a = eval_l[e];
-          } else {
-            j = ecol[ebase + e];
-            a = eval[ebase + e];
-          }
-          float xv[8];
-          if (windowed)
-            bf16x8_to_f32(*reinterpret_cast<const bf16x8_t*>(
-                              xwin + (j - wlo) * KP + q * 8),
-                          xv);
-          else
-            load_vec<__hip_bfloat16, 8>(X + (size_t)j * K + q * 8, xv);
-#pragma unroll
-          for (int c = 0; c < 8; ++c) acc[p][c] = fmaf(a, xv[c], acc[p][c]);
-        }
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      const int r = p * RPP + rg;
-      const bf16x8_t v = pack_bf16x8(acc[p]);
-      *reinterpret_cast<bf16x8_t*>(zb + r * KP + q * 8) = v;
-      if constexpr (WRITE_Z) {
-        if (blockIdx.y == 0 && r < rows)
-          *reinterpret_cast<bf16x8_t*>(
-              reinterpret_cast<__bf16*>(Z) +
-              ((size_t)(i0 + r) * S + k) * K + q * 8) = v;
-      }
-    }
+    DGMC_LDS __bf16* zb = sh.zbuf + buf * BM * KP;
+    if (windowed)
+      gg_gather<K, true, true, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
+                                        ecol, eval, Z, i0, write_z, gt);
+    else if (staged)
+      gg_gather<K, true, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
+                                         ecol, eval, Z, i0, write_z, gt);
+    else
+      gg_gather<K, false, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
+                                          ecol, eval, Z, i0, write_z, gt);
   };
 
-  // ---- MFMA tiles (MFMA waves) -------------------------------------------
-  const int wr = (wave >> 1) & 1, wc = wave & 1;
+  // ---- MFMA tiles (MFMA waves: 32 rows x 32 columns each) ----------------
   const int lr = lane & 31, lh = lane >> 5;
-  const int col = n0 + wc * 32 + lr;
-  const bool wave_active = mfma_role && n0 + wc * 32 < M;  // wave-uniform
+  const int col = n0 + wave * 32 + lr;
+  const bool wave_active = mfma_role && n0 + wave * 32 < M;  // wave-uniform
   const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
-  bf16x8_t bcur[KS], bnext[KS];
+  bf16x8_t b0[KS], b1[KS], b2[KS];
   auto load_b = [&](int k, bf16x8_t* b) {
     const __bf16* base = W + (size_t)k * ss + (size_t)col * sn + 8 * lh;
 #pragma unroll
@@ -218,23 +264,33 @@ __global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  if (wave_active) load_b(0, bcur);
+  // Prefetch depth 2 where registers allow (K <= 128), else 1.
+  constexpr bool PF2 = K <= 128;
+  if (wave_active) {
+    load_b(0, b0);
+    if (PF2 && S > 1) load_b(1, b1);
+  }
   if (!mfma_role) gather(0, 0);
   __syncthreads();
   for (int k = 0; k < S; ++k) {
     const int buf = k & 1;
-    if (wave_active) {
-      if (k + 1 < S) load_b(k + 1, bnext);
-      const __bf16* za = zbuf + buf * BM * KP + (wr * 32 + lr) * KP + 8 * lh;
+    if (wave_active && !(dbg & 2)) {
+      if (PF2 && k + 2 < S) load_b(k + 2, b2);
+      if (!PF2 && k + 1 < S) load_b(k + 1, b1);
+      DGMC_LDS const __bf16* za = sh.zbuf + buf * BM * KP + lr * KP + 8 * lh;
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(za + 16 * s2);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bcur[s2], acc, 0, 0,
+        const bf16x8_t a =
+            *reinterpret_cast<DGMC_LDS const bf16x8_t*>(za + 16 * s2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0[s2], acc, 0, 0,
                                                        0);
       }
 #pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) bcur[s2] = bnext[s2];
-    } else if (!mfma_role && k + 1 < S) {
+      for (int s2 = 0; s2 < KS; ++s2) {
+        b0[s2] = b1[s2];
+        if (PF2) b1[s2] = b2[s2];
+      }
+    } else if (!mfma_role && k + 1 < S && !(dbg & 1)) {
       gather(k + 1, buf ^ 1);
     }
     __syncthreads();
@@ -245,13 +301,21 @@ __global__ __launch_bounds__(kGG_THREADS, 1) void gather_gemm_kernel(
   const float b = bias ? bias[col] : 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int row = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
     if (row < rows) {
       float v = acc[r] + b;
       if (relu) v = fmaxf(v, 0.f);
       out[(size_t)(i0 + row) * M + col] = Cvt<TOUT>::from_f(v);
     }
   }
+}
+
+static int gg_debug() {
+  static int v = [] {
+    const char* e = getenv("DGMC_GG_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int K, bool WRITE_Z, typename TOUT>
@@ -262,19 +326,23 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                       __hip_bfloat16* Z, int Ndst, int S, int M) {
   const size_t row_bytes = (size_t)(K + 8) * 2;
   const size_t srp_n = (size_t)kGG_BM * S + 1;
-  const size_t fixed = (size_t)2 * kGG_BM * row_bytes +
-                       ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8 +
-                       64;
-  TORCH_CHECK(fixed <= (size_t)kGG_LDS, "gather_gemm: LDS budget exceeded (S=",
-              S, ")");
-  const int wcap = (int)std::min<size_t>((kGG_LDS - fixed) / row_bytes, 1024);
-  const size_t lds = fixed - 64 + (size_t)wcap * row_bytes;
+  const size_t fixed = 16 + (size_t)2 * kGG_BM * row_bytes +
+                       ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8;
+  TORCH_CHECK(fixed + 16 * row_bytes <= (size_t)kGG_LDS_MAX,
+              "gather_gemm: LDS budget exceeded (S=", S, ")");
+  // Source window: what fits next to the fixed part within the 3-blocks-per
+  // -CU target (at least 2 * BM rows; beyond that the block reads L2).
+  const size_t budget = std::max<size_t>(kGG_LDS_TARGET,
+                                         fixed + 2 * kGG_BM * row_bytes);
+  const int wcap = (int)std::min<size_t>(
+      (std::min<size_t>(budget, kGG_LDS_MAX) - fixed) / row_bytes, 1024);
+  const size_t lds = fixed + (size_t)wcap * row_bytes;
   auto kern = gather_gemm_kernel<K, WRITE_Z, TOUT>;
   static bool attr_set = false;
   if (!attr_set) {
     DGMC_CHECK_HIP(hipFuncSetAttribute(
         reinterpret_cast<const void*>(kern),
-        hipFuncAttributeMaxDynamicSharedMemorySize, kGG_LDS - 64));
+        hipFuncAttributeMaxDynamicSharedMemorySize, kGG_LDS_MAX));
     attr_set = true;
   }
   dim3 grid((Ndst + kGG_BM - 1) / kGG_BM, (M + kGG_BN - 1) / kGG_BN);
@@ -284,8 +352,8 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                      eval.data_ptr<float>(),
                      reinterpret_cast<const __hip_bfloat16*>(W.data_ptr()), ss,
                      sn, bias, relu ? 1 : 0,
-                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst,
-                     (int)X.size(0), S, M, wcap);
+                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst, S, M,
+                     wcap, gg_debug());
 }
 
 template <int K>
