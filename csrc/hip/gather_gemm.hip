@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
   const bool mfma_role = wave < 4;
   const bool write_z = blockIdx.y == 0;
   const int gt = tid - 256;
-  auto gather = [&](int k, int buf) {
+  auto gather = [&](int k, int buf) __attribute__((always_inline)) {
     DGMC_LDS __bf16* zb = sh.zbuf + buf * BM * KP;
     if (windowed)
       gg_gather<K, true, true, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
   const bool wave_active = mfma_role && n0 + wave * 32 < M;  // wave-uniform
   const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
   bf16x8_t b0[KS], b1[KS], b2[KS];
-  auto load_b = [&](int k, bf16x8_t* b) {
+  auto load_b = [&](int k, bf16x8_t* b) __attribute__((always_inline)) {
     const __bf16* base = W + (size_t)k * ss + (size_t)col * sn + 8 * lh;
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2)
@@ -264,36 +264,51 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  // Prefetch depth 2 where registers allow (K <= 128), else 1.
-  constexpr bool PF2 = K <= 128;
+  // W_k fragments are prefetched PF slots ahead (2 where registers allow,
+  // K <= 128, else 1) into a register ring that is rotated by unrolling the
+  // slot loop - no register copies, so a load is waited for only by the
+  // MFMAs that consume it, PF slots later.
+  constexpr int PF = K <= 128 ? 2 : 1;
+  auto mfma_slot = [&](int buf, const bf16x8_t* b)
+                       __attribute__((always_inline)) {
+    DGMC_LDS const __bf16* za = sh.zbuf + buf * BM * KP + lr * KP + 8 * lh;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      const bf16x8_t a =
+          *reinterpret_cast<DGMC_LDS const bf16x8_t*>(za + 16 * s2);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[s2], acc, 0, 0, 0);
+    }
+  };
+  // One slot: MFMA waves consume buffer k&1 with fragments `use` and
+  // prefetch slot k+PF into `into`; gather waves fill buffer (k+1)&1.
+  auto step = [&](int k, const bf16x8_t* use, bf16x8_t* into)
+                  __attribute__((always_inline)) {
+    if (wave_active && !(dbg & 2)) {
+      if (k + PF < S) load_b(k + PF, into);
+      mfma_slot(k & 1, use);
+    } else if (!mfma_role && k + 1 < S && !(dbg & 1)) {
+      gather(k + 1, (k + 1) & 1);
+    }
+    __syncthreads();
+  };
+
   if (wave_active) {
     load_b(0, b0);
-    if (PF2 && S > 1) load_b(1, b1);
+    if (PF == 2 && S > 1) load_b(1, b1);
   }
   if (!mfma_role) gather(0, 0);
   __syncthreads();
-  for (int k = 0; k < S; ++k) {
-    const int buf = k & 1;
-    if (wave_active && !(dbg & 2)) {
-      if (PF2 && k + 2 < S) load_b(k + 2, b2);
-      if (!PF2 && k + 1 < S) load_b(k + 1, b1);
-      DGMC_LDS const __bf16* za = sh.zbuf + buf * BM * KP + lr * KP + 8 * lh;
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) {
-        const bf16x8_t a =
-            *reinterpret_cast<DGMC_LDS const bf16x8_t*>(za + 16 * s2);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b0[s2], acc, 0, 0,
-                                                       0);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) {
-        b0[s2] = b1[s2];
-        if (PF2) b1[s2] = b2[s2];
-      }
-    } else if (!mfma_role && k + 1 < S && !(dbg & 1)) {
-      gather(k + 1, buf ^ 1);
+  if constexpr (PF == 2) {
+    for (int k = 0; k < S; k += 3) {
+      step(k, b0, b2);
+      if (k + 1 < S) step(k + 1, b1, b0);
+      if (k + 2 < S) step(k + 2, b2, b1);
     }
-    __syncthreads();
+  } else {
+    for (int k = 0; k < S; k += 2) {
+      step(k, b0, b1);
+      if (k + 1 < S) step(k + 1, b1, b0);
+    }
   }
 
   // ---- epilogue ----------------------------------------------------------
