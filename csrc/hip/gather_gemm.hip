@@ -11,16 +11,17 @@
 // skinny-GEMM kernels and the SpMM (45 us per layer).  Here Z never leaves
 // the CU:
 //
-// * block = 32 destination rows x 128 output columns; 4 MFMA waves (tiles
+// * block = 64 destination rows x 128 output columns; 8 MFMA waves (tiles
 //   of 32 x 32, v_mfma_f32_32x32x16_bf16, fp32 accumulators in registers)
-//   and 4 gather waves; ~52 KB of LDS -> 3 blocks (24 waves) per CU;
+//   and 4 gather waves;
 // * the block's slot-CSR metadata (row pointers, source ids, coefficients)
 //   and, when the sources are local, the window of X rows they touch are
 //   staged in LDS once;
 // * per slot: the gather waves build the Z_k tile (16-byte bf16 reads, fp32
 //   FMA, one bf16 rounding) in one LDS buffer while the MFMA waves consume
-//   the other - one barrier per slot; the W_k fragments of slot k+1 are
-//   loaded from L2 into registers two slots ahead;
+//   the other - one barrier per slot; W_k^T slices stream through LDS
+//   (coalesced loads two slots ahead).  W is re-read by every block, so
+//   rows per block (64) set the L2 traffic: 144 blocks x 852 KB for psi_2;
 // * epilogue: + bias, ReLU, store (bf16/fp32).
 //
 // The backward of the same layer is the same kernel on the transposed
@@ -38,12 +39,13 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 #define DGMC_LDS __attribute__((address_space(3)))
 
-constexpr int kGG_BM = 32;              // destination rows per block
+constexpr int kGG_BM = 64;              // destination rows per block
 constexpr int kGG_BN = 128;             // output columns per block
 constexpr int kGG_ECAP = 2048;          // staged (col, val) entries per block
-constexpr int kGG_LDS_TARGET = 52 * 1024;  // => 3 blocks (24 waves) per CU
 constexpr int kGG_LDS_MAX = 160 * 1024;
-constexpr int kGG_THREADS = 512;        // 4 MFMA waves + 4 gather waves
+constexpr int kGG_MFMA_WAVES = 8;       // 2 row halves x 4 column quarters
+constexpr int kGG_GATHER_THREADS = 256; // 4 gather waves
+constexpr int kGG_THREADS = kGG_MFMA_WAVES * 64 + kGG_GATHER_THREADS;
 
 __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
   bf16x8_t r;
@@ -55,31 +57,32 @@ __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
 // Block-shared state, all in the dynamic LDS region carved at 16-byte
 // multiples (a static __shared__ in front of it would misalign every
 // ds_*_b128 access) and typed address_space(3) so every access is a ds_*
-// instruction (generic pointers would become flat_* loads that wait on
-// vmcnt and lgkmcnt together).
+// instruction (generic pointers become flat_* loads that wait on vmcnt and
+// lgkmcnt together - measured 2x slower here).
 struct GGShared {
   DGMC_LDS int* minmax;     // [2]
-  DGMC_LDS __bf16* zbuf;    // [2][BM][KP]
-  DGMC_LDS __bf16* xwin;    // [wcap][KP]
+  DGMC_LDS __bf16* zbuf;    // [2][BM][KP]   gathered Z_k tiles
+  DGMC_LDS __bf16* bbuf;    // [2][BN][KP]   W_k^T slices (B operand)
+  DGMC_LDS __bf16* xwin;    // [wcap][KP]    source window of X
   DGMC_LDS int* srp;        // [BM*S + 1]
   DGMC_LDS int* ecol;       // [ECAP]
   DGMC_LDS float* eval;     // [ECAP]
 };
 
-// Gather Z_k of the block's rows into `zb` (gather waves, 256 threads).
-// Branch-free in the entry loop: every row slot of a thread issues its load
-// each iteration (exhausted slots read a valid dummy with weight 0), so all
-// of a thread's loads are in flight together.
+// Gather Z_k of the block's rows into `zb` (gather waves).  Branch-free in
+// the entry loop: every row slot of a thread issues its read each iteration
+// (exhausted slots read a valid dummy with weight 0), so all of a thread's
+// reads are in flight together.
 template <int K, bool STAGED, bool WINDOWED, bool WRITE_Z>
 __device__ __forceinline__ void gg_gather(
     const GGShared& sh, DGMC_LDS __bf16* zb, int k, int S, int rows,
     int ebase, int wlo, const __hip_bfloat16* __restrict__ X,
     const int* __restrict__ ecol, const float* __restrict__ eval,
-    __hip_bfloat16* __restrict__ Z, int i0, bool write_z, int gt) {
+    __hip_bfloat16* __restrict__ Z, int i0, int gt) {
   constexpr int BM = kGG_BM;
   constexpr int KP = K + 8;
   constexpr int LPR = K / 8;
-  constexpr int RPP = 256 / LPR;
+  constexpr int RPP = kGG_GATHER_THREADS / LPR;
   constexpr int PASSES = BM >= RPP ? BM / RPP : 1;
   const int q = gt % LPR, rg = gt / LPR;
   int eb[PASSES], cnt[PASSES];
@@ -139,7 +142,7 @@ __device__ __forceinline__ void gg_gather(
       const bf16x8_t v = pack_bf16x8(acc[p]);
       *reinterpret_cast<DGMC_LDS bf16x8_t*>(zb + r * KP + q * 8) = v;
       if constexpr (WRITE_Z) {
-        if (write_z && r < rows)
+        if (r < rows)
           *reinterpret_cast<bf16x8_t*>(reinterpret_cast<__bf16*>(Z) +
                                        ((size_t)(i0 + r) * S + k) * K +
                                        q * 8) = v;
@@ -148,31 +151,36 @@ __device__ __forceinline__ void gg_gather(
   }
 }
 
-// Warp-specialised: waves 0-3 run the MFMAs of slot k while waves 4-7 gather
-// slot k+1 into the other LDS buffer (one barrier per slot).  When the
-// block's source rows span a small window (graphs batched as disjoint unions
-// keep their edges local), that window of X is staged in LDS once and every
-// gather is an LDS read; otherwise gathers read L2.  W_k fragments are
-// prefetched two slots ahead into registers.
+// Warp-specialised: 8 MFMA waves run slot k while 4 gather waves build slot
+// k+1 in the other Z buffer (one barrier per slot).  The W_k^T slice
+// (BN x K) is streamed through LDS: coalesced 16-B loads of slot k+2 go to
+// registers during slot k and are written to the free B buffer during slot
+// k+1, so W (re-read by every block) moves at full cache-line efficiency.
+// When the block's source rows span a small window (graphs batched as
+// disjoint unions keep their edges local) that window of X is staged in LDS
+// once and every gather is an LDS read; otherwise gathers read L2.
 template <int K, bool WRITE_Z, typename TOUT>
 __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
     const __hip_bfloat16* __restrict__ X, const int* __restrict__ srp,
     const int* __restrict__ ecol, const float* __restrict__ eval,
     const __hip_bfloat16* __restrict__ Wb, int64_t ss, int64_t sn,
     const float* __restrict__ bias, int relu, TOUT* __restrict__ out,
-    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M, int wcap,
-    int dbg) {
+    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M, int wcap) {
   constexpr int BM = kGG_BM, BN = kGG_BN;
   constexpr int KP = K + 8;          // padded LDS row (bf16 elements)
-  constexpr int LPR = K / 8;
+  constexpr int LPR = K / 8;         // 16-byte chunks per row
   constexpr int KS = K / 16;         // MFMA k-steps per slot
+  constexpr int MT = kGG_MFMA_WAVES * 64;
+  constexpr int BCH = BN * LPR;      // 16-byte chunks of one W_k^T slice
+  constexpr int BPT = (BCH + MT - 1) / MT;  // chunks per MFMA thread
 
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS char* smem = (DGMC_LDS char*)smem_raw;
   GGShared sh;
   sh.minmax = (DGMC_LDS int*)smem;
   sh.zbuf = (DGMC_LDS __bf16*)(smem + 16);
-  sh.xwin = sh.zbuf + 2 * BM * KP;
+  sh.bbuf = sh.zbuf + 2 * BM * KP;
+  sh.xwin = sh.bbuf + 2 * BN * KP;
   sh.srp = (DGMC_LDS int*)(sh.xwin + (size_t)wcap * KP);
   const int srp_n = BM * S + 1;
   sh.ecol = sh.srp + ((srp_n + 3) & ~3);
@@ -183,6 +191,33 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
   const int i0 = tile * BM;
   const int n0 = blockIdx.y * BN;
   const int rows = min(BM, Ndst - i0);
+  const int wave = tid / 64, lane = tid % 64;
+  const bool mfma_role = wave < kGG_MFMA_WAVES;
+
+  // W_k^T slice loads (MFMA threads): chunk c -> row n0 + c / LPR.
+  const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
+  bf16x8_t breg[BPT];
+  auto load_w = [&](int k) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int c = tid + i * MT;
+      const int n = n0 + c / LPR;
+      if (c < BCH && n < M)
+        breg[i] = *reinterpret_cast<const bf16x8_t*>(
+            W + (size_t)k * ss + (size_t)n * sn + (c % LPR) * 8);
+    }
+  };
+  auto store_w = [&](int buf) __attribute__((always_inline)) {
+    DGMC_LDS __bf16* bb = sh.bbuf + buf * BN * KP;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int c = tid + i * MT;
+      if (c < BCH && n0 + c / LPR < M)
+        *reinterpret_cast<DGMC_LDS bf16x8_t*>(bb + (c / LPR) * KP +
+                                              (c % LPR) * 8) = breg[i];
+    }
+  };
+  if (mfma_role) load_w(0);   // in flight during the metadata staging
 
   // ---- stage the block's slot-CSR metadata (+ source window) -----------
   const int nsrp = rows * S + 1;
@@ -210,7 +245,7 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
       lo = min(lo, __shfl_xor(lo, o));
       hi = max(hi, __shfl_xor(hi, o));
     }
-    if ((tid & 63) == 0 && hi >= 0) {
+    if (lane == 0 && hi >= 0) {
       atomicMin((int*)&sh.minmax[0], lo);
       atomicMax((int*)&sh.minmax[1], hi);
     }
@@ -229,86 +264,75 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
               c * 8);
     }
   }
+  if (mfma_role) {
+    store_w(0);
+    if (S > 1) load_w(1);
+  }
   __syncthreads();
 
-  const int wave = tid / 64, lane = tid % 64;
-  const bool mfma_role = wave < 4;
-  const bool write_z = blockIdx.y == 0;
-  const int gt = tid - 256;
+  const bool write_z = WRITE_Z && blockIdx.y == 0;
+  const int gt = tid - MT;
   auto gather = [&](int k, int buf) __attribute__((always_inline)) {
     DGMC_LDS __bf16* zb = sh.zbuf + buf * BM * KP;
-    if (windowed)
-      gg_gather<K, true, true, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
-                                        ecol, eval, Z, i0, write_z, gt);
-    else if (staged)
-      gg_gather<K, true, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
-                                         ecol, eval, Z, i0, write_z, gt);
-    else
-      gg_gather<K, false, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
-                                          ecol, eval, Z, i0, write_z, gt);
+    if (write_z) {
+      if (windowed)
+        gg_gather<K, true, true, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
+                                          ecol, eval, Z, i0, gt);
+      else if (staged)
+        gg_gather<K, true, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo, X,
+                                           ecol, eval, Z, i0, gt);
+      else
+        gg_gather<K, false, false, WRITE_Z>(sh, zb, k, S, rows, ebase, wlo,
+                                            X, ecol, eval, Z, i0, gt);
+    } else {
+      if (windowed)
+        gg_gather<K, true, true, false>(sh, zb, k, S, rows, ebase, wlo, X,
+                                        ecol, eval, Z, i0, gt);
+      else if (staged)
+        gg_gather<K, true, false, false>(sh, zb, k, S, rows, ebase, wlo, X,
+                                         ecol, eval, Z, i0, gt);
+      else
+        gg_gather<K, false, false, false>(sh, zb, k, S, rows, ebase, wlo, X,
+                                          ecol, eval, Z, i0, gt);
+    }
   };
 
-  // ---- MFMA tiles (MFMA waves: 32 rows x 32 columns each) ----------------
+  // ---- MFMA tiles: wave (rh, cq) owns rows 32rh.., columns 32cq.. -------
+  const int rh = (wave >> 2) & 1, cq = wave & 3;
   const int lr = lane & 31, lh = lane >> 5;
-  const int col = n0 + wave * 32 + lr;
-  const bool wave_active = mfma_role && n0 + wave * 32 < M;  // wave-uniform
-  const __bf16* W = reinterpret_cast<const __bf16*>(Wb);
-  bf16x8_t b0[KS], b1[KS], b2[KS];
-  auto load_b = [&](int k, bf16x8_t* b) __attribute__((always_inline)) {
-    const __bf16* base = W + (size_t)k * ss + (size_t)col * sn + 8 * lh;
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2)
-      b[s2] = *reinterpret_cast<const bf16x8_t*>(base + 16 * s2);
-  };
+  const int col = n0 + cq * 32 + lr;
+  const bool wave_active = mfma_role && n0 + cq * 32 < M;  // wave-uniform
   f32x16_t acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
-  // W_k fragments are prefetched PF slots ahead (2 where registers allow,
-  // K <= 128, else 1) into a register ring that is rotated by unrolling the
-  // slot loop - no register copies, so a load is waited for only by the
-  // MFMAs that consume it, PF slots later.
-  constexpr int PF = K <= 128 ? 2 : 1;
-  auto mfma_slot = [&](int buf, const bf16x8_t* b)
-                       __attribute__((always_inline)) {
-    DGMC_LDS const __bf16* za = sh.zbuf + buf * BM * KP + lr * KP + 8 * lh;
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      const bf16x8_t a =
-          *reinterpret_cast<DGMC_LDS const bf16x8_t*>(za + 16 * s2);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[s2], acc, 0, 0, 0);
-    }
-  };
-  // One slot: MFMA waves consume buffer k&1 with fragments `use` and
-  // prefetch slot k+PF into `into`; gather waves fill buffer (k+1)&1.
-  auto step = [&](int k, const bf16x8_t* use, bf16x8_t* into)
-                  __attribute__((always_inline)) {
-    if (wave_active && !(dbg & 2)) {
-      if (k + PF < S) load_b(k + PF, into);
-      mfma_slot(k & 1, use);
-    } else if (!mfma_role && k + 1 < S && !(dbg & 1)) {
-      gather(k + 1, (k + 1) & 1);
-    }
-    __syncthreads();
-  };
-
-  if (wave_active) {
-    load_b(0, b0);
-    if (PF == 2 && S > 1) load_b(1, b1);
-  }
   if (!mfma_role) gather(0, 0);
   __syncthreads();
-  if constexpr (PF == 2) {
-    for (int k = 0; k < S; k += 3) {
-      step(k, b0, b2);
-      if (k + 1 < S) step(k + 1, b1, b0);
-      if (k + 2 < S) step(k + 2, b2, b1);
+  for (int k = 0; k < S; ++k) {
+    const int buf = k & 1;
+    if (mfma_role) {
+      // W_{k+1}: registers (loaded during slot k-1) -> the free B buffer;
+      // then start W_{k+2}.
+      if (k + 1 < S) store_w(buf ^ 1);
+      if (k + 2 < S) load_w(k + 2);
+      if (wave_active) {
+        DGMC_LDS const __bf16* za =
+            sh.zbuf + buf * BM * KP + (rh * 32 + lr) * KP + 8 * lh;
+        DGMC_LDS const __bf16* zbp =
+            sh.bbuf + buf * BN * KP + (cq * 32 + lr) * KP + 8 * lh;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bf16x8_t a =
+              *reinterpret_cast<DGMC_LDS const bf16x8_t*>(za + 16 * s2);
+          const bf16x8_t b =
+              *reinterpret_cast<DGMC_LDS const bf16x8_t*>(zbp + 16 * s2);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+      }
+    } else if (k + 1 < S) {
+      gather(k + 1, buf ^ 1);
     }
-  } else {
-    for (int k = 0; k < S; k += 2) {
-      step(k, b0, b1);
-      if (k + 1 < S) step(k + 1, b1, b0);
-    }
+    __syncthreads();
   }
 
   // ---- epilogue ----------------------------------------------------------
@@ -316,7 +340,7 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
   const float b = bias ? bias[col] : 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const int row = rh * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
     if (row < rows) {
       float v = acc[r] + b;
       if (relu) v = fmaxf(v, 0.f);
@@ -325,12 +349,12 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
   }
 }
 
-static int gg_debug() {
-  static int v = [] {
-    const char* e = getenv("DGMC_GG_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
+template <int K>
+static size_t gg_fixed_lds(int S) {
+  const size_t row_bytes = (size_t)(K + 8) * 2;
+  const size_t srp_n = (size_t)kGG_BM * S + 1;
+  return 16 + (size_t)2 * (kGG_BM + kGG_BN) * row_bytes +
+         ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8;
 }
 
 template <int K, bool WRITE_Z, typename TOUT>
@@ -340,17 +364,12 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                       const float* bias, bool relu, at::Tensor& out,
                       __hip_bfloat16* Z, int Ndst, int S, int M) {
   const size_t row_bytes = (size_t)(K + 8) * 2;
-  const size_t srp_n = (size_t)kGG_BM * S + 1;
-  const size_t fixed = 16 + (size_t)2 * kGG_BM * row_bytes +
-                       ((srp_n + 3) & ~size_t(3)) * 4 + (size_t)kGG_ECAP * 8;
-  TORCH_CHECK(fixed + 16 * row_bytes <= (size_t)kGG_LDS_MAX,
+  const size_t fixed = gg_fixed_lds<K>(S);
+  TORCH_CHECK(fixed <= (size_t)kGG_LDS_MAX,
               "gather_gemm: LDS budget exceeded (S=", S, ")");
-  // Source window: what fits next to the fixed part within the 3-blocks-per
-  // -CU target (at least 2 * BM rows; beyond that the block reads L2).
-  const size_t budget = std::max<size_t>(kGG_LDS_TARGET,
-                                         fixed + 2 * kGG_BM * row_bytes);
-  const int wcap = (int)std::min<size_t>(
-      (std::min<size_t>(budget, kGG_LDS_MAX) - fixed) / row_bytes, 1024);
+  // Source window: whatever LDS is left (beyond it the block reads L2).
+  const int wcap =
+      (int)std::min<size_t>((kGG_LDS_MAX - fixed) / row_bytes, 1024);
   const size_t lds = fixed + (size_t)wcap * row_bytes;
   auto kern = gather_gemm_kernel<K, WRITE_Z, TOUT>;
   static bool attr_set = false;
@@ -368,7 +387,7 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                      reinterpret_cast<const __hip_bfloat16*>(W.data_ptr()), ss,
                      sn, bias, relu ? 1 : 0,
                      reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst, S, M,
-                     wcap, gg_debug());
+                     wcap);
 }
 
 template <int K>
@@ -449,8 +468,7 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
     case 32: dispatch_gg<32>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
     case 64: dispatch_gg<64>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
     case 128: dispatch_gg<128>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
-    case 256: dispatch_gg<256>(X, srp, ecol, eval, W, ss, sn, bp, relu, out, zp, Ndst, S, M); break;
-    default: TORCH_CHECK(false, "gather_gemm: K must be 32, 64, 128 or 256");
+    default: TORCH_CHECK(false, "gather_gemm: K must be 32, 64 or 128");
   }
   DGMC_CHECK_LAUNCH();
   return out;

@@ -285,7 +285,7 @@ class _GemmSpMM(torch.autograd.Function):
         return gx, gw, None, gb, None, None, None, None
 
 
-_FUSED_WIDTHS = (32, 64, 128, 256)
+_FUSED_WIDTHS = (32, 64, 128)
 
 
 def _fused_ok(x, K, M):

@@ -421,7 +421,8 @@ def _slot_op(N, S, E, device):
 
 
 @pytest.mark.parametrize('K,C,S', [(128, 128, 26), (32, 32, 3), (64, 96, 5),
-                                   (256, 64, 26), (128, 256, 4)])
+                                   (128, 64, 26), (128, 256, 4),
+                                   (64, 128, 26)])
 def test_gather_gemm_fused_forward_backward(K, C, S):
     from deep_graph_matching_consensus_amd.ops.sparse import gemm_spmm
     N = 300
