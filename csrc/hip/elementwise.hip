@@ -112,9 +112,10 @@ void launch_colsum(const at::Tensor& grad, const void* out, void* g,
                      reinterpret_cast<const TO*>(out),
                      reinterpret_cast<TR*>(g), part.data_ptr<float>(), rows, C,
                      relu ? 1 : 0);
-  hipLaunchKernelGGL(fold_rows_kernel, dim3((C + 31) / 32), dim3(256), 0,
-                     stream(), part.data_ptr<float>(), dst, blocks, C,
-                     accumulate ? 1 : 0);
+  if (dst)  // dst == nullptr: the caller keeps the per-block partials
+    hipLaunchKernelGGL(fold_rows_kernel, dim3((C + 31) / 32), dim3(256), 0,
+                       stream(), part.data_ptr<float>(), dst, blocks, C,
+                       accumulate ? 1 : 0);
 }
 
 template <typename T, typename TR, bool WRITE_G>
@@ -142,8 +143,26 @@ void dispatch_colsum(const at::Tensor& grad, const void* out, void* g,
   }
 }
 
+// Keep in sync with ops/gemm.py::col_partial_rows.
 static int colsum_blocks(int rows) {
   return std::max(1, std::min((rows + 15) / 16, kMaxColBlocks));
+}
+
+// Optional caller-owned partial buffer [blocks, C] fp32 (a loop-gradient
+// stack slot): then only the partials are written and the fold is skipped.
+static at::Tensor partials_or_new(const c10::optional<at::Tensor>& part_out,
+                                  int blocks, int C, const at::Tensor& like,
+                                  bool& keep) {
+  keep = part_out.has_value() && part_out->defined();
+  if (keep) {
+    TORCH_CHECK(part_out->scalar_type() == at::kFloat &&
+                    part_out->is_contiguous() &&
+                    part_out->numel() == (int64_t)blocks * C,
+                "colsum: part_out must be contiguous fp32 [", blocks, ", ", C,
+                "]");
+    return *part_out;
+  }
+  return at::empty({blocks, C}, like.options().dtype(at::kFloat));
 }
 
 static at::Tensor dst_or_new(const c10::optional<at::Tensor>& dst, int64_t C,
@@ -161,7 +180,7 @@ static at::Tensor dst_or_new(const c10::optional<at::Tensor>& dst, int64_t C,
 std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     const at::Tensor& grad, const at::Tensor& out, bool relu,
     at::ScalarType g_dtype, const c10::optional<at::Tensor>& dbias,
-    bool accumulate) {
+    bool accumulate, const c10::optional<at::Tensor>& part_out) {
   TORCH_CHECK(grad.is_cuda() && grad.dim() == 2 && grad.is_contiguous() &&
                   out.is_contiguous() && out.sizes() == grad.sizes(),
               "relu_bias_bwd: grad/out must be contiguous [rows, C]");
@@ -178,22 +197,23 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     return {g, db};
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({blocks, C}, grad.options().dtype(at::kFloat));
+  bool keep;
+  at::Tensor part = partials_or_new(part_out, blocks, C, grad, keep);
   const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
                    aligned16(g.data_ptr());
   DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
     DGMC_DISPATCH_FLOAT(g_dtype, TR, [&] {
       dispatch_colsum<T, TR, true>(grad, out.data_ptr(), g.data_ptr(), part,
-                                   db.data_ptr<float>(), blocks, rows, C,
-                                   relu, accumulate, vec);
+                                   keep ? nullptr : db.data_ptr<float>(),
+                                   blocks, rows, C, relu, accumulate, vec);
     });
   });
   DGMC_CHECK_LAUNCH();
-  return {g, db};
+  return {g, keep ? part : db};
 }
 
 at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
-                   bool accumulate) {
+                   bool accumulate, const c10::optional<at::Tensor>& part_out) {
   TORCH_CHECK(src.is_cuda() && src.dim() == 2 && src.is_contiguous(),
               "col_sum: contiguous [rows, C] expected");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
@@ -206,15 +226,16 @@ at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
     return out;
   }
   const int blocks = colsum_blocks(rows);
-  at::Tensor part = at::empty({blocks, C}, src.options().dtype(at::kFloat));
+  bool keep;
+  at::Tensor part = partials_or_new(part_out, blocks, C, src, keep);
   const bool vec = aligned16(src.data_ptr());
   DGMC_DISPATCH_FLOAT(src.scalar_type(), T, [&] {
     dispatch_colsum<T, float, false>(src, src.data_ptr(), nullptr, part,
-                                     out.data_ptr<float>(), blocks, rows, C,
-                                     false, accumulate, vec);
+                                     keep ? nullptr : out.data_ptr<float>(),
+                                     blocks, rows, C, false, accumulate, vec);
   });
   DGMC_CHECK_LAUNCH();
-  return out;
+  return keep ? part : out;
 }
 
 // dst (+)= sum over the leading dim of src [S, n] (fp32), float4 vectorised.

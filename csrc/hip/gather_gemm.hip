@@ -46,6 +46,10 @@ constexpr int kGG_LDS_MAX = 160 * 1024;
 constexpr int kGG_MFMA_WAVES = 8;       // 2 row halves x 4 column quarters
 constexpr int kGG_GATHER_THREADS = 256; // 4 gather waves
 constexpr int kGG_THREADS = kGG_MFMA_WAVES * 64 + kGG_GATHER_THREADS;
+__device__ long long g_gg_stamps[16];
+#define GG_STAMP(i)                                                   \
+  if ((dbg & 4) && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)    \
+    g_gg_stamps[i] = wall_clock64();
 
 __device__ __forceinline__ bf16x8_t pack_bf16x8(const float* v) {
   bf16x8_t r;
@@ -165,7 +169,8 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
     const int* __restrict__ ecol, const float* __restrict__ eval,
     const __hip_bfloat16* __restrict__ Wb, int64_t ss, int64_t sn,
     const float* __restrict__ bias, int relu, TOUT* __restrict__ out,
-    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M, int wcap) {
+    __hip_bfloat16* __restrict__ Z, int Ndst, int S, int M, int wcap,
+    int dbg) {
   constexpr int BM = kGG_BM, BN = kGG_BN;
   constexpr int KP = K + 8;          // padded LDS row (bf16 elements)
   constexpr int LPR = K / 8;         // 16-byte chunks per row
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
                                               (c % LPR) * 8) = breg[i];
     }
   };
+  GG_STAMP(0);
   if (mfma_role) load_w(0);   // in flight during the metadata staging
 
   // ---- stage the block's slot-CSR metadata (+ source window) -----------
@@ -306,11 +312,13 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 
+  GG_STAMP(1);
   if (!mfma_role) gather(0, 0);
   __syncthreads();
+  GG_STAMP(2);
   for (int k = 0; k < S; ++k) {
     const int buf = k & 1;
-    if (mfma_role) {
+    if (mfma_role && !(dbg & 2)) {
       // W_{k+1}: registers (loaded during slot k-1) -> the free B buffer;
       // then start W_{k+2}.
       if (k + 1 < S) store_w(buf ^ 1);
@@ -329,12 +337,13 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
         }
       }
-    } else if (k + 1 < S) {
+    } else if (!mfma_role && k + 1 < S && !(dbg & 1)) {
       gather(k + 1, buf ^ 1);
     }
     __syncthreads();
   }
 
+  GG_STAMP(3);
   // ---- epilogue ----------------------------------------------------------
   if (!wave_active || col >= M) return;
   const float b = bias ? bias[col] : 0.f;
@@ -347,6 +356,14 @@ __global__ __launch_bounds__(kGG_THREADS) void gather_gemm_kernel(
       out[(size_t)(i0 + row) * M + col] = Cvt<TOUT>::from_f(v);
     }
   }
+}
+
+static int gg_debug() {  // DGMC_GG_DEBUG: 1 = skip gathers, 2 = skip MFMA
+  static int v = [] {
+    const char* e = getenv("DGMC_GG_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 template <int K>
@@ -387,7 +404,7 @@ static void launch_gg(const at::Tensor& X, const at::Tensor& srp,
                      reinterpret_cast<const __hip_bfloat16*>(W.data_ptr()), ss,
                      sn, bias, relu ? 1 : 0,
                      reinterpret_cast<TOUT*>(out.data_ptr()), Z, Ndst, S, M,
-                     wcap);
+                     wcap, gg_debug());
 }
 
 template <int K>
@@ -417,6 +434,17 @@ static void dispatch_gg(const at::Tensor& X, const at::Tensor& srp,
 // X [Nsrc, K] bf16; srp [Ndst*S + 1] int32 slot-CSR (row i*S + k);
 // ecol/eval entries; W bf16 with element (slot k, out col n, in kk) at
 // W[k*ss + n*sn + kk]; optional bias [M]; optional Z [Ndst*S, K] bf16 output.
+// Debug: block (0,0) wall-clock stamps of the last launch with
+// DGMC_GG_DEBUG & 4 (prologue start, metadata staged, slot 0 gathered, loop
+// done).
+at::Tensor gather_gemm_stamps() {
+  long long h[16];
+  DGMC_CHECK_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_gg_stamps), sizeof(h)));
+  at::Tensor t = at::empty({16}, at::kLong);
+  memcpy(t.data_ptr<int64_t>(), h, sizeof(h));
+  return t;
+}
+
 at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const at::Tensor& ecol, const at::Tensor& eval,
                        const at::Tensor& W, int64_t ss, int64_t sn,

@@ -63,9 +63,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
 std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     const at::Tensor& grad, const at::Tensor& out, bool relu,
     at::ScalarType g_dtype, const c10::optional<at::Tensor>& dbias,
-    bool accumulate);
+    bool accumulate, const c10::optional<at::Tensor>& part_out);
 at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
-                   bool accumulate);
+                   bool accumulate, const c10::optional<at::Tensor>& part_out);
 void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
 at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const at::Tensor& ecol, const at::Tensor& eval,
@@ -74,6 +74,7 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const c10::optional<at::Tensor>& bias, bool relu,
                        at::ScalarType out_dtype,
                        const c10::optional<at::Tensor>& Z);
+at::Tensor gather_gemm_stamps();
 
 }  // namespace dgmc
 
@@ -110,15 +111,17 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
       "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype, "
-      "Tensor(a!)? dbias=None, bool accumulate=False) -> (Tensor, Tensor)");
+      "Tensor(a!)? dbias=None, bool accumulate=False, Tensor(b!)? "
+      "part_out=None) -> (Tensor, Tensor)");
   m.def(
-      "col_sum(Tensor src, Tensor(a!)? dst=None, bool accumulate=False) -> "
-      "Tensor");
+      "col_sum(Tensor src, Tensor(a!)? dst=None, bool accumulate=False, "
+      "Tensor(b!)? part_out=None) -> Tensor");
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
   m.def(
       "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
       "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
+  m.def("gather_gemm_stamps() -> Tensor");
   m.def(
       "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
       "Tensor Q, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
@@ -126,6 +129,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "sparse_consensus_bwd(Tensor rowptr, Tensor col, Tensor colptr, Tensor "
       "row_of, Tensor perm, Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
       "w2) -> (Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
+  m.impl("gather_gemm_stamps", &dgmc::gather_gemm_stamps);
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {

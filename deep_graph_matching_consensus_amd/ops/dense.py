@@ -26,7 +26,8 @@ import torch
 
 from . import _backend
 from . import reference as ref
-from .gemm import _col_sum, lowp_weight_t, mixed_matmul
+from .gemm import (_col_sum, loop_col_sum, loop_col_total, lowp_weight_t,
+                   mixed_matmul)
 from ..runtime import loopgrad
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
@@ -113,8 +114,7 @@ class _ConsensusUpdate(torch.autograd.Function):
         ctx.save_for_backward(P, Q, b1, w2, ptr_s, ptr_t)
         ctx.meta = (S_hat.dtype, b1.dtype, w2.dtype, b2.dtype, b2.shape)
         ctx.loop = loop
-        if loop is not None:
-            loop.register()
+        ctx.idx = loop.register() if loop is not None else None
         return out
 
     @staticmethod
@@ -131,11 +131,10 @@ class _ConsensusUpdate(torch.autograd.Function):
             db1, dw2, db2 = [_col_sum(t) for _, t in parts]
         else:
             for name, t in parts:
-                buf, acc = loop.acc(name, (t.size(1), ), t.device)
-                _col_sum(t, buf, acc)
+                loop_col_sum(loop, name, ctx.idx, t)
             db1 = dw2 = db2 = None
             if loop.arrive():
-                db1, dw2, db2 = [loop.get_acc(n) for n, _ in parts]
+                db1, dw2, db2 = [loop_col_total(loop, n) for n, _ in parts]
                 loop.release()
         if db1 is not None:
             db1 = db1.to(b1_dt)

@@ -92,8 +92,7 @@ class _MixedMatmul(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.loop = loop
-        if loop is not None:
-            loop.register()
+        ctx.idx = loop.register() if loop is not None else None
         return out
 
     @staticmethod
@@ -118,15 +117,39 @@ class _MixedMatmul(torch.autograd.Function):
             buf, acc = loop.acc('w', w_lp.shape, g.device)
             matmul_tn_fp32(xc.contiguous(), g, out=buf, accumulate=acc)
         if need_b:
-            buf, acc = loop.acc('b', (g.size(1), ), g.device)
-            _col_sum(g, buf, acc)
+            loop_col_sum(loop, 'b', ctx.idx, g)
         if loop.arrive():
             if need_w:
                 gw = loop.get_acc('w').to(ctx.w_dtype)
             if need_b:
-                gb = loop.get_acc('b').to(ctx.bias_dtype)
+                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
             loop.release()
         return gx, gw, None, gb, None
+
+
+def col_partial_rows(rows):
+    """Per-block partial rows of the HIP column reductions (keep in sync
+    with csrc/hip/elementwise.hip::colsum_blocks)."""
+    return max(1, min((rows + 15) // 16, 256))
+
+
+def loop_col_sum(loop, name, idx, src):
+    """Deposit ``src.sum(0)`` of loop use ``idx`` as per-block partials in
+    stack ``name`` (folded once by :func:`loop_col_total`)."""
+    if _backend.use_hip(src):
+        slot = loop.slot(name, idx, (col_partial_rows(src.size(0)),
+                                     src.size(1)), torch.float32, src.device)
+        _backend.ops().col_sum(src.contiguous(), None, False, slot)
+    else:
+        loop.add_to(name, src.float().sum(0))
+
+
+def loop_col_total(loop, name):
+    """Total of the contributions deposited by :func:`loop_col_sum`."""
+    if name in loop._stacks:
+        st = loop.stack(name)
+        return _col_sum(st.view(-1, st.size(-1)))
+    return loop.get_acc(name)
 
 
 def _col_sum(src, out=None, accumulate=False):

@@ -18,6 +18,8 @@ atomics anywhere (the reference's torch_scatter / spline_weighting backward
 use atomicAdd).  Plans are built once per batch and reused by every layer and
 every consensus step.
 """
+import os
+
 import torch
 
 from . import _backend
@@ -212,7 +214,7 @@ class _GemmSpMM(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad):
-        from .gemm import matmul_tn_fp32
+        from .gemm import col_partial_rows, loop_col_total, matmul_tn_fp32
         xc, w_lp, out = ctx.saved_tensors
         loop, idx, C = ctx.loop, ctx.idx, ctx.C
         grad = grad.contiguous()
@@ -222,11 +224,14 @@ class _GemmSpMM(torch.autograd.Function):
         # 1. g' = grad * relu'(out) and the bias gradient.
         db = None
         if hip:
-            dbuf, acc = loop.acc('b', (C, ), dev) if (loop and need_b) \
-                else (None, False)
+            # Loop uses keep per-block bias partials (folded once at the
+            # end); a single use folds right away.
+            part = loop.slot('b', idx, (col_partial_rows(grad.size(0)), C),
+                             torch.float32, dev) \
+                if (loop is not None and need_b) else None
             g, db = _backend.ops().relu_bias_bwd(
-                grad, out if ctx.relu else grad, ctx.relu, w_lp.dtype, dbuf,
-                acc)
+                grad, out if ctx.relu else grad, ctx.relu, w_lp.dtype, None,
+                False, part)
         else:
             g = grad.float()
             if ctx.relu:
@@ -280,7 +285,7 @@ class _GemmSpMM(torch.autograd.Function):
                 gw = matmul_tn_fp32(X, loop.stack('dy').view(X.size(0), -1))
                 gw = gw.to(ctx.w_dtype)
             if need_b:
-                gb = loop.get_acc('b').to(ctx.bias_dtype)
+                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
             loop.release()
         return gx, gw, None, gb, None, None, None, None
 
@@ -288,9 +293,16 @@ class _GemmSpMM(torch.autograd.Function):
 _FUSED_WIDTHS = (32, 64, 128)
 
 
+# The fused gather-MFMA SplineConv/RelConv kernel (csrc/hip/gather_gemm.hip)
+# is opt-in: measured on MI355X it is LDS-bandwidth bound at ~1.5 us per
+# slot (54 us per psi_2 layer vs 45 us for hipBLASLt GEMM + SpMM), see
+# docs/performance.md.  DGMC_AMD_FUSED_CONV=1 enables it.
+FUSED_CONV = os.environ.get('DGMC_AMD_FUSED_CONV', '0') == '1'
+
+
 def _fused_ok(x, K, M):
     """Shapes/dtypes served by the fused gather-MFMA kernel."""
-    return (_backend.use_hip(x) and x.dtype == torch.bfloat16
+    return (FUSED_CONV and _backend.use_hip(x) and x.dtype == torch.bfloat16
             and K in _FUSED_WIDTHS and M % 32 == 0)
 
 

@@ -391,6 +391,14 @@ def test_col_sum_and_relu_bias_accumulate(rows, C, dtype):
     buf = torch.full((C, ), 2.0, device=DEV)
     g2, db2 = ops.relu_bias_bwd(grad, o, True, dtype, buf, True)
     assert torch.allclose(buf, gm.sum(0) + 2, atol=1e-3, rtol=1e-4)
+    # Partials-only mode (loop-gradient stacks): the caller folds.
+    from deep_graph_matching_consensus_amd.ops.gemm import col_partial_rows
+    part = torch.empty(col_partial_rows(rows), C, device=DEV)
+    ops.col_sum(src, None, False, part)
+    assert torch.allclose(part.sum(0), ref_sum, atol=1e-3, rtol=1e-4)
+    part2 = torch.empty_like(part)
+    g3, _ = ops.relu_bias_bwd(grad, o, True, dtype, None, False, part2)
+    assert torch.allclose(part2.sum(0), gm.sum(0), atol=1e-3, rtol=1e-4)
     # Deterministic: repeated calls are bit-identical.
     assert torch.equal(ops.col_sum(src), ops.col_sum(src))
 
@@ -423,8 +431,12 @@ def _slot_op(N, S, E, device):
 @pytest.mark.parametrize('K,C,S', [(128, 128, 26), (32, 32, 3), (64, 96, 5),
                                    (128, 64, 26), (128, 256, 4),
                                    (64, 128, 26)])
-def test_gather_gemm_fused_forward_backward(K, C, S):
+def test_gather_gemm_fused_forward_backward(K, C, S, monkeypatch):
+    from deep_graph_matching_consensus_amd.ops import sparse as sparse_ops
     from deep_graph_matching_consensus_amd.ops.sparse import gemm_spmm
+    monkeypatch.setattr(sparse_ops, 'FUSED_CONV', True)
+    assert sparse_ops._fused_ok(torch.empty(1, K, device=DEV,
+                                            dtype=torch.bfloat16), K, C)
     N = 300
     op = _slot_op(N, S, 2000, DEV)
     x = torch.randn(N, K, device=DEV).bfloat16().requires_grad_()

@@ -64,3 +64,20 @@ for S in (2, 8, 26):
                                           None, None, True, torch.bfloat16))
         print('S=%2d local=%d fused %.1f us | gemm %.1f + spmm %.1f us | '
               'nnz %d' % (S, local, t_f, t_g, t_s, op.nnz), flush=True)
+
+# Stamps (DGMC_GG_DEBUG & 4): wall_clock64 runs at 100 MHz on gfx950.
+import os
+if int(os.environ.get('DGMC_GG_DEBUG', '0')) & 4:
+    for S in (2, 26):
+        op = make_op(N, S, 5, True)
+        sc = op.slot_csr(S)
+        x = torch.randn(N, K, device=dev).bfloat16()
+        w = (torch.randn(K, S * C, device=dev) / K ** .5).bfloat16()
+        wt = w.t().contiguous()
+        for _ in range(3):
+            ops.gather_gemm(x, sc.rowptr, sc.col, sc.val, wt, C * K, K, S, C,
+                            None, True, torch.bfloat16, None)
+        torch.cuda.synchronize()
+        st = ops.gather_gemm_stamps()[:4].tolist()
+        print('S=%d stamps (us from start):' % S,
+              [(v - st[0]) / 100.0 for v in st])
