@@ -210,17 +210,19 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
     if (wave == 0) sW[lane] = c < R ? w2[c] : 0.f;
     __syncthreads();
     const int cmax = min(kCh, R - c0);
+    // Channel-outer: the lane's Q value and w2 are read once per channel and
+    // feed up to kRowsPerWave independent accumulator chains (ILP).
+    const int nq = (ns - wave + kWaves - 1) / kWaves;  // rows of this wave
     if (lane < nt) {
+      for (int cc = 0; cc < cmax; ++cc) {
+        const float qv = sQ[lane * kPitch + cc];
+        const float wv = sW[cc];
 #pragma unroll
-      for (int q = 0; q < kRowsPerWave; ++q) {
-        const int i = wave + q * kWaves;
-        if (i < ns) {
-          float a = acc[q];
-          for (int cc = 0; cc < cmax; ++cc) {
-            const float z = sP[i * kPitch + cc] - sQ[lane * kPitch + cc];
-            a = fmaf(fmaxf(z, 0.f), sW[cc], a);
+        for (int q = 0; q < kRowsPerWave; ++q) {
+          if (q < nq) {
+            const float z = sP[(wave + q * kWaves) * kPitch + cc] - qv;
+            acc[q] = fmaf(fmaxf(z, 0.f), wv, acc[q]);
           }
-          acc[q] = a;
         }
       }
     }
@@ -291,29 +293,49 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     const float w = cv ? w2[c] : 0.f;
 
     // dP[i][c] and dw2 partial: rows owned by this wave, lane = channel.
+    // Branch-free, 4 independent partial sums so the LDS reads of 4 j's are
+    // in flight together (the loop is LDS-latency bound otherwise).
     float dw = 0.f;
     for (int i = wave; i < ns; i += kWaves) {
-      float dp = 0.f;
-      {
-        const float p = sP[i * kPitch + lane];
-        for (int j = 0; j < nt; ++j) {
-          const float z = p - sQ[j * kPitch + lane];
-          const float gij = sG[i * kPitch + j];
-          if (z > 0.f) {
-            dp += gij;
-            dw = fmaf(gij, z, dw);
-          }
+      const float p = sP[i * kPitch + lane];
+      float dp[4] = {0.f, 0.f, 0.f, 0.f}, dwq[4] = {0.f, 0.f, 0.f, 0.f};
+      int j = 0;
+      for (; j + 4 <= nt; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = fmaxf(p - sQ[(j + u) * kPitch + lane], 0.f);
+          const float gij = sG[i * kPitch + j + u];
+          dp[u] += z > 0.f ? gij : 0.f;
+          dwq[u] = fmaf(gij, z, dwq[u]);
         }
       }
-      if (cv) dPb[(size_t)i * R + c] = Cvt<TPQ>::from_f(dp * w);
+      for (; j < nt; ++j) {
+        const float z = fmaxf(p - sQ[j * kPitch + lane], 0.f);
+        const float gij = sG[i * kPitch + j];
+        dp[0] += z > 0.f ? gij : 0.f;
+        dwq[0] = fmaf(gij, z, dwq[0]);
+      }
+      dw += (dwq[0] + dwq[1]) + (dwq[2] + dwq[3]);
+      if (cv)
+        dPb[(size_t)i * R + c] =
+            Cvt<TPQ>::from_f(((dp[0] + dp[1]) + (dp[2] + dp[3])) * w);
     }
     // dQ[j][c] = -w * sum_i G[i][j] [P_ic > Q_jc]
     for (int j = wave; j < nt; j += kWaves) {
-      float dq = 0.f;
       const float qv = sQ[j * kPitch + lane];
-      for (int i = 0; i < ns; ++i)
-        if (sP[i * kPitch + lane] > qv) dq += sG[i * kPitch + j];
-      if (cv) dQb[(size_t)j * R + c] = Cvt<TPQ>::from_f(-dq * w);
+      float dq[4] = {0.f, 0.f, 0.f, 0.f};
+      int i = 0;
+      for (; i + 4 <= ns; i += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          dq[u] += sP[(i + u) * kPitch + lane] > qv
+                       ? sG[(i + u) * kPitch + j] : 0.f;
+      }
+      for (; i < ns; ++i)
+        dq[0] += sP[i * kPitch + lane] > qv ? sG[i * kPitch + j] : 0.f;
+      if (cv)
+        dQb[(size_t)j * R + c] =
+            Cvt<TPQ>::from_f(-((dq[0] + dq[1]) + (dq[2] + dq[3])) * w);
     }
     // Reduce dw over the 4 waves.
     sRed[wave * kCh + lane] = dw;
