@@ -210,19 +210,17 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
     if (wave == 0) sW[lane] = c < R ? w2[c] : 0.f;
     __syncthreads();
     const int cmax = min(kCh, R - c0);
-    // Channel-outer: the lane's Q value and w2 are read once per channel and
-    // feed up to kRowsPerWave independent accumulator chains (ILP).
-    const int nq = (ns - wave + kWaves - 1) / kWaves;  // rows of this wave
     if (lane < nt) {
-      for (int cc = 0; cc < cmax; ++cc) {
-        const float qv = sQ[lane * kPitch + cc];
-        const float wv = sW[cc];
 #pragma unroll
-        for (int q = 0; q < kRowsPerWave; ++q) {
-          if (q < nq) {
-            const float z = sP[(wave + q * kWaves) * kPitch + cc] - qv;
-            acc[q] = fmaf(fmaxf(z, 0.f), wv, acc[q]);
+      for (int q = 0; q < kRowsPerWave; ++q) {
+        const int i = wave + q * kWaves;
+        if (i < ns) {
+          float a = acc[q];
+          for (int cc = 0; cc < cmax; ++cc) {
+            const float z = sP[i * kPitch + cc] - sQ[lane * kPitch + cc];
+            a = fmaf(fmaxf(z, 0.f), sW[cc], a);
           }
+          acc[q] = a;
         }
       }
     }
@@ -413,7 +411,8 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
 // r_s: packed [sum N_s, R]; returns (S [B, Ns, Nt], r_t packed [rows_t, R]).
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t) {
+    const at::Tensor& ptr_t, int64_t rows_t,
+    const c10::optional<at::Tensor>& r_t_out) {
   check_pair_tensor(S_hat, "S_hat");
   check_packed(r_s, "r_s");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
@@ -422,7 +421,18 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor S = at::empty_like(S_hat);
-  at::Tensor r_t = at::empty({rows_t, R}, r_s.options());
+  at::Tensor r_t;
+  if (r_t_out.has_value() && r_t_out->defined()) {
+    // Caller-owned rows (e.g. the target half of psi_2's joint input), so no
+    // concatenation kernel is needed afterwards.
+    r_t = *r_t_out;
+    TORCH_CHECK(r_t.is_contiguous() && r_t.size(0) == rows_t &&
+                    r_t.size(1) == R && r_t.scalar_type() == r_s.scalar_type(),
+                "dense_softmax_transport: r_t_out must be contiguous [rows_t, "
+                "R] of r_s's dtype");
+  } else {
+    r_t = at::empty({rows_t, R}, r_s.options());
+  }
   if (B == 0) return {S, r_t};
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
     hipLaunchKernelGGL(softmax_transport_kernel<T>, dim3(B), dim3(256), 0,
@@ -503,7 +513,7 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t) {
+    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out) {
   check_pair_tensor(G, "grad");
   check_packed(P, "P");
   check_packed(Q, "Q");
@@ -512,8 +522,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   const int R = P.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
   check_ptr(ptr_s, ptr_t, B);
-  at::Tensor dP = at::empty_like(P);
-  at::Tensor dQ = at::empty_like(Q);
+  at::Tensor dP, dQ;
+  if (dpq_out.has_value() && dpq_out->defined()) {
+    // Joint [P; Q] gradient buffer: no slice-backward (fill + 2 copies).
+    const at::Tensor& d = *dpq_out;
+    TORCH_CHECK(d.is_contiguous() && d.scalar_type() == P.scalar_type() &&
+                    d.size(0) == P.size(0) + Q.size(0) && d.size(1) == R,
+                "dense_consensus_bwd: dpq_out must be [rows_s + rows_t, R]");
+    dP = d.narrow(0, 0, P.size(0));
+    dQ = d.narrow(0, P.size(0), Q.size(0));
+  } else {
+    dP = at::empty_like(P);
+    dQ = at::empty_like(Q);
+  }
   at::Tensor dw2 = at::empty({B, R}, G.options());
   at::Tensor db2 = at::empty({B}, G.options());
   if (B == 0) return {dP, dQ, dw2.zero_(), db2.zero_()};

@@ -31,7 +31,8 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
                                     const at::Tensor& n_t);
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t);
+    const at::Tensor& ptr_t, int64_t rows_t,
+    const c10::optional<at::Tensor>& r_t_out);
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
@@ -44,7 +45,7 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t);
+    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out);
 
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
 
@@ -97,7 +98,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "-> Tensor");
   m.def(
       "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor ptr_s, Tensor "
-      "ptr_t, int rows_t) -> (Tensor, Tensor)");
+      "ptr_t, int rows_t, Tensor(a!)? r_t_out=None) -> (Tensor, Tensor)");
   m.def(
       "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
       "ptr_s, Tensor ptr_t) -> Tensor");
@@ -106,7 +107,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor b2, Tensor ptr_s, Tensor ptr_t) -> Tensor");
   m.def(
       "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
-      "w2, Tensor ptr_s, Tensor ptr_t) -> (Tensor, Tensor, Tensor, Tensor)");
+      "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None) -> (Tensor, "
+      "Tensor, Tensor, Tensor)");
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(

@@ -188,14 +188,17 @@ class DGMC(torch.nn.Module):
                 r_all = torch.randn((steps, lay_s.num_nodes, R_in),
                                     dtype=r_dtype, device=device)
 
-            def refine(r_s, r_t):
+            def refine(r_s, r_t, r_joint=None):
                 """psi_2 on both graphs (packed in/out) under the caller's
-                autocast policy; returns (o_s, o_t, o_joint or None)."""
+                autocast policy; returns (o_s, o_t, o_joint or None).
+                ``r_joint`` = ``[r_s; r_t]`` already assembled."""
                 with torch.autocast(device_type=dev_type, dtype=outer_dtype,
                                     enabled=outer_autocast):
                     if pair is not None and self._fusable(self.psi_2):
-                        o = self.psi_2(torch.cat([r_s, r_t], dim=0),
-                                       pair.edge_index, pair.edge_attr)
+                        if r_joint is None:
+                            r_joint = torch.cat([r_s, r_t], dim=0)
+                        o = self.psi_2(r_joint, pair.edge_index,
+                                       pair.edge_attr)
                         return o[:pair.n_s], o[pair.n_s:], o
                     o_s = self.psi_2(r_s, edge_index_s, edge_attr_s)
                     o_t = self.psi_2(r_t, edge_index_t, edge_attr_t)
@@ -206,11 +209,26 @@ class DGMC(torch.nn.Module):
                 S_hat = hs @ ht.transpose(-1, -2)            # [B, N_s, N_t]
                 S_0 = lay_s.to_sparse(
                     dense_ops.masked_softmax(S_hat, lay_s, lay_t))
+                # Fused pair encoding: the transport kernel writes r_t
+                # straight into psi_2's joint input [r_s; r_t] (no cat).
+                joint = steps > 0 and pair is not None and \
+                    self._fusable(self.psi_2) and \
+                    dense_ops.transport_joint_supported(S_hat, lay_s, lay_t)
+                if joint:
+                    r_joint_all = torch.empty(
+                        (steps, lay_s.num_nodes + lay_t.num_nodes, R_in),
+                        dtype=r_all.dtype, device=device)
+                    r_joint_all[:, :lay_s.num_nodes].copy_(r_all)
                 for step in range(steps):
                     r_s = r_all[step]
-                    r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,
-                                                      lay_t)
-                    o_s, o_t, o = refine(r_s, r_t)
+                    if joint:
+                        r_joint = dense_ops.softmax_transport_joint(
+                            S_hat, r_joint_all[step], lay_s, lay_t)
+                        o_s, o_t, o = refine(None, None, r_joint)
+                    else:
+                        r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,
+                                                          lay_t)
+                        o_s, o_t, o = refine(r_s, r_t)
                     S_hat = dense_ops.consensus_update(
                         S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o)
                 S_L = lay_s.to_sparse(dense_ops.masked_softmax(

@@ -88,6 +88,47 @@ class _SoftmaxTransport(torch.autograd.Function):
         return g.to(ctx.dtype), None, None, None, None
 
 
+class _SoftmaxTransportJoint(torch.autograd.Function):
+    """Writes ``r_t`` into rows ``[n_s:]`` of ``joint`` (whose first rows
+    hold ``r_s``) and returns ``joint`` - psi_2's input without a cat."""
+
+    @staticmethod
+    def forward(ctx, S_hat, joint, n_s, ptr_s, ptr_t, rows_t):
+        r_s = joint[:n_s]
+        S, _ = _backend.ops().dense_softmax_transport(
+            S_hat.float().contiguous(), r_s, ptr_s, ptr_t, rows_t,
+            joint[n_s:])
+        ctx.mark_dirty(joint)
+        ctx.save_for_backward(S, ptr_s, ptr_t)
+        ctx.n_s = n_s
+        ctx.dtype = S_hat.dtype
+        ctx.r_s = r_s          # non-differentiable random indicators
+        return joint
+
+    @staticmethod
+    def backward(ctx, grad):
+        S, ptr_s, ptr_t = ctx.saved_tensors
+        r_s = ctx.r_s
+        g = _backend.ops().dense_softmax_transport_bwd(
+            S, r_s, grad[ctx.n_s:].to(r_s.dtype).contiguous(), ptr_s, ptr_t)
+        return g.to(ctx.dtype), None, None, None, None, None
+
+
+def transport_joint_supported(S_hat, lay_s, lay_t):
+    B, N_s, N_t = S_hat.shape
+    return _hip_ok(S_hat, N_s, N_t)
+
+
+def softmax_transport_joint(S_hat, joint, lay_s, lay_t):
+    r"""Like :func:`softmax_transport` for ``joint = [r_s; buffer]``
+    ``[sum N_s + sum N_t, R]``: fills the target rows in place and returns
+    ``joint`` (differentiable w.r.t. ``S_hat``)."""
+    assert joint.size(0) == lay_s.num_nodes + lay_t.num_nodes
+    return _SoftmaxTransportJoint.apply(S_hat, joint, lay_s.num_nodes,
+                                        lay_s.ptr, lay_t.ptr,
+                                        lay_t.num_nodes)
+
+
 def softmax_transport(S_hat, r_s, lay_s, lay_t):
     r"""``masked_softmax(S_hat)^T r_s`` with packed ``r_s [sum N_s, R]``;
     returns packed ``r_t [sum N_t, R]`` in ``r_s``'s dtype (fp32 or bf16;
@@ -105,8 +146,16 @@ def softmax_transport(S_hat, r_s, lay_s, lay_t):
 
 # ---------------------------------------------------------------------------
 class _ConsensusUpdate(torch.autograd.Function):
+    """``P``/``Q`` separately, or ``P`` = joint ``[P; Q]`` with ``Q`` an int
+    row split (then the joint gradient buffer is produced directly - no
+    slice-backward fill + copies)."""
+
     @staticmethod
     def forward(ctx, S_hat, P, Q, b1, w2, b2, ptr_s, ptr_t, loop):
+        ctx.split = None
+        if isinstance(Q, int):
+            ctx.split = Q
+            P, Q = P[:Q], P[Q:]
         out = _backend.ops().dense_consensus(
             S_hat.float().contiguous(), P.contiguous(), Q.contiguous(),
             b1.float().contiguous(), w2.float().contiguous().view(-1),
@@ -120,10 +169,16 @@ class _ConsensusUpdate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         P, Q, b1, w2, ptr_s, ptr_t = ctx.saved_tensors
+        dPQ = None
+        if ctx.split is not None:
+            dPQ = torch.empty((P.size(0) + Q.size(0), P.size(1)),
+                              dtype=P.dtype, device=P.device)
         dP, dQ, dw2_part, db2_part = _backend.ops().dense_consensus_bwd(
             grad.float().contiguous(), P.contiguous(), Q.contiguous(),
             b1.float().contiguous(), w2.float().contiguous().view(-1), ptr_s,
-            ptr_t)
+            ptr_t, dPQ)
+        if dPQ is not None:
+            dP, dQ = dPQ, None
         s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
         loop = ctx.loop
         parts = (('b1', dP), ('w2', dw2_part), ('b2', db2_part.view(-1, 1)))
@@ -159,7 +214,7 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None):
             PQ = mixed_matmul(o_joint, w1t,
                               lowp_weight_t(lin1.weight, o_joint.dtype),
                               loop_key=key + (o_joint.size(0), ))
-            P, Q = PQ[:lay_s.num_nodes], PQ[lay_s.num_nodes:]
+            P, Q = PQ, lay_s.num_nodes   # joint: split inside the op
         else:
             P = mixed_matmul(o_s, w1t, lowp_weight_t(lin1.weight, o_s.dtype),
                              loop_key=key + (o_s.size(0), ))
