@@ -38,11 +38,20 @@ def world_size():
     return dist.get_world_size() if is_distributed() else 1
 
 
-def init_distributed(backend=None, timeout_s=600):
+def init_distributed(backend=None, timeout_s=None):
     """Initialise the default process group from the environment.
 
     Returns the device this rank should use.  No-op for a single process.
+
+    Failure detection: collectives time out after ``timeout_s`` seconds
+    (default ``DGMC_AMD_DIST_TIMEOUT`` or 600) and RCCL's asynchronous error
+    handling is enabled, so a crashed or hung rank makes its peers raise
+    instead of blocking forever (gloo peers fail at once on a closed
+    connection, see tests/test_failures.py).
     """
+    if timeout_s is None:
+        timeout_s = float(os.environ.get('DGMC_AMD_DIST_TIMEOUT', '600'))
+    os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
     use_cuda = torch.cuda.is_available()
     if use_cuda:
         device = torch.device('cuda', env_local_rank() %

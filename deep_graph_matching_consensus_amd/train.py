@@ -43,10 +43,15 @@ class PairTrainer(object):
         bf16 (bool): bf16 autocast for the encoder GEMMs.
         seed (int): data-order seed (offset by rank).
         overlap (bool): overlap gradient all-reduce with backward (eager).
+        guard_nonfinite (bool): skip the optimizer update of any step whose
+            (all-reduced) gradients contain NaN/Inf - on the device, inside
+            the captured graph, via the fused Adam ``found_inf`` input; the
+            skipped-step count is reported by :meth:`read_stats`.
     """
 
     def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
-                 bf16=True, seed=0, overlap=True, sources=None):
+                 bf16=True, seed=0, overlap=True, sources=None,
+                 guard_nonfinite=True):
         self.model = model
         self.store = store
         self.device = store.device
@@ -63,7 +68,15 @@ class PairTrainer(object):
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda,
                                           capturable=mode == 'graph')
-        self.stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        # loss sum, correct, ground truths, skipped (non-finite) steps
+        self.stats = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.guard = guard_nonfinite
+        self._found_inf = torch.zeros(1, dtype=torch.float32,
+                                      device=self.device)
+        if self.guard and cuda:
+            # Read by the fused Adam kernel: a nonzero value skips the update
+            # (and the step counter) on the device - no host sync, capturable.
+            self.optimizer.found_inf = self._found_inf
         self.step_count = 0
         data_seed = seed + 1000 * self.rank
         if mode == 'eager':
@@ -99,12 +112,28 @@ class PairTrainer(object):
         self.stats[1] += model.correct(S_L.detach(), y, mask).double()
         self.stats[2] += y.size(1) if mask is None else mask.sum().double()
 
+    def _check_finite(self):
+        """Flag non-finite gradients in ``_found_inf`` (device-side)."""
+        if not self.guard:
+            return
+        bad = torch.logical_not(torch.isfinite(self.reducer.flat).all())
+        self._found_inf.copy_(bad.float().view(1))
+        self.stats[3] += self._found_inf[0].double()
+
+    def _optimizer_step(self):
+        if self.guard and self.device.type != 'cuda':
+            # Unfused CPU Adam has no found_inf input: skip on the host.
+            if self._found_inf.item() != 0:
+                return
+        self.optimizer.step()
+
     def _static_body(self):
         self.reducer.flat.zero_()
         batch = self.batcher.materialize()
         self._forward_backward(batch, self._rows, batch.y_mask)
         if self.world == 1:
-            self.optimizer.step()
+            self._check_finite()
+            self._optimizer_step()
 
     def step(self):
         """One training step (data, forward, backward, all-reduce, Adam)."""
@@ -115,7 +144,8 @@ class PairTrainer(object):
             rows = torch.arange(batch.y.numel(), device=self.device)
             self._forward_backward(batch, rows, None)
             self.reducer.finish()
-            self.optimizer.step()
+            self._check_finite()
+            self._optimizer_step()
         else:
             while not self.batcher.load():
                 pass
@@ -125,7 +155,8 @@ class PairTrainer(object):
                 self._static_body()
             if self.world > 1:
                 self.reducer.finish()
-                self.optimizer.step()
+                self._check_finite()
+                self._optimizer_step()
         self.step_count += 1
 
     def read_stats(self, reset=True):
@@ -135,7 +166,8 @@ class PairTrainer(object):
         parallel.all_reduce_sum(s)
         out = {'loss_sum': float(s[0]), 'correct': float(s[1]),
                'count': float(s[2]),
-               'hits@1': float(s[1] / s[2]) if s[2] > 0 else None}
+               'hits@1': float(s[1] / s[2]) if s[2] > 0 else None,
+               'skipped_steps': int(s[3] / max(self.world, 1))}
         if reset:
             self.stats.zero_()
         return out
