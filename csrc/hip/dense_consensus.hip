@@ -80,11 +80,17 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
     const float* __restrict__ S_hat, const TR* __restrict__ r_s,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     float* __restrict__ S, TR* __restrict__ r_t, int Ns, int Nt, int R,
-    int rows_t) {
+    int rows_t, TR* __restrict__ r_s_copy, int rows_s) {
   __shared__ float sS[kMaxN * kPitch];
   __shared__ float sR[kMaxN * kPitch];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  if (blockIdx.x == gridDim.x - 1) zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
+  if (blockIdx.x == gridDim.x - 1) {
+    zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
+    if (r_s_copy)  // rows past the last pair (static-batch padding)
+      for (size_t e = (size_t)ptr_s[gridDim.x] * R + threadIdx.x;
+           e < (size_t)rows_s * R; e += blockDim.x)
+        r_s_copy[e] = r_s[e];
+  }
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
   const float* Sh = S_hat + (size_t)b * Ns * Nt;
@@ -108,8 +114,12 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
   for (int c0 = 0; c0 < R; c0 += kCh) {
     const int c = c0 + lane;
     __syncthreads();
-    for (int i = wave; i < ns; i += kWaves)
-      sR[i * kPitch + lane] = c < R ? Cvt<TR>::to_f(rs[(size_t)i * R + c]) : 0.f;
+    for (int i = wave; i < ns; i += kWaves) {
+      const TR v = c < R ? rs[(size_t)i * R + c] : Cvt<TR>::from_f(0.f);
+      sR[i * kPitch + lane] = Cvt<TR>::to_f(v);
+      // Joint output [r_s; r_t]: psi_2's input without a concatenation.
+      if (r_s_copy && c < R) r_s_copy[(size_t)(ptr_s[b] + i) * R + c] = v;
+    }
     __syncthreads();
     for (int j = wave; j < nt; j += kWaves) {
       float acc = 0.f;
@@ -411,8 +421,7 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
 // r_s: packed [sum N_s, R]; returns (S [B, Ns, Nt], r_t packed [rows_t, R]).
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t,
-    const c10::optional<at::Tensor>& r_t_out) {
+    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out) {
   check_pair_tensor(S_hat, "S_hat");
   check_packed(r_s, "r_s");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
@@ -421,29 +430,33 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor S = at::empty_like(S_hat);
-  at::Tensor r_t;
-  if (r_t_out.has_value() && r_t_out->defined()) {
-    // Caller-owned rows (e.g. the target half of psi_2's joint input), so no
-    // concatenation kernel is needed afterwards.
-    r_t = *r_t_out;
-    TORCH_CHECK(r_t.is_contiguous() && r_t.size(0) == rows_t &&
-                    r_t.size(1) == R && r_t.scalar_type() == r_s.scalar_type(),
-                "dense_softmax_transport: r_t_out must be contiguous [rows_t, "
-                "R] of r_s's dtype");
+  at::Tensor r_t, joint;
+  const int64_t rows_s = r_s.size(0);
+  if (joint_out) {
+    // Joint [r_s; r_t] (psi_2's fused input): r_s rows are copied by the
+    // same kernel, so no concatenation kernel is needed afterwards.
+    joint = at::empty({rows_s + rows_t, R}, r_s.options());
+    r_t = joint.narrow(0, rows_s, rows_t);
   } else {
     r_t = at::empty({rows_t, R}, r_s.options());
   }
-  if (B == 0) return {S, r_t};
+  if (B == 0) {
+    if (joint_out) joint.narrow(0, 0, rows_s).copy_(r_s);
+    return {S, joint_out ? joint : r_t};
+  }
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
     hipLaunchKernelGGL(softmax_transport_kernel<T>, dim3(B), dim3(256), 0,
                        stream(), S_hat.data_ptr<float>(),
                        reinterpret_cast<const T*>(r_s.data_ptr()),
                        ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
                        S.data_ptr<float>(), reinterpret_cast<T*>(r_t.data_ptr()),
-                       Ns, Nt, R, (int)rows_t);
+                       Ns, Nt, R, (int)rows_t,
+                       joint_out ? reinterpret_cast<T*>(joint.data_ptr())
+                                 : nullptr,
+                       (int)rows_s);
   });
   DGMC_CHECK_LAUNCH();
-  return {S, r_t};
+  return {S, joint_out ? joint : r_t};
 }
 
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,

@@ -31,8 +31,7 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
                                     const at::Tensor& n_t);
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t,
-    const c10::optional<at::Tensor>& r_t_out);
+    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out);
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
@@ -98,7 +97,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "-> Tensor");
   m.def(
       "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor ptr_s, Tensor "
-      "ptr_t, int rows_t, Tensor(a!)? r_t_out=None) -> (Tensor, Tensor)");
+      "ptr_t, int rows_t, bool joint_out=False) -> (Tensor, Tensor)");
   m.def(
       "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
       "ptr_s, Tensor ptr_t) -> Tensor");

@@ -214,16 +214,11 @@ class DGMC(torch.nn.Module):
                 joint = steps > 0 and pair is not None and \
                     self._fusable(self.psi_2) and \
                     dense_ops.transport_joint_supported(S_hat, lay_s, lay_t)
-                if joint:
-                    r_joint_all = torch.empty(
-                        (steps, lay_s.num_nodes + lay_t.num_nodes, R_in),
-                        dtype=r_all.dtype, device=device)
-                    r_joint_all[:, :lay_s.num_nodes].copy_(r_all)
                 for step in range(steps):
                     r_s = r_all[step]
                     if joint:
                         r_joint = dense_ops.softmax_transport_joint(
-                            S_hat, r_joint_all[step], lay_s, lay_t)
+                            S_hat, r_s, lay_s, lay_t)
                         o_s, o_t, o = refine(None, None, r_joint)
                     else:
                         r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,

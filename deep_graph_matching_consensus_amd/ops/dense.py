@@ -89,29 +89,26 @@ class _SoftmaxTransport(torch.autograd.Function):
 
 
 class _SoftmaxTransportJoint(torch.autograd.Function):
-    """Writes ``r_t`` into rows ``[n_s:]`` of ``joint`` (whose first rows
-    hold ``r_s``) and returns ``joint`` - psi_2's input without a cat."""
+    """Returns ``[r_s; r_t]`` (psi_2's fused input) from one kernel: the
+    transport kernel also copies ``r_s`` - no concatenation kernel."""
 
     @staticmethod
-    def forward(ctx, S_hat, joint, n_s, ptr_s, ptr_t, rows_t):
-        r_s = joint[:n_s]
-        S, _ = _backend.ops().dense_softmax_transport(
-            S_hat.float().contiguous(), r_s, ptr_s, ptr_t, rows_t,
-            joint[n_s:])
-        ctx.mark_dirty(joint)
-        ctx.save_for_backward(S, ptr_s, ptr_t)
-        ctx.n_s = n_s
+    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t):
+        S, joint = _backend.ops().dense_softmax_transport(
+            S_hat.float().contiguous(), r_s.contiguous(), ptr_s, ptr_t,
+            rows_t, True)
+        ctx.save_for_backward(S, r_s, ptr_s, ptr_t)
         ctx.dtype = S_hat.dtype
-        ctx.r_s = r_s          # non-differentiable random indicators
+        ctx.n_s = r_s.size(0)
         return joint
 
     @staticmethod
     def backward(ctx, grad):
-        S, ptr_s, ptr_t = ctx.saved_tensors
-        r_s = ctx.r_s
+        S, r_s, ptr_s, ptr_t = ctx.saved_tensors
         g = _backend.ops().dense_softmax_transport_bwd(
-            S, r_s, grad[ctx.n_s:].to(r_s.dtype).contiguous(), ptr_s, ptr_t)
-        return g.to(ctx.dtype), None, None, None, None, None
+            S, r_s.contiguous(), grad[ctx.n_s:].to(r_s.dtype).contiguous(),
+            ptr_s, ptr_t)
+        return g.to(ctx.dtype), None, None, None, None
 
 
 def transport_joint_supported(S_hat, lay_s, lay_t):
@@ -119,13 +116,10 @@ def transport_joint_supported(S_hat, lay_s, lay_t):
     return _hip_ok(S_hat, N_s, N_t)
 
 
-def softmax_transport_joint(S_hat, joint, lay_s, lay_t):
-    r"""Like :func:`softmax_transport` for ``joint = [r_s; buffer]``
-    ``[sum N_s + sum N_t, R]``: fills the target rows in place and returns
-    ``joint`` (differentiable w.r.t. ``S_hat``)."""
-    assert joint.size(0) == lay_s.num_nodes + lay_t.num_nodes
-    return _SoftmaxTransportJoint.apply(S_hat, joint, lay_s.num_nodes,
-                                        lay_s.ptr, lay_t.ptr,
+def softmax_transport_joint(S_hat, r_s, lay_s, lay_t):
+    r"""``[r_s; masked_softmax(S_hat)^T r_s]`` as one packed
+    ``[sum N_s + sum N_t, R]`` tensor (differentiable w.r.t. ``S_hat``)."""
+    return _SoftmaxTransportJoint.apply(S_hat, r_s, lay_s.ptr, lay_t.ptr,
                                         lay_t.num_nodes)
 
 
@@ -177,11 +171,13 @@ class _ConsensusUpdate(torch.autograd.Function):
             grad.float().contiguous(), P.contiguous(), Q.contiguous(),
             b1.float().contiguous(), w2.float().contiguous().view(-1), ptr_s,
             ptr_t, dPQ)
+        dP_rows = dP                    # db1 = column sum over P rows only
         if dPQ is not None:
             dP, dQ = dPQ, None
         s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
         loop = ctx.loop
-        parts = (('b1', dP), ('w2', dw2_part), ('b2', db2_part.view(-1, 1)))
+        parts = (('b1', dP_rows), ('w2', dw2_part),
+                 ('b2', db2_part.view(-1, 1)))
         if loop is None:
             db1, dw2, db2 = [_col_sum(t) for _, t in parts]
         else:
