@@ -71,7 +71,8 @@ class PairTrainer(object):
         # loss sum, correct, ground truths, skipped (non-finite) steps
         self.stats = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.guard = guard_nonfinite
-        self._found_inf = torch.zeros(1, dtype=torch.float32,
+        # 0-dim: fused Adam subtracts it from the (0-dim) step counters.
+        self._found_inf = torch.zeros((), dtype=torch.float32,
                                       device=self.device)
         if self.guard and cuda:
             # Read by the fused Adam kernel: a nonzero value skips the update
@@ -117,8 +118,8 @@ class PairTrainer(object):
         if not self.guard:
             return
         bad = torch.logical_not(torch.isfinite(self.reducer.flat).all())
-        self._found_inf.copy_(bad.float().view(1))
-        self.stats[3] += self._found_inf[0].double()
+        self._found_inf.copy_(bad.float())
+        self.stats[3] += self._found_inf.double()
 
     def _optimizer_step(self):
         if self.guard and self.device.type != 'cuda':
