@@ -84,12 +84,16 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
   __shared__ float sS[kMaxN * kPitch];
   __shared__ float sR[kMaxN * kPitch];
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  if (blockIdx.x == gridDim.x - 1) {
-    zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
-    if (r_s_copy)  // rows past the last pair (static-batch padding)
-      for (size_t e = (size_t)ptr_s[gridDim.x] * R + threadIdx.x;
-           e < (size_t)rows_s * R; e += blockDim.x)
-        r_s_copy[e] = r_s[e];
+  if (blockIdx.x == gridDim.x - 1) zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
+  if (r_s_copy) {
+    // r_s rows past the last pair (static-batch padding), spread over the
+    // whole grid: one element per thread instead of a serial loop in one
+    // block (which put ~60 us on the kernel's critical path).
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t e = (size_t)ptr_s[gridDim.x] * R +
+                    (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+         e < (size_t)rows_s * R; e += stride)
+      r_s_copy[e] = r_s[e];
   }
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
