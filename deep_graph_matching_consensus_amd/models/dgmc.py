@@ -33,6 +33,7 @@ from ..ops import sparse_corr
 from ..ops.plans import _IdentityCache
 from ..runtime import loopgrad
 from ..runtime.cache import forward_cache
+from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
 
 EPS = 1e-8
@@ -158,8 +159,9 @@ class DGMC(torch.nn.Module):
                     edge_index_s, edge_attr_s, x_s.size(0), edge_index_t,
                     edge_attr_t))
 
-        h_s, h_t = self._encode(self.psi_1, pair, x_s, x_t, edge_index_s,
-                                edge_attr_s, edge_index_t, edge_attr_t)
+        with trace_range('dgmc.psi_1'):
+            h_s, h_t = self._encode(self.psi_1, pair, x_s, x_t, edge_index_s,
+                                    edge_attr_s, edge_index_t, edge_attr_t)
         if self.detach:
             h_s, h_t = h_s.detach(), h_t.detach()
 
@@ -215,6 +217,7 @@ class DGMC(torch.nn.Module):
                     self._fusable(self.psi_2) and \
                     dense_ops.transport_joint_supported(S_hat, lay_s, lay_t)
                 for step in range(steps):
+                    mark('dgmc.consensus_step')
                     r_s = r_all[step]
                     if joint:
                         r_joint = dense_ops.softmax_transport_joint(
@@ -231,7 +234,8 @@ class DGMC(torch.nn.Module):
                 return S_0, S_L
 
             # ------------------- sparse variant ---------------------- #
-            S_idx = self.__top_k__(hs, ht)                    # [B, N_s, k]
+            with trace_range('dgmc.top_k'):
+                S_idx = self.__top_k__(hs, ht)                # [B, N_s, k]
             if self.training and y is not None:
                 rnd_size = (B, N_s, min(self.k, N_t - self.k))
                 S_rnd_idx = torch.randint(N_t, rnd_size, dtype=torch.long,

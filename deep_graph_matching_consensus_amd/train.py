@@ -29,6 +29,7 @@ from . import parallel
 from .datasets.device_loader import DevicePairLoader
 from .datasets.static_batch import StaticPairBatcher
 from .runtime.graphs import GraphedStep
+from .runtime.profiling import trace_range
 
 
 class PairTrainer(object):
@@ -140,24 +141,33 @@ class PairTrainer(object):
         """One training step (data, forward, backward, all-reduce, Adam)."""
         self.model.train()
         if self.mode == 'eager':
-            batch = next(self._batches)
+            with trace_range('train.load'):
+                batch = next(self._batches)
             self.reducer.zero_grad()
             rows = torch.arange(batch.y.numel(), device=self.device)
-            self._forward_backward(batch, rows, None)
-            self.reducer.finish()
-            self._check_finite()
-            self._optimizer_step()
-        else:
-            while not self.batcher.load():
-                pass
-            if self._graph is not None:
-                self._graph()
-            else:
-                self._static_body()
-            if self.world > 1:
+            with trace_range('train.forward_backward'):
+                self._forward_backward(batch, rows, None)
+            with trace_range('train.allreduce'):
                 self.reducer.finish()
+            with trace_range('train.optimizer'):
                 self._check_finite()
                 self._optimizer_step()
+        else:
+            with trace_range('train.load'):
+                while not self.batcher.load():
+                    pass
+            with trace_range('train.graph_replay' if self._graph is not None
+                             else 'train.forward_backward'):
+                if self._graph is not None:
+                    self._graph()
+                else:
+                    self._static_body()
+            if self.world > 1:
+                with trace_range('train.allreduce'):
+                    self.reducer.finish()
+                with trace_range('train.optimizer'):
+                    self._check_finite()
+                    self._optimizer_step()
         self.step_count += 1
 
     def read_stats(self, reset=True):
