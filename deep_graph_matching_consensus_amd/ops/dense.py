@@ -182,10 +182,10 @@ class _ConsensusUpdate(torch.autograd.Function):
             db1, dw2, db2 = [_col_sum(t) for _, t in parts]
         else:
             for name, t in parts:
-                loop_col_sum(loop, name, ctx.idx, t)
+                loop.keep(name, ctx.idx, t)
             db1 = dw2 = db2 = None
             if loop.arrive():
-                db1, dw2, db2 = [loop_col_total(loop, n) for n, _ in parts]
+                db1, dw2, db2 = [_col_sum(loop.kept(n)) for n, _ in parts]
                 loop.release()
         if db1 is not None:
             db1 = db1.to(b1_dt)

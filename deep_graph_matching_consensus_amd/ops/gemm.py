@@ -113,16 +113,17 @@ class _MixedMatmul(torch.autograd.Function):
             if need_b:
                 gb = _col_sum(g).to(ctx.bias_dtype)
             return gx, gw, None, gb, None
-        if need_w:
-            buf, acc = loop.acc('w', w_lp.shape, g.device)
-            matmul_tn_fp32(xc.contiguous(), g, out=buf, accumulate=acc)
-        if need_b:
-            loop_col_sum(loop, 'b', ctx.idx, g)
+        # Kept: reference x and g per use; ONE long-K GEMM (and column sum)
+        # over the concatenation when the last use arrives.
+        loop.keep('x', ctx.idx, xc)
+        loop.keep('g', ctx.idx, g)
         if loop.arrive():
+            G = loop.kept('g')
             if need_w:
-                gw = loop.get_acc('w').to(ctx.w_dtype)
+                gw = matmul_tn_fp32(loop.kept('x').contiguous(), G)
+                gw = gw.to(ctx.w_dtype)
             if need_b:
-                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+                gb = _col_sum(G).to(ctx.bias_dtype)
             loop.release()
         return gx, gw, None, gb, None
 

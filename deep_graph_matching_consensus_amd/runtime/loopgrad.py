@@ -19,7 +19,11 @@ deposits *contributions* instead of returning gradients:
 * **accumulated** - small reductions (bias/vector gradients, small GEMMs)
   are folded into a persistent fp32 buffer by the producing kernel itself
   (``accumulate`` flags of ``col_sum``/``relu_bias_bwd``/``reduce_add_rows``)
-  - no separate add kernels.
+  - no separate add kernels;
+* **kept** - operands that already exist as separate tensors (a GEMM input
+  saved by autograd, an incoming gradient) are only referenced per use and
+  concatenated once at the end: one ``cat`` + one GEMM / column sum replace
+  a split-K GEMM, combine and reduction per use.
 
 Only the use whose backward completes the set returns the gradients; the
 others return ``None``.  This is order-independent (the count, not the order,
@@ -45,6 +49,7 @@ class LoopGrad(object):
         self.arrived = 0
         self._stacks = {}
         self._accs = {}
+        self._kept = {}
 
     def register(self):
         """Called by every forward use; returns the use index."""
@@ -90,6 +95,19 @@ class LoopGrad(object):
     def get_acc(self, name):
         return self._accs.get(name)
 
+    def keep(self, name, idx, tensor):
+        """Reference ``tensor`` as use ``idx``'s contribution ``name``."""
+        lst = self._kept.get(name)
+        if lst is None:
+            lst = self._kept[name] = [None] * self.uses
+        lst[idx] = tensor
+
+    def kept(self, name):
+        """Concatenation (dim 0, use order) of the kept contributions."""
+        lst = self._kept[name]
+        assert all(t is not None for t in lst), name
+        return lst[0] if len(lst) == 1 else torch.cat(lst, dim=0)
+
     def arrive(self):
         """Called once per backward use; True for the use completing the set
         (which then computes/returns the gradients and calls
@@ -100,6 +118,7 @@ class LoopGrad(object):
     def release(self):
         self._stacks = {}
         self._accs = {}
+        self._kept = {}
         self.arrived = 0
 
 
