@@ -84,9 +84,14 @@ class _MixedMatmul(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w_lp, bias, loop):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
-        out = xc @ w_lp
         if bias is not None:
-            out = out + bias.to(out.dtype)
+            # Bias in the GEMM epilogue (hipBLASLt), cast once per forward.
+            b_lp = bias if bias.dtype == w_lp.dtype else cached(
+                ('bias_lp', id(bias), w_lp.dtype),
+                lambda: (bias, bias.detach().to(w_lp.dtype)))[1]
+            out = torch.addmm(b_lp, xc, w_lp)
+        else:
+            out = xc @ w_lp
         ctx.save_for_backward(xc, w_lp)
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
         ctx.has_bias = bias is not None

@@ -248,7 +248,7 @@ class _GemmSpMM(torch.autograd.Function):
         fused = ctx.needs_input_grad[0] and _fused_ok(g, C, K)
         if loop is not None:
             dy = loop.slot('dy', idx, (opt.num_rows, C), w_lp.dtype, dev)
-            loop.slot('x', idx, xc.shape, xc.dtype, dev).copy_(xc)
+            loop.keep('x', idx, xc)      # concatenated once at the end
         elif fused:
             dy = torch.empty((opt.num_rows, C), dtype=w_lp.dtype, device=dev)
         else:
@@ -280,8 +280,7 @@ class _GemmSpMM(torch.autograd.Function):
                 gb = db.to(ctx.bias_dtype)
         elif loop.arrive():
             if ctx.needs_input_grad[1]:
-                X = loop.stack('x')
-                X = X.view(-1, X.size(-1))
+                X = loop.kept('x').contiguous()
                 gw = matmul_tn_fp32(X, loop.stack('dy').view(X.size(0), -1))
                 gw = gw.to(ctx.w_dtype)
             if need_b:
