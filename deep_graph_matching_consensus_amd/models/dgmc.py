@@ -71,15 +71,23 @@ class DGMC(torch.nn.Module):
         num_steps (int): number of consensus iterations.
         k (int, optional): sparsity.  ``-1`` keeps dense correspondences.
         detach (bool, optional): stop gradients into ``psi_1``.
+        normalization (str, optional): extension - ``'softmax'`` (the
+            reference, default) or ``'sinkhorn'`` (dense path only:
+            log-domain Sinkhorn with ``sinkhorn_iters`` iterations for
+            ``S_0``, every consensus step and ``S_L``).
     """
 
-    def __init__(self, psi_1, psi_2, num_steps, k=-1, detach=False):
+    def __init__(self, psi_1, psi_2, num_steps, k=-1, detach=False,
+                 normalization='softmax', sinkhorn_iters=10):
         super(DGMC, self).__init__()
+        assert normalization in ('softmax', 'sinkhorn')
         self.psi_1 = psi_1
         self.psi_2 = psi_2
         self.num_steps = num_steps
         self.k = k
         self.detach = detach
+        self.normalization = normalization
+        self.sinkhorn_iters = sinkhorn_iters
         self.backend = 'auto'
         R = psi_2.out_channels
         self.mlp = Sequential(Linear(R, R), ReLU(), Linear(R, 1))
@@ -206,6 +214,12 @@ class DGMC(torch.nn.Module):
                     o_t = self.psi_2(r_t, edge_index_t, edge_attr_t)
                     return o_s, o_t, None
 
+            if self.k < 1 and self.normalization == 'sinkhorn':
+                # ---------- dense variant, Sinkhorn (extension) ---------- #
+                return self._dense_sinkhorn(hs, ht, r_all, steps, lay_s,
+                                            lay_t, refine)
+            assert self.normalization == 'softmax', \
+                'Sinkhorn normalisation is only defined for k=-1 (dense)'
             if self.k < 1:
                 # ------------------ dense variant -------------------- #
                 S_hat = hs @ ht.transpose(-1, -2)            # [B, N_s, N_t]
@@ -273,6 +287,28 @@ class DGMC(torch.nn.Module):
             S.__val__ = val
             out.append(S)
         return tuple(out)
+
+    def _dense_sinkhorn(self, hs, ht, r_all, steps, lay_s, lay_t, refine):
+        """Dense path with Sinkhorn normalisation (opt-in extension): the
+        same consensus loop with ``masked_sinkhorn`` in place of the row
+        softmax; transport ``r_t = S^T r_s`` as a batched GEMM."""
+        from ..ops import reference as ref
+        mask = ref.count_mask(lay_s.counts, lay_t.counts, lay_s.N, lay_t.N)
+
+        def norm(S_hat):
+            return ref.masked_sinkhorn(S_hat, mask, self.sinkhorn_iters)
+
+        S_hat = hs @ ht.transpose(-1, -2)
+        S_0 = lay_s.to_sparse(norm(S_hat))
+        for step in range(steps):
+            r_s = r_all[step]
+            S = norm(S_hat)
+            r_t = lay_t.to_sparse(S.transpose(-1, -2) @
+                                  lay_s.to_dense(r_s.to(S.dtype)))
+            o_s, o_t, o = refine(r_s, r_t.to(r_s.dtype))
+            S_hat = dense_ops.consensus_update(S_hat, o_s, o_t, self.mlp,
+                                               lay_s, lay_t, o_joint=o)
+        return S_0, lay_s.to_sparse(norm(S_hat))
 
     # ------------------------------------------------------------------
     # Objectives and metrics (dgmc.py:246-311)

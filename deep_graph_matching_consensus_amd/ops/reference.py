@@ -81,6 +81,26 @@ def masked_softmax(src, mask, dim=-1):
     return out
 
 
+def masked_sinkhorn(src, mask, num_iters=10, tau=1.0):
+    r"""Log-domain Sinkhorn normalisation over the valid entries (opt-in
+    extension; the reference only uses row softmax).
+
+    Alternates row and column normalisation of ``exp(src / tau)`` and ends
+    with a row normalisation, so every valid row sums to 1 like
+    :func:`masked_softmax` while columns are pushed towards 1.  Invalid
+    entries are 0; fully masked rows/columns stay 0 (no NaN).
+    """
+    neg = torch.finfo(src.dtype).min / 4
+    log = (src / tau).masked_fill(~mask, neg)
+    for _ in range(num_iters):
+        log = log - torch.logsumexp(log, dim=-1, keepdim=True)
+        log = log.masked_fill(~mask, neg)
+        log = log - torch.logsumexp(log, dim=-2, keepdim=True)
+        log = log.masked_fill(~mask, neg)
+    log = log - torch.logsumexp(log, dim=-1, keepdim=True)
+    return log.exp().masked_fill(~mask, 0)
+
+
 def count_mask(n_s, n_t, N_s, N_t):
     """``[B, N_s, N_t]`` validity mask from per-pair node counts."""
     device = n_s.device

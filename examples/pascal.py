@@ -37,6 +37,10 @@ parser.add_argument('--graphs', type=int, default=256,
                     help='synthetic training graphs per category')
 parser.add_argument('--mode', default=None, choices=['graph', 'static',
                                                      'eager'])
+parser.add_argument('--normalization', default='softmax',
+                    choices=['softmax', 'sinkhorn'],
+                    help='extension: Sinkhorn instead of the reference '
+                         'row softmax (dense path)')
 parser.add_argument('--checkpoint', default=None)
 parser.add_argument('--log', default=None, help='JSONL metrics file')
 args = parser.parse_args()
@@ -58,7 +62,8 @@ psi_1 = SplineCNN(num_node_features, args.dim, num_edge_features,
                   args.num_layers, cat=False, dropout=0.5)
 psi_2 = SplineCNN(args.rnd_dim, args.rnd_dim, num_edge_features,
                   args.num_layers, cat=True, dropout=0.0)
-model = DGMC(psi_1, psi_2, num_steps=args.num_steps).to(device)
+model = DGMC(psi_1, psi_2, num_steps=args.num_steps,
+             normalization=args.normalization).to(device)
 mode = args.mode or ('graph' if device.type == 'cuda' else 'eager')
 trainer = PairTrainer(model, store, args.batch_size, lr=args.lr, mode=mode)
 logger = MetricsLogger(args.log)
