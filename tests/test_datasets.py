@@ -47,3 +47,11 @@ def test_kg_pair_sizes():
     assert n == int(15000 * 0.05)
     assert d.train_y[0].max() < d.x1.size(0)
     assert d.train_y[1].max() < d.x2.size(0)
+
+
+def test_cli_presets_list_and_er_train(capsys):
+    from deep_graph_matching_consensus_amd import cli
+    assert cli.main(['list']) == 0
+    out = capsys.readouterr().out
+    for name in ('er', 'willow', 'pascal', 'pascal_pf', 'dbp15k'):
+        assert name in out
