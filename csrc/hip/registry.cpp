@@ -75,6 +75,9 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        at::ScalarType out_dtype,
                        const c10::optional<at::Tensor>& Z);
 at::Tensor gather_gemm_stamps();
+at::Tensor gemm_abt(const at::Tensor& A, const at::Tensor& Bt,
+                    const c10::optional<at::Tensor>& out, bool accumulate,
+                    c10::optional<at::ScalarType> out_dtype);
 
 }  // namespace dgmc
 
@@ -124,6 +127,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
   m.def("gather_gemm_stamps() -> Tensor");
   m.def(
+      "gemm_abt(Tensor A, Tensor Bt, Tensor(a!)? out=None, bool "
+      "accumulate=False, ScalarType? out_dtype=None) -> Tensor");
+  m.def(
       "sparse_consensus_fwd(Tensor rowptr, Tensor col, Tensor S_hat, Tensor P, "
       "Tensor Q, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
   m.def(
@@ -152,6 +158,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
   m.impl("gather_gemm", &dgmc::gather_gemm);
+  m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
 }

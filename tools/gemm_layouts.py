@@ -24,7 +24,7 @@ def timeit(fn, iters=50, warmup=10):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument('--nodes', type=int, default=9216)
-    args = p.parse_args()
+    args, _ = p.parse_known_args()
     N, K, S, C = args.nodes, 128, 26, 128
     dev, dt = 'cuda', torch.bfloat16
     x = torch.randn(N, K, device=dev, dtype=dt)
@@ -54,5 +54,40 @@ def main():
         print('%-36s %7.1f us  %5.2f TB/s(in)' % (k, v, gb / 2 / v * 1e3))
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and '--custom' not in __import__('sys').argv:
     main()
+
+
+def custom():
+    """dgmc_amd::gemm_abt vs hipBLASLt on the same shapes (+ max error)."""
+    import os.path as osp
+    import sys
+    sys.path.insert(0, osp.dirname(osp.dirname(osp.abspath(__file__))))
+    from deep_graph_matching_consensus_amd.ops import _backend
+    assert _backend.hip_available()
+    ops = _backend.ops()
+    N, K, S, C = 9216, 128, 26, 128
+    dev, dt = 'cuda', torch.bfloat16
+    x = torch.randn(N, K, device=dev, dtype=dt)
+    w = torch.randn(K, S * C, device=dev, dtype=dt) / K ** .5
+    wt = w.t().contiguous()
+    ref = x @ w
+    y = ops.gemm_abt(x, wt)
+    print('custom fwd  err %.3e' % (y.float() - ref.float()).abs().max())
+    t = timeit(lambda: ops.gemm_abt(x, wt))
+    print('custom fwd  %7.1f us  %5.2f TB/s(out)' % (t, N * S * C * 2 / t / 1e6))
+    dY = torch.randn(N, S * C, device=dev, dtype=dt)
+    ref = dY @ w.t()
+    dx = ops.gemm_abt(dY, w)
+    print('custom dX   err %.3e (ref max %.2f)' % (
+        (dx.float() - ref.float()).abs().max(), ref.float().abs().max()))
+    t = timeit(lambda: ops.gemm_abt(dY, w))
+    print('custom dX   %7.1f us  %5.2f TB/s(in)' % (t, N * S * C * 2 / t / 1e6))
+    acc = ref.clone()
+    ops.gemm_abt(dY, w, acc, True)
+    print('custom dX accumulate err %.3e' % (acc.float() - 2 * ref.float())
+          .abs().max())
+
+
+if __name__ == '__main__' and '--custom' in __import__('sys').argv:
+    custom()
