@@ -110,7 +110,7 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
   }
 }
 
-inline bool aligned16(const void* p) {
+__host__ __device__ inline bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 

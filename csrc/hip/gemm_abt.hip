@@ -125,8 +125,11 @@ __global__ __launch_bounds__(256) void gemm_abt_kernel(
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
+          // Operands swapped (Bt . A^T): the accumulator's lane index is
+          // the C row and its registers run along C columns, so the
+          // epilogue writes 4 consecutive columns per 8-byte LDS store.
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              af[i], bf[j], acc[i][j], 0, 0, 0);
+              bf[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (NBUF == 2) {
       if (kt + 1 < nk) store(buf ^ 1);  // other buffer: free since last barrier
@@ -138,24 +141,64 @@ __global__ __launch_bounds__(256) void gemm_abt_kernel(
     }
   }
 
-  // Epilogue: C layout col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Epilogue through LDS: the C tile is assembled row-major in LDS (8-byte
+  // writes of 4 consecutive columns), then written with coalesced 16-byte
+  // row stores (2-byte scattered stores ran at ~1.7 TB/s).
+  constexpr int CP = BN + (16 / (int)sizeof(TC));   // padded C row
+  static_assert((size_t)BM * CP * sizeof(TC) <=
+                    (size_t)NBUF * (BM + BN) * KP * 2,
+                "C tile must fit in the operand LDS");
+  GAB_LDS TC* sC = (GAB_LDS TC*)smem_raw;
+  __syncthreads();   // operand tiles no longer read
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn + j * 32 + lr;
-      if (col >= M) continue;
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row < N) {
-          TC* p = C + (size_t)row * ldc + col;
-          float v = acc[i][j][r];
-          if (accumulate) v += Cvt<TC>::to_f(*p);
-          *p = Cvt<TC>::from_f(v);
+      for (int g = 0; g < 4; ++g) {
+        // lane -> row wm + 32i + lr; regs 4g..4g+3 -> columns
+        // wn + 32j + 8g + 4lh + 0..3
+        const int row = wm + i * 32 + lr;
+        const int col = wn + j * 32 + 8 * g + 4 * lh;
+        TC pk[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = Cvt<TC>::from_f(acc[i][j][4 * g + e]);
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+        if constexpr (sizeof(TC) == 2) {
+          *reinterpret_cast<GAB_LDS u32x2*>(sC + row * CP + col) =
+              *reinterpret_cast<const u32x2*>(pk);
+        } else {
+          *reinterpret_cast<GAB_LDS u32x4v*>(sC + row * CP + col) =
+              *reinterpret_cast<const u32x4v*>(pk);
         }
       }
+  __syncthreads();
+  constexpr int VC = 16 / sizeof(TC);              // elements per 16 bytes
+  constexpr int RCH = BN / VC;                     // 16-byte chunks per row
+  for (int c = tid; c < BM * RCH; c += 256) {
+    const int r = c / RCH, cc = (c % RCH) * VC;
+    const int row = m0 + r, col = n0 + cc;
+    if (row >= N || col >= M) continue;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 raw = *reinterpret_cast<GAB_LDS const u32x4*>(sC + r * CP + cc);
+    const TC* ev = reinterpret_cast<const TC*>(&raw);
+    float v[VC], o[VC];
+#pragma unroll
+    for (int e = 0; e < VC; ++e) v[e] = Cvt<TC>::to_f(ev[e]);
+    TC* p = C + (size_t)row * ldc + col;
+    if (col + VC <= M && aligned16(p)) {
+      if (accumulate) {
+        load_vec<TC, VC>(p, o);
+#pragma unroll
+        for (int e = 0; e < VC; ++e) v[e] += o[e];
+      }
+      store_vec<TC, VC>(p, v);
+    } else {
+      for (int e = 0; e < VC && col + e < M; ++e)
+        p[e] = Cvt<TC>::from_f(v[e] + (accumulate ? Cvt<TC>::to_f(p[e]) : 0.f));
     }
+  }
 }
 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, typename TC>
