@@ -5,7 +5,10 @@
 //
 // Both are memory-bound (61 MB of Y written / dY read per layer); hipBLASLt
 // picks MT256x192 / MT128x64 kernels that reach ~2.5-2.9 TB/s on them
-// (tools/gemm_layouts.py).  This kernel is a plain LDS-tiled MFMA GEMM
+// (tools/gemm_layouts.py).  Measured: this kernel reaches 2.2 / 1.4 TB/s
+// (27.8 / 43.6 us vs hipBLASLt 22 / 21 us), so the model keeps hipBLASLt;
+// the op stays available (bit-identical results, beta=1 accumulation).
+// It is a plain LDS-tiled MFMA GEMM
 // (v_mfma_f32_32x32x16_bf16, fp32 accumulators) specialised for the two
 // shapes:
 //
@@ -201,163 +204,6 @@ __global__ __launch_bounds__(256) void gemm_abt_kernel(
   }
 }
 
-// Short-K variant (K <= 128, the forward Y = X W): each block owns BM rows of
-// A (staged once) and sweeps column tiles of Bt; B tile t+1 is loaded into
-// registers while tile t runs on the MFMAs, and tile t's output leaves
-// through an LDS staging tile with 16-byte row stores that overlap the next
-// tile's MFMAs.  2 blocks per CU (68 KB LDS each).
-template <int K, typename TC>
-__global__ __launch_bounds__(256, 2) void gemm_abt_shortk_kernel(
-    const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-    TC* __restrict__ C, int N, int M, int64_t lda, int64_t ldb, int64_t ldc,
-    int col_groups, int accumulate) {
-  constexpr int BM = 64, BN = 128;
-  constexpr int KP = K + 8;
-  constexpr int CH = K / 8;
-  constexpr int B_PT = BN * CH / 256;            // 16-byte chunks / thread
-  constexpr int CP = BN + 16 / (int)sizeof(TC);
-  constexpr int VC = 16 / sizeof(TC), RCH = BN / VC;
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  GAB_LDS __bf16* sA = (GAB_LDS __bf16*)smem_raw;          // [BM][KP]
-  GAB_LDS __bf16* sB = sA + BM * KP;                       // [BN][KP]
-  GAB_LDS TC* sC = (GAB_LDS TC*)(sB + BN * KP);            // [BM][CP]
-
-  const int tid = threadIdx.x;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int bm = bid / col_groups, g = bid % col_groups;
-  const int m0 = bm * BM;
-  if (m0 >= N) return;
-  const int nbn = (M + BN - 1) / BN;
-
-  // A panel (once).
-  for (int c = tid; c < BM * CH; c += 256) {
-    const int r = c / CH, kk = (c % CH) * 8;
-    gab_bf16x8 v = {};
-    if (m0 + r < N)
-      v = *reinterpret_cast<const gab_bf16x8*>(A + (size_t)(m0 + r) * lda + kk);
-    *reinterpret_cast<GAB_LDS gab_bf16x8*>(sA + r * KP + kk) = v;
-  }
-  gab_bf16x8 rb[B_PT];
-  auto load_b = [&](int t) __attribute__((always_inline)) {
-    const int n0 = t * BN;
-#pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int c = tid + i * 256;
-      const int r = c / CH, kk = (c % CH) * 8;
-      gab_bf16x8 v = {};
-      if (n0 + r < M)
-        v = *reinterpret_cast<const gab_bf16x8*>(Bt + (size_t)(n0 + r) * ldb +
-                                                 kk);
-      rb[i] = v;
-    }
-  };
-  auto store_b = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < B_PT; ++i) {
-      const int c = tid + i * 256;
-      *reinterpret_cast<GAB_LDS gab_bf16x8*>(sB + (c / CH) * KP +
-                                             (c % CH) * 8) = rb[i];
-    }
-  };
-
-  const int wave = tid / 64, lane = tid % 64;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 64;   // 32 x 64 / wave
-  const int lr = lane & 31, lh = lane >> 5;
-
-  int t = g;
-  if (t < nbn) load_b(t);
-  __syncthreads();                     // A panel visible
-  for (; t < nbn; t += col_groups) {
-    store_b();                         // B(t): regs -> LDS
-    __syncthreads();
-    const int tn = t + col_groups;
-    if (tn < nbn) load_b(tn);          // in flight during the MFMAs
-    gab_f32x16 acc[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-    GAB_LDS const __bf16* a0 = sA + (wm + lr) * KP + 8 * lh;
-    GAB_LDS const __bf16* b0 = sB + (wn + lr) * KP + 8 * lh;
-#pragma unroll
-    for (int s = 0; s < K / 16; ++s) {
-      const gab_bf16x8 af =
-          *reinterpret_cast<GAB_LDS const gab_bf16x8*>(a0 + 16 * s);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const gab_bf16x8 bf = *reinterpret_cast<GAB_LDS const gab_bf16x8*>(
-            b0 + j * 32 * KP + 16 * s);
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf, af, acc[j], 0,
-                                                         0, 0);
-      }
-    }
-    // Swapped operands: lane = C row, registers 4g..4g+3 = 4 columns.
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        TC pk[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) pk[e] = Cvt<TC>::from_f(acc[j][4 * q + e]);
-        GAB_LDS TC* dst = sC + (wm + lr) * CP + wn + j * 32 + 8 * q + 4 * lh;
-        if constexpr (sizeof(TC) == 2)
-          *reinterpret_cast<GAB_LDS u32x2*>(dst) =
-              *reinterpret_cast<const u32x2*>(pk);
-        else
-          *reinterpret_cast<GAB_LDS u32x4*>(dst) =
-              *reinterpret_cast<const u32x4*>(pk);
-      }
-    __syncthreads();                   // C tile complete; sB free
-    const int n0 = t * BN;
-    for (int c = tid; c < BM * RCH; c += 256) {
-      const int r = c / RCH, cc = (c % RCH) * VC;
-      const int row = m0 + r, col = n0 + cc;
-      if (row >= N || col >= M) continue;
-      const u32x4 raw =
-          *reinterpret_cast<GAB_LDS const u32x4*>(sC + r * CP + cc);
-      const TC* ev = reinterpret_cast<const TC*>(&raw);
-      TC* p = C + (size_t)row * ldc + col;
-      if (col + VC <= M && !accumulate) {
-        *reinterpret_cast<u32x4*>(p) = raw;
-      } else {
-        for (int e = 0; e < VC && col + e < M; ++e)
-          p[e] = Cvt<TC>::from_f(Cvt<TC>::to_f(ev[e]) +
-                                 (accumulate ? Cvt<TC>::to_f(p[e]) : 0.f));
-      }
-    }
-    // The next iteration's store_b + barrier orders sC reuse after these
-    // LDS reads (stores of sC happen after that barrier).
-  }
-}
-
-template <int K, typename TC>
-static void launch_shortk(const at::Tensor& A, const at::Tensor& Bt,
-                          at::Tensor& C, bool accumulate) {
-  const int N = A.size(0), M = Bt.size(0);
-  const size_t lds = (size_t)(64 + 128) * (K + 8) * 2 +
-                     (size_t)64 * (128 + 16 / sizeof(TC)) * sizeof(TC);
-  auto kern = gemm_abt_shortk_kernel<K, TC>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    DGMC_CHECK_HIP(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(kern),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
-  const int row_tiles = (N + 63) / 64, nbn = (M + 127) / 128;
-  // Enough column groups for ~2 blocks on each of the 256 CUs.
-  const int groups = std::max(1, std::min(nbn, (512 + row_tiles - 1) /
-                                                   row_tiles));
-  hipLaunchKernelGGL(kern, dim3(row_tiles * groups), dim3(256), lds, stream(),
-                     reinterpret_cast<const __bf16*>(A.data_ptr()),
-                     reinterpret_cast<const __bf16*>(Bt.data_ptr()),
-                     reinterpret_cast<TC*>(C.data_ptr()), N, M, A.stride(0),
-                     Bt.stride(0), C.stride(0), groups, accumulate ? 1 : 0);
-}
-
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, typename TC>
 static void launch_gab(const at::Tensor& A, const at::Tensor& Bt,
                        at::Tensor& C, bool accumulate) {
@@ -409,18 +255,7 @@ at::Tensor gemm_abt(const at::Tensor& A, const at::Tensor& Bt,
   if (N == 0 || M == 0) return C;
   const bool f32 = C.scalar_type() == at::kFloat;
   TORCH_CHECK(f32 || C.scalar_type() == at::kBFloat16, "gemm_abt: out dtype");
-  if (K == 128 || K == 64 || K == 32) {
-    // Short K (forward Y = X W): row panels sweeping column tiles.
-#define GAB_SHORTK(KK)                                               \
-  if (K == KK) {                                                     \
-    if (f32)                                                         \
-      launch_shortk<KK, float>(A, Bt, C, accumulate);                \
-    else                                                             \
-      launch_shortk<KK, __hip_bfloat16>(A, Bt, C, accumulate);       \
-  }
-    GAB_SHORTK(128) else GAB_SHORTK(64) else GAB_SHORTK(32)
-#undef GAB_SHORTK
-  } else if (K <= 128) {
+  if (K <= 128) {
     // Other short K: one K tile, 128 x 128 output tiles, one LDS buffer.
     if (f32)
       launch_gab<128, 128, 128, 64, 64, 1, float>(A, Bt, C, accumulate);

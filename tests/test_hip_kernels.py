@@ -471,3 +471,17 @@ def test_gather_gemm_fused_forward_backward(K, C, S, monkeypatch):
     assert close(gx, rx, 3e-2)
     assert close(gw, rw, 3e-2)
     assert close(gb, rb, 1e-2)
+
+
+@pytest.mark.parametrize('N,K,M', [(300, 128, 3328), (257, 3328, 128),
+                                   (64, 64, 96), (100, 32, 130)])
+def test_gemm_abt(N, K, M):
+    ops = _backend.ops()
+    a = torch.randn(N, K, device=DEV).bfloat16()
+    bt = torch.randn(M, K, device=DEV).bfloat16()
+    ref_ = a.float() @ bt.float().t()
+    out = ops.gemm_abt(a, bt)
+    assert torch.allclose(out.float(), ref_, atol=0.1, rtol=1e-2)
+    acc = torch.ones(N, M, device=DEV)
+    ops.gemm_abt(a, bt, acc, True)
+    assert torch.allclose(acc, ref_ + 1, atol=0.1, rtol=1e-2)
