@@ -26,6 +26,10 @@
 namespace dgmc {
 
 constexpr int kWave = 64;
+
+// LDS-typed pointers: generic pointers into shared memory compile to flat_*
+// accesses (vmcnt + lgkmcnt waits); address_space(3) gives ds_* ops.
+#define DGMC_LDS __attribute__((address_space(3)))
 constexpr int kNumXcd = 8;
 
 inline hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }

@@ -37,7 +37,6 @@ namespace dgmc {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
-#define DGMC_LDS __attribute__((address_space(3)))
 
 constexpr int kGG_BM = 64;              // destination rows per block
 constexpr int kGG_BN = 128;             // output columns per block

@@ -46,7 +46,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
     const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out);
 
-at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k);
+at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
+                    bool exact);
 
 at::Tensor sddmm(const at::Tensor& rowptr, const at::Tensor& col,
                  const at::Tensor& A, const at::Tensor& B);
@@ -111,7 +112,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
       "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None) -> (Tensor, "
       "Tensor, Tensor, Tensor)");
-  m.def("topk_dot(Tensor h_s, Tensor h_t, int k) -> Tensor");
+  m.def("topk_dot(Tensor h_s, Tensor h_t, int k, bool exact=False) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
       "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype, "

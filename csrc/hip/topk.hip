@@ -27,7 +27,7 @@ constexpr int kSPitch = 65;
 template <int CT>
 __global__ __launch_bounds__(256) void topk_dot_kernel(
     const float* __restrict__ h_s, const float* __restrict__ h_t,
-    int64_t* __restrict__ out, int Ns, int Nt, int C, int k) {
+    int64_t* __restrict__ out, int Ns, int Nt, int C, int k, int dbg) {
   constexpr int CP = CT * 64;          // padded channel count
   constexpr int P = CP + 4;            // LDS row pitch (floats)
   constexpr int F4_ROW = CP / 4;       // float4 per padded row
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll 4
-    for (int s = 0; s < CP / 8; ++s) {
+    for (int s = 0; s < ((dbg & 2) ? 0 : CP / 8); ++s) {
       const float4 a = *reinterpret_cast<const float4*>(aRow + 8 * s);
       const float4 bb = *reinterpret_cast<const float4*>(bRow + 8 * s);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bb.x, acc, 0, 0, 0);
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
     if (t + 1 < ntiles) store_tile(sB, pre);
 
     const int j = t * kTile + lane;
-    const bool col_ok = j < Nt;
+    const bool col_ok = j < Nt && !(dbg & 1);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int row = wave * 16 + q;
@@ -141,7 +141,302 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
   }
 }
 
-at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k) {
+
+// ---------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") variant.  Each fp32 operand is split as x = hi + lo
+// with hi = bf16(x), lo = bf16(x - hi) (16 mantissa bits together) and the
+// score is accumulated in fp32 as hi_s.hi_t + hi_s.lo_t + lo_s.hi_t on
+// v_mfma_f32_32x32x16_bf16 - 3 MFMA passes at 16x the f32-MFMA rate, i.e.
+// ~5x fewer matrix-core cycles than exact f32, with score errors ~2^-16
+// relative (only exact near-ties can order differently from fp32).
+//
+// Layout: a workgroup of 4 waves owns 128 source rows; every wave keeps the
+// hi/lo A fragments of its 32 rows in registers for the whole kernel (128
+// VGPRs at C=256), so only the 32-target B tiles stream through LDS (double
+// buffered, one barrier per tile, next tile prefetched into registers during
+// the MFMAs).  Two workgroups fit per CU (67.6 KB LDS, <=256 VGPRs), so one
+// block's selection overlaps the other's MFMAs.  The 32x32 accumulator is
+// used in place for selection: acc[r] of lanes 0..31 is source row
+// R(r) = (r&3)+8(r>>2) over the 32 targets of the tile, lanes 32..63 hold row
+// R(r)+4, so each half-wave keeps the top-k list of one row in lanes
+// 0..k-1 of that half (k <= 32) and candidates are filtered with one
+// compare against the half's k-th value (read with v_readlane).
+// The target range can be split over gridDim.y blocks (to fill 256 CUs when
+// N_s is small); per-split lists are then merged by topk_merge_kernel.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kX3Rows = 128;   // source rows per workgroup (4 waves x 32)
+constexpr int kX3Tile = 32;    // targets per streamed tile
+
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ int shr1(int v) {   // v of lane - 1 (DPP)
+  return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float shr1(float v) {
+  return __int_as_float(shr1(__float_as_int(v)));
+}
+
+template <int NKS>
+__global__ __launch_bounds__(256, 2) void topk_x3_kernel(
+    const float* __restrict__ h_s, const float* __restrict__ h_t,
+    float* __restrict__ part_v, int* __restrict__ part_i,
+    int64_t* __restrict__ out, int Ns, int Nt, int C, int k, int span,
+    int dbg) {
+  constexpr int CP = NKS * 16;              // padded channels
+  constexpr int BP = CP + 8;                // LDS row pitch (bf16)
+  constexpr int TILE = kX3Tile * BP;        // one hi or lo tile (bf16)
+  constexpr int F4_ROW = CP / 4;
+  constexpr int PRE = kX3Tile * F4_ROW / 256;   // float4 per thread per tile
+  static_assert(PRE >= 1 && kX3Tile * F4_ROW % 256 == 0, "tile split");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS __bf16* sB = (DGMC_LDS __bf16*)smem_raw;   // [2 buf][hi, lo][TILE]
+
+  const int b = blockIdx.z, split = blockIdx.y;
+  const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
+  const int h = lane >> 5, hl = lane & 31, hb = lane & 32;
+  const int row0 = blockIdx.x * kX3Rows + wave * 32;
+  const int j_begin = split * span;
+  const int j_end = min(Nt, j_begin + span);
+  const float* hs = h_s + (size_t)b * Ns * C;
+  const float* ht = h_t + (size_t)b * Nt * C;
+
+  // A fragments (this wave's 32 source rows), split once.
+  bf16x8 ahi[NKS], alo[NKS];
+  {
+    const int r = row0 + hl;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = ks * 16 + 8 * h + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < Ns && c < C)
+          v = *reinterpret_cast<const float4*>(hs + (size_t)r * C + c);
+        const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const __bf16 hi = (__bf16)f[e];
+          ahi[ks][4 * q + e] = hi;
+          alo[ks][4 * q + e] = (__bf16)(f[e] - (float)hi);
+        }
+      }
+    }
+  }
+
+  auto load_tile = [&](int j0, float4* regs) {
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+      const int f = tid + 256 * u;
+      const int r = f / F4_ROW, c = (f % F4_ROW) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j0 + r < j_end && c < C)
+        v = *reinterpret_cast<const float4*>(ht + (size_t)(j0 + r) * C + c);
+      regs[u] = v;
+    }
+  };
+  auto store_tile = [&](int buf, const float4* regs) {
+    DGMC_LDS __bf16* hi_t = sB + buf * 2 * TILE;
+    DGMC_LDS __bf16* lo_t = hi_t + TILE;
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+      const int f = tid + 256 * u;
+      const int r = f / F4_ROW, c = (f % F4_ROW) * 4;
+      const float x[4] = {regs[u].x, regs[u].y, regs[u].z, regs[u].w};
+      bf16x4 vh, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __bf16 hi = (__bf16)x[e];
+        vh[e] = hi;
+        vl[e] = (__bf16)(x[e] - (float)hi);
+      }
+      *reinterpret_cast<DGMC_LDS bf16x4*>(hi_t + r * BP + c) = vh;
+      *reinterpret_cast<DGMC_LDS bf16x4*>(lo_t + r * BP + c) = vl;
+    }
+  };
+
+  float lv[16];
+  int li[16];
+  const int init_i = part_v ? Nt + split * 64 + hl : 0;   // unique sentinels
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { lv[r] = -INFINITY; li[r] = init_i; }
+
+  const int ntiles = (j_end - j_begin + kX3Tile - 1) / kX3Tile;
+  float4 pre[PRE];
+  if (ntiles > 0) {
+    load_tile(j_begin, pre);
+    store_tile(0, pre);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int j0 = j_begin + t * kX3Tile;
+    if (t + 1 < ntiles) load_tile(j0 + kX3Tile, pre);
+    const DGMC_LDS __bf16* bh = sB + (t & 1) * 2 * TILE + hl * BP + 8 * h;
+    const DGMC_LDS __bf16* bl = bh + TILE;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if (!(dbg & 2)) {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 vh = *reinterpret_cast<const DGMC_LDS bf16x8*>(bh + 16 * ks);
+        const bf16x8 vl = *reinterpret_cast<const DGMC_LDS bf16x8*>(bl + 16 * ks);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[ks], vh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ks], vl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ks], vh, acc, 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntiles) store_tile((t + 1) & 1, pre);
+
+    const bool col_ok = j0 + hl < j_end && !(dbg & 1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = col_ok ? acc[r] : -INFINITY;
+      const float thr = hb ? lane_f(lv[r], 32 + k - 1) : lane_f(lv[r], k - 1);
+      unsigned long long mask = __ballot(v > thr);
+      while (mask) {
+        const int src = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const int sh = src & 32;
+        const float cv = lane_f(v, src);
+        if (!(cv > lane_f(lv[r], sh + k - 1))) continue;
+        const bool mine = hb == sh && hl < k;
+        const int pos = __popcll(__ballot(mine && lv[r] >= cv));
+        // shift the tail of the half's list down one lane (DPP wave_shr:1;
+        // lane hl > pos >= 0 always reads a lane of its own half)
+        const float pv = shr1(lv[r]);
+        const int pi = shr1(li[r]);
+        if (mine && hl > pos) { lv[r] = pv; li[r] = pi; }
+        if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + (src & 31); }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (hl < k) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (row >= Ns) continue;
+      const size_t g = (size_t)b * Ns + row;
+      if (part_v) {
+        const size_t o = (g * gridDim.y + split) * k + hl;
+        part_v[o] = lv[r];
+        part_i[o] = li[r];
+      } else {
+        out[g * k + hl] = (int64_t)li[r];
+      }
+    }
+  }
+}
+
+// Merge of per-split top-k lists: one thread per candidate computes its rank
+// among the row's S*k candidates (value desc, index asc) and scatters itself.
+__global__ __launch_bounds__(256) void topk_merge_kernel(
+    const float* __restrict__ part_v, const int* __restrict__ part_i,
+    int64_t* __restrict__ out, int64_t rows, int S, int k, int Nt) {
+  const int n = S * k;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = g / n;
+  if (row >= rows) return;
+  const float* v = part_v + row * n;
+  const int* ix = part_i + row * n;
+  const int c = (int)(g - row * n);
+  const float mv = v[c];
+  const int mj = ix[c];
+  int rank = 0;
+  for (int e = 0; e < n; ++e) {
+    const float ov = v[e];
+    const int oj = ix[e];
+    rank += (ov > mv) || (ov == mv && oj < mj);
+  }
+  if (rank < k) out[row * k + rank] = mj < Nt ? mj : 0;
+}
+
+static int topk_debug() {  // DGMC_TOPK_DEBUG: 1 skip selection, 2 skip MFMA
+  static int v = [] {
+    const char* e = getenv("DGMC_TOPK_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// Target splits for the bf16x3 kernel: the smallest S whose blocks fill the
+// 2-blocks-per-CU slots of the chip to >= 85% (a partial last wave of blocks
+// idles CUs), keeping every split >= 2 tiles.
+static int x3_splits(int64_t row_blocks, int Nt) {
+  const int64_t slots = 2 * 256;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int S = 1; S <= 16; ++S) {
+    if (S > 1 && (int64_t)S * 2 * kX3Tile > Nt) break;
+    const int64_t blocks = row_blocks * S;
+    const double eff =
+        (double)blocks / (double)(slots * ((blocks + slots - 1) / slots));
+    if (eff >= 0.85) return S;
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = S; }
+  }
+  return best;
+}
+
+static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
+                              int64_t k) {
+  const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
+  const int Nt = h_t.size(1);
+  at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
+  if (B == 0 || Ns == 0) return out;
+  const int NKS = (C + 63) / 64 * 4;
+  const int CP = NKS * 16;
+  const size_t lds = (size_t)4 * kX3Tile * (CP + 8) * sizeof(__bf16);
+  const int row_blocks = (Ns + kX3Rows - 1) / kX3Rows;
+  int S = x3_splits((int64_t)row_blocks * B, Nt);
+  int span = (Nt + S - 1) / S;
+  span = (span + kX3Tile - 1) / kX3Tile * kX3Tile;
+  S = (Nt + span - 1) / span;
+  if (S > 1 && Nt - (S - 1) * span < (int)k) S = 1, span = Nt;  // tiny tails
+  at::Tensor pv, pi;
+  if (S > 1) {
+    pv = at::empty({(int64_t)B * Ns * S * k}, h_s.options());
+    pi = at::empty({(int64_t)B * Ns * S * k}, h_s.options().dtype(at::kInt));
+  }
+  dim3 grid(row_blocks, S, B);
+  auto launch = [&](auto kernel) {
+    DGMC_CHECK_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kernel, grid, dim3(256), lds, stream(),
+                       h_s.data_ptr<float>(), h_t.data_ptr<float>(),
+                       S > 1 ? pv.data_ptr<float>() : nullptr,
+                       S > 1 ? pi.data_ptr<int>() : nullptr,
+                       out.data_ptr<int64_t>(), Ns, Nt, C, (int)k, span,
+                       topk_debug());
+  };
+  switch (NKS) {
+    case 4: launch(topk_x3_kernel<4>); break;
+    case 8: launch(topk_x3_kernel<8>); break;
+    case 12: launch(topk_x3_kernel<12>); break;
+    default: launch(topk_x3_kernel<16>); break;
+  }
+  DGMC_CHECK_LAUNCH();
+  if (S > 1) {
+    const int64_t rows = (int64_t)B * Ns;
+    const int64_t n = rows * S * k;
+    hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)((n + 255) / 256)),
+                       dim3(256), 0, stream(), pv.data_ptr<float>(),
+                       pi.data_ptr<int>(), out.data_ptr<int64_t>(), rows, S,
+                       (int)k, Nt);
+    DGMC_CHECK_LAUNCH();
+  }
+  return out;
+}
+
+at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
+                    bool exact) {
   TORCH_CHECK(h_s.is_cuda() && h_t.is_cuda() && h_s.dim() == 3 &&
                   h_t.dim() == 3 && h_s.scalar_type() == at::kFloat &&
                   h_t.scalar_type() == at::kFloat && h_s.is_contiguous() &&
@@ -153,6 +448,7 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k) {
   TORCH_CHECK(h_t.size(0) == B && h_t.size(2) == C, "topk_dot: shape");
   TORCH_CHECK(k >= 1 && k <= 64 && k <= Nt, "topk_dot: need 1 <= k <= min(64, N_t)");
   TORCH_CHECK(C % 4 == 0 && C <= 256, "topk_dot: C % 4 == 0 and C <= 256");
+  if (!exact && k <= 32) return topk_dot_x3(h_s, h_t, k);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
   if (B == 0 || Ns == 0) return out;
   const int CT = (C + 63) / 64;
@@ -165,7 +461,8 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k) {
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kernel, grid, dim3(256), lds, stream(),
                        h_s.data_ptr<float>(), h_t.data_ptr<float>(),
-                       out.data_ptr<int64_t>(), Ns, Nt, C, (int)k);
+                       out.data_ptr<int64_t>(), Ns, Nt, C, (int)k,
+                       topk_debug());
   };
   switch (CT) {
     case 1: launch(topk_dot_kernel<1>); break;

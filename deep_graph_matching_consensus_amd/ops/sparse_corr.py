@@ -2,9 +2,11 @@
 
 * :func:`top_k`            - candidate search ``argtopk_j <h_s[b,i], h_t[b,j]>``
   (``dgmc.py:85-94``; KeOps ``argKmin`` in the reference).  On the GPU a fused
-  HIP kernel streams ``h_t`` tiles through LDS, computes the dot tiles with
-  exact-f32 MFMA and keeps a per-row register top-k, so the ``N_s x N_t``
-  score matrix is never materialised.
+  HIP kernel streams ``h_t`` tiles through LDS, computes the dot tiles on
+  MFMA and keeps a per-row register top-k, so the ``N_s x N_t`` score matrix
+  is never materialised.  Default scores use the split-bf16 ("bf16x3",
+  ~2^-16 relative) kernel; ``DGMC_AMD_TOPK_EXACT=1`` (or ``exact=True``)
+  selects the exact-f32 MFMA kernel.
 * :class:`CandidateGraph`  - the candidate set ``S_idx [B, N_s, k]`` as a CSR
   matrix over flattened source rows (global target columns ``b*N_t + idx``)
   plus its transpose, built once per forward.
@@ -20,6 +22,8 @@
 The reference quirks are kept: no masking of padded targets or rows in the
 sparse path (``dgmc.py:202,223``).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -28,13 +32,22 @@ from . import reference as ref
 from .sparse import SparseOperator
 
 
-def top_k(h_s, h_t, k):
-    """``[B, N_s, k]`` int64 indices of the k best targets per source row."""
+TOPK_EXACT = os.environ.get('DGMC_AMD_TOPK_EXACT', '0') == '1'
+
+
+def top_k(h_s, h_t, k, exact=None):
+    """``[B, N_s, k]`` int64 indices of the k best targets per source row.
+
+    ``exact`` (default ``DGMC_AMD_TOPK_EXACT``) selects exact-f32 scores on
+    the GPU; otherwise scores are split-bf16 (3 MFMA passes, ~2^-16
+    relative error - only near-exact ties can rank differently)."""
     B, N_s, C = h_s.shape
+    if exact is None:
+        exact = TOPK_EXACT
     if _backend.use_hip(h_s) and k <= 64 and C % 4 == 0 and C <= 256 \
             and h_s.dtype == torch.float32:
         return _backend.ops().topk_dot(h_s.contiguous(), h_t.contiguous(),
-                                       int(k))
+                                       int(k), bool(exact))
     return ref.top_k(h_s, h_t, k)
 
 
