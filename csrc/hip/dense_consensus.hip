@@ -1,7 +1,7 @@
 // Per-pair fused kernels of the dense DGMC consensus loop
 // (reference dgmc.py:161-183).  One workgroup (4 waves) per graph pair; the
-// padded pair tile (N_s, N_t <= 64) lives in LDS, masks are derived from the
-// per-pair node counts n_s[b], n_t[b] (valid nodes occupy the leading rows).
+// pair's node tiles live in LDS, masks are derived from the per-pair node
+// counts (valid nodes occupy the leading rows of the padded tile).
 //
 //   dense_masked_softmax      S = masked_softmax(S_hat)          (dgmc.py:15-19)
 //   dense_softmax_transport   S, r_t = S^T r_s                   (dgmc.py:168-171)
@@ -10,17 +10,25 @@
 // and their backward kernels.  The consensus backward recomputes relu(P-Q)
 // instead of storing the [B, N_s, N_t, R] activation the reference keeps.
 //
-// LDS tiles use a row pitch of 65 floats so that lanes reading different rows
-// of the same column (ds_read_b32, 32-bank groups) are conflict-free.
+// Latency design (MI355X): a pair is tiny (~9x9 nodes x 128 channels, a few
+// kFLOP), so these kernels are bound by dependent memory round trips, not by
+// bandwidth or ALU.  Every kernel therefore
+//   * issues ALL loads of its operand tiles before the first LDS store
+//     (`stage_rows`: up to 4 independent 16-byte loads per thread per batch,
+//     P and Q tiles in the same batch) - one round trip per tile set instead
+//     of one per row;
+//   * computes from LDS with several independent partial sums per thread
+//     (LDS latency overlapped), channel-parallel lanes (conflict-free rows) or
+//     4 lanes per (i, j) entry with strided channels (odd LDS pitch);
+//   * sizes LDS dynamically from the padded pair tile (Ns, Nt <= 64).
 #include "common.h"
 
 namespace dgmc {
 
 constexpr int kMaxN = 64;      // max padded nodes per graph of a pair
-constexpr int kPitch = 65;     // LDS row pitch (floats)
-constexpr int kCh = 64;        // channel chunk staged per pass
 constexpr int kWaves = 4;      // waves per workgroup
-constexpr int kRowsPerWave = kMaxN / kWaves;
+constexpr int kThreads = kWaves * kWave;
+constexpr int kPrefetch = 4;   // S/G tile entries prefetched per thread
 
 // Zero rows [row0, rows) of a packed [rows, R] tensor (padding rows of static
 // batches; executed by the last workgroup of a launch).
@@ -31,6 +39,92 @@ __device__ __forceinline__ void zero_tail(T* __restrict__ x, int row0,
   for (size_t e = begin + threadIdx.x; e < end; e += blockDim.x)
     x[e] = Cvt<T>::from_f(0.f);
 }
+
+// Stage rows [0, na) of the packed row block a[na, R] and rows [0, nb) of
+// b[nb, R] into LDS fp32 tiles dA / dB (row pitch `pitch`).  Each thread
+// issues up to 4 independent loads before its first LDS store, so both tiles
+// arrive in one memory round trip for pair-sized blocks.  `vec`: 16-byte
+// aligned rows (R * sizeof(T) % 16 == 0 and aligned bases).
+template <typename T>
+__device__ __forceinline__ void stage_rows(DGMC_LDS float* dA,
+                                           const T* __restrict__ a, int na,
+                                           DGMC_LDS float* dB,
+                                           const T* __restrict__ b, int nb,
+                                           int pitch, int R, bool vec) {
+  const int tid = threadIdx.x;
+  if (vec) {
+    constexpr int V = Vec16<T>::N;
+    const int vpr = R / V;
+    const int nva = na * vpr, nv = nva + nb * vpr;
+    for (int base = tid; base < nv; base += 4 * kThreads) {
+      float v[4][V];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = base + u * kThreads;
+        if (q < nv)
+          load_vec<T, V>(q < nva ? a + (size_t)q * V : b + (size_t)(q - nva) * V,
+                         v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = base + u * kThreads;
+        if (q < nv) {
+          const bool in_a = q < nva;
+          const int qq = in_a ? q : q - nva;
+          const int r = qq / vpr, c = (qq - r * vpr) * V;
+          DGMC_LDS float* d = (in_a ? dA : dB) + r * pitch + c;
+#pragma unroll
+          for (int k = 0; k < V; ++k) d[k] = v[u][k];
+        }
+      }
+    }
+  } else {
+    const int nea = na * R, ne = nea + nb * R;
+    for (int base = tid; base < ne; base += 4 * kThreads) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = base + u * kThreads;
+        v[u] = q < ne ? Cvt<T>::to_f(q < nea ? a[q] : b[q - nea]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = base + u * kThreads;
+        if (q < ne) {
+          const bool in_a = q < nea;
+          const int qq = in_a ? q : q - nea;
+          (in_a ? dA : dB)[(qq / R) * pitch + qq % R] = v[u];
+        }
+      }
+    }
+  }
+}
+
+// Prefetch the first kPrefetch * kThreads entries of a pair's fp32 [Ns, Nt]
+// tile into registers (issued before the operand staging, consumed after).
+__device__ __forceinline__ void prefetch_tile(const float* __restrict__ t,
+                                              int NN, float (&v)[kPrefetch]) {
+#pragma unroll
+  for (int u = 0; u < kPrefetch; ++u) {
+    const int e = threadIdx.x + u * kThreads;
+    v[u] = e < NN ? t[e] : 0.f;
+  }
+}
+
+// Channel mapping shared by the channel-parallel loops: chunk of up to
+// kThreads channels; RP row groups when R < kThreads.
+struct ChanMap {
+  int cw, rp, c, r0;
+  bool active;
+  __device__ __forceinline__ ChanMap(int c0, int R) {
+    cw = min(kThreads, R - c0);
+    rp = kThreads / cw;
+    const int tid = threadIdx.x;
+    active = tid < rp * cw;
+    c = c0 + tid % cw;
+    r0 = tid / cw;
+  }
+};
 
 // ---------------------------------------------------------------------------
 // Row-wise masked softmax (+ backward).  One wave per (b, i) row.
@@ -74,122 +168,158 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
 
 // ---------------------------------------------------------------------------
 // Softmax + transport:  S = masked_softmax(S_hat[b]);  r_t[b] = S^T r_s[b].
+// LDS: sR [Ns][R] (r_s, fp32), sS [Ns][Nt] (S_hat, then S).
 // ---------------------------------------------------------------------------
 template <typename TR>
 __global__ __launch_bounds__(256) void softmax_transport_kernel(
     const float* __restrict__ S_hat, const TR* __restrict__ r_s,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     float* __restrict__ S, TR* __restrict__ r_t, int Ns, int Nt, int R,
-    int rows_t, TR* __restrict__ r_s_copy, int rows_s) {
-  __shared__ float sS[kMaxN * kPitch];
-  __shared__ float sR[kMaxN * kPitch];
+    int rows_t, TR* __restrict__ r_s_copy, int rows_s, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sS = sR + Ns * R;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sh = S_hat + (size_t)b * NN;
+  float pre[kPrefetch];
+  prefetch_tile(Sh, NN, pre);
+  stage_rows<TR>(sR, r_s + (size_t)s0 * R, ns, sR, r_s, 0, R, R, vec != 0);
+#pragma unroll
+  for (int u = 0; u < kPrefetch; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < NN) sS[e] = pre[u];
+  }
+  for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) sS[e] = Sh[e];
   if (blockIdx.x == gridDim.x - 1) zero_tail(r_t, ptr_t[gridDim.x], rows_t, R);
   if (r_s_copy) {
     // r_s rows past the last pair (static-batch padding), spread over the
-    // whole grid: one element per thread instead of a serial loop in one
-    // block (which put ~60 us on the kernel's critical path).
+    // whole grid: one element per thread.
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t e = (size_t)ptr_s[gridDim.x] * R +
-                    (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+                    (size_t)blockIdx.x * blockDim.x + tid;
          e < (size_t)rows_s * R; e += stride)
       r_s_copy[e] = r_s[e];
   }
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
-  const float* Sh = S_hat + (size_t)b * Ns * Nt;
-  float* Sb = S + (size_t)b * Ns * Nt;
+  __syncthreads();
 
+  float* Sb = S + (size_t)b * NN;
   for (int i = wave; i < Ns; i += kWaves) {
     const bool valid = i < ns && lane < nt;
-    const float v = valid ? Sh[i * Nt + lane] : -INFINITY;
+    const float v = valid ? sS[i * Nt + lane] : -INFINITY;
     const float m = wave_max(v);
     const float e = valid ? __expf(v - m) : 0.f;
     const float s = wave_sum(e);
     const float p = valid ? e / s : 0.f;
     if (lane < Nt) {
-      sS[i * kPitch + lane] = p;
+      sS[i * Nt + lane] = p;
       Sb[i * Nt + lane] = p;
     }
   }
+  if (r_s_copy) {
+    // Joint output [r_s; r_t]: psi_2's input without a concatenation
+    // (bf16/fp32 -> fp32 -> same type is exact).
+    TR* dst = r_s_copy + (size_t)s0 * R;
+    for (int e = tid; e < ns * R; e += kThreads)
+      dst[e] = Cvt<TR>::from_f(sR[e]);
+  }
+  __syncthreads();
 
-  const TR* rs = r_s + (size_t)ptr_s[b] * R;
-  TR* rt = r_t + (size_t)ptr_t[b] * R;
-  for (int c0 = 0; c0 < R; c0 += kCh) {
-    const int c = c0 + lane;
-    __syncthreads();
-    for (int i = wave; i < ns; i += kWaves) {
-      const TR v = c < R ? rs[(size_t)i * R + c] : Cvt<TR>::from_f(0.f);
-      sR[i * kPitch + lane] = Cvt<TR>::to_f(v);
-      // Joint output [r_s; r_t]: psi_2's input without a concatenation.
-      if (r_s_copy && c < R) r_s_copy[(size_t)(ptr_s[b] + i) * R + c] = v;
-    }
-    __syncthreads();
-    for (int j = wave; j < nt; j += kWaves) {
-      float acc = 0.f;
-      for (int i = 0; i < ns; ++i)
-        acc = fmaf(sS[i * kPitch + j], sR[i * kPitch + lane], acc);
-      if (c < R) rt[(size_t)j * R + c] = Cvt<TR>::from_f(acc);
+  TR* rt = r_t + (size_t)t0 * R;
+  for (int c0 = 0; c0 < R; c0 += kThreads) {
+    const ChanMap cm(c0, R);
+    if (!cm.active) continue;
+    for (int j = cm.r0; j < nt; j += cm.rp) {
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      int i = 0;
+      for (; i + 4 <= ns; i += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          a[u] = fmaf(sS[(i + u) * Nt + j], sR[(i + u) * R + cm.c], a[u]);
+      }
+      for (; i < ns; ++i) a[0] = fmaf(sS[i * Nt + j], sR[i * R + cm.c], a[0]);
+      rt[(size_t)j * R + cm.c] = Cvt<TR>::from_f((a[0] + a[1]) + (a[2] + a[3]));
     }
   }
 }
 
 // dS_hat = softmax_bwd(S, dS),  dS[i][j] = sum_c r_s[i][c] * g[j][c].
+// LDS: sR [Ns][R+1], sG [Nt][R+1], sD [Ns][Nt].
 template <typename TR>
 __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
     const float* __restrict__ S, const TR* __restrict__ r_s,
     const TR* __restrict__ g, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, float* __restrict__ dS_hat, int Ns,
-    int Nt, int R) {
-  __shared__ float sR[kMaxN * kPitch];
-  __shared__ float sG[kMaxN * kPitch];
+    int Nt, int R, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int pitch = R + 1;
+  DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sG = sR + Ns * pitch;
+  DGMC_LDS float* sD = sG + Nt * pitch;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
-  const TR* rs = r_s + (size_t)ptr_s[b] * R;
-  const TR* gb = g + (size_t)ptr_t[b] * R;
-
-  float acc[kRowsPerWave];
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sb = S + (size_t)b * NN;
+  // S rows of this wave (i = wave + kWaves * q), fetched up front.
+  constexpr int QMAX = kMaxN / kWaves;
+  float sv[QMAX];
 #pragma unroll
-  for (int q = 0; q < kRowsPerWave; ++q) acc[q] = 0.f;
-
-  for (int c0 = 0; c0 < R; c0 += kCh) {
-    const int c = c0 + lane;
-    __syncthreads();
-    for (int i = wave; i < ns; i += kWaves)
-      sR[i * kPitch + lane] = c < R ? Cvt<TR>::to_f(rs[(size_t)i * R + c]) : 0.f;
-    for (int j = wave; j < nt; j += kWaves)
-      sG[j * kPitch + lane] = c < R ? Cvt<TR>::to_f(gb[(size_t)j * R + c]) : 0.f;
-    __syncthreads();
-    const int cmax = min(kCh, R - c0);
-    if (lane < nt) {
-#pragma unroll
-      for (int q = 0; q < kRowsPerWave; ++q) {
-        const int i = wave + q * kWaves;
-        if (i < ns) {
-          float a = acc[q];
-          for (int cc = 0; cc < cmax; ++cc)
-            a = fmaf(sR[i * kPitch + cc], sG[lane * kPitch + cc], a);
-          acc[q] = a;
-        }
-      }
-    }
+  for (int q = 0; q < QMAX; ++q) {
+    const int i = wave + q * kWaves;
+    sv[q] = (i < Ns && lane < Nt) ? Sb[i * Nt + lane] : 0.f;
   }
-  const float* Sb = S + (size_t)b * Ns * Nt;
-  float* out = dS_hat + (size_t)b * Ns * Nt;
+  stage_rows<TR>(sR, r_s + (size_t)s0 * R, ns, sG, g + (size_t)t0 * R, nt,
+                 pitch, R, vec != 0);
+  __syncthreads();
+
+  // dS[i][j]: 4 lanes per entry, channels strided by 4.
+  const int qd = tid & 3;
+  const int pairs = ns * nt;
+  for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
+    const int p = p0 + (tid >> 2);
+    const bool valid = p < pairs;
+    const int i = valid ? p / nt : 0;
+    const int j = valid ? p - i * nt : 0;
+    const DGMC_LDS float* rr = sR + i * pitch;
+    const DGMC_LDS float* gr = sG + j * pitch;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int c = qd;
+    for (; c + 12 < R; c += 16) {
 #pragma unroll
-  for (int q = 0; q < kRowsPerWave; ++q) {
+      for (int u = 0; u < 4; ++u)
+        a[u] = fmaf(rr[c + 4 * u], gr[c + 4 * u], a[u]);
+    }
+    for (; c < R; c += 4) a[0] = fmaf(rr[c], gr[c], a[0]);
+    float acc = (a[0] + a[1]) + (a[2] + a[3]);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (valid && qd == 0) sD[i * Nt + j] = acc;
+  }
+  __syncthreads();
+
+  float* out = dS_hat + (size_t)b * NN;
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
     const int i = wave + q * kWaves;
     if (i < Ns) {
-      const float s = lane < Nt ? Sb[i * Nt + lane] : 0.f;
-      const float dot = wave_sum(s * acc[q]);
-      if (lane < Nt) out[i * Nt + lane] = s * (acc[q] - dot);
+      const float d = (i < ns && lane < nt) ? sD[i * Nt + lane] : 0.f;
+      const float dot = wave_sum(sv[q] * d);
+      if (lane < Nt) out[i * Nt + lane] = sv[q] * (d - dot);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Consensus update: out = S_hat + mask * (sum_c relu(P_ic - Q_jc) w2_c + b2)
+// Consensus update: out = S_hat + mask * (sum_c relu(P_ic + b1_c - Q_jc) w2_c
+//                                         + b2)
+// LDS: sP [Ns][R+1], sQ [Nt][R+1], sB [R] (b1), sW [R] (w2).
 // ---------------------------------------------------------------------------
 template <typename TPQ>
 __global__ __launch_bounds__(256) void consensus_fwd_kernel(
@@ -197,61 +327,79 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
     const TPQ* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
-    float* __restrict__ out, int Ns, int Nt, int R) {
-  __shared__ float sP[kMaxN * kPitch];
-  __shared__ float sQ[kMaxN * kPitch];
-  __shared__ float sW[kCh];
+    float* __restrict__ out, int Ns, int Nt, int R, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int pitch = R + 1;
+  DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sQ = sP + Ns * pitch;
+  DGMC_LDS float* sB = sQ + Nt * pitch;
+  DGMC_LDS float* sW = sB + R;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
-  const TPQ* Pb = P + (size_t)ptr_s[b] * R;
-  const TPQ* Qb = Q + (size_t)ptr_t[b] * R;
+  const int tid = threadIdx.x;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sh = S_hat + (size_t)b * NN;
+  float* ob = out + (size_t)b * NN;
+  float bw[2] = {0.f, 0.f};
+  if (tid < R) {
+    bw[0] = b1[tid];
+    bw[1] = w2[tid];
+  }
+  stage_rows<TPQ>(sP, P + (size_t)s0 * R, ns, sQ, Q + (size_t)t0 * R, nt,
+                  pitch, R, vec != 0);
+  if (tid < R) {
+    sB[tid] = bw[0];
+    sW[tid] = bw[1];
+  }
+  for (int c = tid + kThreads; c < R; c += kThreads) {
+    sB[c] = b1[c];
+    sW[c] = w2[c];
+  }
+  // Entries outside the valid ns x nt block pass S_hat through unchanged.
+  for (int e = tid; e < NN; e += kThreads) {
+    const int i = e / Nt, j = e - (e / Nt) * Nt;
+    if (i >= ns || j >= nt) ob[e] = Sh[e];
+  }
+  const float bias2 = b2[0];
+  __syncthreads();
 
-  float acc[kRowsPerWave];
+  // 4 lanes per (i, j) entry, channels strided by 4 (odd pitch: the rows of
+  // neighbouring entries fall on different banks).
+  const int qd = tid & 3;
+  const int pairs = ns * nt;
+  for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
+    const int p = p0 + (tid >> 2);
+    const bool valid = p < pairs;
+    const int i = valid ? p / nt : 0;
+    const int j = valid ? p - i * nt : 0;
+    const float sh = (valid && qd == 0) ? Sh[i * Nt + j] : 0.f;
+    const DGMC_LDS float* pr = sP + i * pitch;
+    const DGMC_LDS float* qr = sQ + j * pitch;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int c = qd;
+    for (; c + 12 < R; c += 16) {
 #pragma unroll
-  for (int q = 0; q < kRowsPerWave; ++q) acc[q] = 0.f;
-
-  for (int c0 = 0; c0 < R; c0 += kCh) {
-    const int c = c0 + lane;
-    __syncthreads();
-    const float bias1 = c < R ? b1[c] : 0.f;
-    for (int i = wave; i < ns; i += kWaves)
-      sP[i * kPitch + lane] =
-          c < R ? Cvt<TPQ>::to_f(Pb[(size_t)i * R + c]) + bias1 : 0.f;
-    for (int j = wave; j < nt; j += kWaves)
-      sQ[j * kPitch + lane] =
-          c < R ? Cvt<TPQ>::to_f(Qb[(size_t)j * R + c]) : 0.f;
-    if (wave == 0) sW[lane] = c < R ? w2[c] : 0.f;
-    __syncthreads();
-    const int cmax = min(kCh, R - c0);
-    if (lane < nt) {
-#pragma unroll
-      for (int q = 0; q < kRowsPerWave; ++q) {
-        const int i = wave + q * kWaves;
-        if (i < ns) {
-          float a = acc[q];
-          for (int cc = 0; cc < cmax; ++cc) {
-            const float z = sP[i * kPitch + cc] - sQ[lane * kPitch + cc];
-            a = fmaf(fmaxf(z, 0.f), sW[cc], a);
-          }
-          acc[q] = a;
-        }
+      for (int u = 0; u < 4; ++u) {
+        const int cc = c + 4 * u;
+        a[u] = fmaf(fmaxf(pr[cc] + sB[cc] - qr[cc], 0.f), sW[cc], a[u]);
       }
     }
-  }
-  const float bias = b2[0];
-  const float* Sb = S_hat + (size_t)b * Ns * Nt;
-  float* ob = out + (size_t)b * Ns * Nt;
-#pragma unroll
-  for (int q = 0; q < kRowsPerWave; ++q) {
-    const int i = wave + q * kWaves;
-    if (i < Ns && lane < Nt) {
-      const bool valid = i < ns && lane < nt;
-      ob[i * Nt + lane] = Sb[i * Nt + lane] + (valid ? acc[q] + bias : 0.f);
-    }
+    for (; c < R; c += 4)
+      a[0] = fmaf(fmaxf(pr[c] + sB[c] - qr[c], 0.f), sW[c], a[0]);
+    float acc = (a[0] + a[1]) + (a[2] + a[3]);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (valid && qd == 0) ob[i * Nt + j] = sh + acc + bias2;
   }
 }
 
+// dP[i][c]  =  w2_c * sum_j G_ij [P_ic + b1_c > Q_jc]
+// dQ[j][c]  = -w2_c * sum_i G_ij [P_ic + b1_c > Q_jc]
+// dw2[c]    =  sum_ij G_ij relu(P_ic + b1_c - Q_jc)    (per-pair partial)
+// db2       =  sum_ij G_ij                             (per-pair partial)
+// LDS: sP [Ns][R], sQ [Nt][R] (lanes run along channels: conflict-free),
+//      sG [Ns][Nt], sB [R], sW [R], sRed [kThreads].
 template <typename TPQ>
 __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     const float* __restrict__ G, const TPQ* __restrict__ P,
@@ -260,102 +408,124 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     const int* __restrict__ ptr_t, TPQ* __restrict__ dP,
     TPQ* __restrict__ dQ, float* __restrict__ dw2_part,
     float* __restrict__ db2_part, int Ns, int Nt, int R, int rows_s,
-    int rows_t) {
-  __shared__ float sG[kMaxN * kPitch];
-  __shared__ float sP[kMaxN * kPitch];
-  __shared__ float sQ[kMaxN * kPitch];
-  __shared__ float sRed[kWaves * kCh];
+    int rows_t, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sQ = sP + Ns * R;
+  DGMC_LDS float* sG = sQ + Nt * R;
+  DGMC_LDS float* sB = sG + Ns * Nt;
+  DGMC_LDS float* sW = sB + R;
+  DGMC_LDS float* sRed = sW + R;
   const int b = xcd_remap(blockIdx.x, gridDim.x);
-  if (blockIdx.x == gridDim.x - 1) {
-    zero_tail(dP, ptr_s[gridDim.x], rows_s, R);
-    zero_tail(dQ, ptr_t[gridDim.x], rows_t, R);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Gb = G + (size_t)b * NN;
+  float pre[kPrefetch];
+  prefetch_tile(Gb, NN, pre);
+  float bw[2] = {0.f, 0.f};
+  if (tid < R) {
+    bw[0] = b1[tid];
+    bw[1] = w2[tid];
   }
-  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int ns = ptr_s[b + 1] - ptr_s[b], nt = ptr_t[b + 1] - ptr_t[b];
-  const float* Gb = G + (size_t)b * Ns * Nt;
-  const TPQ* Pb = P + (size_t)ptr_s[b] * R;
-  const TPQ* Qb = Q + (size_t)ptr_t[b] * R;
-  TPQ* dPb = dP + (size_t)ptr_s[b] * R;
-  TPQ* dQb = dQ + (size_t)ptr_t[b] * R;
-
+  stage_rows<TPQ>(sP, P + (size_t)s0 * R, ns, sQ, Q + (size_t)t0 * R, nt, R,
+                  R, vec != 0);
+  if (tid < R) {
+    sB[tid] = bw[0];
+    sW[tid] = bw[1];
+  }
+  for (int c = tid + kThreads; c < R; c += kThreads) {
+    sB[c] = b1[c];
+    sW[c] = w2[c];
+  }
   // Masked upstream gradient tile + db2 partial.
   float gsum = 0.f;
-  for (int i = wave; i < ns; i += kWaves) {
-    const float v = lane < nt ? Gb[i * Nt + lane] : 0.f;
-    sG[i * kPitch + lane] = v;
+#pragma unroll
+  for (int u = 0; u < kPrefetch; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < NN) {
+      const int i = e / Nt, j = e - (e / Nt) * Nt;
+      const float v = (i < ns && j < nt) ? pre[u] : 0.f;
+      sG[e] = v;
+      gsum += v;
+    }
+  }
+  for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) {
+    const int i = e / Nt, j = e - (e / Nt) * Nt;
+    const float v = (i < ns && j < nt) ? Gb[e] : 0.f;
+    sG[e] = v;
     gsum += v;
   }
   gsum = wave_sum(gsum);
   if (lane == 0) sRed[wave] = gsum;
+  if (blockIdx.x == gridDim.x - 1) {
+    zero_tail(dP, ptr_s[gridDim.x], rows_s, R);
+    zero_tail(dQ, ptr_t[gridDim.x], rows_t, R);
+  }
   __syncthreads();
-  if (threadIdx.x == 0)
-    db2_part[b] = sRed[0] + sRed[1] + sRed[2] + sRed[3];
+  if (tid == 0) db2_part[b] = (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+  TPQ* dPb = dP + (size_t)s0 * R;
+  TPQ* dQb = dQ + (size_t)t0 * R;
 
-  for (int c0 = 0; c0 < R; c0 += kCh) {
-    const int c = c0 + lane;
-    const bool cv = c < R;
-    __syncthreads();
-    const float bias1 = cv ? b1[c] : 0.f;
-    for (int i = wave; i < ns; i += kWaves)
-      sP[i * kPitch + lane] =
-          cv ? Cvt<TPQ>::to_f(Pb[(size_t)i * R + c]) + bias1 : 0.f;
-    for (int j = wave; j < nt; j += kWaves)
-      sQ[j * kPitch + lane] = cv ? Cvt<TPQ>::to_f(Qb[(size_t)j * R + c]) : 0.f;
-    __syncthreads();
-    const float w = cv ? w2[c] : 0.f;
-
-    // dP[i][c] and dw2 partial: rows owned by this wave, lane = channel.
-    // Branch-free, 4 independent partial sums so the LDS reads of 4 j's are
-    // in flight together (the loop is LDS-latency bound otherwise).
+  for (int c0 = 0; c0 < R; c0 += kThreads) {
+    const ChanMap cm(c0, R);
+    const int c = cm.c;
+    __syncthreads();   // sRed reuse
     float dw = 0.f;
-    for (int i = wave; i < ns; i += kWaves) {
-      const float p = sP[i * kPitch + lane];
-      float dp[4] = {0.f, 0.f, 0.f, 0.f}, dwq[4] = {0.f, 0.f, 0.f, 0.f};
-      int j = 0;
-      for (; j + 4 <= nt; j += 4) {
+    if (cm.active) {
+      const float bias1 = sB[c], w = sW[c];
+      // dP rows i = r0, r0 + rp, ...; dw2 partial over the same rows.
+      for (int i = cm.r0; i < ns; i += cm.rp) {
+        const float p = sP[i * R + c] + bias1;
+        float dp[4] = {0.f, 0.f, 0.f, 0.f}, dwq[4] = {0.f, 0.f, 0.f, 0.f};
+        int j = 0;
+        for (; j + 4 <= nt; j += 4) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float z = fmaxf(p - sQ[(j + u) * kPitch + lane], 0.f);
-          const float gij = sG[i * kPitch + j + u];
-          dp[u] += z > 0.f ? gij : 0.f;
-          dwq[u] = fmaf(gij, z, dwq[u]);
+          for (int u = 0; u < 4; ++u) {
+            const float z = fmaxf(p - sQ[(j + u) * R + c], 0.f);
+            const float gij = sG[i * Nt + j + u];
+            dp[u] += z > 0.f ? gij : 0.f;
+            dwq[u] = fmaf(gij, z, dwq[u]);
+          }
         }
-      }
-      for (; j < nt; ++j) {
-        const float z = fmaxf(p - sQ[j * kPitch + lane], 0.f);
-        const float gij = sG[i * kPitch + j];
-        dp[0] += z > 0.f ? gij : 0.f;
-        dwq[0] = fmaf(gij, z, dwq[0]);
-      }
-      dw += (dwq[0] + dwq[1]) + (dwq[2] + dwq[3]);
-      if (cv)
+        for (; j < nt; ++j) {
+          const float z = fmaxf(p - sQ[j * R + c], 0.f);
+          const float gij = sG[i * Nt + j];
+          dp[0] += z > 0.f ? gij : 0.f;
+          dwq[0] = fmaf(gij, z, dwq[0]);
+        }
+        dw += (dwq[0] + dwq[1]) + (dwq[2] + dwq[3]);
         dPb[(size_t)i * R + c] =
             Cvt<TPQ>::from_f(((dp[0] + dp[1]) + (dp[2] + dp[3])) * w);
-    }
-    // dQ[j][c] = -w * sum_i G[i][j] [P_ic > Q_jc]
-    for (int j = wave; j < nt; j += kWaves) {
-      const float qv = sQ[j * kPitch + lane];
-      float dq[4] = {0.f, 0.f, 0.f, 0.f};
-      int i = 0;
-      for (; i + 4 <= ns; i += 4) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          dq[u] += sP[(i + u) * kPitch + lane] > qv
-                       ? sG[(i + u) * kPitch + j] : 0.f;
       }
-      for (; i < ns; ++i)
-        dq[0] += sP[i * kPitch + lane] > qv ? sG[i * kPitch + j] : 0.f;
-      if (cv)
+      // dQ rows j = r0, r0 + rp, ...
+      for (int j = cm.r0; j < nt; j += cm.rp) {
+        // Same predicate as the forward: (P + b1) - Q > 0.
+        const float qv = sQ[j * R + c];
+        float dq[4] = {0.f, 0.f, 0.f, 0.f};
+        int i = 0;
+        for (; i + 4 <= ns; i += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            dq[u] += (sP[(i + u) * R + c] + bias1) - qv > 0.f
+                         ? sG[(i + u) * Nt + j] : 0.f;
+        }
+        for (; i < ns; ++i)
+          dq[0] += (sP[i * R + c] + bias1) - qv > 0.f ? sG[i * Nt + j] : 0.f;
         dQb[(size_t)j * R + c] =
             Cvt<TPQ>::from_f(-((dq[0] + dq[1]) + (dq[2] + dq[3])) * w);
+      }
     }
-    // Reduce dw over the 4 waves.
-    sRed[wave * kCh + lane] = dw;
+    // dw2: fixed-order reduction over the row groups (deterministic).
+    sRed[tid] = dw;
     __syncthreads();
-    if (wave == 0 && cv)
-      dw2_part[(size_t)b * R + c] = sRed[lane] + sRed[kCh + lane] +
-                                    sRed[2 * kCh + lane] +
-                                    sRed[3 * kCh + lane];
+    if (tid < cm.cw) {
+      float s = 0.f;
+      for (int r = 0; r < cm.rp; ++r) s += sRed[r * cm.cw + tid];
+      dw2_part[(size_t)b * R + c0 + tid] = s;
+    }
   }
 }
 
@@ -386,6 +556,24 @@ static void check_ptr(const at::Tensor& ptr_s, const at::Tensor& ptr_t,
 static void check_packed(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous(), name,
               " must be a contiguous [rows, R] GPU tensor");
+}
+
+// 16-byte vector loads possible for every pair's row block of t.
+static bool rows_vec_ok(const at::Tensor& t) {
+  return aligned16(t.data_ptr()) && (t.size(1) * t.element_size()) % 16 == 0;
+}
+
+// Dynamic LDS of a pair kernel; raises the per-kernel limit when needed.
+template <typename K>
+static size_t pair_lds(K kern, size_t floats) {
+  const size_t bytes = floats * sizeof(float);
+  TORCH_CHECK(bytes <= 160 * 1024, "pair tile exceeds the 160 KiB LDS (",
+              bytes, " bytes)");
+  if (bytes > 64 * 1024)
+    DGMC_CHECK_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kern),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return bytes;
 }
 
 at::Tensor dense_masked_softmax(const at::Tensor& S_hat, const at::Tensor& n_s,
@@ -448,16 +636,19 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     if (joint_out) joint.narrow(0, 0, rows_s).copy_(r_s);
     return {S, joint_out ? joint : r_t};
   }
+  const int vec = rows_vec_ok(r_s) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
-    hipLaunchKernelGGL(softmax_transport_kernel<T>, dim3(B), dim3(256), 0,
-                       stream(), S_hat.data_ptr<float>(),
+    auto kern = softmax_transport_kernel<T>;
+    const size_t lds = pair_lds(kern, (size_t)Ns * R + (size_t)Ns * Nt);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                       S_hat.data_ptr<float>(),
                        reinterpret_cast<const T*>(r_s.data_ptr()),
                        ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
                        S.data_ptr<float>(), reinterpret_cast<T*>(r_t.data_ptr()),
                        Ns, Nt, R, (int)rows_t,
                        joint_out ? reinterpret_cast<T*>(joint.data_ptr())
                                  : nullptr,
-                       (int)rows_s);
+                       (int)rows_s, vec);
   });
   DGMC_CHECK_LAUNCH();
   return {S, joint_out ? joint : r_t};
@@ -480,13 +671,17 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S);
   if (B == 0) return out;
+  const int vec = (rows_vec_ok(r_s) && rows_vec_ok(g)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
-    hipLaunchKernelGGL(softmax_transport_bwd_kernel<T>, dim3(B), dim3(256), 0,
-                       stream(), S.data_ptr<float>(),
+    auto kern = softmax_transport_bwd_kernel<T>;
+    const size_t lds = pair_lds(
+        kern, (size_t)(Ns + Nt) * (R + 1) + (size_t)Ns * Nt);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                       S.data_ptr<float>(),
                        reinterpret_cast<const T*>(r_s.data_ptr()),
                        reinterpret_cast<const T*>(g.data_ptr()),
                        ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
-                       out.data_ptr<float>(), Ns, Nt, R);
+                       out.data_ptr<float>(), Ns, Nt, R, vec);
   });
   DGMC_CHECK_LAUNCH();
   return out;
@@ -513,15 +708,19 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S_hat);
   if (B == 0) return out;
+  const int vec = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
-    hipLaunchKernelGGL(consensus_fwd_kernel<T>, dim3(B), dim3(256), 0,
-                       stream(), S_hat.data_ptr<float>(),
+    auto kern = consensus_fwd_kernel<T>;
+    const size_t lds =
+        pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) + 2 * (size_t)R);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                       S_hat.data_ptr<float>(),
                        reinterpret_cast<const T*>(P.data_ptr()),
                        reinterpret_cast<const T*>(Q.data_ptr()),
                        b1.data_ptr<float>(), w2.data_ptr<float>(),
                        b2.data_ptr<float>(), ptr_s.data_ptr<int>(),
                        ptr_t.data_ptr<int>(), out.data_ptr<float>(), Ns, Nt,
-                       R);
+                       R, vec);
   });
   DGMC_CHECK_LAUNCH();
   return out;
@@ -538,6 +737,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   const int B = G.size(0), Ns = G.size(1), Nt = G.size(2);
   const int R = P.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
+  TORCH_CHECK(b1.numel() == R && w2.numel() == R, "b1/w2 size");
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor dP, dQ;
   if (dpq_out.has_value() && dpq_out->defined()) {
@@ -555,9 +755,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   at::Tensor dw2 = at::empty({B, R}, G.options());
   at::Tensor db2 = at::empty({B}, G.options());
   if (B == 0) return {dP, dQ, dw2.zero_(), db2.zero_()};
+  const int vec = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
-    hipLaunchKernelGGL(consensus_bwd_kernel<T>, dim3(B), dim3(256), 0,
-                       stream(), G.data_ptr<float>(),
+    auto kern = consensus_bwd_kernel<T>;
+    const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * R +
+                                          (size_t)Ns * Nt + 2 * (size_t)R +
+                                          kThreads);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                       G.data_ptr<float>(),
                        reinterpret_cast<const T*>(P.data_ptr()),
                        reinterpret_cast<const T*>(Q.data_ptr()),
                        b1.data_ptr<float>(), w2.data_ptr<float>(),
@@ -565,7 +770,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
                        reinterpret_cast<T*>(dP.data_ptr()),
                        reinterpret_cast<T*>(dQ.data_ptr()),
                        dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R,
-                       (int)P.size(0), (int)Q.size(0));
+                       (int)P.size(0), (int)Q.size(0), vec);
   });
   DGMC_CHECK_LAUNCH();
   return {dP, dQ, dw2, db2};

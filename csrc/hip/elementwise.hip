@@ -281,4 +281,90 @@ void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate) {
   DGMC_CHECK_LAUNCH();
 }
 
+// ---------------------------------------------------------------------------
+// Row concatenation of up to kCatMax 2-D blocks in ONE launch (loop-gradient
+// operand stacks, runtime/loopgrad.py).  torch.cat splits such a list over
+// several batched launches at ~0.7 TB/s; here every source is a 2-D grid of
+// 16-byte chunks (rows may be strided - column-slice views are copied without
+// a contiguous() pass) and blockIdx.y selects the source.
+// ---------------------------------------------------------------------------
+constexpr int kCatMax = 32;
+
+struct CatArgs {
+  const char* src[kCatMax];
+  int64_t ld_bytes[kCatMax];    // source row stride
+  int64_t rows[kCatMax];
+  int64_t dst_row0[kCatMax];    // first output row of the block
+};
+
+__global__ __launch_bounds__(256) void cat_rows_kernel(CatArgs args,
+                                                       char* __restrict__ dst,
+                                                       int64_t row_bytes) {
+  const int s = blockIdx.y;
+  const int64_t cpr = row_bytes / 16;             // 16-byte chunks per row
+  const int64_t total = args.rows[s] * cpr;
+  const char* __restrict__ src = args.src[s];
+  const int64_t ld = args.ld_bytes[s];
+  char* __restrict__ out = dst + args.dst_row0[s] * row_bytes;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < total;
+       c += stride) {
+    const int64_t r = c / cpr, q = c - r * cpr;
+    *reinterpret_cast<uint4*>(out + r * row_bytes + q * 16) =
+        *reinterpret_cast<const uint4*>(src + r * ld + q * 16);
+  }
+}
+
+at::Tensor cat_rows(at::TensorList srcs, const c10::optional<at::Tensor>& out) {
+  TORCH_CHECK(!srcs.empty() && (int64_t)srcs.size() <= kCatMax,
+              "cat_rows: 1..", kCatMax, " tensors");
+  const at::Tensor& first = srcs[0];
+  TORCH_CHECK(first.is_cuda() && first.dim() == 2, "cat_rows: 2-D CUDA tensors");
+  const int64_t C = first.size(1);
+  const int64_t es = first.element_size();
+  const int64_t row_bytes = C * es;
+  TORCH_CHECK(row_bytes % 16 == 0,
+              "cat_rows: row bytes must be a multiple of 16");
+  CatArgs args;
+  int64_t rows = 0, max_rows = 0;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const at::Tensor& t = srcs[i];
+    TORCH_CHECK(t.dim() == 2 && t.size(1) == C &&
+                    t.scalar_type() == first.scalar_type() &&
+                    t.device() == first.device() && t.stride(1) == 1,
+                "cat_rows: tensors must share dtype/device/columns and have "
+                "unit column stride");
+    const int64_t ld = (t.size(0) > 1 ? t.stride(0) : C) * es;
+    TORCH_CHECK(aligned16(t.data_ptr()) && ld % 16 == 0,
+                "cat_rows: 16-byte aligned rows required");
+    args.src[i] = reinterpret_cast<const char*>(t.data_ptr());
+    args.ld_bytes[i] = ld;
+    args.rows[i] = t.size(0);
+    args.dst_row0[i] = rows;
+    rows += t.size(0);
+    max_rows = std::max(max_rows, t.size(0));
+  }
+  at::Tensor dst;
+  if (out.has_value() && out->defined()) {
+    dst = *out;
+    TORCH_CHECK(dst.is_contiguous() && dst.numel() == rows * C &&
+                    dst.scalar_type() == first.scalar_type() &&
+                    dst.device() == first.device() && aligned16(dst.data_ptr()),
+                "cat_rows: out must be contiguous [sum rows, C], same dtype");
+  } else {
+    dst = at::empty({rows, C}, first.options());
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(first.device());
+  if (rows == 0 || C == 0) return dst;
+  const int64_t chunks = max_rows * (row_bytes / 16);
+  const int64_t want = (chunks + 255) / 256;
+  const int64_t cap = std::max<int64_t>(1, 4096 / (int64_t)srcs.size());
+  const int bx = (int)std::max<int64_t>(1, std::min<int64_t>(want, cap));
+  hipLaunchKernelGGL(cat_rows_kernel, dim3(bx, (unsigned)srcs.size()),
+                     dim3(256), 0, stream(), args,
+                     reinterpret_cast<char*>(dst.data_ptr()), row_bytes);
+  DGMC_CHECK_LAUNCH();
+  return dst;
+}
+
 }  // namespace dgmc

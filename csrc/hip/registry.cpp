@@ -68,6 +68,7 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
 at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
                    bool accumulate, const c10::optional<at::Tensor>& part_out);
 void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
+at::Tensor cat_rows(at::TensorList srcs, const c10::optional<at::Tensor>& out);
 at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const at::Tensor& ecol, const at::Tensor& eval,
                        const at::Tensor& W, int64_t ss, int64_t sn,
@@ -122,6 +123,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "col_sum(Tensor src, Tensor(a!)? dst=None, bool accumulate=False, "
       "Tensor(b!)? part_out=None) -> Tensor");
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
+  m.def("cat_rows(Tensor[] srcs, Tensor(a!)? out=None) -> Tensor");
   m.def(
       "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
       "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
@@ -158,6 +160,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
   m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
+  m.impl("cat_rows", &dgmc::cat_rows);
   m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);

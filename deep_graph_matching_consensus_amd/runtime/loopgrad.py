@@ -41,6 +41,14 @@ _TLS = threading.local()
 ENABLED = True
 
 
+def _rows16(t):
+    """2-D tensor whose rows are 16-byte aligned with unit column stride."""
+    es = t.element_size()
+    return (t.dim() == 2 and t.stride(1) == 1 and
+            (t.size(1) * es) % 16 == 0 and (t.stride(0) * es) % 16 == 0 and
+            t.data_ptr() % 16 == 0)
+
+
 class LoopGrad(object):
     """Collects the gradient contributions of one op reused in a loop."""
 
@@ -103,10 +111,18 @@ class LoopGrad(object):
         lst[idx] = tensor
 
     def kept(self, name):
-        """Concatenation (dim 0, use order) of the kept contributions."""
+        """Concatenation (dim 0, use order) of the kept contributions (one
+        ``cat_rows`` HIP launch on the GPU: torch.cat splits a 10-way list
+        over several slower batched launches)."""
         lst = self._kept[name]
         assert all(t is not None for t in lst), name
-        return lst[0] if len(lst) == 1 else torch.cat(lst, dim=0)
+        if len(lst) == 1:
+            return lst[0]
+        from ..ops import _backend
+        if len(lst) <= 32 and _backend.use_hip(lst[0]) and \
+                all(_rows16(t) for t in lst):
+            return _backend.ops().cat_rows(lst)
+        return torch.cat(lst, dim=0)
 
     def arrive(self):
         """Called once per backward use; True for the use completing the set

@@ -125,12 +125,29 @@ def test_dense_masked_softmax(shape):
                           torch.autograd.grad(out2, S2, g)[0], atol=1e-5)
 
 
-@pytest.mark.parametrize('R', [8, 64, 100, 128])
-def test_dense_softmax_transport(R):
+@pytest.mark.parametrize('R,dtype', [(8, torch.float32), (64, torch.float32),
+                                     (100, torch.float32),
+                                     (128, torch.float32),
+                                     (128, torch.bfloat16),
+                                     (300, torch.float32)])
+def test_dense_softmax_transport(R, dtype):
     B, Ns, Nt = 6, 19, 23
     lay_s, lay_t = _layouts(B, Ns, Nt)
     S_hat = torch.randn(B, Ns, Nt, device=DEV, requires_grad=True)
-    r_s = torch.randn(lay_s.num_nodes, R, device=DEV)
+    r_s = torch.randn(lay_s.num_nodes, R, device=DEV).to(dtype)
+    if dtype != torch.float32:
+        r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s, lay_t)
+        S2 = S_hat.detach().clone().requires_grad_()
+        r_t2 = lay_t.to_sparse(ref.masked_softmax(
+            S2, _mask(lay_s, lay_t)).transpose(-1, -2) @
+            lay_s.to_dense(r_s.float()))
+        assert r_t.dtype == dtype
+        assert torch.allclose(r_t.float(), r_t2, atol=2e-2, rtol=2e-2)
+        g = torch.randn_like(r_t2)
+        ga = torch.autograd.grad(r_t, S_hat, g.to(dtype))[0]
+        gb = torch.autograd.grad(r_t2, S2, g.to(dtype).float())[0]
+        assert torch.allclose(ga, gb, atol=1e-3, rtol=1e-3)
+        return
     r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s, lay_t)
     assert r_t.shape == (lay_t.num_nodes, R)
     S2 = S_hat.detach().clone().requires_grad_()
@@ -151,7 +168,7 @@ def test_dense_softmax_transport(R):
                           atol=1e-4)
 
 
-@pytest.mark.parametrize('R', [8, 32, 100, 128])
+@pytest.mark.parametrize('R', [8, 32, 100, 128, 300])
 @pytest.mark.parametrize('joint', [False, True])
 def test_dense_consensus_update(R, joint):
     B, Ns, Nt = 5, 21, 18
@@ -432,6 +449,48 @@ def test_col_sum_and_relu_bias_accumulate(rows, C, dtype):
     assert torch.allclose(part2.sum(0), gm.sum(0), atol=1e-3, rtol=1e-4)
     # Deterministic: repeated calls are bit-identical.
     assert torch.equal(ops.col_sum(src), ops.col_sum(src))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_consensus_update_bf16_node_operands(dtype):
+    # The training path feeds bf16 P/Q (encoder GEMM dtype): compare the HIP
+    # kernels against the fp32 oracle on the same rounded operands.
+    B, Ns, Nt, R = 7, 19, 17, 128
+    lay_s, lay_t = _layouts(B, Ns, Nt)
+    S_hat = torch.randn(B, Ns, Nt, device=DEV, requires_grad=True)
+    mlp = torch.nn.Sequential(torch.nn.Linear(R, R), torch.nn.ReLU(),
+                              torch.nn.Linear(R, 1)).to(DEV)
+    o = torch.randn(lay_s.num_nodes + lay_t.num_nodes, R, device=DEV)
+    o = o.to(dtype).requires_grad_()
+    o_s, o_t = o[:lay_s.num_nodes], o[lay_s.num_nodes:]
+    with torch.autocast('cuda', dtype=torch.bfloat16,
+                        enabled=dtype != torch.float32):
+        out = dense_ops.consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t,
+                                         o_joint=o)
+    with reference_mode():
+        out2 = dense_ops.consensus_update(S_hat, o_s.float(), o_t.float(),
+                                          mlp, lay_s, lay_t)
+    tol = 1e-4 if dtype == torch.float32 else 0.1
+    assert torch.allclose(out, out2, atol=tol, rtol=tol)
+    g = torch.randn_like(out)
+    ga = torch.autograd.grad(out, (S_hat, ) + tuple(mlp.parameters()), g)
+    gb = torch.autograd.grad(out2, (S_hat, ) + tuple(mlp.parameters()), g)
+    assert torch.equal(ga[0], gb[0])
+    for a, b in zip(ga[1:], gb[1:]):
+        rel = (a - b).norm() / b.norm().clamp(min=1e-6)
+        assert rel < (1e-4 if dtype == torch.float32 else 5e-2), rel
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_cat_rows(dtype):
+    parts = [torch.randn(n, 384, device=DEV).to(dtype) for n in
+             (1, 7, 1000, 9216)]
+    parts.append(torch.randn(500, 512, device=DEV).to(dtype)[:, 128:512])
+    out = _backend.ops().cat_rows(parts)
+    assert torch.equal(out, torch.cat(parts))
+    buf = torch.empty_like(out)
+    _backend.ops().cat_rows(parts, buf)
+    assert torch.equal(buf, out)
 
 
 def test_split_k_accumulate():
