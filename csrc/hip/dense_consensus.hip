@@ -1,5 +1,5 @@
 // Per-pair fused kernels of the dense DGMC consensus loop
-// (reference dgmc.py:161-183).  One workgroup (4 waves) per graph pair; the
+// (reference dgmc.py:161-183).  One workgroup (16 waves) per graph pair; the
 // pair's node tiles live in LDS, masks are derived from the per-pair node
 // counts (valid nodes occupy the leading rows of the padded tile).
 //
@@ -19,16 +19,23 @@
 //     of one per row;
 //   * computes from LDS with several independent partial sums per thread
 //     (LDS latency overlapped), channel-parallel lanes (conflict-free rows) or
-//     4 lanes per (i, j) entry with strided channels (odd LDS pitch);
+//     8 lanes per (i, j) entry with strided channels (odd LDS pitch);
 //   * sizes LDS dynamically from the padded pair tile (Ns, Nt <= 64).
 #include "common.h"
 
 namespace dgmc {
 
 constexpr int kMaxN = 64;      // max padded nodes per graph of a pair
-constexpr int kWaves = 4;      // waves per workgroup
+// Pair kernels run 16 waves per workgroup: the grid (one workgroup per pair,
+// 512 for the PascalVOC batch) is a single dispatch wave, so the kernel time
+// is the latency of the slowest pair - more lanes per pair = shorter
+// per-thread loops.  2 workgroups/CU x 16 waves = full occupancy at <= 64
+// VGPRs.
+constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * kWave;
 constexpr int kPrefetch = 4;   // S/G tile entries prefetched per thread
+constexpr int kTPE = 8;        // lanes per (i, j) entry in channel dot loops
+constexpr int kRowWaves = 4;   // row-softmax kernels: waves per 256 threads
 
 // Zero rows [row0, rows) of a packed [rows, R] tensor (padding rows of static
 // batches; executed by the last workgroup of a launch).
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(256) void masked_softmax_kernel(
     const int* __restrict__ n_t, float* __restrict__ S, int B, int Ns,
     int Nt) {
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int row = blockIdx.x * kWaves + wave;
+  const int row = blockIdx.x * kRowWaves + wave;
   if (row >= B * Ns) return;
   const int b = row / Ns, i = row % Ns;
   const float* src = S_hat + (size_t)row * Nt;
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
     const float* __restrict__ S, const float* __restrict__ G,
     float* __restrict__ out, int rows, int Nt) {
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int row = blockIdx.x * kWaves + wave;
+  const int row = blockIdx.x * kRowWaves + wave;
   if (row >= rows) return;
   const float* s = S + (size_t)row * Nt;
   const float* g = G + (size_t)row * Nt;
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(256) void masked_softmax_bwd_kernel(
 // LDS: sR [Ns][R] (r_s, fp32), sS [Ns][Nt] (S_hat, then S).
 // ---------------------------------------------------------------------------
 template <typename TR>
-__global__ __launch_bounds__(256) void softmax_transport_kernel(
+__global__ __launch_bounds__(kThreads) void softmax_transport_kernel(
     const float* __restrict__ S_hat, const TR* __restrict__ r_s,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     float* __restrict__ S, TR* __restrict__ r_t, int Ns, int Nt, int R,
@@ -250,7 +257,7 @@ __global__ __launch_bounds__(256) void softmax_transport_kernel(
 // dS_hat = softmax_bwd(S, dS),  dS[i][j] = sum_c r_s[i][c] * g[j][c].
 // LDS: sR [Ns][R+1], sG [Nt][R+1], sD [Ns][Nt].
 template <typename TR>
-__global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
+__global__ __launch_bounds__(kThreads) void softmax_transport_bwd_kernel(
     const float* __restrict__ S, const TR* __restrict__ r_s,
     const TR* __restrict__ g, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, float* __restrict__ dS_hat, int Ns,
@@ -279,11 +286,11 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
                  pitch, R, vec != 0);
   __syncthreads();
 
-  // dS[i][j]: 4 lanes per entry, channels strided by 4.
-  const int qd = tid & 3;
+  // dS[i][j]: kTPE lanes per entry, channels strided by kTPE.
+  const int qd = tid % kTPE;
   const int pairs = ns * nt;
-  for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
-    const int p = p0 + (tid >> 2);
+  for (int p0 = 0; p0 < pairs; p0 += kThreads / kTPE) {
+    const int p = p0 + tid / kTPE;
     const bool valid = p < pairs;
     const int i = valid ? p / nt : 0;
     const int j = valid ? p - i * nt : 0;
@@ -291,15 +298,15 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
     const DGMC_LDS float* gr = sG + j * pitch;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     int c = qd;
-    for (; c + 12 < R; c += 16) {
+    for (; c + 3 * kTPE < R; c += 4 * kTPE) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        a[u] = fmaf(rr[c + 4 * u], gr[c + 4 * u], a[u]);
+        a[u] = fmaf(rr[c + kTPE * u], gr[c + kTPE * u], a[u]);
     }
-    for (; c < R; c += 4) a[0] = fmaf(rr[c], gr[c], a[0]);
+    for (; c < R; c += kTPE) a[0] = fmaf(rr[c], gr[c], a[0]);
     float acc = (a[0] + a[1]) + (a[2] + a[3]);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
+#pragma unroll
+    for (int o = 1; o < kTPE; o <<= 1) acc += __shfl_xor(acc, o);
     if (valid && qd == 0) sD[i * Nt + j] = acc;
   }
   __syncthreads();
@@ -322,7 +329,7 @@ __global__ __launch_bounds__(256) void softmax_transport_bwd_kernel(
 // LDS: sP [Ns][R+1], sQ [Nt][R+1], sB [R] (b1), sW [R] (w2).
 // ---------------------------------------------------------------------------
 template <typename TPQ>
-__global__ __launch_bounds__(256) void consensus_fwd_kernel(
+__global__ __launch_bounds__(kThreads) void consensus_fwd_kernel(
     const float* __restrict__ S_hat, const TPQ* __restrict__ P,
     const TPQ* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2,
@@ -364,12 +371,12 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
   const float bias2 = b2[0];
   __syncthreads();
 
-  // 4 lanes per (i, j) entry, channels strided by 4 (odd pitch: the rows of
-  // neighbouring entries fall on different banks).
-  const int qd = tid & 3;
+  // kTPE lanes per (i, j) entry, channels strided by kTPE (odd pitch: the
+  // rows of neighbouring entries fall on different banks).
+  const int qd = tid % kTPE;
   const int pairs = ns * nt;
-  for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
-    const int p = p0 + (tid >> 2);
+  for (int p0 = 0; p0 < pairs; p0 += kThreads / kTPE) {
+    const int p = p0 + tid / kTPE;
     const bool valid = p < pairs;
     const int i = valid ? p / nt : 0;
     const int j = valid ? p - i * nt : 0;
@@ -378,18 +385,18 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
     const DGMC_LDS float* qr = sQ + j * pitch;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     int c = qd;
-    for (; c + 12 < R; c += 16) {
+    for (; c + 3 * kTPE < R; c += 4 * kTPE) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int cc = c + 4 * u;
+        const int cc = c + kTPE * u;
         a[u] = fmaf(fmaxf(pr[cc] + sB[cc] - qr[cc], 0.f), sW[cc], a[u]);
       }
     }
-    for (; c < R; c += 4)
+    for (; c < R; c += kTPE)
       a[0] = fmaf(fmaxf(pr[c] + sB[c] - qr[c], 0.f), sW[c], a[0]);
     float acc = (a[0] + a[1]) + (a[2] + a[3]);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
+#pragma unroll
+    for (int o = 1; o < kTPE; o <<= 1) acc += __shfl_xor(acc, o);
     if (valid && qd == 0) ob[i * Nt + j] = sh + acc + bias2;
   }
 }
@@ -401,7 +408,7 @@ __global__ __launch_bounds__(256) void consensus_fwd_kernel(
 // LDS: sP [Ns][R], sQ [Nt][R] (lanes run along channels: conflict-free),
 //      sG [Ns][Nt], sB [R], sW [R], sRed [kThreads].
 template <typename TPQ>
-__global__ __launch_bounds__(256) void consensus_bwd_kernel(
+__global__ __launch_bounds__(kThreads) void consensus_bwd_kernel(
     const float* __restrict__ G, const TPQ* __restrict__ P,
     const TPQ* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, const int* __restrict__ ptr_s,
@@ -465,7 +472,11 @@ __global__ __launch_bounds__(256) void consensus_bwd_kernel(
     zero_tail(dQ, ptr_t[gridDim.x], rows_t, R);
   }
   __syncthreads();
-  if (tid == 0) db2_part[b] = (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kWaves; ++w) t += sRed[w];
+    db2_part[b] = t;
+  }
   TPQ* dPb = dP + (size_t)s0 * R;
   TPQ* dQb = dQ + (size_t)t0 * R;
 
