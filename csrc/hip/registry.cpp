@@ -69,6 +69,15 @@ at::Tensor col_sum(const at::Tensor& src, const c10::optional<at::Tensor>& dst,
                    bool accumulate, const c10::optional<at::Tensor>& part_out);
 void reduce_add_rows(const at::Tensor& src, at::Tensor dst, bool accumulate);
 at::Tensor cat_rows(at::TensorList srcs, const c10::optional<at::Tensor>& out);
+void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
+                        const at::Tensor& st_val, const at::Tensor& st_trowptr,
+                        const at::Tensor& st_tcol, const at::Tensor& st_tval,
+                        const at::Tensor& node_ptr, const at::Tensor& gid,
+                        const at::Tensor& ptr_s, const at::Tensor& ptr_t,
+                        int64_t cap_s, int64_t cap_t, int64_t S,
+                        int64_t root_slot, at::Tensor rowptr, at::Tensor col,
+                        at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
+                        at::Tensor tval);
 at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const at::Tensor& ecol, const at::Tensor& eval,
                        const at::Tensor& W, int64_t ss, int64_t sn,
@@ -125,6 +134,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
   m.def("cat_rows(Tensor[] srcs, Tensor(a!)? out=None) -> Tensor");
   m.def(
+      "assemble_slot_plan(Tensor st_rowptr, Tensor st_col, Tensor st_val, "
+      "Tensor st_trowptr, Tensor st_tcol, Tensor st_tval, Tensor node_ptr, "
+      "Tensor gid, Tensor ptr_s, Tensor ptr_t, int cap_s, int cap_t, int S, "
+      "int root_slot, Tensor(a!) rowptr, Tensor(b!) col, Tensor(c!) val, "
+      "Tensor(d!) trowptr, Tensor(e!) tcol, Tensor(f!) tval) -> ()");
+  m.def(
       "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
       "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
@@ -161,6 +176,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
   m.impl("cat_rows", &dgmc::cat_rows);
+  m.impl("assemble_slot_plan", &dgmc::assemble_slot_plan);
   m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);

@@ -141,7 +141,7 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   const int64_t B = s_ids.numel();
   TORCH_CHECK(t_ids.numel() == B, "s_ids / t_ids size mismatch");
   const int64_t need = cap_s * 4 + cap_t * 2 + ecap_s * 3 + ecap_t * 3 +
-                       2 * (B + 1);
+                       2 * (B + 1) + 2 * B;
   TORCH_CHECK(out.numel() >= need, "collate_pairs_padded: buffer too small");
   const int64_t G = node_ptr.numel() - 1;
   const int64_t C = pos_of_class.size(1);
@@ -172,14 +172,18 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
       et_off[B] > ecap_t)
     return false;
 
+  // Layout (int64 words; see datasets/static_batch.py::_views).  Source and
+  // target regions of nodes / edge attributes / edge endpoints are adjacent,
+  // so the disjoint union [s; t] psi_1/psi_2 run on is a VIEW of the buffer:
+  // target edge endpoints are stored offset by cap_s (union numbering).
   int64_t* o = out.data_ptr<int64_t>();
   int64_t* node_s = o;            o += cap_s;
   int64_t* node_t = o;            o += cap_t;
   int64_t* ea_s = o;              o += ecap_s;
   int64_t* ea_t = o;              o += ecap_t;
   int64_t* ei_s0 = o;             o += ecap_s;
-  int64_t* ei_s1 = o;             o += ecap_s;
   int64_t* ei_t0 = o;             o += ecap_t;
+  int64_t* ei_s1 = o;             o += ecap_s;
   int64_t* ei_t1 = o;             o += ecap_t;
   int64_t* yv = o;                o += cap_s;
   int64_t* ym = o;                o += cap_s;
@@ -187,6 +191,7 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   int64_t* dn_t = o;              o += cap_t;
   int64_t* ptr_s = o;             o += B + 1;
   int64_t* ptr_t = o;             o += B + 1;
+  int64_t* gid = o;               o += 2 * B;   // store ids: [s_ids; t_ids]
   const int64_t trash = B * n_max;
 
 #pragma omp parallel for schedule(static)
@@ -219,8 +224,8 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
     for (int64_t e = 0; e < net; ++e) {
       const int64_t r = et_off[b] + e;
       ea_t[r] = e0t + e;
-      ei_t0[r] = src_[e0t + e] + nt_off[b];
-      ei_t1[r] = dst_[e0t + e] + nt_off[b];
+      ei_t0[r] = src_[e0t + e] + nt_off[b] + cap_s;
+      ei_t1[r] = dst_[e0t + e] + nt_off[b] + cap_s;
     }
   }
   for (int64_t r = ns_off[B]; r < cap_s; ++r) {
@@ -238,12 +243,16 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
     ea_s[r] = zero_edge; ei_s0[r] = node; ei_s1[r] = node;
   }
   for (int64_t r = et_off[B]; r < ecap_t; ++r) {
-    const int64_t node = nt_off[B] + (r - et_off[B]) % pad_t;
+    const int64_t node = nt_off[B] + (r - et_off[B]) % pad_t + cap_s;
     ea_t[r] = zero_edge; ei_t0[r] = node; ei_t1[r] = node;
   }
   for (int64_t b = 0; b <= B; ++b) {
     ptr_s[b] = ns_off[b];
     ptr_t[b] = nt_off[b];
+  }
+  for (int64_t b = 0; b < B; ++b) {
+    gid[b] = sid[b];
+    gid[B + b] = tid[b];
   }
   return true;
 }

@@ -26,6 +26,8 @@ import torch
 from ..graph.data import Batch
 from ..graph.meta import StaticBatchInfo, register_batch_info
 from ..ops import _backend
+from ..ops import plans as _plans
+from ..ops.sparse import SparseOperator
 
 
 def _round_up(x, m):
@@ -69,7 +71,7 @@ class StaticPairBatcher(object):
 
         cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
             self.B
-        self.words = cs * 4 + ct * 2 + es * 3 + et * 3 + 2 * (B + 1)
+        self.words = cs * 4 + ct * 2 + es * 3 + et * 3 + 2 * (B + 1) + 2 * B
         pin = self.device.type == 'cuda'
         self._host = [torch.zeros(self.words, dtype=torch.long,
                                   pin_memory=pin) for _ in range(2)]
@@ -83,6 +85,7 @@ class StaticPairBatcher(object):
         self._order = None
         self._pos = 0
         self.overflows = 0
+        self._assembler = SlotPlanAssembler(self)
 
     # ------------------------------------------------------------------
     def _size_capacities(self, probes, headroom):
@@ -105,16 +108,19 @@ class StaticPairBatcher(object):
     def _views(self):
         cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
             self.B
+        # Layout written by dgmc_host::collate_pairs_padded: source/target
+        # regions are adjacent, so the disjoint union [s; t] of nodes, edge
+        # attributes and edges (target endpoints stored offset by cap_s) is a
+        # view - no concatenation kernels in the step.
         o = 0
         v = {}
-        for name, n in [('node_s', cs), ('node_t', ct), ('ea_s', es),
-                        ('ea_t', et), ('ei_s', 2 * es), ('ei_t', 2 * et),
-                        ('y', cs), ('ymask', cs), ('dense_s', cs),
-                        ('dense_t', ct), ('ptr_s', B + 1), ('ptr_t', B + 1)]:
+        for name, n in [('node', cs + ct), ('ea', es + et),
+                        ('ei', 2 * (es + et)), ('y', cs), ('ymask', cs),
+                        ('dense_s', cs), ('dense_t', ct), ('ptr_s', B + 1),
+                        ('ptr_t', B + 1), ('gid', 2 * B)]:
             v[name] = self.buf[o:o + n]
             o += n
-        v['ei_s'] = v['ei_s'].view(2, es)
-        v['ei_t'] = v['ei_t'].view(2, et)
+        v['ei'] = v['ei'].view(2, es + et)
         self.v = v
 
     # ------------------------------------------------------------------
@@ -159,14 +165,28 @@ class StaticPairBatcher(object):
 
     def materialize(self):
         """Device-side batch from the static buffer (graph-capturable)."""
+        from ..models.dgmc import register_pair_graph
         v = self.v
+        cs, es = self.cap_s, self.ecap_s
         batch = Batch()
-        batch.x_s = self.x.index_select(0, v['node_s'])
-        batch.x_t = self.x.index_select(0, v['node_t'])
-        batch.edge_index_s, batch.edge_index_t = v['ei_s'], v['ei_t']
+        x_u = self.x.index_select(0, v['node'])
+        batch.x_s, batch.x_t = x_u[:cs], x_u[cs:]
+        ei_u = v['ei']
+        batch.edge_index_s = ei_u[:, :es]
+        batch.edge_index_t = ei_u[:, es:] - cs
+        ea_u = None
         if self.edge_attr is not None:
-            batch.edge_attr_s = self.edge_attr.index_select(0, v['ea_s'])
-            batch.edge_attr_t = self.edge_attr.index_select(0, v['ea_t'])
+            ea_u = self.edge_attr.index_select(0, v['ea'])
+            batch.edge_attr_s, batch.edge_attr_t = ea_u[:es], ea_u[es:]
+        else:
+            batch.edge_attr_s = batch.edge_attr_t = None
+        # DGMC encodes source and target as one disjoint union: hand it the
+        # union graph directly, and route its sparse-operator requests to the
+        # per-graph plan assembler (no per-step plan construction).
+        register_pair_graph(batch.edge_index_s, batch.edge_attr_s,
+                            batch.edge_index_t, batch.edge_attr_t, cs, ei_u,
+                            ea_u)
+        _plans.register_plan_provider(ei_u, ea_u, self._assembler)
         batch.y = v['y']
         batch.y_mask = v['ymask'].to(torch.bool)
         ptr_s = v['ptr_s'].to(torch.int32)
@@ -186,3 +206,90 @@ class StaticPairBatcher(object):
                 'ecap_t={})').format(type(self).__name__, self.B, self.n_max,
                                      self.cap_s, self.cap_t, self.ecap_s,
                                      self.ecap_t)
+
+
+class _StaticSlotOperator(SparseOperator):
+    """Fixed-capacity operator filled by ``assemble_slot_plan``: entries past
+    ``rowptr[-1]`` are inert (col 0, val 0)."""
+
+    @property
+    def row(self):
+        if self._row is None:
+            pos = torch.arange(self.nnz, device=self.device, dtype=torch.int32)
+            r = torch.searchsorted(self.rowptr[1:], pos, right=True)
+            self._row = r.clamp_(max=max(self.num_rows - 1, 0)).long()
+        return self._row
+
+
+class SlotPlanAssembler(object):
+    r"""Spline operators (``A`` and ``A^T``) of a static batch's union graph,
+    assembled per step by ONE kernel (``csrc/hip/plan_assembly.hip``) from
+    the store-level operator built once per conv configuration - instead of
+    basis + degree + two stable sorts + scans every step.
+
+    Valid rows are identical to :func:`~..ops.plans.spline_plan` on the batch
+    (same per-graph entries, same order); padding rows carry only their root
+    entry.  Returns None (generic build) off-GPU or during a first capture.
+    """
+
+    def __init__(self, batcher):
+        self.b = batcher
+        self._store = {}
+        self._out = {}
+        self._store_ei = None
+        self._node_ptr = None
+
+    def _store_graph(self):
+        st = self.b.store
+        if self._store_ei is None:
+            e = st.edge_ptr[1:] - st.edge_ptr[:-1]
+            off = torch.from_numpy(np.repeat(st.node_ptr[:-1], e))
+            self._store_ei = (st.edge_local + off.view(1, -1)).to(st.device)
+            self._node_ptr = torch.from_numpy(st.node_ptr).to(st.device)
+        return self._store_ei
+
+    def spline_plan(self, num_nodes, kernel_size, is_open_spline, degree,
+                    root):
+        b = self.b
+        st = b.store
+        if (b.device.type != 'cuda' or st.edge_attr is None or
+                not _backend.hip_available() or
+                num_nodes != b.cap_s + b.cap_t):
+            return None
+        key = (tuple(kernel_size), tuple(is_open_spline), degree, root)
+        pieces = self._store.get(key)
+        if pieces is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None            # built eagerly (warm-up steps) first
+            A = _plans.spline_plan(self._store_graph(), st.edge_attr,
+                                   int(st.node_ptr[-1]), kernel_size,
+                                   is_open_spline, degree, root)
+            pieces = self._store[key] = (A, A.t())
+        A, At = pieces
+        K = 1
+        for k in kernel_size:
+            K *= int(k)
+        S = K + (1 if root else 0)
+        N = b.cap_s + b.cap_t
+        out = self._out.get(key)
+        if out is None:
+            per_edge = (degree + 1) ** len(kernel_size)
+            cap = per_edge * (b.ecap_s + b.ecap_t) + (N if root else 0)
+            dev = b.device
+            i32 = dict(dtype=torch.int32, device=dev)
+            f32 = dict(dtype=torch.float32, device=dev)
+            out = self._out[key] = (
+                torch.zeros(N + 1, **i32), torch.zeros(cap, **i32),
+                torch.zeros(cap, **f32), torch.zeros(N * S + 1, **i32),
+                torch.zeros(cap, **i32), torch.zeros(cap, **f32))
+        rowptr, col, val, trowptr, tcol, tval = out
+        v = b.v
+        _backend.ops().assemble_slot_plan(
+            A.rowptr, A.col, A.val, At.rowptr, At.col, At.val,
+            self._node_ptr, v['gid'], v['ptr_s'], v['ptr_t'], b.cap_s,
+            b.cap_t, S, K if root else -1, rowptr, col, val, trowptr, tcol,
+            tval)
+        op = _StaticSlotOperator(rowptr, col, val, N, N * S)
+        op._t = _StaticSlotOperator(trowptr, tcol, tval, N * S, N)
+        op._t._t = op
+        return op

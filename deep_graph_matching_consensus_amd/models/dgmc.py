@@ -57,6 +57,42 @@ class _PairGraph(object):
         else:
             self.edge_attr = None
 
+    @classmethod
+    def from_union(cls, n_s, edge_index, edge_attr):
+        pair = cls.__new__(cls)
+        pair.n_s, pair.edge_index, pair.edge_attr = n_s, edge_index, edge_attr
+        return pair
+
+
+def register_pair_graph(edge_index_s, edge_attr_s, edge_index_t, edge_attr_t,
+                        n_s, edge_index, edge_attr):
+    """Provide the disjoint union of a batch's source/target graphs (e.g. a
+    static batch whose buffer already holds it) so :meth:`DGMC.forward` does
+    not concatenate it.  Keyed on the identity of the four batch tensors."""
+    _PAIR_CACHE.put((edge_index_s, edge_attr_s, edge_index_t, edge_attr_t),
+                    ('pair', int(n_s)),
+                    _PairGraph.from_union(int(n_s), edge_index, edge_attr))
+
+
+def _cat_rows(a, b):
+    """``torch.cat([a, b])`` - or, when ``a`` and ``b`` are consecutive row
+    blocks of one contiguous base tensor (static batches), that slice of the
+    base (no copy; autograd flows through the base)."""
+    base = a._base
+    if (base is not None and b._base is base and base.is_contiguous() and
+            a.is_contiguous() and b.is_contiguous() and a.dim() >= 1 and
+            a.dim() == base.dim() and a.shape[1:] == b.shape[1:] and
+            a.shape[1:] == base.shape[1:]):
+        row = 1
+        for d in a.shape[1:]:
+            row *= d
+        oa = a.storage_offset() - base.storage_offset()
+        ob = b.storage_offset() - base.storage_offset()
+        if row > 0 and oa % row == 0 and ob == oa + a.numel():
+            i = oa // row
+            return base[i:i + a.size(0) + b.size(0)]
+    return torch.cat([a, b], dim=0)
+
 
 class DGMC(torch.nn.Module):
     r"""Two-stage deep graph matching (local feature matching followed by
@@ -108,8 +144,7 @@ class DGMC(torch.nn.Module):
 
     def _encode(self, psi, pair, x_s, x_t, ei_s, ea_s, ei_t, ea_t):
         if pair is not None and self._fusable(psi):
-            h = psi(torch.cat([x_s, x_t], dim=0), pair.edge_index,
-                    pair.edge_attr)
+            h = psi(_cat_rows(x_s, x_t), pair.edge_index, pair.edge_attr)
             return h[:pair.n_s], h[pair.n_s:]
         return psi(x_s, ei_s, ea_s), psi(x_t, ei_t, ea_t)
 

@@ -58,10 +58,22 @@ class _IdentityCache(object):
 
 
 _CACHE = _IdentityCache()
+# Plan providers: objects that can produce the operators of a specific graph
+# without the generic device build (e.g. a static batcher assembling them
+# from per-graph pieces precomputed once, datasets/static_batch.py).
+_PROVIDERS = _IdentityCache()
 
 
 def clear_plan_cache():
     _CACHE.clear()
+    _PROVIDERS.clear()
+
+
+def register_plan_provider(edge_index, pseudo, provider):
+    """Route plan requests for ``(edge_index, pseudo)`` (tensor identity) to
+    ``provider.spline_plan(num_nodes, kernel_size, is_open_spline, degree,
+    root)``; a provider may return None to fall back to the generic build."""
+    _PROVIDERS.put((edge_index, pseudo), ('provider', ), provider)
 
 
 def _degree(index, num_nodes):
@@ -111,6 +123,12 @@ def spline_plan(edge_index, pseudo, num_nodes, kernel_size, is_open_spline,
     plan = _CACHE.get((edge_index, pseudo), params)
     if plan is not None:
         return plan
+    provider = _PROVIDERS.get((edge_index, pseudo), ('provider', ))
+    if provider is not None:
+        plan = provider.spline_plan(int(num_nodes), kernel_size,
+                                    is_open_spline, int(degree), bool(root))
+        if plan is not None:
+            return _CACHE.put((edge_index, pseudo), params, plan)
 
     device = edge_index.device
     K = 1

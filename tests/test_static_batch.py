@@ -81,3 +81,56 @@ def test_capacity_covers_probe():
     for _ in range(20):
         s, t = batcher.next_ids()
         assert n[s].sum() < batcher.cap_s and n[t].sum() < batcher.cap_t
+
+
+@pytest.mark.gpu
+def test_assembled_spline_plan_matches_generic_build():
+    """The per-graph plan assembly (plan_assembly.hip) reproduces the generic
+    per-batch spline operator bit for bit on every valid row, for A and A^T."""
+    from deep_graph_matching_consensus_amd.ops import plans
+    from deep_graph_matching_consensus_amd.ops.sparse import spmm
+    store, batcher, model = _setup('cuda')
+    for _ in range(2):   # second step: a different batch in the same buffers
+        assert batcher.load()
+        batch = batcher.materialize()
+        cs, ct = batcher.cap_s, batcher.cap_t
+        N = cs + ct
+        ei_u = batcher.v['ei']
+        ea_u = torch.cat([batch.edge_attr_s, batch.edge_attr_t])
+        ea_view = batch.edge_attr_s._base
+        op = plans.spline_plan(ei_u, ea_view, N, (5, 5), (1, 1), 1, True)
+        assert type(op).__name__ == '_StaticSlotOperator'
+        ref_op = plans.spline_plan(ei_u.clone(), ea_u, N, (5, 5), (1, 1), 1,
+                                   True)
+        assert type(ref_op).__name__ == 'SparseOperator'
+        ptr_s = batcher.v['ptr_s'].cpu()
+        ptr_t = batcher.v['ptr_t'].cpu()
+        valid = torch.zeros(N, dtype=torch.bool)
+        valid[:int(ptr_s[-1])] = True
+        valid[cs:cs + int(ptr_t[-1])] = True
+        valid = valid.cuda()
+        x = torch.randn(N * 26, 32, device='cuda')
+        ya, yb = spmm(op, x), spmm(ref_op, x)
+        assert torch.equal(ya[valid], yb[valid])
+        g = torch.randn(N, 32, device='cuda') * valid.view(-1, 1)
+        za, zb = spmm(op.t(), g), spmm(ref_op.t(), g)
+        assert torch.equal(za, zb)
+        assert int(op.rowptr[-1]) == int(op.t().rowptr[-1])
+        assert torch.equal(op.rowptr[1:] >= op.rowptr[:-1],
+                           torch.ones(N, dtype=torch.bool, device='cuda'))
+
+
+@pytest.mark.gpu
+def test_static_batch_union_views_gpu():
+    store, batcher, model = _setup('cuda')
+    assert batcher.load()
+    batch = batcher.materialize()
+    cs = batcher.cap_s
+    # x_s / x_t are row blocks of one gathered tensor; DGMC re-joins them
+    # without a copy.
+    from deep_graph_matching_consensus_amd.models.dgmc import _cat_rows
+    joint = _cat_rows(batch.x_s, batch.x_t)
+    assert joint.data_ptr() == batch.x_s.data_ptr()
+    assert torch.equal(joint, torch.cat([batch.x_s, batch.x_t]))
+    ei = torch.cat([batch.edge_index_s, batch.edge_index_t + cs], dim=1)
+    assert torch.equal(ei, batcher.v['ei'])
