@@ -1,0 +1,316 @@
+// Objective-side fused kernels of the dense DGMC training step.
+//
+// * masked_softmax_packed      S_0 / S_L = to_sparse(masked_softmax(S_hat))
+//                              (reference dgmc.py:15-19,165,181): the dense
+//                              [B, Ns, Nt] scores go straight to the packed
+//                              [rows, Nt] output through the layout's dense
+//                              row index (no pack gather, and its backward is
+//                              a plain row scatter - no index_add);
+// * nll_fwd / nll_bwd          DGMC.loss (dgmc.py:246-267) with the optional
+//                              ground-truth mask of padded static batches,
+//                              plus the Hits@1 count of DGMC.acc (dgmc.py:
+//                              269-288) in the same pass; deterministic
+//                              block reduction, no host sync;
+// * nonfinite_partials/_final  device-side "any non-finite gradient" flag
+//                              read by the fused Adam (skipped steps).
+// The reference path for all of these is ~80 small ATen launches per step
+// (advanced-indexing backward sorts its indices).
+#include "common.h"
+
+namespace dgmc {
+
+constexpr int kLossThreads = 1024;
+
+// ---------------------------------------------------------------------------
+// Packed masked softmax.  One wave per packed row r: dense row
+// idx = dense_index[r] (>= B * Ns: padding row -> zeros).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void masked_softmax_packed_kernel(
+    const float* __restrict__ S_hat, const int64_t* __restrict__ dense_index,
+    const int* __restrict__ n_s, const int* __restrict__ n_t,
+    float* __restrict__ out, int rows, int B, int Ns, int Nt) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const int64_t idx = dense_index[r];
+  float* dst = out + (size_t)r * Nt;
+  int nt = 0;
+  const float* src = S_hat;
+  if (idx >= 0 && idx < (int64_t)B * Ns) {
+    const int b = (int)(idx / Ns), i = (int)(idx - (int64_t)b * Ns);
+    nt = i < n_s[b] ? n_t[b] : 0;
+    src = S_hat + (size_t)idx * Nt;
+  }
+  float m = -INFINITY;
+  for (int j = lane; j < nt; j += kWave) m = fmaxf(m, src[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < nt; j += kWave) s += __expf(src[j] - m);
+  s = wave_sum(s);
+  const float inv = nt > 0 ? 1.f / s : 0.f;
+  for (int j = lane; j < Nt; j += kWave)
+    dst[j] = j < nt ? __expf(src[j] - m) * inv : 0.f;
+}
+
+// dS_hat[idx] = S (g - <S, g>) for every non-padding packed row; dS_hat is
+// zero-filled beforehand (rows no packed row maps to get no gradient).
+__global__ __launch_bounds__(256) void masked_softmax_packed_bwd_kernel(
+    const float* __restrict__ S, const float* __restrict__ G,
+    const int64_t* __restrict__ dense_index, float* __restrict__ dS_hat,
+    int rows, int64_t dense_rows, int Nt) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int r = blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const int64_t idx = dense_index[r];
+  if (idx < 0 || idx >= dense_rows) return;
+  const float* s = S + (size_t)r * Nt;
+  const float* g = G + (size_t)r * Nt;
+  float dot = 0.f;
+  for (int j = lane; j < Nt; j += kWave) dot += s[j] * g[j];
+  dot = wave_sum(dot);
+  float* d = dS_hat + (size_t)idx * Nt;
+  for (int j = lane; j < Nt; j += kWave) d[j] = s[j] * (g[j] - dot);
+}
+
+// ---------------------------------------------------------------------------
+// NLL (+ Hits@1).  One workgroup; fixed-order reduction (deterministic).
+//   loss = sum_g w_g * -log(S[y0_g, y1_g] + eps) / (mean ? max(sum w, 1) : 1)
+//   aux  = [sum w, sum w * (argmax_j S[y0_g, j] == y1_g)]
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int w = 0; w < kLossThreads / kWave; ++w) t += red[w];
+  return t;
+}
+
+__global__ __launch_bounds__(kLossThreads) void nll_fwd_kernel(
+    const float* __restrict__ S, const int64_t* __restrict__ y0,
+    const int64_t* __restrict__ y1, const bool* __restrict__ mask,
+    float* __restrict__ loss, float* __restrict__ aux, int G, int Nt,
+    float eps, int mean, int with_correct) {
+  __shared__ float red[kLossThreads / kWave];
+  float acc = 0.f, cnt = 0.f, cor = 0.f;
+  for (int g = threadIdx.x; g < G; g += kLossThreads) {
+    if (mask != nullptr && !mask[g]) continue;
+    const float* row = S + (size_t)y0[g] * Nt;
+    const int64_t t = y1[g];
+    acc += -__logf(row[t] + eps);
+    cnt += 1.f;
+    if (with_correct) {
+      float best = -INFINITY;
+      int64_t arg = 0;
+      for (int j = 0; j < Nt; ++j) {
+        const float v = row[j];
+        if (v > best) { best = v; arg = j; }
+      }
+      cor += arg == t ? 1.f : 0.f;
+    }
+  }
+  acc = block_sum(acc, red);
+  cnt = block_sum(cnt, red);
+  cor = block_sum(cor, red);
+  if (threadIdx.x == 0) {
+    loss[0] = mean ? acc / fmaxf(cnt, 1.f) : acc;
+    aux[0] = cnt;
+    aux[1] = cor;
+  }
+}
+
+// dS[y0_g, y1_g] += -grad * w_g / (S + eps) / divisor   (dS zero-filled).
+__global__ __launch_bounds__(256) void nll_bwd_kernel(
+    const float* __restrict__ grad, const float* __restrict__ S,
+    const int64_t* __restrict__ y0, const int64_t* __restrict__ y1,
+    const bool* __restrict__ mask, const float* __restrict__ aux,
+    float* __restrict__ dS, int G, int Nt, float eps, int mean) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  if (mask != nullptr && !mask[g]) return;
+  const float div = mean ? fmaxf(aux[0], 1.f) : 1.f;
+  const size_t e = (size_t)y0[g] * Nt + y1[g];
+  atomicAdd(dS + e, -grad[0] / ((S[e] + eps) * div));
+}
+
+// ---------------------------------------------------------------------------
+// Non-finite check: per-block flags, then one block folds them into the
+// found_inf scalar (fp32 0/1, read by fused Adam) and the skipped-step count.
+// ---------------------------------------------------------------------------
+constexpr int kFiniteBlocks = 512;
+
+__global__ __launch_bounds__(256) void nonfinite_partials_kernel(
+    const float* __restrict__ x, int64_t n, int* __restrict__ part) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  int bad = 0;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    bad |= !isfinite(v.x) | !isfinite(v.y) | !isfinite(v.z) | !isfinite(v.w);
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+       i < n; i += stride)
+    bad |= !isfinite(x[i]);
+  if (bad) any = 1;   // benign race: every writer stores 1
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = any;
+}
+
+__global__ __launch_bounds__(256) void nonfinite_final_kernel(
+    const int* __restrict__ part, int nparts, float* __restrict__ found_inf,
+    double* __restrict__ counter) {
+  int bad = 0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) bad |= part[i];
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) {
+    found_inf[0] = bad ? 1.f : 0.f;
+    if (counter != nullptr) counter[0] += bad ? 1.0 : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host wrappers
+// ---------------------------------------------------------------------------
+at::Tensor masked_softmax_packed(const at::Tensor& S_hat,
+                                 const at::Tensor& dense_index,
+                                 const at::Tensor& n_s, const at::Tensor& n_t) {
+  TORCH_CHECK(S_hat.is_cuda() && S_hat.scalar_type() == at::kFloat &&
+                  S_hat.is_contiguous() && S_hat.dim() == 3,
+              "masked_softmax_packed: contiguous fp32 [B, Ns, Nt] scores");
+  TORCH_CHECK(dense_index.scalar_type() == at::kLong && dense_index.dim() == 1 &&
+                  dense_index.is_contiguous(),
+              "masked_softmax_packed: int64 dense row index");
+  const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
+  TORCH_CHECK(n_s.scalar_type() == at::kInt && n_t.scalar_type() == at::kInt &&
+                  n_s.numel() == B && n_t.numel() == B,
+              "masked_softmax_packed: int32 [B] node counts");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
+  const int rows = dense_index.numel();
+  at::Tensor out = at::empty({rows, Nt}, S_hat.options());
+  if (rows == 0 || Nt == 0) return out;
+  hipLaunchKernelGGL(masked_softmax_packed_kernel, dim3((rows + 3) / 4),
+                     dim3(256), 0, stream(), S_hat.data_ptr<float>(),
+                     dense_index.data_ptr<int64_t>(), n_s.data_ptr<int>(),
+                     n_t.data_ptr<int>(), out.data_ptr<float>(), rows, B, Ns,
+                     Nt);
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+at::Tensor masked_softmax_packed_bwd(const at::Tensor& S, const at::Tensor& G,
+                                     const at::Tensor& dense_index, int64_t B,
+                                     int64_t Ns) {
+  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kFloat &&
+                  S.is_contiguous() && S.dim() == 2 &&
+                  G.scalar_type() == at::kFloat && G.is_contiguous() &&
+                  G.sizes() == S.sizes(),
+              "masked_softmax_packed_bwd: contiguous fp32 [rows, Nt] S / grad");
+  TORCH_CHECK(dense_index.scalar_type() == at::kLong &&
+                  dense_index.numel() == S.size(0),
+              "masked_softmax_packed_bwd: int64 dense row index per row");
+  const int rows = S.size(0), Nt = S.size(1);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
+  at::Tensor dS = at::zeros({B, Ns, (int64_t)Nt}, S.options());
+  if (rows == 0 || Nt == 0) return dS;
+  hipLaunchKernelGGL(masked_softmax_packed_bwd_kernel, dim3((rows + 3) / 4),
+                     dim3(256), 0, stream(), S.data_ptr<float>(),
+                     G.data_ptr<float>(), dense_index.data_ptr<int64_t>(),
+                     dS.data_ptr<float>(), rows, B * Ns, Nt);
+  DGMC_CHECK_LAUNCH();
+  return dS;
+}
+
+static void check_nll_args(const at::Tensor& S, const at::Tensor& y0,
+                           const at::Tensor& y1,
+                           const c10::optional<at::Tensor>& mask) {
+  TORCH_CHECK(S.is_cuda() && S.scalar_type() == at::kFloat &&
+                  S.is_contiguous() && S.dim() == 2,
+              "nll: contiguous fp32 [rows, Nt] probabilities");
+  TORCH_CHECK(y0.scalar_type() == at::kLong && y1.scalar_type() == at::kLong &&
+                  y0.is_contiguous() && y1.is_contiguous() &&
+                  y0.numel() == y1.numel(),
+              "nll: int64 contiguous y0 / y1 of equal length");
+  if (mask.has_value() && mask->defined())
+    TORCH_CHECK(mask->scalar_type() == at::kBool && mask->is_contiguous() &&
+                    mask->numel() == y0.numel(),
+                "nll: bool mask per ground truth");
+}
+
+std::tuple<at::Tensor, at::Tensor> nll_fwd(const at::Tensor& S,
+                                           const at::Tensor& y0,
+                                           const at::Tensor& y1,
+                                           const c10::optional<at::Tensor>& mask,
+                                           double eps, bool mean,
+                                           bool with_correct) {
+  check_nll_args(S, y0, y1, mask);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
+  at::Tensor loss = at::empty({}, S.options());
+  at::Tensor aux = at::empty({2}, S.options());
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  hipLaunchKernelGGL(nll_fwd_kernel, dim3(1), dim3(kLossThreads), 0, stream(),
+                     S.data_ptr<float>(), y0.data_ptr<int64_t>(),
+                     y1.data_ptr<int64_t>(), mp, loss.data_ptr<float>(),
+                     aux.data_ptr<float>(), (int)y0.numel(), (int)S.size(1),
+                     (float)eps, mean ? 1 : 0, with_correct ? 1 : 0);
+  DGMC_CHECK_LAUNCH();
+  return {loss, aux};
+}
+
+at::Tensor nll_bwd(const at::Tensor& grad, const at::Tensor& S,
+                   const at::Tensor& y0, const at::Tensor& y1,
+                   const c10::optional<at::Tensor>& mask, const at::Tensor& aux,
+                   double eps, bool mean) {
+  check_nll_args(S, y0, y1, mask);
+  TORCH_CHECK(grad.numel() == 1 && grad.scalar_type() == at::kFloat &&
+                  aux.numel() == 2 && aux.scalar_type() == at::kFloat,
+              "nll_bwd: scalar fp32 grad, [2] aux");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
+  at::Tensor dS = at::zeros_like(S);
+  const int G = y0.numel();
+  if (G == 0) return dS;
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  at::Tensor g = grad.contiguous();
+  hipLaunchKernelGGL(nll_bwd_kernel, dim3((G + 255) / 256), dim3(256), 0,
+                     stream(), g.data_ptr<float>(), S.data_ptr<float>(),
+                     y0.data_ptr<int64_t>(), y1.data_ptr<int64_t>(), mp,
+                     aux.data_ptr<float>(), dS.data_ptr<float>(), G,
+                     (int)S.size(1), (float)eps, mean ? 1 : 0);
+  DGMC_CHECK_LAUNCH();
+  return dS;
+}
+
+void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,
+                    const c10::optional<at::Tensor>& counter) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() &&
+                  aligned16(x.data_ptr()),
+              "nonfinite_flag: contiguous aligned fp32 tensor");
+  TORCH_CHECK(found_inf.scalar_type() == at::kFloat && found_inf.numel() == 1,
+              "nonfinite_flag: fp32 scalar found_inf");
+  double* cp = nullptr;
+  if (counter.has_value() && counter->defined()) {
+    TORCH_CHECK(counter->scalar_type() == at::kDouble && counter->numel() == 1,
+                "nonfinite_flag: fp64 scalar counter");
+    cp = counter->data_ptr<double>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t n = x.numel();
+  const int blocks = (int)std::max<int64_t>(
+      1, std::min<int64_t>(kFiniteBlocks, (n / 4 + 255) / 256));
+  at::Tensor part = at::empty({blocks}, x.options().dtype(at::kInt));
+  hipLaunchKernelGGL(nonfinite_partials_kernel, dim3(blocks), dim3(256), 0,
+                     stream(), x.data_ptr<float>(), n, part.data_ptr<int>());
+  hipLaunchKernelGGL(nonfinite_final_kernel, dim3(1), dim3(256), 0, stream(),
+                     part.data_ptr<int>(), blocks, found_inf.data_ptr<float>(),
+                     cp);
+  DGMC_CHECK_LAUNCH();
+}
+
+}  // namespace dgmc

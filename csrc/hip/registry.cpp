@@ -78,6 +78,24 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                         int64_t root_slot, at::Tensor rowptr, at::Tensor col,
                         at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
                         at::Tensor tval);
+at::Tensor masked_softmax_packed(const at::Tensor& S_hat,
+                                 const at::Tensor& dense_index,
+                                 const at::Tensor& n_s, const at::Tensor& n_t);
+at::Tensor masked_softmax_packed_bwd(const at::Tensor& S, const at::Tensor& G,
+                                     const at::Tensor& dense_index, int64_t B,
+                                     int64_t Ns);
+std::tuple<at::Tensor, at::Tensor> nll_fwd(const at::Tensor& S,
+                                           const at::Tensor& y0,
+                                           const at::Tensor& y1,
+                                           const c10::optional<at::Tensor>& mask,
+                                           double eps, bool mean,
+                                           bool with_correct);
+at::Tensor nll_bwd(const at::Tensor& grad, const at::Tensor& S,
+                   const at::Tensor& y0, const at::Tensor& y1,
+                   const c10::optional<at::Tensor>& mask, const at::Tensor& aux,
+                   double eps, bool mean);
+void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,
+                    const c10::optional<at::Tensor>& counter);
 at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const at::Tensor& ecol, const at::Tensor& eval,
                        const at::Tensor& W, int64_t ss, int64_t sn,
@@ -134,6 +152,21 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("reduce_add_rows(Tensor src, Tensor(a!) dst, bool accumulate) -> ()");
   m.def("cat_rows(Tensor[] srcs, Tensor(a!)? out=None) -> Tensor");
   m.def(
+      "masked_softmax_packed(Tensor S_hat, Tensor dense_index, Tensor n_s, "
+      "Tensor n_t) -> Tensor");
+  m.def(
+      "masked_softmax_packed_bwd(Tensor S, Tensor grad, Tensor dense_index, "
+      "int B, int Ns) -> Tensor");
+  m.def(
+      "nll_fwd(Tensor S, Tensor y0, Tensor y1, Tensor? mask, float eps, bool "
+      "mean, bool with_correct) -> (Tensor, Tensor)");
+  m.def(
+      "nll_bwd(Tensor grad, Tensor S, Tensor y0, Tensor y1, Tensor? mask, "
+      "Tensor aux, float eps, bool mean) -> Tensor");
+  m.def(
+      "nonfinite_flag(Tensor x, Tensor(a!) found_inf, Tensor(b!)? counter=None)"
+      " -> ()");
+  m.def(
       "assemble_slot_plan(Tensor st_rowptr, Tensor st_col, Tensor st_val, "
       "Tensor st_trowptr, Tensor st_tcol, Tensor st_tval, Tensor node_ptr, "
       "Tensor gid, Tensor ptr_s, Tensor ptr_t, int cap_s, int cap_t, int S, "
@@ -176,6 +209,11 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("col_sum", &dgmc::col_sum);
   m.impl("reduce_add_rows", &dgmc::reduce_add_rows);
   m.impl("cat_rows", &dgmc::cat_rows);
+  m.impl("masked_softmax_packed", &dgmc::masked_softmax_packed);
+  m.impl("masked_softmax_packed_bwd", &dgmc::masked_softmax_packed_bwd);
+  m.impl("nll_fwd", &dgmc::nll_fwd);
+  m.impl("nll_bwd", &dgmc::nll_bwd);
+  m.impl("nonfinite_flag", &dgmc::nonfinite_flag);
   m.impl("assemble_slot_plan", &dgmc::assemble_slot_plan);
   m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("gemm_abt", &dgmc::gemm_abt);

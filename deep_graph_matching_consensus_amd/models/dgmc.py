@@ -28,6 +28,7 @@ from torch.nn import Linear, ReLU, Sequential
 
 from ..graph.dense import dense_layout
 from ..nn.inits import reset
+from ..ops import _backend
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
 from ..ops.plans import _IdentityCache
@@ -38,6 +39,26 @@ from ..runtime.mode import is_reference_mode
 
 EPS = 1e-8
 _PAIR_CACHE = _IdentityCache(max_entries=8)
+
+
+class _PackedNLL(torch.autograd.Function):
+    """Masked NLL of the dense correspondences (+ Hits@1 count), HIP."""
+
+    @staticmethod
+    def forward(ctx, S, y0, y1, mask, mean, with_correct):
+        loss, aux = _backend.ops().nll_fwd(S, y0, y1, mask, EPS, mean,
+                                           with_correct)
+        ctx.save_for_backward(S, y0, y1, mask, aux)
+        ctx.mean = mean
+        ctx.mark_non_differentiable(aux)
+        return loss, aux
+
+    @staticmethod
+    def backward(ctx, grad, grad_aux):
+        S, y0, y1, mask, aux = ctx.saved_tensors
+        dS = _backend.ops().nll_bwd(grad.float().contiguous(), S, y0, y1,
+                                    mask, aux, EPS, ctx.mean)
+        return dS, None, None, None, None, None
 
 
 def _device_type(device):
@@ -258,8 +279,7 @@ class DGMC(torch.nn.Module):
             if self.k < 1:
                 # ------------------ dense variant -------------------- #
                 S_hat = hs @ ht.transpose(-1, -2)            # [B, N_s, N_t]
-                S_0 = lay_s.to_sparse(
-                    dense_ops.masked_softmax(S_hat, lay_s, lay_t))
+                S_0 = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 # Fused pair encoding: the transport kernel writes r_t
                 # straight into psi_2's joint input [r_s; r_t] (no cat).
                 joint = steps > 0 and pair is not None and \
@@ -278,8 +298,7 @@ class DGMC(torch.nn.Module):
                         o_s, o_t, o = refine(r_s, r_t)
                     S_hat = dense_ops.consensus_update(
                         S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o)
-                S_L = lay_s.to_sparse(dense_ops.masked_softmax(
-                    S_hat, lay_s, lay_t))
+                S_L = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 return S_0, S_L
 
             # ------------------- sparse variant ---------------------- #
@@ -360,6 +379,9 @@ class DGMC(torch.nn.Module):
         truths of a padded static batch; ``'mean'`` then averages over them.
         """
         assert reduction in ['none', 'mean', 'sum']
+        if self._fused_nll_ok(S, y, reduction, mask):
+            return _PackedNLL.apply(S, y[0].contiguous(), y[1].contiguous(),
+                                    mask, reduction == 'mean', False)[0]
         if not S.is_sparse:
             nll = -torch.log(S[y[0], y[1]] + EPS)
             weight = mask
@@ -379,6 +401,28 @@ class DGMC(torch.nn.Module):
         if reduction == 'none':
             return nll
         return nll.mean() if reduction == 'mean' else nll.sum()
+
+    @staticmethod
+    def _fused_nll_ok(S, y, reduction, mask):
+        return (not S.is_sparse and reduction != 'none' and S.dim() == 2 and
+                S.dtype == torch.float32 and S.is_contiguous() and
+                y.dtype == torch.long and
+                (mask is None or mask.dtype == torch.bool) and
+                not is_reference_mode() and _backend.use_hip(S))
+
+    def loss_stats(self, S, y, mask=None):
+        """``(loss (mean), ground-truth count, correct top-1 count)`` as device
+        tensors - :meth:`loss` and :meth:`correct` in one pass (one fused
+        kernel on the GPU, no host sync)."""
+        if self._fused_nll_ok(S, y, 'mean', mask):
+            loss, aux = _PackedNLL.apply(S, y[0].contiguous(),
+                                         y[1].contiguous(), mask, True, True)
+            return loss, aux[0], aux[1]
+        loss = self.loss(S, y, mask=mask)
+        count = (torch.full((), y.size(1), dtype=torch.float32,
+                            device=S.device) if mask is None else
+                 mask.sum().float())
+        return loss, count, self.correct(S.detach(), y, mask).float()
 
     @staticmethod
     def _predict(S, rows):

@@ -68,6 +68,36 @@ def masked_softmax(S_hat, lay_s, lay_t):
     return ref.masked_softmax(S_hat, _count_mask(lay_s, lay_t))
 
 
+class _MaskedSoftmaxPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, S_hat, index, n_s, n_t):
+        S = _backend.ops().masked_softmax_packed(S_hat.float().contiguous(),
+                                                 index, n_s, n_t)
+        ctx.save_for_backward(S, index)
+        ctx.shape, ctx.dtype = tuple(S_hat.shape), S_hat.dtype
+        return S
+
+    @staticmethod
+    def backward(ctx, grad):
+        S, index = ctx.saved_tensors
+        B, N_s, _ = ctx.shape
+        g = _backend.ops().masked_softmax_packed_bwd(
+            S, grad.float().contiguous(), index, B, N_s)
+        return g.to(ctx.dtype), None, None, None
+
+
+def masked_softmax_packed(S_hat, lay_s, lay_t):
+    r"""``lay_s.to_sparse(masked_softmax(S_hat))`` - the packed
+    ``[sum N_s, N_t]`` correspondence output (``dgmc.py:165,181``) in one
+    kernel on the GPU (its backward is a row scatter, no ``index_add``)."""
+    index = getattr(lay_s, 'index', None)
+    if (_backend.use_hip(S_hat) and torch.is_tensor(index) and
+            index.dtype == torch.long and index.is_cuda):
+        return _MaskedSoftmaxPacked.apply(S_hat, index.contiguous(),
+                                          lay_s.counts, lay_t.counts)
+    return lay_s.to_sparse(masked_softmax(S_hat, lay_s, lay_t))
+
+
 # ---------------------------------------------------------------------------
 class _SoftmaxTransport(torch.autograd.Function):
     @staticmethod

@@ -106,19 +106,27 @@ class PairTrainer(object):
                              batch.edge_index_t, batch.edge_attr_t,
                              batch.x_t_batch)
         y = torch.stack([rows, batch.y], dim=0)
-        loss = model.loss(S_0, y, mask=mask)
         if model.num_steps:
-            loss = model.loss(S_L, y, mask=mask) + loss
+            loss_L, count, correct = model.loss_stats(S_L, y, mask)
+            loss = loss_L + model.loss(S_0, y, mask=mask)
+        else:
+            loss, count, correct = model.loss_stats(S_0, y, mask)
         loss.backward()
-        self.stats[0] += loss.detach().double()
-        self.stats[1] += model.correct(S_L.detach(), y, mask).double()
-        self.stats[2] += y.size(1) if mask is None else mask.sum().double()
+        self.stats[:3] += torch.stack(
+            [loss.detach().float(), correct.float(), count.float()]).double()
 
     def _check_finite(self):
         """Flag non-finite gradients in ``_found_inf`` (device-side)."""
         if not self.guard:
             return
-        bad = torch.logical_not(torch.isfinite(self.reducer.flat).all())
+        from .ops import _backend
+        flat = self.reducer.flat
+        if _backend.use_hip(flat) and flat.dtype == torch.float32:
+            # One pass + one fold kernel: found_inf and the skip counter.
+            _backend.ops().nonfinite_flag(flat, self._found_inf,
+                                          self.stats[3:4])
+            return
+        bad = torch.logical_not(torch.isfinite(flat).all())
         self._found_inf.copy_(bad.float())
         self.stats[3] += self._found_inf.double()
 

@@ -567,3 +567,56 @@ def test_gemm_abt(N, K, M):
     acc = torch.ones(N, M, device=DEV)
     ops.gemm_abt(a, bt, acc, True)
     assert torch.allclose(acc, ref_ + 1, atol=0.1, rtol=1e-2)
+
+
+@pytest.mark.parametrize('shape', [(7, 13, 17), (3, 64, 64), (64, 19, 19)])
+def test_masked_softmax_packed(shape):
+    lay_s, lay_t = _layouts(*shape)
+    S_hat = torch.randn(shape, device=DEV, requires_grad=True)
+    out = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
+    S2 = S_hat.detach().clone().requires_grad_()
+    out2 = lay_s.to_sparse(ref.masked_softmax(S2, _mask(lay_s, lay_t)))
+    assert out.shape == out2.shape
+    assert torch.allclose(out, out2, atol=1e-6)
+    g = torch.randn_like(out)
+    assert torch.allclose(torch.autograd.grad(out, S_hat, g)[0],
+                          torch.autograd.grad(out2, S2, g)[0], atol=1e-5)
+
+
+@pytest.mark.parametrize('masked', [False, True])
+@pytest.mark.parametrize('reduction', ['mean', 'sum'])
+def test_fused_nll_and_hits(masked, reduction):
+    from deep_graph_matching_consensus_amd.models import DGMC, MLP
+    rows, Nt, G = 777, 23, 500
+    S = torch.randn(rows, Nt, device=DEV).softmax(-1).requires_grad_()
+    y = torch.stack([torch.randperm(rows, device=DEV)[:G],
+                     torch.randint(0, Nt, (G, ), device=DEV)])
+    mask = (torch.rand(G, device=DEV) > 0.3) if masked else None
+    model = DGMC(MLP(4, 4, 1), MLP(4, 4, 1), num_steps=1)
+    loss = model.loss(S, y, reduction=reduction, mask=mask)
+    with reference_mode():
+        loss2 = model.loss(S, y, reduction=reduction, mask=mask)
+    assert torch.allclose(loss, loss2, rtol=1e-5, atol=1e-6)
+    ga = torch.autograd.grad(loss, S)[0]
+    gb = torch.autograd.grad(loss2, S)[0]
+    assert torch.allclose(ga, gb, rtol=1e-5, atol=1e-6)
+    l3, cnt, cor = model.loss_stats(S, y, mask)
+    m = mask if masked else torch.ones(G, dtype=torch.bool, device=DEV)
+    assert int(cnt) == int(m.sum())
+    pred = S.detach()[y[0]].argmax(-1)
+    assert int(cor) == int(((pred == y[1]) & m).sum())
+
+
+def test_nonfinite_flag():
+    x = torch.randn(1000003, device=DEV)
+    flag = torch.full((), 7.0, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.float64, device=DEV)
+    _backend.ops().nonfinite_flag(x, flag, cnt)
+    assert float(flag) == 0.0 and float(cnt) == 0.0
+    x[123457] = float('nan')
+    _backend.ops().nonfinite_flag(x, flag, cnt)
+    assert float(flag) == 1.0 and float(cnt) == 1.0
+    x[123457] = 0.0
+    x[-1] = float('inf')
+    _backend.ops().nonfinite_flag(x, flag, cnt)
+    assert float(flag) == 1.0 and float(cnt) == 2.0

@@ -26,6 +26,8 @@ def main():
     p.add_argument('--steps', type=int, default=3)
     p.add_argument('--rows', type=int, default=45)
     p.add_argument('--sort', default='device_time_total')
+    p.add_argument('--trace', action='store_true',
+                   help='also write a Chrome trace (large)')
     args, rest = p.parse_known_args()
     os.makedirs(osp.join(ROOT, 'gpurun_out'), exist_ok=True)
 
@@ -43,7 +45,9 @@ def main():
     print(prof.key_averages(group_by_input_shape=True).table(
         sort_by=args.sort, row_limit=args.rows, max_name_column_width=60,
         max_shapes_column_width=80))
-    prof.export_chrome_trace(osp.join(ROOT, 'gpurun_out', 'trace_step.json'))
+    if args.trace:
+        prof.export_chrome_trace(osp.join(ROOT, 'gpurun_out',
+                                          'trace_step.json'))
 
 
 if __name__ == '__main__':
