@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kAsmThreads) void assemble_slot_plan_kernel(
     int B, int64_t cap_s, int64_t cap_t, int S, int root_slot, int64_t cap,
     int* __restrict__ rowptr, int* __restrict__ col, float* __restrict__ val,
     int* __restrict__ trowptr, int* __restrict__ tcol,
-    float* __restrict__ tval) {
+    float* __restrict__ tval, uint8_t* __restrict__ gflag) {
   __shared__ int64_t red[kAsmThreads / kWave];
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
@@ -83,6 +83,12 @@ __global__ __launch_bounds__(kAsmThreads) void assemble_slot_plan_kernel(
   for (int w = 0; w < kAsmThreads / kWave; ++w) eo += red[w];
 
   const SegInfo s = segment(k, gid, ptr_s, ptr_t, B, cap_s, cap_t);
+  if (gflag) {
+    // Graph-start flags (the tiling of csrc/hip/slot_conv.hip): a graph's
+    // first row, and every padding row (padding rows form 1-node graphs).
+    for (int64_t r = tid; r < s.n; r += kAsmThreads)
+      gflag[s.off + r] = (s.gid < 0 || r == 0) ? 1 : 0;
+  }
   if (s.gid >= 0) {
     const int64_t n0 = node_ptr[s.gid];
     const int r0 = st_rowptr[n0];
@@ -146,7 +152,8 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                         int64_t cap_s, int64_t cap_t, int64_t S,
                         int64_t root_slot, at::Tensor rowptr, at::Tensor col,
                         at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
-                        at::Tensor tval) {
+                        at::Tensor tval,
+                        const c10::optional<at::Tensor>& gflag) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{
            &st_rowptr, &st_col, &st_trowptr, &st_tcol, &rowptr, &col,
            &trowptr, &tcol})
@@ -175,6 +182,13 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
               "assemble_slot_plan: store operator shape");
   TORCH_CHECK(root_slot < S && N * S < INT32_MAX,
               "assemble_slot_plan: slot / size range");
+  uint8_t* fp = nullptr;
+  if (gflag.has_value() && gflag->defined()) {
+    TORCH_CHECK(gflag->is_cuda() && gflag->scalar_type() == at::kByte &&
+                    gflag->is_contiguous() && gflag->numel() >= N,
+                "assemble_slot_plan: gflag uint8 [N]");
+    fp = gflag->data_ptr<uint8_t>();
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(col.device());
   hipLaunchKernelGGL(assemble_slot_plan_kernel, dim3(2 * B + 2),
                      dim3(kAsmThreads), 0, stream(), st_rowptr.data_ptr<int>(),
@@ -186,7 +200,7 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                      (int)root_slot, col.numel(), rowptr.data_ptr<int>(),
                      col.data_ptr<int>(), val.data_ptr<float>(),
                      trowptr.data_ptr<int>(), tcol.data_ptr<int>(),
-                     tval.data_ptr<float>());
+                     tval.data_ptr<float>(), fp);
   DGMC_CHECK_LAUNCH();
 }
 

@@ -77,7 +77,8 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                         int64_t cap_s, int64_t cap_t, int64_t S,
                         int64_t root_slot, at::Tensor rowptr, at::Tensor col,
                         at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
-                        at::Tensor tval);
+                        at::Tensor tval,
+                        const c10::optional<at::Tensor>& gflag);
 at::Tensor masked_softmax_packed(const at::Tensor& S_hat,
                                  const at::Tensor& dense_index,
                                  const at::Tensor& n_s, const at::Tensor& n_t);
@@ -104,6 +105,16 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        at::ScalarType out_dtype,
                        const c10::optional<at::Tensor>& Z);
 at::Tensor gather_gemm_stamps();
+at::Tensor slot_conv_stamps();
+at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
+                     const at::Tensor& soff, const at::Tensor& ecode,
+                     const at::Tensor& eval, int64_t S, const at::Tensor& Wimg,
+                     bool trans, const c10::optional<at::Tensor>& bias,
+                     bool relu, at::ScalarType out_dtype,
+                     const c10::optional<at::Tensor>& Z);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_tile_plan(
+    const at::Tensor& flag, const at::Tensor& rowptr, const at::Tensor& col,
+    const at::Tensor& val, int64_t window, int64_t S, at::Tensor err);
 at::Tensor gemm_abt(const at::Tensor& A, const at::Tensor& Bt,
                     const c10::optional<at::Tensor>& out, bool accumulate,
                     c10::optional<at::ScalarType> out_dtype);
@@ -171,12 +182,21 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor st_trowptr, Tensor st_tcol, Tensor st_tval, Tensor node_ptr, "
       "Tensor gid, Tensor ptr_s, Tensor ptr_t, int cap_s, int cap_t, int S, "
       "int root_slot, Tensor(a!) rowptr, Tensor(b!) col, Tensor(c!) val, "
-      "Tensor(d!) trowptr, Tensor(e!) tcol, Tensor(f!) tval) -> ()");
+      "Tensor(d!) trowptr, Tensor(e!) tcol, Tensor(f!) tval, Tensor(g!)? "
+      "gflag=None) -> ()");
   m.def(
       "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
       "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
   m.def("gather_gemm_stamps() -> Tensor");
+  m.def("slot_conv_stamps() -> Tensor");
+  m.def(
+      "slot_conv(Tensor X, Tensor tiles, Tensor soff, Tensor ecode, Tensor "
+      "eval, int S, Tensor Wimg, bool trans, Tensor? bias, bool relu, "
+      "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
+  m.def(
+      "slot_tile_plan(Tensor flag, Tensor rowptr, Tensor col, Tensor val, int "
+      "window, int S, Tensor(a!) err) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "gemm_abt(Tensor A, Tensor Bt, Tensor(a!)? out=None, bool "
       "accumulate=False, ScalarType? out_dtype=None) -> Tensor");
@@ -191,6 +211,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
   m.impl("gather_gemm_stamps", &dgmc::gather_gemm_stamps);
+  m.impl("slot_conv_stamps", &dgmc::slot_conv_stamps);
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
@@ -216,6 +237,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("nonfinite_flag", &dgmc::nonfinite_flag);
   m.impl("assemble_slot_plan", &dgmc::assemble_slot_plan);
   m.impl("gather_gemm", &dgmc::gather_gemm);
+  m.impl("slot_conv", &dgmc::slot_conv);
+  m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);

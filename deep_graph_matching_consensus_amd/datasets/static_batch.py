@@ -30,6 +30,11 @@ from ..ops import plans as _plans
 from ..ops.sparse import SparseOperator
 
 
+# Largest graph (nodes) for which batches use the fused slot conv's tiling
+# (tile window 65 - n_max >= 17 rows).
+SLOT_TILE_MAX_GRAPH = 48
+
+
 def _round_up(x, m):
     return int((int(x) + m - 1) // m * m)
 
@@ -264,8 +269,12 @@ class SlotPlanAssembler(object):
             A = _plans.spline_plan(self._store_graph(), st.edge_attr,
                                    int(st.node_ptr[-1]), kernel_size,
                                    is_open_spline, degree, root)
-            pieces = self._store[key] = (A, A.t())
-        A, At = pieces
+            # The fused slot conv scatters entries into dense tiles without
+            # accumulation: it needs every (row, column) entry to be unique.
+            rc = A.row * A.num_cols + A.col.long()
+            unique = int(torch.unique(rc).numel()) == A.nnz
+            pieces = self._store[key] = (A, A.t(), unique)
+        A, At, unique = pieces
         K = 1
         for k in kernel_size:
             K *= int(k)
@@ -281,15 +290,21 @@ class SlotPlanAssembler(object):
             out = self._out[key] = (
                 torch.zeros(N + 1, **i32), torch.zeros(cap, **i32),
                 torch.zeros(cap, **f32), torch.zeros(N * S + 1, **i32),
-                torch.zeros(cap, **i32), torch.zeros(cap, **f32))
-        rowptr, col, val, trowptr, tcol, tval = out
+                torch.zeros(cap, **i32), torch.zeros(cap, **f32),
+                torch.zeros(N, dtype=torch.uint8, device=dev))
+        rowptr, col, val, trowptr, tcol, tval, gflag = out
         v = b.v
         _backend.ops().assemble_slot_plan(
             A.rowptr, A.col, A.val, At.rowptr, At.col, At.val,
             self._node_ptr, v['gid'], v['ptr_s'], v['ptr_t'], b.cap_s,
             b.cap_t, S, K if root else -1, rowptr, col, val, trowptr, tcol,
-            tval)
+            tval, gflag)
         op = _StaticSlotOperator(rowptr, col, val, N, N * S)
         op._t = _StaticSlotOperator(trowptr, tcol, tval, N * S, N)
         op._t._t = op
+        # Graph-closed row tiles for the fused slot conv: windows of
+        # 65 - n_max rows never cut a graph into a tile of more than 64 rows.
+        if unique and b.n_max <= SLOT_TILE_MAX_GRAPH:
+            op.tile_flag = gflag
+            op.tile_window = 65 - b.n_max
         return op

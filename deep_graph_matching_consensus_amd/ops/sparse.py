@@ -192,7 +192,17 @@ class _GemmSpMM(torch.autograd.Function):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
         K = xc.size(1)
         S = w_lp.size(1) // C
-        if _fused_ok(xc, K, C):
+        ctx.img_b = None
+        if _slot_conv_ok(op, xc, K, C, S):
+            # Graph-closed tiles: Z_k = A_k x and Z_k W_k on MFMA, Y and Z
+            # never materialised (csrc/hip/slot_conv.hip).
+            img = slot_conv_image(w_lp, C, trans=False)
+            if SLOT_CONV_BWD:
+                ctx.img_b = slot_conv_image(w_lp, C, trans=True)
+            out = _backend.ops().slot_conv(
+                xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
+                relu, xc.dtype, None)
+        elif _fused_ok(xc, K, C):
             # Fused gather + MFMA: Y = x @ W is never materialised.
             sc = op.slot_csr(S)
             wt = _slot_major_t(w_lp)                    # [S * C, K]
@@ -242,19 +252,31 @@ class _GemmSpMM(torch.autograd.Function):
                     loop.add_to('b', db)
             g = g.to(w_lp.dtype)
         # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
-        opt = ctx.op.t()
+        op = ctx.op
         K = xc.size(1)
         S = w_lp.size(1) // C
-        fused = ctx.needs_input_grad[0] and _fused_ok(g, C, K)
+        slot = ctx.img_b is not None and ctx.needs_input_grad[0] and \
+            g.dtype == torch.bfloat16
+        fused = not slot and ctx.needs_input_grad[0] and _fused_ok(g, C, K)
+        opt = None if slot else op.t()
+        rows_t = op.num_cols
         if loop is not None:
-            dy = loop.slot('dy', idx, (opt.num_rows, C), w_lp.dtype, dev)
+            dy = loop.slot('dy', idx, (rows_t, C), w_lp.dtype, dev)
             loop.keep('x', idx, xc)      # concatenated once at the end
-        elif fused:
-            dy = torch.empty((opt.num_rows, C), dtype=w_lp.dtype, device=dev)
+        elif fused or slot:
+            dy = torch.empty((rows_t, C), dtype=w_lp.dtype, device=dev)
         else:
             dy = None
         gx = gw = gb = None
-        if fused:
+        if slot:
+            # Same tiles, A_k^T and W_k^T: dx in one kernel, which also
+            # writes dY = A^T g' for the weight gradient.
+            gx = _backend.ops().slot_conv(
+                g.contiguous(), *slot_tile_plan(op, S), S, ctx.img_b, True,
+                None, False, g.dtype, dy)
+            if gx.dtype != ctx.x_dtype:
+                gx = gx.to(ctx.x_dtype)
+        elif fused:
             # Gather over A^T (rows j*S + k) writes dY and contracts it with
             # W_k^T read in place from w_lp [K, S*C] in one kernel.
             gx = _backend.ops().gather_gemm(
@@ -307,6 +329,86 @@ def _fused_ok(x, K, M):
 
 def _contig(t):
     return t if t.is_contiguous() else t.contiguous()
+
+
+# Fused slot convolution on graph-closed row tiles (csrc/hip/slot_conv.hip):
+# used whenever the operator carries graph-start flags (static batches,
+# datasets/static_batch.py) and the layer is 128 -> 128 wide (psi_2 of the
+# PascalVOC/WILLOW configs).  DGMC_AMD_SLOT_CONV: 'fwd' (default) fuses the
+# forward only - measured on MI355X (tools/bench_slot_conv.py, psi_2 layer at
+# batch 512): forward 31.6 us fused vs 38.4 us GEMM + SpMM, backward with the
+# dY output 49.1 us fused vs 44.5 us SpMM + GEMM; '1' fuses both, '0' none.
+_SLOT_MODE = os.environ.get('DGMC_AMD_SLOT_CONV', 'fwd')
+SLOT_CONV = _SLOT_MODE in ('1', 'fwd')
+SLOT_CONV_BWD = _SLOT_MODE == '1'
+_SLOT_C = 128
+_SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
+_SLOT_ERR = {}
+_SLOT_PERM = {}
+
+
+def _slot_conv_ok(op, x, K, C, S):
+    return (SLOT_CONV and getattr(op, 'tile_flag', None) is not None and
+            K == _SLOT_C and C == _SLOT_C and S <= _SLOT_MAX_S and
+            x.dtype == torch.bfloat16 and _backend.use_hip(x))
+
+
+def slot_conv_error(device):
+    """Persistent int32 [1] flag the slot-conv kernel sets if a tile breaks
+    its contract (bit 0: > 64 rows, bit 1: an entry leaves its tile)."""
+    key = str(device)
+    err = _SLOT_ERR.get(key)
+    if err is None:
+        err = _SLOT_ERR[key] = torch.zeros(1, dtype=torch.int32,
+                                           device=device)
+    return err
+
+
+def slot_tile_plan(op, S):
+    """``(tiles, soff, ecode, eval)`` of ``op`` for the slot conv: tile
+    bounds and the tiles' entries bucketed by slot, built once per operator
+    (one launch per training step, shared by every psi_2 use and backward)."""
+    plan = op.__dict__.setdefault('_slot_plan', {})
+    p = plan.get(S)
+    if p is None:
+        p = plan[S] = tuple(_backend.ops().slot_tile_plan(
+            op.tile_flag, op.rowptr, op.col, op.val, op.tile_window, S,
+            slot_conv_error(op.device)))
+    return p
+
+
+def slot_k_order(device):
+    """Position -> channel map of the kernel's 128-wide K axis: inside each
+    32-wide chunk, lane group q holds channels 4q..4q+3 and 16+4q..16+4q+3
+    (the rows an MFMA accumulator leaves in a lane, reused as the next
+    product's B operand without a shuffle)."""
+    key = str(device)
+    p = _SLOT_PERM.get(key)
+    if p is None:
+        c = torch.arange(4).view(4, 1, 1)
+        q = torch.arange(4).view(1, 4, 1)
+        j = torch.arange(8).view(1, 1, 8)
+        ch = 32 * c + torch.where(j < 4, 4 * q + j, 12 + 4 * q + j)
+        p = _SLOT_PERM[key] = ch.reshape(-1).to(device)
+    return p
+
+
+def slot_conv_image(w_lp, C, trans):
+    """``[S, C, C]`` weight image of the slot conv, memoised per forward
+    scope: forward rows = output channels, backward (``trans``) rows = input
+    channels; the K axis in :func:`slot_k_order`."""
+    from ..runtime.cache import cached
+
+    def build():
+        w3 = w_lp.view(w_lp.size(0), -1, C)          # [in, S, out]
+        img = w3.permute(1, 0, 2) if trans else w3.permute(1, 2, 0)
+        return (w_lp, img[:, :, slot_k_order(w_lp.device)].contiguous())
+    # Keyed by storage, not object: autograd hands every use a fresh
+    # ``detach()`` view of the same cached low-precision weight (the entry
+    # keeps it alive, so the address cannot be recycled within the scope).
+    key = ('slot_img', w_lp.data_ptr(), w_lp._version, tuple(w_lp.shape),
+           bool(trans))
+    return cached(key, build)[1]
 
 
 def _slot_major_t(w_lp):

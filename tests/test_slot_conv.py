@@ -1,0 +1,207 @@
+"""Fused slot convolution on graph-closed tiles (csrc/hip/slot_conv.hip).
+
+Oracle: the unfused fp32 expression ``A @ (x @ [W_0 | .. | W_{S-1}])`` of
+SplineConv (``/root/reference/dgmc/models/spline.py:49``) on the same
+bf16-rounded operands, forward and backward (dx, dY = A^T g, dW, dbias).
+"""
+import pytest
+import torch
+
+from deep_graph_matching_consensus_amd.ops import _backend
+from deep_graph_matching_consensus_amd.ops import sparse as sparse_ops
+from deep_graph_matching_consensus_amd.ops.sparse import (
+    SparseOperator, gemm_spmm, slot_conv_error, slot_conv_image,
+    slot_tile_plan)
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+C = 128
+
+
+@pytest.fixture(autouse=True)
+def _require_hip():
+    assert _backend.hip_available(), 'HIP extension must be built'
+    torch.manual_seed(0)
+    slot_conv_error(DEV).zero_()
+
+
+def _graph_batch(sizes, S, deg=4, seed=0):
+    """Disjoint union of random graphs with slot-structured entries (unique
+    (row, col) per slot, root slot S-1 on the diagonal) + graph-start
+    flags."""
+    g = torch.Generator().manual_seed(seed)
+    rows, cols, vals, flag = [], [], [], []
+    off = 0
+    for n in sizes:
+        flag += [1] + [0] * (n - 1)
+        E = n * deg
+        i = torch.randint(n, (E, ), generator=g)
+        j = torch.randint(n, (E, ), generator=g)
+        k = torch.randint(S - 1, (E, ), generator=g)
+        key = torch.unique((i * n + j) * S + k)
+        i, j, k = key // S // n, key // S % n, key % S
+        rows += [i + off]
+        cols += [(j + off) * S + k]
+        vals += [torch.rand(key.numel(), generator=g) / deg]
+        ar = torch.arange(n) + off
+        rows += [ar]
+        cols += [ar * S + S - 1]
+        vals += [torch.ones(n)]
+        off += n
+    N = off
+    op = SparseOperator.from_coo(torch.cat(rows).to(DEV),
+                                 torch.cat(cols).to(DEV),
+                                 torch.cat(vals).to(DEV), N, N * S)
+    flag = torch.tensor(flag, dtype=torch.uint8, device=DEV)
+    return op, flag
+
+
+def _sizes(total_graphs, n_max, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(1, n_max + 1, (total_graphs, ), generator=g).tolist()
+
+
+def _close(a, b, tol):
+    return float((a.float() - b).abs().max()) <= tol * float(b.abs().max()) \
+        + 1e-3
+
+
+@pytest.mark.parametrize('n_max,graphs,S', [(19, 300, 26), (8, 77, 5),
+                                            (33, 40, 26), (1, 50, 3)])
+def test_slot_conv_kernel_forward_backward(n_max, graphs, S):
+    ops = _backend.ops()
+    op, flag = _graph_batch(_sizes(graphs, n_max), S)
+    N = op.num_rows
+    window = 65 - n_max
+    x = torch.randn(N, C, device=DEV).bfloat16()
+    w_lp = (torch.randn(C, S * C, device=DEV) / C ** 0.5).bfloat16()
+    bias = torch.randn(C, device=DEV)
+    err = slot_conv_error(DEV)
+    op.tile_flag, op.tile_window = flag, window
+    plan = slot_tile_plan(op, S)
+    out = ops.slot_conv(x, *plan, S, slot_conv_image(w_lp, C, False), False,
+                        bias, True, torch.float32, None)
+    A = op.to_dense()
+    # The kernel rounds the operator's values to bf16 (MFMA operand).
+    A_lp = A.bfloat16().float()
+    y = (x.float() @ w_lp.float()).view(-1, C)
+    ref = (A_lp @ y + bias).relu()
+    assert int(err) == 0
+    assert _close(out, ref, 2e-2)
+
+    g = torch.randn(N, C, device=DEV).bfloat16()
+    dy = torch.empty(N * S, C, dtype=torch.bfloat16, device=DEV)
+    gx = ops.slot_conv(g, *plan, S, slot_conv_image(w_lp, C, True), True,
+                       None, False, torch.float32, dy)
+    dy_ref = A_lp.t() @ g.float()
+    gx_ref = dy_ref.view(N, -1) @ w_lp.float().t()
+    assert int(err) == 0
+    assert _close(dy, dy_ref, 1e-2)
+    assert _close(gx, gx_ref, 2e-2)
+
+
+def test_slot_conv_flags_oversized_tiles():
+    ops = _backend.ops()
+    S = 4
+    op, flag = _graph_batch([30] * 10, S)
+    N = op.num_rows
+    w_lp = torch.randn(C, S * C, device=DEV).bfloat16()
+    err = slot_conv_error(DEV)
+    x = torch.randn(N, C, device=DEV).bfloat16()
+    # window 64 with 30-node graphs: a tile can reach 64 + 29 rows.
+    ops.slot_tile_plan(flag, op.rowptr, op.col, op.val, 64, S, err)
+    assert int(err) & 1
+    err.zero_()
+    # Flags that split a graph: entries leave their tile.
+    bad = torch.ones_like(flag)
+    ops.slot_tile_plan(bad, op.rowptr, op.col, op.val, 1, S, err)
+    assert int(err) & 2
+    err.zero_()
+
+
+def test_gemm_spmm_uses_slot_conv_forward_backward(monkeypatch):
+    monkeypatch.setattr(sparse_ops, 'SLOT_CONV_BWD', True)
+    S = 26
+    op, flag = _graph_batch(_sizes(120, 19, seed=3), S, seed=3)
+    op.tile_flag, op.tile_window = flag, 65 - 19
+    N = op.num_rows
+    x = torch.randn(N, C, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(C, S * C, device=DEV) / C ** 0.5).requires_grad_()
+    bias = torch.randn(C, device=DEV, requires_grad=True)
+    w_lp = w.detach().bfloat16()
+    calls = []
+    real = _backend.ops().slot_conv
+
+    class _Spy(object):
+        def __getattr__(self, name):
+            if name == 'slot_conv':
+                def f(*a):
+                    calls.append(a[7])
+                    return real(*a)
+                return f
+            return getattr(torch.ops.dgmc_amd, name)
+    orig = _backend.ops
+    _backend.ops = lambda: _Spy()
+    try:
+        out = gemm_spmm(op, x, w, w_lp, C, bias=bias, relu=True)
+        g = torch.randn(N, C, device=DEV).bfloat16().float()
+        gx, gw, gb = torch.autograd.grad(out, (x, w, bias), g.bfloat16())
+    finally:
+        _backend.ops = orig
+    assert calls == [False, True]
+    assert int(slot_conv_error(DEV)) == 0
+    A = op.to_dense().bfloat16().float()
+    xf = x.detach().float().requires_grad_()
+    wf = w_lp.float().requires_grad_()
+    bf = bias.detach().clone().requires_grad_()
+    pre = A @ (xf @ wf).view(-1, C) + bf
+    assert _close(out, pre.relu(), 3e-2)
+    mask = (out.detach().float() > 0).float()
+    rx, rw, rb = torch.autograd.grad(pre, (xf, wf, bf), g * mask)
+    assert _close(gx, rx, 3e-2)
+    assert _close(gw, rw, 3e-2)
+    assert _close(gb, rb, 1e-2)
+
+
+def test_static_training_step_slot_conv_matches_unfused(monkeypatch):
+    """PascalVOC-shaped static batch (psi_2 = SplineCNN(128, 128)): one
+    forward/backward with the fused slot conv vs the GEMM + SpMM path."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.ops import plans
+
+    groups = make_keypoint_datasets(graphs=16, feature_dim=64, seed=2)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 64, seed=0)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(64, 64, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=3).to(DEV)
+    model.eval()   # no dropout: both runs see identical random draws
+    assert batcher.load()
+
+    def run(enabled):
+        monkeypatch.setattr(sparse_ops, 'SLOT_CONV', enabled)
+        plans.clear_plan_cache()
+        batch = batcher.materialize()
+        rows = torch.arange(batcher.cap_s, device=DEV)
+        torch.manual_seed(1)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            S_0, S_L = model(batch.x_s, batch.edge_index_s,
+                             batch.edge_attr_s, batch.x_s_batch, batch.x_t,
+                             batch.edge_index_t, batch.edge_attr_t,
+                             batch.x_t_batch)
+        y = torch.stack([rows, batch.y])
+        loss = model.loss(S_L, y, mask=batch.y_mask)
+        grads = torch.autograd.grad(loss, list(model.psi_2.parameters()))
+        return S_L.detach(), loss.detach(), grads
+
+    S_a, l_a, g_a = run(True)
+    S_b, l_b, g_b = run(False)
+    assert int(slot_conv_error(DEV)) == 0
+    assert torch.allclose(l_a, l_b, rtol=2e-2, atol=2e-2)
+    assert (S_a - S_b).abs().max() < 0.05
+    for a, b in zip(g_a, g_b):
+        assert _close(a, b.float(), 0.1)
