@@ -102,7 +102,9 @@ class GradBucketAllReducer(object):
         self._works = []
 
     def _launch(self, bi):
-        lo, hi = self._bucket_range[bi]
+        self._launch_range(*self._bucket_range[bi])
+
+    def _launch_range(self, lo, hi):
         buf = self.flat[lo:hi]
         if dist.get_backend(self.group) == 'nccl':
             work = dist.all_reduce(buf, op=dist.ReduceOp.AVG,
@@ -123,11 +125,16 @@ class GradBucketAllReducer(object):
         """Complete gradient synchronisation (call after ``backward``)."""
         if not self.distributed:
             return
-        launched = {i for i, c in enumerate(self._pending) if c == 0} \
-            if self.overlap else set()
-        for bi in range(len(self.buckets)):
-            if bi not in launched:
-                self._launch(bi)
+        if not self.overlap:
+            # Nothing in flight (e.g. backward replayed from a hipGraph):
+            # ONE collective over the whole flat buffer - the fewest RCCL
+            # launches and the largest messages for the xGMI rings.
+            self._launch_range(0, self.flat.numel())
+        else:
+            launched = {i for i, c in enumerate(self._pending) if c == 0}
+            for bi in range(len(self.buckets)):
+                if bi not in launched:
+                    self._launch(bi)
         for work, buf in self._works:
             work.wait()
             if buf is not None:

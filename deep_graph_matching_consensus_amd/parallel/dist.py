@@ -61,7 +61,10 @@ def init_distributed(backend=None, timeout_s=None):
         device = torch.device('cpu')
     if env_world_size() > 1 and not is_distributed():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        backend = backend or ('nccl' if use_cuda else 'gloo')
+        # DGMC_AMD_DIST_BACKEND=gloo runs GPU ranks over gloo (rehearsing
+        # the multi-rank path with several ranks on one device).
+        backend = backend or os.environ.get('DGMC_AMD_DIST_BACKEND') or \
+            ('nccl' if use_cuda else 'gloo')
         kwargs = dict(backend=backend,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if backend == 'nccl':
