@@ -78,6 +78,8 @@ def parse_args(argv=None):
     p.add_argument('--num-steps', type=int, default=10)
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--no-overlap', action='store_true')
+    p.add_argument('--no-buckets', action='store_true',
+                   help='one static capacity (no size buckets)')
     p.add_argument('--no-graph', action='store_true',
                    help='disable hipGraph capture of the training step')
     p.add_argument('--mode', default=None,
@@ -202,7 +204,8 @@ def main(argv=None):
                         groups[0].num_edge_features, device)
     trainer = PairTrainer(model, store, args.batch_size, lr=1e-3, mode=mode,
                           bf16=use_bf16, seed=args.seed,
-                          overlap=not args.no_overlap)
+                          overlap=not args.no_overlap,
+                          buckets=not args.no_buckets)
 
     def sync():
         if device.type == 'cuda':
@@ -231,7 +234,7 @@ def main(argv=None):
                                     x_dtype=store.x.dtype)
             test_hits = trainer.evaluate(test_store, args.eval_pairs)
     use_graph = trainer.mode == 'graph'
-    overflows = trainer.batcher.overflows if trainer.mode != 'eager' else 0
+    overflows = trainer.overflows if trainer.mode != 'eager' else 0
     run_stats = trainer.read_stats()
     stats = torch.tensor([run_stats['loss_sum'], run_stats['correct'],
                           run_stats['count']], dtype=torch.float64)

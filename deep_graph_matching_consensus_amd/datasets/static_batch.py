@@ -52,7 +52,7 @@ class StaticPairBatcher(object):
     """
 
     def __init__(self, store, batch_size, sources=None, seed=0,
-                 probe_batches=256, headroom=1.04, n_max=None):
+                 probe_batches=256, headroom=1.04, n_max=None, caps=None):
         if not _backend.host_available():
             raise RuntimeError('StaticPairBatcher needs the native host '
                                'library (_C_host.so); build it first')
@@ -63,7 +63,11 @@ class StaticPairBatcher(object):
             else np.asarray(sources, dtype=np.int64)
         counts = store.node_ptr[1:] - store.node_ptr[:-1]
         self.n_max = int(counts.max()) if n_max is None else int(n_max)
-        self._size_capacities(probe_batches, headroom)
+        if caps is None:
+            self._size_capacities(probe_batches, headroom)
+        else:
+            self.cap_s, self.cap_t, self.ecap_s, self.ecap_t = \
+                (int(c) for c in caps)
         self.device = store.device
 
         # Zero feature row / zero edge-attr row appended once for padding.
@@ -109,6 +113,20 @@ class StaticPairBatcher(object):
         self.cap_t = _round_up(mx[1] * headroom + 1, 64)
         self.ecap_s = _round_up(mx[2] * headroom, 256)
         self.ecap_t = _round_up(mx[3] * headroom, 256)
+
+    @property
+    def caps(self):
+        return (self.cap_s, self.cap_t, self.ecap_s, self.ecap_t)
+
+    def fits(self, s_ids, t_ids):
+        """Whether the pair batch ``(s_ids, t_ids)`` fits the capacities
+        (host-side sizes; the collator applies the same bounds)."""
+        st = self.store
+        n = st.node_ptr[1:] - st.node_ptr[:-1]
+        e = st.edge_ptr[1:] - st.edge_ptr[:-1]
+        return (n[s_ids].sum() < self.cap_s and n[t_ids].sum() < self.cap_t
+                and e[s_ids].sum() <= self.ecap_s and
+                e[t_ids].sum() <= self.ecap_t)
 
     def _views(self):
         cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
@@ -211,6 +229,40 @@ class StaticPairBatcher(object):
                 'ecap_t={})').format(type(self).__name__, self.B, self.n_max,
                                      self.cap_s, self.cap_t, self.ecap_s,
                                      self.ecap_t)
+
+
+def bucket_capacities(store, batch_size, sources=None, z=(-0.5, 0.5, 1.5),
+                      probe_batches=512, seed=12345):
+    r"""Capacity tuples ``(cap_s, cap_t, ecap_s, ecap_t)`` of smaller
+    static-batch size buckets at ``mean + z * std`` of every size (probed on
+    random pair batches), ascending.
+
+    One fixed capacity must cover the largest batch, so a single bucket pads
+    the average PascalVOC-shaped batch by ~8 % (11008 rows for 10171 real);
+    with buckets at z = -0.5, 0.5, 1.5 plus the max-sized one the average
+    capacity drops to ~10330 rows - every node-proportional kernel of the
+    step (encoder GEMMs, SpMMs, dY stacks) shrinks by ~6 %.
+    """
+    n = store.node_ptr[1:] - store.node_ptr[:-1]
+    e = store.edge_ptr[1:] - store.edge_ptr[:-1]
+    src = np.arange(store.num_graphs) if sources is None \
+        else np.asarray(sources, dtype=np.int64)
+    rng = np.random.default_rng(seed)
+    sizes = []
+    for _ in range(probe_batches):
+        s = rng.choice(src, size=batch_size, replace=len(src) < batch_size)
+        t = store.sample_partners(s, rng)
+        sizes.append((n[s].sum(), n[t].sum(), e[s].sum(), e[t].sum()))
+    sizes = np.asarray(sizes, dtype=np.float64)
+    mu, sd = sizes.mean(0), sizes.std(0)
+    out = []
+    for zz in sorted(z):
+        c = mu + zz * sd
+        caps = (_round_up(c[0] + 1, 64), _round_up(c[1] + 1, 64),
+                _round_up(c[2], 256), _round_up(c[3], 256))
+        if not out or caps != out[-1]:
+            out.append(caps)
+    return out
 
 
 class _StaticSlotOperator(SparseOperator):

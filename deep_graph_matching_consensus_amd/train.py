@@ -27,7 +27,7 @@ import torch
 
 from . import parallel
 from .datasets.device_loader import DevicePairLoader
-from .datasets.static_batch import StaticPairBatcher
+from .datasets.static_batch import StaticPairBatcher, bucket_capacities
 from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
 
@@ -52,7 +52,7 @@ class PairTrainer(object):
 
     def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
                  bf16=True, seed=0, overlap=True, sources=None,
-                 guard_nonfinite=True):
+                 guard_nonfinite=True, buckets=True):
         self.model = model
         self.store = store
         self.device = store.device
@@ -86,11 +86,27 @@ class PairTrainer(object):
                                            seed=data_seed)
             self._batches = self.loader.forever()
         else:
+            # The largest bucket covers every batch (and owns the sampler);
+            # in graph mode smaller size buckets, each with its own static
+            # buffers and captured graph, cut the padding (see
+            # datasets/static_batch.py::bucket_capacities).
             self.batcher = StaticPairBatcher(store, batch_size,
                                              sources=sources, seed=data_seed)
-            self._rows = torch.arange(self.batcher.cap_s, device=self.device)
-            self._graph = GraphedStep(self._static_body, warmup=2) \
+            self.batchers = [self.batcher]
+            if mode == 'graph' and buckets:
+                caps = [c for c in bucket_capacities(store, batch_size,
+                                                     sources)
+                        if all(a < b for a, b in zip(c, self.batcher.caps))]
+                self.batchers = [
+                    StaticPairBatcher(store, batch_size, sources=sources,
+                                      seed=data_seed, caps=c)
+                    for c in caps] + [self.batcher]
+            self._rows = [torch.arange(b.cap_s, device=self.device)
+                          for b in self.batchers]
+            self._graphs = [GraphedStep(self._bucket_body(i), warmup=2)
+                            for i in range(len(self.batchers))] \
                 if mode == 'graph' else None
+            self._captured = False
 
     # ------------------------------------------------------------------
     def _autocast(self):
@@ -137,13 +153,47 @@ class PairTrainer(object):
                 return
         self.optimizer.step()
 
-    def _static_body(self):
+    def _static_body(self, bucket=-1):
         self.reducer.flat.zero_()
-        batch = self.batcher.materialize()
-        self._forward_backward(batch, self._rows, batch.y_mask)
+        batch = self.batchers[bucket].materialize()
+        self._forward_backward(batch, self._rows[bucket], batch.y_mask)
         if self.world == 1:
             self._check_finite()
             self._optimizer_step()
+
+    def _bucket_body(self, i):
+        return lambda: self._static_body(i)
+
+    @property
+    def overflows(self):
+        """Batches that fitted no static capacity (resampled)."""
+        return sum(b.overflows for b in getattr(self, 'batchers', []))
+
+    def _load_next(self):
+        """Stage the next batch into the smallest bucket it fits; returns
+        the bucket index."""
+        while True:
+            s, t = self.batcher.next_ids()
+            for i, b in enumerate(self.batchers):
+                if b is self.batcher or b.fits(s, t):
+                    if b.load(s, t):
+                        return i
+                    break
+            else:
+                self.batcher.overflows += 1
+
+    def _capture_all(self):
+        """Capture every bucket's graph up front (so no capture ever lands
+        in a timed step): each is staged with a batch that fits it."""
+        for i, b in enumerate(self.batchers):
+            for _ in range(10000):
+                s, t = self.batcher.next_ids()
+                if b.fits(s, t) and b.load(s, t):
+                    break
+            else:
+                raise RuntimeError('no batch fits bucket {}'.format(b))
+            self._graphs[i].capture()
+        self._captured = True
 
     def step(self):
         """One training step (data, forward, backward, all-reduce, Adam)."""
@@ -161,15 +211,16 @@ class PairTrainer(object):
                 self._check_finite()
                 self._optimizer_step()
         else:
+            if self._graphs is not None and not self._captured:
+                self._capture_all()
             with trace_range('train.load'):
-                while not self.batcher.load():
-                    pass
-            with trace_range('train.graph_replay' if self._graph is not None
+                bucket = self._load_next()
+            with trace_range('train.graph_replay' if self._graphs is not None
                              else 'train.forward_backward'):
-                if self._graph is not None:
-                    self._graph()
+                if self._graphs is not None:
+                    self._graphs[bucket]()
                 else:
-                    self._static_body()
+                    self._static_body(bucket)
             if self.world > 1:
                 with trace_range('train.allreduce'):
                     self.reducer.finish()
