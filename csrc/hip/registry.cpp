@@ -106,6 +106,11 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const c10::optional<at::Tensor>& Z);
 at::Tensor gather_gemm_stamps();
 at::Tensor slot_conv_stamps();
+at::Tensor tr16_probe(const at::Tensor& like);
+at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
+                      const at::Tensor& esrc, const at::Tensor& edst,
+                      const at::Tensor& evals, const at::Tensor& soff,
+                      int64_t U, int64_t nsplit);
 at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      const at::Tensor& soff, const at::Tensor& ecode,
                      const at::Tensor& eval, int64_t S, const at::Tensor& Wimg,
@@ -190,6 +195,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
   m.def("gather_gemm_stamps() -> Tensor");
   m.def("slot_conv_stamps() -> Tensor");
+  m.def("tr16_probe(Tensor like) -> Tensor");
+  m.def(
+      "slot_wgrad(Tensor X, Tensor G, Tensor esrc, Tensor edst, Tensor evals, "
+      "Tensor soff, int U, int nsplit) -> Tensor");
   m.def(
       "slot_conv(Tensor X, Tensor tiles, Tensor soff, Tensor ecode, Tensor "
       "eval, int S, Tensor Wimg, bool trans, Tensor? bias, bool relu, "
@@ -239,6 +248,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("slot_conv", &dgmc::slot_conv);
   m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
+  m.impl("slot_wgrad", &dgmc::slot_wgrad);
+  m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);

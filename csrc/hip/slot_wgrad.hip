@@ -1,0 +1,254 @@
+// Weight gradient of a slot-structured graph convolution WITHOUT the
+// per-slot gradient stack:
+//
+//   dW_k = sum_u sum_{e in slot k} a_e X_u[j_e]^T G_u[i_e]      (128 x 128)
+//
+// for every slot k of SplineConv's operator (/root/reference/dgmc/models/
+// spline.py:49; entry e = (target i, source j, slot k, value a)), summed over
+// the U uses of the layer inside the consensus loop (runtime/loopgrad.py
+// keeps each use's input X_u and output gradient G_u, [N, 128] each).
+//
+// The unfused backward writes dY = A^T G ([N*S, 128], 73 MB per psi_2 use)
+// with an SpMM and contracts the 10-use stack with one long-K GEMM
+// (X^T dY: 730 MB read).  Here the reduction runs directly over the
+// (use, entry) pairs of each slot: rows X_u[j_e] (scaled by a_e) and
+// G_u[i_e] are gathered (L2/MALL-resident: the stacks are 28 MB) into LDS
+// and contracted on MFMA - no dY is ever written.
+//
+// Mapping (gfx950): one workgroup = 8 waves (2 per SIMD) = one (slot,
+// split) pair; K = 32 pairs per step; the 128 x 128 fp32 result is split
+// 2 (channels) x 4 (outputs) over the waves (64 x 32 each).  Operands are
+// staged row-major ([pair][channel], 256-B rows, XOR-swizzled) and read
+// K-contiguous with ds_read_b64_tr_b16 (CDNA4 transposed LDS read) for both
+// the A (X^T) and B (G) fragments of v_mfma_f32_16x16x32_bf16.  Row loads
+// are register-prefetched two steps ahead; LDS is double-buffered; pairs
+// iterate entry-chunk-major / use-minor so each thread's (j, i, a) is loaded
+// once per U steps.  Per-split partials are folded by reduce_add_rows
+// (deterministic; no float atomics).
+#include "common.h"
+
+namespace dgmc {
+
+namespace {
+
+typedef __bf16 sw_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 sw_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float sw_f32x4 __attribute__((ext_vector_type(4)));
+typedef short sw_i16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kSwC = 128;          // channels (in == out)
+constexpr int kSwK = 32;           // pairs per step
+constexpr int kSwThreads = 512;    // 8 waves
+constexpr int kSwTile = kSwK * kSwC;   // bf16 elements per staged operand
+
+// Byte offset of 16-byte chunk `ch` of row `row` in a [rows][128 bf16]
+// image (256-B rows): the XOR keeps both ds_write_b128 row stores and the
+// 4-row transposed reads bank-conflict free (cdna_hip_programming.md T10,
+// image (b)).
+__device__ __forceinline__ int sw_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// 16x16x32 operand fragment (8 K-consecutive elements of one column) of a
+// row-major [K][128] LDS image: rows 8g..8g+7 of column block `cb` (16
+// columns) for lane group g - two transposed 4-row reads.
+__device__ __forceinline__ sw_bf16x8 sw_frag(const DGMC_LDS char* img,
+                                             int cb, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  sw_bf16x4 v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q;
+    const DGMC_LDS char* a = img + sw_off(row, 2 * cb + (p >> 1)) + 8 * (p & 1);
+    // Whole-vector bit casts: element-wise short->bf16 conversion of the
+    // v4i16 result was miscompiled (lanes 2-3 replaced by 0-1).
+    v[h] = __builtin_bit_cast(
+        sw_bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                       (DGMC_LDS sw_i16x4*)a));
+  }
+  return __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
+    const __hip_bfloat16* __restrict__ Xg, const __hip_bfloat16* __restrict__ Gg,
+    const int* __restrict__ esrc, const int* __restrict__ edst,
+    const float* __restrict__ evals, const int* __restrict__ soff, int S,
+    int U, int N, int nsplit, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][kSwTile * 2];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int k = blockIdx.x / nsplit, s = blockIdx.x % nsplit;
+  const int e_lo = soff[k], Ek = soff[k + 1] - e_lo;
+  const int nch = (Ek + kSwK - 1) / kSwK;
+  const int ch0 = (int)((long long)nch * s / nsplit);
+  const int ch1 = (int)((long long)nch * (s + 1) / nsplit);
+  const int steps = (ch1 - ch0) * U;
+  const __bf16* X = reinterpret_cast<const __bf16*>(Xg);
+  const __bf16* G = reinterpret_cast<const __bf16*>(Gg);
+
+  // Staging role: thread -> (pair row r, 16-byte chunk c) of both operands.
+  const int r = tid >> 4, c = tid & 15;
+  auto entry = [&](int chunk, int& j, int& i, float& a) {
+    const int e = chunk * kSwK + r;
+    const bool v = chunk < ch1 && e < Ek;
+    j = v ? esrc[e_lo + e] : 0;
+    i = v ? edst[e_lo + e] : 0;
+    a = v ? evals[e_lo + e] : 0.f;
+  };
+  // Register pipeline: loads of step t+2 are issued at step t.
+  int ej, ei;
+  float ea;
+  int nj, ni;
+  float na;
+  entry(ch0, ej, ei, ea);
+  entry(ch0 + 1, nj, ni, na);
+  sw_bf16x8 xr[2], gr[2];
+  float ar[2];
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+    const int u = t % U;
+    if (u == 0 && t > 0) {          // next entry chunk (loaded U steps ago)
+      ej = nj; ei = ni; ea = na;
+      entry(ch0 + t / U + 1, nj, ni, na);
+    }
+    const size_t base = (size_t)u * N;
+    xr[slot] = *reinterpret_cast<const sw_bf16x8*>(X + (base + ej) * kSwC +
+                                                  8 * c);
+    gr[slot] = *reinterpret_cast<const sw_bf16x8*>(G + (base + ei) * kSwC +
+                                                  8 * c);
+    ar[slot] = ea;
+  };
+  auto stage = [&](int buf, int slot) __attribute__((always_inline)) {
+    sw_bf16x8 xs;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      xs[q] = (__bf16)((float)xr[slot][q] * ar[slot]);
+    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+        (DGMC_LDS char*)lds[buf][0] + sw_off(r, c)) = xs;
+    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+        (DGMC_LDS char*)lds[buf][1] + sw_off(r, c)) = gr[slot];
+  };
+
+  // Accumulators: wave (mi, ni) owns channels 64mi.., outputs 32ni...
+  const int mi = wave >> 2, nw = wave & 3;
+  sw_f32x4 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (steps > 0) {
+    issue(0, 0);
+    if (steps > 1) issue(1, 1);
+    stage(0, 0);
+    __syncthreads();
+    for (int t = 0; t < steps; ++t) {
+      const int buf = t & 1;
+      if (t + 2 < steps) issue(t + 2, t & 1);      // regs of step t: staged
+      const DGMC_LDS char* A = (const DGMC_LDS char*)lds[buf][0];
+      const DGMC_LDS char* B = (const DGMC_LDS char*)lds[buf][1];
+      sw_bf16x8 af[4], bf[2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) af[a] = sw_frag(A, 4 * mi + a, lane);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bf[b] = sw_frag(B, 2 * nw + b, lane);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf[b],
+                                                              acc[a][b], 0, 0,
+                                                              0);
+      if (t + 1 < steps) stage(buf ^ 1, (t + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // Partial [split][slot][channel][output] (fp32): lane holds rows
+  // 4(lane/16) + r of column lane%16 of each 16x16 block.
+  float* out = part + ((size_t)s * S + k) * kSwC * kSwC;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 64 * mi + 16 * a + 4 * (lane >> 4) + q;
+        const int colo = 32 * nw + 16 * b + (lane & 15);
+        out[(size_t)row * kSwC + colo] = acc[a][b][q];
+      }
+}
+
+// X, G [U*N, 128] bf16 (use-major stacks); esrc/edst [E] int32 source /
+// target node of each operator entry, evals [E] fp32, all grouped by slot
+// with offsets soff [S+1]; returns dW [S, 128, 128] fp32 (channel, output).
+at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
+                      const at::Tensor& esrc, const at::Tensor& edst,
+                      const at::Tensor& evals, const at::Tensor& soff,
+                      int64_t U, int64_t nsplit) {
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kBFloat16 &&
+                  X.is_contiguous() && X.dim() == 2 && X.size(1) == kSwC &&
+                  G.sizes() == X.sizes() &&
+                  G.scalar_type() == at::kBFloat16 && G.is_contiguous(),
+              "slot_wgrad: X, G contiguous bf16 [U*N, 128]");
+  TORCH_CHECK(U >= 1 && X.size(0) % U == 0, "slot_wgrad: rows % U");
+  TORCH_CHECK(esrc.scalar_type() == at::kInt &&
+                  edst.scalar_type() == at::kInt &&
+                  evals.scalar_type() == at::kFloat &&
+                  soff.scalar_type() == at::kInt && esrc.is_contiguous() &&
+                  edst.is_contiguous() && evals.is_contiguous() &&
+                  soff.is_contiguous() && esrc.numel() == edst.numel() &&
+                  esrc.numel() == evals.numel(),
+              "slot_wgrad: int32 esrc/edst/soff, fp32 evals");
+  TORCH_CHECK(aligned16(X.data_ptr()) && aligned16(G.data_ptr()),
+              "slot_wgrad: 16-byte aligned operands");
+  const int64_t S = soff.numel() - 1;
+  TORCH_CHECK(S >= 1 && nsplit >= 1 && S * nsplit < (1 << 30),
+              "slot_wgrad: slots / splits");
+  const int64_t N = X.size(0) / U;
+  TORCH_CHECK(N * U < INT32_MAX, "slot_wgrad: size range");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  at::Tensor part = at::empty({nsplit, S * kSwC * kSwC},
+                              X.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(slot_wgrad_kernel, dim3(S * nsplit), dim3(kSwThreads), 0,
+                     stream(),
+                     reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
+                     reinterpret_cast<const __hip_bfloat16*>(G.data_ptr()),
+                     esrc.data_ptr<int>(), edst.data_ptr<int>(),
+                     evals.data_ptr<float>(), soff.data_ptr<int>(), (int)S,
+                     (int)U, (int)N, (int)nsplit, part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return part;
+}
+
+}  // namespace dgmc
+
+namespace dgmc {
+
+// Probe of ds_read_b64_tr_b16 semantics (tools/debug/wgrad_debug.py): LDS
+// tile [16 rows][16 cols] int16 = 100 * row + col; lane 4q+p of each 16-lane
+// group addresses row (q + 4 * (group & 1)), columns 4p..4p+3.  Returns the
+// four elements every lane receives.
+__global__ void tr16_probe_kernel(short* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) short tile[16 * 16];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 256; i += 64) tile[i] = (short)(100 * (i / 16) + i % 16);
+  __syncthreads();
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int row = q + 4 * (g & 1);
+  typedef short i16x4 __attribute__((ext_vector_type(4)));
+  const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (DGMC_LDS i16x4*)((DGMC_LDS short*)tile + row * 16 + 4 * p));
+  for (int j = 0; j < 4; ++j) out[lane * 4 + j] = v[j];
+}
+
+at::Tensor tr16_probe(const at::Tensor& like) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  at::Tensor out = at::empty({64, 4}, like.options().dtype(at::kShort));
+  hipLaunchKernelGGL(tr16_probe_kernel, dim3(1), dim3(64), 0, stream(),
+                     out.data_ptr<short>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+}  // namespace dgmc

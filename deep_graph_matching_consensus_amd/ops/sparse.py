@@ -193,11 +193,12 @@ class _GemmSpMM(torch.autograd.Function):
         K = xc.size(1)
         S = w_lp.size(1) // C
         ctx.img_b = None
-        if _slot_conv_ok(op, xc, K, C, S):
+        ctx.slot = _slot_conv_ok(op, xc, K, C, S)
+        if ctx.slot:
             # Graph-closed tiles: Z_k = A_k x and Z_k W_k on MFMA, Y and Z
             # never materialised (csrc/hip/slot_conv.hip).
             img = slot_conv_image(w_lp, C, trans=False)
-            if SLOT_CONV_BWD:
+            if SLOT_CONV_BWD or (SLOT_WGRAD and loop is not None):
                 ctx.img_b = slot_conv_image(w_lp, C, trans=True)
             out = _backend.ops().slot_conv(
                 xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
@@ -251,10 +252,34 @@ class _GemmSpMM(torch.autograd.Function):
                 if loop is not None:
                     loop.add_to('b', db)
             g = g.to(w_lp.dtype)
-        # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
         op = ctx.op
         K = xc.size(1)
         S = w_lp.size(1) // C
+        if (ctx.slot and loop is not None and SLOT_WGRAD and
+                g.dtype == torch.bfloat16 and ctx.img_b is not None):
+            # 2'. dx by the transposed slot conv; dW from the kept (x, g')
+            #     pairs of all uses - dY is never formed.
+            gx = gw = gb = None
+            if ctx.needs_input_grad[0]:
+                gx = _backend.ops().slot_conv(
+                    g.contiguous(), *slot_tile_plan(op, S), S, ctx.img_b,
+                    True, None, False, g.dtype, None)
+                if gx.dtype != ctx.x_dtype:
+                    gx = gx.to(ctx.x_dtype)
+            loop.keep('x', idx, xc)
+            loop.keep('g', idx, g)
+            if loop.arrive():
+                if ctx.needs_input_grad[1]:
+                    dW = slot_weight_grad(loop.kept('x').contiguous(),
+                                          loop.kept('g').contiguous(), op, S,
+                                          loop.uses)
+                    gw = dW.permute(1, 0, 2).reshape(K, S * C)
+                    gw = gw.to(ctx.w_dtype)
+                if need_b:
+                    gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+                loop.release()
+            return gx, gw, None, gb, None, None, None, None
+        # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
         slot = ctx.img_b is not None and ctx.needs_input_grad[0] and \
             g.dtype == torch.bfloat16
         fused = not slot and ctx.needs_input_grad[0] and _fused_ok(g, C, K)
@@ -341,6 +366,12 @@ def _contig(t):
 _SLOT_MODE = os.environ.get('DGMC_AMD_SLOT_CONV', 'fwd')
 SLOT_CONV = _SLOT_MODE in ('1', 'fwd')
 SLOT_CONV_BWD = _SLOT_MODE == '1'
+# Loop-shared weight gradient straight from the kept (x, g') pairs of every
+# use (csrc/hip/slot_wgrad.hip) - no dY = A^T g' stack - with the fused
+# transposed slot conv for dx.  Opt-in (DGMC_AMD_SLOT_WGRAD=1): correct
+# (tests/test_slot_conv.py) but not yet faster than the SpMM dY stack +
+# long-K GEMM it replaces (docs/performance.md).
+SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '0') == '1'
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}
@@ -375,6 +406,42 @@ def slot_tile_plan(op, S):
             op.tile_flag, op.rowptr, op.col, op.val, op.tile_window, S,
             slot_conv_error(op.device)))
     return p
+
+
+def slot_pair_lists(op, S):
+    """``(esrc, edst, evals, soff)``: the entries of ``op`` grouped by slot
+    (source node, target node, value; slot offsets), built once per operator
+    on the device without host synchronisation."""
+    cache = op.__dict__.setdefault('_slot_pairs', {})
+    p = cache.get(S)
+    if p is None:
+        col = op.col.long()
+        k = col % S
+        perm = torch.argsort(k, stable=True)
+        cnt = torch.zeros(S, dtype=torch.long, device=col.device)
+        cnt.index_add_(0, k, torch.ones_like(k))
+        soff = torch.zeros(S + 1, dtype=torch.int32, device=col.device)
+        soff[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+        p = cache[S] = ((col // S)[perm].to(torch.int32).contiguous(),
+                        op.row[perm].to(torch.int32).contiguous(),
+                        op.val[perm].contiguous(), soff)
+    return p
+
+
+SLOT_WGRAD_SPLITS = 20
+
+
+def slot_weight_grad(X, G, op, S, uses, nsplit=None):
+    """``dW [S, C, C]`` (fp32) with ``dW_k = sum_u sum_{e in k} a_e
+    X_u[j_e]^T G_u[i_e]`` for use-major stacks ``X, G [uses * N, C]``."""
+    nsplit = nsplit or SLOT_WGRAD_SPLITS
+    part = _backend.ops().slot_wgrad(X, G, *slot_pair_lists(op, S), uses,
+                                     nsplit)
+    out = torch.empty(S * _SLOT_C, _SLOT_C, dtype=torch.float32,
+                      device=X.device)
+    _backend.ops().reduce_add_rows(part.view(nsplit, S * _SLOT_C, _SLOT_C),
+                                   out, False)
+    return out.view(S, _SLOT_C, _SLOT_C)
 
 
 def slot_k_order(device):

@@ -205,3 +205,64 @@ def test_static_training_step_slot_conv_matches_unfused(monkeypatch):
     assert (S_a - S_b).abs().max() < 0.05
     for a, b in zip(g_a, g_b):
         assert _close(a, b.float(), 0.1)
+
+
+@pytest.mark.parametrize('uses,S,n_max',
+                         [(3, 26, 19), (1, 5, 8), (10, 26, 12)])
+def test_slot_weight_grad_matches_dense(uses, S, n_max):
+    from deep_graph_matching_consensus_amd.ops.sparse import slot_weight_grad
+    op, flag = _graph_batch(_sizes(90, n_max, seed=5), S, seed=5)
+    N = op.num_rows
+    X = torch.randn(uses * N, C, device=DEV).bfloat16()
+    G = torch.randn(uses * N, C, device=DEV).bfloat16()
+    dW = slot_weight_grad(X, G, op, S, uses, nsplit=3)
+    A = op.to_dense()                                   # [N, N*S]
+    ref = torch.zeros(S, C, C, device=DEV)
+    for u in range(uses):
+        Xu, Gu = X[u * N:(u + 1) * N].float(), G[u * N:(u + 1) * N].float()
+        dY = (A.t() @ Gu).view(N, S, C)                 # dY[j, k, :]
+        ref += torch.einsum('jc,jko->kco', Xu, dY)
+    # The kernel rounds a_e * X to bf16 (MFMA operand).
+    assert _close(dW, ref, 2e-2)
+
+
+def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch):
+    """num_steps=4 consensus loop on a static batch: psi_2 weight gradients
+    from the slot wgrad kernel vs the dY stack + GEMM path."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.ops import plans
+
+    groups = make_keypoint_datasets(graphs=16, feature_dim=64, seed=3)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 64, seed=1)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(64, 64, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=4).to(DEV)
+    model.eval()
+    assert batcher.load()
+
+    def run(enabled):
+        monkeypatch.setattr(sparse_ops, 'SLOT_WGRAD', enabled)
+        plans.clear_plan_cache()
+        batch = batcher.materialize()
+        rows = torch.arange(batcher.cap_s, device=DEV)
+        torch.manual_seed(1)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            S_0, S_L = model(batch.x_s, batch.edge_index_s,
+                             batch.edge_attr_s, batch.x_s_batch, batch.x_t,
+                             batch.edge_index_t, batch.edge_attr_t,
+                             batch.x_t_batch)
+        y = torch.stack([rows, batch.y])
+        loss = model.loss(S_L, y, mask=batch.y_mask)
+        return torch.autograd.grad(loss, list(model.parameters()))
+
+    g_a = run(True)
+    g_b = run(False)
+    assert int(slot_conv_error(DEV)) == 0
+    for a, b in zip(g_a, g_b):
+        assert torch.isfinite(a).all()
+        assert _close(a, b.float(), 0.1)

@@ -107,6 +107,22 @@ def main():
         res['dx_splitk%d_us' % sk] = timeit(split, args.reps)
     res['y_gemm_us'] = timeit(lambda: x @ w_lp, args.reps)
     res['unfused_bwd_us'] = timeit(unfused_bwd, args.reps)
+    # Weight gradient over 10 loop uses: slot_wgrad vs dY stack + GEMM.
+    from deep_graph_matching_consensus_amd.ops.sparse import (
+        slot_pair_lists, slot_weight_grad)
+    from deep_graph_matching_consensus_amd.ops.gemm import matmul_tn_fp32
+    U = 10
+    Xs = torch.randn(U * N, C, device=dev).bfloat16()
+    Gs = torch.randn(U * N, C, device=dev).bfloat16()
+    slot_pair_lists(op, S)
+    res['pair_lists_us'] = timeit(lambda: (op.__dict__.pop('_slot_pairs',
+                                                           None),
+                                           slot_pair_lists(op, S)), 10)
+    for ns in (10, 20, 40):
+        res['wgrad_slot_s%d_us' % ns] = timeit(
+            lambda: slot_weight_grad(Xs, Gs, op, S, U, nsplit=ns), 10)
+    dYs = torch.randn(U * N, S * C, device=dev).bfloat16()
+    res['wgrad_gemm_us'] = timeit(lambda: matmul_tn_fp32(Xs, dYs), 10)
     res['err'] = int(err)
     if res['debug'] & 8:
         # Stamps of the last launch (unfused ran after: re-run fwd once).
