@@ -107,6 +107,9 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
 at::Tensor gather_gemm_stamps();
 at::Tensor slot_conv_stamps();
 at::Tensor tr16_probe(const at::Tensor& like);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_pair_lists(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& val,
+    const at::Tensor& row, int64_t S);
 at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                       const at::Tensor& esrc, const at::Tensor& edst,
                       const at::Tensor& evals, const at::Tensor& soff,
@@ -197,6 +200,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("slot_conv_stamps() -> Tensor");
   m.def("tr16_probe(Tensor like) -> Tensor");
   m.def(
+      "slot_pair_lists(Tensor rowptr, Tensor col, Tensor val, Tensor row, int "
+      "S) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
       "slot_wgrad(Tensor X, Tensor G, Tensor esrc, Tensor edst, Tensor evals, "
       "Tensor soff, int U, int nsplit) -> Tensor");
   m.def(
@@ -250,6 +256,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
   m.impl("slot_wgrad", &dgmc::slot_wgrad);
   m.impl("tr16_probe", &dgmc::tr16_probe);
+  m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);

@@ -27,6 +27,8 @@
 // (deterministic; no float atomics).
 #include "common.h"
 
+#include <type_traits>
+
 namespace dgmc {
 
 namespace {
@@ -40,6 +42,7 @@ constexpr int kSwC = 128;          // channels (in == out)
 constexpr int kSwK = 32;           // pairs per step
 constexpr int kSwThreads = 512;    // 8 waves
 constexpr int kSwTile = kSwK * kSwC;   // bf16 elements per staged operand
+constexpr int kSwEB = 1024;        // entries staged in LDS per batch
 
 // Byte offset of 16-byte chunk `ch` of row `row` in a [rows][128 bf16]
 // image (256-B rows): the XOR keeps both ds_write_b128 row stores and the
@@ -83,53 +86,21 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
   const int nch = (Ek + kSwK - 1) / kSwK;
   const int ch0 = (int)((long long)nch * s / nsplit);
   const int ch1 = (int)((long long)nch * (s + 1) / nsplit);
-  const int steps = (ch1 - ch0) * U;
   const __bf16* X = reinterpret_cast<const __bf16*>(Xg);
   const __bf16* G = reinterpret_cast<const __bf16*>(Gg);
 
   // Staging role: thread -> (pair row r, 16-byte chunk c) of both operands.
   const int r = tid >> 4, c = tid & 15;
-  auto entry = [&](int chunk, int& j, int& i, float& a) {
-    const int e = chunk * kSwK + r;
-    const bool v = chunk < ch1 && e < Ek;
-    j = v ? esrc[e_lo + e] : 0;
-    i = v ? edst[e_lo + e] : 0;
-    a = v ? evals[e_lo + e] : 0.f;
-  };
-  // Register pipeline: loads of step t+2 are issued at step t.
-  int ej, ei;
-  float ea;
-  int nj, ni;
-  float na;
-  entry(ch0, ej, ei, ea);
-  entry(ch0 + 1, nj, ni, na);
+  // The split's entries (source, target, value) are staged in LDS once per
+  // batch of kSwEB, so the step loop issues only the row gathers (no
+  // dependent index loads, no branches: the compiler keeps the register
+  // prefetch two steps deep instead of draining vmcnt every step).
+  __shared__ int ej_s[kSwEB], ei_s[kSwEB];
+  __shared__ float ea_s[kSwEB];
   sw_bf16x8 xr[2], gr[2];
   float ar[2];
-  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
-    const int u = t % U;
-    if (u == 0 && t > 0) {          // next entry chunk (loaded U steps ago)
-      ej = nj; ei = ni; ea = na;
-      entry(ch0 + t / U + 1, nj, ni, na);
-    }
-    const size_t base = (size_t)u * N;
-    xr[slot] = *reinterpret_cast<const sw_bf16x8*>(X + (base + ej) * kSwC +
-                                                  8 * c);
-    gr[slot] = *reinterpret_cast<const sw_bf16x8*>(G + (base + ei) * kSwC +
-                                                  8 * c);
-    ar[slot] = ea;
-  };
-  auto stage = [&](int buf, int slot) __attribute__((always_inline)) {
-    sw_bf16x8 xs;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      xs[q] = (__bf16)((float)xr[slot][q] * ar[slot]);
-    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
-        (DGMC_LDS char*)lds[buf][0] + sw_off(r, c)) = xs;
-    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
-        (DGMC_LDS char*)lds[buf][1] + sw_off(r, c)) = gr[slot];
-  };
 
-  // Accumulators: wave (mi, ni) owns channels 64mi.., outputs 32ni...
+  // Accumulators: wave (mi, nw) owns channels 64mi.., outputs 32nw...
   const int mi = wave >> 2, nw = wave & 3;
   sw_f32x4 acc[4][2];
 #pragma unroll
@@ -137,14 +108,62 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (steps > 0) {
-    issue(0, 0);
-    if (steps > 1) issue(1, 1);
-    stage(0, 0);
+  for (int cb0 = ch0; cb0 < ch1; cb0 += kSwEB / kSwK) {
+    const int cb1 = min(ch1, cb0 + kSwEB / kSwK);
+    const int nent = (cb1 - cb0) * kSwK;
+    __syncthreads();                      // previous batch fully consumed
+    for (int i = tid; i < kSwEB; i += kSwThreads) {
+      const int e = cb0 * kSwK + i;
+      const bool v = i < nent && e < Ek;   // the rest: row 0, weight 0
+      ej_s[i] = v ? esrc[e_lo + e] : 0;
+      ei_s[i] = v ? edst[e_lo + e] : 0;
+      ea_s[i] = v ? evals[e_lo + e] : 0.f;
+    }
     __syncthreads();
-    for (int t = 0; t < steps; ++t) {
-      const int buf = t & 1;
-      if (t + 2 < steps) issue(t + 2, t & 1);      // regs of step t: staged
+    const int steps = (cb1 - cb0) * U;
+    // (chunk, use) of the step being issued, advanced without division.
+    int iu = 0, ic = 0;
+    // Register slots are compile-time (the step loop is unrolled by two):
+    // a runtime slot index turns the prefetch registers into a dynamically
+    // indexed array, which the compiler resolves with selects that wait on
+    // every load.
+    auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+      constexpr int slot = decltype(slot_c)::value;
+      const int e = ic * kSwK + r;
+      const bool in = e < nent;           // past the batch: weight 0, row 0
+      const int ee = in ? e : 0;
+      const size_t base = (size_t)iu * N;
+      xr[slot] = *reinterpret_cast<const sw_bf16x8*>(
+          X + (base + ej_s[ee]) * kSwC + 8 * c);
+      gr[slot] = *reinterpret_cast<const sw_bf16x8*>(
+          G + (base + ei_s[ee]) * kSwC + 8 * c);
+      ar[slot] = in ? ea_s[ee] : 0.f;
+      const bool wrap = iu + 1 == U;
+      iu = wrap ? 0 : iu + 1;
+      ic += wrap ? 1 : 0;
+    };
+    auto stage = [&](auto slot_c) __attribute__((always_inline)) {
+      constexpr int slot = decltype(slot_c)::value, buf = slot;
+      sw_bf16x8 xs;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        xs[q] = (__bf16)((float)xr[slot][q] * ar[slot]);
+      *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+          (DGMC_LDS char*)lds[buf][0] + sw_off(r, c)) = xs;
+      *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+          (DGMC_LDS char*)lds[buf][1] + sw_off(r, c)) = gr[slot];
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    issue(S0{});
+    issue(S1{});
+    stage(S0{});
+    __syncthreads();
+    // One step: MFMAs on buffer BUF while the rows of step t+2 load into the
+    // registers just staged, then stage step t+1 into the other buffer.
+    auto step = [&](auto buf_c) __attribute__((always_inline)) {
+      constexpr int buf = decltype(buf_c)::value;
+      issue(buf_c);
       const DGMC_LDS char* A = (const DGMC_LDS char*)lds[buf][0];
       const DGMC_LDS char* B = (const DGMC_LDS char*)lds[buf][1];
       sw_bf16x8 af[4], bf[2];
@@ -159,8 +178,13 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf[b],
                                                               acc[a][b], 0, 0,
                                                               0);
-      if (t + 1 < steps) stage(buf ^ 1, (t + 1) & 1);
+      stage(std::integral_constant<int, buf ^ 1>{});
       __syncthreads();
+    };
+    // Steps past `steps` (odd count) carry zero weights.
+    for (int t = 0; t < steps; t += 2) {
+      step(S0{});
+      step(S1{});
     }
   }
 
@@ -249,6 +273,158 @@ at::Tensor tr16_probe(const at::Tensor& like) {
                      out.data_ptr<short>());
   DGMC_CHECK_LAUNCH();
   return out;
+}
+
+}  // namespace dgmc
+
+namespace dgmc {
+
+// ---------------------------------------------------------------------------
+// Entries of a slot-structured CSR operator grouped by slot, in entry order
+// inside each slot (a deterministic, stable counting sort - the weight
+// gradient's summation order is fixed run to run).  Entries past rowptr[N]
+// (the inert tail of a fixed-capacity operator) are dropped.
+constexpr int kPlBlock = 1024;    // entries per block
+constexpr int kPlThreads = 256;
+constexpr int kPlMaxS = 64;
+
+__global__ __launch_bounds__(kPlThreads) void pair_count_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, int N,
+    int S, int* __restrict__ cnt) {
+  __shared__ int hist[kPlMaxS];
+  const int tid = threadIdx.x, blk = blockIdx.x;
+  const int E = rowptr[N];
+  if (tid < S) hist[tid] = 0;
+  __syncthreads();
+  for (int i = 0; i < kPlBlock / kPlThreads; ++i) {
+    const int e = blk * kPlBlock + i * kPlThreads + tid;
+    if (e < E) atomicAdd(&hist[col[e] % S], 1);
+  }
+  __syncthreads();
+  if (tid < S) cnt[blk * S + tid] = hist[tid];
+}
+
+// off[blk][k] = (entries of slots < k) + (entries of slot k in blocks < blk).
+// The counts are staged in LDS first (a serial scan over global memory would
+// pay one load latency per block).
+constexpr int kPlScanLds = 16384;   // ints
+
+__global__ __launch_bounds__(kPlThreads) void pair_scan_kernel(
+    const int* __restrict__ cnt, int nblk, int S, int* __restrict__ off,
+    int* __restrict__ soff) {
+  __shared__ int c_s[kPlScanLds];
+  __shared__ int total[kPlMaxS + 1];
+  const int tid = threadIdx.x;
+  const bool staged = nblk * S <= kPlScanLds;
+  if (staged)
+    for (int i = tid; i < nblk * S; i += kPlThreads) c_s[i] = cnt[i];
+  __syncthreads();
+  const int k = tid;
+  int run = 0;
+  if (k < S) {
+    for (int b = 0; b < nblk; ++b) {
+      const int c = staged ? c_s[b * S + k] : cnt[b * S + k];
+      if (staged) c_s[b * S + k] = run; else off[b * S + k] = run;
+      run += c;
+    }
+    total[k] = run;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int kk = 0; kk < S; ++kk) {
+      soff[kk] = acc;
+      const int t = total[kk];
+      total[kk] = acc;
+      acc += t;
+    }
+    soff[S] = acc;
+  }
+  __syncthreads();
+  for (int i = tid; i < nblk * S; i += kPlThreads)
+    off[i] = (staged ? c_s[i] : off[i]) + total[i % S];
+}
+
+__global__ __launch_bounds__(kPlThreads) void pair_scatter_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ val, const int64_t* __restrict__ row, int N,
+    int S, const int* __restrict__ off, int* __restrict__ esrc,
+    int* __restrict__ edst, float* __restrict__ evals) {
+  constexpr int R = kPlBlock / kPlThreads;   // rounds
+  constexpr int W = kPlThreads / 64;         // waves
+  __shared__ int wcnt[R * W][kPlMaxS];
+  const int tid = threadIdx.x, blk = blockIdx.x, wave = tid >> 6,
+            lane = tid & 63;
+  const int E = rowptr[N];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int key[R], rank[R];
+  for (int i = 0; i < R; ++i) {
+    const int e = blk * kPlBlock + i * kPlThreads + tid;
+    key[i] = e < E ? col[e] % S : -1;
+    rank[i] = 0;
+    for (int k = 0; k < S; ++k) {           // stable rank inside the wave
+      const unsigned long long m = __ballot(key[i] == k);
+      if (key[i] == k) rank[i] = __popcll(m & lt);
+      if (lane == 0) wcnt[i * W + wave][k] = __popcll(m);
+    }
+  }
+  __syncthreads();
+  if (tid < S) {                            // exclusive prefix in entry order
+    int run = 0;
+    for (int g = 0; g < R * W; ++g) {
+      const int c = wcnt[g][tid];
+      wcnt[g][tid] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < R; ++i) {
+    if (key[i] < 0) continue;
+    const int e = blk * kPlBlock + i * kPlThreads + tid;
+    const int k = key[i];
+    const int pos = off[blk * S + k] + wcnt[i * W + wave][k] + rank[i];
+    esrc[pos] = col[e] / S;
+    edst[pos] = (int)row[e];
+    evals[pos] = val[e];
+  }
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_pair_lists(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& val,
+    const at::Tensor& row, int64_t S) {
+  TORCH_CHECK(rowptr.is_cuda() && rowptr.scalar_type() == at::kInt &&
+                  col.scalar_type() == at::kInt &&
+                  val.scalar_type() == at::kFloat &&
+                  row.scalar_type() == at::kLong && rowptr.is_contiguous() &&
+                  col.is_contiguous() && val.is_contiguous() &&
+                  row.is_contiguous() && col.numel() == val.numel() &&
+                  row.numel() == col.numel(),
+              "slot_pair_lists: int32 rowptr/col, fp32 val, int64 row");
+  TORCH_CHECK(S >= 1 && S <= kPlMaxS, "slot_pair_lists: 1 <= S <= 64");
+  const int64_t N = rowptr.numel() - 1, E = col.numel();
+  TORCH_CHECK(E < INT32_MAX, "slot_pair_lists: size range");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(col.device());
+  const int nblk = (int)std::max<int64_t>((E + kPlBlock - 1) / kPlBlock, 1);
+  auto i32 = col.options();
+  at::Tensor cnt = at::empty({nblk, S}, i32);
+  at::Tensor off = at::empty({nblk, S}, i32);
+  at::Tensor soff = at::empty({S + 1}, i32);
+  at::Tensor esrc = at::zeros({E}, i32);
+  at::Tensor edst = at::zeros({E}, i32);
+  at::Tensor evals = at::zeros({E}, val.options());
+  hipLaunchKernelGGL(pair_count_kernel, dim3(nblk), dim3(kPlThreads), 0,
+                     stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+                     (int)N, (int)S, cnt.data_ptr<int>());
+  hipLaunchKernelGGL(pair_scan_kernel, dim3(1), dim3(kPlThreads), 0, stream(),
+                     cnt.data_ptr<int>(), nblk, (int)S, off.data_ptr<int>(),
+                     soff.data_ptr<int>());
+  hipLaunchKernelGGL(pair_scatter_kernel, dim3(nblk), dim3(kPlThreads), 0,
+                     stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+                     val.data_ptr<float>(), row.data_ptr<int64_t>(), (int)N,
+                     (int)S, off.data_ptr<int>(), esrc.data_ptr<int>(),
+                     edst.data_ptr<int>(), evals.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return {esrc, edst, evals, soff};
 }
 
 }  // namespace dgmc

@@ -368,10 +368,10 @@ SLOT_CONV = _SLOT_MODE in ('1', 'fwd')
 SLOT_CONV_BWD = _SLOT_MODE == '1'
 # Loop-shared weight gradient straight from the kept (x, g') pairs of every
 # use (csrc/hip/slot_wgrad.hip) - no dY = A^T g' stack - with the fused
-# transposed slot conv for dx.  Opt-in (DGMC_AMD_SLOT_WGRAD=1): correct
-# (tests/test_slot_conv.py) but not yet faster than the SpMM dY stack +
-# long-K GEMM it replaces (docs/performance.md).
-SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '0') == '1'
+# transposed slot conv for dx (psi_2 backward: 113.7k vs 104.9k pairs/s,
+# docs/performance.md).  DGMC_AMD_SLOT_WGRAD=0 falls back to the SpMM dY
+# stack + long-K GEMM.
+SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '1') == '1'
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}
@@ -414,6 +414,10 @@ def slot_pair_lists(op, S):
     on the device without host synchronisation."""
     cache = op.__dict__.setdefault('_slot_pairs', {})
     p = cache.get(S)
+    if p is None and _backend.use_hip(op.col) and S <= 64:
+        # Stable device counting sort (csrc/hip/slot_wgrad.hip).
+        p = cache[S] = tuple(_backend.ops().slot_pair_lists(
+            op.rowptr, op.col, op.val, op.row.contiguous(), S))
     if p is None:
         col = op.col.long()
         k = col % S
@@ -428,7 +432,7 @@ def slot_pair_lists(op, S):
     return p
 
 
-SLOT_WGRAD_SPLITS = 20
+SLOT_WGRAD_SPLITS = 64
 
 
 def slot_weight_grad(X, G, op, S, uses, nsplit=None):

@@ -266,3 +266,18 @@ def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch):
     for a, b in zip(g_a, g_b):
         assert torch.isfinite(a).all()
         assert _close(a, b.float(), 0.1)
+
+
+def test_slot_pair_lists_stable_counting_sort():
+    from deep_graph_matching_consensus_amd.ops.sparse import slot_pair_lists
+    S = 26
+    op, _ = _graph_batch(_sizes(400, 19, seed=7), S, seed=7)
+    esrc, edst, evals, soff = slot_pair_lists(op, S)
+    col = op.col.long()
+    k = col % S
+    perm = torch.argsort(k, stable=True)
+    assert torch.equal(esrc.long(), (col // S)[perm])
+    assert torch.equal(edst.long(), op.row[perm])
+    assert torch.equal(evals, op.val[perm])
+    cnt = torch.bincount(k, minlength=S)
+    assert torch.equal(soff[1:].long(), torch.cumsum(cnt, 0))

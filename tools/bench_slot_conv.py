@@ -118,7 +118,7 @@ def main():
     res['pair_lists_us'] = timeit(lambda: (op.__dict__.pop('_slot_pairs',
                                                            None),
                                            slot_pair_lists(op, S)), 10)
-    for ns in (10, 20, 40):
+    for ns in (40, 64, 96):
         res['wgrad_slot_s%d_us' % ns] = timeit(
             lambda: slot_weight_grad(Xs, Gs, op, S, U, nsplit=ns), 10)
     dYs = torch.randn(U * N, S * C, device=dev).bfloat16()
