@@ -40,6 +40,8 @@ def timeit(fn, reps):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument('--reps', type=int, default=50)
+    p.add_argument('--only-fwd', action='store_true',
+                   help='time the fused forward only (counter runs)')
     args = p.parse_args()
     dev = torch.device('cuda')
     groups = make_keypoint_datasets(categories=PASCAL_VOC_CATEGORIES,
@@ -73,6 +75,9 @@ def main():
         args.reps)
     res['fused_fwd_us'] = timeit(lambda: ops.slot_conv(
         x, *pl, S, img_f, False, bias, True, torch.bfloat16, None), args.reps)
+    if args.only_fwd:
+        print(json.dumps(res))
+        return
     res['fused_bwd_dy_us'] = timeit(lambda: ops.slot_conv(
         g, *pl, S, img_b, True, None, False, torch.bfloat16, dy), args.reps)
     res['fused_bwd_us'] = timeit(lambda: ops.slot_conv(
