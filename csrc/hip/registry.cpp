@@ -119,7 +119,8 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      const at::Tensor& eval, int64_t S, const at::Tensor& Wimg,
                      bool trans, const c10::optional<at::Tensor>& bias,
                      bool relu, at::ScalarType out_dtype,
-                     const c10::optional<at::Tensor>& Z);
+                     const c10::optional<at::Tensor>& Z,
+                     const c10::optional<at::Tensor>& addend);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_tile_plan(
     const at::Tensor& flag, const at::Tensor& rowptr, const at::Tensor& col,
     const at::Tensor& val, int64_t window, int64_t S, at::Tensor err);
@@ -208,7 +209,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "slot_conv(Tensor X, Tensor tiles, Tensor soff, Tensor ecode, Tensor "
       "eval, int S, Tensor Wimg, bool trans, Tensor? bias, bool relu, "
-      "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
+      "ScalarType out_dtype, Tensor(a!)? Z=None, Tensor? addend=None) -> "
+      "Tensor");
   m.def(
       "slot_tile_plan(Tensor flag, Tensor rowptr, Tensor col, Tensor val, int "
       "window, int S, Tensor(a!) err) -> (Tensor, Tensor, Tensor, Tensor)");

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_kernel(
     const __hip_bfloat16* __restrict__ evalg, int S,
     const __hip_bfloat16* __restrict__ Wimg, const float* __restrict__ bias,
     int relu, TOUT* __restrict__ out, __hip_bfloat16* __restrict__ Zg,
-    int dbg) {
+    const __hip_bfloat16* __restrict__ addg, int ldadd, int dbg) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS char* smem = (DGMC_LDS char*)smem_raw;
   DGMC_LDS __bf16* wbuf = (DGMC_LDS __bf16*)smem;        // [2][128][128]
@@ -425,6 +425,16 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v[r] = ot[m][r] + bsh[64 * oh + 16 * m + 4 * lq + r];
+    }
+    if (addg) {   // fused gradient accumulation (a second consumer's dX)
+      const sc_bf16x4 ad = *reinterpret_cast<const sc_bf16x4*>(
+          reinterpret_cast<const __bf16*>(addg) +
+          (size_t)(r0 + node) * ldadd + 64 * oh + 16 * m + 4 * lq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)ad[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
       if (relu) v[r] = fmaxf(v[r], 0.f);
     }
     if constexpr (sizeof(TOUT) == 2) {
@@ -462,7 +472,8 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                              const at::Tensor& soff, const at::Tensor& ecode,
                              const at::Tensor& eval, int S,
                              const at::Tensor& Wimg, const float* bias,
-                             bool relu, at::Tensor& out, __hip_bfloat16* Z) {
+                             bool relu, at::Tensor& out, __hip_bfloat16* Z,
+                             const __hip_bfloat16* add, int ldadd) {
   auto kern = slot_conv_kernel<TRANS, WRITE_Z, TOUT>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -480,7 +491,8 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      S,
                      reinterpret_cast<const __hip_bfloat16*>(Wimg.data_ptr()),
                      bias, relu ? 1 : 0,
-                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, sc_debug());
+                     reinterpret_cast<TOUT*>(out.data_ptr()), Z, add, ldadd,
+                     sc_debug());
 }
 
 // flag [N] uint8 (1 = graph start); rowptr [N+1] / col / val: CSR of A with
@@ -538,7 +550,8 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      const at::Tensor& eval, int64_t S, const at::Tensor& Wimg,
                      bool trans, const c10::optional<at::Tensor>& bias,
                      bool relu, at::ScalarType out_dtype,
-                     const c10::optional<at::Tensor>& Z) {
+                     const c10::optional<at::Tensor>& Z,
+                     const c10::optional<at::Tensor>& addend) {
   TORCH_CHECK(X.is_cuda() && X.dim() == 2 && X.is_contiguous() &&
                   X.scalar_type() == at::kBFloat16 && X.size(1) == kScC &&
                   aligned16(X.data_ptr()),
@@ -579,6 +592,18 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                 "slot_conv: Z must be contiguous bf16 [N*S, 128]");
     zp = reinterpret_cast<__hip_bfloat16*>(Z->data_ptr());
   }
+  const __hip_bfloat16* ap = nullptr;
+  int lda = 0;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kBFloat16 && addend->dim() == 2 &&
+                    addend->size(0) == N && addend->size(1) == kScC &&
+                    addend->stride(1) == 1 && addend->stride(0) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(addend->data_ptr()) % 8) == 0,
+                "slot_conv: addend bf16 [N, 128], unit column stride, 8-B "
+                "aligned rows");
+    ap = reinterpret_cast<const __hip_bfloat16*>(addend->data_ptr());
+    lda = (int)addend->stride(0);
+  }
   if (N == 0) return out;
   const int s = (int)S;
   const bool f32 = out_dtype == at::kFloat;
@@ -586,10 +611,11 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
   do {                                                                        \
     if (f32)                                                                  \
       launch_slot_conv<TR, WZ, float>(X, tiles, soff, ecode, eval, s, Wimg,  \
-                                      bp, relu, out, zp);                    \
+                                      bp, relu, out, zp, ap, lda);          \
     else                                                                      \
       launch_slot_conv<TR, WZ, __hip_bfloat16>(X, tiles, soff, ecode, eval,  \
-                                               s, Wimg, bp, relu, out, zp);  \
+                                               s, Wimg, bp, relu, out, zp,   \
+                                               ap, lda);                      \
   } while (0)
   if (!trans)
     DGMC_SC_LAUNCH(false, false);

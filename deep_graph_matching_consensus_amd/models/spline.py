@@ -5,10 +5,12 @@ into the aggregation kernel's epilogue here), optional concatenation,
 dropout applied ONCE to the (concatenated) features (``spline.py:52``), then
 the optional final ``Linear``.
 """
+import torch
 import torch.nn.functional as F
 from torch.nn import ModuleList
 
 from ..nn.conv import SplineConv
+from ..ops.sparse import PASSTHROUGH
 from .encoder import StackedEncoder
 
 
@@ -35,7 +37,16 @@ class SplineCNN(StackedEncoder):
     def forward(self, x, edge_index, edge_attr, *args):
         xs = [x]
         for conv in self.convs:
-            xs.append(conv(xs[-1], edge_index, edge_attr, act='relu'))
+            if (self.cat and PASSTHROUGH and xs[-1].requires_grad and
+                    torch.is_grad_enabled()):
+                # xs[-1] also feeds the concatenation: route that consumer
+                # through the conv's alias so both gradients meet inside
+                # the conv backward (no separate add kernel).
+                out, xs[-1] = conv(xs[-1], edge_index, edge_attr, act='relu',
+                                   passthrough=True)
+            else:
+                out = conv(xs[-1], edge_index, edge_attr, act='relu')
+            xs.append(out)
         h = F.dropout(self._head(xs), p=self.dropout, training=self.training)
         return self._project(h)
 

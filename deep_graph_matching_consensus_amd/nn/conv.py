@@ -100,7 +100,7 @@ class SplineConv(torch.nn.Module):
             return w
         return cached(('spline_w', id(self)), build)
 
-    def forward(self, x, edge_index, pseudo, act=None):
+    def forward(self, x, edge_index, pseudo, act=None, passthrough=False):
         x = x.unsqueeze(-1) if x.dim() == 1 else x
         pseudo = pseudo.unsqueeze(-1) if pseudo.dim() == 1 else pseudo
         N = x.size(0)
@@ -114,7 +114,8 @@ class SplineConv(torch.nn.Module):
                       lambda: w.detach().to(dtype))
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),
-                         loop_key=(id(self), N, plan.num_cols))
+                         loop_key=(id(self), N, plan.num_cols),
+                         passthrough=passthrough)
 
     def __repr__(self):
         return '{}({}, {}, dim={})'.format(self.__class__.__name__,

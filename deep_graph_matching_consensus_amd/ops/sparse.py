@@ -188,8 +188,9 @@ class _GemmSpMM(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, w, w_lp, bias, op, relu, C, loop):
+    def forward(ctx, x, w, w_lp, bias, op, relu, C, loop, passthrough=False):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
+        ctx.passthrough = passthrough
         K = xc.size(1)
         S = w_lp.size(1) // C
         ctx.img_b = None
@@ -221,11 +222,16 @@ class _GemmSpMM(torch.autograd.Function):
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.idx = loop.register() if loop is not None else None
+        if passthrough:
+            # A second consumer reads x through this alias: its gradient
+            # arrives here and is fused into dx (no autograd add kernel).
+            return out, x.view_as(x)
         return out
 
     @staticmethod
-    def backward(ctx, grad):
+    def backward(ctx, grad, gpass=None):
         from .gemm import col_partial_rows, loop_col_total, matmul_tn_fp32
+        nones = (None, ) * 5
         xc, w_lp, out = ctx.saved_tensors
         loop, idx, C = ctx.loop, ctx.idx, ctx.C
         grad = grad.contiguous()
@@ -261,11 +267,15 @@ class _GemmSpMM(torch.autograd.Function):
             #     pairs of all uses - dY is never formed.
             gx = gw = gb = None
             if ctx.needs_input_grad[0]:
+                add = gpass if _addend_ok(gpass, g) else None
                 gx = _backend.ops().slot_conv(
                     g.contiguous(), *slot_tile_plan(op, S), S, ctx.img_b,
-                    True, None, False, g.dtype, None)
+                    True, None, False, g.dtype, None, add)
+                if add is not None:
+                    gpass = None
                 if gx.dtype != ctx.x_dtype:
                     gx = gx.to(ctx.x_dtype)
+                gx = _add_pass(gx, gpass)
             loop.keep('x', idx, xc)
             loop.keep('g', idx, g)
             if loop.arrive():
@@ -278,7 +288,7 @@ class _GemmSpMM(torch.autograd.Function):
                 if need_b:
                     gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
                 loop.release()
-            return gx, gw, None, gb, None, None, None, None
+            return (gx, gw, None, gb) + nones
         # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
         slot = ctx.img_b is not None and ctx.needs_input_grad[0] and \
             g.dtype == torch.bfloat16
@@ -333,7 +343,22 @@ class _GemmSpMM(torch.autograd.Function):
             if need_b:
                 gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
             loop.release()
-        return gx, gw, None, gb, None, None, None, None
+        return (_add_pass(gx, gpass), gw, None, gb) + nones
+
+
+def _addend_ok(a, g):
+    """Can the slot conv epilogue add ``a`` into its bf16 output?"""
+    return (a is not None and a.dtype == torch.bfloat16 and
+            a.device == g.device and a.dim() == 2 and
+            a.size(0) == g.size(0) and a.size(1) == _SLOT_C and
+            a.stride(1) == 1 and a.stride(0) % 4 == 0 and
+            a.data_ptr() % 8 == 0)
+
+
+def _add_pass(gx, gpass):
+    if gx is None or gpass is None:
+        return gx
+    return gx + gpass
 
 
 _FUSED_WIDTHS = (32, 64, 128)
@@ -372,6 +397,10 @@ SLOT_CONV_BWD = _SLOT_MODE == '1'
 # docs/performance.md).  DGMC_AMD_SLOT_WGRAD=0 falls back to the SpMM dY
 # stack + long-K GEMM.
 SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '1') == '1'
+# Encoders with ``cat=True`` hand a layer input's second consumer (the
+# concatenation) the conv's passthrough alias, so its gradient is added in
+# the transposed slot conv epilogue instead of by an autograd add kernel.
+PASSTHROUGH = os.environ.get('DGMC_AMD_PASSTHROUGH', '1') == '1'
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}
@@ -491,13 +520,16 @@ def _slot_major_t(w_lp):
 
 
 def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,
-              loop_key=None):
+              loop_key=None, passthrough=False):
     r"""``act(op @ (x @ w).view(-1, out_channels) + bias)``.
 
     ``w [in, S * out]`` is the fp32 stacked weight (receives the gradient),
     ``w_lp`` its compute-dtype copy; ``op`` maps the ``S`` slot rows of
     every node to the output rows.  ``loop_key`` enables loop-shared gradient
     accumulation inside :func:`~..runtime.loopgrad.loop_scope`.
+    ``passthrough`` returns ``(out, x')`` where ``x'`` aliases ``x``: give
+    ``x'`` to x's other consumers and their gradient is accumulated inside
+    this node's backward (fused into the slot conv epilogue).
     """
     from ..runtime import loopgrad
     assert x.dim() == 2 and x.size(0) * (w.size(1) // out_channels) == \
@@ -507,4 +539,4 @@ def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,
     with torch.autocast(device_type='cuda' if x.is_cuda else 'cpu',
                         enabled=False):
         return _GemmSpMM.apply(x, w, w_lp.detach(), bias, op, relu,
-                               out_channels, loop)
+                               out_channels, loop, passthrough)

@@ -100,6 +100,64 @@ def test_slot_conv_kernel_forward_backward(n_max, graphs, S):
     assert _close(gx, gx_ref, 2e-2)
 
 
+def test_slot_conv_fused_addend():
+    """The transposed conv adds a strided bf16 gradient (a slice of the
+    concatenation's gradient) in its epilogue."""
+    ops = _backend.ops()
+    S = 26
+    op, flag = _graph_batch(_sizes(120, 19), S)
+    N = op.num_rows
+    op.tile_flag, op.tile_window = flag, 65 - 19
+    plan = slot_tile_plan(op, S)
+    w_lp = (torch.randn(C, S * C, device=DEV) / C ** 0.5).bfloat16()
+    img = slot_conv_image(w_lp, C, True)
+    g = torch.randn(N, C, device=DEV).bfloat16()
+    wide = torch.randn(N, 3 * C, device=DEV).bfloat16()
+    add = wide[:, C:2 * C]
+    base = ops.slot_conv(g, *plan, S, img, True, None, False, torch.float32,
+                         None)
+    fused = ops.slot_conv(g, *plan, S, img, True, None, False, torch.float32,
+                          None, add)
+    assert int(slot_conv_error(DEV)) == 0
+    torch.testing.assert_close(fused, base + add.float(), atol=1e-5,
+                               rtol=1e-5)
+
+
+def test_spline_cnn_passthrough_gradient_matches_autograd_add(monkeypatch):
+    """SplineCNN(cat=True) routes the concatenation's use of each layer input
+    through the conv (passthrough alias); gradients equal plain autograd."""
+    from deep_graph_matching_consensus_amd.models.spline import SplineCNN
+    from deep_graph_matching_consensus_amd.nn import conv as conv_mod
+    torch.manual_seed(3)
+    model = SplineCNN(C, C, dim=2, num_layers=2, cat=True, lin=False).to(DEV)
+    N, E = 400, 2400
+    ei = torch.randint(N, (2, E), device=DEV)
+    attr = torch.rand(E, 2, device=DEV)
+
+    def run(passthrough):
+        if not passthrough:
+            orig = conv_mod.SplineConv.forward
+            monkeypatch.setattr(
+                conv_mod.SplineConv, 'forward',
+                lambda self, *a, passthrough=False, **k: (
+                    orig(self, *a, **k), a[0]) if passthrough
+                else orig(self, *a, **k))
+        x = torch.randn(N, C, device=DEV, generator=torch.Generator(
+            DEV).manual_seed(0)).requires_grad_()
+        model.zero_grad()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = model(x, ei, attr)
+        out.float().square().sum().backward()
+        monkeypatch.undo()
+        return x.grad.clone(), [p.grad.clone() for p in model.parameters()]
+
+    gx1, gp1 = run(True)
+    gx0, gp0 = run(False)
+    torch.testing.assert_close(gx1, gx0, atol=2e-2, rtol=2e-2)
+    for a, b in zip(gp1, gp0):
+        torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
+
+
 def test_slot_conv_flags_oversized_tiles():
     ops = _backend.ops()
     S = 4
