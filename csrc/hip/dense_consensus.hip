@@ -260,8 +260,8 @@ template <typename TR>
 __global__ __launch_bounds__(kThreads) void softmax_transport_bwd_kernel(
     const float* __restrict__ S, const TR* __restrict__ r_s,
     const TR* __restrict__ g, const int* __restrict__ ptr_s,
-    const int* __restrict__ ptr_t, float* __restrict__ dS_hat, int Ns,
-    int Nt, int R, int vec) {
+    const int* __restrict__ ptr_t, float* __restrict__ dS_hat,
+    const float* __restrict__ addend, int Ns, int Nt, int R, int vec) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int pitch = R + 1;
   DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
@@ -318,7 +318,13 @@ __global__ __launch_bounds__(kThreads) void softmax_transport_bwd_kernel(
     if (i < Ns) {
       const float d = (i < ns && lane < nt) ? sD[i * Nt + lane] : 0.f;
       const float dot = wave_sum(sv[q] * d);
-      if (lane < Nt) out[i * Nt + lane] = sv[q] * (d - dot);
+      if (lane < Nt) {
+        // addend: S_hat's other consumer's gradient (the consensus
+        // update's identity path), summed here instead of by a separate
+        // kernel.
+        const float a = addend ? addend[(size_t)b * NN + i * Nt + lane] : 0.f;
+        out[i * Nt + lane] = sv[q] * (d - dot) + a;
+      }
     }
   }
 }
@@ -669,10 +675,19 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
                                        const at::Tensor& ptr_s,
-                                       const at::Tensor& ptr_t) {
+                                       const at::Tensor& ptr_t,
+                                       const c10::optional<at::Tensor>& addend) {
   check_pair_tensor(S, "S");
   check_packed(r_s, "r_s");
   check_packed(g, "grad r_t");
+  const float* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kFloat &&
+                    addend->is_contiguous() && addend->sizes() == S.sizes() &&
+                    addend->device() == S.device(),
+                "dense_softmax_transport_bwd: addend fp32 like S");
+    add = addend->data_ptr<float>();
+  }
   TORCH_CHECK(r_s.scalar_type() == g.scalar_type(), "r_s/grad dtype");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S.device());
   const int B = S.size(0), Ns = S.size(1), Nt = S.size(2);
@@ -692,7 +707,7 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                        reinterpret_cast<const T*>(r_s.data_ptr()),
                        reinterpret_cast<const T*>(g.data_ptr()),
                        ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
-                       out.data_ptr<float>(), Ns, Nt, R, vec);
+                       out.data_ptr<float>(), add, Ns, Nt, R, vec);
   });
   DGMC_CHECK_LAUNCH();
   return out;

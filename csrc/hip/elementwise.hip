@@ -34,7 +34,7 @@ template <typename TG, typename TO, typename TR, int VEC, int LPR, bool WRITE_G>
 __global__ __launch_bounds__(256) void colsum_kernel(
     const TG* __restrict__ grad, const TO* __restrict__ out,
     TR* __restrict__ g_out, float* __restrict__ part, int rows, int C,
-    int relu) {
+    int64_t ldg, int relu) {
   constexpr int RPB = 256 / LPR;
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [RPB][C]
   const int slot = threadIdx.x / LPR, lane = threadIdx.x % LPR;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(
     for (int r = r0 + slot; r < r1; r += RPB) {
       const size_t o = (size_t)r * C + c0;
       float g[VEC], m[VEC];
-      load_vec<TG, VEC>(grad + o, g);
+      load_vec<TG, VEC>(grad + (size_t)r * ldg + c0, g);   // row stride ldg
       if (relu) {
         load_vec<TO, VEC>(out + o, m);
 #pragma unroll
@@ -111,7 +111,7 @@ void launch_colsum(const at::Tensor& grad, const void* out, void* g,
                      reinterpret_cast<const TG*>(grad.data_ptr()),
                      reinterpret_cast<const TO*>(out),
                      reinterpret_cast<TR*>(g), part.data_ptr<float>(), rows, C,
-                     relu ? 1 : 0);
+                     grad.stride(0), relu ? 1 : 0);
   if (dst)  // dst == nullptr: the caller keeps the per-block partials
     hipLaunchKernelGGL(fold_rows_kernel, dim3((C + 31) / 32), dim3(256), 0,
                        stream(), part.data_ptr<float>(), dst, blocks, C,
@@ -181,9 +181,13 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     const at::Tensor& grad, const at::Tensor& out, bool relu,
     at::ScalarType g_dtype, const c10::optional<at::Tensor>& dbias,
     bool accumulate, const c10::optional<at::Tensor>& part_out) {
-  TORCH_CHECK(grad.is_cuda() && grad.dim() == 2 && grad.is_contiguous() &&
-                  out.is_contiguous() && out.sizes() == grad.sizes(),
-              "relu_bias_bwd: grad/out must be contiguous [rows, C]");
+  // grad may be a column slice (unit column stride, any row stride), e.g. the
+  // gradient of one block of a concatenation.
+  TORCH_CHECK(grad.is_cuda() && grad.dim() == 2 && grad.stride(1) == 1 &&
+                  grad.stride(0) >= grad.size(1) &&
+                  (!relu || (out.is_contiguous() && out.sizes() == grad.sizes())),
+              "relu_bias_bwd: grad [rows, C] with unit column stride, out "
+              "contiguous");
   TORCH_CHECK(grad.scalar_type() == out.scalar_type(),
               "relu_bias_bwd: grad/out dtype mismatch");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
@@ -200,7 +204,8 @@ std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
   bool keep;
   at::Tensor part = partials_or_new(part_out, blocks, C, grad, keep);
   const bool vec = aligned16(grad.data_ptr()) && aligned16(out.data_ptr()) &&
-                   aligned16(g.data_ptr());
+                   aligned16(g.data_ptr()) &&
+                   (grad.stride(0) * grad.element_size()) % 16 == 0;
   DGMC_DISPATCH_FLOAT(grad.scalar_type(), T, [&] {
     DGMC_DISPATCH_FLOAT(g_dtype, TR, [&] {
       dispatch_colsum<T, TR, true>(grad, out.data_ptr(), g.data_ptr(), part,

@@ -36,7 +36,8 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
                                        const at::Tensor& ptr_s,
-                                       const at::Tensor& ptr_t);
+                                       const at::Tensor& ptr_t,
+                                       const c10::optional<at::Tensor>& addend);
 at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
                            const at::Tensor& Q, const at::Tensor& b1,
                            const at::Tensor& w2, const at::Tensor& b2,
@@ -152,7 +153,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ptr_t, int rows_t, bool joint_out=False) -> (Tensor, Tensor)");
   m.def(
       "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
-      "ptr_s, Tensor ptr_t) -> Tensor");
+      "ptr_s, Tensor ptr_t, Tensor? addend=None) -> Tensor");
   m.def(
       "dense_consensus(Tensor S_hat, Tensor P, Tensor Q, Tensor b1, Tensor w2, "
       "Tensor b2, Tensor ptr_s, Tensor ptr_t) -> Tensor");

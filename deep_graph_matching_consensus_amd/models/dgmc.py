@@ -31,6 +31,7 @@ from ..nn.inits import reset
 from ..ops import _backend
 from ..ops import dense as dense_ops
 from ..ops import sparse_corr
+from ..ops.sparse import PASSTHROUGH
 from ..ops.plans import _IdentityCache
 from ..runtime import loopgrad
 from ..runtime.cache import forward_cache
@@ -288,7 +289,15 @@ class DGMC(torch.nn.Module):
                 for step in range(steps):
                     mark('dgmc.consensus_step')
                     r_s = r_all[step]
-                    if joint:
+                    if joint and PASSTHROUGH and S_hat.requires_grad and \
+                            torch.is_grad_enabled():
+                        # S_hat feeds the transport AND the update: the
+                        # update reads it through the transport's alias, so
+                        # both gradients meet in the transport backward.
+                        r_joint, S_hat = dense_ops.softmax_transport_joint(
+                            S_hat, r_s, lay_s, lay_t, passthrough=True)
+                        o_s, o_t, o = refine(None, None, r_joint)
+                    elif joint:
                         r_joint = dense_ops.softmax_transport_joint(
                             S_hat, r_s, lay_s, lay_t)
                         o_s, o_t, o = refine(None, None, r_joint)

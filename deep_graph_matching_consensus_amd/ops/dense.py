@@ -120,25 +120,37 @@ class _SoftmaxTransport(torch.autograd.Function):
 
 class _SoftmaxTransportJoint(torch.autograd.Function):
     """Returns ``[r_s; r_t]`` (psi_2's fused input) from one kernel: the
-    transport kernel also copies ``r_s`` - no concatenation kernel."""
+    transport kernel also copies ``r_s`` - no concatenation kernel.  With
+    ``passthrough`` it also returns an alias of ``S_hat`` for S_hat's other
+    consumer (the consensus update): that gradient is added inside the
+    backward kernel instead of by a separate autograd add."""
 
     @staticmethod
-    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t):
+    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t, passthrough=False):
         S, joint = _backend.ops().dense_softmax_transport(
             S_hat.float().contiguous(), r_s.contiguous(), ptr_s, ptr_t,
             rows_t, True)
         ctx.save_for_backward(S, r_s, ptr_s, ptr_t)
         ctx.dtype = S_hat.dtype
         ctx.n_s = r_s.size(0)
+        if passthrough:
+            return joint, S_hat.view_as(S_hat)
         return joint
 
     @staticmethod
-    def backward(ctx, grad):
+    def backward(ctx, grad, gpass=None):
         S, r_s, ptr_s, ptr_t = ctx.saved_tensors
+        add = gpass if (gpass is not None and
+                        gpass.dtype == torch.float32 and
+                        gpass.is_contiguous() and
+                        gpass.shape == S.shape) else None
         g = _backend.ops().dense_softmax_transport_bwd(
             S, r_s.contiguous(), grad[ctx.n_s:].to(r_s.dtype).contiguous(),
-            ptr_s, ptr_t)
-        return g.to(ctx.dtype), None, None, None, None
+            ptr_s, ptr_t, add)
+        g = g.to(ctx.dtype)
+        if gpass is not None and add is None:
+            g = g + gpass
+        return g, None, None, None, None, None
 
 
 def transport_joint_supported(S_hat, lay_s, lay_t):
@@ -146,11 +158,13 @@ def transport_joint_supported(S_hat, lay_s, lay_t):
     return _hip_ok(S_hat, N_s, N_t)
 
 
-def softmax_transport_joint(S_hat, r_s, lay_s, lay_t):
+def softmax_transport_joint(S_hat, r_s, lay_s, lay_t, passthrough=False):
     r"""``[r_s; masked_softmax(S_hat)^T r_s]`` as one packed
-    ``[sum N_s + sum N_t, R]`` tensor (differentiable w.r.t. ``S_hat``)."""
+    ``[sum N_s + sum N_t, R]`` tensor (differentiable w.r.t. ``S_hat``).
+    ``passthrough`` returns ``(joint, S_hat')`` with ``S_hat'`` an alias of
+    ``S_hat`` whose gradient is summed inside this op's backward kernel."""
     return _SoftmaxTransportJoint.apply(S_hat, r_s, lay_s.ptr, lay_t.ptr,
-                                        lay_t.num_nodes)
+                                        lay_t.num_nodes, passthrough)
 
 
 def softmax_transport(S_hat, r_s, lay_s, lay_t):

@@ -234,10 +234,11 @@ class _GemmSpMM(torch.autograd.Function):
         nones = (None, ) * 5
         xc, w_lp, out = ctx.saved_tensors
         loop, idx, C = ctx.loop, ctx.idx, ctx.C
-        grad = grad.contiguous()
         dev = grad.device
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         hip = _backend.use_hip(grad)
+        if not hip or grad.stride(-1) != 1 or grad.stride(0) < grad.size(1):
+            grad = grad.contiguous()    # (the kernel reads column slices)
         # 1. g' = grad * relu'(out) and the bias gradient.
         db = None
         if hip:

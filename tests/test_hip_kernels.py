@@ -447,6 +447,17 @@ def test_col_sum_and_relu_bias_accumulate(rows, C, dtype):
     part2 = torch.empty_like(part)
     g3, _ = ops.relu_bias_bwd(grad, o, True, dtype, None, False, part2)
     assert torch.allclose(part2.sum(0), gm.sum(0), atol=1e-3, rtol=1e-4)
+    # Column slice of a wider gradient (one block of a concatenation).
+    wide = torch.randn(rows, 3 * C + 8, device=DEV).to(dtype)
+    gs = wide[:, C + 8:2 * C + 8]
+    g4, db4 = ops.relu_bias_bwd(gs, o, True, dtype)
+    gsm = gs.float() * (o.float() > 0)
+    assert torch.equal(g4, ops.relu_bias_bwd(gs.contiguous(), o, True,
+                                             dtype)[0])
+    assert torch.allclose(db4, gsm.sum(0), atol=1e-3, rtol=1e-4)
+    g5, db5 = ops.relu_bias_bwd(gs, gs, False, dtype)
+    assert torch.equal(g5.float(), gs.float())
+    assert torch.allclose(db5, gs.float().sum(0), atol=1e-3, rtol=1e-4)
     # Deterministic: repeated calls are bit-identical.
     assert torch.equal(ops.col_sum(src), ops.col_sum(src))
 
