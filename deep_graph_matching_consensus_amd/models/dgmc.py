@@ -23,6 +23,9 @@ What differs is the execution plan (MI355X-first):
   the encoders' GEMMs drop to bf16);
 * all random indicators of the L steps are drawn with one ``randn`` call.
 """
+import contextlib
+import os
+
 import torch
 from torch.nn import Linear, ReLU, Sequential
 
@@ -37,6 +40,10 @@ from ..runtime import loopgrad
 from ..runtime.cache import forward_cache
 from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
+from .encoder import StackedEncoder
+
+# DGMC_AMD_FOLD_PROJECTION=0 keeps psi_2's final Linear as its own GEMM.
+FOLD_PROJECTION = os.environ.get('DGMC_AMD_FOLD_PROJECTION', '1') == '1'
 
 EPS = 1e-8
 _PAIR_CACHE = _IdentityCache(max_entries=8)
@@ -196,6 +203,11 @@ class DGMC(torch.nn.Module):
         dense_rows = s_mask.view(-1).nonzero().view(-1)
         return self._include_gt(S_idx, dense_rows, y)
 
+    def _foldable(self):
+        return (FOLD_PROJECTION and not is_reference_mode() and
+                isinstance(self.psi_2, StackedEncoder) and self.psi_2.lin and
+                isinstance(self.mlp[0], Linear))
+
     # ------------------------------------------------------------------
     def forward(self, x_s, edge_index_s, edge_attr_s, batch_s, x_t,
                 edge_index_t, edge_attr_t, batch_t, y=None):
@@ -255,12 +267,15 @@ class DGMC(torch.nn.Module):
                 r_all = torch.randn((steps, lay_s.num_nodes, R_in),
                                     dtype=r_dtype, device=device)
 
-            def refine(r_s, r_t, r_joint=None):
+            def refine(r_s, r_t, r_joint=None, features=False):
                 """psi_2 on both graphs (packed in/out) under the caller's
                 autocast policy; returns (o_s, o_t, o_joint or None).
-                ``r_joint`` = ``[r_s; r_t]`` already assembled."""
+                ``r_joint`` = ``[r_s; r_t]`` already assembled; ``features``
+                skips psi_2's final Linear (folded by the caller)."""
+                ctx = self.psi_2.features_only() if features else \
+                    contextlib.nullcontext()
                 with torch.autocast(device_type=dev_type, dtype=outer_dtype,
-                                    enabled=outer_autocast):
+                                    enabled=outer_autocast), ctx:
                     if pair is not None and self._fusable(self.psi_2):
                         if r_joint is None:
                             r_joint = torch.cat([r_s, r_t], dim=0)
@@ -286,6 +301,20 @@ class DGMC(torch.nn.Module):
                 joint = steps > 0 and pair is not None and \
                     self._fusable(self.psi_2) and \
                     dense_ops.transport_joint_supported(S_hat, lay_s, lay_t)
+                # psi_2's final Linear folded into the MLP's first layer:
+                # P_i - Q_j = (o_s,i - o_t,j) W1^T with o = h W_f^T + b_f, so
+                # [P; Q] = h (W1 W_f)^T - b_f cancels in the difference.  One
+                # node-level GEMM per step instead of two (forward and
+                # backward); the fold's weight gradient flows through the
+                # tiny W1 W_f product once per step.
+                fold = None
+                if joint and self._foldable():
+                    w_fold = self.mlp[0].weight @ self.psi_2.final.weight
+                    if self.psi_2.final.bias is not None:
+                        # b_f's exact gradient is zero; keep it in the graph
+                        # so it receives that zero (autograd.grad, DDP).
+                        w_fold = w_fold + 0 * self.psi_2.final.bias.sum()
+                    fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)))
                 for step in range(steps):
                     mark('dgmc.consensus_step')
                     r_s = r_all[step]
@@ -296,17 +325,20 @@ class DGMC(torch.nn.Module):
                         # both gradients meet in the transport backward.
                         r_joint, S_hat = dense_ops.softmax_transport_joint(
                             S_hat, r_s, lay_s, lay_t, passthrough=True)
-                        o_s, o_t, o = refine(None, None, r_joint)
+                        o_s, o_t, o = refine(None, None, r_joint,
+                                             features=fold is not None)
                     elif joint:
                         r_joint = dense_ops.softmax_transport_joint(
                             S_hat, r_s, lay_s, lay_t)
-                        o_s, o_t, o = refine(None, None, r_joint)
+                        o_s, o_t, o = refine(None, None, r_joint,
+                                             features=fold is not None)
                     else:
                         r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,
                                                           lay_t)
                         o_s, o_t, o = refine(r_s, r_t)
                     S_hat = dense_ops.consensus_update(
-                        S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o)
+                        S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o,
+                        w1_fold=fold)
                 S_L = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 return S_0, S_L
 

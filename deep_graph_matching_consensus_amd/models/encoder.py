@@ -15,6 +15,8 @@ and target graphs in ONE call on their disjoint union gives the same result as
 two calls (true unless BatchNorm runs in training mode), which halves the
 kernel launches and doubles GEMM sizes on the hot path.
 """
+import contextlib
+
 import torch
 from torch.nn import Linear
 
@@ -40,9 +42,21 @@ class StackedEncoder(torch.nn.Module):
         return x
 
     def _project(self, x):
-        if not self.lin:
+        if not self.lin or getattr(self, '_features_only', False):
             return x
         return linear(x, self.final.weight, self.final.bias)
+
+    @contextlib.contextmanager
+    def features_only(self):
+        """Inside the block ``forward`` returns the features BEFORE the final
+        ``Linear`` (callers that fold the projection into a following linear
+        map, e.g. DGMC's consensus MLP)."""
+        prev = getattr(self, '_features_only', False)
+        self._features_only = True
+        try:
+            yield self
+        finally:
+            self._features_only = prev
 
     @property
     def pair_fusable(self):

@@ -238,15 +238,32 @@ class _ConsensusUpdate(torch.autograd.Function):
         return (grad.to(s_dt), dP, dQ, db1, dw2, db2, None, None, None)
 
 
-def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None):
+def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
+                     w1_fold=None):
     r"""``S_hat + mask * mlp(o_s[:, :, None] - o_t[:, None])`` for packed
     ``o_s [sum N_s, R]`` / ``o_t [sum N_t, R]``.  ``o_joint`` may pass the
     concatenation ``[o_s; o_t]`` (fused encoder output) to compute both
     projections with one GEMM.  ``mlp`` must be ``Seq(Lin(R, R), ReLU,
-    Lin(R, 1))`` (``dgmc.py:74-78``).
+    Lin(R, 1))`` (``dgmc.py:74-78``).  ``w1_fold = (W^T, lp_cache, key)``
+    replaces ``W1^T`` by a folded ``[K, R]`` map applied to ``o_joint``
+    (the encoder's pre-projection features; see ``DGMC._forward``).
     """
     lin1, lin2 = mlp[0], mlp[2]
     B, N_s, N_t = S_hat.shape
+    if w1_fold is not None and (o_joint is None or
+                                not _hip_ok(S_hat, N_s, N_t)):
+        raise ValueError('w1_fold needs the joint HIP path')
+    if w1_fold is not None:
+        w_t, lp, key = w1_fold
+        w_lp = lp.get(o_joint.dtype)
+        if w_lp is None:
+            w_lp = lp[o_joint.dtype] = w_t.detach().to(o_joint.dtype)
+        PQ = mixed_matmul(o_joint, w_t, w_lp, loop_key=key + (
+            o_joint.size(0), ))
+        loop = loopgrad.group(('consensus', id(mlp)))
+        return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes, lin1.bias,
+                                      lin2.weight, lin2.bias, lay_s.ptr,
+                                      lay_t.ptr, loop)
     if _hip_ok(S_hat, N_s, N_t):
         w1t = lin1.weight.t()
         key = (id(lin1.weight), )

@@ -262,6 +262,41 @@ def test_dgmc_dense_hip_vs_reference_mode():
         assert torch.allclose(a, b, atol=1e-3, rtol=1e-2)
 
 
+def test_dgmc_folded_projection_matches_unfolded(monkeypatch):
+    """psi_2's final Linear folded into the consensus MLP's first layer
+    (one GEMM on the pre-projection features) gives the same outputs and
+    gradients as the two-GEMM form (the final bias' gradient is exactly 0)."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, DevicePairLoader, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.models import dgmc as dgmc_mod
+    groups = make_keypoint_datasets(graphs=8, feature_dim=32, seed=0)
+    store = GraphStore(groups, DEV)
+    batch = next(iter(DevicePairLoader(store, batch_size=24, seed=0)))
+    torch.manual_seed(3)
+    model = DGMC(SplineCNN(32, 32, 2, 2, cat=False),
+                 SplineCNN(16, 16, 2, 2, cat=True), num_steps=3).to(DEV)
+    args = (batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+            batch.x_s_batch, batch.x_t, batch.edge_index_t,
+            batch.edge_attr_t, batch.x_t_batch)
+    y = torch.stack([torch.arange(batch.y.numel(), device=DEV), batch.y])
+
+    def run(fold):
+        monkeypatch.setattr(dgmc_mod, 'FOLD_PROJECTION', fold)
+        torch.manual_seed(5)
+        S_0, S_L = model(*args)
+        loss = model.loss(S_0, y) + model.loss(S_L, y)
+        return S_L, torch.autograd.grad(loss, list(model.parameters()))
+
+    S1, g1 = run(True)
+    S0, g0 = run(False)
+    assert torch.allclose(S1, S0, atol=1e-4)
+    names = [n for n, _ in model.named_parameters()]
+    for n, a, b in zip(names, g1, g0):
+        assert torch.allclose(a, b, atol=1e-3, rtol=1e-2), n
+    assert float(g1[names.index('psi_2.final.bias')].abs().max()) == 0.0
+
+
 def test_dgmc_sparse_gpu_matches_dense():
     from deep_graph_matching_consensus_amd.models import DGMC, GIN
     torch.manual_seed(0)
