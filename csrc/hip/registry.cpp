@@ -115,6 +115,10 @@ at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                       const at::Tensor& esrc, const at::Tensor& edst,
                       const at::Tensor& evals, const at::Tensor& soff,
                       int64_t U, int64_t nsplit);
+at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
+                           const at::Tensor& esrc, const at::Tensor& edst,
+                           const at::Tensor& evals, const at::Tensor& soff,
+                           int64_t nsplit);
 at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      const at::Tensor& soff, const at::Tensor& ecode,
                      const at::Tensor& eval, int64_t S, const at::Tensor& Wimg,
@@ -208,6 +212,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_wgrad(Tensor X, Tensor G, Tensor esrc, Tensor edst, Tensor evals, "
       "Tensor soff, int U, int nsplit) -> Tensor");
   m.def(
+      "slot_wgrad_list(Tensor[] xs, Tensor[] gs, Tensor esrc, Tensor edst, "
+      "Tensor evals, Tensor soff, int nsplit) -> Tensor");
+  m.def(
       "slot_conv(Tensor X, Tensor tiles, Tensor soff, Tensor ecode, Tensor "
       "eval, int S, Tensor Wimg, bool trans, Tensor? bias, bool relu, "
       "ScalarType out_dtype, Tensor(a!)? Z=None, Tensor? addend=None) -> "
@@ -258,6 +265,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_conv", &dgmc::slot_conv);
   m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
   m.impl("slot_wgrad", &dgmc::slot_wgrad);
+  m.impl("slot_wgrad_list", &dgmc::slot_wgrad_list);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

@@ -43,6 +43,14 @@ constexpr int kSwK = 32;           // pairs per step
 constexpr int kSwThreads = 512;    // 8 waves
 constexpr int kSwTile = kSwK * kSwC;   // bf16 elements per staged operand
 constexpr int kSwEB = 1024;        // entries staged in LDS per batch
+constexpr int kSwMaxU = 16;        // uses addressed through the pointer table
+
+// Per-use row bases of X and G (kernel argument: captured by value in a
+// hipGraph; the uses' tensors are read in place, no stacking copy).
+struct SwUses {
+  const __bf16* x[kSwMaxU];
+  const __bf16* g[kSwMaxU];
+};
 
 // Byte offset of 16-byte chunk `ch` of row `row` in a [rows][128 bf16]
 // image (256-B rows): the XOR keeps both ds_write_b128 row stores and the
@@ -75,8 +83,7 @@ __device__ __forceinline__ sw_bf16x8 sw_frag(const DGMC_LDS char* img,
 }  // namespace
 
 __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
-    const __hip_bfloat16* __restrict__ Xg, const __hip_bfloat16* __restrict__ Gg,
-    const int* __restrict__ esrc, const int* __restrict__ edst,
+    const SwUses P, const int* __restrict__ esrc, const int* __restrict__ edst,
     const float* __restrict__ evals, const int* __restrict__ soff, int S,
     int U, int N, int nsplit, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][kSwTile * 2];
@@ -86,8 +93,6 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
   const int nch = (Ek + kSwK - 1) / kSwK;
   const int ch0 = (int)((long long)nch * s / nsplit);
   const int ch1 = (int)((long long)nch * (s + 1) / nsplit);
-  const __bf16* X = reinterpret_cast<const __bf16*>(Xg);
-  const __bf16* G = reinterpret_cast<const __bf16*>(Gg);
 
   // Staging role: thread -> (pair row r, 16-byte chunk c) of both operands.
   const int r = tid >> 4, c = tid & 15;
@@ -132,11 +137,11 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
       const int e = ic * kSwK + r;
       const bool in = e < nent;           // past the batch: weight 0, row 0
       const int ee = in ? e : 0;
-      const size_t base = (size_t)iu * N;
+      // iu is wave-uniform: the table lookup is a scalar load.
       xr[slot] = *reinterpret_cast<const sw_bf16x8*>(
-          X + (base + ej_s[ee]) * kSwC + 8 * c);
+          P.x[iu] + (size_t)ej_s[ee] * kSwC + 8 * c);
       gr[slot] = *reinterpret_cast<const sw_bf16x8*>(
-          G + (base + ei_s[ee]) * kSwC + 8 * c);
+          P.g[iu] + (size_t)ei_s[ee] * kSwC + 8 * c);
       ar[slot] = in ? ea_s[ee] : 0.f;
       const bool wrap = iu + 1 == U;
       iu = wrap ? 0 : iu + 1;
@@ -203,9 +208,44 @@ __global__ __launch_bounds__(kSwThreads, 1) void slot_wgrad_kernel(
       }
 }
 
+static void check_pairs(const at::Tensor& esrc, const at::Tensor& edst,
+                        const at::Tensor& evals, const at::Tensor& soff) {
+  TORCH_CHECK(esrc.scalar_type() == at::kInt &&
+                  edst.scalar_type() == at::kInt &&
+                  evals.scalar_type() == at::kFloat &&
+                  soff.scalar_type() == at::kInt && esrc.is_contiguous() &&
+                  edst.is_contiguous() && evals.is_contiguous() &&
+                  soff.is_contiguous() && esrc.numel() == edst.numel() &&
+                  esrc.numel() == evals.numel(),
+              "slot_wgrad: int32 esrc/edst/soff, fp32 evals");
+}
+
+static at::Tensor launch_slot_wgrad(const SwUses& P, int U, int64_t N,
+                                    const at::Tensor& like,
+                                    const at::Tensor& esrc,
+                                    const at::Tensor& edst,
+                                    const at::Tensor& evals,
+                                    const at::Tensor& soff, int64_t nsplit) {
+  check_pairs(esrc, edst, evals, soff);
+  const int64_t S = soff.numel() - 1;
+  TORCH_CHECK(S >= 1 && nsplit >= 1 && S * nsplit < (1 << 30),
+              "slot_wgrad: slots / splits");
+  TORCH_CHECK(N < INT32_MAX / kSwC, "slot_wgrad: size range");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(like.device());
+  at::Tensor part = at::empty({nsplit, S * kSwC * kSwC},
+                              like.options().dtype(at::kFloat));
+  hipLaunchKernelGGL(slot_wgrad_kernel, dim3(S * nsplit), dim3(kSwThreads), 0,
+                     stream(), P, esrc.data_ptr<int>(), edst.data_ptr<int>(),
+                     evals.data_ptr<float>(), soff.data_ptr<int>(), (int)S,
+                     U, (int)N, (int)nsplit, part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return part;
+}
+
 // X, G [U*N, 128] bf16 (use-major stacks); esrc/edst [E] int32 source /
 // target node of each operator entry, evals [E] fp32, all grouped by slot
-// with offsets soff [S+1]; returns dW [S, 128, 128] fp32 (channel, output).
+// with offsets soff [S+1]; returns per-split partials [nsplit, S*128*128]
+// fp32 of dW [S, 128, 128] (channel, output).
 at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                       const at::Tensor& esrc, const at::Tensor& edst,
                       const at::Tensor& evals, const at::Tensor& soff,
@@ -215,34 +255,43 @@ at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                   G.sizes() == X.sizes() &&
                   G.scalar_type() == at::kBFloat16 && G.is_contiguous(),
               "slot_wgrad: X, G contiguous bf16 [U*N, 128]");
-  TORCH_CHECK(U >= 1 && X.size(0) % U == 0, "slot_wgrad: rows % U");
-  TORCH_CHECK(esrc.scalar_type() == at::kInt &&
-                  edst.scalar_type() == at::kInt &&
-                  evals.scalar_type() == at::kFloat &&
-                  soff.scalar_type() == at::kInt && esrc.is_contiguous() &&
-                  edst.is_contiguous() && evals.is_contiguous() &&
-                  soff.is_contiguous() && esrc.numel() == edst.numel() &&
-                  esrc.numel() == evals.numel(),
-              "slot_wgrad: int32 esrc/edst/soff, fp32 evals");
+  TORCH_CHECK(U >= 1 && U <= kSwMaxU && X.size(0) % U == 0,
+              "slot_wgrad: 1 <= U <= 16, rows % U");
   TORCH_CHECK(aligned16(X.data_ptr()) && aligned16(G.data_ptr()),
               "slot_wgrad: 16-byte aligned operands");
-  const int64_t S = soff.numel() - 1;
-  TORCH_CHECK(S >= 1 && nsplit >= 1 && S * nsplit < (1 << 30),
-              "slot_wgrad: slots / splits");
   const int64_t N = X.size(0) / U;
-  TORCH_CHECK(N * U < INT32_MAX, "slot_wgrad: size range");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
-  at::Tensor part = at::empty({nsplit, S * kSwC * kSwC},
-                              X.options().dtype(at::kFloat));
-  hipLaunchKernelGGL(slot_wgrad_kernel, dim3(S * nsplit), dim3(kSwThreads), 0,
-                     stream(),
-                     reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
-                     reinterpret_cast<const __hip_bfloat16*>(G.data_ptr()),
-                     esrc.data_ptr<int>(), edst.data_ptr<int>(),
-                     evals.data_ptr<float>(), soff.data_ptr<int>(), (int)S,
-                     (int)U, (int)N, (int)nsplit, part.data_ptr<float>());
-  DGMC_CHECK_LAUNCH();
-  return part;
+  SwUses P{};
+  const __bf16* xb = reinterpret_cast<const __bf16*>(X.data_ptr());
+  const __bf16* gb = reinterpret_cast<const __bf16*>(G.data_ptr());
+  for (int u = 0; u < U; ++u) {
+    P.x[u] = xb + (size_t)u * N * kSwC;
+    P.g[u] = gb + (size_t)u * N * kSwC;
+  }
+  return launch_slot_wgrad(P, (int)U, N, X, esrc, edst, evals, soff, nsplit);
+}
+
+// Same, with the U uses' X_u / G_u [N, 128] read in place (no stacks).
+at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
+                           const at::Tensor& esrc, const at::Tensor& edst,
+                           const at::Tensor& evals, const at::Tensor& soff,
+                           int64_t nsplit) {
+  const int64_t U = (int64_t)xs.size();
+  TORCH_CHECK(U >= 1 && U <= kSwMaxU && (int64_t)gs.size() == U,
+              "slot_wgrad_list: 1 <= uses <= 16, one G per X");
+  const int64_t N = xs[0].size(0);
+  SwUses P{};
+  for (int u = 0; u < U; ++u) {
+    for (const at::Tensor* t : {&xs[u], &gs[u]})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 &&
+                      t->is_contiguous() && t->dim() == 2 &&
+                      t->size(0) == N && t->size(1) == kSwC &&
+                      aligned16(t->data_ptr()),
+                  "slot_wgrad_list: contiguous 16-B aligned bf16 [N, 128]");
+    P.x[u] = reinterpret_cast<const __bf16*>(xs[u].data_ptr());
+    P.g[u] = reinterpret_cast<const __bf16*>(gs[u].data_ptr());
+  }
+  return launch_slot_wgrad(P, (int)U, N, xs[0], esrc, edst, evals, soff,
+                           nsplit);
 }
 
 }  // namespace dgmc

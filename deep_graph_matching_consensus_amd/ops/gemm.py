@@ -27,7 +27,10 @@ def _split_factor(m, n, k):
     elems = m * n
     if elems >= (4 << 20) or k < 2048:
         return 1
-    s = 8 if elems >= (1 << 20) else 16
+    # Small outputs get many splits: 64 x [384, 128] partials of the 92k-row
+    # consensus weight gradient run 55 us vs 69 us at 16 (tools/
+    # bench_wgrad_tn.py).
+    s = 8 if elems >= (1 << 20) else (16 if elems >= (1 << 17) else 64)
     while s > 1 and k // s < 512:
         s //= 2
     return s

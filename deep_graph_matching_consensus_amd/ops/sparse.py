@@ -281,8 +281,8 @@ class _GemmSpMM(torch.autograd.Function):
             loop.keep('g', idx, g)
             if loop.arrive():
                 if ctx.needs_input_grad[1]:
-                    dW = slot_weight_grad(loop.kept('x').contiguous(),
-                                          loop.kept('g').contiguous(), op, S,
+                    dW = slot_weight_grad(loop.kept_list('x'),
+                                          loop.kept_list('g'), op, S,
                                           loop.uses)
                     gw = dW.permute(1, 0, 2).reshape(K, S * C)
                     gw = gw.to(ctx.w_dtype)
@@ -463,14 +463,29 @@ def slot_pair_lists(op, S):
 
 
 SLOT_WGRAD_SPLITS = 64
+_SLOT_WGRAD_MAX_LIST = 16    # pointer table size (csrc/hip/slot_wgrad.hip)
 
 
 def slot_weight_grad(X, G, op, S, uses, nsplit=None):
     """``dW [S, C, C]`` (fp32) with ``dW_k = sum_u sum_{e in k} a_e
-    X_u[j_e]^T G_u[i_e]`` for use-major stacks ``X, G [uses * N, C]``."""
+    X_u[j_e]^T G_u[i_e]`` for use-major stacks ``X, G [uses * N, C]`` or
+    lists of the ``uses`` per-use ``[N, C]`` tensors (read in place)."""
     nsplit = nsplit or SLOT_WGRAD_SPLITS
-    part = _backend.ops().slot_wgrad(X, G, *slot_pair_lists(op, S), uses,
-                                     nsplit)
+    if isinstance(X, (list, tuple)):
+        if len(X) <= _SLOT_WGRAD_MAX_LIST:
+            part = _backend.ops().slot_wgrad_list(
+                [x.contiguous() for x in X], [g.contiguous() for g in G],
+                *slot_pair_lists(op, S), nsplit)
+            X = X[0]
+        else:
+            X, G = torch.cat(X, 0), torch.cat(G, 0)
+            part = None
+    else:
+        part = None
+    if part is None:
+        part = _backend.ops().slot_wgrad(X.contiguous(), G.contiguous(),
+                                         *slot_pair_lists(op, S), uses,
+                                         nsplit)
     out = torch.empty(S * _SLOT_C, _SLOT_C, dtype=torch.float32,
                       device=X.device)
     _backend.ops().reduce_add_rows(part.view(nsplit, S * _SLOT_C, _SLOT_C),

@@ -110,6 +110,13 @@ class LoopGrad(object):
             lst = self._kept[name] = [None] * self.uses
         lst[idx] = tensor
 
+    def kept_list(self, name):
+        """The kept contributions of all uses, in use order (for kernels
+        that read them in place)."""
+        lst = self._kept[name]
+        assert all(t is not None for t in lst), name
+        return list(lst)
+
     def kept(self, name):
         """Concatenation (dim 0, use order) of the kept contributions (one
         ``cat_rows`` HIP launch on the GPU: torch.cat splits a 10-way list

@@ -282,6 +282,11 @@ def test_slot_weight_grad_matches_dense(uses, S, n_max):
         ref += torch.einsum('jc,jko->kco', Xu, dY)
     # The kernel rounds a_e * X to bf16 (MFMA operand).
     assert _close(dW, ref, 2e-2)
+    # Per-use tensors read in place through the pointer table: identical
+    # summation order, hence bit-identical to the stacked form.
+    Xs = [X[u * N:(u + 1) * N].clone() for u in range(uses)]
+    Gs = [G[u * N:(u + 1) * N].clone() for u in range(uses)]
+    assert torch.equal(slot_weight_grad(Xs, Gs, op, S, uses, nsplit=3), dW)
 
 
 def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch):
