@@ -449,6 +449,242 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_kernel(
   SC_STAMP(4);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-specialised variant (no Z output): waves 0-3 are MFMA waves, each owns
+// 16 tile rows and ALL 128 output channels (Z_k computed once per row block,
+// no duplicate), waves 4-7 are helpers that clear / scatter the A tiles and
+// issue the W_{k+1} DMA while the MFMA waves run slot k.  One barrier per
+// slot; the ablations of the 8-wave kernel (docs/performance.md) showed its
+// DMA, scatter and MFMA phases adding up instead of overlapping.
+constexpr size_t kScLdsWs = (size_t)3 * kScWImg * 2 +
+                            (size_t)3 * kScATile * 2 + (size_t)kScECap * 6 +
+                            kScC * 4 + 16;
+static_assert(kScC * kScAP <= 3 * kScATile, "xt must fit the A tiles");
+
+template <bool TRANS, typename TOUT>
+__global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
+    const __hip_bfloat16* __restrict__ Xg, const int* __restrict__ tiles,
+    const int* __restrict__ soff, const int* __restrict__ ecode,
+    const __hip_bfloat16* __restrict__ evalg, int S,
+    const __hip_bfloat16* __restrict__ Wimg, const float* __restrict__ bias,
+    int relu, TOUT* __restrict__ out, const __hip_bfloat16* __restrict__ addg,
+    int ldadd) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS char* smem = (DGMC_LDS char*)smem_raw;
+  DGMC_LDS __bf16* wbuf = (DGMC_LDS __bf16*)smem;        // [3][128][128]
+  DGMC_LDS __bf16* abuf = wbuf + 3 * kScWImg;             // [3][64][72]
+  DGMC_LDS __bf16* xt = abuf;                 // [128][72], prologue only
+  DGMC_LDS int* ecs = (DGMC_LDS int*)(abuf + 3 * kScATile); // [kScECap]
+  DGMC_LDS __bf16* evs = (DGMC_LDS __bf16*)(ecs + kScECap);  // [kScECap]
+  DGMC_LDS float* bsh = (DGMC_LDS float*)(evs + kScECap);    // [128]
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ln = lane & 15, lq = lane >> 4;
+  // Roles: waves 0-3 MFMA, 4-5 A-tile maintenance (LDS only), 6-7 W DMA
+  // (global_load_lds only, never an LDS read: nothing makes them wait on
+  // their own DMA except the counted wait before the barrier).
+  const bool mw = wave < 4;
+  const bool sw = wave == 4 || wave == 5;
+  const int sid = tid - 256, did = tid - 384;
+  const __bf16* X = reinterpret_cast<const __bf16*>(Xg);
+  const __bf16* W = reinterpret_cast<const __bf16*>(Wimg);
+  const __bf16* ev = reinterpret_cast<const __bf16*>(evalg);
+
+  const int t = blockIdx.x;
+  const int r0 = tiles[4 * t], rows = tiles[4 * t + 1] - r0;
+  const int e0 = tiles[4 * t + 2];
+  const int E = tiles[4 * t + 3] & 0xffff;
+  if (rows <= 0) return;
+
+  const int sof_v = lane <= S ? soff[t * (S + 1) + lane] : 0;
+  auto sof = [&](int k) __attribute__((always_inline)) {
+    return __builtin_amdgcn_readlane(sof_v, k);
+  };
+  const bool staged = E <= kScECap;
+  // W_k image (rows = output channels) -> wbuf[k & 1]; LDS chunk p (16 B)
+  // of row p/16 holds global chunk (p%16) ^ (row%16).  nthr threads from
+  // thread index i0 issue it (all 512 in the prologue, the helpers later).
+  // The thread count is a compile-time constant: the unrolled pieces then
+  // have provably disjoint LDS targets (a runtime count made the compiler
+  // wait vmcnt(0) between consecutive global_load_lds).
+  auto load_w = [&](int k, int i, auto nthr_c) __attribute__((always_inline)) {
+    constexpr int nthr = decltype(nthr_c)::value;
+    const __bf16* src = W + (size_t)k * kScWImg;
+    DGMC_LDS __bf16* dst = wbuf + (k % 3) * kScWImg;
+    const int wv = i >> 6;
+    constexpr int nw = nthr >> 6;
+#pragma unroll
+    for (int j = 0; j < kScWImg / 8 / nthr; ++j) {
+      const int p = (j * nw + wv) * 64 + (i & 63);
+      const int row = p >> 4, jj = p & 15;
+      __builtin_amdgcn_global_load_lds(
+          (sc_gptr)(src + row * kScC + ((jj ^ (row & 15)) << 3)),
+          (DGMC_LDS void*)(dst + (j * nw + wv) * 64 * 8), 16, 0, 0);
+    }
+  };
+  auto scatter = [&](int k, bool clear, int i, int nthr)
+      __attribute__((always_inline)) {
+    DGMC_LDS __bf16* tile = abuf + (k % 3) * kScATile;
+    const int hi = sof(k + 1);
+    for (int e = sof(k) + i; e < hi; e += nthr) {
+      const int code = staged ? ecs[e] : ecode[e0 + e];
+      const __bf16 v = clear ? (__bf16)0.f : (staged ? evs[e] : ev[e0 + e]);
+      const int dl = code >> 8, sl = code & 255;
+      tile[TRANS ? sl * kScAP + dl : dl * kScAP + sl] = v;
+    }
+  };
+
+  // ---- prologue (all waves) -------------------------------------------------
+  if (staged)
+    for (int e = tid; e < E; e += kScCT) {
+      ecs[e] = ecode[e0 + e];
+      evs[e] = ev[e0 + e];
+    }
+  using All = std::integral_constant<int, kScCT>;
+  load_w(0, tid, All{});
+  if (S > 1) load_w(1, tid, All{});
+  if (tid < kScC) bsh[tid] = bias ? bias[tid] : 0.f;
+#pragma unroll
+  for (int i = 0; i < kScT * kScC / 8 / kScCT; ++i) {
+    const int c = tid + i * kScCT;
+    const int row = c & 63, cc = c >> 6;
+    sc_bf16x8 v = {};
+    if (row < rows)
+      v = *reinterpret_cast<const sc_bf16x8*>(X + (size_t)(r0 + row) * kScC +
+                                              cc * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xt[(cc * 8 + e) * kScAP + row] = v[e];
+  }
+  __syncthreads();
+  sc_bf16x8 xa[8][2];
+  if (mw) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        xa[m][c] = *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(
+            xt + (16 * m + ln) * kScAP + 32 * c + 8 * lq);
+  }
+  __syncthreads();                                // xt (= A tiles) free
+  {
+    const sc_bf16x8 z = {};
+    for (int i = tid; i < 3 * kScATile / 8; i += kScCT)
+      *reinterpret_cast<DGMC_LDS sc_bf16x8*>(abuf + i * 8) = z;
+  }
+  __syncthreads();
+  scatter(0, false, tid, kScCT);
+  __syncthreads();                                // W_0, A_0 ready
+
+  // MFMA wave w: tile rows 16 w .. +15, ALL 128 output channels (Z_k is
+  // computed once per row block).
+  const int node = 16 * (wave & 3) + ln;
+  sc_f32x4 ot[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) ot[m] = sc_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k = 0; k < S; ++k) {
+    if (mw) {
+      DGMC_LDS const __bf16* at =
+          abuf + (k % 3) * kScATile + node * kScAP + 8 * lq;
+      const sc_bf16x8 b0 = *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(at);
+      const sc_bf16x8 b1 =
+          *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(at + 32);
+      DGMC_LDS const __bf16* wb = wbuf + (k % 3) * kScWImg + ln * kScC;
+      sc_bf16x8 wf[2][8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+        wf[0][m] = *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(
+            wb + m * 16 * kScC + ((lq ^ ln) << 3));
+      sc_f32x4 zt[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        zt[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            xa[m][0], b0, sc_f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        zt[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[m][1], b1, zt[m],
+                                                        0, 0, 0);
+      }
+      sc_bf16x8 zb[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          zb[c][r] = (__bf16)zt[2 * c][r];
+          zb[c][4 + r] = (__bf16)zt[2 * c + 1][r];
+        }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c + 1 < 4) {
+#pragma unroll
+          for (int m = 0; m < 8; ++m)
+            wf[(c + 1) & 1][m] = *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(
+                wb + m * 16 * kScC + (((4 * (c + 1) + lq) ^ ln) << 3));
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+          ot[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c & 1][m], zb[c],
+                                                          ot[m], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 10, 0);  // A + W chunk 0
+#pragma unroll
+      for (int i = 0; i < 16; ++i)                          // Z_k
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int i = 0; i < 24; ++i) {                        // chunks 0-2
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);    // chunk 3
+      __builtin_amdgcn_s_barrier();
+    } else if (sw) {
+      // A tile of slot k-1 cleared, slot k+1 scattered (buffers the MFMA
+      // waves do not read this step); stores visible before the barrier.
+      if (k >= 1) scatter(k - 1, true, sid, 128);
+      if (k + 1 < S) scatter(k + 1, false, sid, 128);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      // W_{k+2} into the buffer of slot k-1 (two steps to land); before the
+      // barrier only W_{k+1} (the previous step's 16 pieces) must be in.
+      if (k + 2 < S) {
+        load_w(k + 2, did, std::integral_constant<int, 128>{});
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  // ---- epilogue: MFMA lane holds out[node][16m + 4q + r] --------------------
+  if (!mw || node >= rows) return;
+  TOUT* orow = out + (size_t)(r0 + node) * kScC + 4 * lq;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = ot[m][r] + bsh[16 * m + 4 * lq + r];
+    if (addg) {
+      const sc_bf16x4 ad = *reinterpret_cast<const sc_bf16x4*>(
+          reinterpret_cast<const __bf16*>(addg) +
+          (size_t)(r0 + node) * ldadd + 16 * m + 4 * lq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (float)ad[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (relu) v[r] = fmaxf(v[r], 0.f);
+    }
+    if constexpr (sizeof(TOUT) == 2) {
+      const sc_bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2],
+                           (__bf16)v[3]};
+      *reinterpret_cast<sc_bf16x4*>(orow + 16 * m) = o;
+    } else {
+      *reinterpret_cast<sc_f32x4*>(orow + 16 * m) =
+          sc_f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+}
+
 at::Tensor slot_conv_stamps() {
   long long h[16];
   DGMC_CHECK_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sc_stamps), sizeof(h)));
@@ -467,6 +703,15 @@ static int sc_debug() {
   return v;
 }
 
+// DGMC_SC_WS=0 selects the 8-wave kernel without wave specialisation.
+static bool sc_ws() {
+  static bool v = [] {
+    const char* e = getenv("DGMC_SC_WS");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 template <bool TRANS, bool WRITE_Z, typename TOUT>
 static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                              const at::Tensor& soff, const at::Tensor& ecode,
@@ -474,6 +719,27 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                              const at::Tensor& Wimg, const float* bias,
                              bool relu, at::Tensor& out, __hip_bfloat16* Z,
                              const __hip_bfloat16* add, int ldadd) {
+  const int T = tiles.size(0);
+  if constexpr (!WRITE_Z) {
+    if (sc_ws()) {
+      auto kw = slot_conv_ws_kernel<TRANS, TOUT>;
+      static bool ws_attr = false;
+      if (!ws_attr) {
+        DGMC_CHECK_HIP(hipFuncSetAttribute(
+            reinterpret_cast<const void*>(kw),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScLdsWs));
+        ws_attr = true;
+      }
+      hipLaunchKernelGGL(
+          kw, dim3(T), dim3(kScCT), kScLdsWs, stream(),
+          reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
+          tiles.data_ptr<int>(), soff.data_ptr<int>(), ecode.data_ptr<int>(),
+          reinterpret_cast<const __hip_bfloat16*>(eval.data_ptr()), S,
+          reinterpret_cast<const __hip_bfloat16*>(Wimg.data_ptr()), bias,
+          relu ? 1 : 0, reinterpret_cast<TOUT*>(out.data_ptr()), add, ldadd);
+      return;
+    }
+  }
   auto kern = slot_conv_kernel<TRANS, WRITE_Z, TOUT>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -482,7 +748,6 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScLds));
     attr_set = true;
   }
-  const int T = tiles.size(0);
   hipLaunchKernelGGL(kern, dim3(T), dim3(kScCT), kScLds, stream(),
                      reinterpret_cast<const __hip_bfloat16*>(X.data_ptr()),
                      tiles.data_ptr<int>(), soff.data_ptr<int>(),
