@@ -115,6 +115,13 @@ at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                       const at::Tensor& esrc, const at::Tensor& edst,
                       const at::Tensor& evals, const at::Tensor& soff,
                       int64_t U, int64_t nsplit);
+void adam_multi(at::TensorList params, at::TensorList grads,
+                at::TensorList exp_avg, at::TensorList exp_avg_sq,
+                const at::Tensor& step,
+                const c10::optional<at::Tensor>& found_inf, double lr,
+                double beta1, double beta2, double eps, double weight_decay);
+void adam_step_inc(const at::Tensor& step,
+                   const c10::optional<at::Tensor>& found_inf);
 at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
                            const at::Tensor& esrc, const at::Tensor& edst,
                            const at::Tensor& evals, const at::Tensor& soff,
@@ -212,6 +219,11 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_wgrad(Tensor X, Tensor G, Tensor esrc, Tensor edst, Tensor evals, "
       "Tensor soff, int U, int nsplit) -> Tensor");
   m.def(
+      "adam_multi(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, "
+      "Tensor(c!)[] exp_avg_sq, Tensor step, Tensor? found_inf, float lr, "
+      "float beta1, float beta2, float eps, float weight_decay) -> ()");
+  m.def("adam_step_inc(Tensor(a!) step, Tensor? found_inf) -> ()");
+  m.def(
       "slot_wgrad_list(Tensor[] xs, Tensor[] gs, Tensor esrc, Tensor edst, "
       "Tensor evals, Tensor soff, int nsplit) -> Tensor");
   m.def(
@@ -266,6 +278,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
   m.impl("slot_wgrad", &dgmc::slot_wgrad);
   m.impl("slot_wgrad_list", &dgmc::slot_wgrad_list);
+  m.impl("adam_multi", &dgmc::adam_multi);
+  m.impl("adam_step_inc", &dgmc::adam_step_inc);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

@@ -24,6 +24,10 @@ import torch.distributed as dist
 from .dist import is_distributed
 
 
+def _pad4(n):
+    return (n + 3) // 4 * 4
+
+
 class GradBucketAllReducer(object):
     r"""Attach to ``module``; call :meth:`finish` after ``backward()``.
 
@@ -44,7 +48,9 @@ class GradBucketAllReducer(object):
             if self.distributed else 1
         self.overlap = overlap and self.distributed
         dev = self.params[0].device if self.params else torch.device('cpu')
-        total = sum(p.numel() for p in self.params)
+        # Every gradient view starts on a 16-byte boundary (vectorised
+        # optimizer / finiteness kernels); the padding stays zero.
+        total = sum(_pad4(p.numel()) for p in self.params)
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
 
         # Layout: reverse registration order (≈ backward completion order).
@@ -59,7 +65,7 @@ class GradBucketAllReducer(object):
             self._slot[p] = (offset, n)
             cur.append(p)
             cur_bytes += 4 * n
-            offset += n
+            offset += _pad4(n)
         if cur:
             self.buckets.append(cur)
         self._bucket_of = {}

@@ -151,6 +151,11 @@ class PairTrainer(object):
             # Unfused CPU Adam has no found_inf input: skip on the host.
             if self._found_inf.item() != 0:
                 return
+        from .runtime import optim as hip_optim
+        if hip_optim.supported(self.optimizer):
+            hip_optim.hip_adam_step(
+                self.optimizer, self._found_inf if self.guard else None)
+            return
         self.optimizer.step()
 
     def _static_body(self, bucket=-1):

@@ -666,3 +666,48 @@ def test_nonfinite_flag():
     x[-1] = float('inf')
     _backend.ops().nonfinite_flag(x, flag, cnt)
     assert float(flag) == 1.0 and float(cnt) == 2.0
+
+
+def test_hip_adam_matches_torch_adam():
+    """Multi-tensor HIP Adam == torch.optim.Adam (same state schema), skips
+    on found_inf, and survives a state_dict round trip."""
+    from deep_graph_matching_consensus_amd.runtime import optim as hip_optim
+    torch.manual_seed(0)
+    shapes = [(37, 5), (1, ), (4096 * 3 + 12, ), (128, 128)]
+    p_ref = [torch.randn(s, device=DEV) for s in shapes]
+    p_hip = [p.clone() for p in p_ref]
+    flat = torch.zeros(sum((p.numel() + 3) // 4 * 4 for p in p_hip),
+                       device=DEV)
+    off = 0
+    for p in p_hip:                      # grads as aligned flat-buffer views
+        p.grad = flat[off:off + p.numel()].view_as(p)
+        off += (p.numel() + 3) // 4 * 4
+    ref = torch.optim.Adam([torch.nn.Parameter(p) for p in p_ref], lr=1e-2,
+                           weight_decay=1e-3)
+    hip_params = [torch.nn.Parameter(p) for p in p_hip]
+    for p, q in zip(hip_params, p_hip):
+        p.grad = q.grad
+    opt = torch.optim.Adam(hip_params, lr=1e-2, weight_decay=1e-3)
+    assert hip_optim.supported(opt)
+    found = torch.zeros((), device=DEV)
+    for it in range(4):
+        grads = [torch.randn(s, device=DEV) for s in shapes]
+        for p, g in zip(ref.param_groups[0]['params'], grads):
+            p.grad = g.clone()
+        for p, g in zip(hip_params, grads):
+            p.grad.copy_(g)
+        if it == 2:                      # non-finite step: skipped
+            found.fill_(1.0)
+            hip_optim.hip_adam_step(opt, found)
+            found.zero_()
+            continue
+        ref.step()
+        hip_optim.hip_adam_step(opt, found)
+    for a, b in zip(ref.param_groups[0]['params'], hip_params):
+        torch.testing.assert_close(b, a, atol=1e-6, rtol=1e-5)
+    sd = opt.state_dict()
+    assert float(sd['state'][0]['step']) == 3.0
+    opt2 = torch.optim.Adam(hip_params, lr=1e-2, weight_decay=1e-3)
+    opt2.load_state_dict(sd)
+    hip_optim.hip_adam_step(opt2, None)
+    assert float(opt2.state[hip_params[1]]['step']) == 4.0
