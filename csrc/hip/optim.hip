@@ -7,9 +7,11 @@
 // Replaces the fused torch Adam (multi_tensor_apply: ~122 us for the 9.5 M
 // fp32 parameters of the PascalVOC flagship, ~2.2 TB/s): ONE launch over a
 // pointer table of every parameter, float4 loads/stores, 4 float4 per
-// thread in flight.  Reads the device step counter (incremented by
-// adam_step_inc) and the non-finite flag, so the whole update is
-// capturable in a hipGraph and skips itself on the device.
+// thread in flight.  Every parameter keeps its own fp32 device step counter
+// (torch's per-parameter ``state['step']``, incremented by adam_step_inc -
+// one thread per counter - unless found_inf is set), and the non-finite flag
+// is read on the device, so the whole update is capturable in a hipGraph
+// and skips itself on the device.
 #include "common.h"
 
 namespace dgmc {
@@ -26,6 +28,7 @@ struct AdamTable {
   const float* g[kAdamMax];
   float* m[kAdamMax];
   float* v[kAdamMax];
+  const float* s[kAdamMax];           // per-parameter step (already bumped)
   int n[kAdamMax];
   int first_block[kAdamMax + 1];
   int count;
@@ -33,15 +36,19 @@ struct AdamTable {
 
 }  // namespace
 
-__global__ void adam_step_inc_kernel(float* __restrict__ step,
+struct StepTable {
+  float* s[kAdamMax];
+  int count;
+};
+
+__global__ void adam_step_inc_kernel(const StepTable T,
                                      const float* __restrict__ found_inf) {
-  if (threadIdx.x == 0 && blockIdx.x == 0)
-    *step += (found_inf && *found_inf != 0.f) ? 0.f : 1.f;
+  const int i = threadIdx.x;
+  if (i < T.count && !(found_inf && *found_inf != 0.f)) *T.s[i] += 1.f;
 }
 
 __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
-    const AdamTable T, const float* __restrict__ step,
-    const float* __restrict__ found_inf, float lr, float b1, float b2,
+    const AdamTable T, const float* __restrict__ found_inf, float lr, float b1, float b2,
     float eps, float wd) {
   if (found_inf && *found_inf != 0.f) return;   // non-finite step: skip
   const int b = blockIdx.x;
@@ -49,7 +56,7 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
   while (ti + 1 < T.count && T.first_block[ti + 1] <= b) ++ti;
   const int n = T.n[ti];
   const int base = (b - T.first_block[ti]) * kAdamBlock;
-  const float t = *step;
+  const float t = *T.s[ti];
   const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
   const float step_size = lr / bc1, rs2 = 1.f / sqrtf(bc2);
   float* __restrict__ P = T.p[ti];
@@ -96,21 +103,27 @@ __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
 }
 
 // params / grads / exp_avg / exp_avg_sq: fp32 contiguous, 16-byte aligned,
-// pairwise equal sizes; step: fp32 0-dim device counter (already
-// incremented for this step); found_inf: optional fp32 0-dim flag.
+// pairwise equal sizes; steps: one fp32 1-element device counter per param
+// (already incremented for this step); found_inf: optional fp32 0-dim flag.
+namespace {
+void check_step(const at::Tensor& s, const at::Tensor& like) {
+  TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat &&
+                  s.numel() == 1 && s.device() == like.device(),
+              "adam: fp32 1-element step counter on the parameter's device");
+}
+}  // namespace
+
 void adam_multi(at::TensorList params, at::TensorList grads,
                 at::TensorList exp_avg, at::TensorList exp_avg_sq,
-                const at::Tensor& step,
+                at::TensorList steps,
                 const c10::optional<at::Tensor>& found_inf, double lr,
                 double beta1, double beta2, double eps, double weight_decay) {
   const int64_t count = (int64_t)params.size();
   TORCH_CHECK(count >= 1 && (int64_t)grads.size() == count &&
                   (int64_t)exp_avg.size() == count &&
-                  (int64_t)exp_avg_sq.size() == count,
-              "adam_multi: one grad / exp_avg / exp_avg_sq per param");
-  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat &&
-                  step.numel() == 1,
-              "adam_multi: fp32 device step counter");
+                  (int64_t)exp_avg_sq.size() == count &&
+                  (int64_t)steps.size() == count,
+              "adam_multi: one grad / exp_avg / exp_avg_sq / step per param");
   const float* fi = nullptr;
   if (found_inf.has_value() && found_inf->defined()) {
     TORCH_CHECK(found_inf->is_cuda() &&
@@ -119,7 +132,7 @@ void adam_multi(at::TensorList params, at::TensorList grads,
                 "adam_multi: fp32 found_inf flag");
     fi = found_inf->data_ptr<float>();
   }
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(step.device());
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(params[0].device());
   for (int64_t c0 = 0; c0 < count; c0 += kAdamMax) {
     AdamTable T{};
     T.count = (int)std::min<int64_t>(kAdamMax, count - c0);
@@ -134,6 +147,8 @@ void adam_multi(at::TensorList params, at::TensorList grads,
                     "adam_multi: fp32 contiguous 16-B aligned tensors of "
                     "equal size");
       TORCH_CHECK(params[c0 + j].numel() < INT32_MAX, "adam_multi: size");
+      check_step(steps[c0 + j], params[c0 + j]);
+      T.s[j] = steps[c0 + j].data_ptr<float>();
       T.p[j] = params[c0 + j].data_ptr<float>();
       T.g[j] = grads[c0 + j].data_ptr<float>();
       T.m[j] = exp_avg[c0 + j].data_ptr<float>();
@@ -145,25 +160,32 @@ void adam_multi(at::TensorList params, at::TensorList grads,
     T.first_block[T.count] = blocks;
     if (blocks == 0) continue;
     hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(kAdamThreads), 0,
-                       stream(), T, step.data_ptr<float>(), fi, (float)lr,
+                       stream(), T, fi, (float)lr,
                        (float)beta1, (float)beta2, (float)eps,
                        (float)weight_decay);
     DGMC_CHECK_LAUNCH();
   }
 }
 
-void adam_step_inc(const at::Tensor& step,
+void adam_step_inc(at::TensorList steps,
                    const c10::optional<at::Tensor>& found_inf) {
-  TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat &&
-                  step.numel() == 1,
-              "adam_step_inc: fp32 device step counter");
+  const int64_t count = (int64_t)steps.size();
+  if (count == 0) return;
   const float* fi = nullptr;
   if (found_inf.has_value() && found_inf->defined())
     fi = found_inf->data_ptr<float>();
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(step.device());
-  hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(64), 0, stream(),
-                     step.data_ptr<float>(), fi);
-  DGMC_CHECK_LAUNCH();
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(steps[0].device());
+  for (int64_t c0 = 0; c0 < count; c0 += kAdamMax) {
+    StepTable T{};
+    T.count = (int)std::min<int64_t>(kAdamMax, count - c0);
+    for (int j = 0; j < T.count; ++j) {
+      check_step(steps[c0 + j], steps[0]);
+      T.s[j] = steps[c0 + j].data_ptr<float>();
+    }
+    hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(kAdamMax), 0,
+                       stream(), T, fi);
+    DGMC_CHECK_LAUNCH();
+  }
 }
 
 }  // namespace dgmc

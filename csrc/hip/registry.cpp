@@ -117,10 +117,10 @@ at::Tensor slot_wgrad(const at::Tensor& X, const at::Tensor& G,
                       int64_t U, int64_t nsplit);
 void adam_multi(at::TensorList params, at::TensorList grads,
                 at::TensorList exp_avg, at::TensorList exp_avg_sq,
-                const at::Tensor& step,
+                at::TensorList steps,
                 const c10::optional<at::Tensor>& found_inf, double lr,
                 double beta1, double beta2, double eps, double weight_decay);
-void adam_step_inc(const at::Tensor& step,
+void adam_step_inc(at::TensorList steps,
                    const c10::optional<at::Tensor>& found_inf);
 at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
                            const at::Tensor& esrc, const at::Tensor& edst,
@@ -220,9 +220,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor soff, int U, int nsplit) -> Tensor");
   m.def(
       "adam_multi(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, "
-      "Tensor(c!)[] exp_avg_sq, Tensor step, Tensor? found_inf, float lr, "
+      "Tensor(c!)[] exp_avg_sq, Tensor[] steps, Tensor? found_inf, float lr, "
       "float beta1, float beta2, float eps, float weight_decay) -> ()");
-  m.def("adam_step_inc(Tensor(a!) step, Tensor? found_inf) -> ()");
+  m.def("adam_step_inc(Tensor(a!)[] steps, Tensor? found_inf) -> ()");
   m.def(
       "slot_wgrad_list(Tensor[] xs, Tensor[] gs, Tensor esrc, Tensor edst, "
       "Tensor evals, Tensor soff, int nsplit) -> Tensor");

@@ -120,6 +120,9 @@ __global__ __launch_bounds__(kScThreads) void slot_tile_plan_kernel(
   for (int i = tid; i <= rows; i += kScThreads) rp[i] = rowptr[r0 + i];
   __syncthreads();
   const int e0 = rp[0], E = rp[rows] - rp[0];
+  if (E > 0xFFFF) {                   // E is packed into 16 bits below
+    if (tid == 0) atomicOr(err, 4);
+  }
   if (tid == 0) {
     tiles[4 * t + 0] = r0;
     tiles[4 * t + 1] = r0 + rows;
@@ -461,6 +464,17 @@ constexpr size_t kScLdsWs = (size_t)3 * kScWImg * 2 +
                             kScC * 4 + 16;
 static_assert(kScC * kScAP <= 3 * kScATile, "xt must fit the A tiles");
 
+// Raw workgroup barrier of the wave-specialised kernel (no implicit
+// waitcnt: each role drains exactly the counters it must before arriving).
+// The empty asm statements with a memory clobber are compiler fences: no LDS
+// access of one slot step may be scheduled across the barrier into another
+// (s_barrier alone is not a memory operation to the optimiser).
+__device__ __forceinline__ void sc_raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <bool TRANS, typename TOUT>
 __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
     const __hip_bfloat16* __restrict__ Xg, const int* __restrict__ tiles,
@@ -634,14 +648,14 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);    // chunk 3
-      __builtin_amdgcn_s_barrier();
+      sc_raw_barrier();
     } else if (sw) {
       // A tile of slot k-1 cleared, slot k+1 scattered (buffers the MFMA
       // waves do not read this step); stores visible before the barrier.
       if (k >= 1) scatter(k - 1, true, sid, 128);
       if (k + 1 < S) scatter(k + 1, false, sid, 128);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      sc_raw_barrier();
     } else {
       // W_{k+2} into the buffer of slot k-1 (two steps to land); before the
       // barrier only W_{k+1} (the previous step's 16 pieces) must be in.
@@ -651,7 +665,7 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      __builtin_amdgcn_s_barrier();
+      sc_raw_barrier();
     }
   }
 

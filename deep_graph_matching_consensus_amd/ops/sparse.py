@@ -416,7 +416,8 @@ def _slot_conv_ok(op, x, K, C, S):
 
 def slot_conv_error(device):
     """Persistent int32 [1] flag the slot-conv kernel sets if a tile breaks
-    its contract (bit 0: > 64 rows, bit 1: an entry leaves its tile)."""
+    its contract (bit 0: > 64 rows, bit 1: an entry leaves its tile,
+    bit 2: > 65535 entries in one tile)."""
     key = str(device)
     err = _SLOT_ERR.get(key)
     if err is None:
@@ -471,25 +472,33 @@ def slot_weight_grad(X, G, op, S, uses, nsplit=None):
     X_u[j_e]^T G_u[i_e]`` for use-major stacks ``X, G [uses * N, C]`` or
     lists of the ``uses`` per-use ``[N, C]`` tensors (read in place)."""
     nsplit = nsplit or SLOT_WGRAD_SPLITS
-    if isinstance(X, (list, tuple)):
-        if len(X) <= _SLOT_WGRAD_MAX_LIST:
-            part = _backend.ops().slot_wgrad_list(
-                [x.contiguous() for x in X], [g.contiguous() for g in G],
-                *slot_pair_lists(op, S), nsplit)
-            X = X[0]
-        else:
-            X, G = torch.cat(X, 0), torch.cat(G, 0)
-            part = None
+    lists = slot_pair_lists(op, S)
+    M = _SLOT_WGRAD_MAX_LIST
+    stacked = not isinstance(X, (list, tuple))
+    if stacked and uses > M:
+        # More uses than the kernel's pointer table (num_steps > 16): per-use
+        # row views of the stacks, chunked below.
+        X, G = list(X.chunk(uses, 0)), list(G.chunk(uses, 0))
+        stacked = False
+    dev = X.device if stacked else X[0].device
+    out = torch.empty(S * _SLOT_C, _SLOT_C, dtype=torch.float32, device=dev)
+    if stacked:
+        chunks = [None]
     else:
-        part = None
-    if part is None:
-        part = _backend.ops().slot_wgrad(X.contiguous(), G.contiguous(),
-                                         *slot_pair_lists(op, S), uses,
-                                         nsplit)
-    out = torch.empty(S * _SLOT_C, _SLOT_C, dtype=torch.float32,
-                      device=X.device)
-    _backend.ops().reduce_add_rows(part.view(nsplit, S * _SLOT_C, _SLOT_C),
-                                   out, False)
+        X = [x.contiguous() for x in X]
+        G = [g.contiguous() for g in G]
+        chunks = range(0, len(X), M)
+    # <= M uses per launch; the chunks' split partials are folded into the
+    # same output in order (deterministic, no atomics).
+    for i, c in enumerate(chunks):
+        if c is None:
+            part = _backend.ops().slot_wgrad(X.contiguous(), G.contiguous(),
+                                             *lists, uses, nsplit)
+        else:
+            part = _backend.ops().slot_wgrad_list(X[c:c + M], G[c:c + M],
+                                                  *lists, nsplit)
+        _backend.ops().reduce_add_rows(
+            part.view(nsplit, S * _SLOT_C, _SLOT_C), out, i > 0)
     return out.view(S, _SLOT_C, _SLOT_C)
 
 

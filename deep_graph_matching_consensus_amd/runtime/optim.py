@@ -5,10 +5,17 @@
 ``exp_avg``, ``exp_avg_sq`` per parameter) - but the update itself is ONE
 launch over a pointer table of all parameters instead of torch's fused
 ``multi_tensor_apply`` (122 us -> see docs/performance.md for the PascalVOC
-flagship's 9.5 M parameters).  The step counter is a single fp32 device
-tensor shared by every parameter's state (re-shared after a load), read by
-the kernel after ``adam_step_inc`` bumps it unless ``found_inf`` is set, so
-the update is capturable and skips itself on the device.
+flagship's 9.5 M parameters).
+
+Every parameter keeps its OWN ``state['step']`` (an fp32 device scalar, as
+torch's capturable Adam keeps it): ``adam_step_inc`` bumps each counter on
+the device unless ``found_inf`` is set and the update kernel reads each
+parameter's own counter for its bias correction, so the update is
+capturable, skips itself on the device, and a parameter that gets its first
+gradient late (or a checkpoint with per-parameter steps) follows torch's
+per-parameter semantics exactly.  Counters are never shared between
+parameters, so a state dict saved here resumes correctly under
+``torch.optim.Adam`` and vice versa (``tests/test_checkpoint.py``).
 """
 import os
 
@@ -31,6 +38,20 @@ def supported(optimizer):
                                 for p in ps) and _backend.use_hip(ps[0]))
 
 
+def _device_step(st, p):
+    """``st['step']`` as this parameter's own fp32 device scalar (a torch
+    checkpoint loads it as a CPU tensor; converted once, then kept)."""
+    step = st.get('step')
+    if step is None:
+        step = torch.zeros((), dtype=torch.float32, device=p.device)
+    elif not (torch.is_tensor(step) and step.device == p.device and
+              step.dtype == torch.float32 and step.dim() == 0):
+        step = torch.as_tensor(step, dtype=torch.float32).reshape(()) \
+            .to(p.device).clone()
+    st['step'] = step
+    return step
+
+
 def hip_adam_step(optimizer, found_inf=None):
     """One Adam step of ``optimizer`` (see module docstring)."""
     group = optimizer.param_groups[0]
@@ -38,13 +59,7 @@ def hip_adam_step(optimizer, found_inf=None):
     if not params:
         return
     state = optimizer.state
-    first = state[params[0]]
-    if 'step' not in first:
-        first['step'] = torch.zeros((), dtype=torch.float32,
-                                    device=params[0].device)
-    step = first['step']
-    if step.device != params[0].device or step.dtype != torch.float32:
-        step = first['step'] = step.to(params[0].device, torch.float32)
+    steps = []
     for p in params:
         st = state[p]
         if 'exp_avg' not in st:
@@ -52,12 +67,12 @@ def hip_adam_step(optimizer, found_inf=None):
                 p, memory_format=torch.preserve_format)
             st['exp_avg_sq'] = torch.zeros_like(
                 p, memory_format=torch.preserve_format)
-        st['step'] = step                      # one shared counter
+        steps.append(_device_step(st, p))
     b1, b2 = group['betas']
     ops = _backend.ops()
-    ops.adam_step_inc(step, found_inf)
+    ops.adam_step_inc(steps, found_inf)
     ops.adam_multi(params, [p.grad for p in params],
                    [state[p]['exp_avg'] for p in params],
-                   [state[p]['exp_avg_sq'] for p in params], step, found_inf,
+                   [state[p]['exp_avg_sq'] for p in params], steps, found_inf,
                    float(group['lr']), float(b1), float(b2),
                    float(group['eps']), float(group['weight_decay']))

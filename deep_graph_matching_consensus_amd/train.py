@@ -313,6 +313,12 @@ class PairTrainer(object):
         self.model.load_state_dict(state['model'])
         self.optimizer.load_state_dict(state['optimizer'])
         self.step_count = int(state.get('step', 0))
+        if getattr(self, '_graphs', None) is not None and self._captured:
+            # The optimizer state tensors were replaced: captured graphs
+            # hold their old addresses, so capture again on the next step.
+            self._graphs = [GraphedStep(self._bucket_body(i), warmup=2)
+                            for i in range(len(self.batchers))]
+            self._captured = False
         rng = state.get('rng', {})
         if 'torch' in rng:
             torch.set_rng_state(rng['torch'].cpu())

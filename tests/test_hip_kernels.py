@@ -711,3 +711,52 @@ def test_hip_adam_matches_torch_adam():
     opt2.load_state_dict(sd)
     hip_optim.hip_adam_step(opt2, None)
     assert float(opt2.state[hip_params[1]]['step']) == 4.0
+
+
+def test_hip_adam_state_round_trip_through_torch_adam(tmp_path):
+    """Per-parameter step counters: a HIP Adam state resumes under
+    torch.optim.Adam (and back) along the same trajectory as torch Adam
+    throughout, including a parameter whose first gradient arrives late."""
+    from deep_graph_matching_consensus_amd.runtime import optim as hip_optim
+    torch.manual_seed(1)
+    shapes = [(33, 7), (128, ), (5, )]
+    init = [torch.randn(s, device=DEV) for s in shapes]
+    grads = [[torch.randn(s, device=DEV) for s in shapes] for _ in range(9)]
+
+    def make():
+        ps = [torch.nn.Parameter(p.clone()) for p in init]
+        return ps, torch.optim.Adam(ps, lr=1e-2)
+
+    def feed(ps, it):
+        for j, (p, g) in enumerate(zip(ps, grads[it])):
+            # parameter 2 gets no gradient in the first two steps
+            p.grad = None if (j == 2 and it < 2) else g.clone()
+
+    ref_ps, ref = make()
+    for it in range(9):
+        feed(ref_ps, it)
+        ref.step()
+    ps, opt = make()
+    for it in range(3):                   # HIP
+        feed(ps, it)
+        hip_optim.hip_adam_step(opt)
+    steps = [float(opt.state[p]['step']) for p in ps]
+    assert steps == [3.0, 3.0, 1.0]
+    path = str(tmp_path / 'opt.pt')
+    torch.save(opt.state_dict(), path)
+    opt_t = torch.optim.Adam(ps, lr=1e-2)
+    opt_t.load_state_dict(torch.load(path, weights_only=True))
+    for it in range(3, 6):                # torch
+        feed(ps, it)
+        opt_t.step()
+    assert [float(opt_t.state[p]['step']) for p in ps] == [6.0, 6.0, 4.0]
+    opt_h = torch.optim.Adam(ps, lr=1e-2)
+    opt_h.load_state_dict(opt_t.state_dict())
+    for it in range(6, 9):                # HIP again
+        feed(ps, it)
+        hip_optim.hip_adam_step(opt_h)
+    assert [float(opt_h.state[p]['step']) for p in ps] == [9.0, 9.0, 7.0]
+    ids = {opt_h.state[p]['step'].data_ptr() for p in ps}
+    assert len(ids) == len(ps)            # never shared
+    for a, b in zip(ref_ps, ps):
+        torch.testing.assert_close(b, a, atol=1e-6, rtol=1e-5)

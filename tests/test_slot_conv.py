@@ -62,6 +62,7 @@ def _sizes(total_graphs, n_max, seed=1):
 
 
 def _close(a, b, tol):
+    a, b = a.detach(), b.detach()
     return float((a.float() - b).abs().max()) <= tol * float(b.abs().max()) \
         + 1e-3
 
@@ -266,7 +267,8 @@ def test_static_training_step_slot_conv_matches_unfused(monkeypatch):
 
 
 @pytest.mark.parametrize('uses,S,n_max',
-                         [(3, 26, 19), (1, 5, 8), (10, 26, 12)])
+                         [(3, 26, 19), (1, 5, 8), (10, 26, 12),
+                          (17, 26, 12), (33, 5, 8)])
 def test_slot_weight_grad_matches_dense(uses, S, n_max):
     from deep_graph_matching_consensus_amd.ops.sparse import slot_weight_grad
     op, flag = _graph_batch(_sizes(90, n_max, seed=5), S, seed=5)
@@ -289,9 +291,12 @@ def test_slot_weight_grad_matches_dense(uses, S, n_max):
     assert torch.equal(slot_weight_grad(Xs, Gs, op, S, uses, nsplit=3), dW)
 
 
-def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch):
-    """num_steps=4 consensus loop on a static batch: psi_2 weight gradients
-    from the slot wgrad kernel vs the dY stack + GEMM path."""
+@pytest.mark.parametrize('num_steps', [4, 17])
+def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch,
+                                                            num_steps):
+    """Consensus loop on a static batch: psi_2 weight gradients from the
+    slot wgrad kernel vs the dY stack + GEMM path (17 steps: more uses than
+    the kernel's pointer table, chunked)."""
     from deep_graph_matching_consensus_amd.datasets import (
         GraphStore, make_keypoint_datasets)
     from deep_graph_matching_consensus_amd.datasets.static_batch import \
@@ -304,7 +309,8 @@ def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch):
     batcher = StaticPairBatcher(store, 64, seed=1)
     torch.manual_seed(0)
     model = DGMC(SplineCNN(64, 64, 2, 2, cat=False),
-                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=4).to(DEV)
+                 SplineCNN(128, 128, 2, 2, cat=True),
+                 num_steps=num_steps).to(DEV)
     model.eval()
     assert batcher.load()
 
@@ -344,3 +350,72 @@ def test_slot_pair_lists_stable_counting_sort():
     assert torch.equal(evals, op.val[perm])
     cnt = torch.bincount(k, minlength=S)
     assert torch.equal(soff[1:].long(), torch.cumsum(cnt, 0))
+
+
+def _dense_case(seed=11):
+    """Dense 32-node graphs: two per 64-row tile with > 4096 entries per
+    tile, so the kernels read entries from global memory (unstaged path,
+    E > kScECap in csrc/hip/slot_conv.hip)."""
+    S = 26
+    op, flag = _graph_batch([32] * 24 + [17, 9, 30], S, deg=100, seed=seed)
+    op.tile_flag, op.tile_window = flag, 65 - 32
+    N = op.num_rows
+    g = torch.Generator(DEV).manual_seed(seed)
+    x = torch.randn(N, C, device=DEV, generator=g).bfloat16()
+    gy = torch.randn(N, C, device=DEV, generator=g).bfloat16()
+    w_lp = (torch.randn(C, S * C, device=DEV, generator=g) /
+            C ** 0.5).bfloat16()
+    bias = torch.randn(C, device=DEV, generator=g)
+    return op, S, x, gy, w_lp, bias
+
+
+def _dense_case_outputs():
+    ops = _backend.ops()
+    op, S, x, gy, w_lp, bias = _dense_case()
+    plan = slot_tile_plan(op, S)
+    out = ops.slot_conv(x, *plan, S, slot_conv_image(w_lp, C, False), False,
+                        bias, True, torch.float32, None)
+    gx = ops.slot_conv(gy, *plan, S, slot_conv_image(w_lp, C, True), True,
+                       None, False, torch.float32, None)
+    return op, plan, out, gx
+
+
+def test_slot_conv_unstaged_dense_tiles():
+    _, S, x, gy, w_lp, bias = _dense_case()
+    op, plan, out, gx = _dense_case_outputs()
+    # tiles[t] = (r0, r1, e0, E | largest slot bucket << 16): at least one
+    # tile holds more entries than the LDS staging capacity (4096)
+    E_tile = plan[0].view(-1, 4)[:, 3] & 0xFFFF
+    assert int(E_tile.max()) > 4096
+    A = op.to_dense().bfloat16().float()
+    y = (x.float() @ w_lp.float()).view(-1, C)
+    assert int(slot_conv_error(DEV)) == 0
+    assert _close(out, (A @ y + bias).relu(), 2e-2)
+    gx_ref = (A.t() @ gy.float()).view(op.num_rows, -1) @ w_lp.float().t()
+    assert _close(gx, gx_ref, 2e-2)
+
+
+def test_slot_conv_ws_matches_eight_wave_kernel(tmp_path):
+    """The wave-specialised kernel (default) against the 8-wave kernel
+    (DGMC_SC_WS=0, read once per process: run in a child process)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = str(tmp_path / 'eight_wave.pt')
+    code = (
+        'import sys, torch; sys.path.insert(0, {r!r}); '
+        'sys.path.insert(0, {t!r}); import test_slot_conv as t; '
+        'assert t._backend.hip_available(); '
+        '_, _, out, gx = t._dense_case_outputs(); '
+        'torch.save({{"out": out.cpu(), "gx": gx.cpu()}}, {p!r})').format(
+            r=root, t=os.path.join(root, 'tests'), p=path)
+    env = dict(os.environ, DGMC_SC_WS='0')
+    subprocess.run([sys.executable, '-c', code], env=env, check=True,
+                   timeout=300)
+    ref = torch.load(path, weights_only=True)
+    _, _, out, gx = _dense_case_outputs()
+    # Same operands, same fp32 accumulation per slot; the kernels differ in
+    # MFMA operand order only.
+    assert _close(out.cpu(), ref['out'], 1e-2)
+    assert _close(gx.cpu(), ref['gx'], 1e-2)
