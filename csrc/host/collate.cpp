@@ -142,7 +142,11 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   TORCH_CHECK(t_ids.numel() == B, "s_ids / t_ids size mismatch");
   const int64_t need = cap_s * 4 + cap_t * 2 + ecap_s * 3 + ecap_t * 3 +
                        2 * (B + 1) + 2 * B;
-  TORCH_CHECK(out.numel() >= need, "collate_pairs_padded: buffer too small");
+  // The buffer layout (datasets/static_batch.py::_views) is sized for exactly
+  // B pairs: any other count would shift every region after dense_t.
+  TORCH_CHECK(out.numel() == need,
+              "collate_pairs_padded: buffer size does not match B pairs at "
+              "these capacities");
   const int64_t G = node_ptr.numel() - 1;
   const int64_t C = pos_of_class.size(1);
   const int64_t E_all = edge_local.size(1);

@@ -200,6 +200,17 @@ class DevicePairLoader(object):
             yield self.store.collate(s_ids, t_ids)
 
     def forever(self):
+        """Endless full batches: epoch permutations are concatenated, so a
+        batch may straddle an epoch boundary and a shard with fewer sources
+        than ``batch_size`` (e.g. 2560 graphs over 8 ranks at batch 512)
+        still yields ``batch_size`` pairs per step (some sources twice)."""
+        bs = self.batch_size
+        order = np.empty(0, dtype=np.int64)
         while True:
-            for batch in self:
-                yield batch
+            while len(order) < bs:
+                nxt = self.rng.permutation(self.sources) if self.shuffle \
+                    else self.sources
+                order = np.concatenate([order, nxt])
+            s_ids, order = order[:bs], order[bs:]
+            t_ids = self.store.sample_partners(s_ids, self.rng)
+            yield self.store.collate(s_ids, t_ids)

@@ -148,9 +148,15 @@ class StaticPairBatcher(object):
 
     # ------------------------------------------------------------------
     def next_ids(self):
-        """Next sources (epoch permutation) and random valid partners."""
-        if self._order is None or self._pos + self.B > len(self._order):
-            self._order = self.rng.permutation(self.sources)
+        """Next ``B`` sources (concatenated epoch permutations: a batch may
+        straddle an epoch boundary, and a rank shard smaller than ``B`` -
+        2560 graphs over 8 ranks at batch 512 - repeats sources) and random
+        valid partners."""
+        while self._order is None or self._pos + self.B > len(self._order):
+            rest = self._order[self._pos:] if self._order is not None \
+                else self.sources[:0]
+            self._order = np.concatenate(
+                [rest, self.rng.permutation(self.sources)])
             self._pos = 0
         s = self._order[self._pos:self._pos + self.B]
         self._pos += self.B
@@ -163,6 +169,11 @@ class StaticPairBatcher(object):
         """
         if s_ids is None:
             s_ids, t_ids = self.next_ids()
+        if len(s_ids) != self.B or len(t_ids) != self.B:
+            # The static buffer layout is sized for exactly B pairs.
+            raise ValueError('static batch of {} pairs needs exactly {} '
+                             'source / target ids, got {} / {}'.format(
+                                 self.B, self.B, len(s_ids), len(t_ids)))
         slot = self._slot
         self._slot ^= 1
         if self._events[slot] is not None:

@@ -30,6 +30,7 @@ from .datasets.device_loader import DevicePairLoader
 from .datasets.static_batch import StaticPairBatcher, bucket_capacities
 from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
+from .runtime.tuning import use_tuned_gemms
 
 
 class PairTrainer(object):
@@ -66,6 +67,8 @@ class PairTrainer(object):
         self.reducer = parallel.GradBucketAllReducer(
             model, overlap=overlap and mode == 'eager')
         cuda = self.device.type == 'cuda'
+        if cuda:
+            use_tuned_gemms()     # measured GEMM solutions (runtime/tuning.py)
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda,
                                           capturable=mode == 'graph')
@@ -365,6 +368,8 @@ class KGTrainer(object):
         cuda = self.device.type == 'cuda'
         self.graph = graph and cuda
         self.bf16 = bf16 and cuda
+        if cuda:
+            use_tuned_gemms()
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda, capturable=self.graph)
         self.last_loss = torch.zeros((), device=self.device)

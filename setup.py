@@ -44,6 +44,6 @@ setup(
     version=__version__,
     description='MI355X-native Deep Graph Matching Consensus',
     packages=find_packages(include=[PKG, PKG + '.*']),
-    package_data={PKG: ['_C_*.so']},
+    package_data={PKG: ['_C_*.so', 'runtime/tuned/*.csv']},
     cmdclass={'build_ext': NativeBuild, 'clean_native': NativeClean},
 )

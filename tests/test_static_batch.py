@@ -74,6 +74,38 @@ def test_static_consensus_finite_cpu():
         assert p.grad is None or torch.isfinite(p.grad).all()
 
 
+@pytest.mark.skipif(not _backend.host_available(),
+                    reason='native host library not built')
+def test_rank_shard_smaller_than_batch():
+    """8-rank sharding of a small store: every rank's shard has fewer source
+    graphs than the batch; every batch still has exactly B pairs with
+    consistent pair pointers (regression: a short id list shifted the
+    static buffer layout)."""
+    from deep_graph_matching_consensus_amd.datasets import DevicePairLoader
+    groups = make_keypoint_datasets(graphs=8, feature_dim=16, seed=4)
+    store = GraphStore(groups, 'cpu')
+    B, world = 64, 8
+    for rank in range(world):
+        sources = np.arange(store.num_graphs)[rank::world]
+        assert len(sources) < B
+        batcher = StaticPairBatcher(store, B, sources=sources, seed=rank)
+        n = store.node_ptr[1:] - store.node_ptr[:-1]
+        for _ in range(3):
+            s, t = batcher.next_ids()
+            assert len(s) == len(t) == B
+            assert set(s.tolist()) <= set(sources.tolist())
+            assert batcher.load(s, t)
+            ptr = batcher.v['ptr_s'].clone()
+            assert int(ptr[0]) == 0 and int(ptr[-1]) == int(n[s].sum())
+            assert bool((ptr[1:] >= ptr[:-1]).all())
+        with pytest.raises(ValueError):
+            batcher.load(s[:B - 1], t[:B - 1])
+        loader = DevicePairLoader(store, B, sources=sources, seed=rank)
+        it = loader.forever()
+        for _ in range(3):
+            assert next(it).num_graphs == B
+
+
 def test_capacity_covers_probe():
     store, batcher, _ = _setup()
     n = store.node_ptr[1:] - store.node_ptr[:-1]
