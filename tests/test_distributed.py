@@ -103,27 +103,32 @@ def test_grad_allreduce_matches_average(overlap):
     assert torch.equal(p0, p1)
 
 
-def _bench_worker(rank, world, port, mode, out_path):
+def _bench_worker(rank, world, port, mode, out_path, batch=16):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
                       RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS='1')
+    torch.set_num_threads(1)
     import bench
-    bench.main(['--steps', '2', '--warmup', '1', '--batch-size', '16',
+    bench.main(['--steps', '2', '--warmup', '1', '--batch-size', str(batch),
                 '--graphs-per-category', '8', '--dtype', 'fp32', '--mode',
                 mode, '--json-out', out_path])
 
 
-@pytest.mark.parametrize('mode', ['eager', 'static'])
-def test_bench_two_ranks_gloo(tmp_path, mode):
+@pytest.mark.parametrize('mode,world,batch', [('eager', 2, 16),
+                                              ('static', 2, 16),
+                                              ('eager', 8, 32),
+                                              ('static', 8, 32)])
+def test_bench_ranks_gloo(tmp_path, mode, world, batch):
     """The bench's distributed path (rank sharding, all-reduce, max-time
-    reduction, rank-0 JSON) runs end to end with two gloo ranks."""
+    reduction, rank-0 JSON) runs end to end with gloo ranks.  With 8 ranks
+    each shard (160 graphs / 8 = 20 sources) is smaller than the batch, as
+    in the 8-GPU PascalVOC run (2560 / 8 = 320 < 512)."""
     import json
-    world = 2
     out_path = str(tmp_path / 'bench.json')
     ctx = mp.get_context('spawn')
     port = _free_port()
     procs = [ctx.Process(target=_bench_worker,
-                         args=(r, world, port, mode, out_path))
+                         args=(r, world, port, mode, out_path, batch))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -132,7 +137,7 @@ def test_bench_two_ranks_gloo(tmp_path, mode):
         assert p.exitcode == 0
     with open(out_path) as f:
         result = json.loads(f.read())
-    assert result['n_gpus'] == 2
-    assert result['config']['global_batch'] == 32
-    assert result['config']['parallelism'] == 'dp2'
+    assert result['n_gpus'] == world
+    assert result['config']['global_batch'] == batch * world
+    assert result['config']['parallelism'] == 'dp{}'.format(world)
     assert result['value'] > 0
