@@ -139,6 +139,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_tile_plan(
 at::Tensor gemm_abt(const at::Tensor& A, const at::Tensor& Bt,
                     const c10::optional<at::Tensor>& out, bool accumulate,
                     c10::optional<at::ScalarType> out_dtype);
+at::Tensor spline_weight_pack(const at::Tensor& weight,
+                              const c10::optional<at::Tensor>& root,
+                              at::ScalarType dtype);
+std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
+                                                        int64_t K,
+                                                        bool has_root);
 
 }  // namespace dgmc
 
@@ -224,6 +230,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "float beta1, float beta2, float eps, float weight_decay) -> ()");
   m.def("adam_step_inc(Tensor(a!)[] steps, Tensor? found_inf) -> ()");
   m.def(
+      "spline_weight_pack(Tensor weight, Tensor? root, ScalarType dtype) -> "
+      "Tensor");
+  m.def(
+      "spline_weight_unpack(Tensor g, int K, bool has_root) -> (Tensor, "
+      "Tensor)");
+  m.def(
       "slot_wgrad_list(Tensor[] xs, Tensor[] gs, Tensor esrc, Tensor edst, "
       "Tensor evals, Tensor soff, int nsplit) -> Tensor");
   m.def(
@@ -280,6 +292,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_wgrad_list", &dgmc::slot_wgrad_list);
   m.impl("adam_multi", &dgmc::adam_multi);
   m.impl("adam_step_inc", &dgmc::adam_step_inc);
+  m.impl("spline_weight_pack", &dgmc::spline_weight_pack);
+  m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

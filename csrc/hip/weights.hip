@@ -1,0 +1,146 @@
+// SplineConv weight layouts (per training step, once per forward scope).
+//
+// The reference keeps PyG's parameter layout (``weight [K, in, out]``,
+// ``root [in, out]``; /root/reference/dgmc/models/spline.py:21 via
+// SplineConv) and torch_spline_conv indexes it per edge.  Here a SplineConv
+// is ONE GEMM ``x @ [W_0 | .. | W_{K-1} | root]`` followed by the sparse
+// slot aggregation, so every forward needs the stacked low-precision operand
+//
+//   w_lp[i, s * O + o] = s < K ? weight[s, i, o] : root[i, o]     (bf16)
+//
+// and every backward maps the stacked fp32 gradient back:
+//
+//   gweight[s, i, o] = g[i, s * O + o],   groot[i, o] = g[i, K * O + o].
+//
+// Eager PyTorch spends a permute copy + a concatenation + a cast in the
+// forward (3 kernels, 2 fp32 intermediates: ~32 us for psi_1's first layer
+// [1024, 26 x 256]) and slice / permute-backward copies in the backward.
+// Both directions are single bandwidth-bound passes here: 16-byte fp32
+// loads, contiguous along ``o`` on both sides.
+#include "common.h"
+
+namespace dgmc {
+
+namespace {
+
+// One thread per 4 consecutive ``o`` of one (i, s) row segment; thread ids
+// run o-fastest, then s, then i, so the stacked side is written (or read)
+// contiguously and the parameter side in O-long contiguous runs.
+template <typename TOUT>
+__global__ __launch_bounds__(256) void spline_weight_pack_kernel(
+    const float* __restrict__ weight, const float* __restrict__ root,
+    TOUT* __restrict__ out, int in, int K, int S, int O) {
+  const int O4 = O / 4;
+  const int64_t total = (int64_t)in * S * O4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(t % O4) * 4;
+    const int64_t rs = t / O4;
+    const int s = (int)(rs % S);
+    const int i = (int)(rs / S);
+    const float* src = s < K ? weight + ((int64_t)s * in + i) * O + o
+                             : root + (int64_t)i * O + o;
+    const float4 v = *reinterpret_cast<const float4*>(src);
+    TOUT* dst = out + (int64_t)i * S * O + (int64_t)s * O + o;
+    if constexpr (sizeof(TOUT) == 2) {
+      typedef TOUT v4 __attribute__((ext_vector_type(4)));
+      const v4 w = {(TOUT)v.x, (TOUT)v.y, (TOUT)v.z, (TOUT)v.w};
+      *reinterpret_cast<v4*>(dst) = w;
+    } else {
+      *reinterpret_cast<float4*>(dst) = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void spline_weight_unpack_kernel(
+    const float* __restrict__ g, float* __restrict__ gweight,
+    float* __restrict__ groot, int in, int K, int S, int O) {
+  const int O4 = O / 4;
+  const int64_t total = (int64_t)in * S * O4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int o = (int)(t % O4) * 4;
+    const int64_t rs = t / O4;
+    const int s = (int)(rs % S);
+    const int i = (int)(rs / S);
+    const float4 v = *reinterpret_cast<const float4*>(
+        g + (int64_t)i * S * O + (int64_t)s * O + o);
+    float* dst = s < K ? gweight + ((int64_t)s * in + i) * O + o
+                       : groot + (int64_t)i * O + o;
+    *reinterpret_cast<float4*>(dst) = v;
+  }
+}
+
+int grid_for(int64_t work) {
+  return (int)std::min<int64_t>((work + 255) / 256, 4096);
+}
+
+void check_params(const at::Tensor& weight,
+                  const c10::optional<at::Tensor>& root) {
+  TORCH_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat &&
+                  weight.dim() == 3 && weight.is_contiguous() &&
+                  aligned16(weight.data_ptr()),
+              "spline_weight: fp32 contiguous weight [K, in, out] expected");
+  TORCH_CHECK(weight.size(2) % 4 == 0, "spline_weight: out % 4 != 0");
+  if (root.has_value() && root->defined())
+    TORCH_CHECK(root->is_cuda() && root->scalar_type() == at::kFloat &&
+                    root->is_contiguous() && aligned16(root->data_ptr()) &&
+                    root->dim() == 2 && root->size(0) == weight.size(1) &&
+                    root->size(1) == weight.size(2),
+                "spline_weight: fp32 contiguous root [in, out] expected");
+}
+
+}  // namespace
+
+at::Tensor spline_weight_pack(const at::Tensor& weight,
+                              const c10::optional<at::Tensor>& root,
+                              at::ScalarType dtype) {
+  check_params(weight, root);
+  const bool has_root = root.has_value() && root->defined();
+  const int K = weight.size(0), in = weight.size(1), O = weight.size(2);
+  const int S = K + (has_root ? 1 : 0);
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat,
+              "spline_weight_pack: bf16 or fp32 output");
+  at::Tensor out = at::empty({in, (int64_t)S * O}, weight.options().dtype(dtype));
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
+  const int64_t work = (int64_t)in * S * (O / 4);
+  if (work == 0) return out;
+  const float* rp = has_root ? root->data_ptr<float>() : nullptr;
+  if (dtype == at::kBFloat16)
+    hipLaunchKernelGGL(spline_weight_pack_kernel<__bf16>, dim3(grid_for(work)),
+                       dim3(256), 0, stream(), weight.data_ptr<float>(), rp,
+                       reinterpret_cast<__bf16*>(out.data_ptr()), in, K, S, O);
+  else
+    hipLaunchKernelGGL(spline_weight_pack_kernel<float>, dim3(grid_for(work)),
+                       dim3(256), 0, stream(), weight.data_ptr<float>(), rp,
+                       out.data_ptr<float>(), in, K, S, O);
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
+                                                        int64_t K,
+                                                        bool has_root) {
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat && g.dim() == 2 &&
+                  g.is_contiguous() && aligned16(g.data_ptr()),
+              "spline_weight_unpack: fp32 contiguous [in, S * out] expected");
+  const int S = (int)K + (has_root ? 1 : 0);
+  TORCH_CHECK(K >= 1 && g.size(1) % S == 0, "spline_weight_unpack: shape");
+  const int in = g.size(0), O = g.size(1) / S;
+  TORCH_CHECK(O % 4 == 0, "spline_weight_unpack: out % 4 != 0");
+  at::Tensor gw = at::empty({K, in, O}, g.options());
+  at::Tensor gr = has_root ? at::empty({in, O}, g.options()) : at::Tensor();
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  const int64_t work = (int64_t)in * S * (O / 4);
+  if (work > 0) {
+    hipLaunchKernelGGL(spline_weight_unpack_kernel, dim3(grid_for(work)),
+                       dim3(256), 0, stream(), g.data_ptr<float>(),
+                       gw.data_ptr<float>(),
+                       has_root ? gr.data_ptr<float>() : nullptr, in, (int)K,
+                       S, O);
+    DGMC_CHECK_LAUNCH();
+  }
+  return {gw, gr};
+}
+
+}  // namespace dgmc

@@ -20,6 +20,7 @@ root term, bias and (optionally) ReLU.  Its backward is the same kernel on
 import torch
 from torch.nn import Parameter
 
+from ..ops import _backend
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.gemm import compute_dtype
 from ..ops.sparse import gemm_spmm, spmm
@@ -32,6 +33,29 @@ def repeat(src, length):
         assert len(src) == length
         return list(src)
     return [src] * length
+
+
+class _StackedSplineWeight(torch.autograd.Function):
+    """``(w, w_lp)`` for :func:`~..ops.sparse.gemm_spmm` straight from the
+    parameters (csrc/hip/weights.hip): ``w_lp [in, S * out]`` is the stacked
+    low-precision GEMM operand written by ONE kernel (no fp32 permute / cat
+    intermediates), ``w`` an fp32 placeholder of the same shape that only
+    carries the stacked fp32 gradient back - mapped to ``weight`` / ``root``
+    by one unpack kernel."""
+
+    @staticmethod
+    def forward(ctx, weight, root, dtype):
+        w_lp = _backend.ops().spline_weight_pack(weight, root, dtype)
+        ctx.K, ctx.has_root = weight.size(0), root is not None
+        token = weight.new_empty(1).expand(w_lp.shape)
+        ctx.mark_non_differentiable(w_lp)
+        return token, w_lp
+
+    @staticmethod
+    def backward(ctx, g, _):
+        gw, gr = _backend.ops().spline_weight_unpack(
+            g.float().contiguous(), ctx.K, ctx.has_root)
+        return gw, (gr if ctx.has_root else None), None
 
 
 class SplineConv(torch.nn.Module):
@@ -100,6 +124,19 @@ class SplineConv(torch.nn.Module):
             return w
         return cached(('spline_w', id(self)), build)
 
+    def stacked_operands(self, dtype, like):
+        """``(w, w_lp)``: the fp32 stacked weight (gradient carrier) and its
+        ``dtype`` copy, memoised per forward scope."""
+        if (_backend.use_hip(like) and self.weight.is_cuda and
+                dtype in (torch.bfloat16, torch.float32) and
+                self.out_channels % 4 == 0):
+            return cached(('spline_w_pack', id(self), dtype),
+                          lambda: _StackedSplineWeight.apply(
+                              self.weight, self.root, dtype))
+        w = self.stacked_weight()
+        return w, cached(('spline_w_lp', id(self), dtype),
+                         lambda: w.detach().to(dtype))
+
     def forward(self, x, edge_index, pseudo, act=None, passthrough=False):
         x = x.unsqueeze(-1) if x.dim() == 1 else x
         pseudo = pseudo.unsqueeze(-1) if pseudo.dim() == 1 else pseudo
@@ -109,9 +146,7 @@ class SplineConv(torch.nn.Module):
                            device_params=(self.kernel_size,
                                           self.is_open_spline))
         dtype = compute_dtype(x)
-        w = self.stacked_weight()
-        w_lp = cached(('spline_w_lp', id(self), dtype),
-                      lambda: w.detach().to(dtype))
+        w, w_lp = self.stacked_operands(dtype, x)
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),
                          loop_key=(id(self), N, plan.num_cols),

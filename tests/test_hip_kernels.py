@@ -760,3 +760,59 @@ def test_hip_adam_state_round_trip_through_torch_adam(tmp_path):
     assert len(ids) == len(ps)            # never shared
     for a, b in zip(ref_ps, ps):
         torch.testing.assert_close(b, a, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize('K,cin,cout,root', [(25, 1024, 256, True),
+                                             (25, 128, 128, True),
+                                             (4, 3, 8, False)])
+def test_spline_weight_pack_unpack(K, cin, cout, root):
+    """Stacked SplineConv operand / gradient layouts vs torch permute+cat."""
+    ops = _backend.ops()
+    w = torch.randn(K, cin, cout, device=DEV)
+    r = torch.randn(cin, cout, device=DEV) if root else None
+    ref = w.permute(1, 0, 2).reshape(cin, K * cout)
+    if root:
+        ref = torch.cat([ref, r], dim=1)
+    assert torch.equal(ops.spline_weight_pack(w, r, torch.float32), ref)
+    assert torch.equal(ops.spline_weight_pack(w, r, torch.bfloat16),
+                       ref.bfloat16())
+    g = torch.randn_like(ref)
+    gw, gr = ops.spline_weight_unpack(g, K, root)
+    S = K + int(root)
+    g3 = g.view(cin, S, cout)
+    assert torch.equal(gw, g3[:, :K].permute(1, 0, 2))
+    if root:
+        assert torch.equal(gr, g3[:, K])
+
+
+def test_spline_conv_packed_weight_gradients_match_stacked(monkeypatch):
+    """SplineConv with the one-kernel packed operand == the permute + cat
+    autograd path (forward and parameter gradients)."""
+    from deep_graph_matching_consensus_amd.nn import conv as conv_mod
+    torch.manual_seed(5)
+    conv = conv_mod.SplineConv(64, 32, dim=2, kernel_size=5).to(DEV)
+    N, E = 300, 1500
+    ei = torch.randint(N, (2, E), device=DEV)
+    attr = torch.rand(E, 2, device=DEV)
+    x = torch.randn(N, 64, device=DEV)
+
+    def run():
+        conv.zero_grad()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = conv(x, ei, attr, act='relu')
+        out.float().square().sum().backward()
+        return out.detach().float(), [p.grad.clone() for p in
+                                      (conv.weight, conv.root, conv.bias)]
+
+    o1, g1 = run()
+    orig = conv_mod.SplineConv.stacked_operands
+
+    def stacked(self, dtype, like):
+        w = self.stacked_weight()
+        return w, w.detach().to(dtype)
+    monkeypatch.setattr(conv_mod.SplineConv, 'stacked_operands', stacked)
+    o0, g0 = run()
+    monkeypatch.setattr(conv_mod.SplineConv, 'stacked_operands', orig)
+    torch.testing.assert_close(o1, o0, atol=0, rtol=0)
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-6)
