@@ -145,6 +145,15 @@ at::Tensor spline_weight_pack(const at::Tensor& weight,
 std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         int64_t K,
                                                         bool has_root);
+at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
+                              const c10::optional<at::Tensor>& relu_out,
+                              const at::Tensor& tiles, const at::Tensor& soff,
+                              const at::Tensor& ecode, const at::Tensor& eval,
+                              int64_t S, const at::Tensor& Wimg,
+                              at::ScalarType out_dtype,
+                              const c10::optional<at::Tensor>& addend,
+                              at::Tensor g_out,
+                              const c10::optional<at::Tensor>& bias_part);
 
 }  // namespace dgmc
 
@@ -236,6 +245,11 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "spline_weight_unpack(Tensor g, int K, bool has_root) -> (Tensor, "
       "Tensor)");
   m.def(
+      "slot_conv_relu_bwd(Tensor G, Tensor? relu_out, Tensor tiles, Tensor "
+      "soff, Tensor ecode, Tensor eval, int S, Tensor Wimg, ScalarType "
+      "out_dtype, Tensor? addend, Tensor(a!) g_out, Tensor(b!)? bias_part) -> "
+      "Tensor");
+  m.def(
       "slot_wgrad_list(Tensor[] xs, Tensor[] gs, Tensor esrc, Tensor edst, "
       "Tensor evals, Tensor soff, int nsplit) -> Tensor");
   m.def(
@@ -294,6 +308,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("adam_step_inc", &dgmc::adam_step_inc);
   m.impl("spline_weight_pack", &dgmc::spline_weight_pack);
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
+  m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

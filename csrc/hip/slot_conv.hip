@@ -482,7 +482,8 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
     const __hip_bfloat16* __restrict__ evalg, int S,
     const __hip_bfloat16* __restrict__ Wimg, const float* __restrict__ bias,
     int relu, TOUT* __restrict__ out, const __hip_bfloat16* __restrict__ addg,
-    int ldadd) {
+    int ldadd, int ldx, const __hip_bfloat16* __restrict__ maskg,
+    __hip_bfloat16* __restrict__ goutg, float* __restrict__ bpart) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS char* smem = (DGMC_LDS char*)smem_raw;
   DGMC_LDS __bf16* wbuf = (DGMC_LDS __bf16*)smem;        // [3][128][128]
@@ -508,7 +509,12 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
   const int r0 = tiles[4 * t], rows = tiles[4 * t + 1] - r0;
   const int e0 = tiles[4 * t + 2];
   const int E = tiles[4 * t + 3] & 0xffff;
-  if (rows <= 0) return;
+  if (rows <= 0) {                    // empty tile (no graph starts in it)
+    if constexpr (TRANS) {
+      if (bpart && tid < kScC) bpart[(size_t)t * kScC + tid] = 0.f;
+    }
+    return;
+  }
 
   const int sof_v = lane <= S ? soff[t * (S + 1) + lane] : 0;
   auto sof = [&](int k) __attribute__((always_inline)) {
@@ -558,14 +564,32 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
   load_w(0, tid, All{});
   if (S > 1) load_w(1, tid, All{});
   if (tid < kScC) bsh[tid] = bias ? bias[tid] : 0.f;
+  // Transposed pass with the fused ReLU/bias backward (maskg != null): the
+  // tile's rows of g' = G * (out > 0) are formed here, written to goutg (the
+  // slot weight gradient's operand) and summed per channel into bpart[t]
+  // (the bias gradient's tile partial) - no separate relu_bias_bwd pass.
 #pragma unroll
   for (int i = 0; i < kScT * kScC / 8 / kScCT; ++i) {
     const int c = tid + i * kScCT;
     const int row = c & 63, cc = c >> 6;
     sc_bf16x8 v = {};
-    if (row < rows)
-      v = *reinterpret_cast<const sc_bf16x8*>(X + (size_t)(r0 + row) * kScC +
+    if (row < rows) {
+      v = *reinterpret_cast<const sc_bf16x8*>(X + (size_t)(r0 + row) * ldx +
                                               cc * 8);
+      if constexpr (TRANS) {
+        const size_t o = (size_t)(r0 + row) * kScC + cc * 8;
+        if (maskg) {
+          const sc_bf16x8 m = *reinterpret_cast<const sc_bf16x8*>(
+              reinterpret_cast<const __bf16*>(maskg) + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            v[e] = (float)m[e] > 0.f ? v[e] : (__bf16)0.f;
+        }
+        if (goutg)
+          *reinterpret_cast<sc_bf16x8*>(reinterpret_cast<__bf16*>(goutg) + o) =
+              v;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) xt[(cc * 8 + e) * kScAP + row] = v[e];
   }
@@ -578,6 +602,25 @@ __global__ __launch_bounds__(kScCT, 1) void slot_conv_ws_kernel(
       for (int c = 0; c < 2; ++c)
         xa[m][c] = *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(
             xt + (16 * m + ln) * kScAP + 32 * c + 8 * lq);
+  }
+  if constexpr (TRANS) {
+    if (bpart && sw) {
+      // Helper waves 4-5: one channel per thread, rows in a fixed order
+      // (deterministic).  xt is [channel][row]: a channel's 64 rows are
+      // contiguous, read as eight 16-byte vectors (rows past `rows` were
+      // staged as zeros).
+      DGMC_LDS const __bf16* xr = xt + sid * kScAP;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < kScT; r += 8) {
+        const sc_bf16x8 v =
+            *reinterpret_cast<DGMC_LDS const sc_bf16x8*>(xr + r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
+      }
+      bpart[(size_t)t * kScC + sid] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) +
+                                      ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    }
   }
   __syncthreads();                                // xt (= A tiles) free
   {
@@ -726,13 +769,21 @@ static bool sc_ws() {
   return v;
 }
 
+struct ScBwdFuse {          // fused ReLU/bias backward (ws kernel only)
+  int ldx = kScC;
+  const __hip_bfloat16* mask = nullptr;
+  __hip_bfloat16* gout = nullptr;
+  float* bpart = nullptr;
+};
+
 template <bool TRANS, bool WRITE_Z, typename TOUT>
 static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                              const at::Tensor& soff, const at::Tensor& ecode,
                              const at::Tensor& eval, int S,
                              const at::Tensor& Wimg, const float* bias,
                              bool relu, at::Tensor& out, __hip_bfloat16* Z,
-                             const __hip_bfloat16* add, int ldadd) {
+                             const __hip_bfloat16* add, int ldadd,
+                             const ScBwdFuse& fz = ScBwdFuse()) {
   const int T = tiles.size(0);
   if constexpr (!WRITE_Z) {
     if (sc_ws()) {
@@ -750,10 +801,14 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
           tiles.data_ptr<int>(), soff.data_ptr<int>(), ecode.data_ptr<int>(),
           reinterpret_cast<const __hip_bfloat16*>(eval.data_ptr()), S,
           reinterpret_cast<const __hip_bfloat16*>(Wimg.data_ptr()), bias,
-          relu ? 1 : 0, reinterpret_cast<TOUT*>(out.data_ptr()), add, ldadd);
+          relu ? 1 : 0, reinterpret_cast<TOUT*>(out.data_ptr()), add, ldadd,
+          fz.ldx, fz.mask, fz.gout, fz.bpart);
       return;
     }
   }
+  TORCH_CHECK(fz.ldx == kScC && !fz.mask && !fz.gout && !fz.bpart,
+              "slot_conv: fused ReLU/bias backward needs the wave-specialised "
+              "kernel");
   auto kern = slot_conv_kernel<TRANS, WRITE_Z, TOUT>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -903,6 +958,127 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
   else
     DGMC_SC_LAUNCH(true, false);
 #undef DGMC_SC_LAUNCH
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+// Transposed slot conv with the ReLU/bias backward fused into its prologue:
+//   g' = G * (relu_out > 0)   (G: bf16 [N, 128], unit column stride, row
+//                               stride ldg % 8 == 0 - e.g. a column slice of
+//                               the concatenation's gradient)
+//   g_out <- g'  (bf16 [N, 128] contiguous, the weight gradient's operand)
+//   bias_part[t] <- sum of g' over tile t's rows (fp32 [T, 128], optional)
+//   returns dX = sum_k (A_k^T g') W_k^T (+ addend)
+// Without the wave-specialised kernel (DGMC_SC_WS=0) the prologue runs as
+// ATen ops before the plain transposed pass.
+at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
+                              const c10::optional<at::Tensor>& relu_out,
+                              const at::Tensor& tiles, const at::Tensor& soff,
+                              const at::Tensor& ecode, const at::Tensor& eval,
+                              int64_t S, const at::Tensor& Wimg,
+                              at::ScalarType out_dtype,
+                              const c10::optional<at::Tensor>& addend,
+                              at::Tensor g_out,
+                              const c10::optional<at::Tensor>& bias_part) {
+  TORCH_CHECK(G.is_cuda() && G.dim() == 2 && G.scalar_type() == at::kBFloat16 &&
+                  G.size(1) == kScC && G.stride(1) == 1 &&
+                  G.stride(0) >= kScC && G.stride(0) % 8 == 0 &&
+                  aligned16(G.data_ptr()),
+              "slot_conv_relu_bwd: G bf16 [N, 128], unit column stride, "
+              "16-B aligned rows");
+  const int64_t N = G.size(0);
+  TORCH_CHECK(g_out.scalar_type() == at::kBFloat16 && g_out.is_contiguous() &&
+                  g_out.numel() == N * kScC && aligned16(g_out.data_ptr()),
+              "slot_conv_relu_bwd: g_out contiguous bf16 [N, 128]");
+  const bool has_mask = relu_out.has_value() && relu_out->defined();
+  if (has_mask)
+    TORCH_CHECK(relu_out->scalar_type() == at::kBFloat16 &&
+                    relu_out->is_contiguous() &&
+                    relu_out->numel() == N * kScC &&
+                    aligned16(relu_out->data_ptr()),
+                "slot_conv_relu_bwd: relu_out contiguous bf16 [N, 128]");
+  const bool has_bp = bias_part.has_value() && bias_part->defined();
+  if (has_bp)
+    TORCH_CHECK(bias_part->scalar_type() == at::kFloat &&
+                    bias_part->is_contiguous() &&
+                    bias_part->numel() == tiles.size(0) * kScC,
+                "slot_conv_relu_bwd: bias_part fp32 [T, 128]");
+  if (!sc_ws()) {
+    at::Tensor g = has_mask ? at::where(relu_out->gt(0), G,
+                                        at::zeros({}, G.options()))
+                            : G;
+    g_out.view({N, kScC}).copy_(g);
+    if (has_bp) {
+      bias_part->zero_();
+      bias_part->view({-1, kScC})[0].copy_(g.to(at::kFloat).sum(0));
+    }
+    return slot_conv(g_out.view({N, kScC}), tiles, soff, ecode, eval, S, Wimg,
+                     true, c10::nullopt, false, out_dtype, c10::nullopt,
+                     addend);
+  }
+  // Same checks as slot_conv for the shared operands (X validated above).
+  TORCH_CHECK(tiles.scalar_type() == at::kInt && tiles.dim() == 2 &&
+                  tiles.size(1) == 4 && tiles.is_contiguous(),
+              "slot_conv_relu_bwd: tiles int32 [T, 4] (slot_tile_plan)");
+  TORCH_CHECK(S >= 1 && S <= kScMaxS - 1 && N * S < INT32_MAX,
+              "slot_conv_relu_bwd: slot count / size range");
+  TORCH_CHECK(soff.scalar_type() == at::kInt && soff.is_contiguous() &&
+                  soff.numel() == tiles.size(0) * (S + 1),
+              "slot_conv_relu_bwd: soff int32 [T, S + 1]");
+  TORCH_CHECK(ecode.scalar_type() == at::kInt &&
+                  eval.scalar_type() == at::kBFloat16 &&
+                  ecode.numel() == eval.numel() && ecode.is_contiguous() &&
+                  eval.is_contiguous(),
+              "slot_conv_relu_bwd: int32 ecode / bf16 eval");
+  TORCH_CHECK(Wimg.scalar_type() == at::kBFloat16 && Wimg.is_contiguous() &&
+                  Wimg.numel() == S * kScWImg && aligned16(Wimg.data_ptr()),
+              "slot_conv_relu_bwd: Wimg contiguous bf16 [S, 128, 128]");
+  TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kFloat,
+              "slot_conv_relu_bwd: bf16 or fp32 output");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(G.device());
+  at::Tensor out = at::empty({N, kScC}, G.options().dtype(out_dtype));
+  const __hip_bfloat16* ap = nullptr;
+  int lda = 0;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kBFloat16 && addend->dim() == 2 &&
+                    addend->size(0) == N && addend->size(1) == kScC &&
+                    addend->stride(1) == 1 && addend->stride(0) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(addend->data_ptr()) % 8) == 0,
+                "slot_conv_relu_bwd: addend bf16 [N, 128], unit column "
+                "stride, 8-B aligned rows");
+    ap = reinterpret_cast<const __hip_bfloat16*>(addend->data_ptr());
+    lda = (int)addend->stride(0);
+  }
+  if (N == 0) return out;
+  ScBwdFuse fz;
+  fz.ldx = (int)G.stride(0);
+  fz.mask = has_mask
+                ? reinterpret_cast<const __hip_bfloat16*>(relu_out->data_ptr())
+                : nullptr;
+  fz.gout = reinterpret_cast<__hip_bfloat16*>(g_out.data_ptr());
+  {
+    // Ablation knob (tools/sc_fz_ablation.sh; results timing-only, NOT
+    // numerically valid): bit 0 drops the g' stores, bit 1 the ReLU mask,
+    // bit 2 the bias partials.  Measured per transposed call: 25.9 us fused
+    // vs 23.6 + 5.4 us (slot conv + relu_bias_bwd) unfused; the g' stores
+    // cost 1.2 us (the prologue's __syncthreads waits for them).
+    static int abl = [] {
+      const char* e = getenv("DGMC_SC_FZ_ABL");
+      return e ? atoi(e) : 0;
+    }();
+    if (abl & 1) fz.gout = nullptr;
+    if (abl & 2) fz.mask = nullptr;
+    if (abl & 4) fz.bpart = nullptr;
+  }
+  fz.bpart = has_bp ? bias_part->data_ptr<float>() : nullptr;
+  if (out_dtype == at::kFloat)
+    launch_slot_conv<true, false, float>(G, tiles, soff, ecode, eval, (int)S,
+                                         Wimg, nullptr, false, out, nullptr,
+                                         ap, lda, fz);
+  else
+    launch_slot_conv<true, false, __hip_bfloat16>(G, tiles, soff, ecode, eval,
+                                                  (int)S, Wimg, nullptr, false,
+                                                  out, nullptr, ap, lda, fz);
   DGMC_CHECK_LAUNCH();
   return out;
 }

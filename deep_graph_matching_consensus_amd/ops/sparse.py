@@ -229,6 +229,44 @@ class _GemmSpMM(torch.autograd.Function):
         return out
 
     @staticmethod
+    def _slot_loop_backward(ctx, grad, gpass, xc, out, op, K, S, need_b):
+        """Consensus-loop use on the fused slot kernels: g' (ReLU mask), the
+        bias gradient's tile partials and dx in ONE transposed slot conv
+        (``slot_conv_relu_bwd``); dW later from the kept (x, g') pairs of all
+        uses (``slot_weight_grad``)."""
+        from .gemm import loop_col_total
+        loop, idx, C = ctx.loop, ctx.idx, ctx.C
+        plan = slot_tile_plan(op, S)
+        if (grad.stride(-1) != 1 or grad.stride(0) < C or
+                grad.stride(0) % 8 or grad.data_ptr() % 16):
+            grad = grad.contiguous()
+        part = loop.slot('b', idx, (plan[0].size(0), C), torch.float32,
+                         grad.device) if need_b else None
+        g = torch.empty((grad.size(0), C), dtype=torch.bfloat16,
+                        device=grad.device)
+        add = gpass if _addend_ok(gpass, g) else None
+        gx = _backend.ops().slot_conv_relu_bwd(
+            grad, out if ctx.relu else None, *plan, S, ctx.img_b, g.dtype,
+            add, g, part)
+        if add is not None:
+            gpass = None
+        if gx.dtype != ctx.x_dtype:
+            gx = gx.to(ctx.x_dtype)
+        gx = _add_pass(gx, gpass) if ctx.needs_input_grad[0] else None
+        loop.keep('x', idx, xc)
+        loop.keep('g', idx, g)
+        gw = gb = None
+        if loop.arrive():
+            if ctx.needs_input_grad[1]:
+                dW = slot_weight_grad(loop.kept_list('x'),
+                                      loop.kept_list('g'), op, S, loop.uses)
+                gw = dW.permute(1, 0, 2).reshape(K, S * C).to(ctx.w_dtype)
+            if need_b:
+                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+            loop.release()
+        return (gx, gw, None, gb) + (None, ) * 5
+
+    @staticmethod
     def backward(ctx, grad, gpass=None):
         from .gemm import col_partial_rows, loop_col_total, matmul_tn_fp32
         nones = (None, ) * 5
@@ -237,6 +275,15 @@ class _GemmSpMM(torch.autograd.Function):
         dev = grad.device
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
         hip = _backend.use_hip(grad)
+        op = ctx.op
+        K = xc.size(1)
+        S = w_lp.size(1) // C
+        if (hip and ctx.slot and loop is not None and SLOT_WGRAD and
+                FUSED_RELU_BWD and ctx.img_b is not None and
+                grad.dtype == torch.bfloat16 and w_lp.dtype == torch.bfloat16
+                and (out is None or out.dtype == torch.bfloat16)):
+            return _GemmSpMM._slot_loop_backward(ctx, grad, gpass, xc, out,
+                                                 op, K, S, need_b)
         if not hip or grad.stride(-1) != 1 or grad.stride(0) < grad.size(1):
             grad = grad.contiguous()    # (the kernel reads column slices)
         # 1. g' = grad * relu'(out) and the bias gradient.
@@ -259,9 +306,6 @@ class _GemmSpMM(torch.autograd.Function):
                 if loop is not None:
                     loop.add_to('b', db)
             g = g.to(w_lp.dtype)
-        op = ctx.op
-        K = xc.size(1)
-        S = w_lp.size(1) // C
         if (ctx.slot and loop is not None and SLOT_WGRAD and
                 g.dtype == torch.bfloat16 and ctx.img_b is not None):
             # 2'. dx by the transposed slot conv; dW from the kept (x, g')
@@ -402,6 +446,9 @@ SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '1') == '1'
 # concatenation) the conv's passthrough alias, so its gradient is added in
 # the transposed slot conv epilogue instead of by an autograd add kernel.
 PASSTHROUGH = os.environ.get('DGMC_AMD_PASSTHROUGH', '1') == '1'
+# Consensus-loop backward: the ReLU mask, g' and the bias-gradient partials
+# are formed inside the transposed slot conv (no relu_bias_bwd pass).
+FUSED_RELU_BWD = os.environ.get('DGMC_AMD_FUSED_RELU_BWD', '1') == '1'
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}

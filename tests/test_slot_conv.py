@@ -419,3 +419,33 @@ def test_slot_conv_ws_matches_eight_wave_kernel(tmp_path):
     # MFMA operand order only.
     assert _close(out.cpu(), ref['out'], 1e-2)
     assert _close(gx.cpu(), ref['gx'], 1e-2)
+
+
+def test_slot_conv_relu_bwd_fused_prologue():
+    """Transposed slot conv with the fused ReLU/bias backward == ReLU mask +
+    column sums + plain transposed conv (strided G, addend)."""
+    ops = _backend.ops()
+    S = 26
+    op, flag = _graph_batch(_sizes(150, 19, seed=9), S, seed=9)
+    N = op.num_rows
+    op.tile_flag, op.tile_window = flag, 65 - 19
+    plan = slot_tile_plan(op, S)
+    w_lp = (torch.randn(C, S * C, device=DEV) / C ** 0.5).bfloat16()
+    img = slot_conv_image(w_lp, C, True)
+    wide = torch.randn(N, 3 * C, device=DEV).bfloat16()
+    G = wide[:, C:2 * C]                         # row stride 384
+    relu_out = torch.randn(N, C, device=DEV).relu().bfloat16()
+    add = torch.randn(N, 2 * C, device=DEV).bfloat16()[:, :C]
+    g_out = torch.empty(N, C, dtype=torch.bfloat16, device=DEV)
+    T = plan[0].size(0)
+    part = torch.full((T, C), float('nan'), device=DEV)
+    gx = ops.slot_conv_relu_bwd(G, relu_out, *plan, S, img, torch.float32,
+                                add, g_out, part)
+    g_ref = torch.where(relu_out > 0, G, torch.zeros_like(G))
+    assert torch.equal(g_out, g_ref)
+    torch.testing.assert_close(part.sum(0), g_ref.float().sum(0), atol=1e-3,
+                               rtol=1e-4)
+    base = ops.slot_conv(g_ref.contiguous(), *plan, S, img, True, None, False,
+                         torch.float32, None, add)
+    assert int(slot_conv_error(DEV)) == 0
+    torch.testing.assert_close(gx, base, atol=0, rtol=0)
