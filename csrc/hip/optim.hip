@@ -188,4 +188,96 @@ void adam_step_inc(at::TensorList steps,
   }
 }
 
+// ---------------------------------------------------------------------------
+// pack_grads: flat[off_i : off_i + n_i] = grads[i] (or 0 for an undefined
+// gradient) for every parameter, in ONE launch over a pointer table.
+//
+// The trainer lets autograd's AccumulateGrad *steal* each parameter's
+// freshly computed gradient (p.grad = None before backward) and then packs
+// them into the flat all-reduce / optimizer buffer here - instead of keeping
+// p.grad as views of a zeroed flat buffer, which costs one zero-fill of the
+// whole buffer plus one read-modify-write add kernel per parameter
+// (~20 adds of ~5 us each per PascalVOC step).
+namespace {
+struct PackTable {
+  const float* g[kAdamMax];
+  float* dst[kAdamMax];
+  int n[kAdamMax];
+  int first_block[kAdamMax + 1];
+  int count;
+};
+}  // namespace
+
+__global__ __launch_bounds__(kAdamThreads) void pack_grads_kernel(
+    const PackTable T) {
+  const int b = blockIdx.x;
+  int ti = 0;
+  while (ti + 1 < T.count && T.first_block[ti + 1] <= b) ++ti;
+  const int n = T.n[ti];
+  const int base = (b - T.first_block[ti]) * kAdamBlock;
+  const float* __restrict__ G = T.g[ti];
+  float* __restrict__ D = T.dst[ti];
+  if (base + kAdamBlock <= n) {
+    float4 v[kAdamVec];
+#pragma unroll
+    for (int u = 0; u < kAdamVec; ++u) {
+      const int i = base + 4 * (u * kAdamThreads + threadIdx.x);
+      v[u] = G ? *reinterpret_cast<const float4*>(G + i)
+               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kAdamVec; ++u) {
+      const int i = base + 4 * (u * kAdamThreads + threadIdx.x);
+      *reinterpret_cast<float4*>(D + i) = v[u];
+    }
+  } else {
+    for (int i = base + threadIdx.x; i < min(n, base + kAdamBlock);
+         i += kAdamThreads)
+      D[i] = G ? G[i] : 0.f;
+  }
+}
+
+// grads[i]: fp32 contiguous 16-B aligned gradient of numel n_i (or None);
+// views[i]: the destination fp32 contiguous 16-B aligned view (numel n_i).
+void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
+                at::TensorList views) {
+  const int64_t count = (int64_t)views.size();
+  TORCH_CHECK((int64_t)grads.size() == count,
+              "pack_grads: one gradient slot per destination view");
+  if (count == 0) return;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(views[0].device());
+  for (int64_t c0 = 0; c0 < count; c0 += kAdamMax) {
+    PackTable T{};
+    T.count = (int)std::min<int64_t>(kAdamMax, count - c0);
+    int blocks = 0;
+    for (int j = 0; j < T.count; ++j) {
+      const at::Tensor& d = views[c0 + j];
+      TORCH_CHECK(d.is_cuda() && d.scalar_type() == at::kFloat &&
+                      d.is_contiguous() && aligned16(d.data_ptr()) &&
+                      d.numel() < INT32_MAX,
+                  "pack_grads: fp32 contiguous 16-B aligned destination");
+      const c10::optional<at::Tensor> g = grads.get(c0 + j);
+      const float* gp = nullptr;
+      if (g.has_value() && g->defined()) {
+        TORCH_CHECK(g->is_cuda() && g->scalar_type() == at::kFloat &&
+                        g->is_contiguous() && aligned16(g->data_ptr()) &&
+                        g->numel() == d.numel(),
+                    "pack_grads: fp32 contiguous 16-B aligned gradient of "
+                    "the destination's size");
+        gp = g->data_ptr<float>();
+      }
+      T.g[j] = gp;
+      T.dst[j] = d.data_ptr<float>();
+      T.n[j] = (int)d.numel();
+      T.first_block[j] = blocks;
+      blocks += (T.n[j] + kAdamBlock - 1) / kAdamBlock;
+    }
+    T.first_block[T.count] = blocks;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(pack_grads_kernel, dim3(blocks), dim3(kAdamThreads), 0,
+                       stream(), T);
+    DGMC_CHECK_LAUNCH();
+  }
+}
+
 }  // namespace dgmc

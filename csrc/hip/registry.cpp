@@ -145,6 +145,8 @@ at::Tensor spline_weight_pack(const at::Tensor& weight,
 std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         int64_t K,
                                                         bool has_root);
+void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
+                at::TensorList views);
 at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                               const c10::optional<at::Tensor>& relu_out,
                               const at::Tensor& tiles, const at::Tensor& soff,
@@ -244,6 +246,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "spline_weight_unpack(Tensor g, int K, bool has_root) -> (Tensor, "
       "Tensor)");
+  m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
   m.def(
       "slot_conv_relu_bwd(Tensor G, Tensor? relu_out, Tensor tiles, Tensor "
       "soff, Tensor ecode, Tensor eval, int S, Tensor Wimg, ScalarType "
@@ -309,6 +312,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_weight_pack", &dgmc::spline_weight_pack);
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
+  m.impl("pack_grads", &dgmc::pack_grads);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

@@ -59,10 +59,13 @@ class _PackedNLL(torch.autograd.Function):
         ctx.save_for_backward(S, y0, y1, mask, aux)
         ctx.mean = mean
         ctx.mark_non_differentiable(aux)
+        ctx.set_materialize_grads(False)     # (no zero grad for aux)
         return loss, aux
 
     @staticmethod
     def backward(ctx, grad, grad_aux):
+        if grad is None:
+            return (None, ) * 6
         S, y0, y1, mask, aux = ctx.saved_tensors
         dS = _backend.ops().nll_bwd(grad.float().contiguous(), S, y0, y1,
                                     mask, aux, EPS, ctx.mean)

@@ -49,10 +49,14 @@ class _StackedSplineWeight(torch.autograd.Function):
         ctx.K, ctx.has_root = weight.size(0), root is not None
         token = weight.new_empty(1).expand(w_lp.shape)
         ctx.mark_non_differentiable(w_lp)
+        # w_lp never receives a gradient: do not materialise a zero one.
+        ctx.set_materialize_grads(False)
         return token, w_lp
 
     @staticmethod
     def backward(ctx, g, _):
+        if g is None:
+            return None, None, None
         gw, gr = _backend.ops().spline_weight_unpack(
             g.float().contiguous(), ctx.K, ctx.has_root)
         return gw, (gr if ctx.has_root else None), None

@@ -97,6 +97,46 @@ class GradBucketAllReducer(object):
         self.flat.zero_()
         self.attach_grads()
 
+    # ------------------------------------------------------------------
+    # Static / captured steps: let AccumulateGrad *steal* the gradients.
+    def release_grads(self):
+        """Drop every ``p.grad`` before backward: AccumulateGrad then stores
+        the freshly computed gradient tensor as ``p.grad`` (no copy) instead
+        of adding it into a zeroed view of the flat buffer - which costs a
+        zero-fill of the whole buffer plus one add kernel per parameter."""
+        for p in self.params:
+            p.grad = None
+
+    def pack_grads(self):
+        """After backward: copy the stolen gradients into the flat buffer in
+        ONE multi-tensor kernel (zeros for parameters without a gradient)
+        and re-bind every ``p.grad`` to its flat view."""
+        from ..ops import _backend
+        views = [self.flat[o:o + n].view_as(p)
+                 for p, (o, n) in ((p, self._slot[p]) for p in self.params)]
+        grads = [p.grad for p in self.params]
+        if _backend.use_hip(self.flat):
+            fast, slow = [], []
+            for g, v in zip(grads, views):
+                ok = g is None or (g.dtype == torch.float32 and g.is_cuda and
+                                   g.is_contiguous() and
+                                   g.data_ptr() % 16 == 0 and
+                                   g.numel() == v.numel())
+                fast.append(g if ok else None)
+                if not ok:
+                    slow.append((g, v))
+            _backend.ops().pack_grads(fast, views)
+            for g, v in slow:
+                v.copy_(g)
+        else:
+            for g, v in zip(grads, views):
+                if g is None:
+                    v.zero_()
+                else:
+                    v.copy_(g)
+        for p, v in zip(self.params, views):
+            p.grad = v
+
     def broadcast_state(self):
         with torch.no_grad():
             for t in list(self.module.parameters()) + \

@@ -162,9 +162,12 @@ class PairTrainer(object):
         self.optimizer.step()
 
     def _static_body(self, bucket=-1):
-        self.reducer.flat.zero_()
+        # Gradients are stolen by AccumulateGrad and packed into the flat
+        # buffer by one kernel (parallel/ddp.py::pack_grads).
+        self.reducer.release_grads()
         batch = self.batchers[bucket].materialize()
         self._forward_backward(batch, self._rows[bucket], batch.y_mask)
+        self.reducer.pack_grads()
         if self.world == 1:
             self._check_finite()
             self._optimizer_step()

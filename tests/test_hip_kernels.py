@@ -816,3 +816,23 @@ def test_spline_conv_packed_weight_gradients_match_stacked(monkeypatch):
     torch.testing.assert_close(o1, o0, atol=0, rtol=0)
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a, b, atol=1e-6, rtol=1e-6)
+
+
+def test_pack_grads_multi_tensor():
+    """pack_grads copies every gradient into its flat view (zeros for a
+    missing one) in one launch."""
+    ops = _backend.ops()
+    sizes = [37 * 5, 4, 4096 * 3 + 12, 128 * 128, 8]
+    pad = [(n + 3) // 4 * 4 for n in sizes]
+    flat = torch.full((sum(pad), ), 7.0, device=DEV)
+    views, grads, off = [], [], 0
+    for i, (n, pn) in enumerate(zip(sizes, pad)):
+        views.append(flat[off:off + n])
+        grads.append(None if i == 1 else torch.randn(n, device=DEV))
+        off += pn
+    ops.pack_grads(grads, views)
+    for g, v in zip(grads, views):
+        if g is None:
+            assert bool((v == 0).all())
+        else:
+            assert torch.equal(v, g)
