@@ -32,6 +32,11 @@ from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
 from .runtime.tuning import use_tuned_gemms
 
+# Static/captured steps: gradients stolen by AccumulateGrad and packed into
+# the flat buffer by one kernel (DGMC_AMD_STEAL_GRADS=0: zeroed flat views +
+# per-parameter accumulation).
+STEAL_GRADS = os.environ.get('DGMC_AMD_STEAL_GRADS', '1') == '1'
+
 
 class PairTrainer(object):
     r"""DGMC trainer over an HBM-resident :class:`GraphStore`.
@@ -164,10 +169,14 @@ class PairTrainer(object):
     def _static_body(self, bucket=-1):
         # Gradients are stolen by AccumulateGrad and packed into the flat
         # buffer by one kernel (parallel/ddp.py::pack_grads).
-        self.reducer.release_grads()
+        if STEAL_GRADS:
+            self.reducer.release_grads()
+        else:
+            self.reducer.zero_grad()
         batch = self.batchers[bucket].materialize()
         self._forward_backward(batch, self._rows[bucket], batch.y_mask)
-        self.reducer.pack_grads()
+        if STEAL_GRADS:
+            self.reducer.pack_grads()
         if self.world == 1:
             self._check_finite()
             self._optimizer_step()
