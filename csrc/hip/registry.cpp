@@ -147,6 +147,9 @@ std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         bool has_root);
 void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
                 at::TensorList views);
+std::tuple<at::Tensor, at::Tensor> spline_slot_images(
+    const at::Tensor& weight, const c10::optional<at::Tensor>& root,
+    const at::Tensor& perm);
 at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                               const c10::optional<at::Tensor>& relu_out,
                               const at::Tensor& tiles, const at::Tensor& soff,
@@ -248,6 +251,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor)");
   m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
   m.def(
+      "spline_slot_images(Tensor weight, Tensor? root, Tensor perm) -> "
+      "(Tensor, Tensor)");
+  m.def(
       "slot_conv_relu_bwd(Tensor G, Tensor? relu_out, Tensor tiles, Tensor "
       "soff, Tensor ecode, Tensor eval, int S, Tensor Wimg, ScalarType "
       "out_dtype, Tensor? addend, Tensor(a!) g_out, Tensor(b!)? bias_part) -> "
@@ -313,6 +319,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
   m.impl("pack_grads", &dgmc::pack_grads);
+  m.impl("spline_slot_images", &dgmc::spline_slot_images);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);

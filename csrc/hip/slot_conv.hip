@@ -858,8 +858,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_tile_plan(
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(flag.device());
   const int64_t T = std::max<int64_t>((N + window - 1) / window, 1);
   auto i32 = flag.options().dtype(at::kInt);
-  at::Tensor tiles = at::zeros({T, 4}, i32);
-  at::Tensor soff = at::zeros({T, S + 1}, i32);
+  // Every tile's row and slot offsets are written by the plan kernel.
+  at::Tensor tiles = at::empty({T, 4}, i32);
+  at::Tensor soff = at::empty({T, S + 1}, i32);
   at::Tensor ecode = at::empty({col.numel()}, i32);
   at::Tensor eval = at::empty({col.numel()}, flag.options().dtype(
       at::kBFloat16));

@@ -143,4 +143,68 @@ std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
   return {gw, gr};
 }
 
+// ---------------------------------------------------------------------------
+// spline_slot_images: the two weight images of the fused slot conv
+// (csrc/hip/slot_conv.hip) straight from the parameters, for 128 -> 128
+// SplineConvs (psi_2):
+//   fwd  [S, out, in]:  img[s, o, p] = W_s[perm[p], o]
+//   trans[S, in, out]:  img[s, i, p] = W_s[i, perm[p]]
+// with W_s = weight[s] (s < K) or root, perm the kernel's K order
+// (ops/sparse.py::slot_k_order).  One launch instead of a bf16 pack plus
+// two permute-gather kernels (ops/sparse.py::slot_conv_image).
+namespace {
+__global__ __launch_bounds__(256) void spline_slot_images_kernel(
+    const float* __restrict__ weight, const float* __restrict__ root,
+    const int64_t* __restrict__ perm, __bf16* __restrict__ img_f,
+    __bf16* __restrict__ img_t, int K, int S) {
+  constexpr int C = 128;
+  const int64_t total = (int64_t)2 * S * C * (C / 8);
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int p8 = (int)(t % (C / 8)) * 8;
+    const int64_t rest = t / (C / 8);
+    const int r = (int)(rest % C);
+    const int64_t rest2 = rest / C;
+    const int s = (int)(rest2 % S);
+    const bool trans = rest2 >= S;
+    const float* W = s < K ? weight + (int64_t)s * C * C : root;
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = (int)perm[p8 + e];
+      v[e] = (__bf16)(trans ? W[r * C + q] : W[q * C + r]);
+    }
+    __bf16* dst = (trans ? img_t : img_f) + ((int64_t)s * C + r) * C + p8;
+    *reinterpret_cast<bf16x8*>(dst) = v;
+  }
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> spline_slot_images(
+    const at::Tensor& weight, const c10::optional<at::Tensor>& root,
+    const at::Tensor& perm) {
+  check_params(weight, root);
+  TORCH_CHECK(weight.size(1) == 128 && weight.size(2) == 128,
+              "spline_slot_images: 128 -> 128 SplineConv only");
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == at::kLong &&
+                  perm.numel() == 128 && perm.is_contiguous(),
+              "spline_slot_images: int64 perm [128]");
+  const bool has_root = root.has_value() && root->defined();
+  const int K = weight.size(0), S = K + (has_root ? 1 : 0);
+  auto opt = weight.options().dtype(at::kBFloat16);
+  at::Tensor img_f = at::empty({S, 128, 128}, opt);
+  at::Tensor img_t = at::empty({S, 128, 128}, opt);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
+  const int64_t work = (int64_t)2 * S * 128 * 16;
+  hipLaunchKernelGGL(spline_slot_images_kernel, dim3(grid_for(work)),
+                     dim3(256), 0, stream(), weight.data_ptr<float>(),
+                     has_root ? root->data_ptr<float>() : nullptr,
+                     perm.data_ptr<int64_t>(),
+                     reinterpret_cast<__bf16*>(img_f.data_ptr()),
+                     reinterpret_cast<__bf16*>(img_t.data_ptr()), K, S);
+  DGMC_CHECK_LAUNCH();
+  return {img_f, img_t};
+}
+
 }  // namespace dgmc

@@ -23,7 +23,7 @@ from torch.nn import Parameter
 from ..ops import _backend
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.gemm import compute_dtype
-from ..ops.sparse import gemm_spmm, spmm
+from ..ops.sparse import SLOT_CONV, gemm_spmm, prime_slot_images, spmm
 from ..runtime.cache import cached
 from .inits import reset, uniform
 
@@ -128,15 +128,23 @@ class SplineConv(torch.nn.Module):
             return w
         return cached(('spline_w', id(self)), build)
 
-    def stacked_operands(self, dtype, like):
+    def stacked_operands(self, dtype, like, plan=None):
         """``(w, w_lp)``: the fp32 stacked weight (gradient carrier) and its
         ``dtype`` copy, memoised per forward scope."""
         if (_backend.use_hip(like) and self.weight.is_cuda and
                 dtype in (torch.bfloat16, torch.float32) and
                 self.out_channels % 4 == 0):
-            return cached(('spline_w_pack', id(self), dtype),
-                          lambda: _StackedSplineWeight.apply(
-                              self.weight, self.root, dtype))
+            def build():
+                w, w_lp = _StackedSplineWeight.apply(self.weight, self.root,
+                                                     dtype)
+                if (dtype == torch.bfloat16 and self.in_channels == 128 and
+                        self.out_channels == 128 and SLOT_CONV and
+                        getattr(plan, 'tile_flag', None) is not None):
+                    # psi_2-shaped: the fused slot conv's two weight images
+                    # from the parameters in one kernel (ops/sparse.py).
+                    prime_slot_images(w_lp, self.weight, self.root)
+                return w, w_lp
+            return cached(('spline_w_pack', id(self), dtype), build)
         w = self.stacked_weight()
         return w, cached(('spline_w_lp', id(self), dtype),
                          lambda: w.detach().to(dtype))
@@ -150,7 +158,7 @@ class SplineConv(torch.nn.Module):
                            device_params=(self.kernel_size,
                                           self.is_open_spline))
         dtype = compute_dtype(x)
-        w, w_lp = self.stacked_operands(dtype, x)
+        w, w_lp = self.stacked_operands(dtype, x, plan)
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),
                          loop_key=(id(self), N, plan.num_cols),

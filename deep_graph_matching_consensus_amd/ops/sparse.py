@@ -565,6 +565,27 @@ def slot_k_order(device):
     return p
 
 
+def _slot_img_key(w_lp, trans):
+    # Keyed by storage, not object: autograd hands every use a fresh
+    # ``detach()`` view of the same cached low-precision weight (the entry
+    # keeps it alive, so the address cannot be recycled within the scope).
+    return ('slot_img', w_lp.data_ptr(), w_lp._version, tuple(w_lp.shape),
+            bool(trans))
+
+
+def prime_slot_images(w_lp, weight, root):
+    """Compute both slot-conv weight images of a 128 -> 128 SplineConv from
+    its parameters in ONE kernel (``spline_slot_images``) and store them in
+    the forward scope under ``w_lp``'s keys, so :func:`slot_conv_image` finds
+    them instead of permuting ``w_lp`` twice."""
+    from ..runtime.cache import prime
+    img_f, img_t = _backend.ops().spline_slot_images(
+        weight.detach(), root.detach() if root is not None else None,
+        slot_k_order(weight.device))
+    prime(_slot_img_key(w_lp, False), (w_lp, img_f))
+    prime(_slot_img_key(w_lp, True), (w_lp, img_t))
+
+
 def slot_conv_image(w_lp, C, trans):
     """``[S, C, C]`` weight image of the slot conv, memoised per forward
     scope: forward rows = output channels, backward (``trans``) rows = input
@@ -575,12 +596,7 @@ def slot_conv_image(w_lp, C, trans):
         w3 = w_lp.view(w_lp.size(0), -1, C)          # [in, S, out]
         img = w3.permute(1, 0, 2) if trans else w3.permute(1, 2, 0)
         return (w_lp, img[:, :, slot_k_order(w_lp.device)].contiguous())
-    # Keyed by storage, not object: autograd hands every use a fresh
-    # ``detach()`` view of the same cached low-precision weight (the entry
-    # keeps it alive, so the address cannot be recycled within the scope).
-    key = ('slot_img', w_lp.data_ptr(), w_lp._version, tuple(w_lp.shape),
-           bool(trans))
-    return cached(key, build)[1]
+    return cached(_slot_img_key(w_lp, trans), build)[1]
 
 
 def _slot_major_t(w_lp):

@@ -39,3 +39,12 @@ def cached(key, fn):
         value = fn()
         store[key] = value
     return value
+
+
+def prime(key, value):
+    """Store ``value`` under ``key`` in the active scope (if any), for a
+    producer that computes several cached tensors in one kernel."""
+    import torch
+    store = getattr(_TLS, 'store', None)
+    if store is not None:
+        store[key + (torch.is_grad_enabled(), )] = value

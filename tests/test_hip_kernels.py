@@ -807,7 +807,7 @@ def test_spline_conv_packed_weight_gradients_match_stacked(monkeypatch):
     o1, g1 = run()
     orig = conv_mod.SplineConv.stacked_operands
 
-    def stacked(self, dtype, like):
+    def stacked(self, dtype, like, plan=None):
         w = self.stacked_weight()
         return w, w.detach().to(dtype)
     monkeypatch.setattr(conv_mod.SplineConv, 'stacked_operands', stacked)
@@ -836,3 +836,17 @@ def test_pack_grads_multi_tensor():
             assert bool((v == 0).all())
         else:
             assert torch.equal(v, g)
+
+
+def test_spline_slot_images_match_permuted_pack():
+    """Both slot-conv weight images from the parameters in one kernel ==
+    slot_conv_image of the stacked bf16 operand."""
+    from deep_graph_matching_consensus_amd.ops.sparse import (
+        slot_conv_image, slot_k_order)
+    ops = _backend.ops()
+    w = torch.randn(25, 128, 128, device=DEV)
+    r = torch.randn(128, 128, device=DEV)
+    w_lp = ops.spline_weight_pack(w, r, torch.bfloat16)
+    img_f, img_t = ops.spline_slot_images(w, r, slot_k_order(w.device))
+    assert torch.equal(img_f, slot_conv_image(w_lp, 128, False))
+    assert torch.equal(img_t, slot_conv_image(w_lp, 128, True))
