@@ -147,6 +147,12 @@ std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         bool has_root);
 void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
                 at::TensorList views);
+at::Tensor pair_scores(const at::Tensor& h, int64_t t_off,
+                       const at::Tensor& ptr_s, const at::Tensor& ptr_t,
+                       int64_t Ns, int64_t Nt);
+at::Tensor pair_scores_bwd(const at::Tensor& dS, const at::Tensor& h,
+                           int64_t t_off, const at::Tensor& ptr_s,
+                           const at::Tensor& ptr_t);
 std::tuple<at::Tensor, at::Tensor> spline_slot_images(
     const at::Tensor& weight, const c10::optional<at::Tensor>& root,
     const at::Tensor& perm);
@@ -251,6 +257,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor)");
   m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
   m.def(
+      "pair_scores(Tensor h, int t_off, Tensor ptr_s, Tensor ptr_t, int Ns, "
+      "int Nt) -> Tensor");
+  m.def(
+      "pair_scores_bwd(Tensor dS, Tensor h, int t_off, Tensor ptr_s, Tensor "
+      "ptr_t) -> Tensor");
+  m.def(
       "spline_slot_images(Tensor weight, Tensor? root, Tensor perm) -> "
       "(Tensor, Tensor)");
   m.def(
@@ -319,6 +331,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
   m.impl("pack_grads", &dgmc::pack_grads);
+  m.impl("pair_scores", &dgmc::pair_scores);
+  m.impl("pair_scores_bwd", &dgmc::pair_scores_bwd);
   m.impl("spline_slot_images", &dgmc::spline_slot_images);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);

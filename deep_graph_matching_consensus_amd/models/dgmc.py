@@ -138,6 +138,8 @@ def _cat_rows(a, b):
         ob = b.storage_offset() - base.storage_offset()
         if row > 0 and oa % row == 0 and ob == oa + a.numel():
             i = oa // row
+            if i == 0 and a.size(0) + b.size(0) == base.size(0):
+                return base      # (no slice: no SliceBackward fill + copy)
             return base[i:i + a.size(0) + b.size(0)]
     return torch.cat([a, b], dim=0)
 
@@ -275,8 +277,16 @@ class DGMC(torch.nn.Module):
                 loopgrad.loop_scope(not is_reference_mode()):
             f32 = torch.float64 if h_s.dtype == torch.float64 \
                 else torch.float32
-            hs = lay_s.to_dense(h_s.to(f32))
-            ht = lay_t.to_dense(h_t.to(f32))
+            # Dense path on the GPU: S_hat straight from the packed joint
+            # encoder output (one per-pair kernel, no padded copies).
+            h_joint = _cat_rows(h_s, h_t) if self.k < 1 and \
+                self.normalization == 'softmax' else None
+            direct = h_joint is not None and h_joint.data_ptr() == \
+                h_s.data_ptr() and dense_ops.pair_scores_supported(
+                    h_joint, lay_s, lay_t)
+            if not direct:
+                hs = lay_s.to_dense(h_s.to(f32))
+                ht = lay_t.to_dense(h_t.to(f32))
             # Random node indicators for all steps, packed [steps, sum N_s, R]
             # (drawn directly in the encoder GEMM dtype under autocast).
             r_dtype = outer_dtype if (outer_autocast and self.k < 1 and
@@ -313,7 +323,11 @@ class DGMC(torch.nn.Module):
                 'Sinkhorn normalisation is only defined for k=-1 (dense)'
             if self.k < 1:
                 # ------------------ dense variant -------------------- #
-                S_hat = hs @ ht.transpose(-1, -2)            # [B, N_s, N_t]
+                if direct:
+                    S_hat = dense_ops.pair_scores(h_joint, h_s.size(0),
+                                                  lay_s, lay_t)
+                else:
+                    S_hat = hs @ ht.transpose(-1, -2)        # [B, N_s, N_t]
                 S_0 = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 # Fused pair encoding: the transport kernel writes r_t
                 # straight into psi_2's joint input [r_s; r_t] (no cat).

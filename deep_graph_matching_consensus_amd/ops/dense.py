@@ -43,6 +43,42 @@ def _count_mask(lay_s, lay_t):
 
 
 # ---------------------------------------------------------------------------
+class _PairScores(torch.autograd.Function):
+    """``S_hat = h_s h_t^T`` per pair straight from the packed joint encoder
+    output (csrc/hip/pair_scores.hip); the backward returns the joint
+    gradient (padding rows zero) - no dense layouts, no slice backward."""
+
+    @staticmethod
+    def forward(ctx, h, t_off, ptr_s, ptr_t, N_s, N_t):
+        S = _backend.ops().pair_scores(h, t_off, ptr_s, ptr_t, N_s, N_t)
+        ctx.save_for_backward(h, ptr_s, ptr_t)
+        ctx.t_off = t_off
+        return S
+
+    @staticmethod
+    def backward(ctx, grad):
+        h, ptr_s, ptr_t = ctx.saved_tensors
+        dh = _backend.ops().pair_scores_bwd(grad.float().contiguous(), h,
+                                            ctx.t_off, ptr_s, ptr_t)
+        return dh, None, None, None, None, None
+
+
+def pair_scores_supported(h, lay_s, lay_t):
+    return (_hip_ok(h, lay_s.N, lay_t.N) and h.dim() == 2 and
+            h.is_contiguous() and h.dtype in (torch.bfloat16, torch.float32)
+            and h.size(1) <= 256 and lay_s.N >= 1 and lay_t.N >= 1)
+
+
+def pair_scores(h, t_off, lay_s, lay_t):
+    r"""Dense initial scores ``[B, N_s, N_t]`` (fp32) of the joint encoder
+    output ``h = [h_s; h_t]`` (target rows from ``t_off``): entry
+    ``(b, i, j) = <h_s[ptr_s[b] + i], h_t[ptr_t[b] + j]>``, zero outside
+    each pair's ``n_s x n_t`` block (``dgmc.py:154-163``)."""
+    return _PairScores.apply(h, int(t_off), lay_s.ptr, lay_t.ptr, lay_s.N,
+                             lay_t.N)
+
+
+# ---------------------------------------------------------------------------
 class _MaskedSoftmax(torch.autograd.Function):
     @staticmethod
     def forward(ctx, S_hat, n_s, n_t):

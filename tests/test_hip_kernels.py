@@ -850,3 +850,48 @@ def test_spline_slot_images_match_permuted_pack():
     img_f, img_t = ops.spline_slot_images(w, r, slot_k_order(w.device))
     assert torch.equal(img_f, slot_conv_image(w_lp, 128, False))
     assert torch.equal(img_t, slot_conv_image(w_lp, 128, True))
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_pair_scores_matches_dense_bmm(dtype):
+    """Per-pair S_hat = h_s h_t^T from the packed joint embedding (+ its
+    backward into the joint rows, padding rows zero) vs to_dense + bmm."""
+    torch.manual_seed(7)
+    B, C = 37, 256
+    n_s = torch.randint(1, 20, (B, ))
+    n_t = torch.randint(1, 20, (B, ))
+    pad_s, pad_t = 5, 3
+    rows_s = int(n_s.sum()) + pad_s
+    rows_t = int(n_t.sum()) + pad_t
+    h = torch.randn(rows_s + rows_t, C, device=DEV).to(dtype) \
+        .requires_grad_()
+    ptr_s = torch.zeros(B + 1, dtype=torch.int32)
+    ptr_t = torch.zeros(B + 1, dtype=torch.int32)
+    ptr_s[1:] = torch.cumsum(n_s, 0)
+    ptr_t[1:] = torch.cumsum(n_t, 0)
+    Ns, Nt = int(n_s.max()), int(n_t.max())
+
+    class Lay(object):
+        pass
+    lay_s, lay_t = Lay(), Lay()
+    lay_s.ptr, lay_s.N = ptr_s.to(DEV), Ns
+    lay_t.ptr, lay_t.N = ptr_t.to(DEV), Nt
+    S = dense_ops.pair_scores(h, rows_s, lay_s, lay_t)
+    hf = h.detach().float().requires_grad_()
+    ref = torch.zeros(B, Ns, Nt, device=DEV)
+    parts = []
+    for b in range(B):
+        a = hf[int(ptr_s[b]):int(ptr_s[b + 1])]
+        t = hf[rows_s + int(ptr_t[b]):rows_s + int(ptr_t[b + 1])]
+        parts.append((b, a, t))
+    ref = torch.stack([torch.nn.functional.pad(
+        a @ t.t(), (0, Nt - t.size(0), 0, Ns - a.size(0)))
+        for b, a, t in parts])
+    torch.testing.assert_close(S, ref, atol=1e-3, rtol=1e-4)
+    g = torch.randn_like(ref)
+    (dh, ) = torch.autograd.grad(S, h, g)
+    (dref, ) = torch.autograd.grad(ref, hf, g)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(dh.float(), dref, atol=tol, rtol=tol)
+    assert bool((dh[int(ptr_s[-1]):rows_s] == 0).all())
+    assert bool((dh[rows_s + int(ptr_t[-1]):] == 0).all())
