@@ -136,6 +136,133 @@ __global__ __launch_bounds__(256) void nll_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Fused masked row softmax + NLL + Hits@1 of the dense correspondences, for
+// the training objective (DGMC.loss / DGMC.acc, dgmc.py:246-288, on
+// masked_softmax(S_hat), dgmc.py:15-19,165,181).  Ground truth of packed row
+// r = ptr_s[b] + i is column y[r] (weight mask[r]); rows are visited in the
+// dense [B, Ns] grid, so the backward writes every dense row (zeros outside
+// the valid n_s x n_t blocks) without a zero-fill pass.
+//   fwd: per-block partials (sum -log(S_y + eps), count, correct) -> fold
+//   bwd: dS_hat[b, i, j] = d S_j (delta_jy - S_y),  d = -g / ((S_y + eps) n)
+// The packed probabilities themselves are never written (the training step
+// does not read them).
+// ---------------------------------------------------------------------------
+constexpr int kSnWaves = 4;
+
+__global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_fwd_kernel(
+    const float* __restrict__ S_hat, const int* __restrict__ ptr_s,
+    const int* __restrict__ n_t, const int64_t* __restrict__ y,
+    const bool* __restrict__ mask, float* __restrict__ part, int B, int Ns,
+    int Nt, float eps) {
+  __shared__ float red[kSnWaves][3];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int row = blockIdx.x * kSnWaves + wave;     // dense row b * Ns + i
+  float l = 0.f, c = 0.f, k = 0.f;
+  if (row < B * Ns) {
+    const int b = row / Ns, i = row - b * Ns;
+    const int r = ptr_s[b] + i;
+    const int nt = n_t[b];
+    if (r < ptr_s[b + 1] && nt > 0 && (mask == nullptr || mask[r])) {
+      const float* src = S_hat + (size_t)row * Nt;
+      const int t = (int)y[r];
+      float m = -INFINITY;
+      int arg = 0;
+      for (int j = lane; j < nt; j += kWave) {
+        const float v = src[j];
+        if (v > m) { m = v; arg = j; }
+      }
+      // wave argmax (first index among equal maxima)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float mo = __shfl_xor(m, o);
+        const int ao = __shfl_xor(arg, o);
+        if (mo > m || (mo == m && ao < arg)) { m = mo; arg = ao; }
+      }
+      float s = 0.f;
+      for (int j = lane; j < nt; j += kWave) s += __expf(src[j] - m);
+      s = wave_sum(s);
+      const float st = (t >= 0 && t < nt) ? __expf(src[t] - m) / s : 0.f;
+      l = -__logf(st + eps);
+      c = 1.f;
+      k = arg == t ? 1.f : 0.f;
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = l;
+    red[wave][1] = c;
+    red[wave][2] = k;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float a = 0.f;
+    for (int w = 0; w < kSnWaves; ++w) a += red[w][threadIdx.x];
+    part[(size_t)blockIdx.x * 3 + threadIdx.x] = a;
+  }
+}
+
+// Fixed-order fold of the block partials: loss (mean over counted rows),
+// aux = [count, correct].
+__global__ __launch_bounds__(kLossThreads) void softmax_nll_fold_kernel(
+    const float* __restrict__ part, int nblocks, float* __restrict__ loss,
+    float* __restrict__ aux) {
+  __shared__ float red[kLossThreads / kWave];
+  float a = 0.f, c = 0.f, k = 0.f;
+  for (int i = threadIdx.x; i < nblocks; i += kLossThreads) {
+    a += part[3 * i];
+    c += part[3 * i + 1];
+    k += part[3 * i + 2];
+  }
+  a = block_sum(a, red);
+  c = block_sum(c, red);
+  k = block_sum(k, red);
+  if (threadIdx.x == 0) {
+    loss[0] = a / fmaxf(c, 1.f);
+    aux[0] = c;
+    aux[1] = k;
+  }
+}
+
+__global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_bwd_kernel(
+    const float* __restrict__ grad, const float* __restrict__ S_hat,
+    const int* __restrict__ ptr_s, const int* __restrict__ n_t,
+    const int64_t* __restrict__ y, const bool* __restrict__ mask,
+    const float* __restrict__ aux, float* __restrict__ dS, int B, int Ns,
+    int Nt, float eps) {
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int row = blockIdx.x * kSnWaves + wave;
+  if (row >= B * Ns) return;
+  const int b = row / Ns, i = row - b * Ns;
+  const int r = ptr_s[b] + i;
+  const int nt = n_t[b];
+  float* d = dS + (size_t)row * Nt;
+  const bool valid =
+      r < ptr_s[b + 1] && nt > 0 && (mask == nullptr || mask[r]);
+  const int t = valid ? (int)y[r] : -1;
+  if (!valid || t < 0 || t >= nt) {
+    for (int j = lane; j < Nt; j += kWave) d[j] = 0.f;
+    return;
+  }
+  const float* src = S_hat + (size_t)row * Nt;
+  float m = -INFINITY;
+  for (int j = lane; j < nt; j += kWave) m = fmaxf(m, src[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < nt; j += kWave) s += __expf(src[j] - m);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  const float st = __expf(src[t] - m) * inv;
+  const float dy = -grad[0] / ((st + eps) * fmaxf(aux[0], 1.f));
+  for (int j = lane; j < Nt; j += kWave) {
+    float v = 0.f;
+    if (j < nt) {
+      const float sj = __expf(src[j] - m) * inv;
+      v = dy * sj * ((j == t ? 1.f : 0.f) - st);
+    }
+    d[j] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Non-finite check: per-block flags, then one block folds them into the
 // found_inf scalar (fp32 0/1, read by fused Adam) and the skipped-step count.
 // ---------------------------------------------------------------------------
@@ -311,6 +438,79 @@ void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,
                      part.data_ptr<int>(), blocks, found_inf.data_ptr<float>(),
                      cp);
   DGMC_CHECK_LAUNCH();
+}
+
+namespace {
+void check_snll(const at::Tensor& S_hat, const at::Tensor& ptr_s,
+                const at::Tensor& n_t, const at::Tensor& y,
+                const c10::optional<at::Tensor>& mask) {
+  TORCH_CHECK(S_hat.is_cuda() && S_hat.scalar_type() == at::kFloat &&
+                  S_hat.dim() == 3 && S_hat.is_contiguous(),
+              "softmax_nll: contiguous fp32 S_hat [B, Ns, Nt]");
+  const int64_t B = S_hat.size(0);
+  TORCH_CHECK(ptr_s.scalar_type() == at::kInt && ptr_s.numel() == B + 1 &&
+                  n_t.scalar_type() == at::kInt && n_t.numel() == B,
+              "softmax_nll: int32 ptr_s [B + 1] / n_t [B]");
+  TORCH_CHECK(y.scalar_type() == at::kLong && y.is_contiguous(),
+              "softmax_nll: int64 y per packed row");
+  if (mask.has_value() && mask->defined())
+    TORCH_CHECK(mask->scalar_type() == at::kBool &&
+                    mask->numel() == y.numel() && mask->is_contiguous(),
+                "softmax_nll: bool mask per packed row");
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
+    const at::Tensor& S_hat, const at::Tensor& ptr_s, const at::Tensor& n_t,
+    const at::Tensor& y, const c10::optional<at::Tensor>& mask, double eps) {
+  check_snll(S_hat, ptr_s, n_t, y, mask);
+  const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
+  auto opt = S_hat.options();
+  at::Tensor loss = at::empty({}, opt);
+  at::Tensor aux = at::empty({2}, opt);
+  const int rows = B * Ns;
+  const int nblocks = std::max(1, (rows + kSnWaves - 1) / kSnWaves);
+  at::Tensor part = at::empty({nblocks * 3}, opt);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  hipLaunchKernelGGL(softmax_nll_fwd_kernel, dim3(nblocks),
+                     dim3(kSnWaves * 64), 0, stream(), S_hat.data_ptr<float>(),
+                     ptr_s.data_ptr<int>(), n_t.data_ptr<int>(),
+                     y.data_ptr<int64_t>(), mp, part.data_ptr<float>(), B, Ns,
+                     Nt, (float)eps);
+  hipLaunchKernelGGL(softmax_nll_fold_kernel, dim3(1), dim3(kLossThreads), 0,
+                     stream(), part.data_ptr<float>(), nblocks,
+                     loss.data_ptr<float>(), aux.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return {loss, aux};
+}
+
+at::Tensor softmax_nll_bwd(const at::Tensor& grad, const at::Tensor& S_hat,
+                           const at::Tensor& ptr_s, const at::Tensor& n_t,
+                           const at::Tensor& y,
+                           const c10::optional<at::Tensor>& mask,
+                           const at::Tensor& aux, double eps) {
+  check_snll(S_hat, ptr_s, n_t, y, mask);
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.numel() == 1 &&
+                  aux.scalar_type() == at::kFloat && aux.numel() == 2,
+              "softmax_nll_bwd: fp32 scalar grad / aux [2]");
+  const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
+  at::Tensor dS = at::empty_like(S_hat);
+  const int rows = B * Ns;
+  if (rows == 0) return dS;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  hipLaunchKernelGGL(softmax_nll_bwd_kernel,
+                     dim3((rows + kSnWaves - 1) / kSnWaves),
+                     dim3(kSnWaves * 64), 0, stream(), grad.data_ptr<float>(),
+                     S_hat.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                     n_t.data_ptr<int>(), y.data_ptr<int64_t>(), mp,
+                     aux.data_ptr<float>(), dS.data_ptr<float>(), B, Ns, Nt,
+                     (float)eps);
+  DGMC_CHECK_LAUNCH();
+  return dS;
 }
 
 }  // namespace dgmc

@@ -147,6 +147,14 @@ std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         bool has_root);
 void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
                 at::TensorList views);
+std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
+    const at::Tensor& S_hat, const at::Tensor& ptr_s, const at::Tensor& n_t,
+    const at::Tensor& y, const c10::optional<at::Tensor>& mask, double eps);
+at::Tensor softmax_nll_bwd(const at::Tensor& grad, const at::Tensor& S_hat,
+                           const at::Tensor& ptr_s, const at::Tensor& n_t,
+                           const at::Tensor& y,
+                           const c10::optional<at::Tensor>& mask,
+                           const at::Tensor& aux, double eps);
 at::Tensor pair_scores(const at::Tensor& h, int64_t t_off,
                        const at::Tensor& ptr_s, const at::Tensor& ptr_t,
                        int64_t Ns, int64_t Nt);
@@ -257,6 +265,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor)");
   m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
   m.def(
+      "softmax_nll_fwd(Tensor S_hat, Tensor ptr_s, Tensor n_t, Tensor y, "
+      "Tensor? mask, float eps) -> (Tensor, Tensor)");
+  m.def(
+      "softmax_nll_bwd(Tensor grad, Tensor S_hat, Tensor ptr_s, Tensor n_t, "
+      "Tensor y, Tensor? mask, Tensor aux, float eps) -> Tensor");
+  m.def(
       "pair_scores(Tensor h, int t_off, Tensor ptr_s, Tensor ptr_t, int Ns, "
       "int Nt) -> Tensor");
   m.def(
@@ -331,6 +345,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
   m.impl("pack_grads", &dgmc::pack_grads);
+  m.impl("softmax_nll_fwd", &dgmc::softmax_nll_fwd);
+  m.impl("softmax_nll_bwd", &dgmc::softmax_nll_bwd);
   m.impl("pair_scores", &dgmc::pair_scores);
   m.impl("pair_scores_bwd", &dgmc::pair_scores_bwd);
   m.impl("spline_slot_images", &dgmc::spline_slot_images);

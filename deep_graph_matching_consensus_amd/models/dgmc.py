@@ -88,6 +88,14 @@ class _TieUnused(torch.autograd.Function):
         return grad, grad.new_zeros(shape, dtype=dtype)
 
 
+class _RawScores(object):
+    """Dense-path scores before the output softmax (``DGMC.objective``)."""
+
+    def __init__(self, S_hat_0, S_hat_L, lay_s, lay_t):
+        self.S_hat_0, self.S_hat_L = S_hat_0, S_hat_L
+        self.lay_s, self.lay_t = lay_s, lay_t
+
+
 def _device_type(device):
     return 'cuda' if device.type == 'cuda' else 'cpu'
 
@@ -239,7 +247,7 @@ class DGMC(torch.nn.Module):
                                  edge_index_t, edge_attr_t, batch_t, y)
 
     def _forward(self, x_s, edge_index_s, edge_attr_s, batch_s, x_t,
-                 edge_index_t, edge_attr_t, batch_t, y):
+                 edge_index_t, edge_attr_t, batch_t, y, raw=False):
         device = x_s.device
         dev_type = _device_type(device)
         outer_autocast = torch.is_autocast_enabled(dev_type)
@@ -328,7 +336,12 @@ class DGMC(torch.nn.Module):
                                                   lay_s, lay_t)
                 else:
                     S_hat = hs @ ht.transpose(-1, -2)        # [B, N_s, N_t]
-                S_0 = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
+                # raw: the caller (objective) fuses softmax + NLL on the
+                # scores themselves; the probabilities are never formed.
+                raw = raw and dense_ops.softmax_nll_supported(S_hat, lay_s)
+                S_hat_0 = S_hat
+                S_0 = None if raw else \
+                    dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 # Fused pair encoding: the transport kernel writes r_t
                 # straight into psi_2's joint input [r_s; r_t] (no cat).
                 joint = steps > 0 and pair is not None and \
@@ -373,6 +386,8 @@ class DGMC(torch.nn.Module):
                     S_hat = dense_ops.consensus_update(
                         S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o,
                         w1_fold=fold)
+                if raw:
+                    return _RawScores(S_hat_0, S_hat, lay_s, lay_t)
                 S_L = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 return S_0, S_L
 
@@ -442,6 +457,40 @@ class DGMC(torch.nn.Module):
     # ------------------------------------------------------------------
     # Objectives and metrics (dgmc.py:246-311)
     # ------------------------------------------------------------------
+    def objective(self, x_s, edge_index_s, edge_attr_s, batch_s, x_t,
+                  edge_index_t, edge_attr_t, batch_t, y_col, mask=None):
+        r"""The reference drivers' training objective (``pascal.py:67-72``):
+        ``NLL(S_0) + NLL(S_L)`` (``NLL(S_0)`` alone when ``num_steps`` is 0)
+        for ground truth ``y = (arange(sum N_s), y_col)``, plus the Hits@1
+        count of ``S_L``.  Returns ``(loss, count, correct)`` as device
+        tensors (``mask`` selects the valid ground truths of a padded
+        batch).
+
+        On the GPU's dense path the row softmax, NLL and arg-max run as ONE
+        fused kernel on the raw scores per output (``softmax_nll``), whose
+        backward writes the score gradient directly - the packed
+        probabilities are never materialised.  Elsewhere this is
+        ``forward`` + :meth:`loss_stats` / :meth:`loss`."""
+        with forward_cache():
+            out = self._forward(x_s, edge_index_s, edge_attr_s, batch_s, x_t,
+                                edge_index_t, edge_attr_t, batch_t, None,
+                                raw=True)
+        if isinstance(out, _RawScores):
+            y_col = y_col.contiguous()
+            loss, aux = dense_ops.softmax_nll(out.S_hat_L, out.lay_s,
+                                              out.lay_t, y_col, mask, EPS)
+            if self.num_steps:
+                loss = loss + dense_ops.softmax_nll(
+                    out.S_hat_0, out.lay_s, out.lay_t, y_col, mask, EPS)[0]
+            return loss, aux[0], aux[1]
+        S_0, S_L = out
+        rows = torch.arange(y_col.numel(), device=y_col.device)
+        y = torch.stack([rows, y_col], dim=0)
+        if self.num_steps:
+            loss_L, count, correct = self.loss_stats(S_L, y, mask)
+            return loss_L + self.loss(S_0, y, mask=mask), count, correct
+        return self.loss_stats(S_0, y, mask)
+
     def loss(self, S, y, reduction='mean', mask=None):
         r"""Negative log-likelihood of the ground-truth correspondences.
 

@@ -134,6 +134,46 @@ def masked_softmax_packed(S_hat, lay_s, lay_t):
     return lay_s.to_sparse(masked_softmax(S_hat, lay_s, lay_t))
 
 
+class _SoftmaxNLL(torch.autograd.Function):
+    """Masked row softmax + NLL (+ Hits@1) on the dense scores in one fused
+    kernel (csrc/hip/loss.hip::softmax_nll_*); ``aux = [count, correct]``."""
+
+    @staticmethod
+    def forward(ctx, S_hat, ptr_s, n_t, y, mask, eps):
+        S_hat = S_hat.float().contiguous()
+        loss, aux = _backend.ops().softmax_nll_fwd(S_hat, ptr_s, n_t, y, mask,
+                                                   eps)
+        ctx.save_for_backward(S_hat, ptr_s, n_t, y, mask, aux)
+        ctx.eps = eps
+        ctx.mark_non_differentiable(aux)
+        ctx.set_materialize_grads(False)
+        return loss, aux
+
+    @staticmethod
+    def backward(ctx, grad, grad_aux):
+        if grad is None:
+            return (None, ) * 6
+        S_hat, ptr_s, n_t, y, mask, aux = ctx.saved_tensors
+        dS = _backend.ops().softmax_nll_bwd(grad.float().reshape(1), S_hat,
+                                            ptr_s, n_t, y, mask, aux, ctx.eps)
+        return dS, None, None, None, None, None
+
+
+def softmax_nll_supported(S_hat, lay_s):
+    return (_backend.use_hip(S_hat) and S_hat.dim() == 3 and
+            torch.is_tensor(getattr(lay_s, 'ptr', None)) and
+            lay_s.ptr.is_cuda)
+
+
+def softmax_nll(S_hat, lay_s, lay_t, y_col, mask, eps):
+    r"""``(loss, aux)``: mean of ``-log(masked_softmax(S_hat)[r, y_col[r]] +
+    eps)`` over the packed source rows ``r`` (weights ``mask``) and
+    ``aux = [count, correct top-1]`` - ``DGMC.loss`` / ``DGMC.correct`` of
+    ``masked_softmax_packed(S_hat)`` with ``y = (arange, y_col)``."""
+    return _SoftmaxNLL.apply(S_hat, lay_s.ptr, lay_t.counts, y_col, mask,
+                             float(eps))
+
+
 # ---------------------------------------------------------------------------
 class _SoftmaxTransport(torch.autograd.Function):
     @staticmethod

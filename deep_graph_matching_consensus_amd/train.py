@@ -124,17 +124,25 @@ class PairTrainer(object):
 
     def _forward_backward(self, batch, rows, mask):
         model = self.model
-        with self._autocast():
-            S_0, S_L = model(batch.x_s, batch.edge_index_s,
-                             batch.edge_attr_s, batch.x_s_batch, batch.x_t,
-                             batch.edge_index_t, batch.edge_attr_t,
-                             batch.x_t_batch)
-        y = torch.stack([rows, batch.y], dim=0)
-        if model.num_steps:
-            loss_L, count, correct = model.loss_stats(S_L, y, mask)
-            loss = loss_L + model.loss(S_0, y, mask=mask)
+        if hasattr(model, 'objective') and rows.numel() == batch.y.numel():
+            # NLL(S_0) + NLL(S_L) on the raw scores (fused softmax + NLL).
+            with self._autocast():
+                loss, count, correct = model.objective(
+                    batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+                    batch.x_s_batch, batch.x_t, batch.edge_index_t,
+                    batch.edge_attr_t, batch.x_t_batch, batch.y, mask)
         else:
-            loss, count, correct = model.loss_stats(S_0, y, mask)
+            with self._autocast():
+                S_0, S_L = model(batch.x_s, batch.edge_index_s,
+                                 batch.edge_attr_s, batch.x_s_batch,
+                                 batch.x_t, batch.edge_index_t,
+                                 batch.edge_attr_t, batch.x_t_batch)
+            y = torch.stack([rows, batch.y], dim=0)
+            if model.num_steps:
+                loss_L, count, correct = model.loss_stats(S_L, y, mask)
+                loss = loss_L + model.loss(S_0, y, mask=mask)
+            else:
+                loss, count, correct = model.loss_stats(S_0, y, mask)
         loss.backward()
         self.stats[:3] += torch.stack(
             [loss.detach().float(), correct.float(), count.float()]).double()

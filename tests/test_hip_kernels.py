@@ -895,3 +895,48 @@ def test_pair_scores_matches_dense_bmm(dtype):
     torch.testing.assert_close(dh.float(), dref, atol=tol, rtol=tol)
     assert bool((dh[int(ptr_s[-1]):rows_s] == 0).all())
     assert bool((dh[rows_s + int(ptr_t[-1]):] == 0).all())
+
+
+@pytest.mark.parametrize('num_steps', [0, 3])
+def test_objective_fused_softmax_nll_matches_unfused(monkeypatch, num_steps):
+    """DGMC.objective with the fused softmax + NLL kernels == forward +
+    masked_softmax_packed + NLL (loss, count, Hits@1 count, gradients)."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    groups = make_keypoint_datasets(graphs=16, feature_dim=32, seed=4)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 48, seed=2)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(32, 64, 2, 2, cat=False),
+                 SplineCNN(16, 16, 2, 2, cat=True),
+                 num_steps=num_steps).to(DEV)
+    model.eval()
+    assert batcher.load()
+    batch = batcher.materialize()
+
+    def run():
+        torch.manual_seed(1)
+        loss, count, correct = model.objective(
+            batch.x_s, batch.edge_index_s, batch.edge_attr_s, batch.x_s_batch,
+            batch.x_t, batch.edge_index_t, batch.edge_attr_t,
+            batch.x_t_batch, batch.y, batch.y_mask)
+        grads = torch.autograd.grad(loss, list(model.parameters()),
+                                    allow_unused=True)
+        return loss.detach(), count, correct, grads
+
+    fused = run()
+    monkeypatch.setattr(dense_ops, 'softmax_nll_supported',
+                        lambda *a: False)
+    plain = run()
+    torch.testing.assert_close(fused[0], plain[0], atol=1e-5, rtol=1e-5)
+    assert float(fused[1]) == float(plain[1]) == float(batch.y_mask.sum())
+    assert float(fused[2]) == float(plain[2])
+    for a, b in zip(fused[3], plain[3]):
+        if a is None or b is None:
+            assert a is None or b is None or float(a.abs().max()) == 0 or \
+                float(b.abs().max()) == 0
+            continue
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
