@@ -17,6 +17,7 @@ Metrics are accumulated on the device and synchronised only when read.
 Checkpoints store the model in the reference state-dict schema plus
 optimizer state, step counter and RNG states (resume support).
 """
+import gc
 import json
 import os
 import random
@@ -222,6 +223,12 @@ class PairTrainer(object):
                 raise RuntimeError('no batch fits bucket {}'.format(b))
             self._graphs[i].capture()
         self._captured = True
+        # The capture phase leaves large autograd graphs behind: collect them
+        # now and move the survivors out of the collector's generations, so
+        # no full collection pauses the host during the replayed steps.
+        gc.collect()
+        if hasattr(gc, 'freeze'):
+            gc.freeze()
 
     def step(self):
         """One training step (data, forward, backward, all-reduce, Adam)."""
