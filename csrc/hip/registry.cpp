@@ -147,6 +147,8 @@ std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         bool has_root);
 void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
                 at::TensorList views);
+at::Tensor cat_gemm(at::TensorList xs, const at::Tensor& W,
+                    const c10::optional<at::Tensor>& ocat);
 std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
     const at::Tensor& S_hat, const at::Tensor& ptr_s, const at::Tensor& n_t,
     const at::Tensor& y, const c10::optional<at::Tensor>& mask, double eps);
@@ -264,6 +266,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "spline_weight_unpack(Tensor g, int K, bool has_root) -> (Tensor, "
       "Tensor)");
   m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
+  m.def("cat_gemm(Tensor[] xs, Tensor W, Tensor(a!)? ocat=None) -> Tensor");
   m.def(
       "softmax_nll_fwd(Tensor S_hat, Tensor ptr_s, Tensor n_t, Tensor y, "
       "Tensor? mask, float eps) -> (Tensor, Tensor)");
@@ -345,6 +348,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_weight_unpack", &dgmc::spline_weight_unpack);
   m.impl("slot_conv_relu_bwd", &dgmc::slot_conv_relu_bwd);
   m.impl("pack_grads", &dgmc::pack_grads);
+  m.impl("cat_gemm", &dgmc::cat_gemm);
   m.impl("softmax_nll_fwd", &dgmc::softmax_nll_fwd);
   m.impl("softmax_nll_bwd", &dgmc::softmax_nll_bwd);
   m.impl("pair_scores", &dgmc::pair_scores);

@@ -40,7 +40,7 @@ from ..runtime import loopgrad
 from ..runtime.cache import forward_cache
 from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
-from .encoder import StackedEncoder
+from .encoder import CatParts, StackedEncoder
 
 # DGMC_AMD_FOLD_PROJECTION=0 keeps psi_2's final Linear as its own GEMM.
 FOLD_PROJECTION = os.environ.get('DGMC_AMD_FOLD_PROJECTION', '1') == '1'
@@ -309,7 +309,12 @@ class DGMC(torch.nn.Module):
                 autocast policy; returns (o_s, o_t, o_joint or None).
                 ``r_joint`` = ``[r_s; r_t]`` already assembled; ``features``
                 skips psi_2's final Linear (folded by the caller)."""
-                ctx = self.psi_2.features_only() if features else \
+                # features: psi_2's final Linear is folded by the caller; its
+                # concatenated features may stay unformed (CatParts, read
+                # in place by the consensus projection).
+                ctx = (self.psi_2.features_parts() if hasattr(
+                    self.psi_2, 'features_parts') else
+                    self.psi_2.features_only()) if features else \
                     contextlib.nullcontext()
                 with torch.autocast(device_type=dev_type, dtype=outer_dtype,
                                     enabled=outer_autocast), ctx:
@@ -318,6 +323,8 @@ class DGMC(torch.nn.Module):
                             r_joint = torch.cat([r_s, r_t], dim=0)
                         o = self.psi_2(r_joint, pair.edge_index,
                                        pair.edge_attr)
+                        if isinstance(o, CatParts):
+                            return None, None, o
                         return o[:pair.n_s], o[pair.n_s:], o
                     o_s = self.psi_2(r_s, edge_index_s, edge_attr_s)
                     o_t = self.psi_2(r_t, edge_index_t, edge_attr_t)
@@ -361,7 +368,8 @@ class DGMC(torch.nn.Module):
                         # (autograd.grad, DDP) without any kernel.
                         w_fold = _TieUnused.apply(w_fold,
                                                   self.psi_2.final.bias)
-                    fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)))
+                    fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)),
+                            steps)
                 for step in range(steps):
                     mark('dgmc.consensus_step')
                     r_s = r_all[step]

@@ -23,6 +23,27 @@ from torch.nn import Linear
 from ..ops.gemm import linear
 
 
+class CatParts(object):
+    """The concatenation ``torch.cat(parts, -1)`` left unformed: a consumer
+    that reads the parts directly (``ops/dense.py::cat_matmul``) skips the
+    copy; :meth:`cat` forms it for any other consumer."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+
+    def cat(self):
+        return torch.cat(self.parts, dim=-1)
+
+    def size(self, dim=None):
+        n = self.parts[0].size(0)
+        c = sum(p.size(-1) for p in self.parts)
+        return torch.Size([n, c]) if dim is None else (n, c)[dim]
+
+    @property
+    def dtype(self):
+        return self.parts[0].dtype
+
+
 class StackedEncoder(torch.nn.Module):
     def _init_head(self, in_channels, out_channels, num_layers, cat, lin):
         self.in_channels = in_channels
@@ -57,6 +78,26 @@ class StackedEncoder(torch.nn.Module):
             yield self
         finally:
             self._features_only = prev
+
+    @contextlib.contextmanager
+    def features_parts(self):
+        """Like :meth:`features_only`, and with ``cat=True`` (and no active
+        dropout) ``forward`` returns the layer features as a
+        :class:`CatParts` instead of concatenating them."""
+        prev = getattr(self, '_features_parts', False)
+        self._features_parts = True
+        try:
+            with self.features_only():
+                yield self
+        finally:
+            self._features_parts = prev
+
+    def _parts_out(self, xs):
+        """:class:`CatParts` of ``xs`` when :meth:`features_parts` applies."""
+        if (getattr(self, '_features_parts', False) and self.cat and
+                (getattr(self, 'dropout', 0.0) == 0.0 or not self.training)):
+            return CatParts(xs)
+        return None
 
     @property
     def pair_fusable(self):

@@ -47,6 +47,9 @@ class SplineCNN(StackedEncoder):
             else:
                 out = conv(xs[-1], edge_index, edge_attr, act='relu')
             xs.append(out)
+        parts = self._parts_out(xs)
+        if parts is not None:
+            return parts
         h = F.dropout(self._head(xs), p=self.dropout, training=self.training)
         return self._project(h)
 

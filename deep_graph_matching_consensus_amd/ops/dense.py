@@ -314,6 +314,88 @@ class _ConsensusUpdate(torch.autograd.Function):
         return (grad.to(s_dt), dP, dQ, db1, dw2, db2, None, None, None)
 
 
+class _CatMatmul(torch.autograd.Function):
+    """``[X_0 | X_1 | ...] @ W`` (bf16, ``W = w [K, 128]``) without forming
+    the concatenation for the product (``cat_gemm``); the kernel writes the
+    concatenation once into the loop's stacked weight-gradient operand.
+    Backward: ``g W^T`` split into column views (no copies) and, when the
+    last loop use arrives, ONE long-K ``dW`` GEMM over all uses."""
+
+    @staticmethod
+    def forward(ctx, w, w_n, w_nt, loop, total, *parts):
+        M = parts[0].size(0)
+        K = sum(p.size(1) for p in parts)
+        ctx.loop, ctx.widths = loop, [p.size(1) for p in parts]
+        ctx.w_dtype = w.dtype
+        need_w = ctx.needs_input_grad[0] and torch.is_grad_enabled()
+        if loop is not None:
+            ctx.idx = loop.register()
+            ocat = loop.slot_total('x', ctx.idx, (M, K), w_n.dtype,
+                                   w_n.device, total)
+        else:
+            ctx.idx = None
+            ocat = torch.empty((M, K), dtype=w_n.dtype, device=w_n.device) \
+                if need_w else None
+        out = _backend.ops().cat_gemm(list(parts), w_n, ocat)
+        ctx.save_for_backward(w_n, w_nt)
+        ctx.ocat = ocat if loop is None else None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .gemm import matmul_tn_fp32
+        w_n, w_nt = ctx.saved_tensors
+        g = g.contiguous()
+        if g.dtype != w_n.dtype:
+            g = g.to(w_n.dtype)
+        # g W^T = [M, 128] x [128, K]: hipBLASLt (8.7 us at M = 20k,
+        # K = 384, vs 11.0 us for cat_gemm with W^T staged).
+        gx = g @ w_n                                     # [M, K]
+        grads, off = [], 0
+        for i, wd in enumerate(ctx.widths):
+            grads.append(gx[:, off:off + wd]
+                         if ctx.needs_input_grad[5 + i] else None)
+            off += wd
+        gw = None
+        loop = ctx.loop
+        if loop is None:
+            if ctx.needs_input_grad[0]:
+                gw = matmul_tn_fp32(ctx.ocat, g).to(ctx.w_dtype)
+        else:
+            loop.keep('g', ctx.idx, g)
+            if loop.arrive():
+                if ctx.needs_input_grad[0]:
+                    X = loop.stack('x')
+                    gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
+                                        loop.kept('g')).to(ctx.w_dtype)
+                loop.release()
+        return (gw, None, None, None, None) + tuple(grads)
+
+
+def cat_matmul_supported(parts, w_t):
+    return (all(_backend.use_hip(p) and p.dtype == torch.bfloat16 and
+                p.dim() == 2 and p.stride(1) == 1 and p.size(1) % 32 == 0 and
+                p.stride(0) % 8 == 0 and p.data_ptr() % 16 == 0
+                for p in parts) and
+            1 <= len(parts) <= 4 and w_t.size(1) == 128 and
+            w_t.size(0) == sum(p.size(1) for p in parts) and
+            w_t.size(0) in (128, 256, 384))
+
+
+def cat_matmul(parts, w_t, lp, key, total):
+    """``cat(parts, -1) @ w_t`` with ``w_t [K, 128]`` (fp32, receives the
+    gradient) - see :class:`_CatMatmul`; ``total`` = uses of ``key``'s loop
+    collector in this forward (the consensus steps)."""
+    w_n = lp.get('n')
+    if w_n is None:
+        w_n = lp['n'] = w_t.detach().t().to(torch.bfloat16).contiguous()
+        lp['nt'] = w_n.t().contiguous()
+    loop = loopgrad.group(('catmm', ) + key + (parts[0].size(0), )) \
+        if total else None
+    with torch.autocast(device_type='cuda', enabled=False):
+        return _CatMatmul.apply(w_t, w_n, lp['nt'], loop, total, *parts)
+
+
 def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
                      w1_fold=None):
     r"""``S_hat + mask * mlp(o_s[:, :, None] - o_t[:, None])`` for packed
@@ -330,7 +412,16 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
                                 not _hip_ok(S_hat, N_s, N_t)):
         raise ValueError('w1_fold needs the joint HIP path')
     if w1_fold is not None:
-        w_t, lp, key = w1_fold
+        w_t, lp, key, total = w1_fold
+        parts = getattr(o_joint, 'parts', None)
+        if parts is not None and cat_matmul_supported(parts, w_t):
+            PQ = cat_matmul(parts, w_t, lp, key, total)
+            loop = loopgrad.group(('consensus', id(mlp)))
+            return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes,
+                                          lin1.bias, lin2.weight, lin2.bias,
+                                          lay_s.ptr, lay_t.ptr, loop)
+        if parts is not None:
+            o_joint = o_joint.cat()
         w_lp = lp.get(o_joint.dtype)
         if w_lp is None:
             w_lp = lp[o_joint.dtype] = w_t.detach().to(o_joint.dtype)

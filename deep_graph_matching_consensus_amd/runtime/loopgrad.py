@@ -78,6 +78,19 @@ class LoopGrad(object):
                 tuple(buf.shape[1:]), shape)
         return buf[idx]
 
+    def slot_total(self, name, idx, shape, dtype, device, total):
+        """Slot ``idx`` of the ``[total, *shape]`` stack ``name`` - for
+        producers that write their contribution during the FORWARD, when
+        ``uses`` is still growing (the caller knows the final count)."""
+        buf = self._stacks.get(name)
+        shape = tuple(shape)
+        if buf is None:
+            buf = torch.empty((total, ) + shape, dtype=dtype, device=device)
+            self._stacks[name] = buf
+        assert buf.shape[1:] == shape and buf.dtype == dtype and \
+            idx < buf.size(0), 'loop stack {} mismatch'.format(name)
+        return buf[idx]
+
     def stack(self, name):
         return self._stacks[name]
 

@@ -940,3 +940,69 @@ def test_objective_fused_softmax_nll_matches_unfused(monkeypatch, num_steps):
                 float(b.abs().max()) == 0
             continue
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize('widths,M', [((128, 128, 128), 10307),
+                                      ((128, ), 77), ((256, 128), 300)])
+def test_cat_gemm_matches_cat_matmul(widths, M):
+    """cat_gemm: [X_0 | X_1 | ...] @ W^T from strided inputs, plus the
+    concatenation side output."""
+    ops = _backend.ops()
+    torch.manual_seed(3)
+    wide = torch.randn(M, sum(widths) + 64, device=DEV).bfloat16()
+    parts, off = [], 0
+    for w in widths:
+        parts.append(wide[:, off:off + w])      # strided column slices
+        off += w
+    K = sum(widths)
+    W = (torch.randn(128, K, device=DEV) / K ** 0.5).bfloat16()
+    ocat = torch.empty(M, K, dtype=torch.bfloat16, device=DEV)
+    out = ops.cat_gemm(parts, W, ocat)
+    cat = torch.cat(parts, dim=1)
+    assert torch.equal(ocat, cat)
+    ref = cat.float() @ W.float().t()
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    # transposed use (backward): [M, 128] @ [128, K] with W^T staged
+    g = torch.randn(M, 128, device=DEV).bfloat16()
+    gx = ops.cat_gemm([g], W.t().contiguous(), None)
+    torch.testing.assert_close(gx.float(), g.float() @ W.float(), atol=2e-2,
+                               rtol=2e-2)
+
+
+def test_consensus_cat_matmul_matches_formed_concatenation(monkeypatch):
+    """Static-batch consensus loop: the unformed psi_2 concatenation read by
+    cat_gemm == torch.cat + GEMM (forward S_L and every gradient)."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    groups = make_keypoint_datasets(graphs=16, feature_dim=32, seed=5)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 48, seed=3)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(32, 64, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=4).to(DEV)
+    model.eval()
+    assert batcher.load()
+    batch = batcher.materialize()
+
+    def run():
+        torch.manual_seed(1)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss, count, correct = model.objective(
+                batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+                batch.x_s_batch, batch.x_t, batch.edge_index_t,
+                batch.edge_attr_t, batch.x_t_batch, batch.y, batch.y_mask)
+        return loss.detach(), torch.autograd.grad(
+            loss, list(model.parameters()), allow_unused=True)
+
+    l1, g1 = run()
+    monkeypatch.setattr(dense_ops, 'cat_matmul_supported', lambda *a: False)
+    l0, g0 = run()
+    torch.testing.assert_close(l1, l0, atol=1e-3, rtol=1e-3)
+    for a, b in zip(g1, g0):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
