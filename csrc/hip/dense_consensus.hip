@@ -547,6 +547,339 @@ __global__ __launch_bounds__(kThreads) void consensus_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Fused step boundary of the consensus loop: consensus update of step l
+// followed by the softmax + transport of step l + 1, per pair in ONE
+// workgroup (the updated S_hat tile never leaves LDS between the two):
+//
+//   S_hat' = S_hat + mask * (relu(P_i + b1 - Q_j) . w2 + b2)     (step l)
+//   S      = masked_softmax(S_hat')                               (step l+1)
+//   joint  = [r_s; S^T r_s]                                       (step l+1)
+//
+// Outputs S_hat' (the step's result), S (saved for the backward) and the
+// joint psi_2 input.  LDS: sP, sQ [N][R+1], sB, sW [R], sR [Ns][R], sS [NN].
+// ---------------------------------------------------------------------------
+template <typename TPQ, typename TR>
+__global__ __launch_bounds__(kThreads) void consensus_transport_kernel(
+    const float* __restrict__ S_hat, const TPQ* __restrict__ P,
+    const TPQ* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2,
+    const TR* __restrict__ r_s, const int* __restrict__ ptr_s,
+    const int* __restrict__ ptr_t, float* __restrict__ S_new,
+    float* __restrict__ S_prob, TR* __restrict__ joint, int Ns, int Nt,
+    int R, int rows_s, int rows_t, int vec_pq, int vec_r) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int pitch = R + 1;
+  DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sQ = sP + Ns * pitch;
+  DGMC_LDS float* sB = sQ + Nt * pitch;
+  DGMC_LDS float* sW = sB + R;
+  DGMC_LDS float* sR = sW + R;
+  DGMC_LDS float* sS = sR + Ns * R;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sh = S_hat + (size_t)b * NN;
+  float pre[kPrefetch];
+  prefetch_tile(Sh, NN, pre);
+  float bw[2] = {0.f, 0.f};
+  if (tid < R) {
+    bw[0] = b1[tid];
+    bw[1] = w2[tid];
+  }
+  stage_rows<TPQ>(sP, P + (size_t)s0 * R, ns, sQ, Q + (size_t)t0 * R, nt,
+                  pitch, R, vec_pq != 0);
+  stage_rows<TR>(sR, r_s + (size_t)s0 * R, ns, sR, r_s, 0, R, R, vec_r != 0);
+  if (tid < R) {
+    sB[tid] = bw[0];
+    sW[tid] = bw[1];
+  }
+  for (int c = tid + kThreads; c < R; c += kThreads) {
+    sB[c] = b1[c];
+    sW[c] = w2[c];
+  }
+#pragma unroll
+  for (int u = 0; u < kPrefetch; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < NN) sS[e] = pre[u];
+  }
+  for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) sS[e] = Sh[e];
+  // Static-batch padding rows: r_t tail zeroed, r_s tail copied (the joint
+  // buffer covers every row of both graphs).
+  if (blockIdx.x == gridDim.x - 1)
+    zero_tail(joint + (size_t)rows_s * R, ptr_t[gridDim.x], rows_t, R);
+  {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t e = (size_t)ptr_s[gridDim.x] * R +
+                    (size_t)blockIdx.x * blockDim.x + tid;
+         e < (size_t)rows_s * R; e += stride)
+      joint[e] = r_s[e];
+  }
+  const float bias2 = b2[0];
+  __syncthreads();
+
+  // 1. consensus update of the valid ns x nt block (kTPE lanes per entry).
+  float* ob = S_new + (size_t)b * NN;
+  const int qd = tid % kTPE;
+  const int pairs = ns * nt;
+  for (int p0 = 0; p0 < pairs; p0 += kThreads / kTPE) {
+    const int p = p0 + tid / kTPE;
+    const bool valid = p < pairs;
+    const int i = valid ? p / nt : 0;
+    const int j = valid ? p - i * nt : 0;
+    const DGMC_LDS float* pr = sP + i * pitch;
+    const DGMC_LDS float* qr = sQ + j * pitch;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int c = qd;
+    for (; c + 3 * kTPE < R; c += 4 * kTPE) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int cc = c + kTPE * u;
+        a[u] = fmaf(fmaxf(pr[cc] + sB[cc] - qr[cc], 0.f), sW[cc], a[u]);
+      }
+    }
+    for (; c < R; c += kTPE)
+      a[0] = fmaf(fmaxf(pr[c] + sB[c] - qr[c], 0.f), sW[c], a[0]);
+    float acc = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+    for (int o = 1; o < kTPE; o <<= 1) acc += __shfl_xor(acc, o);
+    if (valid && qd == 0) sS[i * Nt + j] += acc + bias2;
+  }
+  __syncthreads();
+
+  // 2. Updated tile out (entries outside the valid block pass through) and
+  //    its masked row softmax; each row belongs to one wave, so the in-place
+  //    LDS update is race free.
+  float* Sb = S_prob + (size_t)b * NN;
+  for (int i = wave; i < Ns; i += kWaves) {
+    const float raw = lane < Nt ? sS[i * Nt + lane] : 0.f;
+    if (lane < Nt) ob[i * Nt + lane] = raw;
+    const bool valid = i < ns && lane < nt;
+    const float v = valid ? raw : -INFINITY;
+    const float m = wave_max(v);
+    const float e = valid ? __expf(v - m) : 0.f;
+    const float sum = wave_sum(e);
+    const float pv = valid ? e / sum : 0.f;
+    if (lane < Nt) {
+      Sb[i * Nt + lane] = pv;
+      sS[i * Nt + lane] = pv;
+    }
+  }
+  {
+    TR* dst = joint + (size_t)s0 * R;
+    for (int e = tid; e < ns * R; e += kThreads)
+      dst[e] = Cvt<TR>::from_f(sR[e]);
+  }
+  __syncthreads();
+
+  // 3. transport r_t = S^T r_s (channel-parallel lanes).
+  TR* rt = joint + ((size_t)rows_s + t0) * R;
+  for (int c0 = 0; c0 < R; c0 += kThreads) {
+    const ChanMap cm(c0, R);
+    if (!cm.active) continue;
+    for (int j = cm.r0; j < nt; j += cm.rp) {
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      int i = 0;
+      for (; i + 4 <= ns; i += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          a[u] = fmaf(sS[(i + u) * Nt + j], sR[(i + u) * R + cm.c], a[u]);
+      }
+      for (; i < ns; ++i) a[0] = fmaf(sS[i * Nt + j], sR[i * R + cm.c], a[0]);
+      rt[(size_t)j * R + cm.c] =
+          Cvt<TR>::from_f((a[0] + a[1]) + (a[2] + a[3]));
+    }
+  }
+}
+
+// Backward of the fused step boundary, per pair:
+//   dS_hat' = softmax_bwd(S, r_s g_t^T) + addend          (step l+1 transport
+//             + the next step's identity path)
+//   then the consensus backward of step l with G = dS_hat':
+//   dP, dQ (joint buffer), dw2 / db2 per-pair partials; G is also written
+//   out as the gradient of step l's input S_hat (identity path).
+// LDS: sR, sGt [N][R+1] (phase 1), sP, sQ [N][R] (phase 2), sD [NN],
+//      sB, sW [R], sRed [kThreads].
+template <typename TPQ, typename TR>
+__global__ __launch_bounds__(kThreads) void transport_consensus_bwd_kernel(
+    const float* __restrict__ S, const TR* __restrict__ r_s,
+    const TR* __restrict__ g_t, const float* __restrict__ addend,
+    const TPQ* __restrict__ P, const TPQ* __restrict__ Q,
+    const float* __restrict__ b1, const float* __restrict__ w2,
+    const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
+    float* __restrict__ G_out, TPQ* __restrict__ dP, TPQ* __restrict__ dQ,
+    float* __restrict__ dw2_part, float* __restrict__ db2_part, int Ns,
+    int Nt, int R, int rows_s, int rows_t, int vec_r, int vec_pq) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int pitch = R + 1;
+  DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sGt = sR + Ns * pitch;
+  DGMC_LDS float* sP = sGt + Nt * pitch;
+  DGMC_LDS float* sQ = sP + Ns * R;
+  DGMC_LDS float* sD = sQ + Nt * R;
+  DGMC_LDS float* sB = sD + Ns * Nt;
+  DGMC_LDS float* sW = sB + R;
+  DGMC_LDS float* sRed = sW + R;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sb = S + (size_t)b * NN;
+  constexpr int QMAX = kMaxN / kWaves;
+  float sv[QMAX], av[QMAX];
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int i = wave + q * kWaves;
+    const bool in = i < Ns && lane < Nt;
+    sv[q] = in ? Sb[i * Nt + lane] : 0.f;
+    av[q] = (in && addend) ? addend[(size_t)b * NN + i * Nt + lane] : 0.f;
+  }
+  float bw[2] = {0.f, 0.f};
+  if (tid < R) {
+    bw[0] = b1[tid];
+    bw[1] = w2[tid];
+  }
+  stage_rows<TR>(sR, r_s + (size_t)s0 * R, ns, sGt, g_t + (size_t)t0 * R, nt,
+                 pitch, R, vec_r != 0);
+  stage_rows<TPQ>(sP, P + (size_t)s0 * R, ns, sQ, Q + (size_t)t0 * R, nt, R,
+                  R, vec_pq != 0);
+  if (tid < R) {
+    sB[tid] = bw[0];
+    sW[tid] = bw[1];
+  }
+  for (int c = tid + kThreads; c < R; c += kThreads) {
+    sB[c] = b1[c];
+    sW[c] = w2[c];
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    zero_tail(dP, ptr_s[gridDim.x], rows_s, R);
+    zero_tail(dQ, ptr_t[gridDim.x], rows_t, R);
+  }
+  __syncthreads();
+
+  // Phase 1: dS[i][j] = <r_s[i], g_t[j]> (kTPE lanes per entry).
+  {
+    const int qd = tid % kTPE;
+    const int pairs = ns * nt;
+    for (int p0 = 0; p0 < pairs; p0 += kThreads / kTPE) {
+      const int p = p0 + tid / kTPE;
+      const bool valid = p < pairs;
+      const int i = valid ? p / nt : 0;
+      const int j = valid ? p - i * nt : 0;
+      const DGMC_LDS float* rr = sR + i * pitch;
+      const DGMC_LDS float* gr = sGt + j * pitch;
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      int c = qd;
+      for (; c + 3 * kTPE < R; c += 4 * kTPE) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          a[u] = fmaf(rr[c + kTPE * u], gr[c + kTPE * u], a[u]);
+      }
+      for (; c < R; c += kTPE) a[0] = fmaf(rr[c], gr[c], a[0]);
+      float acc = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+      for (int o = 1; o < kTPE; o <<= 1) acc += __shfl_xor(acc, o);
+      if (valid && qd == 0) sD[i * Nt + j] = acc;
+    }
+  }
+  __syncthreads();
+  // Softmax backward + addend -> G (global: step l's S_hat gradient; LDS:
+  // the consensus backward's upstream tile, masked to the valid block).
+  float* Gb = G_out + (size_t)b * NN;
+  float gsum = 0.f;
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int i = wave + q * kWaves;
+    if (i < Ns) {
+      const bool valid = i < ns && lane < nt;
+      const float d = valid ? sD[i * Nt + lane] : 0.f;
+      const float dot = wave_sum(sv[q] * d);
+      const float gv = sv[q] * (d - dot) + av[q];
+      if (lane < Nt) Gb[i * Nt + lane] = gv;
+      const float gm = valid ? gv : 0.f;
+      gsum += gm;
+      sv[q] = gm;           // kept for the LDS store after the barrier
+    }
+  }
+  __syncthreads();          // every wave has read its sD row
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int i = wave + q * kWaves;
+    if (i < Ns && lane < Nt) sD[i * Nt + lane] = sv[q];
+  }
+  gsum = wave_sum(gsum);
+  if (lane == 0) sRed[wave] = gsum;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kWaves; ++w) t += sRed[w];
+    db2_part[b] = t;
+  }
+
+  // Phase 2: consensus backward with G = sD (as consensus_bwd_kernel).
+  TPQ* dPb = dP + (size_t)s0 * R;
+  TPQ* dQb = dQ + (size_t)t0 * R;
+  for (int c0 = 0; c0 < R; c0 += kThreads) {
+    const ChanMap cm(c0, R);
+    const int c = cm.c;
+    __syncthreads();   // sRed reuse
+    float dw = 0.f;
+    if (cm.active) {
+      const float bias1 = sB[c], w = sW[c];
+      for (int i = cm.r0; i < ns; i += cm.rp) {
+        const float p = sP[i * R + c] + bias1;
+        float dp[4] = {0.f, 0.f, 0.f, 0.f}, dwq[4] = {0.f, 0.f, 0.f, 0.f};
+        int j = 0;
+        for (; j + 4 <= nt; j += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float z = fmaxf(p - sQ[(j + u) * R + c], 0.f);
+            const float gij = sD[i * Nt + j + u];
+            dp[u] += z > 0.f ? gij : 0.f;
+            dwq[u] = fmaf(gij, z, dwq[u]);
+          }
+        }
+        for (; j < nt; ++j) {
+          const float z = fmaxf(p - sQ[j * R + c], 0.f);
+          const float gij = sD[i * Nt + j];
+          dp[0] += z > 0.f ? gij : 0.f;
+          dwq[0] = fmaf(gij, z, dwq[0]);
+        }
+        dw += (dwq[0] + dwq[1]) + (dwq[2] + dwq[3]);
+        dPb[(size_t)i * R + c] =
+            Cvt<TPQ>::from_f(((dp[0] + dp[1]) + (dp[2] + dp[3])) * w);
+      }
+      for (int j = cm.r0; j < nt; j += cm.rp) {
+        const float qv = sQ[j * R + c];
+        float dq[4] = {0.f, 0.f, 0.f, 0.f};
+        int i = 0;
+        for (; i + 4 <= ns; i += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            dq[u] += (sP[(i + u) * R + c] + bias1) - qv > 0.f
+                         ? sD[(i + u) * Nt + j] : 0.f;
+        }
+        for (; i < ns; ++i)
+          dq[0] += (sP[i * R + c] + bias1) - qv > 0.f ? sD[i * Nt + j] : 0.f;
+        dQb[(size_t)j * R + c] =
+            Cvt<TPQ>::from_f(-((dq[0] + dq[1]) + (dq[2] + dq[3])) * w);
+      }
+    }
+    sRed[tid] = dw;
+    __syncthreads();
+    if (tid < cm.cw) {
+      float s = 0.f;
+      for (int r = 0; r < cm.rp; ++r) s += sRed[r * cm.cw + tid];
+      dw2_part[(size_t)b * R + c0 + tid] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host wrappers
 // ---------------------------------------------------------------------------
 static void check_pair_tensor(const at::Tensor& t, const char* name) {
@@ -800,6 +1133,142 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   });
   DGMC_CHECK_LAUNCH();
   return {dP, dQ, dw2, db2};
+}
+
+// Fused consensus update (step l) + softmax transport (step l + 1):
+// returns (S_hat', S = masked_softmax(S_hat'), joint [r_s; S^T r_s]).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
+    const at::Tensor& S_hat, const at::Tensor& P, const at::Tensor& Q,
+    const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
+    const at::Tensor& r_s, const at::Tensor& ptr_s, const at::Tensor& ptr_t,
+    int64_t rows_t) {
+  check_pair_tensor(S_hat, "S_hat");
+  check_packed(P, "P");
+  check_packed(Q, "Q");
+  check_packed(r_s, "r_s");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
+  const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
+  const int R = P.size(1);
+  TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
+  TORCH_CHECK(Q.size(1) == R && Q.scalar_type() == P.scalar_type() &&
+                  r_s.size(1) == R,
+              "dense_consensus_transport: P / Q / r_s widths");
+  TORCH_CHECK(b1.numel() == R && w2.numel() == R && b2.numel() == 1 &&
+                  b1.scalar_type() == at::kFloat &&
+                  w2.scalar_type() == at::kFloat &&
+                  b2.scalar_type() == at::kFloat,
+              "b1/w2/b2 must be fp32");
+  check_ptr(ptr_s, ptr_t, B);
+  const int64_t rows_s = r_s.size(0);
+  at::Tensor S_new = at::empty_like(S_hat);
+  at::Tensor S_prob = at::empty_like(S_hat);
+  at::Tensor joint = at::empty({rows_s + rows_t, R}, r_s.options());
+  if (B == 0) {
+    joint.narrow(0, 0, rows_s).copy_(r_s);
+    joint.narrow(0, rows_s, rows_t).zero_();
+    return {S_new, S_prob, joint};
+  }
+  const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
+  const int vec_r = rows_vec_ok(r_s) ? 1 : 0;
+  TORCH_CHECK(P.scalar_type() == at::kBFloat16 &&
+                  r_s.scalar_type() == at::kBFloat16,
+              "dense_consensus_transport: bf16 P/Q and r_s");
+  using T = __hip_bfloat16;
+  auto kern = consensus_transport_kernel<T, T>;
+  const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +
+                                        2 * (size_t)R + (size_t)Ns * R +
+                                        (size_t)Ns * Nt);
+  hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                     S_hat.data_ptr<float>(),
+                     reinterpret_cast<const T*>(P.data_ptr()),
+                     reinterpret_cast<const T*>(Q.data_ptr()),
+                     b1.data_ptr<float>(), w2.data_ptr<float>(),
+                     b2.data_ptr<float>(),
+                     reinterpret_cast<const T*>(r_s.data_ptr()),
+                     ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
+                     S_new.data_ptr<float>(), S_prob.data_ptr<float>(),
+                     reinterpret_cast<T*>(joint.data_ptr()), Ns, Nt, R,
+                     (int)rows_s, (int)rows_t, vec_pq, vec_r);
+  DGMC_CHECK_LAUNCH();
+  return {S_new, S_prob, joint};
+}
+
+// Backward of dense_consensus_transport: returns (G = total gradient of
+// S_hat' (also the gradient of S_hat through the identity path), dP, dQ,
+// dw2 [B, R] / db2 [B] per-pair partials); dP / dQ live in dpq_out when
+// given ([rows_s + rows_t, R]).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
+dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
+                              const at::Tensor& g_t,
+                              const c10::optional<at::Tensor>& addend,
+                              const at::Tensor& P, const at::Tensor& Q,
+                              const at::Tensor& b1, const at::Tensor& w2,
+                              const at::Tensor& ptr_s, const at::Tensor& ptr_t,
+                              const c10::optional<at::Tensor>& dpq_out) {
+  check_pair_tensor(S_prob, "S");
+  check_packed(r_s, "r_s");
+  check_packed(g_t, "grad r_t");
+  check_packed(P, "P");
+  check_packed(Q, "Q");
+  const float* add = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kFloat &&
+                    addend->is_contiguous() &&
+                    addend->sizes() == S_prob.sizes(),
+                "dense_transport_consensus_bwd: addend fp32 like S");
+    add = addend->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_prob.device());
+  const int B = S_prob.size(0), Ns = S_prob.size(1), Nt = S_prob.size(2);
+  const int R = P.size(1);
+  TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
+  TORCH_CHECK(r_s.size(1) == R && g_t.size(1) == R && Q.size(1) == R &&
+                  r_s.scalar_type() == at::kBFloat16 &&
+                  g_t.scalar_type() == at::kBFloat16 &&
+                  P.scalar_type() == at::kBFloat16 &&
+                  Q.scalar_type() == at::kBFloat16,
+              "dense_transport_consensus_bwd: bf16 r_s / g_t / P / Q of "
+              "width R");
+  TORCH_CHECK(b1.numel() == R && w2.numel() == R, "b1/w2 size");
+  check_ptr(ptr_s, ptr_t, B);
+  at::Tensor dP, dQ;
+  if (dpq_out.has_value() && dpq_out->defined()) {
+    const at::Tensor& d = *dpq_out;
+    TORCH_CHECK(d.is_contiguous() && d.scalar_type() == P.scalar_type() &&
+                    d.size(0) == P.size(0) + Q.size(0) && d.size(1) == R,
+                "dense_transport_consensus_bwd: dpq_out [rows_s + rows_t, R]");
+    dP = d.narrow(0, 0, P.size(0));
+    dQ = d.narrow(0, P.size(0), Q.size(0));
+  } else {
+    dP = at::empty_like(P);
+    dQ = at::empty_like(Q);
+  }
+  at::Tensor G = at::empty_like(S_prob);
+  at::Tensor dw2 = at::empty({B, R}, S_prob.options());
+  at::Tensor db2 = at::empty({B}, S_prob.options());
+  if (B == 0) return {G, dP, dQ, dw2.zero_(), db2.zero_()};
+  const int vec_r = (rows_vec_ok(r_s) && rows_vec_ok(g_t)) ? 1 : 0;
+  const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
+  using T = __hip_bfloat16;
+  auto kern = transport_consensus_bwd_kernel<T, T>;
+  const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +
+                                        (size_t)(Ns + Nt) * R +
+                                        (size_t)Ns * Nt + 2 * (size_t)R +
+                                        kThreads);
+  hipLaunchKernelGGL(kern, dim3(B), dim3(kThreads), lds, stream(),
+                     S_prob.data_ptr<float>(),
+                     reinterpret_cast<const T*>(r_s.data_ptr()),
+                     reinterpret_cast<const T*>(g_t.data_ptr()), add,
+                     reinterpret_cast<const T*>(P.data_ptr()),
+                     reinterpret_cast<const T*>(Q.data_ptr()),
+                     b1.data_ptr<float>(), w2.data_ptr<float>(),
+                     ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(),
+                     G.data_ptr<float>(), reinterpret_cast<T*>(dP.data_ptr()),
+                     reinterpret_cast<T*>(dQ.data_ptr()),
+                     dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R,
+                     (int)P.size(0), (int)Q.size(0), vec_r, vec_pq);
+  DGMC_CHECK_LAUNCH();
+  return {G, dP, dQ, dw2, db2};
 }
 
 }  // namespace dgmc

@@ -370,10 +370,16 @@ class DGMC(torch.nn.Module):
                                                   self.psi_2.final.bias)
                     fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)),
                             steps)
+                pending = None    # (joint, S_hat) from a fused step boundary
                 for step in range(steps):
                     mark('dgmc.consensus_step')
                     r_s = r_all[step]
-                    if joint and PASSTHROUGH and S_hat.requires_grad and \
+                    if pending is not None:
+                        r_joint, S_hat = pending
+                        pending = None
+                        o_s, o_t, o = refine(None, None, r_joint,
+                                             features=fold is not None)
+                    elif joint and PASSTHROUGH and S_hat.requires_grad and \
                             torch.is_grad_enabled():
                         # S_hat feeds the transport AND the update: the
                         # update reads it through the transport's alias, so
@@ -391,9 +397,17 @@ class DGMC(torch.nn.Module):
                         r_t = dense_ops.softmax_transport(S_hat, r_s, lay_s,
                                                           lay_t)
                         o_s, o_t, o = refine(r_s, r_t)
-                    S_hat = dense_ops.consensus_update(
+                    # With the fold, the consensus update also runs the next
+                    # step's softmax transport (one fused per-pair kernel).
+                    nxt = r_all[step + 1] if (fold is not None and joint and
+                                              step + 1 < steps) else None
+                    res = dense_ops.consensus_update(
                         S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o,
-                        w1_fold=fold)
+                        w1_fold=fold, next_r_s=nxt)
+                    if isinstance(res, tuple):
+                        pending = res
+                    else:
+                        S_hat = res
                 if raw:
                     return _RawScores(S_hat_0, S_hat, lay_s, lay_t)
                 S_L = dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)

@@ -22,6 +22,8 @@ per pair entry.  The reference materialises ``D [B, N_s, N_t, R]`` (25 MiB
 per step for PascalVOC shapes); the backward recomputes the ReLU from
 ``P``/``Q``.  Masks come from per-pair node counts.
 """
+import os
+
 import torch
 
 from . import _backend
@@ -32,6 +34,10 @@ from ..runtime import loopgrad
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
+# Consensus update of step l fused with the softmax transport of step l + 1
+# (one per-pair kernel each way); DGMC_AMD_FUSE_STEPS=0 keeps them apart.
+FUSE_STEPS = os.environ.get('DGMC_AMD_FUSE_STEPS', '1') == '1'
+
 
 
 def _hip_ok(x, N_s, N_t):
@@ -295,23 +301,88 @@ class _ConsensusUpdate(torch.autograd.Function):
         if dPQ is not None:
             dP, dQ = dPQ, None
         s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
-        loop = ctx.loop
-        parts = (('b1', dP_rows), ('w2', dw2_part),
-                 ('b2', db2_part.view(-1, 1)))
-        if loop is None:
-            db1, dw2, db2 = [_col_sum(t) for _, t in parts]
-        else:
-            for name, t in parts:
-                loop.keep(name, ctx.idx, t)
-            db1 = dw2 = db2 = None
-            if loop.arrive():
-                db1, dw2, db2 = [_col_sum(loop.kept(n)) for n, _ in parts]
-                loop.release()
+        db1, dw2, db2 = _consensus_param_grads(ctx.loop, ctx.idx, dP_rows,
+                                               dw2_part, db2_part)
         if db1 is not None:
             db1 = db1.to(b1_dt)
             dw2 = dw2.view_as(w2).to(w2_dt)
             db2 = db2.view(b2_shape).to(b2_dt)
         return (grad.to(s_dt), dP, dQ, db1, dw2, db2, None, None, None)
+
+
+class _ConsensusTransport(torch.autograd.Function):
+    """Consensus update of step ``l`` fused with the softmax transport of step
+    ``l + 1`` (``dense_consensus_transport``): returns ``(joint, S_hat')``
+    with ``joint = [r_s; masked_softmax(S_hat')^T r_s]`` for the next psi_2
+    call.  The backward kernel forms S_hat''s total gradient (transport
+    backward + the next step's identity path) and runs the consensus backward
+    on it in the same workgroup."""
+
+    @staticmethod
+    def forward(ctx, S_hat, PQ, split, b1, w2, b2, r_s, ptr_s, ptr_t, rows_t,
+                loop):
+        P, Q = PQ[:split], PQ[split:]
+        S_new, S_prob, joint = _backend.ops().dense_consensus_transport(
+            S_hat.float().contiguous(), P, Q, b1.float().contiguous(),
+            w2.float().contiguous().view(-1), b2.float().contiguous().view(-1),
+            r_s.contiguous(), ptr_s, ptr_t, rows_t)
+        ctx.save_for_backward(S_prob, r_s, P, Q, b1, w2, ptr_s, ptr_t)
+        ctx.meta = (S_hat.dtype, b1.dtype, w2.dtype, b2.dtype, b2.shape)
+        ctx.n_s = r_s.size(0)
+        ctx.loop = loop
+        ctx.idx = loop.register() if loop is not None else None
+        ctx.set_materialize_grads(False)
+        return joint, S_new
+
+    @staticmethod
+    def backward(ctx, g_joint, g_S):
+        S_prob, r_s, P, Q, b1, w2, ptr_s, ptr_t = ctx.saved_tensors
+        R = P.size(1)
+        if g_joint is None:
+            g_t = r_s.new_zeros((Q.size(0), R))
+        else:
+            g_t = g_joint[ctx.n_s:].to(r_s.dtype).contiguous()
+        add = None
+        if g_S is not None:
+            add = g_S.float().contiguous()
+        dPQ = torch.empty((P.size(0) + Q.size(0), R), dtype=P.dtype,
+                          device=P.device)
+        G, dP, _, dw2_part, db2_part = \
+            _backend.ops().dense_transport_consensus_bwd(
+                S_prob, r_s.contiguous(), g_t, add, P, Q,
+                b1.float().contiguous(), w2.float().contiguous().view(-1),
+                ptr_s, ptr_t, dPQ)
+        s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
+        db1, dw2, db2 = _consensus_param_grads(
+            ctx.loop, ctx.idx, dP, dw2_part, db2_part)
+        if db1 is not None:
+            db1 = db1.to(b1_dt)
+            dw2 = dw2.view_as(w2).to(w2_dt)
+            db2 = db2.view(b2_shape).to(b2_dt)
+        return (G.to(s_dt), dPQ, None, db1, dw2, db2, None, None, None, None,
+                None)
+
+
+def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
+    """``(db1, dw2, db2)`` of one consensus use - folded over all loop uses
+    by the use completing the set (``None`` for the others)."""
+    parts = (('b1', dP), ('w2', dw2_part), ('b2', db2_part.view(-1, 1)))
+    if loop is None:
+        return tuple(_col_sum(t) for _, t in parts)
+    for name, t in parts:
+        loop.keep(name, idx, t)
+    if loop.arrive():
+        out = tuple(_col_sum(loop.kept(n)) for n, _ in parts)
+        loop.release()
+        return out
+    return None, None, None
+
+
+def consensus_transport_supported(PQ, r_s, S_hat):
+    B, N_s, N_t = S_hat.shape
+    return (_hip_ok(S_hat, N_s, N_t) and PQ.dtype == torch.bfloat16 and
+            r_s.dtype == torch.bfloat16 and PQ.is_contiguous() and
+            PQ.size(1) == r_s.size(1))
 
 
 class _CatMatmul(torch.autograd.Function):
@@ -397,7 +468,7 @@ def cat_matmul(parts, w_t, lp, key, total):
 
 
 def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
-                     w1_fold=None):
+                     w1_fold=None, next_r_s=None):
     r"""``S_hat + mask * mlp(o_s[:, :, None] - o_t[:, None])`` for packed
     ``o_s [sum N_s, R]`` / ``o_t [sum N_t, R]``.  ``o_joint`` may pass the
     concatenation ``[o_s; o_t]`` (fused encoder output) to compute both
@@ -417,6 +488,13 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
         if parts is not None and cat_matmul_supported(parts, w_t):
             PQ = cat_matmul(parts, w_t, lp, key, total)
             loop = loopgrad.group(('consensus', id(mlp)))
+            if next_r_s is not None and FUSE_STEPS and \
+                    consensus_transport_supported(PQ, next_r_s, S_hat):
+                # (joint input of the next psi_2 call, S_hat')
+                return _ConsensusTransport.apply(
+                    S_hat, PQ, lay_s.num_nodes, lin1.bias, lin2.weight,
+                    lin2.bias, next_r_s, lay_s.ptr, lay_t.ptr,
+                    lay_t.num_nodes, loop)
             return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes,
                                           lin1.bias, lin2.weight, lin2.bias,
                                           lay_s.ptr, lay_t.ptr, loop)

@@ -1006,3 +1006,58 @@ def test_consensus_cat_matmul_matches_formed_concatenation(monkeypatch):
             assert a is None and b is None
             continue
         torch.testing.assert_close(a, b, atol=2e-2, rtol=2e-2)
+
+
+def test_fused_step_boundary_matches_separate_kernels(monkeypatch):
+    """Consensus update + next softmax transport in one kernel (forward and
+    backward) == the separate consensus / transport kernels."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    groups = make_keypoint_datasets(graphs=16, feature_dim=32, seed=6)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 48, seed=4)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(32, 64, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=5).to(DEV)
+    model.eval()
+    assert batcher.load()
+    batch = batcher.materialize()
+
+    def run():
+        torch.manual_seed(1)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            loss, count, correct = model.objective(
+                batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+                batch.x_s_batch, batch.x_t, batch.edge_index_t,
+                batch.edge_attr_t, batch.x_t_batch, batch.y, batch.y_mask)
+        return loss.detach(), correct, torch.autograd.grad(
+            loss, list(model.parameters()), allow_unused=True)
+
+    calls = []
+    real = _backend.ops().dense_consensus_transport
+
+    class _Spy(object):
+        def __getattr__(self, name):
+            if name == 'dense_consensus_transport':
+                def f(*a):
+                    calls.append(1)
+                    return real(*a)
+                return f
+            return getattr(torch.ops.dgmc_amd, name)
+    orig = _backend.ops
+    monkeypatch.setattr(_backend, 'ops', lambda: _Spy())
+    l1, c1, g1 = run()
+    monkeypatch.setattr(_backend, 'ops', orig)
+    assert len(calls) == 4          # 5 steps: 4 fused boundaries
+    monkeypatch.setattr(dense_ops, 'FUSE_STEPS', False)
+    l0, c0, g0 = run()
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=1e-4)
+    assert float(c1) == float(c0)
+    for a, b in zip(g1, g0):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        torch.testing.assert_close(a, b, atol=1e-2, rtol=1e-2)
