@@ -56,6 +56,41 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// DPP lane exchanges (VALU modifiers, no LDS round trip unlike __shfl_xor's
+// ds_bpermute).  CTRL: 0xB1 / 0x4E quad_perm xor 1 / xor 2, 0x141
+// row_half_mirror, 0x140 row_mirror.  Callers keep EXEC full.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                         0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_of(float v, int l) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// Sum over each aligned group of 4 lanes (every lane gets its group's sum).
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  return v + dpp_mov<0x4E>(v);
+}
+// Whole-wave sum / max: DPP within rows of 16, then the 4 row results by
+// readlane (wave-uniform result).
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = quad_sum(v);
+  v += dpp_mov<0x141>(v);
+  v += dpp_mov<0x140>(v);
+  return (lane_of(v, 0) + lane_of(v, 16)) + (lane_of(v, 32) + lane_of(v, 48));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  return fmaxf(fmaxf(lane_of(v, 0), lane_of(v, 16)),
+               fmaxf(lane_of(v, 32), lane_of(v, 48)));
+}
+
 // ---------------------------------------------------------------------------
 // Scalar conversions
 // ---------------------------------------------------------------------------

@@ -880,6 +880,473 @@ __global__ __launch_bounds__(kThreads) void transport_consensus_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Step-boundary kernels for a compile-time width R (32 / 64 / 128, bf16 rows).
+//
+// Same math as consensus_transport_kernel / transport_consensus_bwd_kernel,
+// re-laid out for the LDS pipe (the generic kernels spend most of their time
+// in ds_read_b32 with 4-way bank conflicts):
+//   * (i, j) entry dots use 4 lanes per entry reading 16-byte quads of
+//     channels (ds_read_b128); rows of the entry operands have the pitch
+//     PP = R + ((16 - R) mod 64) dwords, so the 4 entries sharing one b128
+//     lane group fall on disjoint banks for consecutive j;
+//   * b1 / w2 of a lane's channels live in registers;
+//   * channel-parallel loops (transport, dP / dQ) take one channel quad per
+//     lane (b128 row reads, 8-byte bf16 stores);
+//   * quad / wave reductions by DPP (no ds_bpermute);
+//   * all operand loads of a pair issue in one batch, r_s rows are copied to
+//     the joint output from the load registers, and static-batch padding
+//     rows are handled by every workgroup with 16-byte accesses.
+// ---------------------------------------------------------------------------
+namespace {
+typedef __bf16 ps_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 ps_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float ps_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int R>
+struct StepGeom {
+  static constexpr int PP = R + ((16 - R) & 63);   // entry-operand row pitch
+  static constexpr int RU = R / 16;                // b128 quads per lane/entry
+  static constexpr int V8 = R / 8;                 // bf16x8 vectors per row
+  static constexpr int CQ = R / 4;                 // channel quads
+  static constexpr int RG = kThreads / CQ;         // row groups (channel loops)
+};
+
+// One operand block staged by stage_blocks: rows [0, rows) of a packed bf16
+// [*, R] block into an fp32 LDS tile of pitch `pitch`, optionally copied
+// verbatim to `copy` (same row layout).
+struct StageBlk {
+  const __bf16* src;
+  DGMC_LDS float* dst;
+  __bf16* copy;
+  int rows, pitch;
+};
+
+// All loads of up to NB blocks are issued before the first LDS store (one
+// memory round trip for pair-sized blocks).
+template <int R, int NB>
+__device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
+  constexpr int V8 = R / 8;
+  int end[NB];
+  int total = 0;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    total += blk[k].rows * V8;
+    end[k] = total;
+  }
+  for (int base = threadIdx.x; base < total; base += 4 * kThreads) {
+    ps_bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = base + u * kThreads;
+      if (q < total) {
+        int k = 0, q0 = 0;
+#pragma unroll
+        for (int m = 0; m + 1 < NB; ++m)
+          if (q >= end[m]) { k = m + 1; q0 = end[m]; }
+        const __bf16* src = blk[0].src;
+#pragma unroll
+        for (int m = 1; m < NB; ++m) if (k == m) src = blk[m].src;
+        v[u] = *reinterpret_cast<const ps_bf16x8*>(src + (size_t)(q - q0) * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = base + u * kThreads;
+      if (q < total) {
+        int k = 0, q0 = 0;
+#pragma unroll
+        for (int m = 0; m + 1 < NB; ++m)
+          if (q >= end[m]) { k = m + 1; q0 = end[m]; }
+        StageBlk bk = blk[0];
+#pragma unroll
+        for (int m = 1; m < NB; ++m) if (k == m) bk = blk[m];
+        const int qq = q - q0, r = qq / V8, c = (qq - r * V8) * 8;
+        DGMC_LDS ps_f32x4* d =
+            reinterpret_cast<DGMC_LDS ps_f32x4*>(bk.dst + r * bk.pitch + c);
+        d[0] = ps_f32x4{(float)v[u][0], (float)v[u][1], (float)v[u][2],
+                        (float)v[u][3]};
+        d[1] = ps_f32x4{(float)v[u][4], (float)v[u][5], (float)v[u][6],
+                        (float)v[u][7]};
+        if (bk.copy)
+          *reinterpret_cast<ps_bf16x8*>(bk.copy + (size_t)qq * 8) = v[u];
+      }
+    }
+  }
+}
+
+// Static-batch padding rows spread over the whole grid in 16-byte pieces:
+// rows [z0, z1) of zdst zeroed and rows [c0, c1) of csrc copied to cdst.
+template <int R>
+__device__ __forceinline__ void pad_rows(__bf16* zdst, int z0, int z1,
+                                         __bf16* cdst, const __bf16* csrc,
+                                         int c0, int c1) {
+  constexpr int V8 = R / 8;
+  const int nz = (z1 - z0) * V8, nc = cdst ? (c1 - c0) * V8 : 0;
+  const int stride = gridDim.x * blockDim.x;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nz + nc;
+       e += stride) {
+    if (e < nz) {
+      *reinterpret_cast<ps_bf16x8*>(zdst + (size_t)z0 * R + (size_t)e * 8) =
+          ps_bf16x8{};
+    } else {
+      const size_t off = (size_t)c0 * R + (size_t)(e - nz) * 8;
+      *reinterpret_cast<ps_bf16x8*>(cdst + off) =
+          *reinterpret_cast<const ps_bf16x8*>(csrc + off);
+    }
+  }
+}
+
+__device__ __forceinline__ ps_f32x4 lds4(const DGMC_LDS float* p) {
+  return *reinterpret_cast<const DGMC_LDS ps_f32x4*>(p);
+}
+}  // namespace
+
+// Step kernels.  CONS: consensus update (forward) / its backward; TRANS:
+// masked softmax + transport r_t = S^T r_s (forward) / its backward.  Both:
+// the fused step boundary (consensus of step l, transport of step l + 1).
+// Forward LDS: sP, sQ [N][PP] (CONS), sR [Ns][R] (TRANS), sS [Ns][Nt].
+// Outputs: S_new (CONS: the updated S_hat), S_prob (TRANS), rt_out packed
+// [rows_t, R] (TRANS) and, when rs_copy is given, r_s copied into it (the
+// joint psi_2 input [r_s; r_t]).
+template <int R, bool CONS, bool TRANS>
+__global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
+    const float* __restrict__ S_hat, const __bf16* __restrict__ P,
+    const __bf16* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2,
+    const __bf16* __restrict__ r_s, const int* __restrict__ ptr_s,
+    const int* __restrict__ ptr_t, float* __restrict__ S_new,
+    float* __restrict__ S_prob, __bf16* __restrict__ rs_copy,
+    __bf16* __restrict__ rt_out, int Ns, int Nt, int rows_s, int rows_t) {
+  using G = StepGeom<R>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sQ = sP + (CONS ? Ns * G::PP : 0);
+  DGMC_LDS float* sR = sQ + (CONS ? Nt * G::PP : 0);
+  DGMC_LDS float* sS = sR + (TRANS ? Ns * R : 0);
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sh = S_hat + (size_t)b * NN;
+  float pre[kPrefetch];
+  prefetch_tile(Sh, NN, pre);
+  // This lane's channels in the entry loop: 4 qd + 16 u + (0..3).
+  const int qd = tid & 3;
+  ps_f32x4 bv[CONS ? G::RU : 1], wv[CONS ? G::RU : 1];
+  float bias2 = 0.f;
+  if constexpr (CONS) {
+#pragma unroll
+    for (int u = 0; u < G::RU; ++u) {
+      bv[u] = *reinterpret_cast<const ps_f32x4*>(b1 + 4 * qd + 16 * u);
+      wv[u] = *reinterpret_cast<const ps_f32x4*>(w2 + 4 * qd + 16 * u);
+    }
+    bias2 = b2[0];
+  }
+  __bf16* rsc = rs_copy ? rs_copy + (size_t)s0 * R : nullptr;
+  if constexpr (CONS && TRANS) {
+    const StageBlk blk[3] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
+                             {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP},
+                             {r_s + (size_t)s0 * R, sR, rsc, ns, R}};
+    stage_blocks<R, 3>(blk);
+  } else if constexpr (CONS) {
+    const StageBlk blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
+                             {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP}};
+    stage_blocks<R, 2>(blk);
+  } else {
+    const StageBlk blk[1] = {{r_s + (size_t)s0 * R, sR, rsc, ns, R}};
+    stage_blocks<R, 1>(blk);
+  }
+#pragma unroll
+  for (int u = 0; u < kPrefetch; ++u) {
+    const int e = tid + u * kThreads;
+    if (e < NN) sS[e] = pre[u];
+  }
+  for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) sS[e] = Sh[e];
+  if constexpr (TRANS)
+    pad_rows<R>(rt_out, ptr_t[gridDim.x], rows_t, rs_copy, r_s,
+                ptr_s[gridDim.x], rows_s);
+  __syncthreads();
+
+  // 1. consensus update of the valid block: 4 lanes per (i, j) entry.
+  if constexpr (CONS) {
+    const int pairs = ns * nt;
+    for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
+      const int p = p0 + (tid >> 2);
+      const bool valid = p < pairs;
+      const int i = valid ? p / nt : 0;
+      const int j = valid ? p - i * nt : 0;
+      const DGMC_LDS float* pr = sP + i * G::PP + 4 * qd;
+      const DGMC_LDS float* qr = sQ + j * G::PP + 4 * qd;
+      ps_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < G::RU; ++u) {
+        const ps_f32x4 pv = lds4(pr + 16 * u), qv = lds4(qr + 16 * u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          acc[k] =
+              fmaf(fmaxf(pv[k] + bv[u][k] - qv[k], 0.f), wv[u][k], acc[k]);
+      }
+      const float s = quad_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+      if (valid && qd == 0) sS[i * Nt + j] += s + bias2;
+    }
+    __syncthreads();
+  }
+  float* ob = S_new + (size_t)b * NN;
+  if constexpr (!TRANS) {
+    for (int e = tid; e < NN; e += kThreads) ob[e] = sS[e];
+    return;
+  }
+
+  // 2. (updated tile out and) masked row softmax, one wave per row.
+  float* Sb = S_prob + (size_t)b * NN;
+  for (int i = wave; i < Ns; i += kWaves) {
+    const float raw = lane < Nt ? sS[i * Nt + lane] : 0.f;
+    if (CONS && lane < Nt) ob[i * Nt + lane] = raw;
+    const bool valid = i < ns && lane < nt;
+    const float v = valid ? raw : -INFINITY;
+    const float m = wave_max_dpp(v);
+    const float e = valid ? __expf(v - m) : 0.f;
+    const float sum = wave_sum_dpp(e);
+    const float pv = valid ? e / sum : 0.f;
+    if (lane < Nt) {
+      Sb[i * Nt + lane] = pv;
+      sS[i * Nt + lane] = pv;
+    }
+  }
+  __syncthreads();
+
+  // 3. r_t = S^T r_s: one channel quad per lane, two rows j per pass.
+  __bf16* rt = rt_out + (size_t)t0 * R;
+  const int cq = tid % G::CQ, rg = tid / G::CQ;
+  for (int j0 = rg; j0 < nt; j0 += 2 * G::RG) {
+    const int j1 = j0 + G::RG;
+    const bool has1 = j1 < nt;
+    ps_f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < ns; ++i) {
+      const ps_f32x4 rv = lds4(sR + i * R + 4 * cq);
+      const float w0 = sS[i * Nt + j0];
+      const float w1 = has1 ? sS[i * Nt + j1] : 0.f;
+      a0 += w0 * rv;
+      a1 += w1 * rv;
+    }
+    *reinterpret_cast<ps_bf16x4*>(rt + (size_t)j0 * R + 4 * cq) =
+        ps_bf16x4{(__bf16)a0[0], (__bf16)a0[1], (__bf16)a0[2], (__bf16)a0[3]};
+    if (has1)
+      *reinterpret_cast<ps_bf16x4*>(rt + (size_t)j1 * R + 4 * cq) = ps_bf16x4{
+          (__bf16)a1[0], (__bf16)a1[1], (__bf16)a1[2], (__bf16)a1[3]};
+  }
+}
+
+// Backward.  TRANS: dS = softmax_bwd(S, r_s g_t^T) + addend -> G_out (the
+// S_hat' gradient); CONS: the consensus backward with upstream G (TRANS: the
+// G just formed; otherwise `S` is the upstream gradient tile) -> dP, dQ rows
+// and per-pair dw2 / db2 partials.
+// LDS: sR, sGt [N][PP] (TRANS; reused as sRed [RG][R]), sP, sQ [N][R]
+// (CONS), sD [NN], sSum [kWaves].
+template <int R, bool CONS, bool TRANS>
+__global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
+    const float* __restrict__ S, const __bf16* __restrict__ r_s,
+    const __bf16* __restrict__ g_t, const float* __restrict__ addend,
+    const __bf16* __restrict__ P, const __bf16* __restrict__ Q,
+    const float* __restrict__ b1, const float* __restrict__ w2,
+    const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
+    float* __restrict__ G_out, __bf16* __restrict__ dP,
+    __bf16* __restrict__ dQ, float* __restrict__ dw2_part,
+    float* __restrict__ db2_part, int Ns, int Nt, int rows_s, int rows_t) {
+  using G = StepGeom<R>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
+  DGMC_LDS float* sGt = sR + Ns * G::PP;
+  const int region1 = max(TRANS ? (Ns + Nt) * G::PP : 0, CONS ? G::RG * R : 0);
+  DGMC_LDS float* sP = sR + region1;
+  DGMC_LDS float* sQ = sP + (CONS ? Ns * R : 0);
+  DGMC_LDS float* sD = sQ + (CONS ? Nt * R : 0);
+  DGMC_LDS float* sRed = sR;                 // after phase 1
+  DGMC_LDS float* sSum = sD + Ns * Nt;       // [kWaves]
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave, lane = tid % kWave;
+  const int s0 = ptr_s[b], ns = ptr_s[b + 1] - s0;
+  const int t0 = ptr_t[b], nt = ptr_t[b + 1] - t0;
+  const int NN = Ns * Nt;
+  const float* Sb = S + (size_t)b * NN;
+  constexpr int QMAX = kMaxN / kWaves;
+  float sv[TRANS ? QMAX : 1], av[TRANS ? QMAX : 1];
+  float pre[kPrefetch];
+  if constexpr (TRANS) {
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      const int i = wave + q * kWaves;
+      const bool in = i < Ns && lane < Nt;
+      sv[q] = in ? Sb[i * Nt + lane] : 0.f;
+      av[q] = (in && addend) ? addend[(size_t)b * NN + i * Nt + lane] : 0.f;
+    }
+  } else {
+    prefetch_tile(Sb, NN, pre);
+  }
+  const int cq = tid % G::CQ, rg = tid / G::CQ;
+  ps_f32x4 bv = {0.f, 0.f, 0.f, 0.f}, wv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (CONS) {
+    bv = *reinterpret_cast<const ps_f32x4*>(b1 + 4 * cq);
+    wv = *reinterpret_cast<const ps_f32x4*>(w2 + 4 * cq);
+  }
+  if constexpr (CONS && TRANS) {
+    const StageBlk blk[4] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
+                             {g_t + (size_t)t0 * R, sGt, nullptr, nt, G::PP},
+                             {P + (size_t)s0 * R, sP, nullptr, ns, R},
+                             {Q + (size_t)t0 * R, sQ, nullptr, nt, R}};
+    stage_blocks<R, 4>(blk);
+  } else if constexpr (TRANS) {
+    const StageBlk blk[2] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
+                             {g_t + (size_t)t0 * R, sGt, nullptr, nt, G::PP}};
+    stage_blocks<R, 2>(blk);
+  } else {
+    const StageBlk blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, R},
+                             {Q + (size_t)t0 * R, sQ, nullptr, nt, R}};
+    stage_blocks<R, 2>(blk);
+  }
+  float gsum = 0.f;
+  if constexpr (CONS) {
+    pad_rows<R>(dP, ptr_s[gridDim.x], rows_s, nullptr, nullptr, 0, 0);
+    pad_rows<R>(dQ, ptr_t[gridDim.x], rows_t, nullptr, nullptr, 0, 0);
+  }
+  if constexpr (!TRANS) {
+    // Upstream gradient tile, masked to the valid block.
+#pragma unroll
+    for (int u = 0; u < kPrefetch; ++u) {
+      const int e = tid + u * kThreads;
+      if (e < NN) {
+        const int i = e / Nt, j = e - (e / Nt) * Nt;
+        const float v = (i < ns && j < nt) ? pre[u] : 0.f;
+        sD[e] = v;
+        gsum += v;
+      }
+    }
+    for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) {
+      const int i = e / Nt, j = e - (e / Nt) * Nt;
+      const float v = (i < ns && j < nt) ? Sb[e] : 0.f;
+      sD[e] = v;
+      gsum += v;
+    }
+  }
+  __syncthreads();
+
+  if constexpr (TRANS) {
+    // Phase 1: dS[i][j] = <r_s[i], g_t[j]>, 4 lanes per entry.
+    const int qd = tid & 3;
+    const int pairs = ns * nt;
+    for (int p0 = 0; p0 < pairs; p0 += kThreads / 4) {
+      const int p = p0 + (tid >> 2);
+      const bool valid = p < pairs;
+      const int i = valid ? p / nt : 0;
+      const int j = valid ? p - i * nt : 0;
+      const DGMC_LDS float* rr = sR + i * G::PP + 4 * qd;
+      const DGMC_LDS float* gr = sGt + j * G::PP + 4 * qd;
+      ps_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < G::RU; ++u)
+        acc += lds4(rr + 16 * u) * lds4(gr + 16 * u);
+      const float s = quad_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+      if (valid && qd == 0) sD[i * Nt + j] = s;
+    }
+    __syncthreads();
+    // Softmax backward + addend -> G (global) and, for CONS, the masked
+    // upstream tile of the consensus backward (LDS, after the barrier).
+    float* Gb = G_out + (size_t)b * NN;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      const int i = wave + q * kWaves;
+      if (i < Ns) {
+        const bool valid = i < ns && lane < nt;
+        const float d = valid ? sD[i * Nt + lane] : 0.f;
+        const float dot = wave_sum_dpp(sv[q] * d);
+        const float gv = sv[q] * (d - dot) + av[q];
+        if (lane < Nt) Gb[i * Nt + lane] = gv;
+        const float gm = valid ? gv : 0.f;
+        gsum += gm;
+        sv[q] = gm;
+      }
+    }
+    if constexpr (!CONS) return;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      const int i = wave + q * kWaves;
+      if (i < Ns && lane < Nt) sD[i * Nt + lane] = sv[q];
+    }
+  }
+  gsum = wave_sum_dpp(gsum);
+  if (lane == 0) sSum[wave] = gsum;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kWaves; ++w) t += sSum[w];
+    db2_part[b] = t;
+  }
+
+  // Phase 2: dP / dQ rows (one channel quad per lane), dw2 partials.
+  ps_f32x4 dw = {0.f, 0.f, 0.f, 0.f};
+  for (int r = rg; r < ns + nt; r += G::RG) {
+    ps_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (r < ns) {
+      const int i = r;
+      const ps_f32x4 pv = lds4(sP + i * R + 4 * cq) + bv;
+      for (int j = 0; j < nt; ++j) {
+        const ps_f32x4 qv = lds4(sQ + j * R + 4 * cq);
+        const float g = sD[i * Nt + j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float z = fmaxf(pv[k] - qv[k], 0.f);
+          acc[k] += z > 0.f ? g : 0.f;
+          dw[k] = fmaf(g, z, dw[k]);
+        }
+      }
+      acc *= wv;
+      *reinterpret_cast<ps_bf16x4*>(dP + ((size_t)s0 + i) * R + 4 * cq) =
+          ps_bf16x4{(__bf16)acc[0], (__bf16)acc[1], (__bf16)acc[2],
+                    (__bf16)acc[3]};
+    } else {
+      const int j = r - ns;
+      const ps_f32x4 qv = lds4(sQ + j * R + 4 * cq);
+      for (int i = 0; i < ns; ++i) {
+        const ps_f32x4 pv = lds4(sP + i * R + 4 * cq) + bv;
+        const float g = sD[i * Nt + j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += pv[k] - qv[k] > 0.f ? g : 0.f;
+      }
+      acc *= -wv;
+      *reinterpret_cast<ps_bf16x4*>(dQ + ((size_t)t0 + j) * R + 4 * cq) =
+          ps_bf16x4{(__bf16)acc[0], (__bf16)acc[1], (__bf16)acc[2],
+                    (__bf16)acc[3]};
+    }
+  }
+  *reinterpret_cast<DGMC_LDS ps_f32x4*>(sRed + rg * R + 4 * cq) = dw;
+  __syncthreads();
+  for (int c = tid; c < R; c += kThreads) {
+    float s = 0.f;
+    for (int r = 0; r < G::RG; ++r) s += sRed[r * R + c];
+    dw2_part[(size_t)b * R + c] = s;
+  }
+}
+
+// LDS floats of the step kernels.
+template <int R>
+static size_t step_fwd_lds(bool cons, bool trans, int Ns, int Nt) {
+  using G = StepGeom<R>;
+  return (cons ? (size_t)(Ns + Nt) * G::PP : 0) +
+         (trans ? (size_t)Ns * R : 0) + (size_t)Ns * Nt;
+}
+template <int R>
+static size_t step_bwd_lds(bool cons, bool trans, int Ns, int Nt) {
+  using G = StepGeom<R>;
+  return (size_t)std::max(trans ? (Ns + Nt) * G::PP : 0,
+                          cons ? G::RG * R : 0) +
+         (cons ? (size_t)(Ns + Nt) * R : 0) + (size_t)Ns * Nt + kWaves;
+}
+
+// ---------------------------------------------------------------------------
 // Host wrappers
 // ---------------------------------------------------------------------------
 static void check_pair_tensor(const at::Tensor& t, const char* name) {
@@ -924,6 +1391,87 @@ static size_t pair_lds(K kern, size_t floats) {
         reinterpret_cast<const void*>(kern),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
   return bytes;
+}
+
+// Compile-time-width step kernels (pair_step_fwd/bwd_kernel): R in
+// {32, 64, 128}, 16-byte aligned bf16 operand rows, aligned fp32 b1 / w2.
+// DGMC_PAIR_FAST=0 selects the generic kernels (A/B switch).
+static bool fast_step_ok(int R, std::initializer_list<const at::Tensor*> rows,
+                         std::initializer_list<const void*> vecs = {}) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("DGMC_PAIR_FAST");
+    return !(e && e[0] == '0');
+  }();
+  if (!enabled || !(R == 32 || R == 64 || R == 128)) return false;
+  for (const at::Tensor* t : rows)
+    if (t->scalar_type() != at::kBFloat16 || !rows_vec_ok(*t)) return false;
+  for (const void* v : vecs)
+    if (!aligned16(v)) return false;
+  return true;
+}
+
+static __bf16* bf16_ptr(const at::Tensor& t) {
+  return reinterpret_cast<__bf16*>(t.data_ptr());
+}
+
+struct StepFwdArgs {
+  const float* S_hat;
+  const __bf16 *P, *Q;
+  const float *b1, *w2, *b2;
+  const __bf16* r_s;
+  const int *ptr_s, *ptr_t;
+  float *S_new, *S_prob;
+  __bf16 *rs_copy, *rt_out;
+  int B, Ns, Nt, rows_s, rows_t;
+};
+
+struct StepBwdArgs {
+  const float* S;
+  const __bf16 *r_s, *g_t;
+  const float* addend;
+  const __bf16 *P, *Q;
+  const float *b1, *w2;
+  const int *ptr_s, *ptr_t;
+  float* G_out;
+  __bf16 *dP, *dQ;
+  float *dw2_part, *db2_part;
+  int B, Ns, Nt, rows_s, rows_t;
+};
+
+template <int R, bool C, bool T>
+static void step_fwd_launch(const StepFwdArgs& a) {
+  auto kern = pair_step_fwd_kernel<R, C, T>;
+  const size_t lds = pair_lds(kern, step_fwd_lds<R>(C, T, a.Ns, a.Nt));
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S_hat,
+                     a.P, a.Q, a.b1, a.w2, a.b2, a.r_s, a.ptr_s, a.ptr_t,
+                     a.S_new, a.S_prob, a.rs_copy, a.rt_out, a.Ns, a.Nt,
+                     a.rows_s, a.rows_t);
+  DGMC_CHECK_LAUNCH();
+}
+
+template <int R, bool C, bool T>
+static void step_bwd_launch(const StepBwdArgs& a) {
+  auto kern = pair_step_bwd_kernel<R, C, T>;
+  const size_t lds = pair_lds(kern, step_bwd_lds<R>(C, T, a.Ns, a.Nt));
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S,
+                     a.r_s, a.g_t, a.addend, a.P, a.Q, a.b1, a.w2, a.ptr_s,
+                     a.ptr_t, a.G_out, a.dP, a.dQ, a.dw2_part, a.db2_part,
+                     a.Ns, a.Nt, a.rows_s, a.rows_t);
+  DGMC_CHECK_LAUNCH();
+}
+
+template <bool C, bool T>
+static void step_fwd(int R, const StepFwdArgs& a) {
+  if (R == 32) step_fwd_launch<32, C, T>(a);
+  else if (R == 64) step_fwd_launch<64, C, T>(a);
+  else step_fwd_launch<128, C, T>(a);
+}
+
+template <bool C, bool T>
+static void step_bwd(int R, const StepBwdArgs& a) {
+  if (R == 32) step_bwd_launch<32, C, T>(a);
+  else if (R == 64) step_bwd_launch<64, C, T>(a);
+  else step_bwd_launch<128, C, T>(a);
 }
 
 at::Tensor dense_masked_softmax(const at::Tensor& S_hat, const at::Tensor& n_s,
@@ -986,6 +1534,15 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     if (joint_out) joint.narrow(0, 0, rows_s).copy_(r_s);
     return {S, joint_out ? joint : r_t};
   }
+  if (fast_step_ok(R, {&r_s})) {
+    StepFwdArgs a{S_hat.data_ptr<float>(), nullptr, nullptr, nullptr,
+                  nullptr, nullptr, bf16_ptr(r_s), ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), nullptr, S.data_ptr<float>(),
+                  joint_out ? bf16_ptr(joint) : nullptr, bf16_ptr(r_t), B, Ns,
+                  Nt, (int)rows_s, (int)rows_t};
+    step_fwd<false, true>(R, a);
+    return {S, joint_out ? joint : r_t};
+  }
   const int vec = rows_vec_ok(r_s) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
     auto kern = softmax_transport_kernel<T>;
@@ -1030,6 +1587,15 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S);
   if (B == 0) return out;
+  if (fast_step_ok(R, {&r_s, &g})) {
+    StepBwdArgs a{S.data_ptr<float>(), bf16_ptr(r_s), bf16_ptr(g), add,
+                  nullptr, nullptr, nullptr, nullptr, ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), out.data_ptr<float>(), nullptr,
+                  nullptr, nullptr, nullptr, B, Ns, Nt, (int)r_s.size(0),
+                  (int)g.size(0)};
+    step_bwd<false, true>(R, a);
+    return out;
+  }
   const int vec = (rows_vec_ok(r_s) && rows_vec_ok(g)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(r_s.scalar_type(), T, [&] {
     auto kern = softmax_transport_bwd_kernel<T>;
@@ -1067,6 +1633,17 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor out = at::empty_like(S_hat);
   if (B == 0) return out;
+  if (fast_step_ok(R, {&P, &Q}, {b1.data_ptr(), w2.data_ptr()}) &&
+      b1.is_contiguous() && w2.is_contiguous()) {
+    StepFwdArgs a{S_hat.data_ptr<float>(), bf16_ptr(P), bf16_ptr(Q),
+                  b1.data_ptr<float>(), w2.data_ptr<float>(),
+                  b2.data_ptr<float>(), nullptr, ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), out.data_ptr<float>(), nullptr,
+                  nullptr, nullptr, B, Ns, Nt, (int)P.size(0),
+                  (int)Q.size(0)};
+    step_fwd<true, false>(R, a);
+    return out;
+  }
   const int vec = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
     auto kern = consensus_fwd_kernel<T>;
@@ -1114,6 +1691,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   at::Tensor dw2 = at::empty({B, R}, G.options());
   at::Tensor db2 = at::empty({B}, G.options());
   if (B == 0) return {dP, dQ, dw2.zero_(), db2.zero_()};
+  if (fast_step_ok(R, {&P, &Q, &dP, &dQ}, {b1.data_ptr(), w2.data_ptr()}) &&
+      b1.is_contiguous() && w2.is_contiguous()) {
+    StepBwdArgs a{G.data_ptr<float>(), nullptr, nullptr, nullptr,
+                  bf16_ptr(P), bf16_ptr(Q), b1.data_ptr<float>(),
+                  w2.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), nullptr, bf16_ptr(dP), bf16_ptr(dQ),
+                  dw2.data_ptr<float>(), db2.data_ptr<float>(), B, Ns, Nt,
+                  (int)P.size(0), (int)Q.size(0)};
+    step_bwd<true, false>(R, a);
+    return {dP, dQ, dw2, db2};
+  }
   const int vec = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
     auto kern = consensus_bwd_kernel<T>;
@@ -1173,6 +1761,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
   TORCH_CHECK(P.scalar_type() == at::kBFloat16 &&
                   r_s.scalar_type() == at::kBFloat16,
               "dense_consensus_transport: bf16 P/Q and r_s");
+  if (fast_step_ok(R, {&P, &Q, &r_s}, {b1.data_ptr(), w2.data_ptr()})) {
+    StepFwdArgs a{S_hat.data_ptr<float>(), bf16_ptr(P), bf16_ptr(Q),
+                  b1.data_ptr<float>(), w2.data_ptr<float>(),
+                  b2.data_ptr<float>(), bf16_ptr(r_s), ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), S_new.data_ptr<float>(),
+                  S_prob.data_ptr<float>(), bf16_ptr(joint),
+                  bf16_ptr(joint) + rows_s * R, B, Ns, Nt, (int)rows_s,
+                  (int)rows_t};
+    step_fwd<true, true>(R, a);
+    return {S_new, S_prob, joint};
+  }
   using T = __hip_bfloat16;
   auto kern = consensus_transport_kernel<T, T>;
   const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +
@@ -1249,6 +1848,17 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
   if (B == 0) return {G, dP, dQ, dw2.zero_(), db2.zero_()};
   const int vec_r = (rows_vec_ok(r_s) && rows_vec_ok(g_t)) ? 1 : 0;
   const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
+  if (fast_step_ok(R, {&r_s, &g_t, &P, &Q, &dP, &dQ},
+                   {b1.data_ptr(), w2.data_ptr()})) {
+    StepBwdArgs a{S_prob.data_ptr<float>(), bf16_ptr(r_s), bf16_ptr(g_t), add,
+                  bf16_ptr(P), bf16_ptr(Q), b1.data_ptr<float>(),
+                  w2.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                  ptr_t.data_ptr<int>(), G.data_ptr<float>(), bf16_ptr(dP),
+                  bf16_ptr(dQ), dw2.data_ptr<float>(), db2.data_ptr<float>(),
+                  B, Ns, Nt, (int)P.size(0), (int)Q.size(0)};
+    step_bwd<true, true>(R, a);
+    return {G, dP, dQ, dw2, db2};
+  }
   using T = __hip_bfloat16;
   auto kern = transport_consensus_bwd_kernel<T, T>;
   const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +

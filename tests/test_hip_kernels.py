@@ -1061,3 +1061,143 @@ def test_fused_step_boundary_matches_separate_kernels(monkeypatch):
             assert a is None and b is None
             continue
         torch.testing.assert_close(a, b, atol=1e-2, rtol=1e-2)
+
+
+def _step_problem(R, Ns, Nt, B):
+    torch.manual_seed(R + Ns)
+    c_s = torch.randint(1, Ns + 1, (B, ))
+    c_t = torch.randint(1, Nt + 1, (B, ))
+    c_s[0], c_t[0] = Ns, Nt
+    pad_s, pad_t = 5, 7
+    ptr_s = torch.zeros(B + 1, dtype=torch.int32)
+    ptr_t = torch.zeros(B + 1, dtype=torch.int32)
+    ptr_s[1:], ptr_t[1:] = c_s.cumsum(0), c_t.cumsum(0)
+    rows_s, rows_t = int(ptr_s[-1]) + pad_s, int(ptr_t[-1]) + pad_t
+    bf = torch.bfloat16
+    d = dict(
+        R=R, c_s=c_s, c_t=c_t, ptr_s=ptr_s, ptr_t=ptr_t, rows_s=rows_s,
+        rows_t=rows_t, ps=ptr_s.to(DEV), pt=ptr_t.to(DEV),
+        P=torch.randn(rows_s, R, device=DEV).to(bf),
+        Q=torch.randn(rows_t, R, device=DEV).to(bf),
+        r_s=torch.randn(rows_s, R, device=DEV).to(bf),
+        b1=torch.randn(R, device=DEV) * 0.5,
+        w2=torch.randn(R, device=DEV) / R ** 0.5,
+        b2=torch.randn(1, device=DEV),
+        S_hat=torch.randn(B, Ns, Nt, device=DEV),
+        g_t=torch.randn(rows_t, R, device=DEV).to(bf),
+        add=torch.randn(B, Ns, Nt, device=DEV))
+    ii, jj = torch.arange(Ns), torch.arange(Nt)
+    d['mask'] = ((ii[None, :, None] < c_s[:, None, None]) &
+                 (jj[None, None, :] < c_t[:, None, None])).to(DEV)
+    d['idx_s'] = (ptr_s[:-1, None] + ii[None]).clamp(max=rows_s - 1).to(DEV)
+    d['idx_t'] = (ptr_t[:-1, None] + jj[None]).clamp(max=rows_t - 1).to(DEV)
+    d['vs'] = (ii[None] < c_s[:, None]).to(DEV)
+    d['vt'] = (jj[None] < c_t[:, None]).to(DEV)
+    return d
+
+
+def _step_ref(d, cons, trans):
+    """fp32 autograd reference: S_new (cons), S_prob / r_t (trans), and the
+    gradients of <r_t, g_t> + <S_new, addend> (or <S_new, addend> alone)."""
+    Pf = d['P'].float().requires_grad_()
+    Qf = d['Q'].float().requires_grad_()
+    b1f, w2f, b2f = (d[k].clone().requires_grad_() for k in ('b1', 'w2',
+                                                           'b2'))
+    Sf = d['S_hat'].clone().requires_grad_()
+    mask, vs, vt = d['mask'], d['vs'], d['vt']
+    Sn = Sf
+    if cons:
+        h = torch.relu(Pf[d['idx_s']][:, :, None] + b1f -
+                       Qf[d['idx_t']][:, None, :])
+        Sn = Sf + mask * (h @ w2f + b2f)
+    out = {'S_new': Sn}
+    loss = (Sn * d['add']).sum()
+    if trans:
+        Sm = Sn.masked_fill(~mask, float('-inf')).masked_fill(
+            ~vs[..., None], 0.0)
+        Sp = torch.softmax(Sm, -1) * mask
+        rsd = d['r_s'].float()[d['idx_s']] * vs[..., None]
+        rt = Sp.transpose(1, 2) @ rsd
+        loss = loss + (rt * (d['g_t'].float()[d['idx_t']] *
+                             vt[..., None])).sum()
+        rt_packed = torch.zeros(d['rows_t'], d['R'], device=DEV)
+        rt_packed[d['idx_t'][vt]] = rt.detach()[vt]
+        out.update(S_prob=Sp, r_t=rt_packed)
+    grads = torch.autograd.grad(loss, (Sf, Pf, Qf, b1f, w2f, b2f),
+                                allow_unused=True)
+    out.update(zip(('gS', 'gP', 'gQ', 'gb1', 'gw2', 'gb2'), grads))
+    return out
+
+
+def _check_cons_grads(d, ref, dP, dQ, dw2, db2):
+    n_s, n_t = int(d['ptr_s'][-1]), int(d['ptr_t'][-1])
+    torch.testing.assert_close(dP.float(), ref['gP'], atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(dQ.float(), ref['gQ'], atol=3e-2, rtol=2e-2)
+    assert (dP[n_s:] == 0).all() and (dQ[n_t:] == 0).all()
+    torch.testing.assert_close(dw2.sum(0), ref['gw2'], atol=2e-3, rtol=1e-3)
+    torch.testing.assert_close(db2.sum(), ref['gb2'][0], atol=2e-3,
+                               rtol=1e-3)
+
+
+@pytest.mark.parametrize('R', [32, 64, 128, 48])
+@pytest.mark.parametrize('Ns,Nt,B', [(19, 23, 37), (64, 64, 3), (9, 9, 300)])
+def test_step_boundary_kernels_vs_fp32(R, Ns, Nt, B):
+    """dense_consensus_transport / dense_transport_consensus_bwd (the
+    compile-time-R kernels for R in 32/64/128, the generic ones otherwise)
+    against autograd on the fp32 dense expression, incl. the static-batch
+    padding rows of both graphs."""
+    ops = _backend.ops()
+    d = _step_problem(R, Ns, Nt, B)
+    S_new, S_prob, joint = ops.dense_consensus_transport(
+        d['S_hat'], d['P'], d['Q'], d['b1'], d['w2'], d['b2'], d['r_s'],
+        d['ps'], d['pt'], d['rows_t'])
+    G, dP, dQ, dw2, db2 = ops.dense_transport_consensus_bwd(
+        S_prob, d['r_s'], d['g_t'], d['add'], d['P'], d['Q'], d['b1'],
+        d['w2'], d['ps'], d['pt'], None)
+    ref = _step_ref(d, True, True)
+    rows_s = d['rows_s']
+    torch.testing.assert_close(S_new, ref['S_new'].detach(), atol=1e-4,
+                               rtol=1e-4)
+    torch.testing.assert_close(S_prob, ref['S_prob'].detach(), atol=1e-5,
+                               rtol=1e-4)
+    assert torch.equal(joint[:rows_s], d['r_s'])
+    torch.testing.assert_close(joint[rows_s:].float(), ref['r_t'], atol=2e-2,
+                               rtol=1e-2)
+    assert (joint[rows_s + int(d['ptr_t'][-1]):] == 0).all()
+    torch.testing.assert_close(G, ref['gS'], atol=1e-3, rtol=1e-3)
+    _check_cons_grads(d, ref, dP, dQ, dw2, db2)
+
+
+@pytest.mark.parametrize('R', [32, 128, 48])
+@pytest.mark.parametrize('Ns,Nt,B', [(19, 23, 37), (64, 64, 3)])
+def test_step_kernels_split_vs_fp32(R, Ns, Nt, B):
+    """The consensus-only and transport-only step kernels (first / last
+    consensus step) against the same fp32 reference."""
+    ops = _backend.ops()
+    d = _step_problem(R, Ns, Nt, B)
+    # consensus only
+    ref = _step_ref(d, True, False)
+    out = ops.dense_consensus(d['S_hat'], d['P'], d['Q'], d['b1'], d['w2'],
+                              d['b2'], d['ps'], d['pt'])
+    torch.testing.assert_close(out, ref['S_new'].detach(), atol=1e-4,
+                               rtol=1e-4)
+    dP, dQ, dw2, db2 = ops.dense_consensus_bwd(
+        d['add'], d['P'], d['Q'], d['b1'], d['w2'], d['ps'], d['pt'], None)
+    _check_cons_grads(d, ref, dP, dQ, dw2, db2)
+    # transport only (plain and joint output)
+    ref = _step_ref(d, False, True)
+    rows_s = d['rows_s']
+    for joint in (False, True):
+        S, r = ops.dense_softmax_transport(d['S_hat'], d['r_s'], d['ps'],
+                                           d['pt'], d['rows_t'], joint)
+        torch.testing.assert_close(S, ref['S_prob'].detach(), atol=1e-5,
+                                   rtol=1e-4)
+        if joint:
+            assert torch.equal(r[:rows_s], d['r_s'])
+            r = r[rows_s:]
+        torch.testing.assert_close(r.float(), ref['r_t'], atol=2e-2,
+                                   rtol=1e-2)
+        assert (r[int(d['ptr_t'][-1]):] == 0).all()
+    g = ops.dense_softmax_transport_bwd(S, d['r_s'], d['g_t'], d['ps'],
+                                        d['pt'], d['add'])
+    torch.testing.assert_close(g, ref['gS'], atol=1e-3, rtol=1e-3)

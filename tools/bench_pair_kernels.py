@@ -57,6 +57,10 @@ def main():
             S_hat, r_s, ptr, ptr, rows, True))
         t['trans_bwd'] = timeit(lambda: ops.dense_softmax_transport_bwd(
             S, r_s, r_t, ptr, ptr))
+        t['fused_fwd'] = timeit(lambda: ops.dense_consensus_transport(
+            S_hat, P, Q, b1, w2, b2, r_s, ptr, ptr, rows))
+        t['fused_bwd'] = timeit(lambda: ops.dense_transport_consensus_bwd(
+            S, r_s, r_t, G, P, Q, b1, w2, ptr, ptr, None))
         t['empty_like'] = timeit(lambda: torch.empty_like(S_hat).fill_(0))
         print('B=%5d ' % B + ' '.join('%s=%.1fus' % kv for kv in t.items()),
               flush=True)
