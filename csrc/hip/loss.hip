@@ -149,14 +149,18 @@ __global__ __launch_bounds__(256) void nll_bwd_kernel(
 // ---------------------------------------------------------------------------
 constexpr int kSnWaves = 4;
 
+// Blocks [0, nb) read tile S_hat, blocks [nb, 2 nb) the optional second
+// tile S_hat2 (the objective's two outputs S_L and S_0 in one launch).
 __global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_fwd_kernel(
-    const float* __restrict__ S_hat, const int* __restrict__ ptr_s,
-    const int* __restrict__ n_t, const int64_t* __restrict__ y,
-    const bool* __restrict__ mask, float* __restrict__ part, int B, int Ns,
-    int Nt, float eps) {
+    const float* __restrict__ S_hat1, const float* __restrict__ S_hat2,
+    const int* __restrict__ ptr_s, const int* __restrict__ n_t,
+    const int64_t* __restrict__ y, const bool* __restrict__ mask,
+    float* __restrict__ part, int B, int Ns, int Nt, int nb, float eps) {
   __shared__ float red[kSnWaves][3];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int row = blockIdx.x * kSnWaves + wave;     // dense row b * Ns + i
+  const bool second = (int)blockIdx.x >= nb;
+  const float* __restrict__ S_hat = second ? S_hat2 : S_hat1;
+  const int row = (blockIdx.x - (second ? nb : 0)) * kSnWaves + wave;
   float l = 0.f, c = 0.f, k = 0.f;
   if (row < B * Ns) {
     const int b = row / Ns, i = row - b * Ns;
@@ -200,36 +204,61 @@ __global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_fwd_kernel(
   }
 }
 
-// Fixed-order fold of the block partials: loss (mean over counted rows),
-// aux = [count, correct].
+// Fixed-order fold of the block partials: loss = sum over tiles of the mean
+// over counted rows, aux = [count, correct] of the first tile and the
+// second tile's count.  ``stats`` (optional, fp64): += [loss, correct,
+// count] (the trainer's running sums, no extra kernels).
 __global__ __launch_bounds__(kLossThreads) void softmax_nll_fold_kernel(
-    const float* __restrict__ part, int nblocks, float* __restrict__ loss,
-    float* __restrict__ aux) {
+    const float* __restrict__ part, int nblocks, int tiles,
+    float* __restrict__ loss, float* __restrict__ aux,
+    double* __restrict__ stats) {
   __shared__ float red[kLossThreads / kWave];
-  float a = 0.f, c = 0.f, k = 0.f;
-  for (int i = threadIdx.x; i < nblocks; i += kLossThreads) {
-    a += part[3 * i];
-    c += part[3 * i + 1];
-    k += part[3 * i + 2];
+  float total = 0.f, c0 = 0.f, k0 = 0.f, c1 = 0.f;
+  for (int tile = 0; tile < tiles; ++tile) {
+    const float* pt = part + (size_t)tile * nblocks * 3;
+    float a = 0.f, c = 0.f, k = 0.f;
+    for (int i = threadIdx.x; i < nblocks; i += kLossThreads) {
+      a += pt[3 * i];
+      c += pt[3 * i + 1];
+      k += pt[3 * i + 2];
+    }
+    a = block_sum(a, red);
+    c = block_sum(c, red);
+    k = block_sum(k, red);
+    total += a / fmaxf(c, 1.f);
+    if (tile == 0) {
+      c0 = c;
+      k0 = k;
+    } else {
+      c1 = c;
+    }
   }
-  a = block_sum(a, red);
-  c = block_sum(c, red);
-  k = block_sum(k, red);
   if (threadIdx.x == 0) {
-    loss[0] = a / fmaxf(c, 1.f);
-    aux[0] = c;
-    aux[1] = k;
+    loss[0] = total;
+    aux[0] = c0;
+    aux[1] = k0;
+    aux[2] = c1;
+    if (stats) {
+      stats[0] += (double)total;
+      stats[1] += (double)k0;
+      stats[2] += (double)c0;
+    }
   }
 }
 
 __global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_bwd_kernel(
-    const float* __restrict__ grad, const float* __restrict__ S_hat,
-    const int* __restrict__ ptr_s, const int* __restrict__ n_t,
-    const int64_t* __restrict__ y, const bool* __restrict__ mask,
-    const float* __restrict__ aux, float* __restrict__ dS, int B, int Ns,
-    int Nt, float eps) {
+    const float* __restrict__ grad, const float* __restrict__ S_hat1,
+    const float* __restrict__ S_hat2, const int* __restrict__ ptr_s,
+    const int* __restrict__ n_t, const int64_t* __restrict__ y,
+    const bool* __restrict__ mask, const float* __restrict__ aux,
+    float* __restrict__ dS1, float* __restrict__ dS2, int B, int Ns, int Nt,
+    int nb, float eps) {
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-  const int row = blockIdx.x * kSnWaves + wave;
+  const bool second = (int)blockIdx.x >= nb;
+  const float* __restrict__ S_hat = second ? S_hat2 : S_hat1;
+  float* __restrict__ dS = second ? dS2 : dS1;
+  const float count = second ? aux[2] : aux[0];
+  const int row = (blockIdx.x - (second ? nb : 0)) * kSnWaves + wave;
   if (row >= B * Ns) return;
   const int b = row / Ns, i = row - b * Ns;
   const int r = ptr_s[b] + i;
@@ -251,7 +280,7 @@ __global__ __launch_bounds__(kSnWaves * 64) void softmax_nll_bwd_kernel(
   s = wave_sum(s);
   const float inv = 1.f / s;
   const float st = __expf(src[t] - m) * inv;
-  const float dy = -grad[0] / ((st + eps) * fmaxf(aux[0], 1.f));
+  const float dy = -grad[0] / ((st + eps) * fmaxf(count, 1.f));
   for (int j = lane; j < Nt; j += kWave) {
     float v = 0.f;
     if (j < nt) {
@@ -460,57 +489,87 @@ void check_snll(const at::Tensor& S_hat, const at::Tensor& ptr_s,
 }
 }  // namespace
 
+// loss = NLL(S_hat) [+ NLL(S_hat2)], aux = [count, correct, count2]; the
+// optional fp64 ``stats`` receives += [loss, correct, count].
 std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
-    const at::Tensor& S_hat, const at::Tensor& ptr_s, const at::Tensor& n_t,
-    const at::Tensor& y, const c10::optional<at::Tensor>& mask, double eps) {
+    const at::Tensor& S_hat, const c10::optional<at::Tensor>& S_hat2,
+    const at::Tensor& ptr_s, const at::Tensor& n_t, const at::Tensor& y,
+    const c10::optional<at::Tensor>& mask, double eps,
+    const c10::optional<at::Tensor>& stats) {
   check_snll(S_hat, ptr_s, n_t, y, mask);
+  const bool two = S_hat2.has_value() && S_hat2->defined();
+  if (two)
+    TORCH_CHECK(S_hat2->sizes() == S_hat.sizes() &&
+                    S_hat2->scalar_type() == at::kFloat &&
+                    S_hat2->is_contiguous(),
+                "softmax_nll: S_hat2 like S_hat");
+  double* sp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= 3 &&
+                    stats->is_contiguous() && stats->device() == S_hat.device(),
+                "softmax_nll: stats fp64 [>= 3] on the device");
+    sp = stats->data_ptr<double>();
+  }
   const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
   auto opt = S_hat.options();
   at::Tensor loss = at::empty({}, opt);
-  at::Tensor aux = at::empty({2}, opt);
+  at::Tensor aux = at::empty({3}, opt);
   const int rows = B * Ns;
   const int nblocks = std::max(1, (rows + kSnWaves - 1) / kSnWaves);
-  at::Tensor part = at::empty({nblocks * 3}, opt);
+  const int tiles = two ? 2 : 1;
+  at::Tensor part = at::empty({tiles * nblocks * 3}, opt);
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   const bool* mp = (mask.has_value() && mask->defined())
                        ? mask->data_ptr<bool>() : nullptr;
-  hipLaunchKernelGGL(softmax_nll_fwd_kernel, dim3(nblocks),
+  hipLaunchKernelGGL(softmax_nll_fwd_kernel, dim3(tiles * nblocks),
                      dim3(kSnWaves * 64), 0, stream(), S_hat.data_ptr<float>(),
+                     two ? S_hat2->data_ptr<float>() : nullptr,
                      ptr_s.data_ptr<int>(), n_t.data_ptr<int>(),
                      y.data_ptr<int64_t>(), mp, part.data_ptr<float>(), B, Ns,
-                     Nt, (float)eps);
+                     Nt, nblocks, (float)eps);
   hipLaunchKernelGGL(softmax_nll_fold_kernel, dim3(1), dim3(kLossThreads), 0,
-                     stream(), part.data_ptr<float>(), nblocks,
-                     loss.data_ptr<float>(), aux.data_ptr<float>());
+                     stream(), part.data_ptr<float>(), nblocks, tiles,
+                     loss.data_ptr<float>(), aux.data_ptr<float>(), sp);
   DGMC_CHECK_LAUNCH();
   return {loss, aux};
 }
 
-at::Tensor softmax_nll_bwd(const at::Tensor& grad, const at::Tensor& S_hat,
-                           const at::Tensor& ptr_s, const at::Tensor& n_t,
-                           const at::Tensor& y,
-                           const c10::optional<at::Tensor>& mask,
-                           const at::Tensor& aux, double eps) {
+// Gradients of both tiles (dS2 undefined without S_hat2).
+std::tuple<at::Tensor, at::Tensor> softmax_nll_bwd(
+    const at::Tensor& grad, const at::Tensor& S_hat,
+    const c10::optional<at::Tensor>& S_hat2, const at::Tensor& ptr_s,
+    const at::Tensor& n_t, const at::Tensor& y,
+    const c10::optional<at::Tensor>& mask, const at::Tensor& aux,
+    double eps) {
   check_snll(S_hat, ptr_s, n_t, y, mask);
   TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.numel() == 1 &&
-                  aux.scalar_type() == at::kFloat && aux.numel() == 2,
-              "softmax_nll_bwd: fp32 scalar grad / aux [2]");
+                  aux.scalar_type() == at::kFloat && aux.numel() == 3,
+              "softmax_nll_bwd: fp32 scalar grad / aux [3]");
+  const bool two = S_hat2.has_value() && S_hat2->defined();
+  if (two)
+    TORCH_CHECK(S_hat2->sizes() == S_hat.sizes() &&
+                    S_hat2->scalar_type() == at::kFloat &&
+                    S_hat2->is_contiguous(),
+                "softmax_nll_bwd: S_hat2 like S_hat");
   const int B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
   at::Tensor dS = at::empty_like(S_hat);
+  at::Tensor dS2 = two ? at::empty_like(S_hat) : at::Tensor();
   const int rows = B * Ns;
-  if (rows == 0) return dS;
+  if (rows == 0) return {dS, dS2};
+  const int nblocks = (rows + kSnWaves - 1) / kSnWaves;
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   const bool* mp = (mask.has_value() && mask->defined())
                        ? mask->data_ptr<bool>() : nullptr;
-  hipLaunchKernelGGL(softmax_nll_bwd_kernel,
-                     dim3((rows + kSnWaves - 1) / kSnWaves),
+  hipLaunchKernelGGL(softmax_nll_bwd_kernel, dim3((two ? 2 : 1) * nblocks),
                      dim3(kSnWaves * 64), 0, stream(), grad.data_ptr<float>(),
-                     S_hat.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                     n_t.data_ptr<int>(), y.data_ptr<int64_t>(), mp,
-                     aux.data_ptr<float>(), dS.data_ptr<float>(), B, Ns, Nt,
-                     (float)eps);
+                     S_hat.data_ptr<float>(),
+                     two ? S_hat2->data_ptr<float>() : nullptr,
+                     ptr_s.data_ptr<int>(), n_t.data_ptr<int>(),
+                     y.data_ptr<int64_t>(), mp, aux.data_ptr<float>(),
+                     dS.data_ptr<float>(), two ? dS2.data_ptr<float>() : nullptr,
+                     B, Ns, Nt, nblocks, (float)eps);
   DGMC_CHECK_LAUNCH();
-  return dS;
+  return {dS, dS2};
 }
 
 }  // namespace dgmc

@@ -163,13 +163,16 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                               const at::Tensor& ptr_s, const at::Tensor& ptr_t,
                               const c10::optional<at::Tensor>& dpq_out);
 std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
-    const at::Tensor& S_hat, const at::Tensor& ptr_s, const at::Tensor& n_t,
-    const at::Tensor& y, const c10::optional<at::Tensor>& mask, double eps);
-at::Tensor softmax_nll_bwd(const at::Tensor& grad, const at::Tensor& S_hat,
-                           const at::Tensor& ptr_s, const at::Tensor& n_t,
-                           const at::Tensor& y,
-                           const c10::optional<at::Tensor>& mask,
-                           const at::Tensor& aux, double eps);
+    const at::Tensor& S_hat, const c10::optional<at::Tensor>& S_hat2,
+    const at::Tensor& ptr_s, const at::Tensor& n_t, const at::Tensor& y,
+    const c10::optional<at::Tensor>& mask, double eps,
+    const c10::optional<at::Tensor>& stats);
+std::tuple<at::Tensor, at::Tensor> softmax_nll_bwd(
+    const at::Tensor& grad, const at::Tensor& S_hat,
+    const c10::optional<at::Tensor>& S_hat2, const at::Tensor& ptr_s,
+    const at::Tensor& n_t, const at::Tensor& y,
+    const c10::optional<at::Tensor>& mask, const at::Tensor& aux,
+    double eps);
 at::Tensor pair_scores(const at::Tensor& h, int64_t t_off,
                        const at::Tensor& ptr_s, const at::Tensor& ptr_t,
                        int64_t Ns, int64_t Nt);
@@ -290,11 +293,13 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None) -> (Tensor, Tensor, "
       "Tensor, Tensor, Tensor)");
   m.def(
-      "softmax_nll_fwd(Tensor S_hat, Tensor ptr_s, Tensor n_t, Tensor y, "
-      "Tensor? mask, float eps) -> (Tensor, Tensor)");
+      "softmax_nll_fwd(Tensor S_hat, Tensor? S_hat2, Tensor ptr_s, Tensor "
+      "n_t, Tensor y, Tensor? mask, float eps, Tensor(a!)? stats=None) -> "
+      "(Tensor, Tensor)");
   m.def(
-      "softmax_nll_bwd(Tensor grad, Tensor S_hat, Tensor ptr_s, Tensor n_t, "
-      "Tensor y, Tensor? mask, Tensor aux, float eps) -> Tensor");
+      "softmax_nll_bwd(Tensor grad, Tensor S_hat, Tensor? S_hat2, Tensor "
+      "ptr_s, Tensor n_t, Tensor y, Tensor? mask, Tensor aux, float eps) -> "
+      "(Tensor, Tensor)");
   m.def(
       "pair_scores(Tensor h, int t_off, Tensor ptr_s, Tensor ptr_t, int Ns, "
       "int Nt) -> Tensor");

@@ -129,7 +129,8 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
                           const Tensor& pos_of_class, const Tensor& s_ids,
                           const Tensor& t_ids, Tensor out, int64_t cap_s,
                           int64_t cap_t, int64_t ecap_s, int64_t ecap_t,
-                          int64_t n_max, int64_t zero_node, int64_t zero_edge) {
+                          int64_t n_max, int64_t zero_node, int64_t zero_edge,
+                          const c10::optional<Tensor>& edge_attr) {
   check_cpu_long(node_ptr, "node_ptr");
   check_cpu_long(edge_ptr, "edge_ptr");
   check_cpu_long(edge_local, "edge_local");
@@ -140,8 +141,20 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   check_cpu_long(out, "out");
   const int64_t B = s_ids.numel();
   TORCH_CHECK(t_ids.numel() == B, "s_ids / t_ids size mismatch");
+  // Optional host copy of the edge-attribute table (fp32 [E_all + 1, D]):
+  // the attributes are then written into the buffer (no device gather).
+  const bool has_ea = edge_attr.has_value() && edge_attr->defined();
+  int64_t D = 0;
+  if (has_ea) {
+    TORCH_CHECK(edge_attr->device().is_cpu() &&
+                    edge_attr->scalar_type() == at::kFloat &&
+                    edge_attr->dim() == 2 && edge_attr->is_contiguous(),
+                "edge_attr must be a contiguous CPU fp32 [E, D] tensor");
+    D = edge_attr->size(1);
+  }
   const int64_t need = cap_s * 4 + cap_t * 2 + ecap_s * 3 + ecap_t * 3 +
-                       2 * (B + 1) + 2 * B;
+                       2 * (B + 1) + 2 * B + 2 * ecap_t + (cap_s + 7) / 8 +
+                       (B + 1) + B + ((ecap_s + ecap_t) * D + 1) / 2;
   // The buffer layout (datasets/static_batch.py::_views) is sized for exactly
   // B pairs: any other count would shift every region after dense_t.
   TORCH_CHECK(out.numel() == need,
@@ -196,6 +209,13 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
   int64_t* ptr_s = o;             o += B + 1;
   int64_t* ptr_t = o;             o += B + 1;
   int64_t* gid = o;               o += 2 * B;   // store ids: [s_ids; t_ids]
+  // Typed tail: the views the step consumes in their final dtype (no cast /
+  // subtraction kernels on the device).
+  int64_t* ei_tl = o;             o += 2 * ecap_t;  // target edges, local ids
+  uint8_t* ymb = reinterpret_cast<uint8_t*>(o);  o += (cap_s + 7) / 8;
+  int32_t* p32 = reinterpret_cast<int32_t*>(o);  o += B + 1;  // [ptr_s; ptr_t]
+  int32_t* c32 = reinterpret_cast<int32_t*>(o);  o += B;      // [n_s; n_t]
+  float* eav = reinterpret_cast<float*>(o);      // [(ecap_s + ecap_t), D]
   const int64_t trash = B * n_max;
 
 #pragma omp parallel for schedule(static)
@@ -258,6 +278,35 @@ bool collate_pairs_padded(const Tensor& node_ptr, const Tensor& edge_ptr,
     gid[b] = sid[b];
     gid[B + b] = tid[b];
   }
+  for (int64_t r = 0; r < ecap_t; ++r) {
+    ei_tl[r] = ei_t0[r] - cap_s;
+    ei_tl[ecap_t + r] = ei_t1[r] - cap_s;
+  }
+  for (int64_t r = 0; r < cap_s; ++r) ymb[r] = (uint8_t)(ym[r] != 0);
+  for (int64_t b = 0; b <= B; ++b) {
+    p32[b] = (int32_t)ns_off[b];
+    p32[B + 1 + b] = (int32_t)nt_off[b];
+  }
+  for (int64_t b = 0; b < B; ++b) {
+    c32[b] = (int32_t)(ns_off[b + 1] - ns_off[b]);
+    c32[B + b] = (int32_t)(nt_off[b + 1] - nt_off[b]);
+  }
+  if (has_ea) {
+    const float* ea = edge_attr->data_ptr<float>();
+    const int64_t E_tab = edge_attr->size(0);
+    const int64_t ne = ecap_s + ecap_t;
+    int64_t bad = 0;
+#pragma omp parallel for schedule(static) reduction(+ : bad)
+    for (int64_t r = 0; r < ne; ++r) {
+      const int64_t e = ea_s[r];      // ea_s and ea_t are adjacent
+      if (e < 0 || e >= E_tab) {
+        ++bad;
+        continue;
+      }
+      for (int64_t d = 0; d < D; ++d) eav[r * D + d] = ea[e * D + d];
+    }
+    TORCH_CHECK(bad == 0, "collate_pairs_padded: edge id out of range");
+  }
   return true;
 }
 
@@ -292,7 +341,8 @@ TORCH_LIBRARY(dgmc_host, m) {
       "collate_pairs_padded(Tensor node_ptr, Tensor edge_ptr, Tensor "
       "edge_local, Tensor node_class, Tensor pos_of_class, Tensor s_ids, "
       "Tensor t_ids, Tensor(a!) out, int cap_s, int cap_t, int ecap_s, int "
-      "ecap_t, int n_max, int zero_node, int zero_edge) -> bool");
+      "ecap_t, int n_max, int zero_node, int zero_edge, Tensor? edge_attr=None) "
+      "-> bool");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_host, CPU, m) {

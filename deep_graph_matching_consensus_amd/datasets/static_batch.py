@@ -78,9 +78,18 @@ class StaticPairBatcher(object):
             [store.edge_attr,
              store.edge_attr.new_zeros(1, store.edge_attr.size(1))])
 
+        # Host copy of the fp32 edge-attribute table: the collator writes the
+        # batch's attributes into the staged buffer (no device gather).
+        self._ea_host = None
+        if self.edge_attr is not None and \
+                self.edge_attr.dtype == torch.float32:
+            self._ea_host = self.edge_attr.cpu().contiguous()
+        self.ea_dim = 0 if self._ea_host is None else self._ea_host.size(1)
         cs, ct, es, et, B = self.cap_s, self.cap_t, self.ecap_s, self.ecap_t, \
             self.B
-        self.words = cs * 4 + ct * 2 + es * 3 + et * 3 + 2 * (B + 1) + 2 * B
+        self.words = cs * 4 + ct * 2 + es * 3 + et * 3 + 2 * (B + 1) + \
+            2 * B + 2 * et + (cs + 7) // 8 + (B + 1) + B + \
+            ((es + et) * self.ea_dim + 1) // 2
         pin = self.device.type == 'cuda'
         self._host = [torch.zeros(self.words, dtype=torch.long,
                                   pin_memory=pin) for _ in range(2)]
@@ -140,10 +149,23 @@ class StaticPairBatcher(object):
         for name, n in [('node', cs + ct), ('ea', es + et),
                         ('ei', 2 * (es + et)), ('y', cs), ('ymask', cs),
                         ('dense_s', cs), ('dense_t', ct), ('ptr_s', B + 1),
-                        ('ptr_t', B + 1), ('gid', 2 * B)]:
+                        ('ptr_t', B + 1), ('gid', 2 * B),
+                        # typed tail (final dtypes, no device casts)
+                        ('ei_tl', 2 * et), ('ymask_b', (cs + 7) // 8),
+                        ('ptr32', B + 1), ('cnt32', B),
+                        ('ea_val', ((es + et) * self.ea_dim + 1) // 2)]:
             v[name] = self.buf[o:o + n]
             o += n
         v['ei'] = v['ei'].view(2, es + et)
+        v['ei_tl'] = v['ei_tl'].view(2, et)
+        v['ymask_b'] = v['ymask_b'].view(torch.uint8)[:cs].view(torch.bool)
+        p32 = v['ptr32'].view(torch.int32)
+        v['ptr32_s'], v['ptr32_t'] = p32[:B + 1], p32[B + 1:]
+        c32 = v['cnt32'].view(torch.int32)
+        v['cnt32_s'], v['cnt32_t'] = c32[:B], c32[B:]
+        if self.ea_dim:
+            v['ea_val'] = v['ea_val'].view(torch.float32)[
+                :(es + et) * self.ea_dim].view(es + et, self.ea_dim)
         self.v = v
 
     # ------------------------------------------------------------------
@@ -186,7 +208,7 @@ class StaticPairBatcher(object):
             torch.from_numpy(np.ascontiguousarray(s_ids, dtype=np.int64)),
             torch.from_numpy(np.ascontiguousarray(t_ids, dtype=np.int64)),
             host, self.cap_s, self.cap_t, self.ecap_s, self.ecap_t,
-            self.n_max, self.zero_node, self.zero_edge)
+            self.n_max, self.zero_node, self.zero_edge, self._ea_host)
         if not ok:
             self.overflows += 1
             return False
@@ -201,16 +223,26 @@ class StaticPairBatcher(object):
         """Device-side batch from the static buffer (graph-capturable)."""
         from ..models.dgmc import register_pair_graph
         v = self.v
+        # Every materialisation is a new batch for the identity caches keyed
+        # on (tensor, version) (ops/plans.py): the buffer views are the same
+        # objects each step, so bump their shared version counter (no
+        # kernel).  Otherwise a hipGraph capture following an eager warm-up
+        # on the same staged batch would reuse the warm-up's plans instead of
+        # recording their assembly.
+        torch.autograd.graph.increment_version(self.buf)
         cs, es = self.cap_s, self.ecap_s
         batch = Batch()
         x_u = self.x.index_select(0, v['node'])
         batch.x_s, batch.x_t = x_u[:cs], x_u[cs:]
         ei_u = v['ei']
         batch.edge_index_s = ei_u[:, :es]
-        batch.edge_index_t = ei_u[:, es:] - cs
+        batch.edge_index_t = v['ei_tl']           # local target ids
         ea_u = None
-        if self.edge_attr is not None:
+        if self.ea_dim:
+            ea_u = v['ea_val']                    # written by the collator
+        elif self.edge_attr is not None:
             ea_u = self.edge_attr.index_select(0, v['ea'])
+        if ea_u is not None:
             batch.edge_attr_s, batch.edge_attr_t = ea_u[:es], ea_u[es:]
         else:
             batch.edge_attr_s = batch.edge_attr_t = None
@@ -222,13 +254,11 @@ class StaticPairBatcher(object):
                             ea_u)
         _plans.register_plan_provider(ei_u, ea_u, self._assembler)
         batch.y = v['y']
-        batch.y_mask = v['ymask'].to(torch.bool)
-        ptr_s = v['ptr_s'].to(torch.int32)
-        ptr_t = v['ptr_t'].to(torch.int32)
+        batch.y_mask = v['ymask_b']
         info_s = StaticBatchInfo(self.B, self.n_max, self.cap_s,
-                                 ptr_s[1:] - ptr_s[:-1], ptr_s, v['dense_s'])
+                                 v['cnt32_s'], v['ptr32_s'], v['dense_s'])
         info_t = StaticBatchInfo(self.B, self.n_max, self.cap_t,
-                                 ptr_t[1:] - ptr_t[:-1], ptr_t, v['dense_t'])
+                                 v['cnt32_t'], v['ptr32_t'], v['dense_t'])
         batch.x_s_batch, batch.x_t_batch = self.batch_s, self.batch_t
         register_batch_info(self.batch_s, info_s)
         register_batch_info(self.batch_t, info_t)

@@ -480,13 +480,16 @@ class DGMC(torch.nn.Module):
     # Objectives and metrics (dgmc.py:246-311)
     # ------------------------------------------------------------------
     def objective(self, x_s, edge_index_s, edge_attr_s, batch_s, x_t,
-                  edge_index_t, edge_attr_t, batch_t, y_col, mask=None):
+                  edge_index_t, edge_attr_t, batch_t, y_col, mask=None,
+                  stats=None):
         r"""The reference drivers' training objective (``pascal.py:67-72``):
         ``NLL(S_0) + NLL(S_L)`` (``NLL(S_0)`` alone when ``num_steps`` is 0)
         for ground truth ``y = (arange(sum N_s), y_col)``, plus the Hits@1
         count of ``S_L``.  Returns ``(loss, count, correct)`` as device
         tensors (``mask`` selects the valid ground truths of a padded
-        batch).
+        batch).  ``stats`` (optional fp64 device tensor): ``+= [loss,
+        correct, count]`` - folded into the loss kernel on the fused path;
+        callers check :attr:`last_stats_fused` to know whether it was.
 
         On the GPU's dense path the row softmax, NLL and arg-max run as ONE
         fused kernel on the raw scores per output (``softmax_nll``), whose
@@ -497,13 +500,14 @@ class DGMC(torch.nn.Module):
             out = self._forward(x_s, edge_index_s, edge_attr_s, batch_s, x_t,
                                 edge_index_t, edge_attr_t, batch_t, None,
                                 raw=True)
+        self.last_stats_fused = False
         if isinstance(out, _RawScores):
             y_col = y_col.contiguous()
-            loss, aux = dense_ops.softmax_nll(out.S_hat_L, out.lay_s,
-                                              out.lay_t, y_col, mask, EPS)
-            if self.num_steps:
-                loss = loss + dense_ops.softmax_nll(
-                    out.S_hat_0, out.lay_s, out.lay_t, y_col, mask, EPS)[0]
+            # NLL(S_L) + NLL(S_0) (+ the running stats) in one launch + fold.
+            loss, aux = dense_ops.softmax_nll(
+                out.S_hat_L, out.lay_s, out.lay_t, y_col, mask, EPS,
+                S_hat2=out.S_hat_0 if self.num_steps else None, stats=stats)
+            self.last_stats_fused = stats is not None
             return loss, aux[0], aux[1]
         S_0, S_L = out
         rows = torch.arange(y_col.numel(), device=y_col.device)

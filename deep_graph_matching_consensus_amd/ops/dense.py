@@ -142,14 +142,18 @@ def masked_softmax_packed(S_hat, lay_s, lay_t):
 
 class _SoftmaxNLL(torch.autograd.Function):
     """Masked row softmax + NLL (+ Hits@1) on the dense scores in one fused
-    kernel (csrc/hip/loss.hip::softmax_nll_*); ``aux = [count, correct]``."""
+    kernel (csrc/hip/loss.hip::softmax_nll_*) for one or two score tiles
+    (the objective's ``S_L`` and ``S_0`` in the same launch);
+    ``aux = [count, correct, count of the second tile]``."""
 
     @staticmethod
-    def forward(ctx, S_hat, ptr_s, n_t, y, mask, eps):
+    def forward(ctx, S_hat, S_hat2, ptr_s, n_t, y, mask, eps, stats):
         S_hat = S_hat.float().contiguous()
-        loss, aux = _backend.ops().softmax_nll_fwd(S_hat, ptr_s, n_t, y, mask,
-                                                   eps)
-        ctx.save_for_backward(S_hat, ptr_s, n_t, y, mask, aux)
+        if S_hat2 is not None:
+            S_hat2 = S_hat2.float().contiguous()
+        loss, aux = _backend.ops().softmax_nll_fwd(S_hat, S_hat2, ptr_s, n_t,
+                                                   y, mask, eps, stats)
+        ctx.save_for_backward(S_hat, S_hat2, ptr_s, n_t, y, mask, aux)
         ctx.eps = eps
         ctx.mark_non_differentiable(aux)
         ctx.set_materialize_grads(False)
@@ -158,11 +162,12 @@ class _SoftmaxNLL(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad, grad_aux):
         if grad is None:
-            return (None, ) * 6
-        S_hat, ptr_s, n_t, y, mask, aux = ctx.saved_tensors
-        dS = _backend.ops().softmax_nll_bwd(grad.float().reshape(1), S_hat,
-                                            ptr_s, n_t, y, mask, aux, ctx.eps)
-        return dS, None, None, None, None, None
+            return (None, ) * 8
+        S_hat, S_hat2, ptr_s, n_t, y, mask, aux = ctx.saved_tensors
+        dS, dS2 = _backend.ops().softmax_nll_bwd(
+            grad.float().reshape(1), S_hat, S_hat2, ptr_s, n_t, y, mask, aux,
+            ctx.eps)
+        return (dS, dS2 if S_hat2 is not None else None) + (None, ) * 6
 
 
 def softmax_nll_supported(S_hat, lay_s):
@@ -171,13 +176,17 @@ def softmax_nll_supported(S_hat, lay_s):
             lay_s.ptr.is_cuda)
 
 
-def softmax_nll(S_hat, lay_s, lay_t, y_col, mask, eps):
+def softmax_nll(S_hat, lay_s, lay_t, y_col, mask, eps, S_hat2=None,
+                stats=None):
     r"""``(loss, aux)``: mean of ``-log(masked_softmax(S_hat)[r, y_col[r]] +
-    eps)`` over the packed source rows ``r`` (weights ``mask``) and
-    ``aux = [count, correct top-1]`` - ``DGMC.loss`` / ``DGMC.correct`` of
-    ``masked_softmax_packed(S_hat)`` with ``y = (arange, y_col)``."""
-    return _SoftmaxNLL.apply(S_hat, lay_s.ptr, lay_t.counts, y_col, mask,
-                             float(eps))
+    eps)`` over the packed source rows ``r`` (weights ``mask``) - plus the
+    same term of ``S_hat2`` when given - and ``aux = [count, correct top-1,
+    count]`` (``DGMC.loss`` / ``DGMC.correct`` of
+    ``masked_softmax_packed(S_hat)`` with ``y = (arange, y_col)``).
+    ``stats`` (fp64 device tensor, optional) receives ``+= [loss, correct,
+    count]`` inside the fold kernel."""
+    return _SoftmaxNLL.apply(S_hat, S_hat2, lay_s.ptr, lay_t.counts, y_col,
+                             mask, float(eps), stats)
 
 
 # ---------------------------------------------------------------------------

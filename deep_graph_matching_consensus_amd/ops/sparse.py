@@ -582,8 +582,9 @@ def prime_slot_images(w_lp, weight, root):
     img_f, img_t = _backend.ops().spline_slot_images(
         weight.detach(), root.detach() if root is not None else None,
         slot_k_order(weight.device))
-    prime(_slot_img_key(w_lp, False), (w_lp, img_f))
-    prime(_slot_img_key(w_lp, True), (w_lp, img_t))
+    # Looked up from _GemmSpMM.forward, i.e. with grad mode off.
+    prime(_slot_img_key(w_lp, False), (w_lp, img_f), any_grad_mode=True)
+    prime(_slot_img_key(w_lp, True), (w_lp, img_t), any_grad_mode=True)
 
 
 def slot_conv_image(w_lp, C, trans):

@@ -41,10 +41,16 @@ def cached(key, fn):
     return value
 
 
-def prime(key, value):
+def prime(key, value, any_grad_mode=False):
     """Store ``value`` under ``key`` in the active scope (if any), for a
-    producer that computes several cached tensors in one kernel."""
+    producer that computes several cached tensors in one kernel.
+    ``any_grad_mode``: also serve lookups made with the other grad mode
+    (e.g. from inside an autograd ``Function.forward``, where grad mode is
+    off) - for values that carry no autograd history."""
     import torch
     store = getattr(_TLS, 'store', None)
     if store is not None:
-        store[key + (torch.is_grad_enabled(), )] = value
+        modes = (True, False) if any_grad_mode else \
+            (torch.is_grad_enabled(), )
+        for m in modes:
+            store[key + (m, )] = value

@@ -89,6 +89,7 @@ class PairTrainer(object):
             # (and the step counter) on the device - no host sync, capturable.
             self.optimizer.found_inf = self._found_inf
         self.step_count = 0
+        self._one = None
         data_seed = seed + 1000 * self.rank
         if mode == 'eager':
             self.loader = DevicePairLoader(store, batch_size, sources=sources,
@@ -125,13 +126,17 @@ class PairTrainer(object):
 
     def _forward_backward(self, batch, rows, mask):
         model = self.model
+        fused_stats = False
         if hasattr(model, 'objective') and rows.numel() == batch.y.numel():
-            # NLL(S_0) + NLL(S_L) on the raw scores (fused softmax + NLL).
+            # NLL(S_0) + NLL(S_L) on the raw scores (fused softmax + NLL; the
+            # loss kernel also accumulates the running stats).
             with self._autocast():
                 loss, count, correct = model.objective(
                     batch.x_s, batch.edge_index_s, batch.edge_attr_s,
                     batch.x_s_batch, batch.x_t, batch.edge_index_t,
-                    batch.edge_attr_t, batch.x_t_batch, batch.y, mask)
+                    batch.edge_attr_t, batch.x_t_batch, batch.y, mask,
+                    stats=self.stats)
+            fused_stats = getattr(model, 'last_stats_fused', False)
         else:
             with self._autocast():
                 S_0, S_L = model(batch.x_s, batch.edge_index_s,
@@ -144,9 +149,14 @@ class PairTrainer(object):
                 loss = loss_L + model.loss(S_0, y, mask=mask)
             else:
                 loss, count, correct = model.loss_stats(S_0, y, mask)
-        loss.backward()
-        self.stats[:3] += torch.stack(
-            [loss.detach().float(), correct.float(), count.float()]).double()
+        # A persistent seed gradient: no fill kernel in the captured step.
+        if self._one is None or self._one.device != loss.device:
+            self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(self._one)
+        if not fused_stats:
+            self.stats[:3] += torch.stack(
+                [loss.detach().float(), correct.float(),
+                 count.float()]).double()
 
     def _check_finite(self):
         """Flag non-finite gradients in ``_found_inf`` (device-side)."""

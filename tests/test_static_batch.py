@@ -129,7 +129,8 @@ def test_assembled_spline_plan_matches_generic_build():
         N = cs + ct
         ei_u = batcher.v['ei']
         ea_u = torch.cat([batch.edge_attr_s, batch.edge_attr_t])
-        ea_view = batch.edge_attr_s._base
+        ea_view = batcher.v['ea_val'] if batcher.ea_dim else \
+            batch.edge_attr_s._base
         op = plans.spline_plan(ei_u, ea_view, N, (5, 5), (1, 1), 1, True)
         assert type(op).__name__ == '_StaticSlotOperator'
         ref_op = plans.spline_plan(ei_u.clone(), ea_u, N, (5, 5), (1, 1), 1,
@@ -166,3 +167,28 @@ def test_static_batch_union_views_gpu():
     assert torch.equal(joint, torch.cat([batch.x_s, batch.x_t]))
     ei = torch.cat([batch.edge_index_s, batch.edge_index_t + cs], dim=1)
     assert torch.equal(ei, batcher.v['ei'])
+
+
+def test_static_batch_typed_tail_matches_derived_views():
+    """The collator's typed tail (local target edges, bool mask, int32 ptr /
+    counts, gathered edge attributes) equals what the step used to derive on
+    the device with cast / subtraction / gather kernels."""
+    store, batcher, _ = _setup()
+    for _ in range(2):
+        assert batcher.load()
+        v = batcher.v
+        cs, es = batcher.cap_s, batcher.ecap_s
+        assert torch.equal(v['ei_tl'], v['ei'][:, es:] - cs)
+        assert torch.equal(v['ymask_b'], v['ymask'].to(torch.bool))
+        assert torch.equal(v['ptr32_s'], v['ptr_s'].to(torch.int32))
+        assert torch.equal(v['ptr32_t'], v['ptr_t'].to(torch.int32))
+        assert torch.equal(v['cnt32_s'],
+                           (v['ptr_s'][1:] - v['ptr_s'][:-1]).to(torch.int32))
+        assert torch.equal(v['cnt32_t'],
+                           (v['ptr_t'][1:] - v['ptr_t'][:-1]).to(torch.int32))
+        assert batcher.ea_dim == store.edge_attr.size(1)
+        assert torch.equal(v['ea_val'],
+                           batcher.edge_attr.index_select(0, v['ea']))
+        batch = batcher.materialize()
+        assert batch.y_mask.dtype == torch.bool
+        assert torch.equal(batch.edge_index_t, v['ei'][:, es:] - cs)
