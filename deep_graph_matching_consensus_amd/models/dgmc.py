@@ -37,6 +37,7 @@ from ..ops import sparse_corr
 from ..ops.sparse import PASSTHROUGH
 from ..ops.plans import _IdentityCache
 from ..runtime import loopgrad
+from ..runtime import streams
 from ..runtime.cache import forward_cache
 from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
@@ -72,20 +73,35 @@ class _PackedNLL(torch.autograd.Function):
         return dS, None, None, None, None, None
 
 
-class _TieUnused(torch.autograd.Function):
-    """Identity on ``x`` that makes ``unused`` part of the autograd graph
-    with an exact zero gradient (one fill, vs three launches for
-    ``x + 0 * u.sum()``)."""
+FOLD_FP32 = os.environ.get('DGMC_AMD_FOLD_FP32', '1') == '1'
+
+
+class _FoldProduct(torch.autograd.Function):
+    """``W1 @ W_f`` in fp32 (the folded consensus projection; ``b_f`` rides
+    along with an exact zero gradient).  Its backward only produces
+    parameter gradients, so it runs as part of the side-stream branch
+    (runtime/streams.py) that the folded weight gradient arrives on."""
 
     @staticmethod
-    def forward(ctx, x, unused):
-        ctx.like = (unused.shape, unused.dtype)
-        return x.view_as(x)
+    def forward(ctx, w1, wf, bf):
+        ctx.save_for_backward(w1, wf)
+        ctx.bf_like = None if bf is None else (bf.shape, bf.dtype)
+        with torch.autocast(w1.device.type, enabled=False):
+            return w1.float() @ wf.float()
 
     @staticmethod
-    def backward(ctx, grad):
-        shape, dtype = ctx.like
-        return grad, grad.new_zeros(shape, dtype=dtype)
+    def backward(ctx, g):
+        w1, wf = ctx.saved_tensors
+        with streams.side(g.device, (g, w1, wf)):
+            g = g.float()
+            gw1 = (g @ wf.float().t()).to(w1.dtype) \
+                if ctx.needs_input_grad[0] else None
+            gwf = (w1.float().t() @ g).to(wf.dtype) \
+                if ctx.needs_input_grad[1] else None
+            gbf = None
+            if ctx.bf_like is not None and ctx.needs_input_grad[2]:
+                gbf = g.new_zeros(ctx.bf_like[0], dtype=ctx.bf_like[1])
+        return gw1, gwf, gbf
 
 
 class _RawScores(object):
@@ -362,12 +378,14 @@ class DGMC(torch.nn.Module):
                 # tiny W1 W_f product once per step.
                 fold = None
                 if joint and self._foldable():
-                    w_fold = self.mlp[0].weight @ self.psi_2.final.weight
-                    if self.psi_2.final.bias is not None:
-                        # b_f's exact gradient is zero; keep it in the graph
-                        # (autograd.grad, DDP) without any kernel.
-                        w_fold = _TieUnused.apply(w_fold,
-                                                  self.psi_2.final.bias)
+                    # (b_f's exact gradient is zero; it stays in the graph
+                    # for autograd.grad / DDP.)
+                    if FOLD_FP32:
+                        w_fold = _FoldProduct.apply(self.mlp[0].weight,
+                                                    self.psi_2.final.weight,
+                                                    self.psi_2.final.bias)
+                    else:
+                        w_fold = self.mlp[0].weight @ self.psi_2.final.weight
                     fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)),
                             steps)
                 pending = None    # (joint, S_hat) from a fused step boundary

@@ -24,6 +24,7 @@ from ..ops import _backend
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.gemm import compute_dtype
 from ..ops.sparse import SLOT_CONV, gemm_spmm, prime_slot_images, spmm
+from ..runtime import streams
 from ..runtime.cache import cached
 from .inits import reset, uniform
 
@@ -48,6 +49,8 @@ class _StackedSplineWeight(torch.autograd.Function):
         w_lp = _backend.ops().spline_weight_pack(weight, root, dtype)
         ctx.K, ctx.has_root = weight.size(0), root is not None
         token = weight.new_empty(1).expand(w_lp.shape)
+        ctx.takes_slot_major = True     # see backward
+        ctx.slot_major = None
         ctx.mark_non_differentiable(w_lp)
         # w_lp never receives a gradient: do not materialise a zero one.
         ctx.set_materialize_grads(False)
@@ -55,10 +58,23 @@ class _StackedSplineWeight(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _):
-        if g is None:
+        # A slot-major [S, in, out] gradient deposited on this node by the
+        # fused slot conv's loop fold (ops/sparse.py): weight / root are
+        # views (AccumulateGrad steals them - no kernel).
+        pend, ctx.slot_major = ctx.slot_major, None
+        if g is None and pend is None:
             return None, None, None
-        gw, gr = _backend.ops().spline_weight_unpack(
-            g.float().contiguous(), ctx.K, ctx.has_root)
+        gw = gr = None
+        if g is not None:
+            if pend is not None:
+                streams.join()      # (a side-stream pend: combine after it)
+            gw, gr = _backend.ops().spline_weight_unpack(
+                g.float().contiguous(), ctx.K, ctx.has_root)
+        if pend is not None:
+            pw, pr = pend[:ctx.K], pend[ctx.K] if ctx.has_root else None
+            gw = pw if gw is None else gw + pw
+            if ctx.has_root:
+                gr = pr if gr is None else gr + pr
         return gw, (gr if ctx.has_root else None), None
 
 

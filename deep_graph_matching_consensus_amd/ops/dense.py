@@ -30,7 +30,7 @@ from . import _backend
 from . import reference as ref
 from .gemm import (_col_sum, loop_col_sum, loop_col_total, lowp_weight_t,
                    mixed_matmul)
-from ..runtime import loopgrad
+from ..runtime import loopgrad, streams
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
@@ -381,7 +381,10 @@ def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
     for name, t in parts:
         loop.keep(name, idx, t)
     if loop.arrive():
-        out = tuple(_col_sum(loop.kept(n)) for n, _ in parts)
+        # Parameter gradients only (b1, w2, b2): side-stream branch.
+        lists = [loop.kept_list(n) for n, _ in parts]
+        with streams.side(dP.device, lists):
+            out = tuple(_col_sum(loop.kept(n)) for n, _ in parts)
         loop.release()
         return out
     return None, None, None
@@ -445,9 +448,13 @@ class _CatMatmul(torch.autograd.Function):
             loop.keep('g', ctx.idx, g)
             if loop.arrive():
                 if ctx.needs_input_grad[0]:
+                    # Off psi_1's backward path: side-stream branch
+                    # (runtime/streams.py).
                     X = loop.stack('x')
-                    gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
-                                        loop.kept('g')).to(ctx.w_dtype)
+                    gl = loop.kept_list('g')
+                    with streams.side(g.device, (X, gl)):
+                        gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
+                                            loop.kept('g')).to(ctx.w_dtype)
                 loop.release()
         return (gw, None, None, None, None) + tuple(grads)
 

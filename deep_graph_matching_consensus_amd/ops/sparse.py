@@ -23,6 +23,7 @@ import os
 import torch
 
 from . import _backend
+from ..runtime import streams
 from . import reference as ref
 
 
@@ -220,6 +221,13 @@ class _GemmSpMM(torch.autograd.Function):
         ctx.save_for_backward(xc, w_lp, out if relu else None)
         ctx.op, ctx.relu, ctx.C, ctx.loop = op, relu, C, loop
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
+        # Gradient carrier token of nn/conv.py::_StackedSplineWeight (an
+        # expanded 1-element tensor): its node can take the loop-folded
+        # weight gradient in slot-major layout directly (no permute copy, no
+        # unpack kernel).
+        node = w.grad_fn if (SLOT_HANDOFF and w.dim() == 2 and
+                             w.stride() == (0, 0)) else None
+        ctx.w_node = node if hasattr(node, 'takes_slot_major') else None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.idx = loop.register() if loop is not None else None
         if passthrough:
@@ -257,12 +265,26 @@ class _GemmSpMM(torch.autograd.Function):
         loop.keep('g', idx, g)
         gw = gb = None
         if loop.arrive():
-            if ctx.needs_input_grad[1]:
-                dW = slot_weight_grad(loop.kept_list('x'),
-                                      loop.kept_list('g'), op, S, loop.uses)
-                gw = dW.permute(1, 0, 2).reshape(K, S * C).to(ctx.w_dtype)
-            if need_b:
-                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+            need_w = ctx.needs_input_grad[1]
+            xs, gs = loop.kept_list('x'), loop.kept_list('g')
+            # The folded weight / bias gradients are off psi_1's backward
+            # path: a side-stream branch in the trainer's step
+            # (runtime/streams.py), joined before the gradients are packed.
+            keep = (xs, gs, loop.stack('b') if need_b and 'b' in loop._stacks
+                    else None)
+            with streams.side(grad.device, keep):
+                if need_w:
+                    dW = slot_weight_grad(xs, gs, op, S, loop.uses)
+                if need_b:
+                    gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+            if need_w:
+                if ctx.w_node is not None:
+                    # Slot-major [S, in, out] straight to the stacked-weight
+                    # node (nn/conv.py): weight / root gradients are views.
+                    ctx.w_node.slot_major = dW
+                else:
+                    gw = dW.permute(1, 0, 2).reshape(K, S * C).to(
+                        ctx.w_dtype)
             loop.release()
         return (gx, gw, None, gb) + (None, ) * 5
 
@@ -511,6 +533,9 @@ def slot_pair_lists(op, S):
 
 
 SLOT_WGRAD_SPLITS = 64
+# Loop-folded slot weight gradient handed to the stacked-weight node in
+# slot-major layout (weight / root views; no permute + unpack kernels).
+SLOT_HANDOFF = os.environ.get('DGMC_AMD_SLOT_HANDOFF', '1') == '1'
 _SLOT_WGRAD_MAX_LIST = 16    # pointer table size (csrc/hip/slot_wgrad.hip)
 
 

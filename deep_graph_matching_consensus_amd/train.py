@@ -29,6 +29,7 @@ import torch
 from . import parallel
 from .datasets.device_loader import DevicePairLoader
 from .datasets.static_batch import StaticPairBatcher, bucket_capacities
+from .runtime import streams
 from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
 from .runtime.tuning import use_tuned_gemms
@@ -37,6 +38,11 @@ from .runtime.tuning import use_tuned_gemms
 # the flat buffer by one kernel (DGMC_AMD_STEAL_GRADS=0: zeroed flat views +
 # per-parameter accumulation).
 STEAL_GRADS = os.environ.get('DGMC_AMD_STEAL_GRADS', '1') == '1'
+# Loop-folded weight gradients on a side stream (runtime/streams.py).  Off by
+# default: the hipGraph executor maps the captured branches onto its own
+# queues and serialised them against the psi_1 backward in our measurements
+# (169.5k vs 170.6k pairs/s same-box), so there is no gain to take yet.
+SIDE_STREAMS = os.environ.get('DGMC_AMD_SIDE_STREAMS', '0') == '1'
 
 
 class PairTrainer(object):
@@ -193,7 +199,12 @@ class PairTrainer(object):
         else:
             self.reducer.zero_grad()
         batch = self.batchers[bucket].materialize()
-        self._forward_backward(batch, self._rows[bucket], batch.y_mask)
+        # Loop-folded weight gradients run on a side stream (overlapping the
+        # psi_1 backward); joined before the gradients are packed.  Needs the
+        # stolen-gradient path (no main-stream AccumulateGrad kernels).
+        with streams.side_streams(SIDE_STREAMS and STEAL_GRADS and
+                                  self.device.type == 'cuda'):
+            self._forward_backward(batch, self._rows[bucket], batch.y_mask)
         if STEAL_GRADS:
             self.reducer.pack_grads()
         if self.world == 1:

@@ -36,3 +36,38 @@ def test_training_is_bitwise_deterministic(mode):
     assert s1['loss_sum'] == s2['loss_sum']
     for k in p1:
         assert torch.equal(p1[k], p2[k]), k
+
+
+def _run_slot(side, steps=3):
+    """Flagship-shaped psi_2 (128 -> 128: fused slot conv, loop-folded slot
+    weight gradients) in the captured step."""
+    from deep_graph_matching_consensus_amd import train
+    old = train.SIDE_STREAMS
+    train.SIDE_STREAMS = side
+    try:
+        groups = make_keypoint_datasets(graphs=16, feature_dim=64, seed=7)
+        store = GraphStore(groups, 'cuda')
+        torch.manual_seed(0)
+        torch.cuda.manual_seed(0)
+        model = DGMC(SplineCNN(64, 64, 2, 2, cat=False, dropout=0.5),
+                     SplineCNN(128, 128, 2, 2, cat=True), num_steps=4).cuda()
+        tr = PairTrainer(model, store, 32, mode='graph', bf16=True, seed=0)
+        torch.manual_seed(1)
+        torch.cuda.manual_seed(1)
+        for _ in range(steps):
+            tr.step()
+        torch.cuda.synchronize()
+        return tr.read_stats(), {k: v.detach().clone()
+                                 for k, v in model.state_dict().items()}
+    finally:
+        train.SIDE_STREAMS = old
+
+
+def test_side_stream_branch_matches_single_stream():
+    """The side-stream weight-gradient branch (runtime/streams.py) changes
+    where kernels run, not what they compute: bitwise equal to one stream."""
+    s1, p1 = _run_slot(True)
+    s0, p0 = _run_slot(False)
+    assert s1['loss_sum'] == s0['loss_sum']
+    for k in p1:
+        assert torch.equal(p1[k], p0[k]), k
