@@ -1154,12 +1154,14 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     float* __restrict__ G_out, __bf16* __restrict__ dP,
     __bf16* __restrict__ dQ, float* __restrict__ dw2_part,
-    float* __restrict__ db2_part, int Ns, int Nt, int rows_s, int rows_t) {
+    float* __restrict__ db2_part, float* __restrict__ part, int accumulate,
+    int Ns, int Nt, int rows_s, int rows_t) {
   using G = StepGeom<R>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS float* sR = (DGMC_LDS float*)smem_raw;
   DGMC_LDS float* sGt = sR + Ns * G::PP;
-  const int region1 = max(TRANS ? (Ns + Nt) * G::PP : 0, CONS ? G::RG * R : 0);
+  const int region1 =
+      max(TRANS ? (Ns + Nt) * G::PP : 0, CONS ? 2 * G::RG * R : 0);
   DGMC_LDS float* sP = sR + region1;
   DGMC_LDS float* sQ = sP + (CONS ? Ns * R : 0);
   DGMC_LDS float* sD = sQ + (CONS ? Nt * R : 0);
@@ -1280,14 +1282,21 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
   gsum = wave_sum_dpp(gsum);
   if (lane == 0) sSum[wave] = gsum;
   __syncthreads();
+  // Parameter-gradient partials of this pair: into [db1 | dw2 | db2] row b
+  // of ``part`` (accumulated over the loop's uses in backward order: one
+  // column sum at the end instead of per-use lists), else dw2 / db2 rows.
+  float* pb = part ? part + (size_t)b * (2 * R + 1) : nullptr;
   if (tid == 0) {
     float t = 0.f;
     for (int w = 0; w < kWaves; ++w) t += sSum[w];
-    db2_part[b] = t;
+    if (pb)
+      pb[2 * R] = (accumulate ? pb[2 * R] : 0.f) + t;
+    else
+      db2_part[b] = t;
   }
 
-  // Phase 2: dP / dQ rows (one channel quad per lane), dw2 partials.
-  ps_f32x4 dw = {0.f, 0.f, 0.f, 0.f};
+  // Phase 2: dP / dQ rows (one channel quad per lane), dw2 / db1 partials.
+  ps_f32x4 dw = {0.f, 0.f, 0.f, 0.f}, db1v = {0.f, 0.f, 0.f, 0.f};
   for (int r = rg; r < ns + nt; r += G::RG) {
     ps_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (r < ns) {
@@ -1304,6 +1313,7 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
         }
       }
       acc *= wv;
+      db1v += acc;
       *reinterpret_cast<ps_bf16x4*>(dP + ((size_t)s0 + i) * R + 4 * cq) =
           ps_bf16x4{(__bf16)acc[0], (__bf16)acc[1], (__bf16)acc[2],
                     (__bf16)acc[3]};
@@ -1323,11 +1333,21 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
     }
   }
   *reinterpret_cast<DGMC_LDS ps_f32x4*>(sRed + rg * R + 4 * cq) = dw;
+  *reinterpret_cast<DGMC_LDS ps_f32x4*>(sRed + (G::RG + rg) * R + 4 * cq) =
+      db1v;
   __syncthreads();
   for (int c = tid; c < R; c += kThreads) {
-    float s = 0.f;
-    for (int r = 0; r < G::RG; ++r) s += sRed[r * R + c];
-    dw2_part[(size_t)b * R + c] = s;
+    float s = 0.f, s1 = 0.f;
+    for (int r = 0; r < G::RG; ++r) {
+      s += sRed[r * R + c];
+      s1 += sRed[(G::RG + r) * R + c];
+    }
+    if (pb) {
+      pb[c] = (accumulate ? pb[c] : 0.f) + s1;
+      pb[R + c] = (accumulate ? pb[R + c] : 0.f) + s;
+    } else {
+      dw2_part[(size_t)b * R + c] = s;
+    }
   }
 }
 
@@ -1342,7 +1362,7 @@ template <int R>
 static size_t step_bwd_lds(bool cons, bool trans, int Ns, int Nt) {
   using G = StepGeom<R>;
   return (size_t)std::max(trans ? (Ns + Nt) * G::PP : 0,
-                          cons ? G::RG * R : 0) +
+                          cons ? 2 * G::RG * R : 0) +
          (cons ? (size_t)(Ns + Nt) * R : 0) + (size_t)Ns * Nt + kWaves;
 }
 
@@ -1436,6 +1456,8 @@ struct StepBwdArgs {
   __bf16 *dP, *dQ;
   float *dw2_part, *db2_part;
   int B, Ns, Nt, rows_s, rows_t;
+  float* part = nullptr;       // [B, 2R + 1] loop-accumulated partials
+  int accumulate = 0;
 };
 
 template <int R, bool C, bool T>
@@ -1456,7 +1478,7 @@ static void step_bwd_launch(const StepBwdArgs& a) {
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S,
                      a.r_s, a.g_t, a.addend, a.P, a.Q, a.b1, a.w2, a.ptr_s,
                      a.ptr_t, a.G_out, a.dP, a.dQ, a.dw2_part, a.db2_part,
-                     a.Ns, a.Nt, a.rows_s, a.rows_t);
+                     a.part, a.accumulate, a.Ns, a.Nt, a.rows_s, a.rows_t);
   DGMC_CHECK_LAUNCH();
 }
 
@@ -1662,10 +1684,36 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
   return out;
 }
 
+// part (optional, fp32 [B, 2R + 1]): the fast kernels write the per-pair
+// [db1 | dw2 | db2] partials there (added to the existing rows when
+// ``accumulate``) and return undefined dw2 / db2.
+static float* step_part(const c10::optional<at::Tensor>& part, int B, int R,
+                        const at::Tensor& like) {
+  if (!part.has_value() || !part->defined()) return nullptr;
+  TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                  part->dim() == 2 && part->size(0) == B &&
+                  part->size(1) == 2 * R + 1 &&
+                  part->device() == like.device(),
+              "pair step: part must be fp32 [B, 2R + 1]");
+  return part->data_ptr<float>();
+}
+
+// Generic-kernel fallback of the ``part`` contract (only its column sums
+// matter: the P-row sum of dP goes into row 0).
+static void fold_part_generic(at::Tensor part, bool accumulate,
+                              const at::Tensor& dP, const at::Tensor& dw2,
+                              const at::Tensor& db2, int R) {
+  if (!accumulate) part.zero_();
+  part.select(0, 0).narrow(0, 0, R).add_(dP.to(at::kFloat).sum(0));
+  part.narrow(1, R, R).add_(dw2);
+  part.narrow(1, 2 * R, 1).add_(db2.view({-1, 1}));
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out) {
+    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out,
+    const c10::optional<at::Tensor>& part, bool accumulate) {
   check_pair_tensor(G, "grad");
   check_packed(P, "P");
   check_packed(Q, "Q");
@@ -1699,7 +1747,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
                   ptr_t.data_ptr<int>(), nullptr, bf16_ptr(dP), bf16_ptr(dQ),
                   dw2.data_ptr<float>(), db2.data_ptr<float>(), B, Ns, Nt,
                   (int)P.size(0), (int)Q.size(0)};
+    a.part = step_part(part, B, R, G);
+    a.accumulate = accumulate ? 1 : 0;
     step_bwd<true, false>(R, a);
+    if (a.part) return {dP, dQ, at::Tensor(), at::Tensor()};
     return {dP, dQ, dw2, db2};
   }
   const int vec = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
@@ -1720,6 +1771,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
                        (int)P.size(0), (int)Q.size(0), vec);
   });
   DGMC_CHECK_LAUNCH();
+  if (step_part(part, B, R, G)) {
+    fold_part_generic(*part, accumulate, dP, dw2, db2, R);
+    return {dP, dQ, at::Tensor(), at::Tensor()};
+  }
   return {dP, dQ, dw2, db2};
 }
 
@@ -1803,7 +1858,9 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                               const at::Tensor& P, const at::Tensor& Q,
                               const at::Tensor& b1, const at::Tensor& w2,
                               const at::Tensor& ptr_s, const at::Tensor& ptr_t,
-                              const c10::optional<at::Tensor>& dpq_out) {
+                              const c10::optional<at::Tensor>& dpq_out,
+                              const c10::optional<at::Tensor>& part,
+                              bool accumulate) {
   check_pair_tensor(S_prob, "S");
   check_packed(r_s, "r_s");
   check_packed(g_t, "grad r_t");
@@ -1856,7 +1913,10 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                   ptr_t.data_ptr<int>(), G.data_ptr<float>(), bf16_ptr(dP),
                   bf16_ptr(dQ), dw2.data_ptr<float>(), db2.data_ptr<float>(),
                   B, Ns, Nt, (int)P.size(0), (int)Q.size(0)};
+    a.part = step_part(part, B, R, S_prob);
+    a.accumulate = accumulate ? 1 : 0;
     step_bwd<true, true>(R, a);
+    if (a.part) return {G, dP, dQ, at::Tensor(), at::Tensor()};
     return {G, dP, dQ, dw2, db2};
   }
   using T = __hip_bfloat16;
@@ -1878,6 +1938,10 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                      dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R,
                      (int)P.size(0), (int)Q.size(0), vec_r, vec_pq);
   DGMC_CHECK_LAUNCH();
+  if (step_part(part, B, R, S_prob)) {
+    fold_part_generic(*part, accumulate, dP, dw2, db2, R);
+    return {G, dP, dQ, at::Tensor(), at::Tensor()};
+  }
   return {G, dP, dQ, dw2, db2};
 }
 

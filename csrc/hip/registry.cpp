@@ -45,7 +45,8 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& G, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out);
+    const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out,
+    const c10::optional<at::Tensor>& part, bool accumulate);
 
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
                     bool exact);
@@ -161,7 +162,9 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                               const at::Tensor& P, const at::Tensor& Q,
                               const at::Tensor& b1, const at::Tensor& w2,
                               const at::Tensor& ptr_s, const at::Tensor& ptr_t,
-                              const c10::optional<at::Tensor>& dpq_out);
+                              const c10::optional<at::Tensor>& dpq_out,
+                              const c10::optional<at::Tensor>& part,
+                              bool accumulate);
 std::tuple<at::Tensor, at::Tensor> softmax_nll_fwd(
     const at::Tensor& S_hat, const c10::optional<at::Tensor>& S_hat2,
     const at::Tensor& ptr_s, const at::Tensor& n_t, const at::Tensor& y,
@@ -222,8 +225,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor b2, Tensor ptr_s, Tensor ptr_t) -> Tensor");
   m.def(
       "dense_consensus_bwd(Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
-      "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None) -> (Tensor, "
-      "Tensor, Tensor, Tensor)");
+      "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None, Tensor(b!)? "
+      "part=None, bool accumulate=False) -> (Tensor, Tensor, Tensor, "
+      "Tensor)");
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k, bool exact=False) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
@@ -290,8 +294,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "dense_transport_consensus_bwd(Tensor S, Tensor r_s, Tensor g_t, "
       "Tensor? addend, Tensor P, Tensor Q, Tensor b1, Tensor w2, Tensor "
-      "ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None) -> (Tensor, Tensor, "
-      "Tensor, Tensor, Tensor)");
+      "ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None, Tensor(b!)? part=None, "
+      "bool accumulate=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "softmax_nll_fwd(Tensor S_hat, Tensor? S_hat2, Tensor ptr_s, Tensor "
       "n_t, Tensor y, Tensor? mask, float eps, Tensor(a!)? stats=None) -> "

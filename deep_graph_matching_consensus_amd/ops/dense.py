@@ -302,10 +302,12 @@ class _ConsensusUpdate(torch.autograd.Function):
         if ctx.split is not None:
             dPQ = torch.empty((P.size(0) + Q.size(0), P.size(1)),
                               dtype=P.dtype, device=P.device)
+        part, accum = _loop_part(ctx.loop, grad.size(0), P.size(1),
+                                 grad.device)
         dP, dQ, dw2_part, db2_part = _backend.ops().dense_consensus_bwd(
             grad.float().contiguous(), P.contiguous(), Q.contiguous(),
             b1.float().contiguous(), w2.float().contiguous().view(-1), ptr_s,
-            ptr_t, dPQ)
+            ptr_t, dPQ, part, accum)
         dP_rows = dP                    # db1 = column sum over P rows only
         if dPQ is not None:
             dP, dQ = dPQ, None
@@ -356,11 +358,12 @@ class _ConsensusTransport(torch.autograd.Function):
             add = g_S.float().contiguous()
         dPQ = torch.empty((P.size(0) + Q.size(0), R), dtype=P.dtype,
                           device=P.device)
+        part, accum = _loop_part(ctx.loop, S_prob.size(0), R, P.device)
         G, dP, _, dw2_part, db2_part = \
             _backend.ops().dense_transport_consensus_bwd(
                 S_prob, r_s.contiguous(), g_t, add, P, Q,
                 b1.float().contiguous(), w2.float().contiguous().view(-1),
-                ptr_s, ptr_t, dPQ)
+                ptr_s, ptr_t, dPQ, part, accum)
         s_dt, b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
         db1, dw2, db2 = _consensus_param_grads(
             ctx.loop, ctx.idx, dP, dw2_part, db2_part)
@@ -372,21 +375,29 @@ class _ConsensusTransport(torch.autograd.Function):
                 None)
 
 
-def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
-    """``(db1, dw2, db2)`` of one consensus use - folded over all loop uses
-    by the use completing the set (``None`` for the others)."""
-    parts = (('b1', dP), ('w2', dw2_part), ('b2', db2_part.view(-1, 1)))
+def _loop_part(loop, B, R, device):
+    """``(part, accumulate)``: the loop's ``[B, 2R + 1]`` fp32 accumulator of
+    per-pair ``[db1 | dw2 | db2]`` partials, written by the backward kernels
+    of every use in turn (``(None, False)`` outside a loop)."""
     if loop is None:
-        return tuple(_col_sum(t) for _, t in parts)
-    for name, t in parts:
-        loop.keep(name, idx, t)
+        return None, False
+    return loop.acc('pq_part', (B, 2 * R + 1), device)
+
+
+def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
+    """``(db1, dw2, db2)`` of one consensus use; inside a loop the kernels
+    accumulated them into the loop's part buffer and the use completing the
+    set folds it with ONE column sum (``None`` for the others)."""
+    if loop is None:
+        parts = (dP, dw2_part, db2_part.view(-1, 1))
+        return tuple(_col_sum(t) for t in parts)
     if loop.arrive():
-        # Parameter gradients only (b1, w2, b2): side-stream branch.
-        lists = [loop.kept_list(n) for n, _ in parts]
-        with streams.side(dP.device, lists):
-            out = tuple(_col_sum(loop.kept(n)) for n, _ in parts)
+        part = loop.get_acc('pq_part')
+        R = (part.size(1) - 1) // 2
+        with streams.side(part.device, (part, )):
+            tot = _col_sum(part)
         loop.release()
-        return out
+        return tot[:R], tot[R:2 * R], tot[2 * R:]
     return None, None, None
 
 

@@ -1166,6 +1166,24 @@ def test_step_boundary_kernels_vs_fp32(R, Ns, Nt, B):
     assert (joint[rows_s + int(d['ptr_t'][-1]):] == 0).all()
     torch.testing.assert_close(G, ref['gS'], atol=1e-3, rtol=1e-3)
     _check_cons_grads(d, ref, dP, dQ, dw2, db2)
+    # Loop accumulator contract: [db1 | dw2 | db2] per pair, added over uses.
+    part = torch.full((B, 2 * R + 1), float('nan'), device=DEV)
+    for accumulate in (False, True):
+        out = ops.dense_transport_consensus_bwd(
+            S_prob, d['r_s'], d['g_t'], d['add'], d['P'], d['Q'], d['b1'],
+            d['w2'], d['ps'], d['pt'], None, part, accumulate)
+        assert out[3] is None and out[4] is None
+        torch.testing.assert_close(out[1], dP, atol=0, rtol=0)
+    tot = part.sum(0)
+    # (db1 from the fp32 dP rows: closer to the fp32 reference than the sum
+    # of the bf16-rounded dP output)
+    # (generic kernels: sum of the bf16 dP rows)
+    tol = 5e-3 if R in (32, 64, 128) else 0.1
+    torch.testing.assert_close(tot[:R], 2 * ref['gb1'], atol=tol, rtol=2e-2)
+    torch.testing.assert_close(tot[R:2 * R], 2 * dw2.sum(0), atol=2e-3,
+                               rtol=1e-3)
+    torch.testing.assert_close(tot[2 * R], 2 * db2.sum(), atol=2e-3,
+                               rtol=1e-3)
 
 
 @pytest.mark.parametrize('R', [32, 128, 48])
@@ -1184,6 +1202,15 @@ def test_step_kernels_split_vs_fp32(R, Ns, Nt, B):
     dP, dQ, dw2, db2 = ops.dense_consensus_bwd(
         d['add'], d['P'], d['Q'], d['b1'], d['w2'], d['ps'], d['pt'], None)
     _check_cons_grads(d, ref, dP, dQ, dw2, db2)
+    part = torch.full((B, 2 * R + 1), float('nan'), device=DEV)
+    out = ops.dense_consensus_bwd(d['add'], d['P'], d['Q'], d['b1'],
+                                  d['w2'], d['ps'], d['pt'], None, part, False)
+    assert out[2] is None and out[3] is None
+    tot = part.sum(0)
+    tol = 5e-3 if R in (32, 64, 128) else 0.1
+    torch.testing.assert_close(tot[:R], ref['gb1'], atol=tol, rtol=2e-2)
+    torch.testing.assert_close(tot[R:2 * R], dw2.sum(0), atol=2e-3,
+                               rtol=1e-3)
     # transport only (plain and joint output)
     ref = _step_ref(d, False, True)
     rows_s = d['rows_s']
