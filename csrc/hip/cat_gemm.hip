@@ -77,11 +77,30 @@ __global__ __launch_bounds__(kCgWaves * 64, 1) void cat_gemm_kernel(
   const int tile0 = wave * gridDim.x + blockIdx.x;
   if (tile0 < ntiles) load_a(tile0);
 
-  // Stage W [N, K] (16-byte chunks).
-  for (int c = tid; c < N * K / 8; c += kCgWaves * 64) {
-    const int n = c / (K / 8), k8 = c - n * (K / 8);
-    *reinterpret_cast<DGMC_LDS cg_bf16x8*>(Ws + n * WP + 8 * k8) =
-        *reinterpret_cast<const cg_bf16x8*>(W + (int64_t)n * K + 8 * k8);
+  // Stage W [N, K] (16-byte chunks): every chunk of this thread is requested
+  // before the first LDS store (one memory round trip instead of one per
+  // chunk - the loop form waited on each load before its store).
+  {
+    constexpr int kChunks = N * K / 8;
+    constexpr int kPer = (kChunks + kCgWaves * 64 - 1) / (kCgWaves * 64);
+    cg_bf16x8 wv[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int c = tid + u * kCgWaves * 64;
+      if (c < kChunks) {
+        const int n = c / (K / 8), k8 = c - n * (K / 8);
+        wv[u] = *reinterpret_cast<const cg_bf16x8*>(W + (int64_t)n * K +
+                                                     8 * k8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int c = tid + u * kCgWaves * 64;
+      if (c < kChunks) {
+        const int n = c / (K / 8), k8 = c - n * (K / 8);
+        *reinterpret_cast<DGMC_LDS cg_bf16x8*>(Ws + n * WP + 8 * k8) = wv[u];
+      }
+    }
   }
   __syncthreads();
 
