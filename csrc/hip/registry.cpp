@@ -108,6 +108,7 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const c10::optional<at::Tensor>& Z);
 at::Tensor gather_gemm_stamps();
 at::Tensor slot_conv_stamps();
+at::Tensor dense_wgrad(at::TensorList xs, at::TensorList gs, int64_t nsplit);
 at::Tensor tr16_probe(const at::Tensor& like);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_pair_lists(
     const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& val,
@@ -267,6 +268,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
   m.def("gather_gemm_stamps() -> Tensor");
   m.def("slot_conv_stamps() -> Tensor");
+  m.def("dense_wgrad(Tensor[] xs, Tensor[] gs, int nsplit) -> Tensor");
   m.def("tr16_probe(Tensor like) -> Tensor");
   m.def(
       "slot_pair_lists(Tensor rowptr, Tensor col, Tensor val, Tensor row, int "
@@ -389,6 +391,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("pair_scores_bwd", &dgmc::pair_scores_bwd);
   m.impl("spline_slot_images", &dgmc::spline_slot_images);
   m.impl("tr16_probe", &dgmc::tr16_probe);
+  m.impl("dense_wgrad", &dgmc::dense_wgrad);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);

@@ -298,6 +298,153 @@ at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
 
 namespace dgmc {
 
+// ---------------------------------------------------------------------------
+// Dense TN weight gradient over loop uses, the same MFMA pipeline without the
+// entry lists:
+//
+//   dW_s = sum_u X_u[:, 128 s : 128 s + 128]^T G_u          (s < S, 128x128)
+//
+// for X_u [N, 128 S] (row stride ldx) and G_u [N, 128] (row stride 128): the
+// weight gradient of a K = 128 S -> 128 projection summed over the loop's
+// uses (the folded consensus projection, ops/dense.py::_CatMatmul), read in
+// place (no concatenation of the kept gradients, no split-K GEMM over a
+// 10x-long K at hipBLASLt's 0.16 PF/s on this skinny shape).  Workgroup =
+// (block s, split); each split walks a contiguous row-chunk range, all uses
+// per chunk.
+// ---------------------------------------------------------------------------
+struct DwUses {
+  const __bf16* x[kSwMaxU];
+  const __bf16* g[kSwMaxU];
+};
+
+__global__ __launch_bounds__(kSwThreads, 1) void dense_wgrad_kernel(
+    const DwUses P, int U, int N, int64_t ldx, int S, int nsplit,
+    float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][kSwTile * 2];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int k = blockIdx.x / nsplit, s = blockIdx.x % nsplit;
+  const int nch = (N + kSwK - 1) / kSwK;
+  const int ch0 = (int)((long long)nch * s / nsplit);
+  const int ch1 = (int)((long long)nch * (s + 1) / nsplit);
+  const int r = tid >> 4, c = tid & 15;
+  const int mi = wave >> 2, nw = wave & 3;
+  sw_f32x4 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
+  sw_bf16x8 xr[2], gr[2];
+  const int steps = (ch1 - ch0) * U;
+  int iu = 0, ic = ch0;
+  auto issue = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value;
+    const int row = ic * kSwK + r;
+    const bool in = row < N && ic < ch1;     // padding rows contribute 0
+    const int rr = in ? row : 0;
+    const sw_bf16x8 z = {};
+    const sw_bf16x8 xv = *reinterpret_cast<const sw_bf16x8*>(
+        P.x[iu] + (size_t)rr * ldx + 128 * k + 8 * c);
+    const sw_bf16x8 gv = *reinterpret_cast<const sw_bf16x8*>(
+        P.g[iu] + (size_t)rr * kSwC + 8 * c);
+    xr[slot] = in ? xv : z;
+    gr[slot] = in ? gv : z;
+    const bool wrap = iu + 1 == U;
+    iu = wrap ? 0 : iu + 1;
+    ic += wrap ? 1 : 0;
+  };
+  auto stage = [&](auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value, buf = slot;
+    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+        (DGMC_LDS char*)lds[buf][0] + sw_off(r, c)) = xr[slot];
+    *reinterpret_cast<DGMC_LDS sw_bf16x8*>(
+        (DGMC_LDS char*)lds[buf][1] + sw_off(r, c)) = gr[slot];
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  issue(S0{});
+  issue(S1{});
+  stage(S0{});
+  __syncthreads();
+  auto step = [&](auto buf_c) __attribute__((always_inline)) {
+    constexpr int buf = decltype(buf_c)::value;
+    issue(buf_c);
+    const DGMC_LDS char* A = (const DGMC_LDS char*)lds[buf][0];
+    const DGMC_LDS char* B = (const DGMC_LDS char*)lds[buf][1];
+    sw_bf16x8 af[4], bf[2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) af[a] = sw_frag(A, 4 * mi + a, lane);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) bf[b] = sw_frag(B, 2 * nw + b, lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf[b],
+                                                            acc[a][b], 0, 0,
+                                                            0);
+    stage(std::integral_constant<int, buf ^ 1>{});
+    __syncthreads();
+  };
+  // Steps past `steps` (odd count) read past ch1: zero rows.
+  for (int t = 0; t < steps; t += 2) {
+    step(S0{});
+    step(S1{});
+  }
+  float* out = part + ((size_t)s * S + k) * kSwC * kSwC;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 64 * mi + 16 * a + 4 * (lane >> 4) + q;
+        const int colo = 32 * nw + 16 * b + (lane & 15);
+        out[(size_t)row * kSwC + colo] = acc[a][b][q];
+      }
+}
+
+// xs[u] [N, 128 S] bf16 (unit column stride, 16-byte aligned rows), gs[u]
+// [N, 128] bf16 contiguous; returns per-split partials [nsplit, S*128*128]
+// fp32 of dW [S, 128, 128] = [128 S, 128] (X column, output).
+at::Tensor dense_wgrad(at::TensorList xs, at::TensorList gs, int64_t nsplit) {
+  const int64_t U = (int64_t)xs.size();
+  TORCH_CHECK(U >= 1 && U <= kSwMaxU && (int64_t)gs.size() == U,
+              "dense_wgrad: 1 <= uses <= 16, one G per X");
+  const int64_t N = xs[0].size(0);
+  TORCH_CHECK(xs[0].dim() == 2 && xs[0].size(1) % kSwC == 0 &&
+                  xs[0].size(1) >= kSwC,
+              "dense_wgrad: X [N, 128 S]");
+  const int64_t S = xs[0].size(1) / kSwC;
+  const int64_t ldx = xs[0].stride(0);
+  DwUses P{};
+  for (int u = 0; u < U; ++u) {
+    const at::Tensor& x = xs[u];
+    const at::Tensor& g = gs[u];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 &&
+                    x.dim() == 2 && x.size(0) == N &&
+                    x.size(1) == S * kSwC && x.stride(1) == 1 &&
+                    x.stride(0) == ldx && ldx % 8 == 0 &&
+                    aligned16(x.data_ptr()),
+                "dense_wgrad: X_u bf16 [N, 128 S], equal 16-byte row strides");
+    TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kBFloat16 &&
+                    g.is_contiguous() && g.dim() == 2 && g.size(0) == N &&
+                    g.size(1) == kSwC && aligned16(g.data_ptr()),
+                "dense_wgrad: G_u contiguous bf16 [N, 128]");
+    P.x[u] = reinterpret_cast<const __bf16*>(x.data_ptr());
+    P.g[u] = reinterpret_cast<const __bf16*>(g.data_ptr());
+  }
+  TORCH_CHECK(nsplit >= 1 && S * nsplit < (1 << 30) && N < INT32_MAX / kSwC,
+              "dense_wgrad: size range");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(xs[0].device());
+  at::Tensor part = at::empty({nsplit, S * kSwC * kSwC},
+                              xs[0].options().dtype(at::kFloat));
+  hipLaunchKernelGGL(dense_wgrad_kernel, dim3(S * nsplit), dim3(kSwThreads),
+                     0, stream(), P, (int)U, (int)N, ldx, (int)S, (int)nsplit,
+                     part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return part;
+}
+
 // Probe of ds_read_b64_tr_b16 semantics (tools/debug/wgrad_debug.py): LDS
 // tile [16 rows][16 cols] int16 = 100 * row + col; lane 4q+p of each 16-lane
 // group addresses row (q + 4 * (group & 1)), columns 4p..4p+3.  Returns the

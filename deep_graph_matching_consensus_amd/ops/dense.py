@@ -464,10 +464,44 @@ class _CatMatmul(torch.autograd.Function):
                     X = loop.stack('x')
                     gl = loop.kept_list('g')
                     with streams.side(g.device, (X, gl)):
-                        gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
-                                            loop.kept('g')).to(ctx.w_dtype)
+                        if dense_wgrad_supported(X, gl):
+                            gw = dense_wgrad(list(X.unbind(0)), gl).to(
+                                ctx.w_dtype)
+                        else:
+                            gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
+                                                loop.kept('g')).to(
+                                                    ctx.w_dtype)
                 loop.release()
         return (gw, None, None, None, None) + tuple(grads)
+
+
+DENSE_WGRAD = os.environ.get('DGMC_AMD_DENSE_WGRAD', '1') == '1'
+
+
+def dense_wgrad_supported(X, gs):
+    return (DENSE_WGRAD and _backend.use_hip(X) and X.dtype == torch.bfloat16
+            and X.dim() == 3 and X.size(-1) % 128 == 0 and
+            X.size(-1) <= 512 and X.is_contiguous() and
+            X.data_ptr() % 16 == 0 and len(gs) == X.size(0) and
+            all(g.dtype == torch.bfloat16 and g.is_contiguous() and
+                g.shape == (X.size(1), 128) and g.data_ptr() % 16 == 0
+                for g in gs))
+
+
+def dense_wgrad(xs, gs, nsplit=None):
+    r"""``sum_u xs[u]^T gs[u]`` (fp32 ``[K, 128]``) for bf16 ``xs[u] [N, K]``
+    (K = 128 S) and ``gs[u] [N, 128]`` read in place
+    (csrc/hip/slot_wgrad.hip::dense_wgrad: TN MFMA over row chunks,
+    per-split partials folded by ``reduce_add_rows``)."""
+    K = xs[0].size(1)
+    S = K // 128
+    nsplit = nsplit or max(1, 256 // S)
+    out = torch.empty(K * 128, dtype=torch.float32, device=xs[0].device)
+    for i in range(0, len(xs), 16):
+        part = _backend.ops().dense_wgrad(list(xs[i:i + 16]),
+                                          list(gs[i:i + 16]), nsplit)
+        _backend.ops().reduce_add_rows(part.view(nsplit, K * 128), out, i > 0)
+    return out.view(K, 128)
 
 
 def cat_matmul_supported(parts, w_t):

@@ -1228,3 +1228,18 @@ def test_step_kernels_split_vs_fp32(R, Ns, Nt, B):
     g = ops.dense_softmax_transport_bwd(S, d['r_s'], d['g_t'], d['ps'],
                                         d['pt'], d['add'])
     torch.testing.assert_close(g, ref['gS'], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize('U,N,K', [(10, 1000, 384), (3, 77, 128),
+                                   (17, 300, 256)])
+def test_dense_wgrad_matches_fp32(U, N, K):
+    """Loop-use TN weight gradient on MFMA (dense_wgrad) == fp32 sum of
+    X_u^T G_u, incl. a use count above the 16-entry pointer table."""
+    torch.manual_seed(U + N)
+    X = torch.randn(U, N, K, device=DEV).bfloat16()
+    gs = [torch.randn(N, 128, device=DEV).bfloat16() for _ in range(U)]
+    assert dense_ops.dense_wgrad_supported(X, gs)
+    got = dense_ops.dense_wgrad(list(X.unbind(0)), gs)
+    ref_ = sum(x.float().t() @ g.float() for x, g in zip(X.unbind(0), gs))
+    torch.testing.assert_close(got, ref_, atol=2e-3 * N ** 0.5 * U ** 0.5,
+                               rtol=1e-3)
