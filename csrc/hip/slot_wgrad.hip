@@ -318,11 +318,12 @@ struct DwUses {
 };
 
 __global__ __launch_bounds__(kSwThreads, 1) void dense_wgrad_kernel(
-    const DwUses P, int U, int N, int64_t ldx, int S, int nsplit,
-    float* __restrict__ part) {
+    const DwUses P, int U, int N, int64_t ldx, int64_t ldg, int Sx, int Sg,
+    int nsplit, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][kSwTile * 2];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int k = blockIdx.x / nsplit, s = blockIdx.x % nsplit;
+  const int kx = k / Sg, kg = k - kx * Sg;   // 128x128 output block
   const int nch = (N + kSwK - 1) / kSwK;
   const int ch0 = (int)((long long)nch * s / nsplit);
   const int ch1 = (int)((long long)nch * (s + 1) / nsplit);
@@ -343,9 +344,9 @@ __global__ __launch_bounds__(kSwThreads, 1) void dense_wgrad_kernel(
     const int rr = in ? row : 0;
     const sw_bf16x8 z = {};
     const sw_bf16x8 xv = *reinterpret_cast<const sw_bf16x8*>(
-        P.x[iu] + (size_t)rr * ldx + 128 * k + 8 * c);
+        P.x[iu] + (size_t)rr * ldx + 128 * kx + 8 * c);
     const sw_bf16x8 gv = *reinterpret_cast<const sw_bf16x8*>(
-        P.g[iu] + (size_t)rr * kSwC + 8 * c);
+        P.g[iu] + (size_t)rr * ldg + 128 * kg + 8 * c);
     xr[slot] = in ? xv : z;
     gr[slot] = in ? gv : z;
     const bool wrap = iu + 1 == U;
@@ -390,7 +391,10 @@ __global__ __launch_bounds__(kSwThreads, 1) void dense_wgrad_kernel(
     step(S0{});
     step(S1{});
   }
-  float* out = part + ((size_t)s * S + k) * kSwC * kSwC;
+  // Partial [split][128 Sx][128 Sg] (row-major dW block).
+  const int Kg = kSwC * Sg;
+  float* out = part + (size_t)s * kSwC * Sx * Kg + (size_t)kSwC * kx * Kg +
+               kSwC * kg;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -399,47 +403,49 @@ __global__ __launch_bounds__(kSwThreads, 1) void dense_wgrad_kernel(
       for (int q = 0; q < 4; ++q) {
         const int row = 64 * mi + 16 * a + 4 * (lane >> 4) + q;
         const int colo = 32 * nw + 16 * b + (lane & 15);
-        out[(size_t)row * kSwC + colo] = acc[a][b][q];
+        out[(size_t)row * Kg + colo] = acc[a][b][q];
       }
 }
 
-// xs[u] [N, 128 S] bf16 (unit column stride, 16-byte aligned rows), gs[u]
-// [N, 128] bf16 contiguous; returns per-split partials [nsplit, S*128*128]
-// fp32 of dW [S, 128, 128] = [128 S, 128] (X column, output).
+// xs[u] [N, 128 Sx], gs[u] [N, 128 Sg] bf16 (unit column stride, equal
+// 16-byte aligned row strides per list); returns per-split partials
+// [nsplit, 128 Sx * 128 Sg] fp32 of dW = sum_u xs[u]^T gs[u].
 at::Tensor dense_wgrad(at::TensorList xs, at::TensorList gs, int64_t nsplit) {
   const int64_t U = (int64_t)xs.size();
   TORCH_CHECK(U >= 1 && U <= kSwMaxU && (int64_t)gs.size() == U,
               "dense_wgrad: 1 <= uses <= 16, one G per X");
   const int64_t N = xs[0].size(0);
   TORCH_CHECK(xs[0].dim() == 2 && xs[0].size(1) % kSwC == 0 &&
-                  xs[0].size(1) >= kSwC,
-              "dense_wgrad: X [N, 128 S]");
-  const int64_t S = xs[0].size(1) / kSwC;
-  const int64_t ldx = xs[0].stride(0);
+                  xs[0].size(1) >= kSwC && gs[0].dim() == 2 &&
+                  gs[0].size(1) % kSwC == 0 && gs[0].size(1) >= kSwC,
+              "dense_wgrad: X [N, 128 Sx], G [N, 128 Sg]");
+  const int64_t Sx = xs[0].size(1) / kSwC, Sg = gs[0].size(1) / kSwC;
+  const int64_t ldx = xs[0].stride(0), ldg = gs[0].stride(0);
   DwUses P{};
   for (int u = 0; u < U; ++u) {
     const at::Tensor& x = xs[u];
     const at::Tensor& g = gs[u];
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 &&
-                    x.dim() == 2 && x.size(0) == N &&
-                    x.size(1) == S * kSwC && x.stride(1) == 1 &&
-                    x.stride(0) == ldx && ldx % 8 == 0 &&
-                    aligned16(x.data_ptr()),
-                "dense_wgrad: X_u bf16 [N, 128 S], equal 16-byte row strides");
-    TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kBFloat16 &&
-                    g.is_contiguous() && g.dim() == 2 && g.size(0) == N &&
-                    g.size(1) == kSwC && aligned16(g.data_ptr()),
-                "dense_wgrad: G_u contiguous bf16 [N, 128]");
+    for (const at::Tensor* t : {&x, &g}) {
+      const bool isx = t == &x;
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 &&
+                      t->dim() == 2 && t->size(0) == N &&
+                      t->size(1) == (isx ? Sx : Sg) * kSwC &&
+                      t->stride(1) == 1 && t->stride(0) == (isx ? ldx : ldg) &&
+                      t->stride(0) % 8 == 0 && aligned16(t->data_ptr()),
+                  "dense_wgrad: bf16 operands with equal 16-byte row strides");
+    }
     P.x[u] = reinterpret_cast<const __bf16*>(x.data_ptr());
     P.g[u] = reinterpret_cast<const __bf16*>(g.data_ptr());
   }
-  TORCH_CHECK(nsplit >= 1 && S * nsplit < (1 << 30) && N < INT32_MAX / kSwC,
+  TORCH_CHECK(nsplit >= 1 && Sx * Sg * nsplit < (1 << 30) &&
+                  N < INT32_MAX / kSwC,
               "dense_wgrad: size range");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(xs[0].device());
-  at::Tensor part = at::empty({nsplit, S * kSwC * kSwC},
+  at::Tensor part = at::empty({nsplit, Sx * Sg * kSwC * kSwC},
                               xs[0].options().dtype(at::kFloat));
-  hipLaunchKernelGGL(dense_wgrad_kernel, dim3(S * nsplit), dim3(kSwThreads),
-                     0, stream(), P, (int)U, (int)N, ldx, (int)S, (int)nsplit,
+  hipLaunchKernelGGL(dense_wgrad_kernel, dim3(Sx * Sg * nsplit),
+                     dim3(kSwThreads), 0, stream(), P, (int)U, (int)N, ldx,
+                     ldg, (int)Sx, (int)Sg, (int)nsplit,
                      part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return part;

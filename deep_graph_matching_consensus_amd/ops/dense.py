@@ -488,20 +488,25 @@ def dense_wgrad_supported(X, gs):
                 for g in gs))
 
 
-def dense_wgrad(xs, gs, nsplit=None):
-    r"""``sum_u xs[u]^T gs[u]`` (fp32 ``[K, 128]``) for bf16 ``xs[u] [N, K]``
-    (K = 128 S) and ``gs[u] [N, 128]`` read in place
-    (csrc/hip/slot_wgrad.hip::dense_wgrad: TN MFMA over row chunks,
-    per-split partials folded by ``reduce_add_rows``)."""
-    K = xs[0].size(1)
-    S = K // 128
-    nsplit = nsplit or max(1, 256 // S)
-    out = torch.empty(K * 128, dtype=torch.float32, device=xs[0].device)
+def dense_wgrad(xs, gs, nsplit=None, out=None, accumulate=False):
+    r"""``sum_u xs[u]^T gs[u]`` (fp32 ``[Kx, Kg]``) for bf16 ``xs[u] [N, Kx]``
+    and ``gs[u] [N, Kg]`` (multiples of 128) read in place
+    (csrc/hip/slot_wgrad.hip::dense_wgrad: TN MFMA over row chunks, per-split
+    partials folded by ``reduce_add_rows``, optionally into ``out``)."""
+    Kx, Kg = xs[0].size(1), gs[0].size(1)
+    blocks = (Kx // 128) * (Kg // 128)
+    n = xs[0].size(0)
+    nsplit = nsplit or max(1, min(256 // blocks, (n + 127) // 128))
+    if out is None:
+        out = torch.empty(Kx * Kg, dtype=torch.float32, device=xs[0].device)
+        accumulate = False
+    flat = out.view(-1)
     for i in range(0, len(xs), 16):
         part = _backend.ops().dense_wgrad(list(xs[i:i + 16]),
                                           list(gs[i:i + 16]), nsplit)
-        _backend.ops().reduce_add_rows(part.view(nsplit, K * 128), out, i > 0)
-    return out.view(K, 128)
+        _backend.ops().reduce_add_rows(part.view(nsplit, Kx * Kg), flat,
+                                       accumulate or i > 0)
+    return out.view(Kx, Kg)
 
 
 def cat_matmul_supported(parts, w_t):

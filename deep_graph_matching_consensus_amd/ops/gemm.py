@@ -36,6 +36,19 @@ def _split_factor(m, n, k):
     return s
 
 
+def _dense_tn_ok(a, b):
+    from . import dense as _dense
+    if not (_dense.DENSE_WGRAD and a.is_cuda and _backend.use_hip(a)):
+        return False
+    K, M = a.shape
+    N = b.shape[1]
+    return (a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and
+            M % 128 == 0 and N % 128 == 0 and M * N <= 512 * 512 and
+            K >= 1024 and b.shape[0] == K and
+            all(t.stride(1) == 1 and t.stride(0) % 8 == 0 and
+                t.data_ptr() % 16 == 0 for t in (a, b)))
+
+
 def matmul_tn_fp32(a, b, out=None, accumulate=False):
     """``a^T @ b`` (``a [K, M]``, ``b [K, N]``) with fp32 output, split-K.
 
@@ -45,6 +58,11 @@ def matmul_tn_fp32(a, b, out=None, accumulate=False):
     """
     K, M = a.shape
     N = b.shape[1]
+    if _dense_tn_ok(a, b):
+        # Small bf16 outputs: the MFMA TN kernel (ops/dense.py::dense_wgrad)
+        # instead of a skinny split-K library GEMM.
+        from .dense import dense_wgrad
+        return dense_wgrad([a], [b], out=out, accumulate=accumulate)
     if not a.is_cuda:
         res = a.float().t() @ b.float()
     else:

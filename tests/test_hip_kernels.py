@@ -1243,3 +1243,21 @@ def test_dense_wgrad_matches_fp32(U, N, K):
     ref_ = sum(x.float().t() @ g.float() for x, g in zip(X.unbind(0), gs))
     torch.testing.assert_close(got, ref_, atol=2e-3 * N ** 0.5 * U ** 0.5,
                                rtol=1e-3)
+
+
+@pytest.mark.parametrize('K,M,N', [(11008, 256, 256), (3000, 128, 384)])
+def test_matmul_tn_fp32_dense_path(K, M, N):
+    """matmul_tn_fp32 on small bf16 outputs (dense_wgrad path), plain and
+    accumulating into an fp32 output."""
+    from deep_graph_matching_consensus_amd.ops.gemm import (_dense_tn_ok,
+                                                            matmul_tn_fp32)
+    a = torch.randn(K, M, device=DEV).bfloat16()
+    b = torch.randn(K, N, device=DEV).bfloat16()
+    assert _dense_tn_ok(a, b)
+    ref_ = a.float().t() @ b.float()
+    tol = 2e-3 * K ** 0.5
+    torch.testing.assert_close(matmul_tn_fp32(a, b), ref_, atol=tol,
+                               rtol=1e-3)
+    out = torch.ones(M, N, device=DEV)
+    matmul_tn_fp32(a, b, out=out, accumulate=True)
+    torch.testing.assert_close(out, ref_ + 1, atol=tol, rtol=1e-3)
