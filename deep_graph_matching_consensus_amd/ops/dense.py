@@ -442,9 +442,13 @@ class _CatMatmul(torch.autograd.Function):
         g = g.contiguous()
         if g.dtype != w_n.dtype:
             g = g.to(w_n.dtype)
-        # g W^T = [M, 128] x [128, K]: hipBLASLt (8.7 us at M = 20k,
-        # K = 384, vs 11.0 us for cat_gemm with W^T staged).
-        gx = g @ w_n                                     # [M, K]
+        # g W^T = [M, 128] x [128, K] on the same kernel (W^T staged in LDS);
+        # DGMC_AMD_CAT_GEMM_BWD=0: hipBLASLt.
+        if CAT_GEMM_BWD and w_nt.size(0) in (128, 256, 384) and \
+                g.data_ptr() % 16 == 0:
+            gx = _backend.ops().cat_gemm([g], w_nt, None)    # [M, K]
+        else:
+            gx = g @ w_n                                     # [M, K]
         grads, off = [], 0
         for i, wd in enumerate(ctx.widths):
             grads.append(gx[:, off:off + wd]
@@ -476,6 +480,7 @@ class _CatMatmul(torch.autograd.Function):
 
 
 DENSE_WGRAD = os.environ.get('DGMC_AMD_DENSE_WGRAD', '1') == '1'
+CAT_GEMM_BWD = os.environ.get('DGMC_AMD_CAT_GEMM_BWD', '1') == '1'
 
 
 def dense_wgrad_supported(X, gs):
