@@ -41,10 +41,31 @@ struct StepTable {
   int count;
 };
 
-__global__ void adam_step_inc_kernel(const StepTable T,
-                                     const float* __restrict__ found_inf) {
+// With ``flags`` (per-block non-finite flags written by pack_grads): fold
+// them first - found_inf = any, skip counter += any - then bump the step
+// counters of a finite step (one launch instead of two check kernels).
+__global__ void adam_step_inc_kernel(const StepTable T, float* found_inf,
+                                     const int* __restrict__ flags,
+                                     int nflags, double* __restrict__ skips) {
   const int i = threadIdx.x;
-  if (i < T.count && !(found_inf && *found_inf != 0.f)) *T.s[i] += 1.f;
+  bool bad;
+  if (flags) {
+    __shared__ int any;
+    if (i == 0) any = 0;
+    __syncthreads();
+    int b = 0;
+    for (int j = i; j < nflags; j += blockDim.x) b |= flags[j];
+    if (b) any = 1;        // benign race: every writer stores 1
+    __syncthreads();
+    bad = any != 0;
+    if (i == 0) {
+      if (found_inf) *found_inf = bad ? 1.f : 0.f;
+      if (skips) *skips += bad ? 1.0 : 0.0;
+    }
+  } else {
+    bad = found_inf && *found_inf != 0.f;
+  }
+  if (i < T.count && !bad) *T.s[i] += 1.f;
 }
 
 __global__ __launch_bounds__(kAdamThreads) void adam_multi_kernel(
@@ -168,12 +189,29 @@ void adam_multi(at::TensorList params, at::TensorList grads,
 }
 
 void adam_step_inc(at::TensorList steps,
-                   const c10::optional<at::Tensor>& found_inf) {
+                   const c10::optional<at::Tensor>& found_inf,
+                   const c10::optional<at::Tensor>& flags,
+                   const c10::optional<at::Tensor>& skips) {
   const int64_t count = (int64_t)steps.size();
   if (count == 0) return;
-  const float* fi = nullptr;
+  float* fi = nullptr;
   if (found_inf.has_value() && found_inf->defined())
     fi = found_inf->data_ptr<float>();
+  const int* fl = nullptr;
+  int nflags = 0;
+  if (flags.has_value() && flags->defined()) {
+    TORCH_CHECK(flags->scalar_type() == at::kInt && flags->is_contiguous() &&
+                    flags->device() == steps[0].device(),
+                "adam_step_inc: int32 flags on the device");
+    fl = flags->data_ptr<int>();
+    nflags = (int)flags->numel();
+  }
+  double* sk = nullptr;
+  if (skips.has_value() && skips->defined()) {
+    TORCH_CHECK(skips->scalar_type() == at::kDouble && skips->numel() == 1,
+                "adam_step_inc: fp64 [1] skip counter");
+    sk = skips->data_ptr<double>();
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(steps[0].device());
   for (int64_t c0 = 0; c0 < count; c0 += kAdamMax) {
     StepTable T{};
@@ -182,8 +220,10 @@ void adam_step_inc(at::TensorList steps,
       check_step(steps[c0 + j], steps[0]);
       T.s[j] = steps[c0 + j].data_ptr<float>();
     }
+    // The flag fold runs once (first launch); later launches read found_inf.
     hipLaunchKernelGGL(adam_step_inc_kernel, dim3(1), dim3(kAdamMax), 0,
-                       stream(), T, fi);
+                       stream(), T, fi, c0 == 0 ? fl : nullptr, nflags,
+                       c0 == 0 ? sk : nullptr);
     DGMC_CHECK_LAUNCH();
   }
 }
@@ -209,8 +249,11 @@ struct PackTable {
 }  // namespace
 
 __global__ __launch_bounds__(kAdamThreads) void pack_grads_kernel(
-    const PackTable T) {
+    const PackTable T, int* __restrict__ flags) {
   const int b = blockIdx.x;
+  __shared__ int any;
+  if (flags && threadIdx.x == 0) any = 0;
+  int bad = 0;
   int ti = 0;
   while (ti + 1 < T.count && T.first_block[ti + 1] <= b) ++ti;
   const int n = T.n[ti];
@@ -229,23 +272,46 @@ __global__ __launch_bounds__(kAdamThreads) void pack_grads_kernel(
     for (int u = 0; u < kAdamVec; ++u) {
       const int i = base + 4 * (u * kAdamThreads + threadIdx.x);
       *reinterpret_cast<float4*>(D + i) = v[u];
+      bad |= !isfinite(v[u].x) | !isfinite(v[u].y) | !isfinite(v[u].z) |
+             !isfinite(v[u].w);
     }
   } else {
     for (int i = base + threadIdx.x; i < min(n, base + kAdamBlock);
-         i += kAdamThreads)
-      D[i] = G ? G[i] : 0.f;
+         i += kAdamThreads) {
+      const float x = G ? G[i] : 0.f;
+      D[i] = x;
+      bad |= !isfinite(x);
+    }
+  }
+  if (flags) {
+    // Per-block non-finite flag (folded by adam_step_inc).
+    __syncthreads();
+    if (bad) any = 1;      // benign race: every writer stores 1
+    __syncthreads();
+    if (threadIdx.x == 0) flags[b] = any;
   }
 }
 
 // grads[i]: fp32 contiguous 16-B aligned gradient of numel n_i (or None);
 // views[i]: the destination fp32 contiguous 16-B aligned view (numel n_i).
-void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
-                at::TensorList views) {
+// with_flags: also returns int32 per-block non-finite flags of the packed
+// gradients (for adam_step_inc's fold; undefined otherwise).
+at::Tensor pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
+                      at::TensorList views, bool with_flags) {
   const int64_t count = (int64_t)views.size();
   TORCH_CHECK((int64_t)grads.size() == count,
               "pack_grads: one gradient slot per destination view");
-  if (count == 0) return;
+  if (count == 0) return at::Tensor();
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(views[0].device());
+  at::Tensor flags;
+  if (with_flags) {
+    int64_t total = 0;
+    for (int64_t j = 0; j < count; ++j)
+      total += (views[j].numel() + kAdamBlock - 1) / kAdamBlock;
+    // Every block writes its flag: no zero-fill.
+    flags = at::empty({total}, views[0].options().dtype(at::kInt));
+  }
+  int64_t flag_off = 0;
   for (int64_t c0 = 0; c0 < count; c0 += kAdamMax) {
     PackTable T{};
     T.count = (int)std::min<int64_t>(kAdamMax, count - c0);
@@ -275,9 +341,12 @@ void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
     T.first_block[T.count] = blocks;
     if (blocks == 0) continue;
     hipLaunchKernelGGL(pack_grads_kernel, dim3(blocks), dim3(kAdamThreads), 0,
-                       stream(), T);
+                       stream(), T,
+                       with_flags ? flags.data_ptr<int>() + flag_off : nullptr);
     DGMC_CHECK_LAUNCH();
+    flag_off += blocks;
   }
+  return flags;
 }
 
 }  // namespace dgmc

@@ -123,7 +123,9 @@ void adam_multi(at::TensorList params, at::TensorList grads,
                 const c10::optional<at::Tensor>& found_inf, double lr,
                 double beta1, double beta2, double eps, double weight_decay);
 void adam_step_inc(at::TensorList steps,
-                   const c10::optional<at::Tensor>& found_inf);
+                   const c10::optional<at::Tensor>& found_inf,
+                   const c10::optional<at::Tensor>& flags,
+                   const c10::optional<at::Tensor>& skips);
 at::Tensor slot_wgrad_list(at::TensorList xs, at::TensorList gs,
                            const at::Tensor& esrc, const at::Tensor& edst,
                            const at::Tensor& evals, const at::Tensor& soff,
@@ -147,8 +149,8 @@ at::Tensor spline_weight_pack(const at::Tensor& weight,
 std::tuple<at::Tensor, at::Tensor> spline_weight_unpack(const at::Tensor& g,
                                                         int64_t K,
                                                         bool has_root);
-void pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
-                at::TensorList views);
+at::Tensor pack_grads(const c10::List<c10::optional<at::Tensor>>& grads,
+                      at::TensorList views, bool with_flags);
 at::Tensor cat_gemm(at::TensorList xs, const at::Tensor& W,
                     const c10::optional<at::Tensor>& ocat);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
@@ -280,14 +282,14 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "adam_multi(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, "
       "Tensor(c!)[] exp_avg_sq, Tensor[] steps, Tensor? found_inf, float lr, "
       "float beta1, float beta2, float eps, float weight_decay) -> ()");
-  m.def("adam_step_inc(Tensor(a!)[] steps, Tensor? found_inf) -> ()");
+  m.def("adam_step_inc(Tensor(a!)[] steps, Tensor(b!)? found_inf, Tensor? flags=None, Tensor(c!)? skips=None) -> ()");
   m.def(
       "spline_weight_pack(Tensor weight, Tensor? root, ScalarType dtype) -> "
       "Tensor");
   m.def(
       "spline_weight_unpack(Tensor g, int K, bool has_root) -> (Tensor, "
       "Tensor)");
-  m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views) -> ()");
+  m.def("pack_grads(Tensor?[] grads, Tensor(a!)[] views, bool with_flags=False) -> Tensor");
   m.def("cat_gemm(Tensor[] xs, Tensor W, Tensor(a!)? ocat=None) -> Tensor");
   m.def(
       "dense_consensus_transport(Tensor S_hat, Tensor P, Tensor Q, Tensor b1, "

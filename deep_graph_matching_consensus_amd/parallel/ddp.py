@@ -107,10 +107,13 @@ class GradBucketAllReducer(object):
         for p in self.params:
             p.grad = None
 
-    def pack_grads(self):
+    def pack_grads(self, with_flags=False):
         """After backward: copy the stolen gradients into the flat buffer in
         ONE multi-tensor kernel (zeros for parameters without a gradient)
-        and re-bind every ``p.grad`` to its flat view."""
+        and re-bind every ``p.grad`` to its flat view.  ``with_flags``: also
+        return the kernel's per-block non-finite flags (HIP path; None
+        otherwise) - the optimizer's step kernel folds them, so no separate
+        finiteness pass is needed."""
         from ..ops import _backend
         views = [self.flat[o:o + n].view_as(p)
                  for p, (o, n) in ((p, self._slot[p]) for p in self.params)]
@@ -125,9 +128,13 @@ class GradBucketAllReducer(object):
                 fast.append(g if ok else None)
                 if not ok:
                     slow.append((g, v))
-            _backend.ops().pack_grads(fast, views)
+            flags = _backend.ops().pack_grads(fast, views,
+                                              with_flags and not slow)
             for g, v in slow:
                 v.copy_(g)
+            for p, v in zip(self.params, views):
+                p.grad = v
+            return flags
         else:
             for g, v in zip(grads, views):
                 if g is None:
@@ -136,6 +143,7 @@ class GradBucketAllReducer(object):
                     v.copy_(g)
         for p, v in zip(self.params, views):
             p.grad = v
+        return None
 
     def broadcast_state(self):
         with torch.no_grad():

@@ -52,8 +52,11 @@ def _device_step(st, p):
     return step
 
 
-def hip_adam_step(optimizer, found_inf=None):
-    """One Adam step of ``optimizer`` (see module docstring)."""
+def hip_adam_step(optimizer, found_inf=None, flags=None, skips=None):
+    """One Adam step of ``optimizer`` (see module docstring).  ``flags``:
+    per-block non-finite flags of the gradients (``pack_grads``) folded into
+    ``found_inf`` (and ``skips += 1`` on a skipped step) by the step-counter
+    kernel."""
     group = optimizer.param_groups[0]
     params = [p for p in group['params'] if p.grad is not None]
     if not params:
@@ -70,7 +73,7 @@ def hip_adam_step(optimizer, found_inf=None):
         steps.append(_device_step(st, p))
     b1, b2 = group['betas']
     ops = _backend.ops()
-    ops.adam_step_inc(steps, found_inf)
+    ops.adam_step_inc(steps, found_inf, flags, skips)
     ops.adam_multi(params, [p.grad for p in params],
                    [state[p]['exp_avg'] for p in params],
                    [state[p]['exp_avg_sq'] for p in params], steps, found_inf,

@@ -205,11 +205,20 @@ class PairTrainer(object):
         with streams.side_streams(SIDE_STREAMS and STEAL_GRADS and
                                   self.device.type == 'cuda'):
             self._forward_backward(batch, self._rows[bucket], batch.y_mask)
+        flags = None
         if STEAL_GRADS:
-            self.reducer.pack_grads()
+            # Single process: the pack kernel also flags non-finite
+            # gradients and the optimizer's step kernel folds the flags.
+            flags = self.reducer.pack_grads(
+                with_flags=self.world == 1 and self.guard)
         if self.world == 1:
-            self._check_finite()
-            self._optimizer_step()
+            from .runtime import optim as hip_optim
+            if flags is not None and hip_optim.supported(self.optimizer):
+                hip_optim.hip_adam_step(self.optimizer, self._found_inf,
+                                        flags, self.stats[3:4])
+            else:
+                self._check_finite()
+                self._optimizer_step()
 
     def _bucket_body(self, i):
         return lambda: self._static_body(i)

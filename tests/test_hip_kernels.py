@@ -836,6 +836,23 @@ def test_pack_grads_multi_tensor():
             assert bool((v == 0).all())
         else:
             assert torch.equal(v, g)
+    # Non-finite flags folded by the step-counter kernel: a finite step bumps
+    # the counters, a step with an inf sets found_inf, counts a skip and
+    # leaves the counters alone.
+    steps = [torch.full((), 3.0, device=DEV) for _ in range(3)]
+    found = torch.zeros((), device=DEV)
+    skips = torch.zeros(1, dtype=torch.float64, device=DEV)
+    flags = ops.pack_grads(grads, views, True)
+    assert flags.dtype == torch.int32 and int(flags.sum()) == 0
+    ops.adam_step_inc(steps, found, flags, skips)
+    assert float(found) == 0 and float(skips) == 0
+    assert all(float(t) == 4.0 for t in steps)
+    grads[2][5000] = float('inf')
+    flags = ops.pack_grads(grads, views, True)
+    assert int(flags.sum()) == 1
+    ops.adam_step_inc(steps, found, flags, skips)
+    assert float(found) == 1 and float(skips) == 1
+    assert all(float(t) == 4.0 for t in steps)
 
 
 def test_spline_slot_images_match_permuted_pack():
