@@ -132,7 +132,8 @@ __device__ __forceinline__ void ps_stage(DGMC_LDS float* dst, const T* src,
 
 template <typename T>
 __global__ __launch_bounds__(kPsThreads) void pair_scores_bwd_kernel(
-    const float* __restrict__ dS, const T* __restrict__ h, int64_t t_off,
+    const float* __restrict__ dS, const float* __restrict__ dS2,
+    const T* __restrict__ h, int64_t t_off,
     int64_t rows, const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
     T* __restrict__ dh, int B, int Ns, int Nt, int C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -163,7 +164,14 @@ __global__ __launch_bounds__(kPsThreads) void pair_scores_bwd_kernel(
   const float* dSb = dS + (int64_t)b * Ns * Nt;
   const T* hs_g = h + (int64_t)s0 * C;
   const T* ht_g = h + (t_off + t0) * C;
-  for (int e = tid; e < Ns * Nt; e += kPsThreads) g[e] = dSb[e];
+  // Two consumers' gradients of S_hat (loss + consensus loop) are summed
+  // here instead of by an autograd add kernel.
+  if (dS2) {
+    const float* dSb2 = dS2 + (int64_t)b * Ns * Nt;
+    for (int e = tid; e < Ns * Nt; e += kPsThreads) g[e] = dSb[e] + dSb2[e];
+  } else {
+    for (int e = tid; e < Ns * Nt; e += kPsThreads) g[e] = dSb[e];
+  }
   ps_stage(hsL, hs_g, ns * C, tid);
   ps_stage(htL, ht_g, nt * C, tid);
   __syncthreads();
@@ -255,10 +263,18 @@ at::Tensor pair_scores(const at::Tensor& h, int64_t t_off,
 
 at::Tensor pair_scores_bwd(const at::Tensor& dS, const at::Tensor& h,
                            int64_t t_off, const at::Tensor& ptr_s,
-                           const at::Tensor& ptr_t) {
+                           const at::Tensor& ptr_t,
+                           const c10::optional<at::Tensor>& dS2) {
   TORCH_CHECK(dS.is_cuda() && dS.scalar_type() == at::kFloat && dS.dim() == 3 &&
                   dS.is_contiguous(),
               "pair_scores_bwd: contiguous fp32 dS [B, Ns, Nt]");
+  const float* d2 = nullptr;
+  if (dS2.has_value() && dS2->defined()) {
+    TORCH_CHECK(dS2->scalar_type() == at::kFloat && dS2->is_contiguous() &&
+                    dS2->sizes() == dS.sizes(),
+                "pair_scores_bwd: dS2 like dS");
+    d2 = dS2->data_ptr<float>();
+  }
   TORCH_CHECK(h.is_cuda() && h.dim() == 2 && h.is_contiguous() &&
                   (h.scalar_type() == at::kBFloat16 ||
                    h.scalar_type() == at::kFloat),
@@ -292,6 +308,7 @@ at::Tensor pair_scores_bwd(const at::Tensor& dS, const at::Tensor& h,
   if (h.scalar_type() == at::kBFloat16)
     hipLaunchKernelGGL(pair_scores_bwd_kernel<__hip_bfloat16>, dim3(B),
                        dim3(kPsThreads), lds, stream(), dS.data_ptr<float>(),
+                       d2,
                        reinterpret_cast<const __hip_bfloat16*>(h.data_ptr()),
                        t_off, rows, ptr_s.data_ptr<int>(),
                        ptr_t.data_ptr<int>(),
@@ -300,7 +317,8 @@ at::Tensor pair_scores_bwd(const at::Tensor& dS, const at::Tensor& h,
   else
     hipLaunchKernelGGL(pair_scores_bwd_kernel<float>, dim3(B),
                        dim3(kPsThreads), lds, stream(), dS.data_ptr<float>(),
-                       h.data_ptr<float>(), t_off, rows, ptr_s.data_ptr<int>(),
+                       d2, h.data_ptr<float>(), t_off, rows,
+                       ptr_s.data_ptr<int>(),
                        ptr_t.data_ptr<int>(), dh.data_ptr<float>(), B, Ns, Nt,
                        C);
   DGMC_CHECK_LAUNCH();

@@ -184,7 +184,8 @@ at::Tensor pair_scores(const at::Tensor& h, int64_t t_off,
                        int64_t Ns, int64_t Nt);
 at::Tensor pair_scores_bwd(const at::Tensor& dS, const at::Tensor& h,
                            int64_t t_off, const at::Tensor& ptr_s,
-                           const at::Tensor& ptr_t);
+                           const at::Tensor& ptr_t,
+                           const c10::optional<at::Tensor>& dS2);
 std::tuple<at::Tensor, at::Tensor> spline_slot_images(
     const at::Tensor& weight, const c10::optional<at::Tensor>& root,
     const at::Tensor& perm);
@@ -313,7 +314,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "int Nt) -> Tensor");
   m.def(
       "pair_scores_bwd(Tensor dS, Tensor h, int t_off, Tensor ptr_s, Tensor "
-      "ptr_t) -> Tensor");
+      "ptr_t, Tensor? dS2=None) -> Tensor");
   m.def(
       "spline_slot_images(Tensor weight, Tensor? root, Tensor perm) -> "
       "(Tensor, Tensor)");

@@ -354,15 +354,24 @@ class DGMC(torch.nn.Module):
                 'Sinkhorn normalisation is only defined for k=-1 (dense)'
             if self.k < 1:
                 # ------------------ dense variant -------------------- #
-                if direct:
-                    S_hat = dense_ops.pair_scores(h_joint, h_s.size(0),
-                                                  lay_s, lay_t)
-                else:
-                    S_hat = hs @ ht.transpose(-1, -2)        # [B, N_s, N_t]
                 # raw: the caller (objective) fuses softmax + NLL on the
                 # scores themselves; the probabilities are never formed.
-                raw = raw and dense_ops.softmax_nll_supported(S_hat, lay_s)
-                S_hat_0 = S_hat
+                two = False
+                if direct:
+                    # Raw objective + consensus steps: S_hat_0 has two
+                    # consumers - one handle each (no autograd add).
+                    two = raw and steps > 0 and torch.is_grad_enabled()
+                    S_hat = dense_ops.pair_scores(h_joint, h_s.size(0),
+                                                  lay_s, lay_t, two=two)
+                else:
+                    S_hat = hs @ ht.transpose(-1, -2)        # [B, N_s, N_t]
+                if two:
+                    S_hat_0, S_hat = S_hat
+                    raw = dense_ops.softmax_nll_supported(S_hat, lay_s)
+                else:
+                    raw = raw and dense_ops.softmax_nll_supported(S_hat,
+                                                                  lay_s)
+                    S_hat_0 = S_hat
                 S_0 = None if raw else \
                     dense_ops.masked_softmax_packed(S_hat, lay_s, lay_t)
                 # Fused pair encoding: the transport kernel writes r_t

@@ -55,18 +55,29 @@ class _PairScores(torch.autograd.Function):
     gradient (padding rows zero) - no dense layouts, no slice backward."""
 
     @staticmethod
-    def forward(ctx, h, t_off, ptr_s, ptr_t, N_s, N_t):
+    def forward(ctx, h, t_off, ptr_s, ptr_t, N_s, N_t, two):
         S = _backend.ops().pair_scores(h, t_off, ptr_s, ptr_t, N_s, N_t)
         ctx.save_for_backward(h, ptr_s, ptr_t)
         ctx.t_off = t_off
+        ctx.set_materialize_grads(False)
+        if two:
+            # Two handles on S_hat for its two consumers (objective / loop):
+            # their gradients meet in the backward kernel, not in an
+            # autograd add.
+            return S, S.view_as(S)
         return S
 
     @staticmethod
-    def backward(ctx, grad):
+    def backward(ctx, grad, grad2=None):
         h, ptr_s, ptr_t = ctx.saved_tensors
-        dh = _backend.ops().pair_scores_bwd(grad.float().contiguous(), h,
-                                            ctx.t_off, ptr_s, ptr_t)
-        return dh, None, None, None, None, None
+        if grad is None:
+            grad, grad2 = grad2, None
+        if grad is None:
+            return (None, ) * 7
+        dh = _backend.ops().pair_scores_bwd(
+            grad.float().contiguous(), h, ctx.t_off, ptr_s, ptr_t,
+            None if grad2 is None else grad2.float().contiguous())
+        return dh, None, None, None, None, None, None
 
 
 def pair_scores_supported(h, lay_s, lay_t):
@@ -75,13 +86,15 @@ def pair_scores_supported(h, lay_s, lay_t):
             and h.size(1) <= 256 and lay_s.N >= 1 and lay_t.N >= 1)
 
 
-def pair_scores(h, t_off, lay_s, lay_t):
+def pair_scores(h, t_off, lay_s, lay_t, two=False):
     r"""Dense initial scores ``[B, N_s, N_t]`` (fp32) of the joint encoder
     output ``h = [h_s; h_t]`` (target rows from ``t_off``): entry
     ``(b, i, j) = <h_s[ptr_s[b] + i], h_t[ptr_t[b] + j]>``, zero outside
-    each pair's ``n_s x n_t`` block (``dgmc.py:154-163``)."""
+    each pair's ``n_s x n_t`` block (``dgmc.py:154-163``).  ``two``: return
+    two aliases (one per consumer; gradients summed in the backward
+    kernel)."""
     return _PairScores.apply(h, int(t_off), lay_s.ptr, lay_t.ptr, lay_s.N,
-                             lay_t.N)
+                             lay_t.N, bool(two))
 
 
 # ---------------------------------------------------------------------------
