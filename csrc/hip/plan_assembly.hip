@@ -61,7 +61,8 @@ __global__ __launch_bounds__(kAsmThreads) void assemble_slot_plan_kernel(
     int B, int64_t cap_s, int64_t cap_t, int S, int root_slot, int64_t cap,
     int* __restrict__ rowptr, int* __restrict__ col, float* __restrict__ val,
     int* __restrict__ trowptr, int* __restrict__ tcol,
-    float* __restrict__ tval, uint8_t* __restrict__ gflag) {
+    float* __restrict__ tval, uint8_t* __restrict__ gflag,
+    const int64_t* __restrict__ st_row, int64_t* __restrict__ row_out) {
   __shared__ int64_t red[kAsmThreads / kWave];
   const int k = blockIdx.x;
   const int tid = threadIdx.x;
@@ -104,6 +105,9 @@ __global__ __launch_bounds__(kAsmThreads) void assemble_slot_plan_kernel(
       val[eo + e] = st_val[r0 + e];
       tcol[eo + e] = (int)(st_tcol[t0 + e] + dt);
       tval[eo + e] = st_tval[t0 + e];
+      // Row of every entry (the slot weight gradient's pair lists need it;
+      // otherwise a searchsorted over rowptr per step).
+      if (row_out) row_out[eo + e] = st_row[r0 + e] + dt;
     }
   } else {
     // Padding rows: root entry only (or nothing without a root weight).
@@ -115,6 +119,7 @@ __global__ __launch_bounds__(kAsmThreads) void assemble_slot_plan_kernel(
         val[eo + r] = 1.f;
         tcol[eo + r] = (int)node;
         tval[eo + r] = 1.f;
+        if (row_out) row_out[eo + r] = node;
       }
     }
     for (int64_t q = tid; q < s.n * S; q += kAsmThreads) {
@@ -153,7 +158,9 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                         int64_t root_slot, at::Tensor rowptr, at::Tensor col,
                         at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
                         at::Tensor tval,
-                        const c10::optional<at::Tensor>& gflag) {
+                        const c10::optional<at::Tensor>& gflag,
+                        const c10::optional<at::Tensor>& st_row,
+                        const c10::optional<at::Tensor>& row_out) {
   for (const at::Tensor* t : std::initializer_list<const at::Tensor*>{
            &st_rowptr, &st_col, &st_trowptr, &st_tcol, &rowptr, &col,
            &trowptr, &tcol})
@@ -189,6 +196,20 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                 "assemble_slot_plan: gflag uint8 [N]");
     fp = gflag->data_ptr<uint8_t>();
   }
+  const int64_t* srp = nullptr;
+  int64_t* rop = nullptr;
+  if (row_out.has_value() && row_out->defined()) {
+    TORCH_CHECK(st_row.has_value() && st_row->defined() &&
+                    st_row->scalar_type() == at::kLong &&
+                    st_row->is_contiguous() &&
+                    st_row->numel() == st_col.numel() &&
+                    row_out->scalar_type() == at::kLong &&
+                    row_out->is_contiguous() &&
+                    row_out->numel() == col.numel(),
+                "assemble_slot_plan: int64 st_row [store nnz], row_out [cap]");
+    srp = st_row->data_ptr<int64_t>();
+    rop = row_out->data_ptr<int64_t>();
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(col.device());
   hipLaunchKernelGGL(assemble_slot_plan_kernel, dim3(2 * B + 2),
                      dim3(kAsmThreads), 0, stream(), st_rowptr.data_ptr<int>(),
@@ -200,7 +221,7 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                      (int)root_slot, col.numel(), rowptr.data_ptr<int>(),
                      col.data_ptr<int>(), val.data_ptr<float>(),
                      trowptr.data_ptr<int>(), tcol.data_ptr<int>(),
-                     tval.data_ptr<float>(), fp);
+                     tval.data_ptr<float>(), fp, srp, rop);
   DGMC_CHECK_LAUNCH();
 }
 

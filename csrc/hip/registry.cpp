@@ -80,7 +80,9 @@ void assemble_slot_plan(const at::Tensor& st_rowptr, const at::Tensor& st_col,
                         int64_t root_slot, at::Tensor rowptr, at::Tensor col,
                         at::Tensor val, at::Tensor trowptr, at::Tensor tcol,
                         at::Tensor tval,
-                        const c10::optional<at::Tensor>& gflag);
+                        const c10::optional<at::Tensor>& gflag,
+                        const c10::optional<at::Tensor>& st_row,
+                        const c10::optional<at::Tensor>& row_out);
 at::Tensor masked_softmax_packed(const at::Tensor& S_hat,
                                  const at::Tensor& dense_index,
                                  const at::Tensor& n_s, const at::Tensor& n_t);
@@ -264,7 +266,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor gid, Tensor ptr_s, Tensor ptr_t, int cap_s, int cap_t, int S, "
       "int root_slot, Tensor(a!) rowptr, Tensor(b!) col, Tensor(c!) val, "
       "Tensor(d!) trowptr, Tensor(e!) tcol, Tensor(f!) tval, Tensor(g!)? "
-      "gflag=None) -> ()");
+      "gflag=None, Tensor? st_row=None, Tensor(h!)? row_out=None) -> ()");
   m.def(
       "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
       "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "

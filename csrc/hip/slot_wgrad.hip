@@ -611,9 +611,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_pair_lists(
   at::Tensor cnt = at::empty({nblk, S}, i32);
   at::Tensor off = at::empty({nblk, S}, i32);
   at::Tensor soff = at::empty({S + 1}, i32);
-  at::Tensor esrc = at::zeros({E}, i32);
-  at::Tensor edst = at::zeros({E}, i32);
-  at::Tensor evals = at::zeros({E}, val.options());
+  // Only the first rowptr[N] entries are written - and read (through soff).
+  at::Tensor esrc = at::empty({E}, i32);
+  at::Tensor edst = at::empty({E}, i32);
+  at::Tensor evals = at::empty({E}, val.options());
   hipLaunchKernelGGL(pair_count_kernel, dim3(nblk), dim3(kPlThreads), 0,
                      stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
                      (int)N, (int)S, cnt.data_ptr<int>());

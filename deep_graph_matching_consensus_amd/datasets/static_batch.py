@@ -414,8 +414,9 @@ class SlotPlanAssembler(object):
             # accumulation: it needs every (row, column) entry to be unique.
             rc = A.row * A.num_cols + A.col.long()
             unique = int(torch.unique(rc).numel()) == A.nnz
-            pieces = self._store[key] = (A, A.t(), unique)
-        A, At, unique = pieces
+            pieces = self._store[key] = (A, A.t(), unique,
+                                         A.row.long().contiguous())
+        A, At, unique, st_row = pieces
         K = 1
         for k in kernel_size:
             K *= int(k)
@@ -432,15 +433,19 @@ class SlotPlanAssembler(object):
                 torch.zeros(N + 1, **i32), torch.zeros(cap, **i32),
                 torch.zeros(cap, **f32), torch.zeros(N * S + 1, **i32),
                 torch.zeros(cap, **i32), torch.zeros(cap, **f32),
-                torch.zeros(N, dtype=torch.uint8, device=dev))
-        rowptr, col, val, trowptr, tcol, tval, gflag = out
+                torch.zeros(N, dtype=torch.uint8, device=dev),
+                torch.zeros(cap, dtype=torch.long, device=dev))
+        rowptr, col, val, trowptr, tcol, tval, gflag, row = out
         v = b.v
         _backend.ops().assemble_slot_plan(
             A.rowptr, A.col, A.val, At.rowptr, At.col, At.val,
             self._node_ptr, v['gid'], v['ptr_s'], v['ptr_t'], b.cap_s,
             b.cap_t, S, K if root else -1, rowptr, col, val, trowptr, tcol,
-            tval, gflag)
+            tval, gflag, st_row, row)
         op = _StaticSlotOperator(rowptr, col, val, N, N * S)
+        # Entry rows written by the same kernel (tail entries past the
+        # total are stale, like col/val there: consumers stop at rowptr[N]).
+        op._row = row
         op._t = _StaticSlotOperator(trowptr, tcol, tval, N * S, N)
         op._t._t = op
         # Graph-closed row tiles for the fused slot conv: windows of

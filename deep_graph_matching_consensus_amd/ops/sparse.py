@@ -532,7 +532,7 @@ def slot_pair_lists(op, S):
     return p
 
 
-SLOT_WGRAD_SPLITS = 64
+SLOT_WGRAD_SPLITS = int(os.environ.get('DGMC_AMD_SLOT_WGRAD_SPLITS', '64'))
 # Loop-folded slot weight gradient handed to the stacked-weight node in
 # slot-major layout (weight / root views; no permute + unpack kernels).
 SLOT_HANDOFF = os.environ.get('DGMC_AMD_SLOT_HANDOFF', '1') == '1'

@@ -149,6 +149,12 @@ def test_assembled_spline_plan_matches_generic_build():
         za, zb = spmm(op.t(), g), spmm(ref_op.t(), g)
         assert torch.equal(za, zb)
         assert int(op.rowptr[-1]) == int(op.t().rowptr[-1])
+        # entry rows written by the assembler == rows derived from rowptr
+        E = int(op.rowptr[-1])
+        rows = torch.repeat_interleave(
+            torch.arange(N, device='cuda'),
+            (op.rowptr[1:] - op.rowptr[:-1]).long())
+        assert torch.equal(op.row[:E], rows)
         assert torch.equal(op.rowptr[1:] >= op.rowptr[:-1],
                            torch.ones(N, dtype=torch.bool, device='cuda'))
 
