@@ -110,6 +110,8 @@ at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
                        const c10::optional<at::Tensor>& Z);
 at::Tensor gather_gemm_stamps();
 at::Tensor slot_conv_stamps();
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fold_weights(
+    const at::Tensor& w1, const at::Tensor& wf);
 at::Tensor dense_wgrad(at::TensorList xs, at::TensorList gs, int64_t nsplit);
 at::Tensor tr16_probe(const at::Tensor& like);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> slot_pair_lists(
@@ -273,6 +275,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
   m.def("gather_gemm_stamps() -> Tensor");
   m.def("slot_conv_stamps() -> Tensor");
+  m.def("fold_weights(Tensor w1, Tensor wf) -> (Tensor, Tensor, Tensor)");
   m.def("dense_wgrad(Tensor[] xs, Tensor[] gs, int nsplit) -> Tensor");
   m.def("tr16_probe(Tensor like) -> Tensor");
   m.def(
@@ -397,6 +400,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spline_slot_images", &dgmc::spline_slot_images);
   m.impl("tr16_probe", &dgmc::tr16_probe);
   m.impl("dense_wgrad", &dgmc::dense_wgrad);
+  m.impl("fold_weights", &dgmc::fold_weights);
   m.impl("slot_pair_lists", &dgmc::slot_pair_lists);
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);

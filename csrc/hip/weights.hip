@@ -207,4 +207,63 @@ std::tuple<at::Tensor, at::Tensor> spline_slot_images(
   return {img_f, img_t};
 }
 
+// ---------------------------------------------------------------------------
+// fold_weights: the folded consensus projection W = W1 @ W_f (fp32, once per
+// training step; models/dgmc.py::_FoldProduct) together with the two bf16
+// operand images the projection kernels read - W (ops/dense.py::cat_gemm
+// forward) and W^T (its backward) - in ONE launch instead of an fp32 GEMM
+// plus a cast and a transposed cast.  Block = one output row r, one thread
+// per output column (coalesced W_f reads, W1[r, :] broadcast from LDS).
+namespace {
+__global__ __launch_bounds__(512) void fold_weights_kernel(
+    const float* __restrict__ w1, const float* __restrict__ wf,
+    float* __restrict__ w, __bf16* __restrict__ wn, __bf16* __restrict__ wnt,
+    int R, int Kin, int K) {
+  extern __shared__ float w1r[];                  // [Kin]
+  const int r = blockIdx.x;
+  for (int q = threadIdx.x; q < Kin; q += blockDim.x)
+    w1r[q] = w1[(size_t)r * Kin + q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < K; c += blockDim.x) {
+    float a0 = 0.f, a1 = 0.f;
+    int q = 0;
+    for (; q + 1 < Kin; q += 2) {
+      a0 = fmaf(w1r[q], wf[(size_t)q * K + c], a0);
+      a1 = fmaf(w1r[q + 1], wf[(size_t)(q + 1) * K + c], a1);
+    }
+    if (q < Kin) a0 = fmaf(w1r[q], wf[(size_t)q * K + c], a0);
+    const float v = a0 + a1;
+    w[(size_t)r * K + c] = v;
+    wn[(size_t)r * K + c] = (__bf16)v;
+    wnt[(size_t)c * R + r] = (__bf16)v;
+  }
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fold_weights(
+    const at::Tensor& w1, const at::Tensor& wf) {
+  TORCH_CHECK(w1.is_cuda() && wf.is_cuda() &&
+                  w1.scalar_type() == at::kFloat &&
+                  wf.scalar_type() == at::kFloat && w1.dim() == 2 &&
+                  wf.dim() == 2 && w1.size(1) == wf.size(0) &&
+                  w1.is_contiguous() && wf.is_contiguous(),
+              "fold_weights: fp32 contiguous W1 [R, Kin], W_f [Kin, K]");
+  const int R = (int)w1.size(0), Kin = (int)w1.size(1), K = (int)wf.size(1);
+  at::Tensor w = at::empty({R, K}, w1.options());
+  at::Tensor wn = at::empty({R, K}, w1.options().dtype(at::kBFloat16));
+  at::Tensor wnt = at::empty({K, R}, w1.options().dtype(at::kBFloat16));
+  if (R == 0 || K == 0) return {w, wn, wnt};
+  TORCH_CHECK(Kin <= 8192, "fold_weights: inner size");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w1.device());
+  hipLaunchKernelGGL(fold_weights_kernel, dim3(R),
+                     dim3(std::min(512, std::max(64, (K + 63) / 64 * 64))),
+                     (size_t)Kin * sizeof(float), stream(),
+                     w1.data_ptr<float>(), wf.data_ptr<float>(),
+                     w.data_ptr<float>(),
+                     reinterpret_cast<__bf16*>(wn.data_ptr()),
+                     reinterpret_cast<__bf16*>(wnt.data_ptr()), R, Kin, K);
+  DGMC_CHECK_LAUNCH();
+  return {w, wn, wnt};
+}
+
 }  // namespace dgmc

@@ -86,12 +86,25 @@ class _FoldProduct(torch.autograd.Function):
     def forward(ctx, w1, wf, bf):
         ctx.save_for_backward(w1, wf)
         ctx.bf_like = None if bf is None else (bf.shape, bf.dtype)
+        if _backend.use_hip(w1) and w1.dtype == torch.float32 and \
+                wf.dtype == torch.float32:
+            # fp32 product + its bf16 images W and W^T in one kernel.
+            w, wn, wnt = _backend.ops().fold_weights(w1.contiguous(),
+                                                     wf.contiguous())
+            ctx.mark_non_differentiable(wn, wnt)
+            return w, wn, wnt
         with torch.autocast(w1.device.type, enabled=False):
-            return w1.float() @ wf.float()
+            return w1.float() @ wf.float(), None, None
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _g_wn=None, _g_wnt=None):
+        return _FoldProduct._backward(ctx, g)
+
+    @staticmethod
+    def _backward(ctx, g):
         w1, wf = ctx.saved_tensors
+        if g is None:
+            return None, None, None
         with streams.side(g.device, (g, w1, wf)):
             g = g.float()
             gw1 = (g @ wf.float().t()).to(w1.dtype) \
@@ -389,13 +402,18 @@ class DGMC(torch.nn.Module):
                 if joint and self._foldable():
                     # (b_f's exact gradient is zero; it stays in the graph
                     # for autograd.grad / DDP.)
+                    lp = {}
                     if FOLD_FP32:
-                        w_fold = _FoldProduct.apply(self.mlp[0].weight,
-                                                    self.psi_2.final.weight,
-                                                    self.psi_2.final.bias)
+                        w_fold, wn, wnt = _FoldProduct.apply(
+                            self.mlp[0].weight, self.psi_2.final.weight,
+                            self.psi_2.final.bias)
+                        if wn is not None:
+                            # bf16 operand images from the same kernel
+                            # (ops/dense.py::cat_matmul reads them here).
+                            lp = {'n': wn, 'nt': wnt}
                     else:
                         w_fold = self.mlp[0].weight @ self.psi_2.final.weight
-                    fold = (w_fold.t(), {}, ('fold', id(self.mlp[0].weight)),
+                    fold = (w_fold.t(), lp, ('fold', id(self.mlp[0].weight)),
                             steps)
                 pending = None    # (joint, S_hat) from a fused step boundary
                 for step in range(steps):

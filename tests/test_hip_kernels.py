@@ -1278,3 +1278,15 @@ def test_matmul_tn_fp32_dense_path(K, M, N):
     out = torch.ones(M, N, device=DEV)
     matmul_tn_fp32(a, b, out=out, accumulate=True)
     torch.testing.assert_close(out, ref_ + 1, atol=tol, rtol=1e-3)
+
+
+def test_fold_weights_kernel():
+    """fold_weights: fp32 W1 @ W_f and its bf16 images W / W^T in one
+    kernel."""
+    w1 = torch.randn(128, 128, device=DEV)
+    wf = torch.randn(128, 384, device=DEV)
+    w, wn, wnt = _backend.ops().fold_weights(w1, wf)
+    ref_ = w1.double() @ wf.double()
+    torch.testing.assert_close(w.double(), ref_, atol=1e-3, rtol=1e-4)
+    assert torch.equal(wn, w.bfloat16())
+    assert torch.equal(wnt, w.t().contiguous().bfloat16())
