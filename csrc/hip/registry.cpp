@@ -61,7 +61,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
     const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& colptr,
     const at::Tensor& row_of, const at::Tensor& perm, const at::Tensor& G,
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
-    const at::Tensor& w2);
+    const at::Tensor& w2, const c10::optional<at::Tensor>& pptr,
+    const c10::optional<at::Tensor>& prow,
+    const c10::optional<at::Tensor>& pbeg,
+    const c10::optional<at::Tensor>& pend);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
+    const at::Tensor& rowptr, int64_t nnz, int64_t T);
+void spmm_pieces_out(const at::Tensor& rowptr, const at::Tensor& col,
+                     const at::Tensor& val, const c10::optional<at::Tensor>& perm,
+                     const at::Tensor& pptr, const at::Tensor& prow,
+                     const at::Tensor& pbeg, const at::Tensor& pend,
+                     const at::Tensor& x,
+                     const c10::optional<at::Tensor>& self_x,
+                     const c10::optional<at::Tensor>& self_scale,
+                     const c10::optional<at::Tensor>& bias, bool relu,
+                     at::Tensor out);
 
 std::tuple<at::Tensor, at::Tensor> relu_bias_bwd(
     const at::Tensor& grad, const at::Tensor& out, bool relu,
@@ -348,7 +362,16 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "sparse_consensus_bwd(Tensor rowptr, Tensor col, Tensor colptr, Tensor "
       "row_of, Tensor perm, Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
-      "w2) -> (Tensor, Tensor, Tensor)");
+      "w2, Tensor? pptr=None, Tensor? prow=None, Tensor? pbeg=None, Tensor? "
+      "pend=None) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "piece_plan(Tensor rowptr, int nnz, int T) -> (Tensor, Tensor, Tensor, "
+      "Tensor)");
+  m.def(
+      "spmm_pieces_out(Tensor rowptr, Tensor col, Tensor val, Tensor? perm, "
+      "Tensor pptr, Tensor prow, Tensor pbeg, Tensor pend, Tensor x, Tensor? "
+      "self_x, Tensor? self_scale, Tensor? bias, bool relu, Tensor(a!) out) -> "
+      "()");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
@@ -405,4 +428,6 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
+  m.impl("spmm_pieces_out", &dgmc::spmm_pieces_out);
+  m.impl("piece_plan", &dgmc::piece_plan);
 }

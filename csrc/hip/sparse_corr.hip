@@ -174,6 +174,252 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_cols_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Lane-group variants (channel count C a multiple of 4, C <= 256): a
+// candidate is owned by G = pow2ceil(C / 4) lanes holding one float4 each, so
+// a wave walks 64 / G candidates at once (R = 32: 8 candidates per step, the
+// 20 candidates of a DBP15K row in one batch of loads) and a dot needs
+// log2(G) xor steps instead of a whole-wave reduction per candidate.
+// Summation order is fixed: results are reproducible run to run.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 ld4(const float* __restrict__ p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+
+template <int G>
+__device__ __forceinline__ float group_sum(float s) {
+#pragma unroll
+  for (int off = 1; off < G; off <<= 1) s += __shfl_xor(s, off);
+  return s;
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void sddmm_g_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ A, const float* __restrict__ Bm,
+    float* __restrict__ val, int rows, int C) {
+  constexpr int NG = kWave / G;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int r = xcd_remap(blockIdx.x, gridDim.x) * kSpWaves + wave;
+  if (r >= rows) return;
+  const int g = lane / G, c = (lane % G) * 4;
+  const bool cok = c < C;
+  const float4 a = cok ? ld4(A + (size_t)r * C + c) : make_float4(0, 0, 0, 0);
+  const int p0 = rowptr[r], p1 = rowptr[r + 1];
+  for (int pb = p0; pb < p1; pb += 2 * NG) {
+    float s[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = pb + u * NG + g;
+      s[u] = 0.f;
+      if (p < p1 && cok) {
+        const float4 b = ld4(Bm + (size_t)col[p] * C + c);
+        s[u] = fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float t = group_sum<G>(s[u]);
+      const int p = pb + u * NG + g;
+      if ((lane % G) == 0 && p < p1) val[p] = t;
+    }
+  }
+}
+
+__device__ __forceinline__ float relu_dot4(float4 pv, float4 q, float4 w) {
+  return fmaf(fmaxf(pv.x - q.x, 0.f), w.x,
+              fmaf(fmaxf(pv.y - q.y, 0.f), w.y,
+                   fmaf(fmaxf(pv.z - q.z, 0.f), w.z,
+                        fmaxf(pv.w - q.w, 0.f) * w.w)));
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ S_hat, const float* __restrict__ P,
+    const float* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ out, int rows, int R) {
+  constexpr int NG = kWave / G;
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int r = xcd_remap(blockIdx.x, gridDim.x) * kSpWaves + wave;
+  if (r >= rows) return;
+  const int g = lane / G, c = (lane % G) * 4;
+  const bool cok = c < R;
+  float4 pv = make_float4(0, 0, 0, 0), wv = pv;
+  if (cok) {
+    const float4 p = ld4(P + (size_t)r * R + c), bb = ld4(b1 + c);
+    pv = make_float4(p.x + bb.x, p.y + bb.y, p.z + bb.z, p.w + bb.w);
+    wv = ld4(w2 + c);
+  }
+  const float bias = b2[0];
+  const int p0 = rowptr[r], p1 = rowptr[r + 1];
+  for (int pb = p0; pb < p1; pb += 2 * NG) {
+    float s[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = pb + u * NG + g;
+      s[u] = 0.f;
+      if (p < p1 && cok) s[u] = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float t = group_sum<G>(s[u]);
+      const int p = pb + u * NG + g;
+      if ((lane % G) == 0 && p < p1) out[p] = S_hat[p] + t + bias;
+    }
+  }
+}
+
+// dP[r] = w2 * sum_p g_p [z_p > 0];  dw2 partial per block (fixed order).
+template <int G>
+__global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ Gr, const float* __restrict__ P,
+    const float* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ w2, float* __restrict__ dP,
+    float* __restrict__ dw2_part, int rows, int R) {
+  constexpr int NG = kWave / G;
+  __shared__ float4 red[kSpWaves][G];
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int g = lane / G, gl = lane % G, c = gl * 4;
+  const bool cok = c < R;
+  const float4 bb = cok ? ld4(b1 + c) : make_float4(0, 0, 0, 0);
+  const float4 wv = cok ? ld4(w2 + c) : make_float4(0, 0, 0, 0);
+  float dw[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = blockIdx.x * kSpWaves + wave; r < rows;
+       r += gridDim.x * kSpWaves) {
+    float pv[4] = {0.f, 0.f, 0.f, 0.f}, dp[4] = {0.f, 0.f, 0.f, 0.f};
+    if (cok) {
+      const float4 p = ld4(P + (size_t)r * R + c);
+      pv[0] = p.x + bb.x; pv[1] = p.y + bb.y;
+      pv[2] = p.z + bb.z; pv[3] = p.w + bb.w;
+    }
+    const int p0 = rowptr[r], p1 = rowptr[r + 1];
+    for (int p = p0 + g; p < p1; p += NG) {
+      if (!cok) continue;
+      const float gv = Gr[p];
+      const float4 q4 = ld4(Q + (size_t)col[p] * R + c);
+      const float q[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float z = pv[k] - q[k];
+        if (z > 0.f) {
+          dp[k] += gv;
+          dw[k] = fmaf(gv, z, dw[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dp[k] += __shfl_xor(dp[k], off);
+    if (g == 0 && cok)
+      *reinterpret_cast<float4*>(dP + (size_t)r * R + c) =
+          make_float4(dp[0] * wv.x, dp[1] * wv.y, dp[2] * wv.z, dp[3] * wv.w);
+  }
+#pragma unroll
+  for (int off = G; off < kWave; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dw[k] += __shfl_xor(dw[k], off);
+  if (g == 0) red[wave][gl] = make_float4(dw[0], dw[1], dw[2], dw[3]);
+  __syncthreads();
+  if (threadIdx.x < G && threadIdx.x * 4 < R) {
+    float4 s = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < kSpWaves; ++w) {
+      const float4 t = red[w][threadIdx.x];
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    *reinterpret_cast<float4*>(dw2_part + (size_t)blockIdx.x * R +
+                               threadIdx.x * 4) = s;
+  }
+}
+
+// dQ[j] = -w2 * sum_{e in col j} g_e [P_row(e) + b1 - Q_j > 0], walked in
+// pieces of <= T entries (spmm.hip's piece plan), one G-lane group per piece:
+// a target picked by thousands of source rows no longer serialises the
+// kernel, and short columns are packed 64 / G to a wave.
+template <int G>
+__global__ __launch_bounds__(256) void sparse_consensus_bwd_cols_piece_kernel(
+    const int* __restrict__ row_of, const int* __restrict__ perm,
+    const int* __restrict__ prow, const int* __restrict__ pbeg,
+    const int* __restrict__ pend, int npieces, const float* __restrict__ Gr,
+    const float* __restrict__ P, const float* __restrict__ Q,
+    const float* __restrict__ b1, const float* __restrict__ w2,
+    float* __restrict__ dQ, float* __restrict__ part, int cols, int R) {
+  constexpr int PPB = 256 / G;
+  const int v = xcd_remap(blockIdx.x, gridDim.x) * PPB + threadIdx.x / G;
+  const int c = (threadIdx.x % G) * 4;
+  if (v >= npieces || c >= R) return;
+  const int code = prow[v];
+  if (code >= cols) return;
+  const bool single = code >= 0;
+  const int j = single ? code : ~code;
+  const int beg = pbeg[v], end = pend[v];
+  const float4 q = ld4(Q + (size_t)j * R + c), bb = ld4(b1 + c);
+  const float qb[4] = {bb.x - q.x, bb.y - q.y, bb.z - q.z, bb.w - q.w};
+  float dq[4] = {0.f, 0.f, 0.f, 0.f};
+  int e = beg;
+  for (; e + 2 <= end; e += 2) {
+    float gv[2];
+    float4 pr[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      gv[u] = Gr[perm[e + u]];
+      pr[u] = ld4(P + (size_t)row_of[e + u] * R + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (pr[u].x + qb[0] > 0.f) dq[0] += gv[u];
+      if (pr[u].y + qb[1] > 0.f) dq[1] += gv[u];
+      if (pr[u].z + qb[2] > 0.f) dq[2] += gv[u];
+      if (pr[u].w + qb[3] > 0.f) dq[3] += gv[u];
+    }
+  }
+  if (e < end) {
+    const float gv = Gr[perm[e]];
+    const float4 pr = ld4(P + (size_t)row_of[e] * R + c);
+    if (pr.x + qb[0] > 0.f) dq[0] += gv;
+    if (pr.y + qb[1] > 0.f) dq[1] += gv;
+    if (pr.z + qb[2] > 0.f) dq[2] += gv;
+    if (pr.w + qb[3] > 0.f) dq[3] += gv;
+  }
+  if (single) {
+    const float4 w = ld4(w2 + c);
+    *reinterpret_cast<float4*>(dQ + (size_t)j * R + c) =
+        make_float4(-dq[0] * w.x, -dq[1] * w.y, -dq[2] * w.z, -dq[3] * w.w);
+  } else {
+    *reinterpret_cast<float4*>(part + (size_t)v * R + c) =
+        make_float4(dq[0], dq[1], dq[2], dq[3]);
+  }
+}
+
+void spmm_piece_fold_f32(const at::Tensor& pptr, const at::Tensor& part,
+                         int R, int C, const float* colscale, float sign,
+                         float* out);
+
+// Lanes per candidate for the group kernels (0: not eligible).
+static int group_lanes(int64_t C, std::initializer_list<const void*> ptrs) {
+  if (C % 4 != 0 || C > 256 || C == 0) return 0;
+  for (const void* p : ptrs)
+    if (!aligned16(p)) return 0;
+  int G = 1;
+  while (G * 4 < C) G <<= 1;
+  return G;
+}
+
+#define DGMC_GROUP_DISPATCH(G, ...)                             \
+  switch (G) {                                                  \
+    case 1: { constexpr int GG = 1; __VA_ARGS__; } break;       \
+    case 2: { constexpr int GG = 2; __VA_ARGS__; } break;       \
+    case 4: { constexpr int GG = 4; __VA_ARGS__; } break;       \
+    case 8: { constexpr int GG = 8; __VA_ARGS__; } break;       \
+    case 16: { constexpr int GG = 16; __VA_ARGS__; } break;     \
+    case 32: { constexpr int GG = 32; __VA_ARGS__; } break;     \
+    default: { constexpr int GG = 64; __VA_ARGS__; } break;     \
+  }
+
+// ---------------------------------------------------------------------------
 static void check_f32_2d(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kFloat &&
                   t.is_contiguous(),
@@ -195,6 +441,16 @@ at::Tensor sddmm(const at::Tensor& rowptr, const at::Tensor& col,
   TORCH_CHECK(rows == A.size(0), "sddmm: rowptr / A rows mismatch");
   at::Tensor val = at::empty({col.numel()}, A.options());
   if (rows == 0 || col.numel() == 0) return val.zero_();
+  const int G = group_lanes(A.size(1), {A.data_ptr(), B.data_ptr()});
+  if (G > 0) {
+    DGMC_GROUP_DISPATCH(G, hipLaunchKernelGGL(
+        sddmm_g_kernel<GG>, dim3(sp_blocks(rows)), dim3(256), 0, stream(),
+        rowptr.data_ptr<int>(), col.data_ptr<int>(), A.data_ptr<float>(),
+        B.data_ptr<float>(), val.data_ptr<float>(), (int)rows,
+        (int)A.size(1)));
+    DGMC_CHECK_LAUNCH();
+    return val;
+  }
   hipLaunchKernelGGL(sddmm_kernel, dim3(sp_blocks(rows)), dim3(256), 0,
                      stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
                      A.data_ptr<float>(), B.data_ptr<float>(),
@@ -219,6 +475,18 @@ at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
               "sparse_consensus_fwd: S_hat");
   at::Tensor out = at::empty_like(S_hat);
   if (rows == 0) return out;
+  const int G = group_lanes(R, {P.data_ptr(), Q.data_ptr(), b1.data_ptr(),
+                                w2.data_ptr()});
+  if (G > 0) {
+    DGMC_GROUP_DISPATCH(G, hipLaunchKernelGGL(
+        sparse_consensus_fwd_g_kernel<GG>, dim3(sp_blocks(rows)), dim3(256),
+        0, stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+        S_hat.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+        out.data_ptr<float>(), (int)rows, R));
+    DGMC_CHECK_LAUNCH();
+    return out;
+  }
   hipLaunchKernelGGL(sparse_consensus_fwd_kernel, dim3(sp_blocks(rows)),
                      dim3(256), 0, stream(), rowptr.data_ptr<int>(),
                      col.data_ptr<int>(), S_hat.data_ptr<float>(),
@@ -234,18 +502,40 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
     const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& colptr,
     const at::Tensor& row_of, const at::Tensor& perm, const at::Tensor& G,
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
-    const at::Tensor& w2) {
+    const at::Tensor& w2, const c10::optional<at::Tensor>& pptr,
+    const c10::optional<at::Tensor>& prow,
+    const c10::optional<at::Tensor>& pbeg,
+    const c10::optional<at::Tensor>& pend) {
   check_f32_2d(P, "P");
   check_f32_2d(Q, "Q");
-  TORCH_CHECK(perm.scalar_type() == at::kLong, "perm must be int64");
+  const bool pieces = pptr.has_value() && pptr->defined() &&
+                      prow.has_value() && prow->defined() &&
+                      pbeg.has_value() && pbeg->defined() &&
+                      pend.has_value() && pend->defined();
+  TORCH_CHECK(pieces ? perm.scalar_type() == at::kInt
+                     : perm.scalar_type() == at::kLong,
+              "perm must be int32 with a piece plan, int64 otherwise");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(P.device());
   const int64_t rows = rowptr.numel() - 1, cols = colptr.numel() - 1;
   const int R = P.size(1);
   TORCH_CHECK(rows == P.size(0) && cols == Q.size(0), "shape mismatch");
+  TORCH_CHECK(G.numel() == col.numel() && perm.numel() == col.numel() &&
+                  row_of.numel() == col.numel(),
+              "sparse_consensus_bwd: entry arrays");
   at::Tensor dP = at::empty_like(P), dQ = at::empty_like(Q);
   const int nb = std::max(1, std::min(sp_blocks(rows), 1024));
   at::Tensor dw2 = at::empty({nb, R}, P.options());
-  if (rows > 0) {
+  const int Gl = group_lanes(R, {P.data_ptr(), Q.data_ptr(), b1.data_ptr(),
+                                 w2.data_ptr()});
+  if (rows > 0 && Gl > 0) {
+    DGMC_GROUP_DISPATCH(Gl, hipLaunchKernelGGL(
+        sparse_consensus_bwd_rows_g_kernel<GG>, dim3(nb), dim3(256), 0,
+        stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+        G.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        b1.data_ptr<float>(), w2.data_ptr<float>(), dP.data_ptr<float>(),
+        dw2.data_ptr<float>(), (int)rows, R));
+    DGMC_CHECK_LAUNCH();
+  } else if (rows > 0) {
     hipLaunchKernelGGL(sparse_consensus_bwd_rows_kernel, dim3(nb), dim3(256),
                        0, stream(), rowptr.data_ptr<int>(),
                        col.data_ptr<int>(), G.data_ptr<float>(),
@@ -257,10 +547,33 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
   } else {
     dw2.zero_();
   }
-  if (cols > 0) {
+  if (cols > 0 && pieces && Gl > 0) {
+    TORCH_CHECK(pptr->scalar_type() == at::kInt &&
+                    prow->scalar_type() == at::kInt &&
+                    pbeg->scalar_type() == at::kInt &&
+                    pend->scalar_type() == at::kInt &&
+                    pptr->numel() == cols + 1 &&
+                    prow->numel() == pbeg->numel() &&
+                    prow->numel() == pend->numel(),
+                "sparse_consensus_bwd: piece plan");
+    const int npieces = (int)prow->numel();
+    at::Tensor part = at::empty({(int64_t)npieces, R}, P.options());
+    DGMC_GROUP_DISPATCH(Gl, hipLaunchKernelGGL(
+        sparse_consensus_bwd_cols_piece_kernel<GG>,
+        dim3((npieces + 256 / GG - 1) / (256 / GG)), dim3(256), 0, stream(),
+        row_of.data_ptr<int>(), perm.data_ptr<int>(), prow->data_ptr<int>(),
+        pbeg->data_ptr<int>(), pend->data_ptr<int>(), npieces,
+        G.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        b1.data_ptr<float>(), w2.data_ptr<float>(), dQ.data_ptr<float>(),
+        part.data_ptr<float>(), (int)cols, R));
+    DGMC_CHECK_LAUNCH();
+    spmm_piece_fold_f32(*pptr, part, (int)cols, R, w2.data_ptr<float>(), -1.f,
+                        dQ.data_ptr<float>());
+  } else if (cols > 0) {
+    at::Tensor perm64 = perm.to(at::kLong);
     hipLaunchKernelGGL(sparse_consensus_bwd_cols_kernel, dim3(sp_blocks(cols)),
                        dim3(256), 0, stream(), colptr.data_ptr<int>(),
-                       row_of.data_ptr<int>(), perm.data_ptr<int64_t>(),
+                       row_of.data_ptr<int>(), perm64.data_ptr<int64_t>(),
                        G.data_ptr<float>(), P.data_ptr<float>(),
                        Q.data_ptr<float>(), b1.data_ptr<float>(),
                        w2.data_ptr<float>(), dQ.data_ptr<float>(), (int)cols,

@@ -212,4 +212,315 @@ void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
   spmm_into(rowptr, col, val, x, self_x, self_scale, bias, relu, out);
 }
 
+// ---------------------------------------------------------------------------
+// Piece-balanced SpMM for operators with skewed row lengths.
+//
+// The row-per-lane-group kernel above walks a row serially, so one hub row
+// sets the kernel time: knowledge-graph entities with hundreds of
+// neighbours (RelConv, reference rel.py:26-31) and, worse, target columns of
+// a top-k candidate set that thousands of source rows picked (the transport
+// r_t = S^T r_s, reference dgmc.py:209-212, walks those columns) - 1.7k
+// entries in one column of the DBP15K-shaped run.  Here every row is cut
+// into pieces of at most T entries; the plan (piece_plan below, built on the
+// device without a host sync) stores per piece its row (bit-inverted when
+// the row has several pieces) and entry range, so a lane group starts its
+// gathers after ONE round of plan loads.
+//
+//   pass 1  a G-lane group per piece (64/G pieces per wave: short rows are
+//           packed 8 to a wave at C = 32 fp32, so the grid stays within one
+//           round of resident waves), 4 gathers in flight per group.  A row
+//           of one piece is finished in place (self term, bias, ReLU);
+//           otherwise the piece's fp32 partial is stored.
+//   pass 2  rows of several pieces add their partials in piece order.
+//
+// Deterministic (fixed summation order, no atomics).  `perm` (optional)
+// reads entry values through a permutation, so a CSC walk over the CSR
+// values (val[perm[e]]) needs no gathered copy of them.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void piece_plan_fill_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ pptr, int R,
+    int T, int* __restrict__ prow, int* __restrict__ pbeg,
+    int* __restrict__ pend) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const int q0 = pptr[r], np = pptr[r + 1] - q0;
+  const int e0 = rowptr[r], e1 = rowptr[r + 1];
+  const int code = np == 1 ? r : ~r;
+  for (int q = 0; q < np; ++q) {
+    const int b = e0 + q * T;
+    prow[q0 + q] = code;
+    pbeg[q0 + q] = b;
+    pend[q0 + q] = min(e1, b + T);
+  }
+}
+
+// (pptr [R+1], prow/pbeg/pend [R + nnz / T + 1]); unused tail slots hold
+// prow = R (skipped by the kernels).
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
+    const at::Tensor& rowptr, int64_t nnz, int64_t T) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rowptr.device());
+  TORCH_CHECK(rowptr.is_cuda() && rowptr.scalar_type() == at::kInt &&
+                  rowptr.dim() == 1 && rowptr.numel() >= 1 && T >= 1,
+              "piece_plan: int32 rowptr expected");
+  const int64_t R = rowptr.numel() - 1;
+  const int64_t P = R + nnz / T + 1;
+  TORCH_CHECK(P < INT32_MAX, "piece_plan: size");
+  at::Tensor counts = rowptr.slice(0, 1) - rowptr.slice(0, 0, R);
+  at::Tensor npc = at::clamp_min(at::floor_divide(counts + (int)(T - 1), T), 1);
+  at::Tensor pptr = at::zeros({R + 1}, rowptr.options());
+  if (R > 0) pptr.slice(0, 1).copy_(at::cumsum(npc, 0, at::kInt));
+  at::Tensor prow = at::full({P}, (int)R, rowptr.options());
+  at::Tensor pbeg = at::zeros({P}, rowptr.options());
+  at::Tensor pend = at::zeros({P}, rowptr.options());
+  if (R > 0) {
+    hipLaunchKernelGGL(piece_plan_fill_kernel, dim3((unsigned)((R + 255) / 256)),
+                       dim3(256), 0, stream(), rowptr.data_ptr<int>(),
+                       pptr.data_ptr<int>(), (int)R, (int)T,
+                       prow.data_ptr<int>(), pbeg.data_ptr<int>(),
+                       pend.data_ptr<int>());
+    DGMC_CHECK_LAUNCH();
+  }
+  return {pptr, prow, pbeg, pend};
+}
+
+template <typename TIn, typename TOut, int VEC>
+__device__ __forceinline__ void spmm_finish(float* acc, int r, int c0, int C,
+                                            const TIn* __restrict__ self_x,
+                                            float scale,
+                                            const float* __restrict__ bias,
+                                            int relu, TOut* __restrict__ out) {
+  if (self_x != nullptr) {
+    float v[VEC];
+    load_vec<TIn, VEC>(self_x + (size_t)r * C + c0, v);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = fmaf(scale, v[k], acc[k]);
+  }
+  if (bias != nullptr) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] += bias[c0 + k];
+  }
+  if (relu) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = fmaxf(acc[k], 0.f);
+  }
+  store_row<TOut, VEC>(out + (size_t)r * C + c0, acc);
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_f32(float* __restrict__ p,
+                                          const float* v) {
+#pragma unroll
+  for (int k = 0; k < VEC; k += 4) store_vec<float, 4>(p + k, v + k);
+}
+
+template <typename TIn, typename TOut, int VEC, int G>
+__global__ __launch_bounds__(256) void spmm_piece_kernel(
+    const int* __restrict__ col, const float* __restrict__ val,
+    const int* __restrict__ perm, const int* __restrict__ prow,
+    const int* __restrict__ pbeg, const int* __restrict__ pend, int npieces,
+    const TIn* __restrict__ x, const TIn* __restrict__ self_x,
+    const float* __restrict__ self_scale, const float* __restrict__ bias,
+    TOut* __restrict__ out, float* __restrict__ part, int R, int C,
+    int relu) {
+  constexpr int PPB = 256 / G;    // pieces per block
+  const int v = xcd_remap(blockIdx.x, gridDim.x) * PPB + threadIdx.x / G;
+  const int gl = threadIdx.x % G;
+  if (v >= npieces) return;
+  const int code = prow[v];
+  if (code >= R) return;          // unused plan slot
+  const int beg = pbeg[v], end = pend[v];
+  const bool single = code >= 0;
+  const int r = single ? code : ~code;
+  const float scale = self_x != nullptr ? self_scale[0] : 0.f;
+
+  for (int c0 = gl * VEC; c0 < C; c0 += G * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    int p = beg;
+    for (; p + 4 <= end; p += 4) {
+      float xv[4][VEC];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = p + u;
+        w[u] = val[perm != nullptr ? perm[e] : e];
+        load_vec<TIn, VEC>(x + (size_t)col[e] * C + c0, xv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
+    }
+    for (; p < end; ++p) {
+      const float w = val[perm != nullptr ? perm[p] : p];
+      float xv[VEC];
+      load_vec<TIn, VEC>(x + (size_t)col[p] * C + c0, xv);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[k], acc[k]);
+    }
+    if (single)
+      spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu,
+                                  out);
+    else
+      store_f32<VEC>(part + (size_t)v * C + c0, acc);
+  }
+}
+
+// Pass 2: rows with several pieces.  `colscale` (optional) multiplies channel
+// c by sign * colscale[c] before the epilogue (the -w2 of the consensus
+// backward, sparse_corr.hip).
+template <typename TIn, typename TOut, int VEC>
+__global__ __launch_bounds__(256) void spmm_piece_fold_kernel(
+    const int* __restrict__ pptr, const float* __restrict__ part, int R, int C,
+    const TIn* __restrict__ self_x, const float* __restrict__ self_scale,
+    const float* __restrict__ bias, int relu,
+    const float* __restrict__ colscale, float sign, TOut* __restrict__ out) {
+  const int nv = C / VEC;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(t / nv);
+  if (r >= R) return;
+  const int c0 = (int)(t % nv) * VEC;
+  const int q0 = pptr[r], q1 = pptr[r + 1];
+  if (q1 - q0 <= 1) return;
+  float acc[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+  for (int q = q0; q < q1; ++q) {
+    float pv[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; k += 4)
+      load_vec<float, 4>(part + (size_t)q * C + c0 + k, pv + k);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] += pv[k];
+  }
+  if (colscale != nullptr) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] *= sign * colscale[c0 + k];
+  }
+  const float scale = self_x != nullptr ? self_scale[0] : 0.f;
+  spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu, out);
+}
+
+void spmm_piece_fold_f32(const at::Tensor& pptr, const at::Tensor& part,
+                         int R, int C, const float* colscale, float sign,
+                         float* out) {
+  const int64_t n = (int64_t)R * (C / 4);
+  if (n == 0) return;
+  hipLaunchKernelGGL((spmm_piece_fold_kernel<float, float, 4>),
+                     dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream(),
+                     pptr.data_ptr<int>(), part.data_ptr<float>(), R, C,
+                     (const float*)nullptr, (const float*)nullptr,
+                     (const float*)nullptr, 0, colscale, sign, out);
+  DGMC_CHECK_LAUNCH();
+}
+
+static void check_plan(const at::Tensor& pptr, const at::Tensor& prow,
+                       const at::Tensor& pbeg, const at::Tensor& pend,
+                       int64_t R) {
+  TORCH_CHECK(pptr.scalar_type() == at::kInt && prow.scalar_type() == at::kInt &&
+                  pbeg.scalar_type() == at::kInt &&
+                  pend.scalar_type() == at::kInt,
+              "piece plan: int32 tensors expected");
+  TORCH_CHECK(pptr.numel() == R + 1 && prow.numel() == pbeg.numel() &&
+                  prow.numel() == pend.numel(),
+              "piece plan: sizes do not match the operator");
+}
+
+void spmm_pieces_out(const at::Tensor& rowptr, const at::Tensor& col,
+                     const at::Tensor& val, const c10::optional<at::Tensor>& perm,
+                     const at::Tensor& pptr, const at::Tensor& prow,
+                     const at::Tensor& pbeg, const at::Tensor& pend,
+                     const at::Tensor& x,
+                     const c10::optional<at::Tensor>& self_x,
+                     const c10::optional<at::Tensor>& self_scale,
+                     const c10::optional<at::Tensor>& bias, bool relu,
+                     at::Tensor out) {
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous(),
+              "spmm_pieces: x");
+  TORCH_CHECK(rowptr.scalar_type() == at::kInt && col.scalar_type() == at::kInt,
+              "spmm_pieces: int32 index expected");
+  TORCH_CHECK(val.scalar_type() == at::kFloat, "spmm_pieces: fp32 values");
+  const int64_t R = rowptr.numel() - 1, C = x.size(1);
+  check_plan(pptr, prow, pbeg, pend, R);
+  TORCH_CHECK(out.is_contiguous() && out.numel() == R * C &&
+                  out.device() == x.device(),
+              "spmm_pieces: out must be a contiguous [R, C] tensor");
+  const int* permp = nullptr;
+  if (perm.has_value() && perm->defined()) {
+    TORCH_CHECK(perm->scalar_type() == at::kInt && perm->numel() == col.numel(),
+                "spmm_pieces: perm must be int32 [nnz]");
+    permp = perm->data_ptr<int>();
+  } else {
+    TORCH_CHECK(val.numel() == col.numel(), "spmm_pieces: col/val size");
+  }
+  if (R == 0 || C == 0) return;
+  at::Tensor sx_c, ss_c, b_c;
+  if (self_x.has_value() && self_x->defined()) {
+    sx_c = self_x->contiguous();
+    TORCH_CHECK(sx_c.scalar_type() == x.scalar_type() && sx_c.size(0) == R &&
+                    sx_c.size(1) == C,
+                "spmm_pieces: self_x must match x dtype and [R, C]");
+    TORCH_CHECK(self_scale.has_value() && self_scale->defined(),
+                "spmm_pieces: self_scale required with self_x");
+    ss_c = self_scale->to(at::kFloat).contiguous();
+  }
+  if (bias.has_value() && bias->defined()) {
+    b_c = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b_c.numel() == C, "spmm_pieces: bias size");
+  }
+  const int elt = (int)x.element_size();
+  const bool vec_ok = aligned16(x.data_ptr()) &&
+                      (!sx_c.defined() || aligned16(sx_c.data_ptr())) &&
+                      aligned16(out.data_ptr()) && (C * elt) % 16 == 0;
+  if (!vec_ok) {
+    // Unvectorisable shapes: the row kernel on the (permuted) values.
+    at::Tensor v = permp ? val.index_select(0, perm->to(at::kLong)) : val;
+    spmm_into(rowptr, col, v, x, sx_c.defined() ? c10::optional<at::Tensor>(sx_c)
+                                                : c10::nullopt,
+              ss_c.defined() ? c10::optional<at::Tensor>(ss_c) : c10::nullopt,
+              b_c.defined() ? c10::optional<at::Tensor>(b_c) : c10::nullopt,
+              relu, out);
+    return;
+  }
+  const int npieces = (int)prow.numel();
+  at::Tensor part = at::empty({(int64_t)npieces, C}, x.options().dtype(at::kFloat));
+  DGMC_DISPATCH_FLOAT(x.scalar_type(), TIn, [&] {
+    constexpr int V = Vec16<TIn>::N;
+    const TIn* xp = reinterpret_cast<const TIn*>(x.data_ptr());
+    const TIn* sp = sx_c.defined() ? reinterpret_cast<const TIn*>(sx_c.data_ptr())
+                                   : nullptr;
+    const float* ssp = ss_c.defined() ? ss_c.data_ptr<float>() : nullptr;
+    const float* bp = b_c.defined() ? b_c.data_ptr<float>() : nullptr;
+    DGMC_DISPATCH_FLOAT(out.scalar_type(), TOut, [&] {
+      TOut* op = reinterpret_cast<TOut*>(out.data_ptr());
+      const int lanes = (int)(C / V);
+      auto go = [&](auto gtag) {
+        constexpr int G = decltype(gtag)::value;
+        const int blocks = (npieces + 256 / G - 1) / (256 / G);
+        hipLaunchKernelGGL((spmm_piece_kernel<TIn, TOut, V, G>), dim3(blocks),
+                           dim3(256), 0, stream(), col.data_ptr<int>(),
+                           val.data_ptr<float>(), permp, prow.data_ptr<int>(),
+                           pbeg.data_ptr<int>(), pend.data_ptr<int>(), npieces,
+                           xp, sp, ssp, bp, op, part.data_ptr<float>(), (int)R,
+                           (int)C, relu ? 1 : 0);
+        DGMC_CHECK_LAUNCH();
+      };
+      if (lanes <= 4) go(std::integral_constant<int, 4>());
+      else if (lanes <= 8) go(std::integral_constant<int, 8>());
+      else if (lanes <= 16) go(std::integral_constant<int, 16>());
+      else if (lanes <= 32) go(std::integral_constant<int, 32>());
+      else go(std::integral_constant<int, 64>());
+      const int64_t n = R * (C / V);
+      hipLaunchKernelGGL((spmm_piece_fold_kernel<TIn, TOut, V>),
+                         dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                         stream(), pptr.data_ptr<int>(), part.data_ptr<float>(),
+                         (int)R, (int)C, sp, ssp, bp, relu ? 1 : 0,
+                         (const float*)nullptr, 1.f, op);
+      DGMC_CHECK_LAUNCH();
+    });
+  });
+}
+
 }  // namespace dgmc

@@ -192,4 +192,7 @@ def relational_plan(edge_index, num_nodes):
     col = torch.cat([src * 3 + 0, dst * 3 + 1, ar * 3 + 2])
     val = torch.cat([inv_in[dst], inv_out[src], torch.ones(N, device=device)])
     plan = SparseOperator.from_coo(row, col, val, N, 3 * N)
+    # Knowledge graphs have hub entities (hundreds of neighbours per flow):
+    # walk rows in pieces so one hub does not serialise the SpMM.
+    plan.balanced = True
     return _CACHE.put((edge_index, ), params, plan)

@@ -27,10 +27,51 @@ from ..runtime import streams
 from . import reference as ref
 
 
-class SparseOperator(object):
-    r"""Fixed-structure, fixed-value CSR matrix of shape ``[R, C]``."""
+PIECE = 16   # entries per piece of the balanced SpMM (spmm.hip)
 
-    def __init__(self, rowptr, col, val, num_rows, num_cols, row=None):
+
+def piece_plan(rowptr, nnz, T=PIECE):
+    """Cut every CSR row into pieces of at most ``T`` entries (an empty row
+    keeps one empty piece, so every row is written).  Returns int32
+    ``pptr [R + 1]`` (first piece of each row) and, per piece slot
+    (``R + nnz // T + 1`` of them, a static bound - no host sync),
+    ``prow`` (the row, bit-inverted ``~r`` when the row has several pieces;
+    ``R`` for unused slots), ``pbeg`` / ``pend`` (entry range).  Built by one
+    HIP kernel on the GPU (``spmm.hip::piece_plan``)."""
+    if _backend.use_hip(rowptr):
+        return tuple(_backend.ops().piece_plan(rowptr, int(nnz), int(T)))
+    R = rowptr.numel() - 1
+    dev = rowptr.device
+    rowptr = rowptr.to(torch.int32)
+    counts = rowptr[1:] - rowptr[:-1]
+    npc = torch.clamp_min(torch.div(counts + (T - 1), T,
+                                    rounding_mode='floor'), 1)
+    pptr = torch.zeros(R + 1, dtype=torch.int32, device=dev)
+    torch.cumsum(npc, 0, dtype=torch.int32, out=pptr[1:])
+    P = R + int(nnz) // T + 1
+    v = torch.arange(P, dtype=torch.int32, device=dev)
+    row = torch.searchsorted(pptr[1:], v, right=True, out_int32=True)
+    used = row < R
+    r = torch.where(used, row, torch.zeros_like(row)).long()
+    beg = rowptr[r] + (v - pptr[r]) * T
+    end = torch.minimum(rowptr[r + 1], beg + T)
+    code = torch.where(npc[r] > 1, -row - 1, row)
+    prow = torch.where(used, code, torch.full_like(row, R))
+    pbeg = torch.where(used, beg, torch.zeros_like(beg))
+    pend = torch.where(used, end, torch.zeros_like(end))
+    return pptr, prow, pbeg.to(torch.int32), pend.to(torch.int32)
+
+
+class SparseOperator(object):
+    r"""Fixed-structure, fixed-value CSR matrix of shape ``[R, C]``.
+
+    ``balanced``: rows can be long and skewed (knowledge-graph hubs), so the
+    HIP SpMM walks them in pieces of :data:`PIECE` entries
+    (:func:`piece_plan`, ``spmm.hip::spmm_piece_kernel``) instead of one
+    lane group per row.  Inherited by the transpose."""
+
+    def __init__(self, rowptr, col, val, num_rows, num_cols, row=None,
+                 balanced=False):
         self.rowptr = rowptr.to(torch.int32).contiguous()
         self.col = col.to(torch.int32).contiguous()
         self.val = val.to(torch.float32).contiguous()
@@ -38,6 +79,14 @@ class SparseOperator(object):
         self.num_cols = int(num_cols)
         self._row = row
         self._t = None
+        self.balanced = balanced
+        self._pieces = None
+
+    def pieces(self):
+        """``(pptr, prow, pbeg, pend)`` of :func:`piece_plan` (cached)."""
+        if self._pieces is None:
+            self._pieces = piece_plan(self.rowptr, self.nnz)
+        return self._pieces
 
     @property
     def nnz(self):
@@ -77,6 +126,7 @@ class SparseOperator(object):
                                               self.val, self.num_cols,
                                               self.num_rows)
             self._t._t = self
+            self._t.balanced = self.balanced
         return self._t
 
     def slot_csr(self, num_slots):
@@ -105,7 +155,27 @@ class SparseOperator(object):
             self.num_rows, self.num_cols, self.nnz)
 
 
+def spmm_out(op, x, out, self_x=None, self_scale=None, bias=None,
+             relu=False):
+    """HIP SpMM into ``out`` (piece-balanced for ``op.balanced``)."""
+    if op.balanced:
+        _backend.ops().spmm_pieces_out(
+            op.rowptr, op.col, op.val, None, *op.pieces(), x, self_x,
+            self_scale, bias, relu, out)
+    else:
+        _backend.ops().spmm_csr_out(op.rowptr, op.col, op.val, x, self_x,
+                                    self_scale, bias, relu, out)
+    return out
+
+
 def _spmm_raw(op, x, self_x, self_scale, bias, relu, out_dtype):
+    if _backend.use_hip(x) and op.balanced:
+        x = x.contiguous()
+        out = torch.empty((op.num_rows, x.size(1)), dtype=out_dtype,
+                          device=x.device)
+        return spmm_out(op, x, out, self_x.contiguous()
+                        if self_x is not None else None, self_scale, bias,
+                        relu)
     if _backend.use_hip(x):
         return _backend.ops().spmm_csr(
             op.rowptr, op.col, op.val, x.contiguous(),
@@ -387,8 +457,7 @@ class _GemmSpMM(torch.autograd.Function):
             if gx.dtype != ctx.x_dtype:
                 gx = gx.to(ctx.x_dtype)
         elif dy is not None and hip:
-            _backend.ops().spmm_csr_out(opt.rowptr, opt.col, opt.val, g,
-                                        None, None, None, False, dy)
+            spmm_out(opt, g, dy)
         elif dy is not None:
             dy.copy_(_spmm_raw(opt, g, None, None, None, False, w_lp.dtype))
         else:

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from . import _backend
 from . import reference as ref
-from .sparse import SparseOperator
+from .sparse import SparseOperator, piece_plan
 
 
 TOPK_EXACT = os.environ.get('DGMC_AMD_TOPK_EXACT', '0') == '1'
@@ -71,6 +71,12 @@ class CandidateGraph(object):
         torch.cumsum(counts, 0, out=colptr[1:])
         self.colptr = colptr.to(torch.int32)
         self.row_of = (self.perm // k).to(torch.int32)
+        self.perm32 = self.perm.to(torch.int32)
+        # Column walks (transport, consensus dQ, gather-dot dB) in pieces of
+        # <= sparse.PIECE entries: with random-init embeddings a few targets sit in
+        # the top-k of thousands of rows (hubness), which would serialise a
+        # column-per-wave kernel.
+        self.col_pieces = piece_plan(self.colptr, col.numel())
 
     def op(self, val):
         """``[rows, cols]`` operator with per-entry values ``val``."""
@@ -88,6 +94,18 @@ def _spmm(op, x):
                                    None, None, None, False, torch.float32)
 
 
+def _spmm_t(cand, val, x):
+    """``op_t(val) @ x`` (targets <- sources) by the piece-balanced SpMM over
+    the CSC, reading ``val`` through the CSC permutation in place."""
+    x = x.contiguous()
+    out = torch.empty((cand.cols, x.size(1)), dtype=torch.float32,
+                      device=x.device)
+    _backend.ops().spmm_pieces_out(cand.colptr, cand.row_of, val.contiguous(),
+                                   cand.perm32, *cand.col_pieces, x, None,
+                                   None, None, False, out)
+    return out
+
+
 # ---------------------------------------------------------------------------
 class _GatherDot(torch.autograd.Function):
     @staticmethod
@@ -102,7 +120,7 @@ class _GatherDot(torch.autograd.Function):
         cand = ctx.cand
         g = g.contiguous().float()
         dA = _spmm(cand.op(g), Bm) if ctx.needs_input_grad[0] else None
-        dB = _spmm(cand.op_t(g), A) if ctx.needs_input_grad[1] else None
+        dB = _spmm_t(cand, g, A) if ctx.needs_input_grad[1] else None
         return dA, dB, None
 
 
@@ -125,7 +143,7 @@ class _SparseTransport(torch.autograd.Function):
     def forward(ctx, S, r_s, cand):
         ctx.cand = cand
         ctx.save_for_backward(r_s)
-        return _spmm(cand.op_t(S), r_s)
+        return _spmm_t(cand, S, r_s)
 
     @staticmethod
     def backward(ctx, g):
@@ -169,8 +187,9 @@ class _SparseConsensus(torch.autograd.Function):
         cand = ctx.cand
         g = g.contiguous().float()
         dP, dQ, dw2_part = _backend.ops().sparse_consensus_bwd(
-            cand.rowptr, cand.col, cand.colptr, cand.row_of, cand.perm, g,
-            P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1))
+            cand.rowptr, cand.col, cand.colptr, cand.row_of, cand.perm32, g,
+            P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1),
+            *cand.col_pieces)
         b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
         db1 = dP.sum(0).to(b1_dt)
         dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)

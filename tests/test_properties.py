@@ -33,6 +33,40 @@ def test_csr_from_coo_and_transpose(R, C, nnz, seed):
 
 
 @settings(**SETTINGS)
+@given(st.lists(st.integers(0, 300), min_size=1, max_size=20),
+       st.sampled_from([1, 4, 64]))
+def test_piece_plan_covers_every_entry_once(degrees, T):
+    """piece_plan: every row gets max(1, ceil(deg / T)) pieces, in row
+    order; pieces tile each row's entries exactly; unused slots map to R."""
+    from deep_graph_matching_consensus_amd.ops.sparse import piece_plan
+    deg = torch.tensor(degrees)
+    rowptr = torch.zeros(len(degrees) + 1, dtype=torch.int32)
+    rowptr[1:] = torch.cumsum(deg, 0)
+    nnz = int(deg.sum())
+    pptr, prow, pbeg, pend = piece_plan(rowptr, nnz, T)
+    R = len(degrees)
+    assert prow.numel() == R + nnz // T + 1
+    seen = torch.zeros(nnz, dtype=torch.int64)
+    for v in range(prow.numel()):
+        code = int(prow[v])
+        if code == R:
+            assert v >= int(pptr[-1])
+            continue
+        r = code if code >= 0 else -code - 1
+        npieces = int(pptr[r + 1] - pptr[r])
+        assert (code < 0) == (npieces > 1)
+        q = v - int(pptr[r])
+        beg = int(rowptr[r]) + q * T
+        end = min(int(rowptr[r + 1]), beg + T)
+        assert 0 <= q < npieces
+        assert (int(pbeg[v]), int(pend[v])) == (beg, end)
+        seen[beg:end] += 1
+    assert (seen == 1).all()
+    assert ((pptr[1:] - pptr[:-1]) ==
+            torch.clamp_min((deg + T - 1) // T, 1)).all()
+
+
+@settings(**SETTINGS)
 @given(st.lists(st.integers(0, 9), min_size=1, max_size=8),
        st.integers(1, 4))
 def test_dense_layout_round_trip_matches_mask_layout(counts, C):

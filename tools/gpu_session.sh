@@ -31,7 +31,7 @@ want() { [ $# -eq 0 ] && return 0; for a in "${ARGS[@]}"; do [ "$a" = "$1" ] && 
 ARGS=("$@")
 [ ${#ARGS[@]} -eq 0 ] && ARGS=(tests smoke bench ref)
 
-want tests && run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout=600
+want tests && run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
 want smoke && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 want bench && run bench_native 600 python bench.py --steps "$STEPS" --warmup "$WARM" --json-out "$OUT/bench_native.json"
 want ref && run bench_reference 900 python bench.py --impl reference --steps "$((STEPS / 2 > 3 ? STEPS / 2 : 3))" --warmup 2 --json-out "$OUT/bench_reference.json"
