@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kX3Rows = 128;   // source rows per workgroup (4 waves x 32)
 constexpr int kX3Tile = 32;    // targets per streamed tile
@@ -181,18 +182,44 @@ __device__ __forceinline__ float shr1(float v) {
   return __int_as_float(shr1(__float_as_int(v)));
 }
 
+// h_t split once into bf16 hi / lo planes [B, Nt, CP] (CP = padded channels,
+// zero tail), so the streaming loop of topk_x3_kernel moves 16-byte vectors
+// straight into LDS with no per-block conversion work.
+__global__ __launch_bounds__(256) void split_bf16_kernel(
+    const float* __restrict__ x, __bf16* __restrict__ hi,
+    __bf16* __restrict__ lo, int64_t rows, int C, int CP) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int vpr = CP / 4;
+  const int64_t r = t / vpr;
+  if (r >= rows) return;
+  const int c = (int)(t % vpr) * 4;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < C) v = *reinterpret_cast<const float4*>(x + r * C + c);
+  const float f[4] = {v.x, v.y, v.z, v.w};
+  bf16x4 vh, vl;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 h = (__bf16)f[e];
+    vh[e] = h;
+    vl[e] = (__bf16)(f[e] - (float)h);
+  }
+  *reinterpret_cast<bf16x4*>(hi + r * CP + c) = vh;
+  *reinterpret_cast<bf16x4*>(lo + r * CP + c) = vl;
+}
+
 template <int NKS>
 __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
-    const float* __restrict__ h_s, const float* __restrict__ h_t,
+    const float* __restrict__ h_s, const __bf16* __restrict__ t_hi,
+    const __bf16* __restrict__ t_lo,
     float* __restrict__ part_v, int* __restrict__ part_i,
     int64_t* __restrict__ out, int Ns, int Nt, int C, int k, int span,
     int dbg) {
   constexpr int CP = NKS * 16;              // padded channels
   constexpr int BP = CP + 8;                // LDS row pitch (bf16)
   constexpr int TILE = kX3Tile * BP;        // one hi or lo tile (bf16)
-  constexpr int F4_ROW = CP / 4;
-  constexpr int PRE = kX3Tile * F4_ROW / 256;   // float4 per thread per tile
-  static_assert(PRE >= 1 && kX3Tile * F4_ROW % 256 == 0, "tile split");
+  constexpr int V_ROW = CP / 8;             // 16-byte vectors per plane row
+  constexpr int PRE = kX3Tile * V_ROW / 256;    // vectors per thread per plane
+  static_assert(PRE >= 1 && kX3Tile * V_ROW % 256 == 0, "tile split");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS __bf16* sB = (DGMC_LDS __bf16*)smem_raw;   // [2 buf][hi, lo][TILE]
 
@@ -203,7 +230,8 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
   const int j_begin = split * span;
   const int j_end = min(Nt, j_begin + span);
   const float* hs = h_s + (size_t)b * Ns * C;
-  const float* ht = h_t + (size_t)b * Nt * C;
+  const __bf16* th = t_hi + (size_t)b * Nt * CP;
+  const __bf16* tl = t_lo + (size_t)b * Nt * CP;
 
   // A fragments (this wave's 32 source rows), split once.
   bf16x8 ahi[NKS], alo[NKS];
@@ -228,34 +256,29 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
     }
   }
 
-  auto load_tile = [&](int j0, float4* regs) {
+  auto load_tile = [&](int j0, u32x4* regs) {
 #pragma unroll
     for (int u = 0; u < PRE; ++u) {
       const int f = tid + 256 * u;
-      const int r = f / F4_ROW, c = (f % F4_ROW) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j0 + r < j_end && c < C)
-        v = *reinterpret_cast<const float4*>(ht + (size_t)(j0 + r) * C + c);
-      regs[u] = v;
+      const int r = f / V_ROW, c = (f % V_ROW) * 8;
+      u32x4 h = {0u, 0u, 0u, 0u}, l = h;
+      if (j0 + r < j_end) {
+        h = *reinterpret_cast<const u32x4*>(th + (size_t)(j0 + r) * CP + c);
+        l = *reinterpret_cast<const u32x4*>(tl + (size_t)(j0 + r) * CP + c);
+      }
+      regs[u] = h;
+      regs[PRE + u] = l;
     }
   };
-  auto store_tile = [&](int buf, const float4* regs) {
+  auto store_tile = [&](int buf, const u32x4* regs) {
     DGMC_LDS __bf16* hi_t = sB + buf * 2 * TILE;
     DGMC_LDS __bf16* lo_t = hi_t + TILE;
 #pragma unroll
     for (int u = 0; u < PRE; ++u) {
       const int f = tid + 256 * u;
-      const int r = f / F4_ROW, c = (f % F4_ROW) * 4;
-      const float x[4] = {regs[u].x, regs[u].y, regs[u].z, regs[u].w};
-      bf16x4 vh, vl;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const __bf16 hi = (__bf16)x[e];
-        vh[e] = hi;
-        vl[e] = (__bf16)(x[e] - (float)hi);
-      }
-      *reinterpret_cast<DGMC_LDS bf16x4*>(hi_t + r * BP + c) = vh;
-      *reinterpret_cast<DGMC_LDS bf16x4*>(lo_t + r * BP + c) = vl;
+      const int r = f / V_ROW, c = (f % V_ROW) * 8;
+      *reinterpret_cast<DGMC_LDS u32x4*>(hi_t + r * BP + c) = regs[u];
+      *reinterpret_cast<DGMC_LDS u32x4*>(lo_t + r * BP + c) = regs[PRE + u];
     }
   };
 
@@ -265,8 +288,14 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) { lv[r] = -INFINITY; li[r] = init_i; }
 
+  // k-th value of each row's list, kept per half-wave (lanes of half h hold
+  // their row's threshold) - no readlane per candidate test.
+  float thr[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) thr[r] = -INFINITY;
+
   const int ntiles = (j_end - j_begin + kX3Tile - 1) / kX3Tile;
-  float4 pre[PRE];
+  u32x4 pre[2 * PRE];
   if (ntiles > 0) {
     load_tile(j_begin, pre);
     store_tile(0, pre);
@@ -297,14 +326,13 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float v = col_ok ? acc[r] : -INFINITY;
-      const float thr = hb ? lane_f(lv[r], 32 + k - 1) : lane_f(lv[r], k - 1);
-      unsigned long long mask = __ballot(v > thr);
+      unsigned long long mask = __ballot(v > thr[r]);
       while (mask) {
         const int src = __builtin_ctzll(mask);
         mask &= mask - 1;
         const int sh = src & 32;
         const float cv = lane_f(v, src);
-        if (!(cv > lane_f(lv[r], sh + k - 1))) continue;
+        if (!(cv > lane_f(thr[r], src))) continue;
         const bool mine = hb == sh && hl < k;
         const int pos = __popcll(__ballot(mine && lv[r] >= cv));
         // shift the tail of the half's list down one lane (DPP wave_shr:1;
@@ -313,6 +341,9 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
         const int pi = shr1(li[r]);
         if (mine && hl > pos) { lv[r] = pv; li[r] = pi; }
         if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + (src & 31); }
+        const float t_lo_half = lane_f(lv[r], k - 1);
+        const float t_hi_half = lane_f(lv[r], 32 + k - 1);
+        thr[r] = hb ? t_hi_half : t_lo_half;
       }
     }
     __syncthreads();
@@ -404,13 +435,27 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
     pv = at::empty({(int64_t)B * Ns * S * k}, h_s.options());
     pi = at::empty({(int64_t)B * Ns * S * k}, h_s.options().dtype(at::kInt));
   }
+  // bf16 hi / lo planes of h_t (read by every row block: split once).
+  at::Tensor planes = at::empty({2, (int64_t)B * Nt, CP},
+                                h_s.options().dtype(at::kBFloat16));
+  {
+    const int64_t rows = (int64_t)B * Nt;
+    const int64_t n = rows * (CP / 4);
+    __bf16* hi = reinterpret_cast<__bf16*>(planes.data_ptr());
+    hipLaunchKernelGGL(split_bf16_kernel, dim3((unsigned)((n + 255) / 256)),
+                       dim3(256), 0, stream(), h_t.data_ptr<float>(), hi,
+                       hi + rows * CP, rows, C, CP);
+    DGMC_CHECK_LAUNCH();
+  }
+  const __bf16* t_hi = reinterpret_cast<const __bf16*>(planes.data_ptr());
+  const __bf16* t_lo = t_hi + (int64_t)B * Nt * CP;
   dim3 grid(row_blocks, S, B);
   auto launch = [&](auto kernel) {
     DGMC_CHECK_HIP(hipFuncSetAttribute(
         reinterpret_cast<const void*>(kernel),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(kernel, grid, dim3(256), lds, stream(),
-                       h_s.data_ptr<float>(), h_t.data_ptr<float>(),
+                       h_s.data_ptr<float>(), t_hi, t_lo,
                        S > 1 ? pv.data_ptr<float>() : nullptr,
                        S > 1 ? pi.data_ptr<int>() : nullptr,
                        out.data_ptr<int64_t>(), Ns, Nt, C, (int)k, span,
