@@ -27,6 +27,11 @@ class DenseLayout(object):
         self.num_nodes = info.num_nodes
         # Static (padded) batches route padding rows to a trash slot B*N.
         self.trash = bool(getattr(info, 'has_trash', False))
+        # No padding at all (e.g. batch=None, the full-graph KG path: B = 1):
+        # the packed and dense layouts coincide, so both directions are
+        # views - no fill / index_copy / index_select kernels (and none in
+        # their backward).
+        self.identity = not self.trash and self.B * self.N == self.num_nodes
         self._mask = None
 
     @property
@@ -42,6 +47,8 @@ class DenseLayout(object):
     def to_dense(self, x, fill_value=0.):
         """``[sum N, *]`` -> ``[B, N_max, *]`` (padding = ``fill_value``)."""
         feat = tuple(x.shape[1:])
+        if self.identity:
+            return x.reshape((self.B, self.N) + feat)
         rows = self.B * self.N
         out = x.new_full((rows + int(self.trash), ) + feat, fill_value)
         out = out.index_copy(0, self.index, x)
@@ -53,6 +60,8 @@ class DenseLayout(object):
         """``[B, N_max, *]`` -> ``[sum N, *]``."""
         feat = tuple(x.shape[2:])
         flat = x.reshape((self.B * self.N, ) + feat)
+        if self.identity:
+            return flat
         if self.trash:
             flat = torch.cat([flat, flat.new_zeros((1, ) + feat)], dim=0)
         return flat.index_select(0, self.index)
@@ -99,4 +108,7 @@ def dense_layout(batch, num_nodes, device, max_nodes=None):
 def to_dense_batch(x, batch=None, fill_value=0.):
     r"""Drop-in for PyG's ``to_dense_batch``: returns ``(dense, mask)``."""
     layout = dense_layout(batch, x.size(0), x.device)
-    return layout.to_dense(x, fill_value), layout.mask
+    out = layout.to_dense(x, fill_value)
+    if getattr(layout, 'identity', False):
+        out = out.clone()    # PyG returns a new tensor, never a view of x
+    return out, layout.mask

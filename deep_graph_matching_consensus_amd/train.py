@@ -456,15 +456,19 @@ class KGTrainer(object):
         key = (self.model.num_steps, self.model.detach, self.model.k)
         g = self._graphs.get(key)
         if g is None:
-            # Grads must exist (zero) as static tensors before capture.
             g = self._graphs[key] = GraphedStep(self._body_static, warmup=2)
         g()
 
     def _body_static(self):
         d, model = self.data, self.model
+        # AccumulateGrad *steals* each freshly computed gradient (no zero
+        # fill + add kernel per parameter); inside the captured graph the
+        # stolen tensors keep their addresses, which the captured Adam
+        # step reads.  Parameters without a gradient this phase (psi_1 under
+        # detach=True) are skipped by Adam, as after torch's default
+        # zero_grad(set_to_none=True) in the reference driver's loop.
         for p in model.parameters():
-            if p.grad is not None:
-                p.grad.zero_()
+            p.grad = None
         with self._autocast():
             _, S_L = model(d.x1, d.edge_index1, None, None, d.x2,
                            d.edge_index2, None, None, d.train_y)
