@@ -67,12 +67,25 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], v[u][k], acc[k]);
     }
-    for (; p < p1; ++p) {
-      float v[VEC];
-      const float w = val[p];
-      load_vec<TIn, VEC>(x + (size_t)col[p] * C + c0, v);
+    if (p < p1) {
+      // Remainder (< UNROLL entries) as ONE predicated batch: its gathers
+      // are in flight together instead of one latency round each.
+      float v[UNROLL][VEC];
+      float w[UNROLL];
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, v[k], acc[k]);
+      for (int u = 0; u < UNROLL; ++u) {
+        w[u] = 0.f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[u][k] = 0.f;
+        if (p + u < p1) {
+          w[u] = val[p + u];
+          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, v[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], v[u][k], acc[k]);
     }
     if (self_x != nullptr) {
       float v[VEC];
@@ -352,12 +365,23 @@ __global__ __launch_bounds__(256) void spmm_piece_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
     }
-    for (; p < end; ++p) {
-      const float w = val[perm != nullptr ? perm[p] : p];
-      float xv[VEC];
-      load_vec<TIn, VEC>(x + (size_t)col[p] * C + c0, xv);
+    if (p < end) {   // remainder: one predicated batch of gathers
+      float xv[4][VEC];
+      float w[4];
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[k], acc[k]);
+      for (int u = 0; u < 4; ++u) {
+        w[u] = 0.f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xv[u][k] = 0.f;
+        if (p + u < end) {
+          w[u] = val[perm != nullptr ? perm[p + u] : p + u];
+          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
     }
     if (single)
       spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu,
