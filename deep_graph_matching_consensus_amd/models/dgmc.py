@@ -33,6 +33,7 @@ from ..graph.dense import dense_layout
 from ..nn.inits import reset
 from ..ops import _backend
 from ..ops import dense as dense_ops
+from ..ops.gemm import mixed_matmul
 from ..ops import sparse_corr
 from ..ops.sparse import PASSTHROUGH
 from ..ops.plans import _IdentityCache
@@ -474,11 +475,33 @@ class DGMC(torch.nn.Module):
 
             S_hat = sparse_corr.gather_dot(hs, ht, S_idx, cand)  # [B,N_s,k]
             S_0 = lay_s.to_sparse(S_hat.softmax(dim=-1))
+            # psi_2's final Linear folded into the MLP's first layer, as in
+            # the dense path: [P; Q] = feat (W1 W_f)^T on psi_2's joint
+            # features (b_f cancels in P_i - Q_idx) - one node GEMM per step
+            # instead of three (final Linear, P, Q), forward and backward.
+            fold_w = None
+            if steps > 0 and cand is not None and pair is not None and \
+                    self._fusable(self.psi_2) and self._foldable() and \
+                    lay_s.identity and lay_t.identity:
+                fold_w = _FoldProduct.apply(self.mlp[0].weight,
+                                            self.psi_2.final.weight,
+                                            self.psi_2.final.bias)[0]
             for step in range(steps):
                 S = S_hat.softmax(dim=-1)
                 r_s = r_all[step]
                 r_t = sparse_corr.sparse_transport(
                     S, lay_s.to_dense(r_s), S_idx, N_t, cand)
+                if fold_w is not None:
+                    _, _, feat = refine(r_s, lay_t.to_sparse(r_t),
+                                        features=True)
+                    # (split-K weight gradient, accumulated over the loop's
+                    # steps into one long-K product: runtime/loopgrad.py)
+                    PQ = mixed_matmul(feat.to(f32), fold_w.t(), fold_w.t(),
+                                      loop_key=('sparse_fold',
+                                                id(self.mlp[0].weight)))
+                    S_hat = sparse_corr.consensus_update_pq(
+                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand)
+                    continue
                 o_s, o_t, _ = refine(r_s, lay_t.to_sparse(r_t))
                 S_hat = sparse_corr.consensus_update(
                     S_hat, lay_s.to_dense(o_s.to(f32)),

@@ -197,6 +197,19 @@ class _SparseConsensus(torch.autograd.Function):
         return g, dP, dQ, db1, dw2, db2, None
 
 
+def consensus_update_pq(S_hat, P, Q, mlp, cand):
+    """``S_hat + relu(P_i + b1 - Q_idx) . w2 + b2`` from node-level
+    projections ``P [B * N_s, R]``, ``Q [B * N_t, R]`` (the folded form
+    ``P = o_s W1^T`` with psi_2's final Linear inside, models/dgmc.py)."""
+    B, N_s, k = S_hat.shape
+    lin1, lin2 = mlp[0], mlp[2]
+    out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
+                                 P.float().contiguous(),
+                                 Q.float().contiguous(), lin1.bias,
+                                 lin2.weight, lin2.bias, cand)
+    return out.view(B, N_s, k)
+
+
 def consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand=None):
     """``S_hat + MLP(o_s[:, :, None] - o_t[S_idx])`` on dense ``o_s
     [B, N_s, R]`` / ``o_t [B, N_t, R]``."""

@@ -372,6 +372,48 @@ def test_dgmc_folded_projection_matches_unfolded(monkeypatch):
     assert float(g1[names.index('psi_2.final.bias')].abs().max()) == 0.0
 
 
+def test_dgmc_sparse_folded_projection_matches_unfolded(monkeypatch):
+    """Sparse (top-k) path: psi_2's final Linear folded into the consensus
+    MLP (one node GEMM on psi_2's joint features) == the unfolded form,
+    outputs and parameter gradients (the final bias' gradient is 0)."""
+    from deep_graph_matching_consensus_amd.models import DGMC, RelCNN
+    from deep_graph_matching_consensus_amd.models import dgmc as dgmc_mod
+    torch.manual_seed(0)
+    N, E = 400, 2000
+    x1 = torch.randn(N, 24, device=DEV)
+    x2 = x1[torch.randperm(N, device=DEV)] + 0.1 * torch.randn(N, 24,
+                                                             device=DEV)
+    e1 = torch.randint(N, (2, E), device=DEV)
+    e2 = torch.randint(N, (2, E), device=DEV)
+    model = DGMC(RelCNN(24, 32, 2), RelCNN(8, 8, 2), num_steps=3,
+                 k=5).to(DEV)
+    y = torch.stack([torch.arange(60, device=DEV),
+                     torch.randint(N, (60, ), device=DEV)])
+
+    def run(fold):
+        monkeypatch.setattr(dgmc_mod, 'FOLD_PROJECTION', fold)
+        torch.manual_seed(7)
+        _, S_L = model(x1, e1, None, None, x2, e2, None, None, y)
+        loss = model.loss(S_L, y)
+        grads = torch.autograd.grad(loss, list(model.parameters()),
+                                    allow_unused=True)
+        return S_L, grads
+
+    S1, g1 = run(True)
+    S0, g0 = run(False)
+    assert torch.equal(S1.__idx__, S0.__idx__)
+    assert torch.allclose(S1.__val__, S0.__val__, atol=1e-5)
+    names = [n for n, _ in model.named_parameters()]
+    for n, a, b in zip(names, g1, g0):
+        if n == 'psi_2.final.bias':
+            assert a is None or float(a.abs().max()) == 0.0
+            continue
+        if a is None or b is None:      # unused modules (e.g. BN, off)
+            assert a is None and b is None, n
+            continue
+        assert torch.allclose(a, b, atol=1e-4, rtol=1e-3), n
+
+
 def test_dgmc_sparse_gpu_matches_dense():
     from deep_graph_matching_consensus_amd.models import DGMC, GIN
     torch.manual_seed(0)
