@@ -29,6 +29,8 @@ import torch.nn.functional as F
 
 from . import _backend
 from . import reference as ref
+from .gemm import _col_sum, loop_col_sum, loop_col_total
+from ..runtime import loopgrad
 from .sparse import SparseOperator, piece_plan
 
 
@@ -171,11 +173,18 @@ def sparse_transport(S, r_s, S_idx, N_t, cand=None):
 
 # ---------------------------------------------------------------------------
 class _SparseConsensus(torch.autograd.Function):
+    """Inside a loop scope the MLP's b1 / w2 / b2 gradients of the
+    consensus steps are deposited as per-use partials and folded once by
+    the last use (runtime/loopgrad.py): no per-step reductions and no
+    AccumulateGrad adds."""
+
     @staticmethod
-    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand):
+    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand, loop=None):
         ctx.cand = cand
         ctx.save_for_backward(P, Q, b1, w2)
         ctx.meta = (b1.dtype, w2.dtype, b2.dtype, b2.shape)
+        ctx.loop = loop
+        ctx.idx = loop.register() if loop is not None else None
         return _backend.ops().sparse_consensus_fwd(
             cand.rowptr, cand.col, S_hat, P, Q, b1.float().contiguous(),
             w2.float().contiguous().view(-1),
@@ -191,10 +200,24 @@ class _SparseConsensus(torch.autograd.Function):
             P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1),
             *cand.col_pieces)
         b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
-        db1 = dP.sum(0).to(b1_dt)
-        dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
-        db2 = g.sum().view(b2_shape).to(b2_dt)
-        return g, dP, dQ, db1, dw2, db2, None
+        loop = ctx.loop
+        if loop is None:
+            db1 = dP.sum(0).to(b1_dt)
+            dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
+            db2 = g.sum().view(b2_shape).to(b2_dt)
+            return g, dP, dQ, db1, dw2, db2, None, None
+        idx = ctx.idx
+        loop_col_sum(loop, 'b1', idx, dP)
+        loop.keep('w2', idx, dw2_part)
+        g4 = g.view(-1, 4) if g.numel() % 4 == 0 else g.view(-1, 1)
+        loop_col_sum(loop, 'b2', idx, g4)
+        db1 = dw2 = db2 = None
+        if loop.arrive():
+            db1 = loop_col_total(loop, 'b1').to(b1_dt)
+            dw2 = _col_sum(loop.kept('w2')).view_as(w2).to(w2_dt)
+            db2 = loop_col_total(loop, 'b2').sum().view(b2_shape).to(b2_dt)
+            loop.release()
+        return g, dP, dQ, db1, dw2, db2, None, None
 
 
 def consensus_update_pq(S_hat, P, Q, mlp, cand):
@@ -206,8 +229,15 @@ def consensus_update_pq(S_hat, P, Q, mlp, cand):
     out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
                                  P.float().contiguous(),
                                  Q.float().contiguous(), lin1.bias,
-                                 lin2.weight, lin2.bias, cand)
+                                 lin2.weight, lin2.bias, cand,
+                                 _consensus_loop(lin1))
     return out.view(B, N_s, k)
+
+
+def _consensus_loop(lin1):
+    """Loop collector of the consensus MLP's vector gradients (taken here:
+    grad mode is off inside ``Function.forward``)."""
+    return loopgrad.group(('sparse_consensus', id(lin1.bias)))
 
 
 def consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand=None):
@@ -221,7 +251,8 @@ def consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand=None):
         Q = F.linear(o_t.reshape(-1, R).float(), lin1.weight.float())
         out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
                                      P.contiguous(), Q.contiguous(),
-                                     lin1.bias, lin2.weight, lin2.bias, cand)
+                                     lin1.bias, lin2.weight, lin2.bias, cand,
+                                     _consensus_loop(lin1))
         return out.view(B, N_s, k)
     idx = S_idx.reshape(B, N_s * k, 1).expand(-1, -1, R)
     o_t_g = torch.gather(o_t, 1, idx).view(B, N_s, k, R)
