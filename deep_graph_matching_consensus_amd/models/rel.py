@@ -15,7 +15,7 @@ from torch.nn import BatchNorm1d, Linear, ModuleList
 
 from ..ops.gemm import compute_dtype
 from ..ops.plans import relational_plan
-from ..ops.sparse import gemm_spmm
+from ..ops.sparse import PASSTHROUGH, gemm_spmm
 from ..runtime.cache import cached
 from .encoder import StackedEncoder
 
@@ -41,7 +41,7 @@ class RelConv(torch.nn.Module):
             [self.lin1.weight, self.lin2.weight, self.root.weight],
             dim=0).t())
 
-    def forward(self, x, edge_index, act=None):
+    def forward(self, x, edge_index, act=None, passthrough=False):
         plan = relational_plan(edge_index, x.size(0))
         dtype = compute_dtype(x)
         w = self.stacked_weight()
@@ -51,7 +51,8 @@ class RelConv(torch.nn.Module):
         # root.bias enters through the root slot (coefficient 1) = output bias.
         return gemm_spmm(plan, x, w, w_lp, self.out_channels,
                          bias=self.root.bias, relu=(act == 'relu'),
-                         loop_key=(id(self), x.size(0), plan.num_cols))
+                         loop_key=(id(self), x.size(0), plan.num_cols),
+                         passthrough=passthrough)
 
     def __repr__(self):
         return '{}({}, {})'.format(type(self).__name__, self.in_channels,
@@ -82,10 +83,22 @@ class RelCNN(StackedEncoder):
     def forward(self, x, edge_index, *args):
         xs = [x]
         for conv, bn in zip(self.convs, self.batch_norms):
+            kw = {}
+            if (self.cat and PASSTHROUGH and xs[-1].requires_grad and
+                    torch.is_grad_enabled()):
+                # xs[-1] also feeds the concatenation: that consumer reads
+                # the conv's alias, so both gradients meet in the conv
+                # backward (added in its dx GEMM epilogue).
+                kw = {'passthrough': True}
             if self.batch_norm:
-                h = bn(F.relu(conv(xs[-1], edge_index)))
+                h = conv(xs[-1], edge_index, **kw)
+                if kw:
+                    h, xs[-1] = h
+                h = bn(F.relu(h))
             else:
-                h = conv(xs[-1], edge_index, act='relu')
+                h = conv(xs[-1], edge_index, act='relu', **kw)
+                if kw:
+                    h, xs[-1] = h
             xs.append(F.dropout(h, p=self.dropout, training=self.training))
         return self._project(self._head(xs))
 

@@ -463,9 +463,16 @@ class _GemmSpMM(torch.autograd.Function):
         else:
             dy = _spmm_raw(opt, g, None, None, None, False, w_lp.dtype)
         dY = dy.view(xc.size(0), -1)
-        # 3. dx (unfused path) and dW.
+        # 3. dx (unfused path) and dW.  A passthrough consumer's gradient
+        #    enters the GEMM epilogue (beta = 1): no separate add kernel.
         if ctx.needs_input_grad[0] and gx is None:
-            gx = (dY @ w_lp.t()).to(ctx.x_dtype)
+            if gpass is not None and gpass.dtype == dY.dtype == \
+                    ctx.x_dtype and gpass.shape == (dY.size(0),
+                                                    w_lp.size(0)):
+                gx = torch.addmm(gpass, dY, w_lp.t())
+                gpass = None
+            else:
+                gx = (dY @ w_lp.t()).to(ctx.x_dtype)
         if loop is None:
             if ctx.needs_input_grad[1]:
                 gw = matmul_tn_fp32(xc.contiguous(), dY).to(ctx.w_dtype)
