@@ -24,3 +24,26 @@ def test_native_equals_reference_mode_cpu():
         b0, bL = model(*args)
     assert torch.allclose(a0, b0, atol=1e-5)
     assert torch.allclose(aL, bL, atol=1e-5)
+
+
+def test_identity_dense_layout_is_a_view():
+    """No padding (batch=None / equal graph sizes): packed <-> dense are
+    views (no copy kernels), the public to_dense_batch still returns a
+    fresh tensor, and padded batches keep the index_copy path."""
+    from deep_graph_matching_consensus_amd.graph.dense import (
+        dense_layout, to_dense_batch)
+    x = torch.randn(7, 3)
+    lay = dense_layout(None, 7, x.device)
+    assert lay.identity and lay.B == 1 and lay.N == 7
+    d = lay.to_dense(x)
+    assert d.shape == (1, 7, 3) and d.data_ptr() == x.data_ptr()
+    assert lay.to_sparse(d).data_ptr() == x.data_ptr()
+    out, mask = to_dense_batch(x)
+    assert torch.equal(out[0], x) and out.data_ptr() != x.data_ptr()
+    assert mask.all()
+    batch = torch.tensor([0, 0, 0, 1, 1, 1, 1])
+    lay2 = dense_layout(batch, 7, x.device)
+    assert not lay2.identity
+    d2 = lay2.to_dense(x)
+    assert d2.shape == (2, 4, 3) and float(d2[0, 3].abs().sum()) == 0.0
+    assert torch.equal(lay2.to_sparse(d2), x)
