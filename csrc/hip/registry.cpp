@@ -57,14 +57,21 @@ at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
                                 const at::Tensor& S_hat, const at::Tensor& P,
                                 const at::Tensor& Q, const at::Tensor& b1,
                                 const at::Tensor& w2, const at::Tensor& b2);
-std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
+std::tuple<at::Tensor, at::Tensor> sparse_consensus_fwd_prob(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& S_hat,
+    const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
+    const at::Tensor& w2, const at::Tensor& b2, int64_t k);
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>
+sparse_consensus_bwd(
     const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& colptr,
     const at::Tensor& row_of, const at::Tensor& perm, const at::Tensor& G,
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
     const at::Tensor& w2, const c10::optional<at::Tensor>& pptr,
     const c10::optional<at::Tensor>& prow,
     const c10::optional<at::Tensor>& pbeg,
-    const c10::optional<at::Tensor>& pend);
+    const c10::optional<at::Tensor>& pend,
+    const c10::optional<at::Tensor>& prob,
+    const c10::optional<at::Tensor>& gS);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
     const at::Tensor& rowptr, int64_t nnz, int64_t T);
 void spmm_pieces_out(const at::Tensor& rowptr, const at::Tensor& col,
@@ -363,7 +370,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "sparse_consensus_bwd(Tensor rowptr, Tensor col, Tensor colptr, Tensor "
       "row_of, Tensor perm, Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
       "w2, Tensor? pptr=None, Tensor? prow=None, Tensor? pbeg=None, Tensor? "
-      "pend=None) -> (Tensor, Tensor, Tensor)");
+      "pend=None, Tensor? prob=None, Tensor? gS=None) -> (Tensor, Tensor, "
+      "Tensor, Tensor)");
+  m.def(
+      "sparse_consensus_fwd_prob(Tensor rowptr, Tensor col, Tensor S_hat, "
+      "Tensor P, Tensor Q, Tensor b1, Tensor w2, Tensor b2, int k) -> (Tensor, "
+      "Tensor)");
   m.def(
       "piece_plan(Tensor rowptr, int nnz, int T) -> (Tensor, Tensor, Tensor, "
       "Tensor)");
@@ -428,6 +440,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("gemm_abt", &dgmc::gemm_abt);
   m.impl("sparse_consensus_fwd", &dgmc::sparse_consensus_fwd);
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
+  m.impl("sparse_consensus_fwd_prob", &dgmc::sparse_consensus_fwd_prob);
   m.impl("spmm_pieces_out", &dgmc::spmm_pieces_out);
   m.impl("piece_plan", &dgmc::piece_plan);
 }

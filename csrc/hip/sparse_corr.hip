@@ -232,14 +232,18 @@ __device__ __forceinline__ float relu_dot4(float4 pv, float4 q, float4 w) {
                         fmaxf(pv.w - q.w, 0.f) * w.w)));
 }
 
-template <int G>
+// SOFT: also the row softmax of the updated scores, prob = softmax(out)
+// over the row's candidates (the next step's S, reference dgmc.py:205,225),
+// from registers: a row of k <= 8 * (64 / G) candidates is one wave.
+template <int G, bool SOFT>
 __global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ S_hat, const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2,
-    float* __restrict__ out, int rows, int R) {
+    float* __restrict__ out, float* __restrict__ prob, int rows, int R) {
   constexpr int NG = kWave / G;
+  constexpr int MAXIT = SOFT ? 4 : 1 << 20;   // 2 * NG candidates each
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int r = xcd_remap(blockIdx.x, gridDim.x) * kSpWaves + wave;
   if (r >= rows) return;
@@ -253,17 +257,58 @@ __global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
   }
   const float bias = b2[0];
   const int p0 = rowptr[r], p1 = rowptr[r + 1];
-  for (int pb = p0; pb < p1; pb += 2 * NG) {
-    float s[2];
+  float vals[SOFT ? 2 * 4 : 1];
+#pragma unroll
+  for (int it = 0; it < (SOFT ? MAXIT : 1); ++it) {
+    // (non-SOFT: a plain runtime loop over the row below)
+    if (!SOFT) break;
+    const int pb = p0 + it * 2 * NG;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int p = pb + u * NG + g;
-      s[u] = 0.f;
-      if (p < p1 && cok) s[u] = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
+      float sv = 0.f;
+      if (p < p1 && cok) sv = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
+      const float t = group_sum<G>(sv);
+      const float o = p < p1 ? S_hat[p] + t + bias : -INFINITY;
+      if constexpr (SOFT) vals[2 * it + u] = o;
+      if ((lane % G) == 0 && p < p1) out[p] = o;
+    }
+  }
+  if constexpr (SOFT) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, vals[j]);
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+    float e[8], sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      e[j] = vals[j] == -INFINITY ? 0.f : __expf(vals[j] - m);
+      sum += e[j];
+    }
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) sum += __shfl_xor(sum, off);
+    const float inv = 1.f / sum;
+    if ((lane % G) == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = p0 + (j >> 1) * 2 * NG + (j & 1) * NG + g;
+        if (p < p1) prob[p] = e[j] * inv;
+      }
+    }
+    return;
+  }
+  for (int pb = p0; pb < p1; pb += 2 * NG) {
+    float s2[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = pb + u * NG + g;
+      s2[u] = 0.f;
+      if (p < p1 && cok) s2[u] = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const float t = group_sum<G>(s[u]);
+      const float t = group_sum<G>(s2[u]);
       const int p = pb + u * NG + g;
       if ((lane % G) == 0 && p < p1) out[p] = S_hat[p] + t + bias;
     }
@@ -271,10 +316,17 @@ __global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
 }
 
 // dP[r] = w2 * sum_p g_p [z_p > 0];  dw2 partial per block (fixed order).
-template <int G>
+// SOFT: the row also fed a softmax (prob, forward SOFT variant) whose
+// gradient gS arrives here: the total score gradient is
+// Gr + prob * (gS - <prob, gS>) (softmax backward + the pass-through add,
+// one value per lane for k <= 64); it is written to Gtot (read by the
+// column kernel and returned as the S_hat gradient).
+template <int G, bool SOFT>
 __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
-    const float* __restrict__ Gr, const float* __restrict__ P,
+    const float* __restrict__ Gr, const float* __restrict__ prob,
+    const float* __restrict__ gS, float* __restrict__ Gtot,
+    const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, float* __restrict__ dP,
     float* __restrict__ dw2_part, int rows, int R) {
@@ -295,9 +347,23 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
       pv[2] = p.z + bb.z; pv[3] = p.w + bb.w;
     }
     const int p0 = rowptr[r], p1 = rowptr[r + 1];
-    for (int p = p0 + g; p < p1; p += NG) {
-      if (!cok) continue;
-      const float gv = Gr[p];
+    float gt = 0.f;     // SOFT: total gradient of candidate p0 + lane
+    if constexpr (SOFT) {
+      const int p = p0 + lane;
+      float sp = 0.f, gs = 0.f, gg = 0.f;
+      if (p < p1) { sp = prob[p]; gs = gS[p]; gg = Gr[p]; }
+      float dot = sp * gs;
+#pragma unroll
+      for (int off = 1; off < kWave; off <<= 1) dot += __shfl_xor(dot, off);
+      gt = gg + sp * (gs - dot);
+      if (p < p1) Gtot[p] = gt;
+    }
+    for (int j = 0; j * NG < p1 - p0; ++j) {   // wave-uniform trip count
+      const int p = p0 + g + NG * j;
+      float gv;
+      if constexpr (SOFT) gv = __shfl(gt, (g + NG * j) & (kWave - 1));
+      if (p >= p1 || !cok) continue;
+      if constexpr (!SOFT) gv = Gr[p];
       const float4 q4 = ld4(Q + (size_t)col[p] * R + c);
       const float q[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
@@ -459,10 +525,14 @@ at::Tensor sddmm(const at::Tensor& rowptr, const at::Tensor& col,
   return val;
 }
 
-at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
-                                const at::Tensor& S_hat, const at::Tensor& P,
-                                const at::Tensor& Q, const at::Tensor& b1,
-                                const at::Tensor& w2, const at::Tensor& b2) {
+// Max candidates per row of the fused-softmax variants (forward: 4
+// iterations x 2 batches x 64 / G; backward: one candidate per lane).
+static int64_t soft_max_k(int G) { return std::min<int64_t>(64, 8 * (kWave / G)); }
+
+std::tuple<at::Tensor, at::Tensor> sparse_consensus_fwd_impl(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& S_hat,
+    const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
+    const at::Tensor& w2, const at::Tensor& b2, int64_t k_soft) {
   check_f32_2d(P, "P");
   check_f32_2d(Q, "Q");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(P.device());
@@ -474,18 +544,36 @@ at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
   TORCH_CHECK(S_hat.numel() == col.numel() && S_hat.is_contiguous(),
               "sparse_consensus_fwd: S_hat");
   at::Tensor out = at::empty_like(S_hat);
-  if (rows == 0) return out;
+  at::Tensor prob;
+  if (rows == 0) return {out, k_soft > 0 ? at::empty_like(S_hat) : prob};
   const int G = group_lanes(R, {P.data_ptr(), Q.data_ptr(), b1.data_ptr(),
                                 w2.data_ptr()});
-  if (G > 0) {
+  if (k_soft > 0) {
+    // uniform rows of k_soft candidates (the top-k candidate CSR)
+    TORCH_CHECK(G > 0 && k_soft <= soft_max_k(G) &&
+                    col.numel() == rows * k_soft,
+                "sparse_consensus_fwd_prob: needs C % 4 == 0, C <= 256 and "
+                "uniform rows of <= ", G > 0 ? soft_max_k(G) : 0,
+                " candidates");
+    prob = at::empty_like(S_hat);
     DGMC_GROUP_DISPATCH(G, hipLaunchKernelGGL(
-        sparse_consensus_fwd_g_kernel<GG>, dim3(sp_blocks(rows)), dim3(256),
-        0, stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+        (sparse_consensus_fwd_g_kernel<GG, true>), dim3(sp_blocks(rows)),
+        dim3(256), 0, stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
         S_hat.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
         b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
-        out.data_ptr<float>(), (int)rows, R));
+        out.data_ptr<float>(), prob.data_ptr<float>(), (int)rows, R));
     DGMC_CHECK_LAUNCH();
-    return out;
+    return {out, prob};
+  }
+  if (G > 0) {
+    DGMC_GROUP_DISPATCH(G, hipLaunchKernelGGL(
+        (sparse_consensus_fwd_g_kernel<GG, false>), dim3(sp_blocks(rows)),
+        dim3(256), 0, stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+        S_hat.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        b1.data_ptr<float>(), w2.data_ptr<float>(), b2.data_ptr<float>(),
+        out.data_ptr<float>(), (float*)nullptr, (int)rows, R));
+    DGMC_CHECK_LAUNCH();
+    return {out, prob};
   }
   hipLaunchKernelGGL(sparse_consensus_fwd_kernel, dim3(sp_blocks(rows)),
                      dim3(256), 0, stream(), rowptr.data_ptr<int>(),
@@ -495,17 +583,37 @@ at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
                      b2.data_ptr<float>(), out.data_ptr<float>(), (int)rows,
                      R);
   DGMC_CHECK_LAUNCH();
-  return out;
+  return {out, prob};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
+at::Tensor sparse_consensus_fwd(const at::Tensor& rowptr, const at::Tensor& col,
+                                const at::Tensor& S_hat, const at::Tensor& P,
+                                const at::Tensor& Q, const at::Tensor& b1,
+                                const at::Tensor& w2, const at::Tensor& b2) {
+  return std::get<0>(
+      sparse_consensus_fwd_impl(rowptr, col, S_hat, P, Q, b1, w2, b2, 0));
+}
+
+// The update and the row softmax of its result (uniform rows of k).
+std::tuple<at::Tensor, at::Tensor> sparse_consensus_fwd_prob(
+    const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& S_hat,
+    const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
+    const at::Tensor& w2, const at::Tensor& b2, int64_t k) {
+  TORCH_CHECK(k >= 1, "sparse_consensus_fwd_prob: k >= 1");
+  return sparse_consensus_fwd_impl(rowptr, col, S_hat, P, Q, b1, w2, b2, k);
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>
+sparse_consensus_bwd(
     const at::Tensor& rowptr, const at::Tensor& col, const at::Tensor& colptr,
     const at::Tensor& row_of, const at::Tensor& perm, const at::Tensor& G,
     const at::Tensor& P, const at::Tensor& Q, const at::Tensor& b1,
     const at::Tensor& w2, const c10::optional<at::Tensor>& pptr,
     const c10::optional<at::Tensor>& prow,
     const c10::optional<at::Tensor>& pbeg,
-    const c10::optional<at::Tensor>& pend) {
+    const c10::optional<at::Tensor>& pend,
+    const c10::optional<at::Tensor>& prob,
+    const c10::optional<at::Tensor>& gS) {
   check_f32_2d(P, "P");
   check_f32_2d(Q, "Q");
   const bool pieces = pptr.has_value() && pptr->defined() &&
@@ -527,11 +635,32 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
   at::Tensor dw2 = at::empty({nb, R}, P.options());
   const int Gl = group_lanes(R, {P.data_ptr(), Q.data_ptr(), b1.data_ptr(),
                                  w2.data_ptr()});
-  if (rows > 0 && Gl > 0) {
+  const bool soft = prob.has_value() && prob->defined() && gS.has_value() &&
+                    gS->defined();
+  at::Tensor Gt = G;   // total score gradient (read by the column walk)
+  if (soft) {
+    TORCH_CHECK(Gl > 0 && rows > 0 && col.numel() % rows == 0 &&
+                    col.numel() / rows <= 64 &&
+                    prob->numel() == col.numel() &&
+                    gS->numel() == col.numel() && prob->is_contiguous() &&
+                    gS->is_contiguous(),
+                "sparse_consensus_bwd: softmax-fused backward needs uniform "
+                "rows of <= 64 candidates");
+    Gt = at::empty_like(G);
     DGMC_GROUP_DISPATCH(Gl, hipLaunchKernelGGL(
-        sparse_consensus_bwd_rows_g_kernel<GG>, dim3(nb), dim3(256), 0,
+        (sparse_consensus_bwd_rows_g_kernel<GG, true>), dim3(nb), dim3(256), 0,
         stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
-        G.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        G.data_ptr<float>(), prob->data_ptr<float>(), gS->data_ptr<float>(),
+        Gt.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        b1.data_ptr<float>(), w2.data_ptr<float>(), dP.data_ptr<float>(),
+        dw2.data_ptr<float>(), (int)rows, R));
+    DGMC_CHECK_LAUNCH();
+  } else if (rows > 0 && Gl > 0) {
+    DGMC_GROUP_DISPATCH(Gl, hipLaunchKernelGGL(
+        (sparse_consensus_bwd_rows_g_kernel<GG, false>), dim3(nb), dim3(256),
+        0, stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+        G.data_ptr<float>(), (const float*)nullptr, (const float*)nullptr,
+        (float*)nullptr, P.data_ptr<float>(), Q.data_ptr<float>(),
         b1.data_ptr<float>(), w2.data_ptr<float>(), dP.data_ptr<float>(),
         dw2.data_ptr<float>(), (int)rows, R));
     DGMC_CHECK_LAUNCH();
@@ -563,7 +692,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
         dim3((npieces + 256 / GG - 1) / (256 / GG)), dim3(256), 0, stream(),
         row_of.data_ptr<int>(), perm.data_ptr<int>(), prow->data_ptr<int>(),
         pbeg->data_ptr<int>(), pend->data_ptr<int>(), npieces,
-        G.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
+        Gt.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
         b1.data_ptr<float>(), w2.data_ptr<float>(), dQ.data_ptr<float>(),
         part.data_ptr<float>(), (int)cols, R));
     DGMC_CHECK_LAUNCH();
@@ -574,13 +703,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sparse_consensus_bwd(
     hipLaunchKernelGGL(sparse_consensus_bwd_cols_kernel, dim3(sp_blocks(cols)),
                        dim3(256), 0, stream(), colptr.data_ptr<int>(),
                        row_of.data_ptr<int>(), perm64.data_ptr<int64_t>(),
-                       G.data_ptr<float>(), P.data_ptr<float>(),
+                       Gt.data_ptr<float>(), P.data_ptr<float>(),
                        Q.data_ptr<float>(), b1.data_ptr<float>(),
                        w2.data_ptr<float>(), dQ.data_ptr<float>(), (int)cols,
                        R);
     DGMC_CHECK_LAUNCH();
   }
-  return {dP, dQ, dw2};
+  return {dP, dQ, dw2, Gt};
 }
 
 }  // namespace dgmc

@@ -474,7 +474,8 @@ class DGMC(torch.nn.Module):
                 if device.type == 'cuda' and not is_reference_mode() else None
 
             S_hat = sparse_corr.gather_dot(hs, ht, S_idx, cand)  # [B,N_s,k]
-            S_0 = lay_s.to_sparse(S_hat.softmax(dim=-1))
+            S = S_hat.softmax(dim=-1)      # S_0 and step 0's S (one softmax)
+            S_0 = lay_s.to_sparse(S)
             # psi_2's final Linear folded into the MLP's first layer, as in
             # the dense path: [P; Q] = feat (W1 W_f)^T on psi_2's joint
             # features (b_f cancels in P_i - Q_idx) - one node GEMM per step
@@ -486,8 +487,14 @@ class DGMC(torch.nn.Module):
                 fold_w = _FoldProduct.apply(self.mlp[0].weight,
                                             self.psi_2.final.weight,
                                             self.psi_2.final.bias)[0]
+            # The consensus kernel also emits softmax(S_hat') - the next
+            # step's S and finally S_L (dgmc.py:205,225) - and runs its
+            # backward: no separate softmax kernels nor gradient add.
+            fused_soft = fold_w is not None and sparse_corr.soft_fusable(
+                k, self.mlp[0].weight.size(0))
             for step in range(steps):
-                S = S_hat.softmax(dim=-1)
+                if step > 0 and not fused_soft:
+                    S = S_hat.softmax(dim=-1)
                 r_s = r_all[step]
                 r_t = sparse_corr.sparse_transport(
                     S, lay_s.to_dense(r_s), S_idx, N_t, cand)
@@ -499,14 +506,20 @@ class DGMC(torch.nn.Module):
                     PQ = mixed_matmul(feat.to(f32), fold_w.t(), fold_w.t(),
                                       loop_key=('sparse_fold',
                                                 id(self.mlp[0].weight)))
-                    S_hat = sparse_corr.consensus_update_pq(
-                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand)
+                    res = sparse_corr.consensus_update_pq(
+                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand,
+                        with_prob=fused_soft)
+                    if fused_soft:
+                        S_hat, S = res
+                    else:
+                        S_hat = res
                     continue
                 o_s, o_t, _ = refine(r_s, lay_t.to_sparse(r_t))
                 S_hat = sparse_corr.consensus_update(
                     S_hat, lay_s.to_dense(o_s.to(f32)),
                     lay_t.to_dense(o_t.to(f32)), S_idx, self.mlp, cand)
-            S_L = lay_s.to_sparse(S_hat.softmax(dim=-1))
+            S_L = lay_s.to_sparse(S if (fused_soft or steps == 0) else
+                                  S_hat.softmax(dim=-1))
             S_idx = lay_s.to_sparse(S_idx)
 
         row = torch.arange(x_s.size(0), device=device).view(-1, 1)

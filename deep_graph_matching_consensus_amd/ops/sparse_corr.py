@@ -176,36 +176,58 @@ class _SparseConsensus(torch.autograd.Function):
     """Inside a loop scope the MLP's b1 / w2 / b2 gradients of the
     consensus steps are deposited as per-use partials and folded once by
     the last use (runtime/loopgrad.py): no per-step reductions and no
-    AccumulateGrad adds."""
+    AccumulateGrad adds.  ``soft_k > 0`` (uniform rows of ``soft_k``
+    candidates) also returns the row softmax of the update - the next
+    step's ``S`` - from the same kernel; its backward (softmax backward +
+    the pass-through add) runs inside the consensus backward kernel."""
 
     @staticmethod
-    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand, loop=None):
+    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand, loop=None, soft_k=0):
         ctx.cand = cand
-        ctx.save_for_backward(P, Q, b1, w2)
         ctx.meta = (b1.dtype, w2.dtype, b2.dtype, b2.shape)
         ctx.loop = loop
         ctx.idx = loop.register() if loop is not None else None
+        ctx.soft = bool(soft_k)
+        ctx.set_materialize_grads(False)
+        b1f = b1.float().contiguous()
+        w2f = w2.float().contiguous().view(-1)
+        b2f = b2.float().contiguous().view(-1)
+        if soft_k:
+            out, prob = _backend.ops().sparse_consensus_fwd_prob(
+                cand.rowptr, cand.col, S_hat, P, Q, b1f, w2f, b2f,
+                int(soft_k))
+            ctx.save_for_backward(P, Q, b1, w2, prob)
+            return out, prob
+        ctx.save_for_backward(P, Q, b1, w2)
         return _backend.ops().sparse_consensus_fwd(
-            cand.rowptr, cand.col, S_hat, P, Q, b1.float().contiguous(),
-            w2.float().contiguous().view(-1),
-            b2.float().contiguous().view(-1))
+            cand.rowptr, cand.col, S_hat, P, Q, b1f, w2f, b2f)
 
     @staticmethod
-    def backward(ctx, g):
-        P, Q, b1, w2 = ctx.saved_tensors
+    def backward(ctx, g, gS=None):
+        if ctx.soft:
+            P, Q, b1, w2, prob = ctx.saved_tensors
+        else:
+            P, Q, b1, w2 = ctx.saved_tensors
+            prob = None
         cand = ctx.cand
+        if g is None:
+            g = torch.zeros(cand.col.numel(), dtype=torch.float32,
+                            device=P.device)
         g = g.contiguous().float()
-        dP, dQ, dw2_part = _backend.ops().sparse_consensus_bwd(
+        soft = prob is not None and gS is not None
+        dP, dQ, dw2_part, g = _backend.ops().sparse_consensus_bwd(
             cand.rowptr, cand.col, cand.colptr, cand.row_of, cand.perm32, g,
             P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1),
-            *cand.col_pieces)
+            *cand.col_pieces, prob if soft else None,
+            gS.contiguous().float() if soft else None)
         b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
+        nones = (None, None, None)
         loop = ctx.loop
         if loop is None:
             db1 = dP.sum(0).to(b1_dt)
             dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
             db2 = g.sum().view(b2_shape).to(b2_dt)
-            return g, dP, dQ, db1, dw2, db2, None, None
+            return (g, dP, dQ, db1, dw2, db2) + nones
         idx = ctx.idx
         loop_col_sum(loop, 'b1', idx, dP)
         loop.keep('w2', idx, dw2_part)
@@ -217,21 +239,36 @@ class _SparseConsensus(torch.autograd.Function):
             dw2 = _col_sum(loop.kept('w2')).view_as(w2).to(w2_dt)
             db2 = loop_col_total(loop, 'b2').sum().view(b2_shape).to(b2_dt)
             loop.release()
-        return g, dP, dQ, db1, dw2, db2, None, None
+        return (g, dP, dQ, db1, dw2, db2) + nones
 
 
-def consensus_update_pq(S_hat, P, Q, mlp, cand):
+def soft_fusable(k, R):
+    """Can the consensus kernel also emit the row softmax (rows of ``k``
+    candidates, ``R`` channels)?  (sparse_corr.hip::soft_max_k)"""
+    if R % 4 or R > 256 or R == 0:
+        return False
+    G = 1
+    while G * 4 < R:
+        G *= 2
+    return 1 <= k <= min(64, 8 * (64 // G))
+
+
+def consensus_update_pq(S_hat, P, Q, mlp, cand, with_prob=False):
     """``S_hat + relu(P_i + b1 - Q_idx) . w2 + b2`` from node-level
     projections ``P [B * N_s, R]``, ``Q [B * N_t, R]`` (the folded form
-    ``P = o_s W1^T`` with psi_2's final Linear inside, models/dgmc.py)."""
+    ``P = o_s W1^T`` with psi_2's final Linear inside, models/dgmc.py).
+    ``with_prob``: returns ``(S_hat', softmax(S_hat'))`` from one kernel."""
     B, N_s, k = S_hat.shape
     lin1, lin2 = mlp[0], mlp[2]
-    out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
+    res = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
                                  P.float().contiguous(),
                                  Q.float().contiguous(), lin1.bias,
                                  lin2.weight, lin2.bias, cand,
-                                 _consensus_loop(lin1))
-    return out.view(B, N_s, k)
+                                 _consensus_loop(lin1),
+                                 k if with_prob else 0)
+    if with_prob:
+        return res[0].view(B, N_s, k), res[1].view(B, N_s, k)
+    return res.view(B, N_s, k)
 
 
 def _consensus_loop(lin1):
