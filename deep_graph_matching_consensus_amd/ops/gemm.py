@@ -115,6 +115,8 @@ class _MixedMatmul(torch.autograd.Function):
             out = xc @ w_lp
         ctx.save_for_backward(xc, w_lp)
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
+        ctx.w_transposed = w.dim() == 2 and w.size(0) > 1 and \
+            w.size(1) > 1 and w.stride(0) == 1 and w.stride(1) == w.size(0)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.loop = loop
@@ -134,7 +136,12 @@ class _MixedMatmul(torch.autograd.Function):
         need_b = ctx.has_bias and ctx.needs_input_grad[3]
         loop = ctx.loop
         if loop is None:
-            if need_w:
+            if need_w and ctx.w_transposed:
+                # w = weight.t(): produce the gradient in the parameter's own
+                # layout ([out, in] contiguous) and hand back its transpose,
+                # so AccumulateGrad keeps it without a layout copy.
+                gw = matmul_tn_fp32(g, xc.contiguous()).to(ctx.w_dtype).t()
+            elif need_w:
                 gw = matmul_tn_fp32(xc.contiguous(), g).to(ctx.w_dtype)
             if need_b:
                 gb = _col_sum(g).to(ctx.bias_dtype)

@@ -1,7 +1,13 @@
-import sys, torch
-sys.path.insert(0, '/root/repo')
+"""psi_1's large weight gradients (``[1024 x 6656]``, ``[256 x 6656]`` over
+K = 11k rows): the MFMA TN kernel (``dense_wgrad``, split over row chunks)
+vs the library path (``matmul_tn_fp32``: hipBLASLt, split-K when small)."""
+import os.path as osp
+import sys
+
+import torch
+
+sys.path.insert(0, osp.dirname(osp.dirname(osp.abspath(__file__))))
 from deep_graph_matching_consensus_amd.ops import dense as D
-from deep_graph_matching_consensus_amd.ops import _backend
 from deep_graph_matching_consensus_amd.ops.gemm import matmul_tn_fp32
 def t(f, n=10):
     for _ in range(3): f()
