@@ -243,7 +243,6 @@ __global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
     const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ out, float* __restrict__ prob, int rows, int R) {
   constexpr int NG = kWave / G;
-  constexpr int MAXIT = SOFT ? 4 : 1 << 20;   // 2 * NG candidates each
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int r = xcd_remap(blockIdx.x, gridDim.x) * kSpWaves + wave;
   if (r >= rows) return;
@@ -257,24 +256,25 @@ __global__ __launch_bounds__(256) void sparse_consensus_fwd_g_kernel(
   }
   const float bias = b2[0];
   const int p0 = rowptr[r], p1 = rowptr[r + 1];
-  float vals[SOFT ? 2 * 4 : 1];
-#pragma unroll
-  for (int it = 0; it < (SOFT ? MAXIT : 1); ++it) {
-    // (non-SOFT: a plain runtime loop over the row below)
-    if (!SOFT) break;
-    const int pb = p0 + it * 2 * NG;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int p = pb + u * NG + g;
-      float sv = 0.f;
-      if (p < p1 && cok) sv = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
-      const float t = group_sum<G>(sv);
-      const float o = p < p1 ? S_hat[p] + t + bias : -INFINITY;
-      if constexpr (SOFT) vals[2 * it + u] = o;
-      if ((lane % G) == 0 && p < p1) out[p] = o;
-    }
-  }
   if constexpr (SOFT) {
+    // the row's <= 8 * NG candidates in four unrolled batch pairs; every
+    // lane of a group keeps its group's values for the softmax
+    float vals[8];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int pb = p0 + it * 2 * NG;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = pb + u * NG + g;
+        float sv = 0.f;
+        if (p < p1 && cok)
+          sv = relu_dot4(pv, ld4(Q + (size_t)col[p] * R + c), wv);
+        const float t = group_sum<G>(sv);
+        const float o = p < p1 ? S_hat[p] + t + bias : -INFINITY;
+        vals[2 * it + u] = o;
+        if ((lane % G) == 0 && p < p1) out[p] = o;
+      }
+    }
     float m = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) m = fmaxf(m, vals[j]);
