@@ -911,21 +911,54 @@ struct StepGeom {
   static constexpr int RG = kThreads / CQ;         // row groups (channel loops)
 };
 
-// One operand block staged by stage_blocks: rows [0, rows) of a packed bf16
-// [*, R] block into an fp32 LDS tile of pitch `pitch`, optionally copied
-// verbatim to `copy` (same row layout).
+// Node-level storage type of the step kernels: bf16 (autocast) or fp32
+// (reference precision).  16-byte vectors: 8 bf16 / 4 fp32 channels.
+template <typename T> struct StepIO;
+template <> struct StepIO<__bf16> {
+  typedef ps_bf16x8 vec;
+  static constexpr int VN = 8;
+  __device__ __forceinline__ static void to_lds(DGMC_LDS float* d,
+                                                const vec& v) {
+    reinterpret_cast<DGMC_LDS ps_f32x4*>(d)[0] =
+        ps_f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+    reinterpret_cast<DGMC_LDS ps_f32x4*>(d)[1] =
+        ps_f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+  }
+  __device__ __forceinline__ static void store4(__bf16* p, ps_f32x4 a) {
+    *reinterpret_cast<ps_bf16x4*>(p) =
+        ps_bf16x4{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3]};
+  }
+};
+template <> struct StepIO<float> {
+  typedef ps_f32x4 vec;
+  static constexpr int VN = 4;
+  __device__ __forceinline__ static void to_lds(DGMC_LDS float* d,
+                                                const vec& v) {
+    *reinterpret_cast<DGMC_LDS ps_f32x4*>(d) = v;
+  }
+  __device__ __forceinline__ static void store4(float* p, ps_f32x4 a) {
+    *reinterpret_cast<ps_f32x4*>(p) = a;
+  }
+};
+
+// One operand block staged by stage_blocks: rows [0, rows) of a packed
+// [*, R] block (storage T) into an fp32 LDS tile of pitch `pitch`,
+// optionally copied verbatim to `copy` (same row layout).
+template <typename T>
 struct StageBlk {
-  const __bf16* src;
+  const T* src;
   DGMC_LDS float* dst;
-  __bf16* copy;
+  T* copy;
   int rows, pitch;
 };
 
 // All loads of up to NB blocks are issued before the first LDS store (one
 // memory round trip for pair-sized blocks).
-template <int R, int NB>
-__device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
-  constexpr int V8 = R / 8;
+template <int R, int NB, typename T>
+__device__ __forceinline__ void stage_blocks(const StageBlk<T> (&blk)[NB]) {
+  using IO = StepIO<T>;
+  constexpr int VN = IO::VN;
+  constexpr int V8 = R / VN;
   int end[NB];
   int total = 0;
 #pragma unroll
@@ -934,7 +967,7 @@ __device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
     end[k] = total;
   }
   for (int base = threadIdx.x; base < total; base += 4 * kThreads) {
-    ps_bf16x8 v[4];
+    typename IO::vec v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = base + u * kThreads;
@@ -943,10 +976,11 @@ __device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
 #pragma unroll
         for (int m = 0; m + 1 < NB; ++m)
           if (q >= end[m]) { k = m + 1; q0 = end[m]; }
-        const __bf16* src = blk[0].src;
+        const T* src = blk[0].src;
 #pragma unroll
         for (int m = 1; m < NB; ++m) if (k == m) src = blk[m].src;
-        v[u] = *reinterpret_cast<const ps_bf16x8*>(src + (size_t)(q - q0) * 8);
+        v[u] = *reinterpret_cast<const typename IO::vec*>(
+            src + (size_t)(q - q0) * VN);
       }
     }
 #pragma unroll
@@ -957,18 +991,14 @@ __device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
 #pragma unroll
         for (int m = 0; m + 1 < NB; ++m)
           if (q >= end[m]) { k = m + 1; q0 = end[m]; }
-        StageBlk bk = blk[0];
+        StageBlk<T> bk = blk[0];
 #pragma unroll
         for (int m = 1; m < NB; ++m) if (k == m) bk = blk[m];
-        const int qq = q - q0, r = qq / V8, c = (qq - r * V8) * 8;
-        DGMC_LDS ps_f32x4* d =
-            reinterpret_cast<DGMC_LDS ps_f32x4*>(bk.dst + r * bk.pitch + c);
-        d[0] = ps_f32x4{(float)v[u][0], (float)v[u][1], (float)v[u][2],
-                        (float)v[u][3]};
-        d[1] = ps_f32x4{(float)v[u][4], (float)v[u][5], (float)v[u][6],
-                        (float)v[u][7]};
+        const int qq = q - q0, r = qq / V8, c = (qq - r * V8) * VN;
+        IO::to_lds(bk.dst + r * bk.pitch + c, v[u]);
         if (bk.copy)
-          *reinterpret_cast<ps_bf16x8*>(bk.copy + (size_t)qq * 8) = v[u];
+          *reinterpret_cast<typename IO::vec*>(bk.copy + (size_t)qq * VN) =
+              v[u];
       }
     }
   }
@@ -976,22 +1006,22 @@ __device__ __forceinline__ void stage_blocks(const StageBlk (&blk)[NB]) {
 
 // Static-batch padding rows spread over the whole grid in 16-byte pieces:
 // rows [z0, z1) of zdst zeroed and rows [c0, c1) of csrc copied to cdst.
-template <int R>
-__device__ __forceinline__ void pad_rows(__bf16* zdst, int z0, int z1,
-                                         __bf16* cdst, const __bf16* csrc,
-                                         int c0, int c1) {
-  constexpr int V8 = R / 8;
+template <int R, typename T>
+__device__ __forceinline__ void pad_rows(T* zdst, int z0, int z1, T* cdst,
+                                         const T* csrc, int c0, int c1) {
+  using V = typename StepIO<T>::vec;
+  constexpr int VN = StepIO<T>::VN;
+  constexpr int V8 = R / VN;
   const int nz = (z1 - z0) * V8, nc = cdst ? (c1 - c0) * V8 : 0;
   const int stride = gridDim.x * blockDim.x;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nz + nc;
        e += stride) {
     if (e < nz) {
-      *reinterpret_cast<ps_bf16x8*>(zdst + (size_t)z0 * R + (size_t)e * 8) =
-          ps_bf16x8{};
+      *reinterpret_cast<V*>(zdst + (size_t)z0 * R + (size_t)e * VN) = V{};
     } else {
-      const size_t off = (size_t)c0 * R + (size_t)(e - nz) * 8;
-      *reinterpret_cast<ps_bf16x8*>(cdst + off) =
-          *reinterpret_cast<const ps_bf16x8*>(csrc + off);
+      const size_t off = (size_t)c0 * R + (size_t)(e - nz) * VN;
+      *reinterpret_cast<V*>(cdst + off) =
+          *reinterpret_cast<const V*>(csrc + off);
     }
   }
 }
@@ -1008,15 +1038,15 @@ __device__ __forceinline__ ps_f32x4 lds4(const DGMC_LDS float* p) {
 // Outputs: S_new (CONS: the updated S_hat), S_prob (TRANS), rt_out packed
 // [rows_t, R] (TRANS) and, when rs_copy is given, r_s copied into it (the
 // joint psi_2 input [r_s; r_t]).
-template <int R, bool CONS, bool TRANS>
+template <int R, bool CONS, bool TRANS, typename T>
 __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
-    const float* __restrict__ S_hat, const __bf16* __restrict__ P,
-    const __bf16* __restrict__ Q, const float* __restrict__ b1,
+    const float* __restrict__ S_hat, const T* __restrict__ P,
+    const T* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, const float* __restrict__ b2,
-    const __bf16* __restrict__ r_s, const int* __restrict__ ptr_s,
+    const T* __restrict__ r_s, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, float* __restrict__ S_new,
-    float* __restrict__ S_prob, __bf16* __restrict__ rs_copy,
-    __bf16* __restrict__ rt_out, int Ns, int Nt, int rows_s, int rows_t) {
+    float* __restrict__ S_prob, T* __restrict__ rs_copy,
+    T* __restrict__ rt_out, int Ns, int Nt, int rows_s, int rows_t) {
   using G = StepGeom<R>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
@@ -1044,18 +1074,18 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
     }
     bias2 = b2[0];
   }
-  __bf16* rsc = rs_copy ? rs_copy + (size_t)s0 * R : nullptr;
+  T* rsc = rs_copy ? rs_copy + (size_t)s0 * R : nullptr;
   if constexpr (CONS && TRANS) {
-    const StageBlk blk[3] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
+    const StageBlk<T> blk[3] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
                              {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP},
                              {r_s + (size_t)s0 * R, sR, rsc, ns, R}};
     stage_blocks<R, 3>(blk);
   } else if constexpr (CONS) {
-    const StageBlk blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
-                             {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP}};
+    const StageBlk<T> blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
+                                {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP}};
     stage_blocks<R, 2>(blk);
   } else {
-    const StageBlk blk[1] = {{r_s + (size_t)s0 * R, sR, rsc, ns, R}};
+    const StageBlk<T> blk[1] = {{r_s + (size_t)s0 * R, sR, rsc, ns, R}};
     stage_blocks<R, 1>(blk);
   }
 #pragma unroll
@@ -1065,8 +1095,8 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
   }
   for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) sS[e] = Sh[e];
   if constexpr (TRANS)
-    pad_rows<R>(rt_out, ptr_t[gridDim.x], rows_t, rs_copy, r_s,
-                ptr_s[gridDim.x], rows_s);
+    pad_rows<R, T>(rt_out, ptr_t[gridDim.x], rows_t, rs_copy, r_s,
+                   ptr_s[gridDim.x], rows_s);
   __syncthreads();
 
   // 1. consensus update of the valid block: 4 lanes per (i, j) entry.
@@ -1118,7 +1148,7 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
   __syncthreads();
 
   // 3. r_t = S^T r_s: one channel quad per lane, two rows j per pass.
-  __bf16* rt = rt_out + (size_t)t0 * R;
+  T* rt = rt_out + (size_t)t0 * R;
   const int cq = tid % G::CQ, rg = tid / G::CQ;
   for (int j0 = rg; j0 < nt; j0 += 2 * G::RG) {
     const int j1 = j0 + G::RG;
@@ -1131,11 +1161,8 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
       a0 += w0 * rv;
       a1 += w1 * rv;
     }
-    *reinterpret_cast<ps_bf16x4*>(rt + (size_t)j0 * R + 4 * cq) =
-        ps_bf16x4{(__bf16)a0[0], (__bf16)a0[1], (__bf16)a0[2], (__bf16)a0[3]};
-    if (has1)
-      *reinterpret_cast<ps_bf16x4*>(rt + (size_t)j1 * R + 4 * cq) = ps_bf16x4{
-          (__bf16)a1[0], (__bf16)a1[1], (__bf16)a1[2], (__bf16)a1[3]};
+    StepIO<T>::store4(rt + (size_t)j0 * R + 4 * cq, a0);
+    if (has1) StepIO<T>::store4(rt + (size_t)j1 * R + 4 * cq, a1);
   }
 }
 
@@ -1145,15 +1172,15 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
 // and per-pair dw2 / db2 partials.
 // LDS: sR, sGt [N][PP] (TRANS; reused as sRed [RG][R]), sP, sQ [N][R]
 // (CONS), sD [NN], sSum [kWaves].
-template <int R, bool CONS, bool TRANS>
+template <int R, bool CONS, bool TRANS, typename T>
 __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
-    const float* __restrict__ S, const __bf16* __restrict__ r_s,
-    const __bf16* __restrict__ g_t, const float* __restrict__ addend,
-    const __bf16* __restrict__ P, const __bf16* __restrict__ Q,
+    const float* __restrict__ S, const T* __restrict__ r_s,
+    const T* __restrict__ g_t, const float* __restrict__ addend,
+    const T* __restrict__ P, const T* __restrict__ Q,
     const float* __restrict__ b1, const float* __restrict__ w2,
     const int* __restrict__ ptr_s, const int* __restrict__ ptr_t,
-    float* __restrict__ G_out, __bf16* __restrict__ dP,
-    __bf16* __restrict__ dQ, float* __restrict__ dw2_part,
+    float* __restrict__ G_out, T* __restrict__ dP,
+    T* __restrict__ dQ, float* __restrict__ dw2_part,
     float* __restrict__ db2_part, float* __restrict__ part, int accumulate,
     int Ns, int Nt, int rows_s, int rows_t) {
   using G = StepGeom<R>;
@@ -1195,24 +1222,24 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
     wv = *reinterpret_cast<const ps_f32x4*>(w2 + 4 * cq);
   }
   if constexpr (CONS && TRANS) {
-    const StageBlk blk[4] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
+    const StageBlk<T> blk[4] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
                              {g_t + (size_t)t0 * R, sGt, nullptr, nt, G::PP},
                              {P + (size_t)s0 * R, sP, nullptr, ns, R},
                              {Q + (size_t)t0 * R, sQ, nullptr, nt, R}};
     stage_blocks<R, 4>(blk);
   } else if constexpr (TRANS) {
-    const StageBlk blk[2] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
+    const StageBlk<T> blk[2] = {{r_s + (size_t)s0 * R, sR, nullptr, ns, G::PP},
                              {g_t + (size_t)t0 * R, sGt, nullptr, nt, G::PP}};
     stage_blocks<R, 2>(blk);
   } else {
-    const StageBlk blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, R},
+    const StageBlk<T> blk[2] = {{P + (size_t)s0 * R, sP, nullptr, ns, R},
                              {Q + (size_t)t0 * R, sQ, nullptr, nt, R}};
     stage_blocks<R, 2>(blk);
   }
   float gsum = 0.f;
   if constexpr (CONS) {
-    pad_rows<R>(dP, ptr_s[gridDim.x], rows_s, nullptr, nullptr, 0, 0);
-    pad_rows<R>(dQ, ptr_t[gridDim.x], rows_t, nullptr, nullptr, 0, 0);
+    pad_rows<R, T>(dP, ptr_s[gridDim.x], rows_s, nullptr, nullptr, 0, 0);
+    pad_rows<R, T>(dQ, ptr_t[gridDim.x], rows_t, nullptr, nullptr, 0, 0);
   }
   if constexpr (!TRANS) {
     // Upstream gradient tile, masked to the valid block.
@@ -1314,9 +1341,7 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
       }
       acc *= wv;
       db1v += acc;
-      *reinterpret_cast<ps_bf16x4*>(dP + ((size_t)s0 + i) * R + 4 * cq) =
-          ps_bf16x4{(__bf16)acc[0], (__bf16)acc[1], (__bf16)acc[2],
-                    (__bf16)acc[3]};
+      StepIO<T>::store4(dP + ((size_t)s0 + i) * R + 4 * cq, acc);
     } else {
       const int j = r - ns;
       const ps_f32x4 qv = lds4(sQ + j * R + 4 * cq);
@@ -1327,9 +1352,7 @@ __global__ __launch_bounds__(kThreads) void pair_step_bwd_kernel(
         for (int k = 0; k < 4; ++k) acc[k] += pv[k] - qv[k] > 0.f ? g : 0.f;
       }
       acc *= -wv;
-      *reinterpret_cast<ps_bf16x4*>(dQ + ((size_t)t0 + j) * R + 4 * cq) =
-          ps_bf16x4{(__bf16)acc[0], (__bf16)acc[1], (__bf16)acc[2],
-                    (__bf16)acc[3]};
+      StepIO<T>::store4(dQ + ((size_t)t0 + j) * R + 4 * cq, acc);
     }
   }
   *reinterpret_cast<DGMC_LDS ps_f32x4*>(sRed + rg * R + 4 * cq) = dw;
@@ -1414,7 +1437,8 @@ static size_t pair_lds(K kern, size_t floats) {
 }
 
 // Compile-time-width step kernels (pair_step_fwd/bwd_kernel): R in
-// {32, 64, 128}, 16-byte aligned bf16 operand rows, aligned fp32 b1 / w2.
+// {32, 64, 128}, 16-byte aligned operand rows of ONE storage type (bf16 under
+// autocast, fp32 at reference precision), aligned fp32 b1 / w2.
 // DGMC_PAIR_FAST=0 selects the generic kernels (A/B switch).
 static bool fast_step_ok(int R, std::initializer_list<const at::Tensor*> rows,
                          std::initializer_list<const void*> vecs = {}) {
@@ -1423,77 +1447,94 @@ static bool fast_step_ok(int R, std::initializer_list<const at::Tensor*> rows,
     return !(e && e[0] == '0');
   }();
   if (!enabled || !(R == 32 || R == 64 || R == 128)) return false;
+  const at::ScalarType st = (*rows.begin())->scalar_type();
+  if (st != at::kBFloat16 && st != at::kFloat) return false;
   for (const at::Tensor* t : rows)
-    if (t->scalar_type() != at::kBFloat16 || !rows_vec_ok(*t)) return false;
+    if (t->scalar_type() != st || !rows_vec_ok(*t)) return false;
   for (const void* v : vecs)
     if (!aligned16(v)) return false;
   return true;
 }
 
-static __bf16* bf16_ptr(const at::Tensor& t) {
-  return reinterpret_cast<__bf16*>(t.data_ptr());
-}
+static void* vp(const at::Tensor& t) { return t.data_ptr(); }
 
 struct StepFwdArgs {
   const float* S_hat;
-  const __bf16 *P, *Q;
+  const void *P, *Q;
   const float *b1, *w2, *b2;
-  const __bf16* r_s;
+  const void* r_s;
   const int *ptr_s, *ptr_t;
   float *S_new, *S_prob;
-  __bf16 *rs_copy, *rt_out;
+  void *rs_copy, *rt_out;
   int B, Ns, Nt, rows_s, rows_t;
+  bool f32 = false;            // node-level storage fp32 (else bf16)
 };
 
 struct StepBwdArgs {
   const float* S;
-  const __bf16 *r_s, *g_t;
+  const void *r_s, *g_t;
   const float* addend;
-  const __bf16 *P, *Q;
+  const void *P, *Q;
   const float *b1, *w2;
   const int *ptr_s, *ptr_t;
   float* G_out;
-  __bf16 *dP, *dQ;
+  void *dP, *dQ;
   float *dw2_part, *db2_part;
   int B, Ns, Nt, rows_s, rows_t;
   float* part = nullptr;       // [B, 2R + 1] loop-accumulated partials
   int accumulate = 0;
+  bool f32 = false;
 };
 
-template <int R, bool C, bool T>
+template <int R, bool C, bool T, typename E>
 static void step_fwd_launch(const StepFwdArgs& a) {
-  auto kern = pair_step_fwd_kernel<R, C, T>;
+  auto kern = pair_step_fwd_kernel<R, C, T, E>;
   const size_t lds = pair_lds(kern, step_fwd_lds<R>(C, T, a.Ns, a.Nt));
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S_hat,
-                     a.P, a.Q, a.b1, a.w2, a.b2, a.r_s, a.ptr_s, a.ptr_t,
-                     a.S_new, a.S_prob, a.rs_copy, a.rt_out, a.Ns, a.Nt,
-                     a.rows_s, a.rows_t);
+                     (const E*)a.P, (const E*)a.Q, a.b1, a.w2, a.b2,
+                     (const E*)a.r_s, a.ptr_s, a.ptr_t, a.S_new, a.S_prob,
+                     (E*)a.rs_copy, (E*)a.rt_out, a.Ns, a.Nt, a.rows_s,
+                     a.rows_t);
   DGMC_CHECK_LAUNCH();
 }
 
-template <int R, bool C, bool T>
+template <int R, bool C, bool T, typename E>
 static void step_bwd_launch(const StepBwdArgs& a) {
-  auto kern = pair_step_bwd_kernel<R, C, T>;
+  auto kern = pair_step_bwd_kernel<R, C, T, E>;
   const size_t lds = pair_lds(kern, step_bwd_lds<R>(C, T, a.Ns, a.Nt));
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S,
-                     a.r_s, a.g_t, a.addend, a.P, a.Q, a.b1, a.w2, a.ptr_s,
-                     a.ptr_t, a.G_out, a.dP, a.dQ, a.dw2_part, a.db2_part,
-                     a.part, a.accumulate, a.Ns, a.Nt, a.rows_s, a.rows_t);
+                     (const E*)a.r_s, (const E*)a.g_t, a.addend,
+                     (const E*)a.P, (const E*)a.Q, a.b1, a.w2, a.ptr_s,
+                     a.ptr_t, a.G_out, (E*)a.dP, (E*)a.dQ, a.dw2_part,
+                     a.db2_part, a.part, a.accumulate, a.Ns, a.Nt, a.rows_s,
+                     a.rows_t);
   DGMC_CHECK_LAUNCH();
+}
+
+template <bool C, bool T, typename E>
+static void step_fwd_t(int R, const StepFwdArgs& a) {
+  if (R == 32) step_fwd_launch<32, C, T, E>(a);
+  else if (R == 64) step_fwd_launch<64, C, T, E>(a);
+  else step_fwd_launch<128, C, T, E>(a);
 }
 
 template <bool C, bool T>
 static void step_fwd(int R, const StepFwdArgs& a) {
-  if (R == 32) step_fwd_launch<32, C, T>(a);
-  else if (R == 64) step_fwd_launch<64, C, T>(a);
-  else step_fwd_launch<128, C, T>(a);
+  if (a.f32) step_fwd_t<C, T, float>(R, a);
+  else step_fwd_t<C, T, __bf16>(R, a);
+}
+
+template <bool C, bool T, typename E>
+static void step_bwd_t(int R, const StepBwdArgs& a) {
+  if (R == 32) step_bwd_launch<32, C, T, E>(a);
+  else if (R == 64) step_bwd_launch<64, C, T, E>(a);
+  else step_bwd_launch<128, C, T, E>(a);
 }
 
 template <bool C, bool T>
 static void step_bwd(int R, const StepBwdArgs& a) {
-  if (R == 32) step_bwd_launch<32, C, T>(a);
-  else if (R == 64) step_bwd_launch<64, C, T>(a);
-  else step_bwd_launch<128, C, T>(a);
+  if (a.f32) step_bwd_t<C, T, float>(R, a);
+  else step_bwd_t<C, T, __bf16>(R, a);
 }
 
 at::Tensor dense_masked_softmax(const at::Tensor& S_hat, const at::Tensor& n_s,
@@ -1558,10 +1599,11 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   }
   if (fast_step_ok(R, {&r_s})) {
     StepFwdArgs a{S_hat.data_ptr<float>(), nullptr, nullptr, nullptr,
-                  nullptr, nullptr, bf16_ptr(r_s), ptr_s.data_ptr<int>(),
+                  nullptr, nullptr, vp(r_s), ptr_s.data_ptr<int>(),
                   ptr_t.data_ptr<int>(), nullptr, S.data_ptr<float>(),
-                  joint_out ? bf16_ptr(joint) : nullptr, bf16_ptr(r_t), B, Ns,
+                  joint_out ? vp(joint) : nullptr, vp(r_t), B, Ns,
                   Nt, (int)rows_s, (int)rows_t};
+    a.f32 = r_s.scalar_type() == at::kFloat;
     step_fwd<false, true>(R, a);
     return {S, joint_out ? joint : r_t};
   }
@@ -1610,11 +1652,12 @@ at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
   at::Tensor out = at::empty_like(S);
   if (B == 0) return out;
   if (fast_step_ok(R, {&r_s, &g})) {
-    StepBwdArgs a{S.data_ptr<float>(), bf16_ptr(r_s), bf16_ptr(g), add,
+    StepBwdArgs a{S.data_ptr<float>(), vp(r_s), vp(g), add,
                   nullptr, nullptr, nullptr, nullptr, ptr_s.data_ptr<int>(),
                   ptr_t.data_ptr<int>(), out.data_ptr<float>(), nullptr,
                   nullptr, nullptr, nullptr, B, Ns, Nt, (int)r_s.size(0),
                   (int)g.size(0)};
+    a.f32 = r_s.scalar_type() == at::kFloat;
     step_bwd<false, true>(R, a);
     return out;
   }
@@ -1657,12 +1700,13 @@ at::Tensor dense_consensus(const at::Tensor& S_hat, const at::Tensor& P,
   if (B == 0) return out;
   if (fast_step_ok(R, {&P, &Q}, {b1.data_ptr(), w2.data_ptr()}) &&
       b1.is_contiguous() && w2.is_contiguous()) {
-    StepFwdArgs a{S_hat.data_ptr<float>(), bf16_ptr(P), bf16_ptr(Q),
+    StepFwdArgs a{S_hat.data_ptr<float>(), vp(P), vp(Q),
                   b1.data_ptr<float>(), w2.data_ptr<float>(),
                   b2.data_ptr<float>(), nullptr, ptr_s.data_ptr<int>(),
                   ptr_t.data_ptr<int>(), out.data_ptr<float>(), nullptr,
                   nullptr, nullptr, B, Ns, Nt, (int)P.size(0),
                   (int)Q.size(0)};
+    a.f32 = P.scalar_type() == at::kFloat;
     step_fwd<true, false>(R, a);
     return out;
   }
@@ -1742,13 +1786,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
   if (fast_step_ok(R, {&P, &Q, &dP, &dQ}, {b1.data_ptr(), w2.data_ptr()}) &&
       b1.is_contiguous() && w2.is_contiguous()) {
     StepBwdArgs a{G.data_ptr<float>(), nullptr, nullptr, nullptr,
-                  bf16_ptr(P), bf16_ptr(Q), b1.data_ptr<float>(),
+                  vp(P), vp(Q), b1.data_ptr<float>(),
                   w2.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                  ptr_t.data_ptr<int>(), nullptr, bf16_ptr(dP), bf16_ptr(dQ),
+                  ptr_t.data_ptr<int>(), nullptr, vp(dP), vp(dQ),
                   dw2.data_ptr<float>(), db2.data_ptr<float>(), B, Ns, Nt,
                   (int)P.size(0), (int)Q.size(0)};
     a.part = step_part(part, B, R, G);
     a.accumulate = accumulate ? 1 : 0;
+    a.f32 = P.scalar_type() == at::kFloat;
     step_bwd<true, false>(R, a);
     if (a.part) return {dP, dQ, at::Tensor(), at::Tensor()};
     return {dP, dQ, dw2, db2};
@@ -1813,21 +1858,23 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
   }
   const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   const int vec_r = rows_vec_ok(r_s) ? 1 : 0;
-  TORCH_CHECK(P.scalar_type() == at::kBFloat16 &&
-                  r_s.scalar_type() == at::kBFloat16,
-              "dense_consensus_transport: bf16 P/Q and r_s");
+  TORCH_CHECK(P.scalar_type() == r_s.scalar_type() &&
+                  (P.scalar_type() == at::kBFloat16 ||
+                   P.scalar_type() == at::kFloat),
+              "dense_consensus_transport: P/Q and r_s both bf16 or fp32");
   if (fast_step_ok(R, {&P, &Q, &r_s}, {b1.data_ptr(), w2.data_ptr()})) {
-    StepFwdArgs a{S_hat.data_ptr<float>(), bf16_ptr(P), bf16_ptr(Q),
+    StepFwdArgs a{S_hat.data_ptr<float>(), vp(P), vp(Q),
                   b1.data_ptr<float>(), w2.data_ptr<float>(),
-                  b2.data_ptr<float>(), bf16_ptr(r_s), ptr_s.data_ptr<int>(),
+                  b2.data_ptr<float>(), vp(r_s), ptr_s.data_ptr<int>(),
                   ptr_t.data_ptr<int>(), S_new.data_ptr<float>(),
-                  S_prob.data_ptr<float>(), bf16_ptr(joint),
-                  bf16_ptr(joint) + rows_s * R, B, Ns, Nt, (int)rows_s,
+                  S_prob.data_ptr<float>(), vp(joint),
+                  vp(joint.narrow(0, rows_s, rows_t)), B, Ns, Nt, (int)rows_s,
                   (int)rows_t};
+    a.f32 = P.scalar_type() == at::kFloat;
     step_fwd<true, true>(R, a);
     return {S_new, S_prob, joint};
   }
-  using T = __hip_bfloat16;
+  DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
   auto kern = consensus_transport_kernel<T, T>;
   const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +
                                         2 * (size_t)R + (size_t)Ns * R +
@@ -1843,6 +1890,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
                      S_new.data_ptr<float>(), S_prob.data_ptr<float>(),
                      reinterpret_cast<T*>(joint.data_ptr()), Ns, Nt, R,
                      (int)rows_s, (int)rows_t, vec_pq, vec_r);
+  });
   DGMC_CHECK_LAUNCH();
   return {S_new, S_prob, joint};
 }
@@ -1879,12 +1927,13 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
   const int R = P.size(1);
   TORCH_CHECK(Ns <= kMaxN && Nt <= kMaxN, "pair tile too large");
   TORCH_CHECK(r_s.size(1) == R && g_t.size(1) == R && Q.size(1) == R &&
-                  r_s.scalar_type() == at::kBFloat16 &&
-                  g_t.scalar_type() == at::kBFloat16 &&
-                  P.scalar_type() == at::kBFloat16 &&
-                  Q.scalar_type() == at::kBFloat16,
-              "dense_transport_consensus_bwd: bf16 r_s / g_t / P / Q of "
-              "width R");
+                  (r_s.scalar_type() == at::kBFloat16 ||
+                   r_s.scalar_type() == at::kFloat) &&
+                  g_t.scalar_type() == r_s.scalar_type() &&
+                  P.scalar_type() == r_s.scalar_type() &&
+                  Q.scalar_type() == r_s.scalar_type(),
+              "dense_transport_consensus_bwd: r_s / g_t / P / Q of width R, "
+              "all bf16 or all fp32");
   TORCH_CHECK(b1.numel() == R && w2.numel() == R, "b1/w2 size");
   check_ptr(ptr_s, ptr_t, B);
   at::Tensor dP, dQ;
@@ -1907,19 +1956,20 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
   const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
   if (fast_step_ok(R, {&r_s, &g_t, &P, &Q, &dP, &dQ},
                    {b1.data_ptr(), w2.data_ptr()})) {
-    StepBwdArgs a{S_prob.data_ptr<float>(), bf16_ptr(r_s), bf16_ptr(g_t), add,
-                  bf16_ptr(P), bf16_ptr(Q), b1.data_ptr<float>(),
+    StepBwdArgs a{S_prob.data_ptr<float>(), vp(r_s), vp(g_t), add,
+                  vp(P), vp(Q), b1.data_ptr<float>(),
                   w2.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                  ptr_t.data_ptr<int>(), G.data_ptr<float>(), bf16_ptr(dP),
-                  bf16_ptr(dQ), dw2.data_ptr<float>(), db2.data_ptr<float>(),
+                  ptr_t.data_ptr<int>(), G.data_ptr<float>(), vp(dP),
+                  vp(dQ), dw2.data_ptr<float>(), db2.data_ptr<float>(),
                   B, Ns, Nt, (int)P.size(0), (int)Q.size(0)};
     a.part = step_part(part, B, R, S_prob);
     a.accumulate = accumulate ? 1 : 0;
+    a.f32 = P.scalar_type() == at::kFloat;
     step_bwd<true, true>(R, a);
     if (a.part) return {G, dP, dQ, at::Tensor(), at::Tensor()};
     return {G, dP, dQ, dw2, db2};
   }
-  using T = __hip_bfloat16;
+  DGMC_DISPATCH_FLOAT(P.scalar_type(), T, [&] {
   auto kern = transport_consensus_bwd_kernel<T, T>;
   const size_t lds = pair_lds(kern, (size_t)(Ns + Nt) * (R + 1) +
                                         (size_t)(Ns + Nt) * R +
@@ -1937,6 +1987,7 @@ dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                      reinterpret_cast<T*>(dQ.data_ptr()),
                      dw2.data_ptr<float>(), db2.data_ptr<float>(), Ns, Nt, R,
                      (int)P.size(0), (int)Q.size(0), vec_r, vec_pq);
+  });
   DGMC_CHECK_LAUNCH();
   if (step_part(part, B, R, S_prob)) {
     fold_part_generic(*part, accumulate, dP, dw2, db2, R);

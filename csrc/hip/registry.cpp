@@ -224,6 +224,23 @@ at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                               at::Tensor g_out,
                               const c10::optional<at::Tensor>& bias_part);
 
+std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
+                                          const at::Tensor& col, int64_t Nsrc,
+                                          int64_t S, int64_t P_cap);
+at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
+                     const at::Tensor& seg, const at::Tensor& weight,
+                     const c10::optional<at::Tensor>& root, bool trans_w);
+at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
+                            const at::Tensor& val, const at::Tensor& cinv,
+                            const at::Tensor& g,
+                            const c10::optional<at::Tensor>& seg);
+at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
+                           int64_t N, int64_t S,
+                           const c10::optional<at::Tensor>& add);
+at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
+                          const at::Tensor& src, const at::Tensor& seg,
+                          int64_t chunk);
+
 }  // namespace dgmc
 
 TORCH_LIBRARY(dgmc_amd, m) {
@@ -384,6 +401,21 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor pptr, Tensor prow, Tensor pbeg, Tensor pend, Tensor x, Tensor? "
       "self_x, Tensor? self_scale, Tensor? bias, bool relu, Tensor(a!) out) -> "
       "()");
+  m.def(
+      "slot_compact_plan(Tensor rowptr, Tensor col, int Nsrc, int S, int "
+      "P_cap) -> Tensor[]");
+  m.def(
+      "slot_gemm(Tensor X, Tensor src, Tensor seg, Tensor weight, Tensor? "
+      "root, bool trans_w) -> Tensor");
+  m.def(
+      "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
+      "Tensor g, Tensor? seg=None) -> Tensor");
+  m.def(
+      "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add) "
+      "-> Tensor");
+  m.def(
+      "slot_wgrad_f32(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
+      "chunk) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
@@ -443,4 +475,9 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("sparse_consensus_fwd_prob", &dgmc::sparse_consensus_fwd_prob);
   m.impl("spmm_pieces_out", &dgmc::spmm_pieces_out);
   m.impl("piece_plan", &dgmc::piece_plan);
+  m.impl("slot_compact_plan", &dgmc::slot_compact_plan);
+  m.impl("slot_gemm", &dgmc::slot_gemm);
+  m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
+  m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
+  m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);
 }

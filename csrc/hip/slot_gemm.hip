@@ -1,0 +1,774 @@
+// fp32 SplineConv on the (node, slot) pairs the edges actually use.
+//
+// Reference: /root/reference/dgmc/models/spline.py:21,49 (PyG SplineConv over
+// torch_spline_conv's weighting kernels: one thread per (edge, channel),
+// atomicAdd weight gradients).  Here the conv is
+//
+//   out = act( A (X W) + bias ),  A [N, N*S] with columns j*S + k (source
+//                                  node j, B-spline slot k; root = slot S-1)
+//
+// and only the columns that carry an entry are ever formed: on PascalVOC
+// batches 42 % of the N*S (node, slot) pairs (10.8 of 26 per node), so the
+// GEMM work is 2.4x smaller than the dense X [W_0 | ... | W_25] projection.
+//
+//   compact plan  mark the used columns, rank them per slot (ballot scans),
+//                 lay the slots out as BM-row segments of the "compact" row
+//                 space p: src[p] = j, the column -> p map and A's columns
+//                 re-indexed to p (4 launches, no host sync);
+//   slot_gemm     Y[p] = X[src[p]] W_{slot(p)}  - a segmented gathered GEMM on
+//                 v_mfma_f32_32x32x2_f32 (exact fp32: a k-ordered fmaf chain),
+//                 128x128 tiles, every tile inside one slot segment;
+//   (SpMM)        out = A_c Y + bias, ReLU (spmm.hip, A_c = re-indexed A);
+//   backward      dY_c = A_c^T g' (rowmap SpMM over the assembled A^T),
+//                 dX = sum_k (dY_c W_k^T)[p(j,k)] (slot_gemm with W^T, then a
+//                 per-node gather-sum), dW_k = sum_p X[src p]^T dY_c[p]
+//                 (gathered TN MFMA over slot segments, fixed-order fold -
+//                 deterministic, no atomics).
+//
+// LDS layouts are chosen so every MFMA operand read (one fp32 per lane) is
+// bank-conflict free: k-contiguous tiles use a pitch of BK + 1 (33 dwords:
+// lanes of consecutive rows step 33 banks), m/n-contiguous tiles a pitch of
+// BN + 32 (the two lane halves read rows k and k + 1 on disjoint banks).
+#include "common.h"
+
+namespace dgmc {
+
+namespace {
+
+typedef float sg_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kSgBM = 128;               // compact rows per tile / segment unit
+constexpr int kSgBN = 128;
+constexpr int kSgBK = 32;
+constexpr int kSgThreads = 256;          // 4 waves, 2 x 2 wave grid of 64x64
+constexpr int kSgKP = kSgBK + 1;         // pitch of k-contiguous LDS tiles
+constexpr int kSgNP = kSgBN + 32;        // pitch of m/n-contiguous LDS tiles
+constexpr int kSgMaxS = 64;
+constexpr int kSgMaxU = 16;              // uses per wgrad launch
+
+__device__ __forceinline__ float4 ld4(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+
+// Slot of compact row m (segments [seg[s], seg[s+1]) are BM-aligned).
+__device__ __forceinline__ int seg_slot(const int* __restrict__ seg, int S,
+                                        int m) {
+  int s = 0;
+  while (s < S - 1 && seg[s + 1] <= m) ++s;
+  return s;
+}
+
+__device__ __forceinline__ const float* slot_weight(const float* weight,
+                                                    const float* root,
+                                                    int nw, int s,
+                                                    size_t stride) {
+  return s < nw ? weight + (size_t)s * stride : root;
+}
+
+int num_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    hipDeviceProp_t prop;
+    DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
+    cached[dev] = prop.multiProcessorCount;
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Compact plan
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sg_mark_kernel(
+    const int* __restrict__ rowptr, int R, const int* __restrict__ col,
+    int cap, int* __restrict__ mark) {
+  const int nnz = rowptr[R];
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < min(cap, nnz);
+       e += gridDim.x * 256)
+    mark[col[e]] = 1;          // same value from every writer
+}
+
+// One block per slot: rank[j*S+k] = rank of j among the used sources of slot
+// k (-1 if unused); cnt[k] = used count.  Ballot prefix sums (0/1 values).
+__global__ __launch_bounds__(1024) void sg_scan_kernel(
+    const int* __restrict__ mark, int Nsrc, int S, int* __restrict__ rank,
+    int* __restrict__ cnt) {
+  __shared__ int wtot[16];
+  __shared__ int base_sh;
+  const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
+            wave = tid >> 6;
+  if (tid == 0) base_sh = 0;
+  __syncthreads();
+  for (int j0 = 0; j0 < Nsrc; j0 += 1024) {
+    const int j = j0 + tid;
+    const int v = j < Nsrc ? (mark[(size_t)j * S + k] != 0) : 0;
+    const unsigned long long m = __ballot(v);
+    const int below = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wtot[wave] = __popcll(m);
+    __syncthreads();
+    int off = base_sh;
+    for (int w = 0; w < wave; ++w) off += wtot[w];
+    if (j < Nsrc) rank[(size_t)j * S + k] = v ? off + below : -1;
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; ++w) t += wtot[w];
+      base_sh += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) cnt[k] = base_sh;
+}
+
+// posmap / src / cinv over the column space, col_c over the entries, seg.
+__global__ __launch_bounds__(256) void sg_fill_kernel(
+    const int* __restrict__ rank, const int* __restrict__ cnt, int Nsrc,
+    int S, const int* __restrict__ rowptr, int R, const int* __restrict__ col,
+    int cap, int* __restrict__ posmap, int* __restrict__ src,
+    int* __restrict__ cinv, int* __restrict__ col_c, int* __restrict__ seg) {
+  __shared__ int sseg[kSgMaxS + 1];
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int k = 0; k < S; ++k) {
+      sseg[k] = run;
+      run += (cnt[k] + kSgBM - 1) / kSgBM * kSgBM;
+    }
+    sseg[S] = run;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k <= S; k += 256) seg[k] = sseg[k];
+  const int ncols = Nsrc * S;
+  const int nnz = min(cap, rowptr[R]);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < ncols) {
+    const int r = rank[i];
+    const int j = i / S, k = i - j * S;
+    if (r >= 0) {
+      const int p = sseg[k] + r;
+      posmap[i] = p;
+      src[p] = j;
+      cinv[p] = i;
+    } else {
+      posmap[i] = -1;
+    }
+  }
+  if (i < cap) {
+    if (i < nnz) {
+      const int c = col[i];
+      const int k = c % S;
+      col_c[i] = sseg[k] + rank[c];
+    } else {
+      col_c[i] = 0;            // inert tail entry (val 0 in static operators)
+    }
+  }
+}
+
+std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
+                                          const at::Tensor& col, int64_t Nsrc,
+                                          int64_t S, int64_t P_cap) {
+  TORCH_CHECK(rowptr.is_cuda() && rowptr.scalar_type() == at::kInt &&
+                  col.scalar_type() == at::kInt,
+              "slot_compact_plan: int32 CSR expected");
+  TORCH_CHECK(S >= 1 && S <= kSgMaxS, "slot_compact_plan: 1 <= S <= 64");
+  TORCH_CHECK(P_cap % kSgBM == 0, "slot_compact_plan: P_cap % 128");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(rowptr.device());
+  const int R = (int)rowptr.numel() - 1;
+  const int cap = (int)col.numel();
+  const int64_t ncols = Nsrc * S;
+  auto i32 = rowptr.options();
+  at::Tensor mark = at::zeros({ncols}, i32);
+  at::Tensor rank = at::empty({ncols}, i32);
+  at::Tensor cnt = at::empty({S}, i32);
+  at::Tensor posmap = at::empty({ncols}, i32);
+  at::Tensor src = at::full({P_cap}, -1, i32);
+  at::Tensor cinv = at::full({P_cap}, -1, i32);
+  at::Tensor col_c = at::empty({cap}, i32);
+  at::Tensor seg = at::empty({S + 1}, i32);
+  if (cap > 0) {
+    const int blocks = std::min((cap + 255) / 256, 4096);
+    hipLaunchKernelGGL(sg_mark_kernel, dim3(blocks), dim3(256), 0, stream(),
+                       rowptr.data_ptr<int>(), R, col.data_ptr<int>(), cap,
+                       mark.data_ptr<int>());
+    DGMC_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(sg_scan_kernel, dim3(S), dim3(1024), 0, stream(),
+                     mark.data_ptr<int>(), (int)Nsrc, (int)S,
+                     rank.data_ptr<int>(), cnt.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  const int64_t span = std::max<int64_t>(ncols, cap);
+  hipLaunchKernelGGL(sg_fill_kernel, dim3((span + 255) / 256), dim3(256), 0,
+                     stream(), rank.data_ptr<int>(), cnt.data_ptr<int>(),
+                     (int)Nsrc, (int)S, rowptr.data_ptr<int>(), R,
+                     col.data_ptr<int>(), cap, posmap.data_ptr<int>(),
+                     src.data_ptr<int>(), cinv.data_ptr<int>(),
+                     col_c.data_ptr<int>(), seg.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  return {src, seg, col_c, posmap, cinv, cnt};
+}
+
+// ---------------------------------------------------------------------------
+// Segmented gathered GEMM (NN):  Y[m, :] = A_m W_{slot(m)}  with
+//   TRANS_W = false: A_m = X[src[m], :K] (zero row if src < 0), W_s [K, Nn]
+//   TRANS_W = true : A_m = X[m, :K] (dX pass: X = dY_c), B = W_s^T,
+//                    W_s stored [Nn, K] (the forward's [in, out] weight).
+// Persistent: each workgroup walks 128x128 output tiles (grid stride) as ONE
+// stream of 32-deep k-chunks, so the next tile's first chunk (and, one tile
+// ahead, its gather indices) is in flight while the current tile finishes -
+// psi_2's K = 128 has only 4 chunks per tile, and a per-tile prologue of two
+// dependent global round trips otherwise dominates.
+// ---------------------------------------------------------------------------
+template <bool TRANS_W>
+__global__ __launch_bounds__(kSgThreads, 3) void slot_gemm_kernel(
+    const float* __restrict__ X, const int* __restrict__ src,
+    const int* __restrict__ seg, int S, const float* __restrict__ weight,
+    const float* __restrict__ root, int nw, int K, int Nn,
+    float* __restrict__ Y) {
+  __shared__ float As[kSgBM * kSgKP];
+  __shared__ float Bs[TRANS_W ? kSgBN * kSgKP : kSgBK * kSgNP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntn = Nn / kSgBN, nk = K / kSgBK;
+  const int U = (seg[S] / kSgBM) * ntn;            // active output tiles
+  const int G = gridDim.x;
+  int u = xcd_remap(blockIdx.x, G);
+  if (u >= U) return;
+
+  // This thread's A slots: rows (tid >> 3) + 32 i, k-quad (tid & 7).
+  const int c4 = (tid & 7) * 4;
+  auto rows_of = [&](int uu, int (&rr)[4]) {
+    const int m0 = (uu / ntn) * kSgBM;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + (tid >> 3) + 32 * i;
+      rr[i] = TRANS_W ? m : src[m];
+    }
+  };
+  auto wptr = [&](int uu) {
+    const int s = seg_slot(seg, S, (uu / ntn) * kSgBM);
+    return slot_weight(weight, root, nw, s, (size_t)K * Nn);
+  };
+  int rcur[4], rnext[4];
+  rows_of(u, rcur);
+  const float* W = wptr(u);
+  int n0 = (u % ntn) * kSgBN;
+  int un = u + G;
+  const float* Wn = W;
+  if (un < U) {
+    rows_of(un, rnext);
+    Wn = wptr(un);
+  }
+
+  float4 ra[4], rb[4];
+  auto load = [&](const int (&rr)[4], const float* Wt, int nn0, int kc) {
+    const int k0 = kc * kSgBK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rr[i];
+      const float4 v = ld4(X + (size_t)(r < 0 ? 0 : r) * K + k0 + c4);
+      ra[i] = r < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + kSgThreads * i;
+      if (TRANS_W) {
+        // B(k, n) = W[n0 + n][k0 + k]: 128 n-rows x 32 k.
+        rb[i] = ld4(Wt + (size_t)(nn0 + (idx >> 3)) * K + k0 + (idx & 7) * 4);
+      } else {
+        // B(k, n) = W[k0 + k][n0 + n]: 32 k-rows x 128 n.
+        rb[i] =
+            ld4(Wt + (size_t)(k0 + (idx >> 5)) * Nn + nn0 + (idx & 31) * 4);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + kSgThreads * i;
+      float* a = As + ((tid >> 3) + 32 * i) * kSgKP + c4;
+      a[0] = ra[i].x; a[1] = ra[i].y; a[2] = ra[i].z; a[3] = ra[i].w;
+      if (TRANS_W) {
+        float* b = Bs + (idx >> 3) * kSgKP + (idx & 7) * 4;
+        b[0] = rb[i].x; b[1] = rb[i].y; b[2] = rb[i].z; b[3] = rb[i].w;
+      } else {
+        *reinterpret_cast<float4*>(Bs + (idx >> 5) * kSgNP + (idx & 31) * 4) =
+            rb[i];
+      }
+    }
+  };
+
+  sg_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const int l32 = lane & 31, h = lane >> 5;
+  load(rcur, W, n0, 0);
+  int kc = 0;
+  while (true) {
+    store();
+    __syncthreads();
+    const bool last = kc + 1 == nk;
+    if (!last) load(rcur, W, n0, kc + 1);
+    else if (un < U) load(rnext, Wn, (un % ntn) * kSgBN, 0);
+#pragma unroll
+    for (int st = 0; st < kSgBK / 2; ++st) {
+      const int kk = 2 * st + h;
+      float av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        av[a] = As[(wm * 64 + a * 32 + l32) * kSgKP + kk];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int n = wn * 64 + b * 32 + l32;
+        bv[b] = TRANS_W ? Bs[n * kSgKP + kk] : Bs[kk * kSgNP + n];
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b],
+                                                           acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+    if (!last) {
+      ++kc;
+      continue;
+    }
+    // C/D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h.
+    const int m0 = (u / ntn) * kSgBM;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int c = wn * 64 + b * 32 + l32;
+          Y[(size_t)(m0 + row) * Nn + n0 + c] = acc[a][b][r];
+          acc[a][b][r] = 0.f;
+        }
+    if (un >= U) break;
+    u = un;
+    n0 = (u % ntn) * kSgBN;
+    W = Wn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rcur[i] = rnext[i];
+    kc = 0;
+    un = u + G;
+    if (un < U) {
+      rows_of(un, rnext);
+      Wn = wptr(un);
+    }
+  }
+}
+
+at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
+                     const at::Tensor& seg, const at::Tensor& weight,
+                     const c10::optional<at::Tensor>& root, bool trans_w) {
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kFloat &&
+                  X.is_contiguous() && X.dim() == 2,
+              "slot_gemm: contiguous fp32 X");
+  TORCH_CHECK(weight.scalar_type() == at::kFloat && weight.is_contiguous() &&
+                  weight.dim() == 3,
+              "slot_gemm: fp32 weight [K, in, out]");
+  const int64_t S = seg.numel() - 1;
+  const int64_t nw = weight.size(0);
+  const int64_t in = weight.size(1), out = weight.size(2);
+  const bool has_root = root.has_value() && root->defined();
+  TORCH_CHECK(S == nw + (has_root ? 1 : 0) && S <= kSgMaxS,
+              "slot_gemm: slots = weight slots + root");
+  if (has_root)
+    TORCH_CHECK(root->scalar_type() == at::kFloat && root->is_contiguous() &&
+                    root->size(0) == in && root->size(1) == out,
+                "slot_gemm: root [in, out]");
+  TORCH_CHECK(in % kSgBN == 0 && out % kSgBN == 0,
+              "slot_gemm: in/out multiples of 128");
+  const int64_t K = trans_w ? out : in;
+  const int64_t Nn = trans_w ? in : out;
+  TORCH_CHECK(X.size(1) == K && aligned16(X.data_ptr()), "slot_gemm: X [*, K]");
+  const int64_t P = src.numel();
+  TORCH_CHECK(P % kSgBM == 0 && src.scalar_type() == at::kInt,
+              "slot_gemm: src [P_cap % 128]");
+  if (trans_w) TORCH_CHECK(X.size(0) == P, "slot_gemm: dY_c rows == P_cap");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  at::Tensor Y = at::empty({P, Nn}, X.options());
+  // Persistent grid: 3 resident workgroups per CU (VGPR-limited).
+  const int64_t blocks = std::min<int64_t>((P / kSgBM) * (Nn / kSgBN),
+                                           3 * num_cus(X.device().index()));
+  if (blocks == 0) return Y;
+  const float* rp = has_root ? root->data_ptr<float>() : nullptr;
+  if (trans_w)
+    hipLaunchKernelGGL(slot_gemm_kernel<true>, dim3(blocks), dim3(kSgThreads),
+                       0, stream(), X.data_ptr<float>(), src.data_ptr<int>(),
+                       seg.data_ptr<int>(), (int)S, weight.data_ptr<float>(),
+                       rp, (int)nw, (int)K, (int)Nn, Y.data_ptr<float>());
+  else
+    hipLaunchKernelGGL(slot_gemm_kernel<false>, dim3(blocks),
+                       dim3(kSgThreads), 0, stream(), X.data_ptr<float>(),
+                       src.data_ptr<int>(), seg.data_ptr<int>(), (int)S,
+                       weight.data_ptr<float>(), rp, (int)nw, (int)K, (int)Nn,
+                       Y.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return Y;
+}
+
+// ---------------------------------------------------------------------------
+// Row-mapped SpMM: out[p, :] = sum_{e in row cinv[p] of (rowptr, col, val)}
+// val[e] * g[col[e], :]  (zero for cinv[p] < 0) - dY_c = A_c^T g' straight
+// from the assembled A^T (rows j*S + k) without re-indexing it.
+// ---------------------------------------------------------------------------
+template <int LPR>
+__global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ val, const int* __restrict__ cinv,
+    const int* __restrict__ tot, const float* __restrict__ g,
+    float* __restrict__ out, int P, int C) {
+  constexpr int RPB = 256 / LPR;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int p = blk * RPB + threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  // Rows past the last slot segment are never read (slot_gemm / wgrad stop
+  // at seg[S]); padding rows inside segments are written as zeros.
+  if (p >= P || (tot != nullptr && p >= *tot)) return;
+  const int c = cinv[p];
+  const int e0 = c >= 0 ? rowptr[c] : 0, e1 = c >= 0 ? rowptr[c + 1] : 0;
+  for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int e = e0;
+    for (; e + 4 <= e1; e += 4) {
+      float4 v[4];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w[u] = val[e + u];
+        v[u] = ld4(g + (size_t)col[e + u] * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x = fmaf(w[u], v[u].x, acc.x);
+        acc.y = fmaf(w[u], v[u].y, acc.y);
+        acc.z = fmaf(w[u], v[u].z, acc.z);
+        acc.w = fmaf(w[u], v[u].w, acc.w);
+      }
+    }
+    for (; e < e1; ++e) {
+      const float w = val[e];
+      const float4 v = ld4(g + (size_t)col[e] * C + c0);
+      acc.x = fmaf(w, v.x, acc.x);
+      acc.y = fmaf(w, v.y, acc.y);
+      acc.z = fmaf(w, v.z, acc.z);
+      acc.w = fmaf(w, v.w, acc.w);
+    }
+    *reinterpret_cast<float4*>(out + (size_t)p * C + c0) = acc;
+  }
+}
+
+at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
+                            const at::Tensor& val, const at::Tensor& cinv,
+                            const at::Tensor& g,
+                            const c10::optional<at::Tensor>& seg) {
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat &&
+                  g.is_contiguous() && g.dim() == 2 && g.size(1) % 4 == 0 &&
+                  aligned16(g.data_ptr()),
+              "slot_spmm_rowmap: contiguous fp32 g [N, C % 4]");
+  TORCH_CHECK(val.scalar_type() == at::kFloat && cinv.scalar_type() == at::kInt,
+              "slot_spmm_rowmap: dtypes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  const int64_t P = cinv.numel(), C = g.size(1);
+  at::Tensor out = at::empty({P, C}, g.options());
+  if (P == 0) return out;
+  const int* totp = nullptr;
+  if (seg.has_value() && seg->defined())
+    totp = seg->data_ptr<int>() + (seg->numel() - 1);
+  const int lanes = (int)(C / 4);
+  auto go = [&](auto lpr) {
+    constexpr int L = decltype(lpr)::value;
+    const int64_t blocks = (P + 256 / L - 1) / (256 / L);
+    hipLaunchKernelGGL(sg_spmm_rowmap_kernel<L>, dim3(blocks), dim3(256), 0,
+                       stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
+                       val.data_ptr<float>(), cinv.data_ptr<int>(), totp,
+                       g.data_ptr<float>(), out.data_ptr<float>(), (int)P,
+                       (int)C);
+  };
+  if (lanes <= 8) go(std::integral_constant<int, 8>());
+  else if (lanes <= 16) go(std::integral_constant<int, 16>());
+  else if (lanes <= 32) go(std::integral_constant<int, 32>());
+  else go(std::integral_constant<int, 64>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Per-node gather-sum over slots: out[j, :] = add[j, :] + sum_k Z[posmap[j*S
+// + k], :]  (slot order fixed: deterministic).  dX of the slot GEMM.
+// ---------------------------------------------------------------------------
+template <int LPR>
+__global__ __launch_bounds__(256) void sg_gather_sum_kernel(
+    const int* __restrict__ posmap, const float* __restrict__ Z,
+    const float* __restrict__ add, int lda, float* __restrict__ out, int N,
+    int S, int C) {
+  constexpr int RPB = 256 / LPR;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int j = blk * RPB + threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  if (j >= N) return;
+  const int* pm = posmap + (size_t)j * S;
+  for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
+    float4 acc = add ? ld4(add + (size_t)j * lda + c0)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < S; ++k) {
+      const int p = pm[k];
+      if (p >= 0) {
+        const float4 v = ld4(Z + (size_t)p * C + c0);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    *reinterpret_cast<float4*>(out + (size_t)j * C + c0) = acc;
+  }
+}
+
+at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
+                           int64_t N, int64_t S,
+                           const c10::optional<at::Tensor>& add) {
+  TORCH_CHECK(Z.is_cuda() && Z.scalar_type() == at::kFloat &&
+                  Z.is_contiguous() && Z.dim() == 2 && Z.size(1) % 4 == 0 &&
+                  aligned16(Z.data_ptr()),
+              "slot_gather_sum: contiguous fp32 Z [P, C % 4]");
+  TORCH_CHECK(posmap.numel() == N * S, "slot_gather_sum: posmap [N * S]");
+  const int64_t C = Z.size(1);
+  const float* ap = nullptr;
+  int64_t lda = 0;
+  if (add.has_value() && add->defined()) {
+    TORCH_CHECK(add->scalar_type() == at::kFloat && add->dim() == 2 &&
+                    add->size(0) == N && add->size(1) == C &&
+                    add->stride(1) == 1 && add->stride(0) % 4 == 0 &&
+                    aligned16(add->data_ptr()),
+                "slot_gather_sum: addend fp32 [N, C], 16-B aligned rows");
+    ap = add->data_ptr<float>();
+    lda = add->stride(0);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
+  at::Tensor out = at::empty({N, C}, Z.options());
+  if (N == 0) return out;
+  const int lanes = (int)(C / 4);
+  auto go = [&](auto lpr) {
+    constexpr int L = decltype(lpr)::value;
+    const int64_t blocks = (N + 256 / L - 1) / (256 / L);
+    hipLaunchKernelGGL(sg_gather_sum_kernel<L>, dim3(blocks), dim3(256), 0,
+                       stream(), posmap.data_ptr<int>(), Z.data_ptr<float>(),
+                       ap, (int)lda, out.data_ptr<float>(), (int)N, (int)S,
+                       (int)C);
+  };
+  if (lanes <= 8) go(std::integral_constant<int, 8>());
+  else if (lanes <= 16) go(std::integral_constant<int, 16>());
+  else if (lanes <= 32) go(std::integral_constant<int, 32>());
+  else go(std::integral_constant<int, 64>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient (TN):  dW_s[i, c] = sum_u sum_{p in slot s} X_u[src p][i]
+// dY_u[p][c].  Work items = (slot, CH consecutive 128-row tiles of its
+// segment), each a 128x128 output tile; the items' fp32 partials are folded
+// per slot in item order (deterministic).
+// ---------------------------------------------------------------------------
+struct SgUses {
+  const float* x[kSgMaxU];
+  const float* g[kSgMaxU];
+};
+
+// Item table: item i -> (slot, first row, end row); ib[s] = first item of s.
+__global__ void sg_items_kernel(const int* __restrict__ seg, int S, int CH,
+                                int G_cap, int* __restrict__ items,
+                                int* __restrict__ ib) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int n = 0;
+  for (int s = 0; s < S; ++s) {
+    ib[s] = n;
+    for (int r = seg[s]; r < seg[s + 1] && n < G_cap; r += CH * kSgBM) {
+      items[3 * n + 0] = s;
+      items[3 * n + 1] = r;
+      items[3 * n + 2] = min(r + CH * kSgBM, seg[s + 1]);
+      ++n;
+    }
+  }
+  ib[S] = n;
+  for (int i = n; i < G_cap; ++i) items[3 * i + 0] = -1;
+}
+
+__global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(
+    SgUses U, int nu, const int* __restrict__ src,
+    const int* __restrict__ items, int Kin, int C,
+    float* __restrict__ part) {
+  __shared__ float As[kSgBK * kSgNP];     // [p][i]
+  __shared__ float Bs[kSgBK * kSgNP];     // [p][c]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tiles_n = C / kSgBN, tiles = (Kin / kSgBM) * tiles_n;
+  const int item = blockIdx.x / tiles, t = blockIdx.x % tiles;
+  const int i0 = (t / tiles_n) * kSgBM, n0 = (t % tiles_n) * kSgBN;
+  float* outp = part + ((size_t)item * Kin + i0) * C + n0;
+  const int s = items[3 * item];
+  const int l32 = lane & 31, h = lane >> 5;
+  if (s < 0) return;
+  const int pb = items[3 * item + 1], pe = items[3 * item + 2];
+
+  sg_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  // Tiles: 32 p-rows x 128 columns, 4 float4 per thread (32 lanes per row:
+  // rows (tid >> 5) + 8 i).  The gather indices of chunk q + 1 are loaded
+  // one chunk ahead, so a chunk's row loads never wait on their index load.
+  float4 ra[4], rb[4];
+  const int nchunk = (pe - pb) / kSgBK;
+  const int total = nchunk * nu;
+  const int c4 = (tid & 31) * 4;
+  auto prow = [&](int q, int i) {
+    return pb + (q % nchunk) * kSgBK + (tid >> 5) + 8 * i;
+  };
+  int rs[4];
+  auto load_idx = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rs[i] = q < total ? src[prow(q, i)] : -1;
+  };
+  auto load = [&](int q) {
+    const int u = q / nchunk;
+    const float* Xu = U.x[u];
+    const float* Gu = U.g[u];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rs[i];
+      const float4 v = ld4(Xu + (size_t)(r < 0 ? 0 : r) * Kin + i0 + c4);
+      ra[i] = r < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+      rb[i] = ld4(Gu + (size_t)prow(q, i) * C + n0 + c4);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + kSgThreads * i;
+      const int o = (idx >> 5) * kSgNP + (idx & 31) * 4;
+      *reinterpret_cast<float4*>(As + o) = ra[i];
+      *reinterpret_cast<float4*>(Bs + o) = rb[i];
+    }
+  };
+  load_idx(0);
+  if (total > 0) load(0);
+  load_idx(1);
+  for (int q = 0; q < total; ++q) {
+    store();
+    __syncthreads();
+    if (q + 1 < total) {
+      load(q + 1);
+      load_idx(q + 2);
+    }
+#pragma unroll
+    for (int st = 0; st < kSgBK / 2; ++st) {
+      const int kk = 2 * st + h;
+      float av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        av[a] = As[kk * kSgNP + wm * 64 + a * 32 + l32];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        bv[b] = Bs[kk * kSgNP + wn * 64 + b * 32 + l32];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b],
+                                                           acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int c = wn * 64 + b * 32 + l32;
+        outp[(size_t)row * C + c] = acc[a][b][r];
+      }
+}
+
+// out[s] = sum_{items of s, in order} part[item]  (float4 per thread).
+__global__ __launch_bounds__(256) void sg_fold_kernel(
+    const float* __restrict__ part, const int* __restrict__ ib, int S,
+    int64_t per, float* __restrict__ out) {
+  const int s = blockIdx.y;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= per) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int g = ib[s]; g < ib[s + 1]; ++g) {
+    const float4 v = ld4(part + (size_t)g * per + i);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + (size_t)s * per + i) = acc;
+}
+
+at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
+                          const at::Tensor& src, const at::Tensor& seg,
+                          int64_t chunk) {
+  const int64_t nu = (int64_t)xs.size();
+  TORCH_CHECK(nu >= 1 && nu <= kSgMaxU && (int64_t)gs.size() == nu,
+              "slot_wgrad_f32: 1 <= uses <= 16, one G per X");
+  const int64_t Kin = xs[0].size(1), C = gs[0].size(1);
+  const int64_t P = src.numel(), S = seg.numel() - 1;
+  TORCH_CHECK(Kin % kSgBM == 0 && C % kSgBN == 0 && P % kSgBM == 0 &&
+                  chunk >= 1 && S <= kSgMaxS,
+              "slot_wgrad_f32: in/out multiples of 128");
+  SgUses U{};
+  for (int64_t u = 0; u < nu; ++u) {
+    const at::Tensor& x = xs[u];
+    const at::Tensor& g = gs[u];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat &&
+                    x.is_contiguous() && x.dim() == 2 && x.size(1) == Kin &&
+                    aligned16(x.data_ptr()),
+                "slot_wgrad_f32: X_u contiguous fp32 [N, in]");
+    TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous() &&
+                    g.dim() == 2 && g.size(0) == P && g.size(1) == C &&
+                    aligned16(g.data_ptr()),
+                "slot_wgrad_f32: dY_u contiguous fp32 [P_cap, out]");
+    U.x[u] = x.data_ptr<float>();
+    U.g[u] = g.data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  const int64_t G_cap = P / (kSgBM * chunk) + S;
+  auto i32 = src.options();
+  at::Tensor items = at::empty({G_cap, 3}, i32);
+  at::Tensor ib = at::empty({S + 1}, i32);
+  hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
+                     seg.data_ptr<int>(), (int)S, (int)chunk, (int)G_cap,
+                     items.data_ptr<int>(), ib.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  const int64_t per = Kin * C;
+  at::Tensor part = at::empty({G_cap, per}, xs[0].options());
+  const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
+  hipLaunchKernelGGL(slot_wgrad_tn_kernel, dim3(G_cap * tiles),
+                     dim3(kSgThreads), 0, stream(), U, (int)nu,
+                     src.data_ptr<int>(), items.data_ptr<int>(), (int)Kin,
+                     (int)C, part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  at::Tensor out = at::empty({S, Kin, C}, xs[0].options());
+  hipLaunchKernelGGL(sg_fold_kernel, dim3((per / 4 + 255) / 256, S), dim3(256),
+                     0, stream(), part.data_ptr<float>(), ib.data_ptr<int>(),
+                     (int)S, per, out.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+}  // namespace dgmc

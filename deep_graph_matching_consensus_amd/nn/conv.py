@@ -21,6 +21,7 @@ import torch
 from torch.nn import Parameter
 
 from ..ops import _backend
+from ..ops import slot_gemm
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.gemm import compute_dtype
 from ..ops.sparse import SLOT_CONV, gemm_spmm, prime_slot_images, spmm
@@ -174,6 +175,14 @@ class SplineConv(torch.nn.Module):
                            device_params=(self.kernel_size,
                                           self.is_open_spline))
         dtype = compute_dtype(x)
+        if dtype == torch.float32 and slot_gemm.supported(
+                plan, x, self.weight, self.root):
+            # fp32: only the (node, slot) pairs edges use are multiplied
+            # (ops/slot_gemm.py, csrc/hip/slot_gemm.hip).
+            return slot_gemm.slot_gemm_spmm(
+                plan, x, self.weight, self.root, self.bias,
+                relu=(act == 'relu'), loop_key=(id(self), N, plan.num_cols),
+                passthrough=passthrough)
         w, w_lp = self.stacked_operands(dtype, x, plan)
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),

@@ -416,8 +416,9 @@ def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
 
 def consensus_transport_supported(PQ, r_s, S_hat):
     B, N_s, N_t = S_hat.shape
-    return (_hip_ok(S_hat, N_s, N_t) and PQ.dtype == torch.bfloat16 and
-            r_s.dtype == torch.bfloat16 and PQ.is_contiguous() and
+    return (_hip_ok(S_hat, N_s, N_t) and
+            PQ.dtype in (torch.bfloat16, torch.float32) and
+            r_s.dtype == PQ.dtype and PQ.is_contiguous() and
             PQ.size(1) == r_s.size(1))
 
 
@@ -571,25 +572,22 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
         parts = getattr(o_joint, 'parts', None)
         if parts is not None and cat_matmul_supported(parts, w_t):
             PQ = cat_matmul(parts, w_t, lp, key, total)
-            loop = loopgrad.group(('consensus', id(mlp)))
-            if next_r_s is not None and FUSE_STEPS and \
-                    consensus_transport_supported(PQ, next_r_s, S_hat):
-                # (joint input of the next psi_2 call, S_hat')
-                return _ConsensusTransport.apply(
-                    S_hat, PQ, lay_s.num_nodes, lin1.bias, lin2.weight,
-                    lin2.bias, next_r_s, lay_s.ptr, lay_t.ptr,
-                    lay_t.num_nodes, loop)
-            return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes,
-                                          lin1.bias, lin2.weight, lin2.bias,
-                                          lay_s.ptr, lay_t.ptr, loop)
-        if parts is not None:
-            o_joint = o_joint.cat()
-        w_lp = lp.get(o_joint.dtype)
-        if w_lp is None:
-            w_lp = lp[o_joint.dtype] = w_t.detach().to(o_joint.dtype)
-        PQ = mixed_matmul(o_joint, w_t, w_lp, loop_key=key + (
-            o_joint.size(0), ))
+        else:
+            if parts is not None:
+                o_joint = o_joint.cat()
+            w_lp = lp.get(o_joint.dtype)
+            if w_lp is None:
+                w_lp = lp[o_joint.dtype] = w_t.detach().to(o_joint.dtype)
+            PQ = mixed_matmul(o_joint, w_t, w_lp, loop_key=key + (
+                o_joint.size(0), ))
         loop = loopgrad.group(('consensus', id(mlp)))
+        if next_r_s is not None and FUSE_STEPS and \
+                consensus_transport_supported(PQ, next_r_s, S_hat):
+            # (joint input of the next psi_2 call, S_hat')
+            return _ConsensusTransport.apply(
+                S_hat, PQ, lay_s.num_nodes, lin1.bias, lin2.weight,
+                lin2.bias, next_r_s, lay_s.ptr, lay_t.ptr,
+                lay_t.num_nodes, loop)
         return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes, lin1.bias,
                                       lin2.weight, lin2.bias, lay_s.ptr,
                                       lay_t.ptr, loop)

@@ -1,0 +1,187 @@
+"""fp32 SplineConv on the (node, slot) pairs the edges use (csrc/hip/slot_gemm.hip).
+
+Reference: ``/root/reference/dgmc/models/spline.py:21,49`` (PyG SplineConv
+over torch_spline_conv, fp32).  With ``A [N, N*S]`` the layer's message
+operator (columns ``j*S + k``: source ``j``, B-spline slot ``k``, root =
+slot ``S-1``; :func:`~.plans.spline_plan`)::
+
+    out = act(A (X W) + bias)
+
+The dense form multiplies every node by every slot's weight; only 42 % of
+those ``(j, k)`` pairs carry an entry on PascalVOC-shaped batches, so this
+path forms exactly those rows (``Y_c = X[src] W_slot``, a segmented gathered
+GEMM on fp32 MFMA) and aggregates them with the CSR SpMM over ``A``'s
+re-indexed columns.  Backward: ``dY_c = A^T g'`` (row-mapped SpMM over the
+assembled transpose), ``dX = sum_k (dY_c W_k^T)`` (same GEMM kernel with
+``W^T`` + a per-node gather-sum), ``dW_k = X[src]^T dY_c`` (gathered TN
+GEMM, per-slot fixed-order fold).  Everything is exact fp32 (the MFMA is a
+k-ordered ``fmaf`` chain) and deterministic.
+
+Inside a :func:`~..runtime.loopgrad.loop_scope` (psi_2 in the consensus
+loop) the weight gradient of all uses is ONE launch over the kept ``(X_u,
+dY_c,u)`` pairs.
+"""
+import os
+
+import torch
+
+from . import _backend
+from .gemm import col_partial_rows, loop_col_total
+
+BM = 128                      # compact segment / tile unit (slot_gemm.hip)
+MAX_USES = 16                 # pointer table of slot_wgrad_f32
+ENABLED = os.environ.get('DGMC_AMD_SLOT_GEMM', '1') == '1'
+
+
+class CompactPlan(object):
+    """Used-column layout of one operator (built once, cached on it)."""
+
+    def __init__(self, op, S):
+        N = op.num_cols // S
+        ncols = op.num_cols
+        cap = op.col.numel()
+        P_cap = (min(cap, ncols) + S * BM + BM - 1) // BM * BM
+        (self.src, self.seg, self.col_c, self.posmap, self.cinv,
+         self.counts) = _backend.ops().slot_compact_plan(
+             op.rowptr, op.col, N, S, P_cap)
+        self.S, self.N, self.P_cap = S, N, P_cap
+
+
+def compact_plan(op, S):
+    cache = op.__dict__.setdefault('_compact_plan', {})
+    p = cache.get(S)
+    if p is None:
+        p = cache[S] = CompactPlan(op, S)
+    return p
+
+
+def supported(op, x, weight, root):
+    """Shapes / dtypes served by the fp32 slot GEMM path."""
+    if not (ENABLED and _backend.use_hip(x) and x.dtype == torch.float32 and
+            weight.dtype == torch.float32 and weight.dim() == 3):
+        return False
+    S = weight.size(0) + (1 if root is not None else 0)
+    cin, cout = weight.size(1), weight.size(2)
+    return (cin % 128 == 0 and cout % 128 == 0 and S <= 64 and
+            x.dim() == 2 and x.size(1) == cin and
+            op.num_cols == x.size(0) * S and op.num_rows == x.size(0))
+
+
+def _wgrad_chunk(P_cap, cin, cout):
+    """Row tiles per weight-gradient work item: ~2048 workgroups."""
+    tiles = (cin // 128) * (cout // 128)
+    return max(1, (P_cap // BM) * tiles // 2048)
+
+
+def weight_grad(xs, dys, plan, cin, cout):
+    """``dW [S, in, out]`` = ``sum_u X_u[src]^T dY_c,u`` per slot."""
+    ops = _backend.ops()
+    chunk = _wgrad_chunk(plan.P_cap, cin, cout)
+    out = None
+    for i in range(0, len(xs), MAX_USES):
+        part = ops.slot_wgrad_f32(list(xs[i:i + MAX_USES]),
+                                  list(dys[i:i + MAX_USES]), plan.src,
+                                  plan.seg, chunk)
+        out = part if out is None else out.add_(part)
+    return out
+
+
+class _SlotGemmSpMM(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, weight, root, bias, op, relu, loop, passthrough):
+        S = weight.size(0) + (1 if root is not None else 0)
+        plan = compact_plan(op, S)
+        xc = x.contiguous()
+        ops = _backend.ops()
+        Y = ops.slot_gemm(xc, plan.src, plan.seg, weight.contiguous(),
+                          root.contiguous() if root is not None else None,
+                          False)
+        out = ops.spmm_csr(op.rowptr, plan.col_c, op.val, Y, None, None,
+                           bias, relu, torch.float32)
+        ctx.save_for_backward(xc, weight, root, out if relu else None)
+        ctx.op, ctx.plan, ctx.relu, ctx.loop = op, plan, relu, loop
+        ctx.has_root = root is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.idx = loop.register() if loop is not None else None
+        if passthrough:
+            return out, x.view_as(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad, gpass=None):
+        x, weight, root, out = ctx.saved_tensors
+        nones = (None, ) * 4
+        op, plan, loop, idx = ctx.op, ctx.plan, ctx.loop, ctx.idx
+        ops = _backend.ops()
+        need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
+        if grad.stride(-1) != 1 or grad.stride(0) < grad.size(1) or \
+                grad.dtype != torch.float32:
+            grad = grad.float().contiguous()
+        part = loop.slot('b', idx, (col_partial_rows(grad.size(0)),
+                                    grad.size(1)), torch.float32,
+                         grad.device) if (loop is not None and need_b) \
+            else None
+        g, db = ops.relu_bias_bwd(grad, out if ctx.relu else grad, ctx.relu,
+                                  torch.float32, None, False, part)
+        At = op.t()
+        dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
+                                    plan.seg)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            Z = ops.slot_gemm(dyc, plan.src, plan.seg, weight.contiguous(),
+                              root.contiguous() if root is not None else None,
+                              True)
+            add = gpass if (gpass is not None and
+                            gpass.dtype == torch.float32 and gpass.dim() == 2
+                            and gpass.stride(1) == 1 and
+                            gpass.stride(0) % 4 == 0 and
+                            gpass.data_ptr() % 16 == 0) else None
+            gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add)
+            if gpass is not None and add is None:
+                gx = gx + gpass
+        elif gpass is not None:
+            gx = gpass
+        need_w = ctx.needs_input_grad[1] or (ctx.has_root and
+                                             ctx.needs_input_grad[2])
+        cin, cout = weight.size(1), weight.size(2)
+        gw = gr = gb = None
+        if loop is None:
+            if need_w:
+                dW = weight_grad([x], [dyc], plan, cin, cout)
+            if need_b:
+                gb = db.to(ctx.bias_dtype)
+        else:
+            if need_w:
+                loop.keep('x', idx, x)
+                loop.keep('dy', idx, dyc)
+            if not loop.arrive():
+                return (gx, None, None, None) + nones
+            if need_w:
+                dW = weight_grad(loop.kept_list('x'), loop.kept_list('dy'),
+                                 plan, cin, cout)
+            if need_b:
+                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+            loop.release()
+        if need_w:
+            nw = weight.size(0)
+            if ctx.needs_input_grad[1]:
+                gw = dW[:nw]
+            if ctx.has_root and ctx.needs_input_grad[2]:
+                gr = dW[nw]
+        return (gx, gw, gr, gb) + nones
+
+
+def slot_gemm_spmm(op, x, weight, root, bias=None, relu=False, loop_key=None,
+                   passthrough=False):
+    r"""``act(A (x @ [W_0 | .. | W_{K-1} | root]).view(-1, C) + bias)`` in
+    fp32 on the used ``(node, slot)`` pairs only; ``weight [K, in, out]``,
+    ``root [in, out]`` are read in place (reference checkpoint layout).
+    ``passthrough`` returns ``(out, x')`` (``x'`` aliases ``x``; its
+    gradient is added inside this op's dX kernel)."""
+    from ..runtime import loopgrad
+    loop = loopgrad.group(('slot_gemm', ) + tuple(loop_key)) \
+        if loop_key is not None else None
+    with torch.autocast(device_type='cuda', enabled=False):
+        return _SlotGemmSpMM.apply(x, weight, root, bias, op, relu, loop,
+                                   passthrough)

@@ -1215,7 +1215,7 @@ def test_fused_step_boundary_matches_separate_kernels(monkeypatch):
         torch.testing.assert_close(a, b, atol=1e-2, rtol=1e-2)
 
 
-def _step_problem(R, Ns, Nt, B):
+def _step_problem(R, Ns, Nt, B, bf=torch.bfloat16):
     torch.manual_seed(R + Ns)
     c_s = torch.randint(1, Ns + 1, (B, ))
     c_t = torch.randint(1, Nt + 1, (B, ))
@@ -1225,7 +1225,6 @@ def _step_problem(R, Ns, Nt, B):
     ptr_t = torch.zeros(B + 1, dtype=torch.int32)
     ptr_s[1:], ptr_t[1:] = c_s.cumsum(0), c_t.cumsum(0)
     rows_s, rows_t = int(ptr_s[-1]) + pad_s, int(ptr_t[-1]) + pad_t
-    bf = torch.bfloat16
     d = dict(
         R=R, c_s=c_s, c_t=c_t, ptr_s=ptr_s, ptr_t=ptr_t, rows_s=rows_s,
         rows_t=rows_t, ps=ptr_s.to(DEV), pt=ptr_t.to(DEV),
@@ -1289,6 +1288,37 @@ def _check_cons_grads(d, ref, dP, dQ, dw2, db2):
     torch.testing.assert_close(dw2.sum(0), ref['gw2'], atol=2e-3, rtol=1e-3)
     torch.testing.assert_close(db2.sum(), ref['gb2'][0], atol=2e-3,
                                rtol=1e-3)
+
+
+@pytest.mark.parametrize('R', [32, 64, 128, 48])
+@pytest.mark.parametrize('Ns,Nt,B', [(19, 23, 37), (9, 9, 300)])
+def test_step_boundary_kernels_fp32_storage(R, Ns, Nt, B):
+    """Reference precision: the same step kernels on fp32 node tensors
+    (P, Q, r_s, g_t, dP, dQ, joint all fp32) at fp32 tolerance."""
+    ops = _backend.ops()
+    d = _step_problem(R, Ns, Nt, B, torch.float32)
+    S_new, S_prob, joint = ops.dense_consensus_transport(
+        d['S_hat'], d['P'], d['Q'], d['b1'], d['w2'], d['b2'], d['r_s'],
+        d['ps'], d['pt'], d['rows_t'])
+    assert joint.dtype == torch.float32
+    G, dP, dQ, dw2, db2 = ops.dense_transport_consensus_bwd(
+        S_prob, d['r_s'], d['g_t'], d['add'], d['P'], d['Q'], d['b1'],
+        d['w2'], d['ps'], d['pt'], None)
+    ref = _step_ref(d, True, True)
+    rows_s, n_s, n_t = d['rows_s'], int(d['ptr_s'][-1]), int(d['ptr_t'][-1])
+    tol = dict(atol=2e-5, rtol=2e-5)
+    torch.testing.assert_close(S_new, ref['S_new'].detach(), **tol)
+    torch.testing.assert_close(S_prob, ref['S_prob'].detach(), **tol)
+    assert torch.equal(joint[:rows_s], d['r_s'])
+    torch.testing.assert_close(joint[rows_s:], ref['r_t'], **tol)
+    assert (joint[rows_s + n_t:] == 0).all()
+    torch.testing.assert_close(G, ref['gS'], **tol)
+    torch.testing.assert_close(dP, ref['gP'], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dQ, ref['gQ'], atol=1e-4, rtol=1e-4)
+    assert (dP[n_s:] == 0).all() and (dQ[n_t:] == 0).all()
+    torch.testing.assert_close(dw2.sum(0), ref['gw2'], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(db2.sum(), ref['gb2'][0], atol=1e-4,
+                               rtol=1e-4)
 
 
 @pytest.mark.parametrize('R', [32, 64, 128, 48])
