@@ -200,6 +200,9 @@ void adam_step_inc(at::TensorList steps,
   const int* fl = nullptr;
   int nflags = 0;
   if (flags.has_value() && flags->defined()) {
+    // Only the first 64-parameter chunk folds the flags; later chunks read
+    // found_inf, so it must be given.
+    TORCH_CHECK(fi != nullptr, "adam_step_inc: flags need found_inf");
     TORCH_CHECK(flags->scalar_type() == at::kInt && flags->is_contiguous() &&
                     flags->device() == steps[0].device(),
                 "adam_step_inc: int32 flags on the device");

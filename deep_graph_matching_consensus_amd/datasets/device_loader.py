@@ -203,14 +203,50 @@ class DevicePairLoader(object):
         """Endless full batches: epoch permutations are concatenated, so a
         batch may straddle an epoch boundary and a shard with fewer sources
         than ``batch_size`` (e.g. 2560 graphs over 8 ranks at batch 512)
-        still yields ``batch_size`` pairs per step (some sources twice)."""
+        still yields ``batch_size`` pairs per step (some sources twice).
+        The pending order lives on the loader, so :meth:`state_dict` /
+        :meth:`load_state_dict` resume the exact stream."""
         bs = self.batch_size
-        order = np.empty(0, dtype=np.int64)
+        if getattr(self, '_order', None) is None:
+            self._order = np.empty(0, dtype=np.int64)
         while True:
-            while len(order) < bs:
+            while len(self._order) < bs:
                 nxt = self.rng.permutation(self.sources) if self.shuffle \
                     else self.sources
-                order = np.concatenate([order, nxt])
-            s_ids, order = order[:bs], order[bs:]
+                self._order = np.concatenate([self._order, nxt])
+            s_ids, self._order = self._order[:bs], self._order[bs:]
             t_ids = self.store.sample_partners(s_ids, self.rng)
             yield self.store.collate(s_ids, t_ids)
+
+    def state_dict(self):
+        """Sampler state (``weights_only``-loadable leaves)."""
+        order = getattr(self, '_order', None)
+        return {'rng': sampler_rng_state(self.rng),
+                'order': None if order is None else
+                torch.from_numpy(np.asarray(order, dtype=np.int64).copy())}
+
+    def load_state_dict(self, state):
+        set_sampler_rng_state(self.rng, state['rng'])
+        order = state.get('order')
+        self._order = None if order is None else order.cpu().numpy()
+
+
+def sampler_rng_state(rng):
+    """``np.random.Generator`` state as tensors / primitives (PCG64)."""
+    st = rng.bit_generator.state
+    # 128-bit PCG64 words as bytes (torch.load(weights_only=True) safe).
+    return {'bit_generator': st['bit_generator'],
+            'state': [int(st['state']['state']).to_bytes(16, 'little'),
+                      int(st['state']['inc']).to_bytes(16, 'little')],
+            'has_uint32': int(st['has_uint32']),
+            'uinteger': int(st['uinteger'])}
+
+
+def set_sampler_rng_state(rng, state):
+    s, inc = state['state']
+    rng.bit_generator.state = {
+        'bit_generator': state['bit_generator'],
+        'state': {'state': int.from_bytes(bytes(s), 'little'),
+                  'inc': int.from_bytes(bytes(inc), 'little')},
+        'has_uint32': int(state['has_uint32']),
+        'uinteger': int(state['uinteger'])}

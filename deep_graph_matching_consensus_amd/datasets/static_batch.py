@@ -192,6 +192,23 @@ class StaticPairBatcher(object):
         self._pos += self.B
         return s, self.store.sample_partners(s, self.rng)
 
+    def state_dict(self):
+        """Sampler state: RNG, pending epoch order and position."""
+        from .device_loader import sampler_rng_state
+        return {'rng': sampler_rng_state(self.rng),
+                'order': None if self._order is None else
+                torch.from_numpy(np.asarray(self._order,
+                                            dtype=np.int64).copy()),
+                'pos': int(self._pos), 'overflows': int(self.overflows)}
+
+    def load_state_dict(self, state):
+        from .device_loader import set_sampler_rng_state
+        set_sampler_rng_state(self.rng, state['rng'])
+        order = state.get('order')
+        self._order = None if order is None else order.cpu().numpy()
+        self._pos = int(state.get('pos', 0))
+        self.overflows = int(state.get('overflows', 0))
+
     def load(self, s_ids=None, t_ids=None):
         """Stage the next batch into the static device buffer.
 

@@ -675,16 +675,37 @@ class DGMC(torch.nn.Module):
         correct = self.correct(S, y).item()
         return correct / y.size(1) if reduction == 'mean' else correct
 
+    def hits_count(self, k, S, y):
+        r"""Device tensor: number of ground truths ranked within the top
+        ``k`` (``dgmc.py:290-311``) - without sorting.  The ground truth's
+        rank is the number of scores above it plus the equal scores at a
+        lower index (the order of a stable descending sort), so one
+        elementwise pass per row replaces the reference's full ``argsort``;
+        sparse duplicates of the ground truth count once per slot, as in the
+        reference's ``(pred == y).sum()``."""
+        if not S.is_sparse:
+            rows = S[y[0]]                                   # [G, N_t]
+            v = rows.gather(1, y[1].view(-1, 1))
+            col = torch.arange(rows.size(1), device=rows.device)
+            rank = (rows > v).sum(1) + ((rows == v) &
+                                        (col < y[1].view(-1, 1))).sum(1)
+            return (rank < k).sum()
+        assert S.__idx__ is not None and S.__val__ is not None
+        idx, val = S.__idx__[y[0]], S.__val__[y[0]]          # [G, k']
+        slot = torch.arange(val.size(1), device=val.device)
+        # rank[g, c] of candidate slot c among its row's values
+        vc = val.unsqueeze(2)                                # [G, k', 1]
+        vo = val.unsqueeze(1)                                # [G, 1, k']
+        rank = (vo > vc).sum(2) + ((vo == vc) &
+                                   (slot.view(1, 1, -1) <
+                                    slot.view(1, -1, 1))).sum(2)
+        hit = (idx == y[1].view(-1, 1)) & (rank < k)
+        return hit.sum()
+
     def hits_at_k(self, k, S, y, reduction='mean'):
         r"""Fraction of ground truths ranked within the top ``k``."""
         assert reduction in ['mean', 'sum']
-        if not S.is_sparse:
-            pred = S[y[0]].argsort(dim=-1, descending=True)[:, :k]
-        else:
-            assert S.__idx__ is not None and S.__val__ is not None
-            perm = S.__val__[y[0]].argsort(dim=-1, descending=True)[:, :k]
-            pred = torch.gather(S.__idx__[y[0]], -1, perm)
-        correct = (pred == y[1].view(-1, 1)).sum().item()
+        correct = self.hits_count(k, S, y).item()
         return correct / y.size(1) if reduction == 'mean' else correct
 
     def __repr__(self):

@@ -81,9 +81,11 @@ class _PairScores(torch.autograd.Function):
 
 
 def pair_scores_supported(h, lay_s, lay_t):
+    # (mirrors pair_scores_bwd's contract: C % 4, 16-byte aligned rows)
     return (_hip_ok(h, lay_s.N, lay_t.N) and h.dim() == 2 and
             h.is_contiguous() and h.dtype in (torch.bfloat16, torch.float32)
-            and h.size(1) <= 256 and lay_s.N >= 1 and lay_t.N >= 1)
+            and h.size(1) <= 256 and h.size(1) % 4 == 0 and
+            h.data_ptr() % 16 == 0 and lay_s.N >= 1 and lay_t.N >= 1)
 
 
 def pair_scores(h, t_off, lay_s, lay_t, two=False):

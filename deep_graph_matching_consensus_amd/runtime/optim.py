@@ -72,6 +72,11 @@ def hip_adam_step(optimizer, found_inf=None, flags=None, skips=None):
                 p, memory_format=torch.preserve_format)
         steps.append(_device_step(st, p))
     b1, b2 = group['betas']
+    if flags is not None and found_inf is None:
+        # The flags are folded into found_inf by the first parameter chunk
+        # and every later chunk reads found_inf: it must exist.
+        found_inf = torch.zeros((), dtype=torch.float32,
+                                device=params[0].device)
     ops = _backend.ops()
     ops.adam_step_inc(steps, found_inf, flags, skips)
     ops.adam_multi(params, [p.grad for p in params],

@@ -241,9 +241,57 @@ class PairTrainer(object):
             else:
                 self.batcher.overflows += 1
 
+    def _snapshot(self):
+        """Everything the capture warm-ups advance (model parameters and
+        buffers, optimizer moments and step counters, running stats, RNG and
+        sampler states), restored IN PLACE by :meth:`_restore` after the
+        capture - the captured graphs keep their tensor addresses, and the
+        training trajectory is the same as without capturing (a resumed
+        graph-mode run continues exactly)."""
+        with torch.no_grad():
+            snap = {
+                'model': {k: t.detach().clone()
+                          for k, t in self.model.state_dict().items()},
+                'opt': {id(p): {k: v.detach().clone()
+                                for k, v in st.items() if torch.is_tensor(v)}
+                        for p, st in self.optimizer.state.items()},
+                'stats': self.stats.clone(),
+                'found_inf': self._found_inf.clone(),
+                'cpu_rng': torch.get_rng_state(),
+                'sampler': self.batcher.state_dict(),
+            }
+        if self.device.type == 'cuda':
+            snap['cuda_rng'] = torch.cuda.get_rng_state(self.device)
+        return snap
+
+    def _restore(self, snap):
+        with torch.no_grad():
+            for k, t in self.model.state_dict().items():
+                t.copy_(snap['model'][k])
+            for p, st in self.optimizer.state.items():
+                old = snap['opt'].get(id(p), {})
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if k in old:
+                        v.copy_(old[k])
+                    else:
+                        v.zero_()     # created by a warm-up: "never stepped"
+            self.stats.copy_(snap['stats'])
+            self._found_inf.copy_(snap['found_inf'])
+        torch.set_rng_state(snap['cpu_rng'])
+        if 'cuda_rng' in snap:
+            torch.cuda.set_rng_state(snap['cuda_rng'], self.device)
+        self.batcher.load_state_dict(snap['sampler'])
+
     def _capture_all(self):
         """Capture every bucket's graph up front (so no capture ever lands
-        in a timed step): each is staged with a batch that fits it."""
+        in a timed step): each is staged with a batch that fits it.  The
+        warm-up iterations before each capture run real steps; their effect
+        on the model, optimizer, RNG and sampler is undone afterwards."""
+        snap = self._snapshot()
+        if hasattr(gc, 'unfreeze'):
+            gc.unfreeze()
         for i, b in enumerate(self.batchers):
             for _ in range(10000):
                 s, t = self.batcher.next_ids()
@@ -253,6 +301,7 @@ class PairTrainer(object):
                 raise RuntimeError('no batch fits bucket {}'.format(b))
             self._graphs[i].capture()
         self._captured = True
+        self._restore(snap)
         # The capture phase leaves large autograd graphs behind: collect them
         # now and move the survivors out of the collector's generations, so
         # no full collection pauses the host during the replayed steps.
@@ -312,14 +361,19 @@ class PairTrainer(object):
     def evaluate(self, store, num_pairs=1024, batch_size=None, seed=123,
                  k=(1, 10)):
         """Hits@k of ``S_L`` (fraction of ground-truth nodes) on
-        ``num_pairs`` random valid pairs of ``store``."""
+        ``num_pairs`` random valid pairs of ``store`` (the reference's test
+        loop, ``/root/reference/examples/pascal.py:80-99``).  Counts stay on
+        the device; one host synchronisation per evaluation."""
         model = self.model
         was_training = model.training
         model.eval()
         bs = batch_size or min(num_pairs, 512)
         loader = DevicePairLoader(store, bs, shuffle=True, drop_last=False,
                                   seed=seed)
-        seen, gt, hits = 0, 0, {kk: 0 for kk in k}
+        seen = 0
+        gt = torch.zeros((), dtype=torch.long, device=self.device)
+        hits = {kk: torch.zeros((), dtype=torch.long, device=self.device)
+                for kk in k}
         while seen < num_pairs:
             for batch in loader:
                 with self._autocast():
@@ -330,23 +384,28 @@ class PairTrainer(object):
                 y = torch.stack([torch.arange(batch.y.numel(),
                                               device=self.device), batch.y])
                 for kk in k:
-                    hits[kk] += model.hits_at_k(kk, S_L, y, reduction='sum')
+                    hits[kk] += model.hits_count(kk, S_L, y)
                 gt += y.size(1)
                 seen += batch.num_graphs
                 if seen >= num_pairs:
                     break
         model.train(was_training)
-        return {kk: v / max(gt, 1) for kk, v in hits.items()}
+        tot = torch.stack([gt] + [hits[kk] for kk in k]).cpu()
+        return {kk: float(tot[i + 1]) / max(float(tot[0]), 1.0)
+                for i, kk in enumerate(k)}
 
     # ------------------------------------------------------------------
     def state_dict(self):
         """Checkpoint content; every leaf is a tensor or a Python primitive
         so it loads with ``torch.load(..., weights_only=True)``."""
         np_state = np.random.get_state()
+        sampler = self.loader if self.mode == 'eager' else self.batcher
         state = {
             'model': self.model.state_dict(),
             'optimizer': self.optimizer.state_dict(),
             'step': self.step_count,
+            'sampler': sampler.state_dict(),
+            'stats': self.stats.detach().cpu(),
             'rng': {
                 'torch': torch.get_rng_state(),
                 'python': random.getstate(),
@@ -367,18 +426,48 @@ class PairTrainer(object):
             os.replace(tmp, path)
         parallel.barrier()
 
+    def _load_optimizer(self, sd):
+        """Load optimizer state; tensors that already exist are updated IN
+        PLACE (captured graphs and the HIP Adam pointer table hold their
+        addresses), missing ones are created by the regular loader."""
+        if not self.optimizer.state:
+            self.optimizer.load_state_dict(sd)
+            return
+        params = [p for g in self.optimizer.param_groups for p in g['params']]
+        ids = [i for g in sd['param_groups'] for i in g['params']]
+        with torch.no_grad():
+            for i, p in zip(ids, params):
+                src = sd['state'].get(i)
+                dst = self.optimizer.state.get(p)
+                if src is None or dst is None:
+                    continue
+                for k, v in src.items():
+                    if k in dst and torch.is_tensor(dst[k]) and \
+                            torch.is_tensor(v):
+                        dst[k].copy_(v.to(dst[k]).reshape(dst[k].shape))
+                    else:
+                        dst[k] = v
+        for g, gs in zip(self.optimizer.param_groups, sd['param_groups']):
+            for k, v in gs.items():
+                if k != 'params':
+                    g[k] = v
+
     def load(self, path):
         state = torch.load(path, map_location=self.device,
                            weights_only=True)
         self.model.load_state_dict(state['model'])
-        self.optimizer.load_state_dict(state['optimizer'])
+        self._load_optimizer(state['optimizer'])
         self.step_count = int(state.get('step', 0))
-        if getattr(self, '_graphs', None) is not None and self._captured:
-            # The optimizer state tensors were replaced: captured graphs
-            # hold their old addresses, so capture again on the next step.
-            self._graphs = [GraphedStep(self._bucket_body(i), warmup=2)
-                            for i in range(len(self.batchers))]
-            self._captured = False
+        if 'sampler' in state:
+            if self.mode == 'eager':
+                self.loader.load_state_dict(state['sampler'])
+                self._batches = self.loader.forever()
+            else:
+                self.batcher.load_state_dict(state['sampler'])
+        if 'stats' in state:
+            self.stats.copy_(state['stats'].to(self.stats))
+        # (Parameters and optimizer tensors were updated in place, so
+        # captured graphs stay valid and are replayed as they are.)
         rng = state.get('rng', {})
         if 'torch' in rng:
             torch.set_rng_state(rng['torch'].cpu())
@@ -431,6 +520,7 @@ class KGTrainer(object):
                                           fused=cuda, capturable=self.graph)
         self.last_loss = torch.zeros((), device=self.device)
         self._graphs = {}
+        self.step_count = 0
 
     def _autocast(self):
         return torch.autocast(device_type=self.device.type,
@@ -452,12 +542,90 @@ class KGTrainer(object):
     def step(self):
         self.model.train()
         if not self.graph:
-            return self._body()
+            self._body()
+            self.step_count += 1
+            return
         key = (self.model.num_steps, self.model.detach, self.model.k)
         g = self._graphs.get(key)
         if g is None:
-            g = self._graphs[key] = GraphedStep(self._body_static, warmup=2)
+            # Capture this phase; its warm-up steps are undone afterwards
+            # (same trajectory as without capturing).
+            snap = self._snapshot()
+            g = self._graphs[key] = GraphedStep(self._body_static,
+                                                warmup=2).capture()
+            self._restore(snap)
         g()
+        self.step_count += 1
+
+    def _snapshot(self):
+        with torch.no_grad():
+            snap = {'model': {k: t.detach().clone()
+                              for k, t in self.model.state_dict().items()},
+                    'opt': {id(p): {k: v.detach().clone()
+                                    for k, v in st.items()
+                                    if torch.is_tensor(v)}
+                            for p, st in self.optimizer.state.items()},
+                    'loss': self.last_loss.clone(),
+                    'cpu_rng': torch.get_rng_state()}
+        if self.device.type == 'cuda':
+            snap['cuda_rng'] = torch.cuda.get_rng_state(self.device)
+        return snap
+
+    def _restore(self, snap):
+        with torch.no_grad():
+            for k, t in self.model.state_dict().items():
+                t.copy_(snap['model'][k])
+            for p, st in self.optimizer.state.items():
+                old = snap['opt'].get(id(p), {})
+                for k, v in st.items():
+                    if torch.is_tensor(v):
+                        if k in old:
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
+            self.last_loss.copy_(snap['loss'])
+        torch.set_rng_state(snap['cpu_rng'])
+        if 'cuda_rng' in snap:
+            torch.cuda.set_rng_state(snap['cuda_rng'], self.device)
+
+    def state_dict(self):
+        """Checkpoint: model (reference key schema), optimizer, step count,
+        schedule knobs (``num_steps`` / ``detach``, ``dbp15k.py:64-69``) and
+        RNG states; loads with ``torch.load(..., weights_only=True)``."""
+        state = {'model': self.model.state_dict(),
+                 'optimizer': self.optimizer.state_dict(),
+                 'step': self.step_count,
+                 'schedule': {'num_steps': self.model.num_steps,
+                              'detach': bool(self.model.detach),
+                              'k': int(self.model.k)},
+                 'rng': {'torch': torch.get_rng_state()}}
+        if self.device.type == 'cuda':
+            state['rng']['cuda'] = torch.cuda.get_rng_state(self.device)
+        return state
+
+    def save(self, path):
+        if parallel.rank() == 0:
+            tmp = path + '.tmp'
+            torch.save(self.state_dict(), tmp)
+            os.replace(tmp, path)
+        parallel.barrier()
+
+    def load(self, path):
+        state = torch.load(path, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(state['model'])
+        PairTrainer._load_optimizer(self, state['optimizer'])
+        self.step_count = int(state.get('step', 0))
+        sch = state.get('schedule', {})
+        if sch:
+            self.model.num_steps = sch['num_steps']
+            self.model.detach = sch['detach']
+            self.model.k = sch['k']
+        rng = state.get('rng', {})
+        if 'torch' in rng:
+            torch.set_rng_state(rng['torch'].cpu())
+        if 'cuda' in rng and self.device.type == 'cuda':
+            torch.cuda.set_rng_state(rng['cuda'].cpu(), self.device)
+        return state
 
     def _body_static(self):
         d, model = self.data, self.model

@@ -31,6 +31,10 @@ parser.add_argument('--k', type=int, default=10)
 parser.add_argument('--epochs', type=int, default=200)
 parser.add_argument('--scale', type=float, default=1.0)
 parser.add_argument('--no_graph', action='store_true')
+parser.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                    help='fp32 = reference precision')
+parser.add_argument('--checkpoint', default=None,
+                    help='save / resume the trainer state here')
 args = parser.parse_args()
 
 device = 'cuda' if torch.cuda.is_available() else 'cpu'
@@ -41,17 +45,25 @@ psi_1 = RelCNN(data.x1.size(-1), args.dim, args.num_layers, batch_norm=False,
 psi_2 = RelCNN(args.rnd_dim, args.rnd_dim, args.num_layers, batch_norm=False,
                cat=True, lin=True, dropout=0.0)
 model = DGMC(psi_1, psi_2, num_steps=None, k=args.k).to(device)
-trainer = KGTrainer(model, data, lr=0.001, graph=not args.no_graph)
+trainer = KGTrainer(model, data, lr=0.001, graph=not args.no_graph,
+                    bf16=args.dtype == 'bf16')
+start = 1
+if args.checkpoint and osp.exists(args.checkpoint):
+    trainer.load(args.checkpoint)
+    start = trainer.step_count + 1
 
 print('Optimize initial feature matching...')
-model.num_steps = 0
 half = args.epochs // 2
-for epoch in range(1, args.epochs + 1):
+if start <= half:
+    model.num_steps = 0
+for epoch in range(start, args.epochs + 1):
     if epoch == half + 1:
         print('Refine correspondence matrix...')
         model.num_steps = args.num_steps
         model.detach = True
     trainer.step()
+    if args.checkpoint:
+        trainer.save(args.checkpoint)
     if epoch % 10 == 0 or epoch > half:
         hits1, hits10 = trainer.evaluate()
         loss = float(trainer.last_loss)

@@ -5,7 +5,7 @@ PascalVOC-shaped keypoint graphs (20 categories, Delaunay + Cartesian/
 Distance), trained with the HBM-resident loader and (on GPU) a
 hipGraph-captured step.  Multi-GPU: launch with torch.distributed.run.
 
-    python examples/pascal.py [--epochs 15] [--batch_size 512]
+    python examples/pascal.py [--epochs 15] [--batch_size 512] [--dtype fp32]
 """
 import argparse
 import os.path as osp
@@ -41,6 +41,9 @@ parser.add_argument('--normalization', default='softmax',
                     choices=['softmax', 'sinkhorn'],
                     help='extension: Sinkhorn instead of the reference '
                          'row softmax (dense path)')
+parser.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                    help='fp32 = reference precision; bf16 = encoder GEMMs '
+                         'under autocast')
 parser.add_argument('--checkpoint', default=None)
 parser.add_argument('--log', default=None, help='JSONL metrics file')
 args = parser.parse_args()
@@ -52,7 +55,8 @@ train_groups = make_keypoint_datasets(PASCAL_VOC_CATEGORIES, args.graphs,
 test_groups = make_keypoint_datasets(PASCAL_VOC_CATEGORIES,
                                      max(args.graphs // 4, 8),
                                      transform=transform, split='test')
-dtype = torch.bfloat16 if device.type == 'cuda' else torch.float32
+bf16 = args.dtype == 'bf16' and device.type == 'cuda'
+dtype = torch.bfloat16 if bf16 else torch.float32
 store = GraphStore(train_groups, device, x_dtype=dtype)
 test_stores = [GraphStore([g], device, x_dtype=dtype) for g in test_groups]
 
@@ -65,7 +69,8 @@ psi_2 = SplineCNN(args.rnd_dim, args.rnd_dim, num_edge_features,
 model = DGMC(psi_1, psi_2, num_steps=args.num_steps,
              normalization=args.normalization).to(device)
 mode = args.mode or ('graph' if device.type == 'cuda' else 'eager')
-trainer = PairTrainer(model, store, args.batch_size, lr=args.lr, mode=mode)
+trainer = PairTrainer(model, store, args.batch_size, lr=args.lr, mode=mode,
+                      bf16=bf16)
 logger = MetricsLogger(args.log)
 if args.checkpoint and osp.exists(args.checkpoint):
     trainer.load(args.checkpoint)

@@ -30,6 +30,9 @@ parser.add_argument('--lr', type=float, default=0.001)
 parser.add_argument('--batch_size', type=int, default=64)
 parser.add_argument('--epochs', type=int, default=32)
 parser.add_argument('--test_pairs', type=int, default=256)
+parser.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'],
+                    help='fp32 = reference precision; bf16 = encoder GEMMs '
+                         'under autocast')
 args = parser.parse_args()
 
 transform = pascal_pf_transform()
@@ -47,6 +50,13 @@ model = DGMC(psi_1, psi_2, num_steps=args.num_steps).to(device)
 optimizer = torch.optim.Adam(model.parameters(), lr=args.lr)
 
 
+def autocast():
+    return torch.autocast(device_type='cuda' if device == 'cuda' else 'cpu',
+                          dtype=torch.bfloat16,
+                          enabled=args.dtype == 'bf16' and device == 'cuda',
+                          cache_enabled=False)
+
+
 def train():
     model.train()
     total_loss = torch.zeros((), device=device)
@@ -55,9 +65,10 @@ def train():
     for data in train_loader:
         optimizer.zero_grad()
         data = data.to(device)
-        S_0, S_L = model(data.x_s, data.edge_index_s, data.edge_attr_s,
-                         data.x_s_batch, data.x_t, data.edge_index_t,
-                         data.edge_attr_t, data.x_t_batch)
+        with autocast():
+            S_0, S_L = model(data.x_s, data.edge_index_s, data.edge_attr_s,
+                             data.x_s_batch, data.x_t, data.edge_index_t,
+                             data.edge_attr_t, data.x_t_batch)
         y = torch.stack([data.y_index_s, data.y_t], dim=0)
         loss = model.loss(S_0, y)
         loss = model.loss(S_L, y) + loss if model.num_steps > 0 else loss
@@ -75,8 +86,10 @@ def test():
     correct = num_examples = 0
     for i in range(len(test_dataset)):
         pair = test_dataset[i].to(device)
-        _, S_L = model(pair.x_s, pair.edge_index_s, pair.edge_attr_s, None,
-                       pair.x_t, pair.edge_index_t, pair.edge_attr_t, None)
+        with autocast():
+            _, S_L = model(pair.x_s, pair.edge_index_s, pair.edge_attr_s,
+                           None, pair.x_t, pair.edge_index_t,
+                           pair.edge_attr_t, None)
         y = torch.stack([pair.y_index_s, pair.y_t], dim=0)
         correct += model.acc(S_L, y, reduction='sum')
         num_examples += y.size(1)

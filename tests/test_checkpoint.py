@@ -1,4 +1,5 @@
 """Checkpoint schema (reference state-dict keys) and trainer resume."""
+import pytest
 import torch
 
 from deep_graph_matching_consensus_amd.datasets import (
@@ -76,3 +77,88 @@ def test_trainer_checkpoint_resume(tmp_path):
     sb = b.optimizer.state_dict()['state']
     for i in sa:
         assert torch.equal(sa[i]['exp_avg'], sb[i]['exp_avg'])
+
+
+def _pair_trainer(store, mode, seed_model=0):
+    torch.manual_seed(seed_model)
+    model = DGMC(SplineCNN(16, 16, 2, 2, cat=False, dropout=0.5),
+                 SplineCNN(8, 8, 2, 2, cat=True), num_steps=2)
+    return PairTrainer(model, store, 8, mode=mode, bf16=False, seed=3)
+
+
+def _run_trajectory(trainer, steps):
+    losses = []
+    for _ in range(steps):
+        trainer.step()
+        losses.append(trainer.read_stats()['loss_sum'])
+    return losses
+
+
+@pytest.mark.parametrize('mode', ['eager', 'static'])
+def test_interrupted_run_continues_bit_for_bit(tmp_path, mode):
+    """Save after 2 of 5 steps, resume in a fresh process-like trainer (other
+    init): losses of steps 3-5 and the final weights / Adam moments equal the
+    uninterrupted run bit for bit (model, optimizer, RNG AND sampler state
+    are in the checkpoint)."""
+    groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=5)
+    store = GraphStore(groups, 'cpu')
+    torch.manual_seed(123)
+    full = _pair_trainer(store, mode)
+    ref_losses = _run_trajectory(full, 5)
+
+    torch.manual_seed(123)
+    first = _pair_trainer(store, mode)
+    assert _run_trajectory(first, 2) == ref_losses[:2]
+    path = str(tmp_path / 'ckpt.pt')
+    first.save(path)
+    torch.manual_seed(999)                  # a different process state
+    resumed = _pair_trainer(store, mode, seed_model=7)
+    resumed.load(path)
+    assert resumed.step_count == 2
+    assert _run_trajectory(resumed, 3) == ref_losses[2:]
+    for (k, v), w in zip(full.model.state_dict().items(),
+                         resumed.model.state_dict().values()):
+        assert torch.equal(v, w), k
+    sa = full.optimizer.state_dict()['state']
+    sb = resumed.optimizer.state_dict()['state']
+    for i in sa:
+        assert torch.equal(sa[i]['exp_avg_sq'], sb[i]['exp_avg_sq'])
+
+
+def test_kg_trainer_checkpoint_resume(tmp_path):
+    from deep_graph_matching_consensus_amd.datasets.kg import make_kg_pair
+    from deep_graph_matching_consensus_amd.train import KGTrainer
+    data = make_kg_pair('zh_en', scale=0.01, seed=0)
+
+    def make(seed):
+        torch.manual_seed(seed)
+        psi_1 = RelCNN(data.x1.size(-1), 16, 2, cat=True, lin=True,
+                       dropout=0.5)
+        psi_2 = RelCNN(8, 8, 2, cat=True, lin=True)
+        model = DGMC(psi_1, psi_2, num_steps=None, k=4)
+        return KGTrainer(model, data, lr=1e-3, graph=False)
+
+    def run(tr, steps):
+        out = []
+        for _ in range(steps):
+            tr.step()
+            out.append(float(tr.last_loss))
+        return out
+
+    torch.manual_seed(1)
+    full = make(0)
+    full.model.num_steps, full.model.detach = 2, True
+    ref = run(full, 4)
+    torch.manual_seed(1)
+    a = make(0)
+    a.model.num_steps, a.model.detach = 2, True
+    assert run(a, 2) == ref[:2]
+    path = str(tmp_path / 'kg.pt')
+    a.save(path)
+    b = make(5)
+    b.load(path)
+    assert b.step_count == 2 and b.model.num_steps == 2 and b.model.detach
+    assert run(b, 2) == ref[2:]
+    for (k, v), w in zip(full.model.state_dict().items(),
+                         b.model.state_dict().values()):
+        assert torch.equal(v, w), k
