@@ -221,7 +221,7 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
 // dependent global round trips otherwise dominates.
 // ---------------------------------------------------------------------------
 template <bool TRANS_W>
-__global__ __launch_bounds__(kSgThreads, 3) void slot_gemm_kernel(
+__global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
     const float* __restrict__ X, const int* __restrict__ src,
     const int* __restrict__ seg, int S, const float* __restrict__ weight,
     const float* __restrict__ root, int nw, int K, int Nn,
@@ -398,9 +398,13 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
   if (trans_w) TORCH_CHECK(X.size(0) == P, "slot_gemm: dY_c rows == P_cap");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   at::Tensor Y = at::empty({P, Nn}, X.options());
-  // Persistent grid: 3 resident workgroups per CU (VGPR-limited).
-  const int64_t blocks = std::min<int64_t>((P / kSgBM) * (Nn / kSgBN),
-                                           3 * num_cus(X.device().index()));
+  // Persistent grid: resident workgroups per CU (VGPR-limited: 2).
+  static const int per_cu = [] {
+    const char* e = std::getenv("DGMC_SG_PER_CU");
+    return e ? std::max(1, atoi(e)) : 2;
+  }();
+  const int64_t blocks = std::min<int64_t>(
+      (P / kSgBM) * (Nn / kSgBN), (int64_t)per_cu * num_cus(X.device().index()));
   if (blocks == 0) return Y;
   const float* rp = has_root ? root->data_ptr<float>() : nullptr;
   if (trans_w)
@@ -631,6 +635,8 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(
   // Tiles: 32 p-rows x 128 columns, 4 float4 per thread (32 lanes per row:
   // rows (tid >> 5) + 8 i).  The gather indices of chunk q + 1 are loaded
   // one chunk ahead, so a chunk's row loads never wait on their index load.
+  // (A second register set, loading rows two chunks ahead, measured slower:
+  // 485 vs 471 us for psi_2's 10-use gradient, tools/bench_slot_gemm.py.)
   float4 ra[4], rb[4];
   const int nchunk = (pe - pb) / kSgBK;
   const int total = nchunk * nu;

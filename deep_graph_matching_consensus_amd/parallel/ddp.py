@@ -15,6 +15,16 @@ Design for MI355X / RCCL over xGMI (each GPU has 7 point-to-point links):
   is used on RCCL, SUM+scale on gloo);
 * parameters and buffers are broadcast from rank 0 at construction.
 
+Static / hipGraph steps (``in_step=True``) let AccumulateGrad *steal* each
+fresh gradient instead of accumulating into the flat views: the hook of the
+parameter that completes a bucket packs that bucket into its flat range (one
+multi-tensor kernel) and launches its all-reduce right away, so on RCCL the
+whole data-parallel step - backward, bucketed all-reduces overlapping the
+rest of the backward, the non-finite check and Adam - is ONE captured
+hipGraph.  Gloo (CPU tensors or the multi-rank rehearsal on one GPU) cannot
+be captured: there the step packs all gradients and the trainer runs one
+flat all-reduce after the replay.
+
 With a single process every call is a no-op, so the same training loop runs
 on 1..8 GPUs.
 """
@@ -39,14 +49,17 @@ class GradBucketAllReducer(object):
     """
 
     def __init__(self, module, bucket_bytes=8 << 20, overlap=True,
-                 process_group=None):
+                 process_group=None, in_step=False):
         self.module = module
         self.group = process_group
         self.params = [p for p in module.parameters() if p.requires_grad]
         self.distributed = is_distributed()
         self.world = dist.get_world_size(process_group) \
             if self.distributed else 1
-        self.overlap = overlap and self.distributed
+        # in_step: stolen gradients, buckets packed + all-reduced from the
+        # backward hooks inside the (captured) step.
+        self.in_step = bool(in_step) and self.distributed
+        self.overlap = (overlap or self.in_step) and self.distributed
         dev = self.params[0].device if self.params else torch.device('cpu')
         # Every gradient view starts on a 16-byte boundary (vectorised
         # optimizer / finiteness kernels); the padding stays zero.
@@ -169,10 +182,35 @@ class GradBucketAllReducer(object):
                                    group=self.group, async_op=True)
             self._works.append((work, buf))
 
+    def _pack_bucket(self, bi):
+        """Copy bucket ``bi``'s stolen gradients into its flat range (one
+        kernel; zeros for parameters without a gradient) and re-bind their
+        ``p.grad`` to the flat views."""
+        from ..ops import _backend
+        bucket = self.buckets[bi]
+        views = [self.flat[o:o + n].view_as(p)
+                 for p, (o, n) in ((p, self._slot[p]) for p in bucket)]
+        grads = [p.grad for p in bucket]
+        if _backend.use_hip(self.flat) and all(
+                g is None or (g.dtype == torch.float32 and g.is_cuda and
+                              g.is_contiguous() and g.data_ptr() % 16 == 0)
+                for g in grads):
+            _backend.ops().pack_grads(grads, views, False)
+        else:
+            for g, v in zip(grads, views):
+                if g is None:
+                    v.zero_()
+                elif g.data_ptr() != v.data_ptr():
+                    v.copy_(g)
+        for p, v in zip(bucket, views):
+            p.grad = v
+
     def _on_grad(self, p):
         bi = self._bucket_of[p]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
+            if self.in_step:
+                self._pack_bucket(bi)
             self._launch(bi)
 
     def finish(self):
@@ -188,6 +226,8 @@ class GradBucketAllReducer(object):
             launched = {i for i, c in enumerate(self._pending) if c == 0}
             for bi in range(len(self.buckets)):
                 if bi not in launched:
+                    if self.in_step:
+                        self._pack_bucket(bi)
                     self._launch(bi)
         for work, buf in self._works:
             work.wait()

@@ -43,6 +43,10 @@ STEAL_GRADS = os.environ.get('DGMC_AMD_STEAL_GRADS', '1') == '1'
 # queues and serialised them against the psi_1 backward in our measurements
 # (169.5k vs 170.6k pairs/s same-box), so there is no gain to take yet.
 SIDE_STREAMS = os.environ.get('DGMC_AMD_SIDE_STREAMS', '0') == '1'
+# Data-parallel gradient all-reduce inside the (captured) step, overlapped
+# with the backward (DGMC_AMD_IN_STEP_ALLREDUCE=0: one flat all-reduce after
+# the step).
+IN_STEP_ALLREDUCE = os.environ.get('DGMC_AMD_IN_STEP_ALLREDUCE', '1') == '1'
 
 
 class PairTrainer(object):
@@ -57,6 +61,7 @@ class PairTrainer(object):
         bf16 (bool): bf16 autocast for the encoder GEMMs.
         seed (int): data-order seed (offset by rank).
         overlap (bool): overlap gradient all-reduce with backward (eager).
+        bucket_bytes (int): data-parallel all-reduce bucket size.
         guard_nonfinite (bool): skip the optimizer update of any step whose
             (all-reduced) gradients contain NaN/Inf - on the device, inside
             the captured graph, via the fused Adam ``found_inf`` input; the
@@ -65,7 +70,7 @@ class PairTrainer(object):
 
     def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
                  bf16=True, seed=0, overlap=True, sources=None,
-                 guard_nonfinite=True, buckets=True):
+                 guard_nonfinite=True, buckets=True, bucket_bytes=8 << 20):
         self.model = model
         self.store = store
         self.device = store.device
@@ -76,8 +81,17 @@ class PairTrainer(object):
         self.bf16 = bf16 and self.device.type == 'cuda'
         if sources is None:
             sources = np.arange(store.num_graphs)[self.rank::self.world]
+        # Data parallel, static / graph modes: bucketed all-reduces from the
+        # backward hooks INSIDE the step (captured with it on RCCL), unless
+        # the backend cannot be captured (gloo: one all-reduce after the
+        # replay) - see parallel/ddp.py.
+        in_step = (mode == 'static' or mode == 'graph' and
+                   parallel.is_distributed() and
+                   torch.distributed.get_backend() == 'nccl') and \
+            STEAL_GRADS and IN_STEP_ALLREDUCE
         self.reducer = parallel.GradBucketAllReducer(
-            model, overlap=overlap and mode == 'eager')
+            model, bucket_bytes=bucket_bytes,
+            overlap=overlap and mode == 'eager', in_step=in_step)
         cuda = self.device.type == 'cuda'
         if cuda:
             use_tuned_gemms()     # measured GEMM solutions (runtime/tuning.py)
@@ -205,6 +219,14 @@ class PairTrainer(object):
         with streams.side_streams(SIDE_STREAMS and STEAL_GRADS and
                                   self.device.type == 'cuda'):
             self._forward_backward(batch, self._rows[bucket], batch.y_mask)
+        if self.reducer.in_step:
+            # DP: the buckets were packed and all-reduced from the backward
+            # hooks; wait for the last ones, then check and update - all
+            # inside the step (and its hipGraph).
+            self.reducer.finish()
+            self._check_finite()
+            self._optimizer_step()
+            return
         flags = None
         if STEAL_GRADS:
             # Single process: the pack kernel also flags non-finite
@@ -335,7 +357,7 @@ class PairTrainer(object):
                     self._graphs[bucket]()
                 else:
                     self._static_body(bucket)
-            if self.world > 1:
+            if self.world > 1 and not self.reducer.in_step:
                 with trace_range('train.allreduce'):
                     self.reducer.finish()
                 with trace_range('train.optimizer'):
