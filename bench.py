@@ -29,7 +29,6 @@ host syncs) used as the BASELINE.md denominator.
 """
 import argparse
 import json
-import os
 import os.path as osp
 import sys
 import time

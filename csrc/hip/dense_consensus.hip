@@ -1439,14 +1439,10 @@ static size_t pair_lds(K kern, size_t floats) {
 // Compile-time-width step kernels (pair_step_fwd/bwd_kernel): R in
 // {32, 64, 128}, 16-byte aligned operand rows of ONE storage type (bf16 under
 // autocast, fp32 at reference precision), aligned fp32 b1 / w2.
-// DGMC_PAIR_FAST=0 selects the generic kernels (A/B switch).
+// Other widths / alignments use the generic kernels.
 static bool fast_step_ok(int R, std::initializer_list<const at::Tensor*> rows,
                          std::initializer_list<const void*> vecs = {}) {
-  static const bool enabled = [] {
-    const char* e = std::getenv("DGMC_PAIR_FAST");
-    return !(e && e[0] == '0');
-  }();
-  if (!enabled || !(R == 32 || R == 64 || R == 128)) return false;
+  if (!(R == 32 || R == 64 || R == 128)) return false;
   const at::ScalarType st = (*rows.begin())->scalar_type();
   if (st != at::kBFloat16 && st != at::kFloat) return false;
   for (const at::Tensor* t : rows)

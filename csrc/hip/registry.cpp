@@ -122,14 +122,6 @@ at::Tensor nll_bwd(const at::Tensor& grad, const at::Tensor& S,
                    double eps, bool mean);
 void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,
                     const c10::optional<at::Tensor>& counter);
-at::Tensor gather_gemm(const at::Tensor& X, const at::Tensor& srp,
-                       const at::Tensor& ecol, const at::Tensor& eval,
-                       const at::Tensor& W, int64_t ss, int64_t sn,
-                       int64_t num_slots, int64_t M,
-                       const c10::optional<at::Tensor>& bias, bool relu,
-                       at::ScalarType out_dtype,
-                       const c10::optional<at::Tensor>& Z);
-at::Tensor gather_gemm_stamps();
 at::Tensor slot_conv_stamps();
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fold_weights(
     const at::Tensor& w1, const at::Tensor& wf);
@@ -240,6 +232,13 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
                           int64_t chunk);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
+    const at::Tensor& S_hat, const at::Tensor& n_s, const at::Tensor& n_t,
+    int64_t iters, double tau);
+at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
+                        const at::Tensor& n_s, const at::Tensor& n_t,
+                        const at::Tensor& a_hist, const at::Tensor& b_hist,
+                        int64_t iters, double tau);
 
 }  // namespace dgmc
 
@@ -307,11 +306,6 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "int root_slot, Tensor(a!) rowptr, Tensor(b!) col, Tensor(c!) val, "
       "Tensor(d!) trowptr, Tensor(e!) tcol, Tensor(f!) tval, Tensor(g!)? "
       "gflag=None, Tensor? st_row=None, Tensor(h!)? row_out=None) -> ()");
-  m.def(
-      "gather_gemm(Tensor X, Tensor srp, Tensor ecol, Tensor eval, Tensor W, "
-      "int ss, int sn, int num_slots, int M, Tensor? bias, bool relu, "
-      "ScalarType out_dtype, Tensor(a!)? Z=None) -> Tensor");
-  m.def("gather_gemm_stamps() -> Tensor");
   m.def("slot_conv_stamps() -> Tensor");
   m.def("fold_weights(Tensor w1, Tensor wf) -> (Tensor, Tensor, Tensor)");
   m.def("dense_wgrad(Tensor[] xs, Tensor[] gs, int nsplit) -> Tensor");
@@ -326,7 +320,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "adam_multi(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, "
       "Tensor(c!)[] exp_avg_sq, Tensor[] steps, Tensor? found_inf, float lr, "
       "float beta1, float beta2, float eps, float weight_decay) -> ()");
-  m.def("adam_step_inc(Tensor(a!)[] steps, Tensor(b!)? found_inf, Tensor? flags=None, Tensor(c!)? skips=None) -> ()");
+  m.def(
+      "adam_step_inc(Tensor(a!)[] steps, Tensor(b!)? found_inf, "
+      "Tensor? flags=None, Tensor(c!)? skips=None) -> ()");
   m.def(
       "spline_weight_pack(Tensor weight, Tensor? root, ScalarType dtype) -> "
       "Tensor");
@@ -416,10 +412,15 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "slot_wgrad_f32(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
       "chunk) -> Tensor");
+  m.def(
+      "sinkhorn_fwd(Tensor S_hat, Tensor n_s, Tensor n_t, int iters, float "
+      "tau) -> (Tensor, Tensor, Tensor)");
+  m.def(
+      "sinkhorn_bwd(Tensor grad, Tensor S_hat, Tensor n_s, Tensor n_t, Tensor "
+      "a_hist, Tensor b_hist, int iters, float tau) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
-  m.impl("gather_gemm_stamps", &dgmc::gather_gemm_stamps);
   m.impl("slot_conv_stamps", &dgmc::slot_conv_stamps);
 }
 
@@ -445,7 +446,6 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("nll_bwd", &dgmc::nll_bwd);
   m.impl("nonfinite_flag", &dgmc::nonfinite_flag);
   m.impl("assemble_slot_plan", &dgmc::assemble_slot_plan);
-  m.impl("gather_gemm", &dgmc::gather_gemm);
   m.impl("slot_conv", &dgmc::slot_conv);
   m.impl("slot_tile_plan", &dgmc::slot_tile_plan);
   m.impl("slot_wgrad", &dgmc::slot_wgrad);
@@ -480,4 +480,6 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);
+  m.impl("sinkhorn_fwd", &dgmc::sinkhorn_fwd);
+  m.impl("sinkhorn_bwd", &dgmc::sinkhorn_bwd);
 }

@@ -750,25 +750,6 @@ at::Tensor slot_conv_stamps() {
   return t;
 }
 
-// DGMC_SC_DEBUG ablations (tools/bench_slot_conv.py): 1 = no W streaming,
-// 4 = no A-tile scatter, 8 = wall-clock stamps.
-static int sc_debug() {
-  static int v = [] {
-    const char* e = getenv("DGMC_SC_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// DGMC_SC_WS=0 selects the 8-wave kernel without wave specialisation.
-static bool sc_ws() {
-  static bool v = [] {
-    const char* e = getenv("DGMC_SC_WS");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
 struct ScBwdFuse {          // fused ReLU/bias backward (ws kernel only)
   int ldx = kScC;
   const __hip_bfloat16* mask = nullptr;
@@ -785,8 +766,10 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                              const __hip_bfloat16* add, int ldadd,
                              const ScBwdFuse& fz = ScBwdFuse()) {
   const int T = tiles.size(0);
+  // Wave-specialised kernel for every pass; the 8-wave kernel only for the
+  // transposed pass that also writes dY = A^T G (WRITE_Z).
   if constexpr (!WRITE_Z) {
-    if (sc_ws()) {
+    {
       auto kw = slot_conv_ws_kernel<TRANS, TOUT>;
       static bool ws_attr = false;
       if (!ws_attr) {
@@ -826,7 +809,7 @@ static void launch_slot_conv(const at::Tensor& X, const at::Tensor& tiles,
                      reinterpret_cast<const __hip_bfloat16*>(Wimg.data_ptr()),
                      bias, relu ? 1 : 0,
                      reinterpret_cast<TOUT*>(out.data_ptr()), Z, add, ldadd,
-                     sc_debug());
+                     0);
 }
 
 // flag [N] uint8 (1 = graph start); rowptr [N+1] / col / val: CSR of A with
@@ -970,8 +953,6 @@ at::Tensor slot_conv(const at::Tensor& X, const at::Tensor& tiles,
 //   g_out <- g'  (bf16 [N, 128] contiguous, the weight gradient's operand)
 //   bias_part[t] <- sum of g' over tile t's rows (fp32 [T, 128], optional)
 //   returns dX = sum_k (A_k^T g') W_k^T (+ addend)
-// Without the wave-specialised kernel (DGMC_SC_WS=0) the prologue runs as
-// ATen ops before the plain transposed pass.
 at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                               const c10::optional<at::Tensor>& relu_out,
                               const at::Tensor& tiles, const at::Tensor& soff,
@@ -1004,19 +985,6 @@ at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                     bias_part->is_contiguous() &&
                     bias_part->numel() == tiles.size(0) * kScC,
                 "slot_conv_relu_bwd: bias_part fp32 [T, 128]");
-  if (!sc_ws()) {
-    at::Tensor g = has_mask ? at::where(relu_out->gt(0), G,
-                                        at::zeros({}, G.options()))
-                            : G;
-    g_out.view({N, kScC}).copy_(g);
-    if (has_bp) {
-      bias_part->zero_();
-      bias_part->view({-1, kScC})[0].copy_(g.to(at::kFloat).sum(0));
-    }
-    return slot_conv(g_out.view({N, kScC}), tiles, soff, ecode, eval, S, Wimg,
-                     true, c10::nullopt, false, out_dtype, c10::nullopt,
-                     addend);
-  }
   // Same checks as slot_conv for the shared operands (X validated above).
   TORCH_CHECK(tiles.scalar_type() == at::kInt && tiles.dim() == 2 &&
                   tiles.size(1) == 4 && tiles.is_contiguous(),
@@ -1057,20 +1025,8 @@ at::Tensor slot_conv_relu_bwd(const at::Tensor& G,
                 ? reinterpret_cast<const __hip_bfloat16*>(relu_out->data_ptr())
                 : nullptr;
   fz.gout = reinterpret_cast<__hip_bfloat16*>(g_out.data_ptr());
-  {
-    // Ablation knob (tools/sc_fz_ablation.sh; results timing-only, NOT
-    // numerically valid): bit 0 drops the g' stores, bit 1 the ReLU mask,
-    // bit 2 the bias partials.  Measured per transposed call: 25.9 us fused
-    // vs 23.6 + 5.4 us (slot conv + relu_bias_bwd) unfused; the g' stores
-    // cost 1.2 us (the prologue's __syncthreads waits for them).
-    static int abl = [] {
-      const char* e = getenv("DGMC_SC_FZ_ABL");
-      return e ? atoi(e) : 0;
-    }();
-    if (abl & 1) fz.gout = nullptr;
-    if (abl & 2) fz.mask = nullptr;
-    if (abl & 4) fz.bpart = nullptr;
-  }
+  // (Measured per transposed call: 25.9 us fused vs 23.6 + 5.4 us slot conv
+  // + relu_bias_bwd unfused; docs/performance.md.)
   fz.bpart = has_bp ? bias_part->data_ptr<float>() : nullptr;
   if (out_dtype == at::kFloat)
     launch_slot_conv<true, false, float>(G, tiles, soff, ecode, eval, (int)S,

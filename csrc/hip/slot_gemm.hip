@@ -398,13 +398,11 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
   if (trans_w) TORCH_CHECK(X.size(0) == P, "slot_gemm: dY_c rows == P_cap");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   at::Tensor Y = at::empty({P, Nn}, X.options());
-  // Persistent grid: resident workgroups per CU (VGPR-limited: 2).
-  static const int per_cu = [] {
-    const char* e = std::getenv("DGMC_SG_PER_CU");
-    return e ? std::max(1, atoi(e)) : 2;
-  }();
+  // Persistent grid: 2 resident workgroups per CU (VGPR-limited; measured
+  // with 1 / 2 / 3 per CU: psi_2 70.8 / 56.6 / 74.7 us, the third one only
+  // starts when others finish - tools/bench_slot_gemm.py).
   const int64_t blocks = std::min<int64_t>(
-      (P / kSgBM) * (Nn / kSgBN), (int64_t)per_cu * num_cus(X.device().index()));
+      (P / kSgBM) * (Nn / kSgBN), 2 * (int64_t)num_cus(X.device().index()));
   if (blocks == 0) return Y;
   const float* rp = has_root ? root->data_ptr<float>() : nullptr;
   if (trans_w)

@@ -389,13 +389,9 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   if (rank < k) out[row * k + rank] = mj < Nt ? mj : 0;
 }
 
-static int topk_debug() {  // DGMC_TOPK_DEBUG: 1 skip selection, 2 skip MFMA
-  static int v = [] {
-    const char* e = getenv("DGMC_TOPK_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// (The kernels' dbg argument - 1 skip selection, 2 skip MFMA - is a
+// diagnostic-build ablation knob; production launches pass 0.)
+static int topk_debug() { return 0; }
 
 // Target splits for the bf16x3 kernel: the smallest S whose blocks fill the
 // 2-blocks-per-CU slots of the chip to >= 85% (a partial last wave of blocks

@@ -1,7 +1,9 @@
 """Command line entry point with presets for the BASELINE configurations.
 
-    python -m deep_graph_matching_consensus_amd.cli train --preset pascal [flags]
-    python -m deep_graph_matching_consensus_amd.cli bench --preset willow [flags]
+    python -m deep_graph_matching_consensus_amd.cli train --preset pascal \
+        [flags]
+    python -m deep_graph_matching_consensus_amd.cli bench --preset willow \
+        [flags]
     python -m deep_graph_matching_consensus_amd.cli list
 
 ``train`` runs the matching example driver (``examples/<preset>.py``, the

@@ -2,7 +2,8 @@
 
 The reference iterates a ``DataLoader(ValidPairDataset(..., sample=True))``
 and collates every batch in Python on the host, then copies the 40 MB of
-1024-d features of a 512-pair batch over PCIe (``examples/pascal.py:42,64-66``).
+1024-d features of a 512-pair batch over PCIe
+(``examples/pascal.py:42,64-66``).
 On MI355X the synthetic (or pre-processed) dataset is small next to 288 GB of
 HBM, so :class:`DevicePairLoader` keeps node features and edge attributes
 resident on the device.  Per step the host:

@@ -20,7 +20,6 @@ the dense grid, carry only self-loop padded edges, and are masked out of the
 loss/metrics.  Batches that exceed a capacity (vanishingly rare with the 6
 sigma headroom) are reported so the caller can run that step eagerly.
 """
-import os
 
 import numpy as np
 import torch
@@ -99,12 +98,6 @@ class StaticPairBatcher(object):
         self._slot = 0
         self.buf = torch.zeros(self.words, dtype=torch.long,
                                device=self.device)
-        # Device staging buffer: the host->device copy of batch n + 1 runs on
-        # a copy stream while step n executes; the step's stream then only
-        # copies stage -> buf (device to device) before its replay.
-        self._stage = torch.zeros_like(self.buf) \
-            if pin and STAGE_COPY else None
-        self._d2d_done = None
         self._views()
         self.batch_s = torch.zeros(cs, dtype=torch.long, device=self.device)
         self.batch_t = torch.zeros(ct, dtype=torch.long, device=self.device)
@@ -223,8 +216,11 @@ class StaticPairBatcher(object):
                                  self.B, self.B, len(s_ids), len(t_ids)))
         slot = self._slot
         self._slot ^= 1
-        wait = self._events[slot] if HOST_AHEAD >= 2 else \
-            self._events[slot ^ 1]
+        # The host stages at most one batch ahead of the device: wait for
+        # the previous batch's copy (i.e. the step before it) before
+        # collating this one (measured faster than two ahead, which lets
+        # the host queue deeper: 179.5k vs 178.7k pairs/s same-box).
+        wait = self._events[slot ^ 1]
         if wait is not None:
             wait.synchronize()
         host = self._host[slot]
@@ -239,29 +235,11 @@ class StaticPairBatcher(object):
         if not ok:
             self.overflows += 1
             return False
-        if self._stage is None:
-            self.buf.copy_(host, non_blocking=True)
-            if self.device.type == 'cuda':
-                ev = torch.cuda.Event()
-                ev.record()
-                self._events[slot] = ev    # guards the pinned host slot
-            return True
-        # H2D into the staging buffer on the copy stream (overlapping the
-        # step in flight), once the previous stage -> buf copy has read it.
-        cstream = _copy_stream(self.device)
-        if self._d2d_done is not None:
-            cstream.wait_event(self._d2d_done)
-        with torch.cuda.stream(cstream):
-            self._stage.copy_(host, non_blocking=True)
+        self.buf.copy_(host, non_blocking=True)
+        if self.device.type == 'cuda':
             ev = torch.cuda.Event()
-            ev.record(cstream)
-        self._events[slot] = ev        # guards the pinned host slot
-        main = torch.cuda.current_stream(self.device)
-        main.wait_event(ev)
-        self.buf.copy_(self._stage, non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(main)
-        self._d2d_done = done
+            ev.record()
+            self._events[slot] = ev    # guards the pinned host slot
         return True
 
     def materialize(self):
@@ -349,26 +327,6 @@ def bucket_capacities(store, batch_size, sources=None, z=(-0.5, 0.5, 1.5),
         if not out or caps != out[-1]:
             out.append(caps)
     return out
-
-
-_COPY_STREAMS = {}
-# Overlapped host->device staging of the next batch on a copy stream
-# (DGMC_AMD_STAGE_COPY=1).  Off by default: it shortens the inter-step gap
-# under the profiler (66 -> 14 us) but lets the host run further ahead, and
-# the 200-step bench measured 173.8k vs 178.6k pairs/s same-box.
-STAGE_COPY = os.environ.get('DGMC_AMD_STAGE_COPY', '0') == '1'
-# How far the host may stage ahead of the device: 1 = wait for the previous
-# batch's copy (i.e. the step before it) before collating the next one; 2 =
-# the pinned double buffer's own limit.  Shallower queues measured faster
-# (179.5k vs 178.7k pairs/s same-box).
-HOST_AHEAD = int(os.environ.get('DGMC_AMD_HOST_AHEAD', '1'))
-
-
-def _copy_stream(device):
-    s = _COPY_STREAMS.get(device)
-    if s is None:
-        s = _COPY_STREAMS[device] = torch.cuda.Stream(device=device)
-    return s
 
 
 class _StaticSlotOperator(SparseOperator):

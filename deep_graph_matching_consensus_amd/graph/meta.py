@@ -46,7 +46,8 @@ class BatchInfo(object):
         self._device_cache = {}
 
     def dense_index(self, device, max_nodes=None):
-        """``[num_nodes]`` flat index of every node in a ``[B * N_max]`` grid."""
+        """``[num_nodes]`` flat index of every node in a ``[B * N_max]``
+        grid."""
         n_max = self.max_nodes if max_nodes is None else max_nodes
         key = ('dense_index', str(device), n_max)
         out = self._device_cache.get(key)

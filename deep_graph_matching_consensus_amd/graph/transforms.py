@@ -32,7 +32,8 @@ class Compose(object):
 
 
 def coalesce_undirected(edge_index, num_nodes):
-    """``to_undirected`` + ``coalesce``: symmetric, sorted (row, col), unique."""
+    """``to_undirected`` + ``coalesce``: symmetric, sorted (row, col),
+    unique."""
     row, col = edge_index
     row, col = torch.cat([row, col]), torch.cat([col, row])
     key = torch.unique(row * num_nodes + col)
@@ -133,7 +134,8 @@ class Distance(object):
 
 
 class Constant(object):
-    r"""Adds a constant node feature (``x = value``, concatenated if ``cat``)."""
+    r"""Adds a constant node feature (``x = value``, concatenated if
+    ``cat``)."""
 
     def __init__(self, value=1, cat=True):
         self.value, self.cat = value, cat

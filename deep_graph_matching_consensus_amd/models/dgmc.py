@@ -1,4 +1,5 @@
-"""Deep Graph Matching Consensus (API of ``/root/reference/dgmc/models/dgmc.py``).
+"""Deep Graph Matching Consensus
+(API of ``/root/reference/dgmc/models/dgmc.py``).
 
 Public surface kept identical to the reference: constructor
 ``DGMC(psi_1, psi_2, num_steps, k=-1, detach=False)`` (``dgmc.py:64``),
@@ -35,10 +36,8 @@ from ..ops import _backend
 from ..ops import dense as dense_ops
 from ..ops.gemm import mixed_matmul
 from ..ops import sparse_corr
-from ..ops.sparse import PASSTHROUGH
 from ..ops.plans import _IdentityCache
 from ..runtime import loopgrad
-from ..runtime import streams
 from ..runtime.cache import forward_cache
 from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
@@ -74,14 +73,9 @@ class _PackedNLL(torch.autograd.Function):
         return dS, None, None, None, None, None
 
 
-FOLD_FP32 = os.environ.get('DGMC_AMD_FOLD_FP32', '1') == '1'
-
-
 class _FoldProduct(torch.autograd.Function):
     """``W1 @ W_f`` in fp32 (the folded consensus projection; ``b_f`` rides
-    along with an exact zero gradient).  Its backward only produces
-    parameter gradients, so it runs as part of the side-stream branch
-    (runtime/streams.py) that the folded weight gradient arrives on."""
+    along with an exact zero gradient)."""
 
     @staticmethod
     def forward(ctx, w1, wf, bf):
@@ -106,15 +100,14 @@ class _FoldProduct(torch.autograd.Function):
         w1, wf = ctx.saved_tensors
         if g is None:
             return None, None, None
-        with streams.side(g.device, (g, w1, wf)):
-            g = g.float()
-            gw1 = (g @ wf.float().t()).to(w1.dtype) \
-                if ctx.needs_input_grad[0] else None
-            gwf = (w1.float().t() @ g).to(wf.dtype) \
-                if ctx.needs_input_grad[1] else None
-            gbf = None
-            if ctx.bf_like is not None and ctx.needs_input_grad[2]:
-                gbf = g.new_zeros(ctx.bf_like[0], dtype=ctx.bf_like[1])
+        g = g.float()
+        gw1 = (g @ wf.float().t()).to(w1.dtype) \
+            if ctx.needs_input_grad[0] else None
+        gwf = (w1.float().t() @ g).to(wf.dtype) \
+            if ctx.needs_input_grad[1] else None
+        gbf = None
+        if ctx.bf_like is not None and ctx.needs_input_grad[2]:
+            gbf = g.new_zeros(ctx.bf_like[0], dtype=ctx.bf_like[1])
         return gw1, gwf, gbf
 
 
@@ -404,16 +397,13 @@ class DGMC(torch.nn.Module):
                     # (b_f's exact gradient is zero; it stays in the graph
                     # for autograd.grad / DDP.)
                     lp = {}
-                    if FOLD_FP32:
-                        w_fold, wn, wnt = _FoldProduct.apply(
-                            self.mlp[0].weight, self.psi_2.final.weight,
-                            self.psi_2.final.bias)
-                        if wn is not None:
-                            # bf16 operand images from the same kernel
-                            # (ops/dense.py::cat_matmul reads them here).
-                            lp = {'n': wn, 'nt': wnt}
-                    else:
-                        w_fold = self.mlp[0].weight @ self.psi_2.final.weight
+                    w_fold, wn, wnt = _FoldProduct.apply(
+                        self.mlp[0].weight, self.psi_2.final.weight,
+                        self.psi_2.final.bias)
+                    if wn is not None:
+                        # bf16 operand images from the same kernel
+                        # (ops/dense.py::cat_matmul reads them here).
+                        lp = {'n': wn, 'nt': wnt}
                     fold = (w_fold.t(), lp, ('fold', id(self.mlp[0].weight)),
                             steps)
                 pending = None    # (joint, S_hat) from a fused step boundary
@@ -425,7 +415,7 @@ class DGMC(torch.nn.Module):
                         pending = None
                         o_s, o_t, o = refine(None, None, r_joint,
                                              features=fold is not None)
-                    elif joint and PASSTHROUGH and S_hat.requires_grad and \
+                    elif joint and S_hat.requires_grad and \
                             torch.is_grad_enabled():
                         # S_hat feeds the transport AND the update: the
                         # update reads it through the transport's alias, so
@@ -537,13 +527,12 @@ class DGMC(torch.nn.Module):
 
     def _dense_sinkhorn(self, hs, ht, r_all, steps, lay_s, lay_t, refine):
         """Dense path with Sinkhorn normalisation (opt-in extension): the
-        same consensus loop with ``masked_sinkhorn`` in place of the row
-        softmax; transport ``r_t = S^T r_s`` as a batched GEMM."""
-        from ..ops import reference as ref
-        mask = ref.count_mask(lay_s.counts, lay_t.counts, lay_s.N, lay_t.N)
-
+        same consensus loop with a masked log-domain Sinkhorn (HIP kernel
+        per pair, ``csrc/hip/sinkhorn.hip``) in place of the row softmax;
+        transport ``r_t = S^T r_s`` as a batched GEMM."""
         def norm(S_hat):
-            return ref.masked_sinkhorn(S_hat, mask, self.sinkhorn_iters)
+            return dense_ops.masked_sinkhorn(S_hat, lay_s, lay_t,
+                                             self.sinkhorn_iters)
 
         S_hat = hs @ ht.transpose(-1, -2)
         S_0 = lay_s.to_sparse(norm(S_hat))

@@ -1,4 +1,5 @@
-"""Multi-layer perceptron encoder (API of ``/root/reference/dgmc/models/mlp.py``).
+"""Multi-layer perceptron encoder
+(API of ``/root/reference/dgmc/models/mlp.py``).
 
 Layer schedule (``mlp.py:31-39``): every hidden ``Linear`` is followed by ReLU
 and, if ``batch_norm``, BatchNorm1d; dropout is applied only to the input of

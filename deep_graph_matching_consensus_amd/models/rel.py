@@ -15,7 +15,7 @@ from torch.nn import BatchNorm1d, Linear, ModuleList
 
 from ..ops.gemm import compute_dtype
 from ..ops.plans import relational_plan
-from ..ops.sparse import PASSTHROUGH, gemm_spmm
+from ..ops.sparse import gemm_spmm
 from ..runtime.cache import cached
 from .encoder import StackedEncoder
 
@@ -84,7 +84,7 @@ class RelCNN(StackedEncoder):
         xs = [x]
         for conv, bn in zip(self.convs, self.batch_norms):
             kw = {}
-            if (self.cat and PASSTHROUGH and xs[-1].requires_grad and
+            if (self.cat and xs[-1].requires_grad and
                     torch.is_grad_enabled()):
                 # xs[-1] also feeds the concatenation: that consumer reads
                 # the conv's alias, so both gradients meet in the conv

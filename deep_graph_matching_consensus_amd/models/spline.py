@@ -10,7 +10,6 @@ import torch.nn.functional as F
 from torch.nn import ModuleList
 
 from ..nn.conv import SplineConv
-from ..ops.sparse import PASSTHROUGH
 from .encoder import StackedEncoder
 
 
@@ -37,7 +36,7 @@ class SplineCNN(StackedEncoder):
     def forward(self, x, edge_index, edge_attr, *args):
         xs = [x]
         for conv in self.convs:
-            if (self.cat and PASSTHROUGH and xs[-1].requires_grad and
+            if (self.cat and xs[-1].requires_grad and
                     torch.is_grad_enabled()):
                 # xs[-1] also feeds the concatenation: route that consumer
                 # through the conv's alias so both gradients meet inside

@@ -25,7 +25,6 @@ from ..ops import slot_gemm
 from ..ops.plans import spline_plan, adjacency_plan
 from ..ops.gemm import compute_dtype
 from ..ops.sparse import SLOT_CONV, gemm_spmm, prime_slot_images, spmm
-from ..runtime import streams
 from ..runtime.cache import cached
 from .inits import reset, uniform
 
@@ -67,8 +66,6 @@ class _StackedSplineWeight(torch.autograd.Function):
             return None, None, None
         gw = gr = None
         if g is not None:
-            if pend is not None:
-                streams.join()      # (a side-stream pend: combine after it)
             gw, gr = _backend.ops().spline_weight_unpack(
                 g.float().contiguous(), ctx.K, ctx.has_root)
         if pend is not None:

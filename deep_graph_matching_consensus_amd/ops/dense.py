@@ -28,16 +28,14 @@ import torch
 
 from . import _backend
 from . import reference as ref
-from .gemm import (_col_sum, loop_col_sum, loop_col_total, lowp_weight_t,
-                   mixed_matmul)
-from ..runtime import loopgrad, streams
+from .gemm import _col_sum, lowp_weight_t, mixed_matmul
+from ..runtime import loopgrad
 
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
 # Consensus update of step l fused with the softmax transport of step l + 1
 # (one per-pair kernel each way); DGMC_AMD_FUSE_STEPS=0 keeps them apart.
 FUSE_STEPS = os.environ.get('DGMC_AMD_FUSE_STEPS', '1') == '1'
-
 
 
 def _hip_ok(x, N_s, N_t):
@@ -202,6 +200,43 @@ def softmax_nll(S_hat, lay_s, lay_t, y_col, mask, eps, S_hat2=None,
     count]`` inside the fold kernel."""
     return _SoftmaxNLL.apply(S_hat, S_hat2, lay_s.ptr, lay_t.counts, y_col,
                              mask, float(eps), stats)
+
+
+# ---------------------------------------------------------------------------
+class _Sinkhorn(torch.autograd.Function):
+    """Masked log-domain Sinkhorn per pair (csrc/hip/sinkhorn.hip): the
+    forward keeps each half-step's potentials, the backward rebuilds the
+    half-step outputs from them and applies the normalisation Jacobians in
+    reverse."""
+
+    @staticmethod
+    def forward(ctx, S_hat, n_s, n_t, iters, tau):
+        S_hat = S_hat.float().contiguous()
+        P, ah, bh = _backend.ops().sinkhorn_fwd(S_hat, n_s, n_t, int(iters),
+                                                float(tau))
+        ctx.save_for_backward(S_hat, n_s, n_t, ah, bh)
+        ctx.iters, ctx.tau = int(iters), float(tau)
+        return P
+
+    @staticmethod
+    def backward(ctx, grad):
+        S_hat, n_s, n_t, ah, bh = ctx.saved_tensors
+        dS = _backend.ops().sinkhorn_bwd(grad.float().contiguous(), S_hat,
+                                         n_s, n_t, ah, bh, ctx.iters,
+                                         ctx.tau)
+        return dS, None, None, None, None
+
+
+def masked_sinkhorn(S_hat, lay_s, lay_t, iters=10, tau=1.0):
+    r"""Sinkhorn normalisation of the dense scores ``[B, N_s, N_t]`` over
+    each pair's valid ``n_s x n_t`` block (``iters`` row + column rounds and
+    a final row step, so rows sum to 1 like the reference's masked softmax;
+    zeros outside).  HIP kernel on the GPU, :func:`.reference.masked_sinkhorn`
+    elsewhere (the oracle of ``tests/test_sinkhorn.py``)."""
+    B, N_s, N_t = S_hat.shape
+    if _hip_ok(S_hat, N_s, N_t):
+        return _Sinkhorn.apply(S_hat, lay_s.counts, lay_t.counts, iters, tau)
+    return ref.masked_sinkhorn(S_hat, _count_mask(lay_s, lay_t), iters, tau)
 
 
 # ---------------------------------------------------------------------------
@@ -409,8 +444,7 @@ def _consensus_param_grads(loop, idx, dP, dw2_part, db2_part):
     if loop.arrive():
         part = loop.get_acc('pq_part')
         R = (part.size(1) - 1) // 2
-        with streams.side(part.device, (part, )):
-            tot = _col_sum(part)
+        tot = _col_sum(part)
         loop.release()
         return tot[:R], tot[R:2 * R], tot[2 * R:]
     return None, None, None
@@ -437,7 +471,9 @@ class _CatMatmul(torch.autograd.Function):
         K = sum(p.size(1) for p in parts)
         ctx.loop, ctx.widths = loop, [p.size(1) for p in parts]
         ctx.w_dtype = w.dtype
-        need_w = ctx.needs_input_grad[0] and torch.is_grad_enabled()
+        # (grad mode is off inside forward: needs_input_grad alone says
+        # whether the backward will want dW.)
+        need_w = ctx.needs_input_grad[0]
         if loop is not None:
             ctx.idx = loop.register()
             ocat = loop.slot_total('x', ctx.idx, (M, K), w_n.dtype,
@@ -458,9 +494,8 @@ class _CatMatmul(torch.autograd.Function):
         g = g.contiguous()
         if g.dtype != w_n.dtype:
             g = g.to(w_n.dtype)
-        # g W^T = [M, 128] x [128, K] on the same kernel (W^T staged in LDS);
-        # DGMC_AMD_CAT_GEMM_BWD=0: hipBLASLt.
-        if CAT_GEMM_BWD and w_nt.size(0) in (128, 256, 384) and \
+        # g W^T = [M, 128] x [128, K] on the same kernel (W^T staged in LDS).
+        if w_nt.size(0) in (128, 256, 384) and \
                 g.data_ptr() % 16 == 0:
             gx = _backend.ops().cat_gemm([g], w_nt, None)    # [M, K]
         else:
@@ -479,28 +514,20 @@ class _CatMatmul(torch.autograd.Function):
             loop.keep('g', ctx.idx, g)
             if loop.arrive():
                 if ctx.needs_input_grad[0]:
-                    # Off psi_1's backward path: side-stream branch
-                    # (runtime/streams.py).
                     X = loop.stack('x')
                     gl = loop.kept_list('g')
-                    with streams.side(g.device, (X, gl)):
-                        if dense_wgrad_supported(X, gl):
-                            gw = dense_wgrad(list(X.unbind(0)), gl).to(
-                                ctx.w_dtype)
-                        else:
-                            gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
-                                                loop.kept('g')).to(
-                                                    ctx.w_dtype)
+                    if dense_wgrad_supported(X, gl):
+                        gw = dense_wgrad(list(X.unbind(0)), gl).to(
+                            ctx.w_dtype)
+                    else:
+                        gw = matmul_tn_fp32(X.view(-1, X.size(-1)),
+                                            loop.kept('g')).to(ctx.w_dtype)
                 loop.release()
         return (gw, None, None, None, None) + tuple(grads)
 
 
-DENSE_WGRAD = os.environ.get('DGMC_AMD_DENSE_WGRAD', '1') == '1'
-CAT_GEMM_BWD = os.environ.get('DGMC_AMD_CAT_GEMM_BWD', '1') == '1'
-
-
 def dense_wgrad_supported(X, gs):
-    return (DENSE_WGRAD and _backend.use_hip(X) and X.dtype == torch.bfloat16
+    return (_backend.use_hip(X) and X.dtype == torch.bfloat16
             and X.dim() == 3 and X.size(-1) % 128 == 0 and
             X.size(-1) <= 512 and X.is_contiguous() and
             X.data_ptr() % 16 == 0 and len(gs) == X.size(0) and

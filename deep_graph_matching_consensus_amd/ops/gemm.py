@@ -37,8 +37,7 @@ def _split_factor(m, n, k):
 
 
 def _dense_tn_ok(a, b):
-    from . import dense as _dense
-    if not (_dense.DENSE_WGRAD and a.is_cuda and _backend.use_hip(a)):
+    if not (a.is_cuda and _backend.use_hip(a)):
         return False
     K, M = a.shape
     N = b.shape[1]

@@ -1,4 +1,5 @@
-"""fp32 SplineConv on the (node, slot) pairs the edges use (csrc/hip/slot_gemm.hip).
+"""fp32 SplineConv on the (node, slot) pairs the edges use
+(csrc/hip/slot_gemm.hip).
 
 Reference: ``/root/reference/dgmc/models/spline.py:21,49`` (PyG SplineConv
 over torch_spline_conv, fp32).  With ``A [N, N*S]`` the layer's message

@@ -23,7 +23,6 @@ import os
 import torch
 
 from . import _backend
-from ..runtime import streams
 from . import reference as ref
 
 
@@ -270,18 +269,11 @@ class _GemmSpMM(torch.autograd.Function):
             # Graph-closed tiles: Z_k = A_k x and Z_k W_k on MFMA, Y and Z
             # never materialised (csrc/hip/slot_conv.hip).
             img = slot_conv_image(w_lp, C, trans=False)
-            if SLOT_CONV_BWD or (SLOT_WGRAD and loop is not None):
+            if loop is not None:
                 ctx.img_b = slot_conv_image(w_lp, C, trans=True)
             out = _backend.ops().slot_conv(
                 xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
                 relu, xc.dtype, None)
-        elif _fused_ok(xc, K, C):
-            # Fused gather + MFMA: Y = x @ W is never materialised.
-            sc = op.slot_csr(S)
-            wt = _slot_major_t(w_lp)                    # [S * C, K]
-            out = _backend.ops().gather_gemm(
-                xc.contiguous(), sc.rowptr, sc.col, sc.val, wt, C * K, K, S,
-                C, bias, relu, xc.dtype, None)
         else:
             y = (xc @ w_lp).view(-1, C)
             out_dtype = y.dtype if y.dtype in (torch.bfloat16,
@@ -295,8 +287,8 @@ class _GemmSpMM(torch.autograd.Function):
         # expanded 1-element tensor): its node can take the loop-folded
         # weight gradient in slot-major layout directly (no permute copy, no
         # unpack kernel).
-        node = w.grad_fn if (SLOT_HANDOFF and w.dim() == 2 and
-                             w.stride() == (0, 0)) else None
+        node = w.grad_fn if (w.dim() == 2 and w.stride() == (0, 0)) \
+            else None
         ctx.w_node = node if hasattr(node, 'takes_slot_major') else None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.idx = loop.register() if loop is not None else None
@@ -337,16 +329,10 @@ class _GemmSpMM(torch.autograd.Function):
         if loop.arrive():
             need_w = ctx.needs_input_grad[1]
             xs, gs = loop.kept_list('x'), loop.kept_list('g')
-            # The folded weight / bias gradients are off psi_1's backward
-            # path: a side-stream branch in the trainer's step
-            # (runtime/streams.py), joined before the gradients are packed.
-            keep = (xs, gs, loop.stack('b') if need_b and 'b' in loop._stacks
-                    else None)
-            with streams.side(grad.device, keep):
-                if need_w:
-                    dW = slot_weight_grad(xs, gs, op, S, loop.uses)
-                if need_b:
-                    gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
+            if need_w:
+                dW = slot_weight_grad(xs, gs, op, S, loop.uses)
+            if need_b:
+                gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
             if need_w:
                 if ctx.w_node is not None:
                     # Slot-major [S, in, out] straight to the stacked-weight
@@ -370,8 +356,8 @@ class _GemmSpMM(torch.autograd.Function):
         op = ctx.op
         K = xc.size(1)
         S = w_lp.size(1) // C
-        if (hip and ctx.slot and loop is not None and SLOT_WGRAD and
-                FUSED_RELU_BWD and ctx.img_b is not None and
+        if (hip and ctx.slot and loop is not None and
+                ctx.img_b is not None and
                 grad.dtype == torch.bfloat16 and w_lp.dtype == torch.bfloat16
                 and (out is None or out.dtype == torch.bfloat16)):
             return _GemmSpMM._slot_loop_backward(ctx, grad, gpass, xc, out,
@@ -398,7 +384,7 @@ class _GemmSpMM(torch.autograd.Function):
                 if loop is not None:
                     loop.add_to('b', db)
             g = g.to(w_lp.dtype)
-        if (ctx.slot and loop is not None and SLOT_WGRAD and
+        if (ctx.slot and loop is not None and
                 g.dtype == torch.bfloat16 and ctx.img_b is not None):
             # 2'. dx by the transposed slot conv; dW from the kept (x, g')
             #     pairs of all uses - dY is never formed.
@@ -429,13 +415,12 @@ class _GemmSpMM(torch.autograd.Function):
         # 2. dY = A^T g' (and dx = sum_k dY_k W_k^T, fused when possible).
         slot = ctx.img_b is not None and ctx.needs_input_grad[0] and \
             g.dtype == torch.bfloat16
-        fused = not slot and ctx.needs_input_grad[0] and _fused_ok(g, C, K)
         opt = None if slot else op.t()
         rows_t = op.num_cols
         if loop is not None:
             dy = loop.slot('dy', idx, (rows_t, C), w_lp.dtype, dev)
             loop.keep('x', idx, xc)      # concatenated once at the end
-        elif fused or slot:
+        elif slot:
             dy = torch.empty((rows_t, C), dtype=w_lp.dtype, device=dev)
         else:
             dy = None
@@ -446,14 +431,6 @@ class _GemmSpMM(torch.autograd.Function):
             gx = _backend.ops().slot_conv(
                 g.contiguous(), *slot_tile_plan(op, S), S, ctx.img_b, True,
                 None, False, g.dtype, dy)
-            if gx.dtype != ctx.x_dtype:
-                gx = gx.to(ctx.x_dtype)
-        elif fused:
-            # Gather over A^T (rows j*S + k) writes dY and contracts it with
-            # W_k^T read in place from w_lp [K, S*C] in one kernel.
-            gx = _backend.ops().gather_gemm(
-                g, opt.rowptr, opt.col, opt.val, _contig(w_lp), C, S * C, S,
-                K, None, False, g.dtype, dy)
             if gx.dtype != ctx.x_dtype:
                 gx = gx.to(ctx.x_dtype)
         elif dy is not None and hip:
@@ -504,49 +481,15 @@ def _add_pass(gx, gpass):
     return gx + gpass
 
 
-_FUSED_WIDTHS = (32, 64, 128)
-
-
-# The fused gather-MFMA SplineConv/RelConv kernel (csrc/hip/gather_gemm.hip)
-# is opt-in: measured on MI355X it is LDS-bandwidth bound at ~1.5 us per
-# slot (54 us per psi_2 layer vs 45 us for hipBLASLt GEMM + SpMM), see
-# docs/performance.md.  DGMC_AMD_FUSED_CONV=1 enables it.
-FUSED_CONV = os.environ.get('DGMC_AMD_FUSED_CONV', '0') == '1'
-
-
-def _fused_ok(x, K, M):
-    """Shapes/dtypes served by the fused gather-MFMA kernel."""
-    return (FUSED_CONV and _backend.use_hip(x) and x.dtype == torch.bfloat16
-            and K in _FUSED_WIDTHS and M % 32 == 0)
-
-
-def _contig(t):
-    return t if t.is_contiguous() else t.contiguous()
-
-
-# Fused slot convolution on graph-closed row tiles (csrc/hip/slot_conv.hip):
-# used whenever the operator carries graph-start flags (static batches,
-# datasets/static_batch.py) and the layer is 128 -> 128 wide (psi_2 of the
-# PascalVOC/WILLOW configs).  DGMC_AMD_SLOT_CONV: 'fwd' (default) fuses the
-# forward only - measured on MI355X (tools/bench_slot_conv.py, psi_2 layer at
-# batch 512): forward 31.6 us fused vs 38.4 us GEMM + SpMM, backward with the
-# dY output 49.1 us fused vs 44.5 us SpMM + GEMM; '1' fuses both, '0' none.
-_SLOT_MODE = os.environ.get('DGMC_AMD_SLOT_CONV', 'fwd')
-SLOT_CONV = _SLOT_MODE in ('1', 'fwd')
-SLOT_CONV_BWD = _SLOT_MODE == '1'
-# Loop-shared weight gradient straight from the kept (x, g') pairs of every
-# use (csrc/hip/slot_wgrad.hip) - no dY = A^T g' stack - with the fused
-# transposed slot conv for dx (psi_2 backward: 113.7k vs 104.9k pairs/s,
-# docs/performance.md).  DGMC_AMD_SLOT_WGRAD=0 falls back to the SpMM dY
-# stack + long-K GEMM.
-SLOT_WGRAD = os.environ.get('DGMC_AMD_SLOT_WGRAD', '1') == '1'
-# Encoders with ``cat=True`` hand a layer input's second consumer (the
-# concatenation) the conv's passthrough alias, so its gradient is added in
-# the transposed slot conv epilogue instead of by an autograd add kernel.
-PASSTHROUGH = os.environ.get('DGMC_AMD_PASSTHROUGH', '1') == '1'
-# Consensus-loop backward: the ReLU mask, g' and the bias-gradient partials
-# are formed inside the transposed slot conv (no relu_bias_bwd pass).
-FUSED_RELU_BWD = os.environ.get('DGMC_AMD_FUSED_RELU_BWD', '1') == '1'
+# Fused slot convolution on graph-closed row tiles (csrc/hip/slot_conv.hip,
+# bf16): used whenever the operator carries graph-start flags (static
+# batches, datasets/static_batch.py) and the layer is 128 -> 128 wide (psi_2
+# of the PascalVOC/WILLOW configs).  Forward: the fused kernel; consensus-loop
+# backward: the transposed slot conv (ReLU mask, g', bias partials and dx in
+# one kernel) + the slot weight gradient from the kept (x, g') pairs of every
+# use (csrc/hip/slot_wgrad.hip; no dY stack).  Measured on MI355X:
+# docs/performance.md.  DGMC_AMD_SLOT_CONV=0 selects GEMM + SpMM.
+SLOT_CONV = os.environ.get('DGMC_AMD_SLOT_CONV', '1') != '0'
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}
@@ -608,10 +551,9 @@ def slot_pair_lists(op, S):
     return p
 
 
-SLOT_WGRAD_SPLITS = int(os.environ.get('DGMC_AMD_SLOT_WGRAD_SPLITS', '64'))
-# Loop-folded slot weight gradient handed to the stacked-weight node in
-# slot-major layout (weight / root views; no permute + unpack kernels).
-SLOT_HANDOFF = os.environ.get('DGMC_AMD_SLOT_HANDOFF', '1') == '1'
+# Split partials of the slot weight gradient (64 measured best among
+# 24..128, docs/performance.md).
+SLOT_WGRAD_SPLITS = 64
 _SLOT_WGRAD_MAX_LIST = 16    # pointer table size (csrc/hip/slot_wgrad.hip)
 
 
@@ -699,14 +641,6 @@ def slot_conv_image(w_lp, C, trans):
         img = w3.permute(1, 0, 2) if trans else w3.permute(1, 2, 0)
         return (w_lp, img[:, :, slot_k_order(w_lp.device)].contiguous())
     return cached(_slot_img_key(w_lp, trans), build)[1]
-
-
-def _slot_major_t(w_lp):
-    """``w_lp [K, S*C]`` -> ``[S*C, K]`` (B operand of the fused forward),
-    memoised per forward scope (``w_lp`` itself is cached there)."""
-    from ..runtime.cache import cached
-    return cached(('slot_major_t', id(w_lp)),
-                  lambda: (w_lp, w_lp.t().contiguous()))[1]
 
 
 def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,

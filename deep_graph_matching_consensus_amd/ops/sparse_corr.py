@@ -1,6 +1,7 @@
-"""Sparse (top-k) correspondence ops (``/root/reference/dgmc/models/dgmc.py:184-244``).
+"""Sparse (top-k) correspondence ops
+(``/root/reference/dgmc/models/dgmc.py:184-244``).
 
-* :func:`top_k`            - candidate search ``argtopk_j <h_s[b,i], h_t[b,j]>``
+* :func:`top_k`      - candidate search ``argtopk_j <h_s[b,i], h_t[b,j]>``
   (``dgmc.py:85-94``; KeOps ``argKmin`` in the reference).  On the GPU a fused
   HIP kernel streams ``h_t`` tiles through LDS, computes the dot tiles on
   MFMA and keeps a per-row register top-k, so the ``N_s x N_t`` score matrix
@@ -10,7 +11,7 @@
 * :class:`CandidateGraph`  - the candidate set ``S_idx [B, N_s, k]`` as a CSR
   matrix over flattened source rows (global target columns ``b*N_t + idx``)
   plus its transpose, built once per forward.
-* :func:`gather_dot`       - ``S_hat[b,i,c] = <h_s[b,i], h_t[b, S_idx[b,i,c]]>``
+* :func:`gather_dot` - ``S_hat[b,i,c] = <h_s[b,i], h_t[b, S_idx[b,i,c]]>``
   (``dgmc.py:197-201``): an SDDMM kernel; backward = two SpMMs.
 * :func:`sparse_transport` - ``r_t = scatter_add(S * r_s, S_idx)``
   (``dgmc.py:209-212``): SpMM over the transpose (deterministic, no atomics);
@@ -75,7 +76,8 @@ class CandidateGraph(object):
         self.row_of = (self.perm // k).to(torch.int32)
         self.perm32 = self.perm.to(torch.int32)
         # Column walks (transport, consensus dQ, gather-dot dB) in pieces of
-        # <= sparse.PIECE entries: with random-init embeddings a few targets sit in
+        # <= sparse.PIECE entries: with random-init embeddings a few
+        # targets sit in
         # the top-k of thousands of rows (hubness), which would serialise a
         # column-per-wave kernel.
         self.col_pieces = piece_plan(self.colptr, col.numel())

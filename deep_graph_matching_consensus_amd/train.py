@@ -29,20 +29,10 @@ import torch
 from . import parallel
 from .datasets.device_loader import DevicePairLoader
 from .datasets.static_batch import StaticPairBatcher, bucket_capacities
-from .runtime import streams
 from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
 from .runtime.tuning import use_tuned_gemms
 
-# Static/captured steps: gradients stolen by AccumulateGrad and packed into
-# the flat buffer by one kernel (DGMC_AMD_STEAL_GRADS=0: zeroed flat views +
-# per-parameter accumulation).
-STEAL_GRADS = os.environ.get('DGMC_AMD_STEAL_GRADS', '1') == '1'
-# Loop-folded weight gradients on a side stream (runtime/streams.py).  Off by
-# default: the hipGraph executor maps the captured branches onto its own
-# queues and serialised them against the psi_1 backward in our measurements
-# (169.5k vs 170.6k pairs/s same-box), so there is no gain to take yet.
-SIDE_STREAMS = os.environ.get('DGMC_AMD_SIDE_STREAMS', '0') == '1'
 # Data-parallel gradient all-reduce inside the (captured) step, overlapped
 # with the backward (DGMC_AMD_IN_STEP_ALLREDUCE=0: one flat all-reduce after
 # the step).
@@ -88,7 +78,7 @@ class PairTrainer(object):
         in_step = (mode == 'static' or mode == 'graph' and
                    parallel.is_distributed() and
                    torch.distributed.get_backend() == 'nccl') and \
-            STEAL_GRADS and IN_STEP_ALLREDUCE
+            IN_STEP_ALLREDUCE
         self.reducer = parallel.GradBucketAllReducer(
             model, bucket_bytes=bucket_bytes,
             overlap=overlap and mode == 'eager', in_step=in_step)
@@ -206,19 +196,12 @@ class PairTrainer(object):
         self.optimizer.step()
 
     def _static_body(self, bucket=-1):
-        # Gradients are stolen by AccumulateGrad and packed into the flat
-        # buffer by one kernel (parallel/ddp.py::pack_grads).
-        if STEAL_GRADS:
-            self.reducer.release_grads()
-        else:
-            self.reducer.zero_grad()
+        # Gradients are stolen by AccumulateGrad (no zero-fill, no add per
+        # parameter) and packed into the flat buffer by one kernel
+        # (parallel/ddp.py::pack_grads).
+        self.reducer.release_grads()
         batch = self.batchers[bucket].materialize()
-        # Loop-folded weight gradients run on a side stream (overlapping the
-        # psi_1 backward); joined before the gradients are packed.  Needs the
-        # stolen-gradient path (no main-stream AccumulateGrad kernels).
-        with streams.side_streams(SIDE_STREAMS and STEAL_GRADS and
-                                  self.device.type == 'cuda'):
-            self._forward_backward(batch, self._rows[bucket], batch.y_mask)
+        self._forward_backward(batch, self._rows[bucket], batch.y_mask)
         if self.reducer.in_step:
             # DP: the buckets were packed and all-reduced from the backward
             # hooks; wait for the last ones, then check and update - all
@@ -227,12 +210,10 @@ class PairTrainer(object):
             self._check_finite()
             self._optimizer_step()
             return
-        flags = None
-        if STEAL_GRADS:
-            # Single process: the pack kernel also flags non-finite
-            # gradients and the optimizer's step kernel folds the flags.
-            flags = self.reducer.pack_grads(
-                with_flags=self.world == 1 and self.guard)
+        # Single process: the pack kernel also flags non-finite gradients
+        # and the optimizer's step kernel folds the flags.
+        flags = self.reducer.pack_grads(
+            with_flags=self.world == 1 and self.guard)
         if self.world == 1:
             from .runtime import optim as hip_optim
             if flags is not None and hip_optim.supported(self.optimizer):

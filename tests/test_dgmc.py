@@ -1,4 +1,5 @@
-"""Port of the reference DGMC tests (``/root/reference/test/models/test_dgmc.py``)."""
+"""Port of the reference DGMC tests
+(``/root/reference/test/models/test_dgmc.py``)."""
 import torch
 
 from deep_graph_matching_consensus_amd.graph import Batch, Data

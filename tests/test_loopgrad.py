@@ -1,4 +1,5 @@
-"""Loop-shared gradient accumulation (runtime/loopgrad.py) == plain autograd."""
+"""Loop-shared gradient accumulation (runtime/loopgrad.py) == plain
+autograd."""
 import pytest
 import torch
 

@@ -9,6 +9,7 @@ import torch
 
 from deep_graph_matching_consensus_amd.ops import _backend
 from deep_graph_matching_consensus_amd.ops import sparse as sparse_ops
+from deep_graph_matching_consensus_amd.runtime import loopgrad
 from deep_graph_matching_consensus_amd.ops.sparse import (
     SparseOperator, gemm_spmm, slot_conv_error, slot_conv_image,
     slot_tile_plan)
@@ -178,8 +179,9 @@ def test_slot_conv_flags_oversized_tiles():
     err.zero_()
 
 
-def test_gemm_spmm_uses_slot_conv_forward_backward(monkeypatch):
-    monkeypatch.setattr(sparse_ops, 'SLOT_CONV_BWD', True)
+def test_gemm_spmm_uses_slot_conv_forward():
+    """Outside a consensus loop: fused slot conv forward, GEMM + SpMM
+    backward."""
     S = 26
     op, flag = _graph_batch(_sizes(120, 19, seed=3), S, seed=3)
     op.tile_flag, op.tile_window = flag, 65 - 19
@@ -207,7 +209,7 @@ def test_gemm_spmm_uses_slot_conv_forward_backward(monkeypatch):
         gx, gw, gb = torch.autograd.grad(out, (x, w, bias), g.bfloat16())
     finally:
         _backend.ops = orig
-    assert calls == [False, True]
+    assert calls == [False]
     assert int(slot_conv_error(DEV)) == 0
     A = op.to_dense().bfloat16().float()
     xf = x.detach().float().requires_grad_()
@@ -315,7 +317,10 @@ def test_loop_training_step_slot_wgrad_matches_stacked_gemm(monkeypatch,
     assert batcher.load()
 
     def run(enabled):
-        monkeypatch.setattr(sparse_ops, 'SLOT_WGRAD', enabled)
+        # enabled: loop-folded slot weight gradient (one slot_wgrad launch
+        # over the kept (x, g') pairs); disabled: per-use autograd through
+        # the unfused backward (dY stack + GEMM).
+        monkeypatch.setattr(loopgrad, 'ENABLED', enabled)
         plans.clear_plan_cache()
         batch = batcher.materialize()
         rows = torch.arange(batcher.cap_s, device=DEV)
@@ -393,32 +398,6 @@ def test_slot_conv_unstaged_dense_tiles():
     assert _close(out, (A @ y + bias).relu(), 2e-2)
     gx_ref = (A.t() @ gy.float()).view(op.num_rows, -1) @ w_lp.float().t()
     assert _close(gx, gx_ref, 2e-2)
-
-
-def test_slot_conv_ws_matches_eight_wave_kernel(tmp_path):
-    """The wave-specialised kernel (default) against the 8-wave kernel
-    (DGMC_SC_WS=0, read once per process: run in a child process)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    path = str(tmp_path / 'eight_wave.pt')
-    code = (
-        'import sys, torch; sys.path.insert(0, {r!r}); '
-        'sys.path.insert(0, {t!r}); import test_slot_conv as t; '
-        'assert t._backend.hip_available(); '
-        '_, _, out, gx = t._dense_case_outputs(); '
-        'torch.save({{"out": out.cpu(), "gx": gx.cpu()}}, {p!r})').format(
-            r=root, t=os.path.join(root, 'tests'), p=path)
-    env = dict(os.environ, DGMC_SC_WS='0')
-    subprocess.run([sys.executable, '-c', code], env=env, check=True,
-                   timeout=300)
-    ref = torch.load(path, weights_only=True)
-    _, _, out, gx = _dense_case_outputs()
-    # Same operands, same fp32 accumulation per slot; the kernels differ in
-    # MFMA operand order only.
-    assert _close(out.cpu(), ref['out'], 1e-2)
-    assert _close(gx.cpu(), ref['gx'], 1e-2)
 
 
 def test_slot_conv_relu_bwd_fused_prologue():

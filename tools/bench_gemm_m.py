@@ -24,6 +24,7 @@ for M in (9984, 10240, 10304, 10496, 10752, 10944, 11008, 11264):
     x1 = torch.randn(M, 256, device='cuda').bfloat16()
     us = t(lambda: x @ w)
     us1 = t(lambda: x1 @ w1)
-    print('M=%d  L0 %.1f us (%.2f PF/s, %.2f ns/row)   L1 %.1f us (%.2f ns/row)'
+    print('M=%d  L0 %.1f us (%.2f PF/s, %.2f ns/row)   '
+          'L1 %.1f us (%.2f ns/row)'
           % (M, us, 2 * M * 1024 * 6656 / us / 1e9, us * 1e3 / M, us1,
              us1 * 1e3 / M), flush=True)

@@ -3,7 +3,6 @@ GEMM + SpMM SplineConv on a PascalVOC-shaped static batch (psi_2 layer,
 128 -> 128, 26 slots).
 
     python tools/bench_slot_conv.py [--reps 50]
-    DGMC_SC_DEBUG=1|2|4 python tools/bench_slot_conv.py   # ablations
 """
 import argparse
 import json

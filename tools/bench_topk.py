@@ -1,5 +1,6 @@
 """Time dgmc_amd::topk_dot (exact-f32 and split-bf16 kernels) on DBP15K-sized
-inputs; ``DGMC_TOPK_DEBUG`` (1 skip selection, 2 skip MFMA) isolates parts."""
+inputs (the kernels' ``dbg`` ablation argument is a diagnostic-build
+knob, fixed to 0 in production launches)."""
 import sys
 import os.path as osp
 import torch

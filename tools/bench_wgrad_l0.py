@@ -1,8 +1,8 @@
-"""Micro-benchmark of the psi_1 layer-0 weight gradient shapes (fp32-output GEMM variants)."""
+"""Micro-benchmark of the psi_1 layer-0 weight gradient shapes (fp32-output
+GEMM variants)."""
 import os.path as osp, sys, time
 import torch
 sys.path.insert(0, osp.dirname(osp.dirname(osp.abspath(__file__))))
-from deep_graph_matching_consensus_amd.runtime.tuning import use_tuned_gemms
 dev='cuda'
 K, M, N = 10304, 1024, 6656
 a = torch.randn(K, M, device=dev).bfloat16()
@@ -12,13 +12,18 @@ def bench(f, n=20):
     torch.cuda.synchronize(); t=time.perf_counter()
     for _ in range(n): f()
     torch.cuda.synchronize(); return (time.perf_counter()-t)/n*1e6
-print('mm fp32 out', bench(lambda: torch.mm(a.t(), b, out_dtype=torch.float32)))
+F32 = torch.float32
+print('mm fp32 out', bench(lambda: torch.mm(a.t(), b, out_dtype=F32)))
 for s in (2, 4, 8):
     k = K//s
     a3 = a[:k*s].view(s, k, M).transpose(1, 2); b3 = b[:k*s].view(s, k, N)
-    print('bmm split', s, bench(lambda: torch.bmm(a3, b3, out_dtype=torch.float32)))
+    print('bmm split', s,
+          bench(lambda: torch.bmm(a3, b3, out_dtype=F32)))
 print('mm bf16 out (untuned)', bench(lambda: torch.mm(a.t(), b)))
-print('mm fp32 out b^T a', bench(lambda: torch.mm(b.t(), a, out_dtype=torch.float32)))
+print('mm fp32 out b^T a',
+      bench(lambda: torch.mm(b.t(), a, out_dtype=F32)))
 at = a.t().contiguous(); bt = b.t().contiguous()
-print('mm fp32 out contiguous A^T', bench(lambda: torch.mm(at, b, out_dtype=torch.float32)))
-print('mm fp32 out (B^T)^T', bench(lambda: torch.mm(at, bt.t(), out_dtype=torch.float32)))
+print('mm fp32 out contiguous A^T',
+      bench(lambda: torch.mm(at, b, out_dtype=F32)))
+print('mm fp32 out (B^T)^T',
+      bench(lambda: torch.mm(at, bt.t(), out_dtype=F32)))

@@ -27,4 +27,6 @@ for K, M, N in [(11008, 1024, 6656), (11008, 256, 6656), (10304, 1024, 6656)]:
         out = D.dense_wgrad([x], [g], nsplit=ns)
         err = (out - ref).abs().max().item() / ref.abs().max().item()
         res[ns] = (t(lambda: D.dense_wgrad([x], [g], nsplit=ns)), err)
-    print(K, M, N, 'lib %.1f us' % us0, ' '.join('dw%d %.1f us (err %.1e)' % (k, v[0], v[1]) for k, v in res.items()), flush=True)
+    rest = ' '.join('dw%d %.1f us (err %.1e)' % (k, v[0], v[1])
+                    for k, v in res.items())
+    print(K, M, N, 'lib %.1f us' % us0, rest, flush=True)

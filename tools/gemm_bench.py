@@ -52,7 +52,8 @@ def main():
 
     def report(name, us, flop):
         rows.append((name, us, flop / us / 1e6))
-        print('{:58s} {:9.1f} us {:8.1f} TF/s'.format(name, us, flop / us / 1e6),
+        print('{:58s} {:9.1f} us {:8.1f} TF/s'.format(name, us,
+                                                     flop / us / 1e6),
               flush=True)
 
     for cin, cols in [(128, 3328), (256, 6656), (1024, 6656), (384, 128)]:

@@ -75,14 +75,16 @@ def custom():
     y = ops.gemm_abt(x, wt)
     print('custom fwd  err %.3e' % (y.float() - ref.float()).abs().max())
     t = timeit(lambda: ops.gemm_abt(x, wt))
-    print('custom fwd  %7.1f us  %5.2f TB/s(out)' % (t, N * S * C * 2 / t / 1e6))
+    print('custom fwd  %7.1f us  %5.2f TB/s(out)'
+          % (t, N * S * C * 2 / t / 1e6))
     dY = torch.randn(N, S * C, device=dev, dtype=dt)
     ref = dY @ w.t()
     dx = ops.gemm_abt(dY, w)
     print('custom dX   err %.3e (ref max %.2f)' % (
         (dx.float() - ref.float()).abs().max(), ref.float().abs().max()))
     t = timeit(lambda: ops.gemm_abt(dY, w))
-    print('custom dX   %7.1f us  %5.2f TB/s(in)' % (t, N * S * C * 2 / t / 1e6))
+    print('custom dX   %7.1f us  %5.2f TB/s(in)'
+          % (t, N * S * C * 2 / t / 1e6))
     acc = ref.clone()
     ops.gemm_abt(dY, w, acc, True)
     print('custom dX accumulate err %.3e' % (acc.float() - 2 * ref.float())

@@ -4,7 +4,8 @@ Splits the dispatch stream at the optimizer kernel (one fused Adam launch per
 training step), takes the LAST complete step and prints: wall span, summed
 kernel time, kernel count, idle gaps and a per-kernel-name table.
 
-    python tools/step_trace.py gpurun_out/prof/.../run_kernel_trace.csv [marker]
+    python tools/step_trace.py \
+        gpurun_out/prof/.../run_kernel_trace.csv [marker]
 """
 import collections
 import csv
