@@ -222,6 +222,11 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
 at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
                      const at::Tensor& seg, const at::Tensor& weight,
                      const c10::optional<at::Tensor>& root, bool trans_w);
+at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
+                      const at::Tensor& seg, const at::Tensor& bt,
+                      const c10::optional<at::Tensor>& broot, bool gather);
+at::Tensor slot_weight_t(const at::Tensor& weight,
+                         const c10::optional<at::Tensor>& root);
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
@@ -404,6 +409,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm(Tensor X, Tensor src, Tensor seg, Tensor weight, Tensor? "
       "root, bool trans_w) -> Tensor");
   m.def(
+      "slot_gemm2(Tensor X, Tensor src, Tensor seg, Tensor bt, Tensor? "
+      "broot, bool gather) -> Tensor");
+  m.def("slot_weight_t(Tensor weight, Tensor? root) -> Tensor");
+  m.def(
       "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
       "Tensor g, Tensor? seg=None) -> Tensor");
   m.def(
@@ -477,6 +486,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("piece_plan", &dgmc::piece_plan);
   m.impl("slot_compact_plan", &dgmc::slot_compact_plan);
   m.impl("slot_gemm", &dgmc::slot_gemm);
+  m.impl("slot_gemm2", &dgmc::slot_gemm2);
+  m.impl("slot_weight_t", &dgmc::slot_weight_t);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);

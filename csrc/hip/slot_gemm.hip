@@ -36,6 +36,7 @@ namespace dgmc {
 namespace {
 
 typedef float sg_f32x16 __attribute__((ext_vector_type(16)));
+typedef float sg_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kSgBM = 128;               // compact rows per tile / segment unit
 constexpr int kSgBN = 128;
@@ -421,6 +422,308 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
 }
 
 // ---------------------------------------------------------------------------
+// Slot GEMM v2 (LDS-DMA, double-buffered, transposed output fragments):
+//
+//   Y[m, :] = A_m Bt_s^T,  Bt_s [Nn, K] k-contiguous (forward: the W^T images
+//   of slot_weight_t; dX: the [in, out] weight itself), A_m = X[src[m]] when
+//   GATHER else X[m].
+//
+// * both operand tiles are [128 rows][32 k] fp32 (128-B rows) staged global
+//   -> LDS with global_load_lds (16 B per lane, no VGPR round trip); lane l of
+//   a wave's 8-row piece fetches logical quad (l & 7) ^ swz(row) of its row,
+//   swz(row) = (row >> 1) & 7, so the fragment reads below are conflict-free;
+// * two buffers per operand (separate LDS objects, the loop unrolled by two):
+//   chunk c + 1 lands while chunk c is multiplied;
+// * each lane reads float4 fragments (4 consecutive k of one row: one
+//   ds_read_b128 per operand block feeds 4 MFMA steps; MFMA step t pairs
+//   k = 8g + t (lanes 0-31) with k = 8g + 4 + t (lanes 32-63) on both
+//   operands);
+// * the weights are the MFMA A operand and the rows the B operand, so the
+//   32x32 accumulator holds Y^T: a lane owns one output row and 4 consecutive
+//   columns per register quad - the epilogue is 16 float4 stores per lane.
+// ---------------------------------------------------------------------------
+constexpr int kG2BK = 32;
+constexpr int kG2Tile = kSgBM * kG2BK;       // floats per operand buffer
+
+typedef const void __attribute__((address_space(1)))* sg_gptr;
+
+// One 16-byte-per-lane global -> LDS copy (global_load_lds_dwordx4; the LDS
+// destination is M0 + 16 * lane).  Issued as inline asm so the compiler does
+// not track it as an LDS write: its own alias model would otherwise drain
+// vmcnt before every fragment read of the other buffer.  The kernel counts
+// these loads itself (s_waitcnt vmcnt before each raw barrier).
+__device__ __forceinline__ void sg_dma16(const float* g, DGMC_LDS float* l) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)l);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :: "v"(g), "s"(m0) : "memory", "m0");
+}
+
+// s_barrier without __syncthreads' workgroup fence (which drains vmcnt and
+// would serialise the next chunk's LDS-DMA with this chunk's MFMAs); the
+// empty asm statements keep the compiler from moving memory ops across it.
+__device__ __forceinline__ void sg_raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(kSgThreads, 2) void slot_gemm2_kernel(
+    const float* __restrict__ X, const int* __restrict__ src,
+    const int* __restrict__ seg, int S, const float* __restrict__ bt,
+    const float* __restrict__ broot, int nb, int K, int Nn,
+    float* __restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) float sA0_[kG2Tile];
+  __shared__ __attribute__((aligned(16))) float sA1_[kG2Tile];
+  __shared__ __attribute__((aligned(16))) float sB0_[kG2Tile];
+  __shared__ __attribute__((aligned(16))) float sB1_[kG2Tile];
+  DGMC_LDS float* sA0 = (DGMC_LDS float*)sA0_;
+  DGMC_LDS float* sA1 = (DGMC_LDS float*)sA1_;
+  DGMC_LDS float* sB0 = (DGMC_LDS float*)sB0_;
+  DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int ntn = Nn / kSgBN, nk = K / kG2BK;
+  // Segment starts in lane registers: slot(m) = #{1 <= s < S: seg[s] <= m}.
+  const int segv = lane <= S ? seg[lane] : 0x7fffffff;
+  const int U = (__builtin_amdgcn_readlane(segv, S) / kSgBM) * ntn;
+  auto slot_of = [&](int m) {
+    return __popcll(__ballot(lane >= 1 && lane < S && segv <= m));
+  };
+  const int G = gridDim.x;
+  int u = xcd_remap(blockIdx.x, G);
+  if (u >= U) return;
+
+  // Staging: this lane's 4 rows (32 wave + 8 j + lane / 8) and the physical
+  // -> logical quad map of each.
+  const int prow = lane >> 3;
+  int sq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 32 * wave + 8 * j + prow;
+    sq[j] = 4 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  // Gather indices of a tile's staged rows (loaded one tile ahead).
+  auto load_idx = [&](int uu, int (&ix)[4]) {
+    const int m0 = (uu / ntn) * kSgBM + 32 * wave + prow;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ix[j] = GATHER ? src[m0 + 8 * j] : m0 + 8 * j;
+  };
+  const float* arow[4];
+  const float* brow;            // this lane's B row of piece 0 (+ 8 j rows)
+  auto tile_ptrs = [&](int uu, const int (&ix)[4]) {
+    const int m0 = (uu / ntn) * kSgBM;
+    const int n0 = (uu % ntn) * kSgBN;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = ix[j] < 0 ? 0 : ix[j];   // padding rows: never read
+      arow[j] = X + (size_t)r * K;
+    }
+    const int s = slot_of(m0);
+    const float* b = s < nb ? bt + (size_t)s * Nn * K : broot;
+    brow = b + (size_t)(n0 + 32 * wave + prow) * K;
+  };
+  auto stage = [&](int kc, DGMC_LDS float* da, DGMC_LDS float* db) {
+    const int k0 = kc * kG2BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      sg_dma16(arow[j] + k0 + sq[j], da + (32 * wave + 8 * j) * kG2BK);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      sg_dma16(brow + (size_t)8 * j * K + k0 + sq[j],
+               db + (32 * wave + 8 * j) * kG2BK);
+  };
+
+  // Fragment offsets (floats): row (wave block + 32 a + i), quad (2g+h)^sw.
+  const int i = lane & 31, h = lane >> 5, sw = (i >> 1) & 7;
+  int qoff[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) qoff[g] = 4 * ((2 * g + h) ^ sw);
+  const int offN = (wn * 64 + i) * kG2BK;    // + 32 a rows
+  const int offM = (wm * 64 + i) * kG2BK;    // + 32 b rows
+
+  sg_f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      sg_f32x4 fa[2], fb[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        fa[a] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+            lb + offN + a * 32 * kG2BK + qoff[g]);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        fb[b] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+            la + offM + b * 32 * kG2BK + qoff[g]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                fa[a][t], fb[b][t], acc[a][b], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](int uu) {
+    const int m0 = (uu / ntn) * kSgBM + wm * 64 + i;
+    const int n0 = (uu % ntn) * kSgBN + wn * 64 + 4 * h;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* yrow = Y + (size_t)(m0 + 32 * b) * Nn + n0 + 32 * a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          *reinterpret_cast<float4*>(yrow + 8 * q) =
+              make_float4(acc[a][b][4 * q], acc[a][b][4 * q + 1],
+                          acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][4 * q + r] = 0.f;
+        }
+      }
+  };
+
+  // One stream of (tile, chunk) work items: (u, kc) is multiplied while the
+  // item after it is staged into the other buffer.  The next tile's gather
+  // indices are loaded while the current tile's chunk 1 is staged (nk >= 4),
+  // so they have landed long before that tile's chunk 0 is staged.
+  int inext[4];
+  {
+    int icur[4];
+    load_idx(u, icur);
+    tile_ptrs(u, icur);
+  }
+  stage(0, sA0, sB0);
+  int kc = 0;
+  auto step = [&](DGMC_LDS float* ca, DGMC_LDS float* cb, DGMC_LDS float* na,
+                  DGMC_LDS float* nbuf) -> bool {
+    // Item after (u, kc).
+    const bool last_chunk = kc + 1 == nk;
+    const int tu = last_chunk ? u + G : u;
+    const int tkc = last_chunk ? 0 : kc + 1;
+    const bool more = tu < U;
+    if (more) {
+      if (last_chunk) tile_ptrs(tu, inext);
+      else if (tkc == 1 && u + G < U) load_idx(u + G, inext);
+      stage(tkc, na, nbuf);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sg_raw_barrier();
+    compute(ca, cb);
+    if (last_chunk) epilogue(u);
+    sg_raw_barrier();
+    u = tu;
+    kc = tkc;
+    return more;
+  };
+  while (step(sA0, sB0, sA1, sB1) && step(sA1, sB1, sA0, sB0)) {
+  }
+}
+
+at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
+                      const at::Tensor& seg, const at::Tensor& bt,
+                      const c10::optional<at::Tensor>& broot, bool gather) {
+  TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kFloat &&
+                  X.is_contiguous() && X.dim() == 2 && aligned16(X.data_ptr()),
+              "slot_gemm2: contiguous fp32 X");
+  TORCH_CHECK(bt.scalar_type() == at::kFloat && bt.is_contiguous() &&
+                  bt.dim() == 3 && aligned16(bt.data_ptr()),
+              "slot_gemm2: fp32 images [S', Nn, K]");
+  const int64_t S = seg.numel() - 1;
+  const int64_t nb = bt.size(0), Nn = bt.size(1), K = bt.size(2);
+  const bool has_root = broot.has_value() && broot->defined();
+  TORCH_CHECK(S == nb + (has_root ? 1 : 0) && S <= kSgMaxS,
+              "slot_gemm2: slots = images (+ root)");
+  if (has_root)
+    TORCH_CHECK(broot->scalar_type() == at::kFloat && broot->is_contiguous() &&
+                    broot->size(0) == Nn && broot->size(1) == K &&
+                    aligned16(broot->data_ptr()),
+                "slot_gemm2: root image [Nn, K]");
+  TORCH_CHECK(K % kSgBN == 0 && Nn % kSgBN == 0,
+              "slot_gemm2: K / Nn multiples of 128");
+  TORCH_CHECK(X.size(1) == K, "slot_gemm2: X [*, K]");
+  const int64_t P = src.numel();
+  TORCH_CHECK(P % kSgBM == 0 && src.scalar_type() == at::kInt,
+              "slot_gemm2: src [P_cap % 128]");
+  if (!gather) TORCH_CHECK(X.size(0) == P, "slot_gemm2: rows == P_cap");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
+  at::Tensor Y = at::empty({P, Nn}, X.options());
+  const int64_t blocks = std::min<int64_t>(
+      (P / kSgBM) * (Nn / kSgBN), 2 * (int64_t)num_cus(X.device().index()));
+  if (blocks == 0) return Y;
+  const float* rp = has_root ? broot->data_ptr<float>() : nullptr;
+  auto go = [&](auto g) {
+    constexpr bool GA = decltype(g)::value;
+    hipLaunchKernelGGL(slot_gemm2_kernel<GA>, dim3(blocks), dim3(kSgThreads),
+                       0, stream(), X.data_ptr<float>(), src.data_ptr<int>(),
+                       seg.data_ptr<int>(), (int)S, bt.data_ptr<float>(), rp,
+                       (int)nb, (int)K, (int)Nn, Y.data_ptr<float>());
+  };
+  if (gather) go(std::true_type());
+  else go(std::false_type());
+  DGMC_CHECK_LAUNCH();
+  return Y;
+}
+
+// W^T images [S, out, in] of weight [S - 1 or S, in, out] (+ root [in, out]
+// as the last slot): 32x32 tiles through LDS.
+__global__ __launch_bounds__(256) void slot_weight_t_kernel(
+    const float* __restrict__ weight, const float* __restrict__ root, int nw,
+    int cin, int cout, float* __restrict__ out) {
+  __shared__ float t[32][33];
+  const int s = blockIdx.z;
+  const float* w = s < nw ? weight + (size_t)s * cin * cout : root;
+  const int i0 = blockIdx.y * 32, o0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int r = 0; r < 32; r += 8)
+    t[ty + r][tx] = w[(size_t)(i0 + ty + r) * cout + o0 + tx];
+  __syncthreads();
+  float* o = out + (size_t)s * cin * cout;
+#pragma unroll
+  for (int r = 0; r < 32; r += 8)
+    o[(size_t)(o0 + ty + r) * cin + i0 + tx] = t[tx][ty + r];
+}
+
+at::Tensor slot_weight_t(const at::Tensor& weight,
+                         const c10::optional<at::Tensor>& root) {
+  TORCH_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat &&
+                  weight.is_contiguous() && weight.dim() == 3,
+              "slot_weight_t: contiguous fp32 weight [K, in, out]");
+  const int64_t nw = weight.size(0), cin = weight.size(1),
+                cout = weight.size(2);
+  const bool has_root = root.has_value() && root->defined();
+  if (has_root)
+    TORCH_CHECK(root->scalar_type() == at::kFloat && root->is_contiguous() &&
+                    root->size(0) == cin && root->size(1) == cout,
+                "slot_weight_t: root [in, out]");
+  TORCH_CHECK(cin % 32 == 0 && cout % 32 == 0, "slot_weight_t: multiples of 32");
+  const int64_t S = nw + (has_root ? 1 : 0);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
+  at::Tensor out = at::empty({S, cout, cin}, weight.options());
+  hipLaunchKernelGGL(slot_weight_t_kernel, dim3(cout / 32, cin / 32, S),
+                     dim3(256), 0, stream(), weight.data_ptr<float>(),
+                     has_root ? root->data_ptr<float>() : nullptr, (int)nw,
+                     (int)cin, (int)cout, out.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+// ---------------------------------------------------------------------------
 // Row-mapped SpMM: out[p, :] = sum_{e in row cinv[p] of (rowptr, col, val)}
 // val[e] * g[col[e], :]  (zero for cinv[p] < 0) - dY_c = A_c^T g' straight
 // from the assembled A^T (rows j*S + k) without re-indexing it.
@@ -587,22 +890,38 @@ struct SgUses {
 };
 
 // Item table: item i -> (slot, first row, end row); ib[s] = first item of s.
-__global__ void sg_items_kernel(const int* __restrict__ seg, int S, int CH,
-                                int G_cap, int* __restrict__ items,
-                                int* __restrict__ ib) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int n = 0;
-  for (int s = 0; s < S; ++s) {
-    ib[s] = n;
-    for (int r = seg[s]; r < seg[s + 1] && n < G_cap; r += CH * kSgBM) {
-      items[3 * n + 0] = s;
-      items[3 * n + 1] = r;
-      items[3 * n + 2] = min(r + CH * kSgBM, seg[s + 1]);
-      ++n;
+// One wave: lane s counts its slot's items, a ballot-free shuffle scan gives
+// the first item of each slot, then every lane fills the table.
+__global__ __launch_bounds__(64) void sg_items_kernel(
+    const int* __restrict__ seg, int S, int CH, int G_cap,
+    int* __restrict__ items, int* __restrict__ ib) {
+  const int lane = threadIdx.x;
+  const int span = CH * kSgBM;
+  int n = 0, b = 0, e = 0;
+  if (lane < S) {
+    b = seg[lane];
+    e = seg[lane + 1];
+    n = (e - b + span - 1) / span;
+  }
+  int incl = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const int first = incl - n;
+  const int total = __shfl(incl, 63);
+  if (lane < S) {
+    ib[lane] = first;
+    for (int q = 0; q < n && first + q < G_cap; ++q) {
+      const int r = b + q * span;
+      items[3 * (first + q) + 0] = lane;
+      items[3 * (first + q) + 1] = r;
+      items[3 * (first + q) + 2] = min(r + span, e);
     }
   }
-  ib[S] = n;
-  for (int i = n; i < G_cap; ++i) items[3 * i + 0] = -1;
+  if (lane == 0) ib[S] = min(total, G_cap);
+  for (int i = total + lane; i < G_cap; i += 64) items[3 * i + 0] = -1;
 }
 
 __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(

@@ -27,6 +27,7 @@ import os
 import torch
 
 from . import _backend
+from ..runtime.cache import cached
 from .gemm import col_partial_rows, loop_col_total
 
 BM = 128                      # compact segment / tile unit (slot_gemm.hip)
@@ -95,9 +96,12 @@ class _SlotGemmSpMM(torch.autograd.Function):
         plan = compact_plan(op, S)
         xc = x.contiguous()
         ops = _backend.ops()
-        Y = ops.slot_gemm(xc, plan.src, plan.seg, weight.contiguous(),
-                          root.contiguous() if root is not None else None,
-                          False)
+        # W^T images [S, out, in] (k-contiguous B operand), built once per
+        # forward scope and shared by the consensus loop's uses.
+        wt = cached(('slot_wt', id(weight)), lambda: ops.slot_weight_t(
+            weight.detach().contiguous(),
+            root.detach().contiguous() if root is not None else None))
+        Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
         out = ops.spmm_csr(op.rowptr, plan.col_c, op.val, Y, None, None,
                            bias, relu, torch.float32)
         ctx.save_for_backward(xc, weight, root, out if relu else None)
@@ -130,9 +134,9 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                     plan.seg)
         gx = None
         if ctx.needs_input_grad[0]:
-            Z = ops.slot_gemm(dyc, plan.src, plan.seg, weight.contiguous(),
-                              root.contiguous() if root is not None else None,
-                              True)
+            Z = ops.slot_gemm2(dyc, plan.src, plan.seg, weight.contiguous(),
+                               root.contiguous() if root is not None else None,
+                               False)
             add = gpass if (gpass is not None and
                             gpass.dtype == torch.float32 and gpass.dim() == 2
                             and gpass.stride(1) == 1 and

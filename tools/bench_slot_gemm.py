@@ -35,6 +35,16 @@ def timeit(fn, reps):
     return t0.elapsed_time(t1) * 1e3 / reps
 
 
+def slot_ids(plan, used):
+    seg = plan.seg.long()
+    rows = torch.arange(used, device=seg.device)
+    return torch.searchsorted(seg[1:], rows, right=True)
+
+
+def rel(a, ref):
+    return float((a.double() - ref).abs().max() / ref.abs().max())
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument('--reps', type=int, default=20)
@@ -71,6 +81,22 @@ def main():
                    args.reps)
         print('%4d->%-4d fwd   %8.1f us  %6.1f TF/s' % (cin, cout, t,
                                                        flop / t / 1e6))
+        valid = plan.src[:used] >= 0
+        y1 = ops.slot_gemm(x, plan.src, plan.seg, w, r, False)[:used][valid]
+        wt = ops.slot_weight_t(w, r)
+        y2 = ops.slot_gemm2(x, plan.src, plan.seg, wt, None, True)
+        y2 = y2[:used][valid]
+        ref = (x.double()[plan.src[:used][valid].long()].unsqueeze(1) @ (
+            torch.cat([w, r[None]]).double()[slot_ids(plan, used)[valid]])
+        ).squeeze(1)
+        print('    v1 err %.2e  v2 err %.2e (rel. to max |Y|)' % (
+            rel(y1, ref), rel(y2, ref)))
+        t = timeit(lambda: ops.slot_gemm2(x, plan.src, plan.seg, wt, None,
+                                          True), args.reps)
+        print('%4d->%-4d fwd2  %8.1f us  %6.1f TF/s' % (cin, cout, t,
+                                                       flop / t / 1e6))
+        t = timeit(lambda: ops.slot_weight_t(w, r), args.reps)
+        print('%4d->%-4d W^T   %8.1f us' % (cin, cout, t))
         dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
                                    plan.seg)
         t = timeit(lambda: ops.slot_spmm_rowmap(At.rowptr, At.col, At.val,
@@ -80,6 +106,16 @@ def main():
         t = timeit(lambda: ops.slot_gemm(dyc, plan.src, plan.seg, w, r,
                                          True), args.reps)
         print('%4d->%-4d dX    %8.1f us  %6.1f TF/s' % (cin, cout, t,
+                                                       flop / t / 1e6))
+        z1 = ops.slot_gemm(dyc, plan.src, plan.seg, w, r, True)[:used]
+        z2 = ops.slot_gemm2(dyc, plan.src, plan.seg, w, r, False)[:used]
+        ref = (dyc[:used].double().unsqueeze(1) @ torch.cat(
+            [w, r[None]]).double()[slot_ids(plan, used)].transpose(1, 2)
+        ).squeeze(1)
+        print('    v1 err %.2e  v2 err %.2e' % (rel(z1, ref), rel(z2, ref)))
+        t = timeit(lambda: ops.slot_gemm2(dyc, plan.src, plan.seg, w, r,
+                                          False), args.reps)
+        print('%4d->%-4d dX2   %8.1f us  %6.1f TF/s' % (cin, cout, t,
                                                        flop / t / 1e6))
         xs, ds = [x] * uses, [dyc] * uses
         t = timeit(lambda: sg.weight_grad(xs, ds, plan, cin, cout),
