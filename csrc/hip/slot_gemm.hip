@@ -662,8 +662,14 @@ at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
   if (!gather) TORCH_CHECK(X.size(0) == P, "slot_gemm2: rows == P_cap");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   at::Tensor Y = at::empty({P, Nn}, X.options());
-  const int64_t blocks = std::min<int64_t>(
-      (P / kSgBM) * (Nn / kSgBN), 2 * (int64_t)num_cus(X.device().index()));
+  // Persistent grid: one workgroup per CU for long K loops, two for K = 128
+  // (tools/bench_slot_gemm.py, per CU 1 / 2: 1024->256 forward 504 / 562
+  // us, 256->256 147 / 160 us, 128->128 53 / 50 us; one workgroup per tile
+  // 866 / 250 / 82 us).
+  const int per_cu = K >= 256 ? 1 : 2;
+  const int64_t tiles = (P / kSgBM) * (Nn / kSgBN);
+  const int64_t blocks =
+      std::min<int64_t>(tiles, per_cu * (int64_t)num_cus(X.device().index()));
   if (blocks == 0) return Y;
   const float* rp = has_root ? broot->data_ptr<float>() : nullptr;
   auto go = [&](auto g) {

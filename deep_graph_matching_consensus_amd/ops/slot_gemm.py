@@ -134,9 +134,13 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                     plan.seg)
         gx = None
         if ctx.needs_input_grad[0]:
-            Z = ops.slot_gemm2(dyc, plan.src, plan.seg, weight.contiguous(),
-                               root.contiguous() if root is not None else None,
-                               False)
+            # K = 128 (psi_2): the register-staged v1 kernel streams dY_c
+            # faster than the LDS-DMA one (51 vs 57 us per call,
+            # tools/bench_slot_gemm.py); longer K: v2.
+            kern = ops.slot_gemm2 if weight.size(2) >= 256 else \
+                lambda *a: ops.slot_gemm(*a[:5], True)
+            Z = kern(dyc, plan.src, plan.seg, weight.contiguous(),
+                     root.contiguous() if root is not None else None, False)
             add = gpass if (gpass is not None and
                             gpass.dtype == torch.float32 and gpass.dim() == 2
                             and gpass.stride(1) == 1 and
