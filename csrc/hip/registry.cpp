@@ -221,7 +221,10 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
                                           int64_t S, int64_t P_cap);
 at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
                      const at::Tensor& seg, const at::Tensor& weight,
-                     const c10::optional<at::Tensor>& root, bool trans_w);
+                     const c10::optional<at::Tensor>& root, bool trans_w,
+                     const c10::optional<at::Tensor>& tiles);
+at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
+                         int64_t N, int64_t row0, int64_t P_cap);
 at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
                       const at::Tensor& seg, const at::Tensor& bt,
                       const c10::optional<at::Tensor>& broot, bool gather);
@@ -233,7 +236,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const c10::optional<at::Tensor>& seg);
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t N, int64_t S,
-                           const c10::optional<at::Tensor>& add);
+                           const c10::optional<at::Tensor>& add,
+                           int64_t row0);
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
                           int64_t chunk);
@@ -407,7 +411,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "P_cap) -> Tensor[]");
   m.def(
       "slot_gemm(Tensor X, Tensor src, Tensor seg, Tensor weight, Tensor? "
-      "root, bool trans_w) -> Tensor");
+      "root, bool trans_w, Tensor? tiles=None) -> Tensor");
+  m.def(
+      "slot_dx_tiles(Tensor posmap, Tensor seg, int N, int row0, int P_cap) "
+      "-> Tensor");
   m.def(
       "slot_gemm2(Tensor X, Tensor src, Tensor seg, Tensor bt, Tensor? "
       "broot, bool gather) -> Tensor");
@@ -416,8 +423,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
       "Tensor g, Tensor? seg=None) -> Tensor");
   m.def(
-      "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add) "
-      "-> Tensor");
+      "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add, "
+      "int row0=0) -> Tensor");
   m.def(
       "slot_wgrad_f32(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
       "chunk) -> Tensor");
@@ -487,6 +494,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_compact_plan", &dgmc::slot_compact_plan);
   m.impl("slot_gemm", &dgmc::slot_gemm);
   m.impl("slot_gemm2", &dgmc::slot_gemm2);
+  m.impl("slot_dx_tiles", &dgmc::slot_dx_tiles);
   m.impl("slot_weight_t", &dgmc::slot_weight_t);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);

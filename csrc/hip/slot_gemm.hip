@@ -226,13 +226,17 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
     const float* __restrict__ X, const int* __restrict__ src,
     const int* __restrict__ seg, int S, const float* __restrict__ weight,
     const float* __restrict__ root, int nw, int K, int Nn,
-    float* __restrict__ Y) {
+    const int* __restrict__ tlist, int tcap, float* __restrict__ Y) {
   __shared__ float As[kSgBM * kSgKP];
   __shared__ float Bs[TRANS_W ? kSgBN * kSgKP : kSgBK * kSgNP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
   const int ntn = Nn / kSgBN, nk = K / kSgBK;
-  const int U = (seg[S] / kSgBM) * ntn;            // active output tiles
+  // Active output tiles: every row tile of the slot segments, or the row
+  // tiles listed in tlist (count at tlist[tcap]; dX of the rows a caller
+  // needs, slot_dx_tiles).
+  const int U = (tlist ? tlist[tcap] : seg[S] / kSgBM) * ntn;
+  auto rtile = [&](int uu) { return tlist ? tlist[uu / ntn] : uu / ntn; };
   const int G = gridDim.x;
   int u = xcd_remap(blockIdx.x, G);
   if (u >= U) return;
@@ -240,7 +244,7 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
   // This thread's A slots: rows (tid >> 3) + 32 i, k-quad (tid & 7).
   const int c4 = (tid & 7) * 4;
   auto rows_of = [&](int uu, int (&rr)[4]) {
-    const int m0 = (uu / ntn) * kSgBM;
+    const int m0 = rtile(uu) * kSgBM;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + (tid >> 3) + 32 * i;
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
     }
   };
   auto wptr = [&](int uu) {
-    const int s = seg_slot(seg, S, (uu / ntn) * kSgBM);
+    const int s = seg_slot(seg, S, rtile(uu) * kSgBM);
     return slot_weight(weight, root, nw, s, (size_t)K * Nn);
   };
   int rcur[4], rnext[4];
@@ -342,7 +346,7 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
       continue;
     }
     // C/D: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 h.
-    const int m0 = (u / ntn) * kSgBM;
+    const int m0 = rtile(u) * kSgBM;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -371,7 +375,8 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm_kernel(
 
 at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
                      const at::Tensor& seg, const at::Tensor& weight,
-                     const c10::optional<at::Tensor>& root, bool trans_w) {
+                     const c10::optional<at::Tensor>& root, bool trans_w,
+                     const c10::optional<at::Tensor>& tiles) {
   TORCH_CHECK(X.is_cuda() && X.scalar_type() == at::kFloat &&
                   X.is_contiguous() && X.dim() == 2,
               "slot_gemm: contiguous fp32 X");
@@ -397,6 +402,13 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
   TORCH_CHECK(P % kSgBM == 0 && src.scalar_type() == at::kInt,
               "slot_gemm: src [P_cap % 128]");
   if (trans_w) TORCH_CHECK(X.size(0) == P, "slot_gemm: dY_c rows == P_cap");
+  const bool listed = tiles.has_value() && tiles->defined();
+  if (listed)
+    TORCH_CHECK(tiles->scalar_type() == at::kInt &&
+                    tiles->numel() == P / kSgBM + 1,
+                "slot_gemm: tile list [P_cap / 128 + 1] (count last)");
+  const int* tl = listed ? tiles->data_ptr<int>() : nullptr;
+  const int tcap = (int)(P / kSgBM);
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(X.device());
   at::Tensor Y = at::empty({P, Nn}, X.options());
   // Persistent grid: 2 resident workgroups per CU (VGPR-limited; measured
@@ -410,15 +422,68 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
     hipLaunchKernelGGL(slot_gemm_kernel<true>, dim3(blocks), dim3(kSgThreads),
                        0, stream(), X.data_ptr<float>(), src.data_ptr<int>(),
                        seg.data_ptr<int>(), (int)S, weight.data_ptr<float>(),
-                       rp, (int)nw, (int)K, (int)Nn, Y.data_ptr<float>());
+                       rp, (int)nw, (int)K, (int)Nn, tl, tcap,
+                       Y.data_ptr<float>());
   else
     hipLaunchKernelGGL(slot_gemm_kernel<false>, dim3(blocks),
                        dim3(kSgThreads), 0, stream(), X.data_ptr<float>(),
                        src.data_ptr<int>(), seg.data_ptr<int>(), (int)S,
                        weight.data_ptr<float>(), rp, (int)nw, (int)K, (int)Nn,
-                       Y.data_ptr<float>());
+                       tl, tcap, Y.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return Y;
+}
+
+// Row tiles of the dX pass that hold sources j >= row0 (slot segments list
+// their sources in ascending j): lane k finds slot k's first such compact
+// row through posmap, the tiles from its row tile to the segment end are
+// listed in slot order; out[tcap] = count.
+__global__ __launch_bounds__(64) void sg_dx_tiles_kernel(
+    const int* __restrict__ posmap, const int* __restrict__ seg, int N, int S,
+    int row0, int tcap, int* __restrict__ out) {
+  const int k = threadIdx.x;
+  int first = 0, last = 0;
+  if (k < S) {
+    int p = seg[k + 1];
+    for (int j = row0; j < N; ++j) {
+      const int q = posmap[(size_t)j * S + k];
+      if (q >= 0) {
+        p = q;
+        break;
+      }
+    }
+    first = p / kSgBM;
+    last = seg[k + 1] / kSgBM;
+    if (first > last) first = last;
+  }
+  const int n = last - first;
+  int incl = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (k >= o) incl += v;
+  }
+  const int base = incl - n;
+  for (int t = 0; t < n && base + t < tcap; ++t) out[base + t] = first + t;
+  if (k == 63) out[tcap] = min(incl, tcap);
+}
+
+at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
+                         int64_t N, int64_t row0, int64_t P_cap) {
+  TORCH_CHECK(posmap.is_cuda() && posmap.scalar_type() == at::kInt &&
+                  seg.scalar_type() == at::kInt,
+              "slot_dx_tiles: int32 plan");
+  const int64_t S = seg.numel() - 1;
+  TORCH_CHECK(S <= 64 && posmap.numel() == N * S && P_cap % kSgBM == 0,
+              "slot_dx_tiles: plan shapes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(posmap.device());
+  const int64_t tcap = P_cap / kSgBM;
+  at::Tensor out = at::empty({tcap + 1}, posmap.options());
+  hipLaunchKernelGGL(sg_dx_tiles_kernel, dim3(1), dim3(64), 0, stream(),
+                     posmap.data_ptr<int>(), seg.data_ptr<int>(), (int)N,
+                     (int)S, (int)row0, (int)tcap, out.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  return out;
 }
 
 // ---------------------------------------------------------------------------
@@ -823,12 +888,18 @@ template <int LPR>
 __global__ __launch_bounds__(256) void sg_gather_sum_kernel(
     const int* __restrict__ posmap, const float* __restrict__ Z,
     const float* __restrict__ add, int lda, float* __restrict__ out, int N,
-    int S, int C) {
+    int S, int C, int row0) {
   constexpr int RPB = 256 / LPR;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int j = blk * RPB + threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   if (j >= N) return;
+  if (j < row0) {          // rows nobody reads the gradient of: zeros
+    for (int c0 = lane * 4; c0 < C; c0 += LPR * 4)
+      *reinterpret_cast<float4*>(out + (size_t)j * C + c0) =
+          make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
   const int* pm = posmap + (size_t)j * S;
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
     float4 acc = add ? ld4(add + (size_t)j * lda + c0)
@@ -846,7 +917,8 @@ __global__ __launch_bounds__(256) void sg_gather_sum_kernel(
 
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t N, int64_t S,
-                           const c10::optional<at::Tensor>& add) {
+                           const c10::optional<at::Tensor>& add,
+                           int64_t row0) {
   TORCH_CHECK(Z.is_cuda() && Z.scalar_type() == at::kFloat &&
                   Z.is_contiguous() && Z.dim() == 2 && Z.size(1) % 4 == 0 &&
                   aligned16(Z.data_ptr()),
@@ -874,7 +946,7 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
     hipLaunchKernelGGL(sg_gather_sum_kernel<L>, dim3(blocks), dim3(256), 0,
                        stream(), posmap.data_ptr<int>(), Z.data_ptr<float>(),
                        ap, (int)lda, out.data_ptr<float>(), (int)N, (int)S,
-                       (int)C);
+                       (int)C, (int)row0);
   };
   if (lanes <= 8) go(std::integral_constant<int, 8>());
   else if (lanes <= 16) go(std::integral_constant<int, 16>());

@@ -344,6 +344,12 @@ class DGMC(torch.nn.Module):
                     if pair is not None and self._fusable(self.psi_2):
                         if r_joint is None:
                             r_joint = torch.cat([r_s, r_t], dim=0)
+                        else:
+                            # [r_s; r_t] from the transport: only the r_t rows
+                            # carry a gradient (r_s is a random constant), so
+                            # psi_2's first layer skips the r_s input
+                            # gradient (ops/slot_gemm.py).
+                            r_joint._dgmc_dx_row0 = int(pair.n_s)
                         o = self.psi_2(r_joint, pair.edge_index,
                                        pair.edge_attr)
                         if isinstance(o, CatParts):

@@ -179,7 +179,8 @@ class SplineConv(torch.nn.Module):
             return slot_gemm.slot_gemm_spmm(
                 plan, x, self.weight, self.root, self.bias,
                 relu=(act == 'relu'), loop_key=(id(self), N, plan.num_cols),
-                passthrough=passthrough)
+                passthrough=passthrough,
+                dx_row0=getattr(x, '_dgmc_dx_row0', 0))
         w, w_lp = self.stacked_operands(dtype, x, plan)
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),

@@ -49,6 +49,16 @@ class CompactPlan(object):
         self.S, self.N, self.P_cap = S, N, P_cap
 
 
+def dx_tiles(plan, row0):
+    """Row-tile list of the dX pass for sources ``j >= row0`` (cached)."""
+    cache = plan.__dict__.setdefault('_dx_tiles', {})
+    t = cache.get(row0)
+    if t is None:
+        t = cache[row0] = _backend.ops().slot_dx_tiles(
+            plan.posmap, plan.seg, plan.N, row0, plan.P_cap)
+    return t
+
+
 def compact_plan(op, S):
     cache = op.__dict__.setdefault('_compact_plan', {})
     p = cache.get(S)
@@ -91,7 +101,8 @@ def weight_grad(xs, dys, plan, cin, cout):
 class _SlotGemmSpMM(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, weight, root, bias, op, relu, loop, passthrough):
+    def forward(ctx, x, weight, root, bias, op, relu, loop, passthrough,
+                dx_row0=0):
         S = weight.size(0) + (1 if root is not None else 0)
         plan = compact_plan(op, S)
         xc = x.contiguous()
@@ -106,6 +117,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
                            bias, relu, torch.float32)
         ctx.save_for_backward(xc, weight, root, out if relu else None)
         ctx.op, ctx.plan, ctx.relu, ctx.loop = op, plan, relu, loop
+        ctx.dx_row0 = int(dx_row0)
         ctx.has_root = root is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.idx = loop.register() if loop is not None else None
@@ -116,7 +128,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad, gpass=None):
         x, weight, root, out = ctx.saved_tensors
-        nones = (None, ) * 4
+        nones = (None, ) * 5
         op, plan, loop, idx = ctx.op, ctx.plan, ctx.loop, ctx.idx
         ops = _backend.ops()
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
@@ -136,17 +148,24 @@ class _SlotGemmSpMM(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # K = 128 (psi_2): the register-staged v1 kernel streams dY_c
             # faster than the LDS-DMA one (51 vs 57 us per call,
-            # tools/bench_slot_gemm.py); longer K: v2.
-            kern = ops.slot_gemm2 if weight.size(2) >= 256 else \
-                lambda *a: ops.slot_gemm(*a[:5], True)
-            Z = kern(dyc, plan.src, plan.seg, weight.contiguous(),
-                     root.contiguous() if root is not None else None, False)
+            # tools/bench_slot_gemm.py); longer K: v2.  Rows below
+            # ``dx_row0`` (psi_2's random r_s half) need no input gradient:
+            # only the row tiles of sources >= dx_row0 are multiplied.
+            row0 = ctx.dx_row0 if weight.size(2) < 256 else 0
+            wc = weight.contiguous()
+            rc = root.contiguous() if root is not None else None
+            if weight.size(2) >= 256:
+                Z = ops.slot_gemm2(dyc, plan.src, plan.seg, wc, rc, False)
+            else:
+                Z = ops.slot_gemm(dyc, plan.src, plan.seg, wc, rc, True,
+                                  dx_tiles(plan, row0) if row0 > 0 else None)
             add = gpass if (gpass is not None and
                             gpass.dtype == torch.float32 and gpass.dim() == 2
                             and gpass.stride(1) == 1 and
                             gpass.stride(0) % 4 == 0 and
                             gpass.data_ptr() % 16 == 0) else None
-            gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add)
+            gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add,
+                                     row0)
             if gpass is not None and add is None:
                 gx = gx + gpass
         elif gpass is not None:
@@ -182,15 +201,16 @@ class _SlotGemmSpMM(torch.autograd.Function):
 
 
 def slot_gemm_spmm(op, x, weight, root, bias=None, relu=False, loop_key=None,
-                   passthrough=False):
+                   passthrough=False, dx_row0=0):
     r"""``act(A (x @ [W_0 | .. | W_{K-1} | root]).view(-1, C) + bias)`` in
     fp32 on the used ``(node, slot)`` pairs only; ``weight [K, in, out]``,
     ``root [in, out]`` are read in place (reference checkpoint layout).
     ``passthrough`` returns ``(out, x')`` (``x'`` aliases ``x``; its
-    gradient is added inside this op's dX kernel)."""
+    gradient is added inside this op's dX kernel).  ``dx_row0``: the input
+    gradient of rows ``< dx_row0`` is not needed (returned as zeros)."""
     from ..runtime import loopgrad
     loop = loopgrad.group(('slot_gemm', ) + tuple(loop_key)) \
         if loop_key is not None else None
     with torch.autocast(device_type='cuda', enabled=False):
         return _SlotGemmSpMM.apply(x, weight, root, bias, op, relu, loop,
-                                   passthrough)
+                                   passthrough, dx_row0)

@@ -131,3 +131,25 @@ def test_passthrough_gradient_added():
     out2 = sg.slot_gemm_spmm(op, x, w, r, b, relu=True)
     gx2, = torch.autograd.grad(out2.square().sum() + (x * 3).sum(), (x, ))
     assert _rel(gx, gx2) < 1e-6
+
+
+@pytest.mark.parametrize('row0', [1, 237, 599])
+def test_dx_row0_matches_full_rows(row0):
+    """``dx_row0`` (psi_2's r_s half needs no input gradient): the listed
+    row tiles give the full input gradient on rows >= row0, zeros below;
+    the weight gradients are unchanged."""
+    n, e, C = 600, 2400, 128
+    ei, pseudo = _graph(n, e, seed=11)
+    op = spline_plan(ei, pseudo, n, (5, 5), (1, 1), 1, root=True)
+    w, r, b = _params(C, C, seed=4)
+    x = torch.randn(n, C, device=DEV, requires_grad=True)
+    g = torch.randn(n, C, device=DEV)
+    full = torch.autograd.grad(
+        sg.slot_gemm_spmm(op, x, w, r, b, relu=True), (x, w, r, b), g)
+    part = torch.autograd.grad(
+        sg.slot_gemm_spmm(op, x, w, r, b, relu=True, dx_row0=row0),
+        (x, w, r, b), g)
+    assert torch.equal(part[0][row0:], full[0][row0:])
+    assert not part[0][:row0].any()
+    for a, bb in zip(part[1:], full[1:]):
+        assert torch.equal(a, bb)
