@@ -59,6 +59,43 @@ __device__ __forceinline__ int seg_slot(const int* __restrict__ seg, int S,
   return s;
 }
 
+// XCD-local row groups of the compact row space: the rows of every slot
+// segment are ordered by source node, so the x-th eighth of each segment
+// covers (about) the x-th eighth of the nodes; work dispatched to XCD x
+// (block id % 8, round-robin dispatch) takes those rows of every slot, and
+// the node rows it gathers (X at the sources, g' at their neighbours) stay
+// within one eighth of the graph batch - XCD x's L2 (rowmap SpMM 40 -> 25
+// us per psi_2 call).  Units are `unit` rows (a multiple dividing every
+// segment length); returns the first row of XCD x's i-th unit (-1 past the
+// end) and, in *total, XCD x's unit count.  Wave-wide: lane s holds slot
+// s's count, an inclusive shuffle scan locates the slot (no serial loop).
+__device__ __forceinline__ int sg_xcd_unit(const int* __restrict__ seg, int S,
+                                           int x, int i, int unit,
+                                           int* total = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const int sv = lane <= S ? seg[lane] : 0;
+  const int sn = __shfl_down(sv, 1);
+  int lo = 0, cnt = 0;
+  if (lane < S) {
+    const int q = (sn - sv) / unit;
+    lo = q * x / kNumXcd;
+    cnt = q * (x + 1) / kNumXcd - lo;
+  }
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (total != nullptr) *total = __shfl(incl, S - 1);
+  const unsigned long long hit = __ballot(lane < S && incl > i);
+  if (hit == 0ull) return -1;
+  const int sl = __ffsll((long long)hit) - 1;
+  const int base = __shfl(sv, sl), first = __shfl(lo, sl),
+            before = __shfl(incl - cnt, sl);
+  return base + (first + i - before) * unit;
+}
+
 __device__ __forceinline__ const float* slot_weight(const float* weight,
                                                     const float* root,
                                                     int nw, int s,
@@ -799,19 +836,27 @@ at::Tensor slot_weight_t(const at::Tensor& weight,
 // val[e] * g[col[e], :]  (zero for cinv[p] < 0) - dY_c = A_c^T g' straight
 // from the assembled A^T (rows j*S + k) without re-indexing it.
 // ---------------------------------------------------------------------------
-template <int LPR>
+template <int LPR, bool XL>
 __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ val, const int* __restrict__ cinv,
-    const int* __restrict__ tot, const float* __restrict__ g,
+    const int* __restrict__ seg, int S, const float* __restrict__ g,
     float* __restrict__ out, int P, int C) {
   constexpr int RPB = 256 / LPR;
-  const int blk = xcd_remap(blockIdx.x, gridDim.x);
-  const int p = blk * RPB + threadIdx.x / LPR;
+  int p;
+  if (XL) {
+    const int r0 = sg_xcd_unit(seg, S, blockIdx.x % kNumXcd,
+                               blockIdx.x / kNumXcd, RPB);
+    if (r0 < 0) return;
+    p = r0 + threadIdx.x / LPR;
+  } else {
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    p = blk * RPB + threadIdx.x / LPR;
+  }
   const int lane = threadIdx.x % LPR;
   // Rows past the last slot segment are never read (slot_gemm / wgrad stop
   // at seg[S]); padding rows inside segments are written as zeros.
-  if (p >= P || (tot != nullptr && p >= *tot)) return;
+  if (p >= P || (seg != nullptr && p >= seg[S])) return;
   const int c = cinv[p];
   const int e0 = c >= 0 ? rowptr[c] : 0, e1 = c >= 0 ? rowptr[c + 1] : 0;
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
@@ -859,16 +904,26 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
   const int64_t P = cinv.numel(), C = g.size(1);
   at::Tensor out = at::empty({P, C}, g.options());
   if (P == 0) return out;
-  const int* totp = nullptr;
-  if (seg.has_value() && seg->defined())
-    totp = seg->data_ptr<int>() + (seg->numel() - 1);
+  const int* segp = nullptr;
+  int S = 0;
+  if (seg.has_value() && seg->defined()) {
+    segp = seg->data_ptr<int>();
+    S = (int)seg->numel() - 1;
+  }
+  const bool xl = segp != nullptr;      // XCD-local row groups (above)
   const int lanes = (int)(C / 4);
   auto go = [&](auto lpr) {
     constexpr int L = decltype(lpr)::value;
-    const int64_t blocks = (P + 256 / L - 1) / (256 / L);
-    hipLaunchKernelGGL(sg_spmm_rowmap_kernel<L>, dim3(blocks), dim3(256), 0,
-                       stream(), rowptr.data_ptr<int>(), col.data_ptr<int>(),
-                       val.data_ptr<float>(), cinv.data_ptr<int>(), totp,
+    constexpr int RPB = 256 / L;
+    // XCD-local groups: every slot's eighth is a whole number of groups, so
+    // per XCD at most P / RPB / 8 + S groups.
+    const int64_t blocks = xl ? (P / RPB / kNumXcd + S + 1) * kNumXcd
+                              : (P + RPB - 1) / RPB;
+    auto kern = xl ? sg_spmm_rowmap_kernel<L, true>
+                   : sg_spmm_rowmap_kernel<L, false>;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream(),
+                       rowptr.data_ptr<int>(), col.data_ptr<int>(),
+                       val.data_ptr<float>(), cinv.data_ptr<int>(), segp, S,
                        g.data_ptr<float>(), out.data_ptr<float>(), (int)P,
                        (int)C);
   };
