@@ -240,7 +240,7 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t row0);
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
-                          int64_t chunk);
+                          int64_t rounds);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
     const at::Tensor& S_hat, const at::Tensor& n_s, const at::Tensor& n_t,
     int64_t iters, double tau);
@@ -427,7 +427,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "int row0=0) -> Tensor");
   m.def(
       "slot_wgrad_f32(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
-      "chunk) -> Tensor");
+      "rounds) -> Tensor");
   m.def(
       "sinkhorn_fwd(Tensor S_hat, Tensor n_s, Tensor n_t, int iters, float "
       "tau) -> (Tensor, Tensor, Tensor)");

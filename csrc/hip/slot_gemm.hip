@@ -1022,20 +1022,27 @@ struct SgUses {
   const float* g[kSgMaxU];
 };
 
-// Item table: item i -> (slot, first row, end row); ib[s] = first item of s.
-// One wave: lane s counts its slot's items, a ballot-free shuffle scan gives
-// the first item of each slot, then every lane fills the table.
+// Item table: item i -> (slot, first step, end step); ib[s] = first item of
+// slot s.  A slot's steps are its 32-row chunks x uses (chunk-major).  The
+// steps per item Q balance the work: with `target` items (one or two rounds
+// of resident workgroups) every slot is cut into ceil(steps / Q) pieces,
+// Q = ceil(total / (target - S)) so that at most `target` items exist, capped
+// by the LDS index buffer (qcap steps).  One wave: lane s owns slot s.
 __global__ __launch_bounds__(64) void sg_items_kernel(
-    const int* __restrict__ seg, int S, int CH, int G_cap,
-    int* __restrict__ items, int* __restrict__ ib) {
+    const int* __restrict__ seg, int S, int nu, int target, int qcap,
+    int G_cap, int* __restrict__ items, int* __restrict__ ib) {
   const int lane = threadIdx.x;
-  const int span = CH * kSgBM;
-  int n = 0, b = 0, e = 0;
+  int b = 0, steps = 0;
   if (lane < S) {
     b = seg[lane];
-    e = seg[lane + 1];
-    n = (e - b + span - 1) / span;
+    steps = (seg[lane + 1] - b) / 32 * nu;
   }
+  int tot = steps;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  int Q = target > S ? (tot + target - S - 1) / (target - S) : tot;
+  Q = max(1, min(Q, qcap));
+  const int n = (steps + Q - 1) / Q;
   int incl = n;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1045,34 +1052,80 @@ __global__ __launch_bounds__(64) void sg_items_kernel(
   const int first = incl - n;
   const int total = __shfl(incl, 63);
   if (lane < S) {
-    ib[lane] = first;
+    ib[lane] = min(first, G_cap);
     for (int q = 0; q < n && first + q < G_cap; ++q) {
-      const int r = b + q * span;
       items[3 * (first + q) + 0] = lane;
-      items[3 * (first + q) + 1] = r;
-      items[3 * (first + q) + 2] = min(r + span, e);
+      items[3 * (first + q) + 1] = q * Q;
+      items[3 * (first + q) + 2] = min((q + 1) * Q, steps);
     }
   }
   if (lane == 0) ib[S] = min(total, G_cap);
   for (int i = total + lane; i < G_cap; i += 64) items[3 * i + 0] = -1;
 }
 
-__global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(
+// Weight gradient: the TN product on LDS-DMA double-buffered operands.
+// Work item (slot, CH row tiles) x output tile (i0, n0); the K loop runs over
+// (32-row chunk, use) steps, chunk-major, so a chunk's gather indices (staged
+// once per item in LDS) serve every use.  The accumulator holds dW^T (A
+// operand = dY rows, B operand = X rows: a lane owns one input channel i and
+// four consecutive output channels per register quad), so the partial tile
+// is written with float4 stores.  Fragment reads are one ds_read_b32 per
+// operand per MFMA step (lanes read 32 consecutive floats of one row: no
+// bank conflicts on the lane-linear DMA image).
+constexpr int kW2Rows = 32;                  // p rows per step
+constexpr int kW2MaxRows = 3072;             // gathered rows per item (LDS)
+
+__global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad2_kernel(
     SgUses U, int nu, const int* __restrict__ src,
-    const int* __restrict__ items, int Kin, int C,
-    float* __restrict__ part) {
-  __shared__ float As[kSgBK * kSgNP];     // [p][i]
-  __shared__ float Bs[kSgBK * kSgNP];     // [p][c]
+    const int* __restrict__ seg, const int* __restrict__ items, int Kin,
+    int C, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float sX0_[kW2Rows * 128];
+  __shared__ __attribute__((aligned(16))) float sX1_[kW2Rows * 128];
+  __shared__ __attribute__((aligned(16))) float sG0_[kW2Rows * 128];
+  __shared__ __attribute__((aligned(16))) float sG1_[kW2Rows * 128];
+  __shared__ int sidx[kW2MaxRows];
+  DGMC_LDS float* sX0 = (DGMC_LDS float*)sX0_;
+  DGMC_LDS float* sX1 = (DGMC_LDS float*)sX1_;
+  DGMC_LDS float* sG0 = (DGMC_LDS float*)sG0_;
+  DGMC_LDS float* sG1 = (DGMC_LDS float*)sG1_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wn = wave & 1, wm = wave >> 1;
   const int tiles_n = C / kSgBN, tiles = (Kin / kSgBM) * tiles_n;
   const int item = blockIdx.x / tiles, t = blockIdx.x % tiles;
   const int i0 = (t / tiles_n) * kSgBM, n0 = (t % tiles_n) * kSgBN;
-  float* outp = part + ((size_t)item * Kin + i0) * C + n0;
   const int s = items[3 * item];
-  const int l32 = lane & 31, h = lane >> 5;
   if (s < 0) return;
-  const int pb = items[3 * item + 1], pe = items[3 * item + 2];
+  // Steps [qb, qe) of slot s: chunk q / nu (32 rows from seg[s]), use
+  // q % nu.  The gather indices of the item's chunks are staged once.
+  const int qb = items[3 * item + 1], qe = items[3 * item + 2];
+  const int c0 = qb / nu;
+  const int pb = seg[s] + c0 * kW2Rows;
+  const int nrows = ((qe - 1) / nu - c0 + 1) * kW2Rows;
+  for (int r = tid; r < nrows; r += kSgThreads) {
+    const int j = src[pb + r];
+    sidx[r] = j < 0 ? 0 : j;          // padding rows: dY row is zero
+  }
+  __syncthreads();
+  const int total = qe - qb;
+
+  // Staging: wave w's pieces j = 0..3 cover rows 8 w + 2 j + (lane >> 5),
+  // 16 B at column 4 (lane & 31) (lane-linear: no swizzle needed).
+  const int prow = lane >> 5, pc = 4 * (lane & 31);
+  auto stage = [&](int q, DGMC_LDS float* dx, DGMC_LDS float* dg) {
+    const int qq = qb + q;
+    const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
+    const float* Xu = U.x[u];
+    const float* Gu = U.g[u];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 8 * wave + 2 * j + prow;
+      const int row = ch * kW2Rows + r;
+      sg_dma16(Xu + (size_t)sidx[row] * Kin + i0 + pc,
+               dx + (8 * wave + 2 * j) * 128);
+      sg_dma16(Gu + (size_t)(pb + row) * C + n0 + pc,
+               dg + (8 * wave + 2 * j) * 128);
+    }
+  };
 
   sg_f32x16 acc[2][2];
 #pragma unroll
@@ -1081,65 +1134,16 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  // Tiles: 32 p-rows x 128 columns, 4 float4 per thread (32 lanes per row:
-  // rows (tid >> 5) + 8 i).  The gather indices of chunk q + 1 are loaded
-  // one chunk ahead, so a chunk's row loads never wait on their index load.
-  // (A second register set, loading rows two chunks ahead, measured slower:
-  // 485 vs 471 us for psi_2's 10-use gradient, tools/bench_slot_gemm.py.)
-  float4 ra[4], rb[4];
-  const int nchunk = (pe - pb) / kSgBK;
-  const int total = nchunk * nu;
-  const int c4 = (tid & 31) * 4;
-  auto prow = [&](int q, int i) {
-    return pb + (q % nchunk) * kSgBK + (tid >> 5) + 8 * i;
-  };
-  int rs[4];
-  auto load_idx = [&](int q) {
+  const int l32 = lane & 31, h = lane >> 5;
+  auto compute = [&](const DGMC_LDS float* lx, const DGMC_LDS float* lg) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rs[i] = q < total ? src[prow(q, i)] : -1;
-  };
-  auto load = [&](int q) {
-    const int u = q / nchunk;
-    const float* Xu = U.x[u];
-    const float* Gu = U.g[u];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = rs[i];
-      const float4 v = ld4(Xu + (size_t)(r < 0 ? 0 : r) * Kin + i0 + c4);
-      ra[i] = r < 0 ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
-      rb[i] = ld4(Gu + (size_t)prow(q, i) * C + n0 + c4);
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + kSgThreads * i;
-      const int o = (idx >> 5) * kSgNP + (idx & 31) * 4;
-      *reinterpret_cast<float4*>(As + o) = ra[i];
-      *reinterpret_cast<float4*>(Bs + o) = rb[i];
-    }
-  };
-  load_idx(0);
-  if (total > 0) load(0);
-  load_idx(1);
-  for (int q = 0; q < total; ++q) {
-    store();
-    __syncthreads();
-    if (q + 1 < total) {
-      load(q + 1);
-      load_idx(q + 2);
-    }
-#pragma unroll
-    for (int st = 0; st < kSgBK / 2; ++st) {
+    for (int st = 0; st < kW2Rows / 2; ++st) {
       const int kk = 2 * st + h;
       float av[2], bv[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
-        av[a] = As[kk * kSgNP + wm * 64 + a * 32 + l32];
+      for (int a = 0; a < 2; ++a) av[a] = lg[kk * 128 + wn * 64 + a * 32 + l32];
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-        bv[b] = Bs[kk * kSgNP + wn * 64 + b * 32 + l32];
+      for (int b = 0; b < 2; ++b) bv[b] = lx[kk * 128 + wm * 64 + b * 32 + l32];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1147,18 +1151,43 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad_tn_kernel(
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b],
                                                            acc[a][b], 0, 0, 0);
     }
-    __syncthreads();
-  }
+  };
+
+  if (total > 0) stage(0, sX0, sG0);
+  int q = 0;
+  auto step = [&](DGMC_LDS float* cx, DGMC_LDS float* cg, DGMC_LDS float* nx,
+                  DGMC_LDS float* ng) -> bool {
+    const bool more = q + 1 < total;
+    if (more) {
+      stage(q + 1, nx, ng);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sg_raw_barrier();
+    compute(cx, cg);
+    sg_raw_barrier();
+    ++q;
+    return more;
+  };
+  if (total > 0)
+    while (step(sX0, sG0, sX1, sG1) && step(sX1, sG1, sX0, sG0)) {
+    }
+  // acc[a][b]: rows c = wn 64 + 32 a + 8 qd + 4 h + e, column i = wm 64 +
+  // 32 b + l32.
+  float* outp = part + (size_t)item * Kin * C;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b) {
+      float* row = outp + (size_t)(i0 + wm * 64 + b * 32 + l32) * C + n0 +
+                   wn * 64 + a * 32 + 4 * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int c = wn * 64 + b * 32 + l32;
-        outp[(size_t)row * C + c] = acc[a][b][r];
-      }
+      for (int qd = 0; qd < 4; ++qd)
+        *reinterpret_cast<float4*>(row + 8 * qd) =
+            make_float4(acc[a][b][4 * qd], acc[a][b][4 * qd + 1],
+                        acc[a][b][4 * qd + 2], acc[a][b][4 * qd + 3]);
+    }
 }
 
 // out[s] = sum_{items of s, in order} part[item]  (float4 per thread).
@@ -1178,14 +1207,14 @@ __global__ __launch_bounds__(256) void sg_fold_kernel(
 
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
-                          int64_t chunk) {
+                          int64_t rounds) {
   const int64_t nu = (int64_t)xs.size();
   TORCH_CHECK(nu >= 1 && nu <= kSgMaxU && (int64_t)gs.size() == nu,
               "slot_wgrad_f32: 1 <= uses <= 16, one G per X");
   const int64_t Kin = xs[0].size(1), C = gs[0].size(1);
   const int64_t P = src.numel(), S = seg.numel() - 1;
   TORCH_CHECK(Kin % kSgBM == 0 && C % kSgBN == 0 && P % kSgBM == 0 &&
-                  chunk >= 1 && S <= kSgMaxS,
+                  rounds >= 1 && S <= kSgMaxS,
               "slot_wgrad_f32: in/out multiples of 128");
   SgUses U{};
   for (int64_t u = 0; u < nu; ++u) {
@@ -1203,21 +1232,28 @@ at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
     U.g[u] = g.data_ptr<float>();
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
-  const int64_t G_cap = P / (kSgBM * chunk) + S;
+  // Items: `rounds` rounds of two resident workgroups per CU; steps per item
+  // capped so an item's rows fit the LDS index buffer.
+  const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
+  const int64_t target = std::max<int64_t>(
+      1, rounds * 2 * (int64_t)num_cus(src.device().index()) / tiles);
+  const int64_t qcap = (kW2MaxRows / kW2Rows - 2) * nu;
+  const int64_t G_cap = target + (P / kW2Rows * nu + qcap - 1) / qcap + S;
   auto i32 = src.options();
   at::Tensor items = at::empty({G_cap, 3}, i32);
   at::Tensor ib = at::empty({S + 1}, i32);
   hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
-                     seg.data_ptr<int>(), (int)S, (int)chunk, (int)G_cap,
-                     items.data_ptr<int>(), ib.data_ptr<int>());
+                     seg.data_ptr<int>(), (int)S, (int)nu, (int)target,
+                     (int)qcap, (int)G_cap, items.data_ptr<int>(),
+                     ib.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
   const int64_t per = Kin * C;
   at::Tensor part = at::empty({G_cap, per}, xs[0].options());
-  const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
-  hipLaunchKernelGGL(slot_wgrad_tn_kernel, dim3(G_cap * tiles),
+  hipLaunchKernelGGL(slot_wgrad2_kernel, dim3(G_cap * tiles),
                      dim3(kSgThreads), 0, stream(), U, (int)nu,
-                     src.data_ptr<int>(), items.data_ptr<int>(), (int)Kin,
-                     (int)C, part.data_ptr<float>());
+                     src.data_ptr<int>(), seg.data_ptr<int>(),
+                     items.data_ptr<int>(), (int)Kin, (int)C,
+                     part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   at::Tensor out = at::empty({S, Kin, C}, xs[0].options());
   hipLaunchKernelGGL(sg_fold_kernel, dim3((per / 4 + 255) / 256, S), dim3(256),

@@ -79,21 +79,24 @@ def supported(op, x, weight, root):
             op.num_cols == x.size(0) * S and op.num_rows == x.size(0))
 
 
-def _wgrad_chunk(P_cap, cin, cout):
-    """Row tiles per weight-gradient work item: ~2048 workgroups."""
-    tiles = (cin // 128) * (cout // 128)
-    return max(1, (P_cap // BM) * tiles // 2048)
-
-
 def weight_grad(xs, dys, plan, cin, cout):
-    """``dW [S, in, out]`` = ``sum_u X_u[src]^T dY_c,u`` per slot."""
+    """``dW [S, in, out]`` = ``sum_u X_u[src]^T dY_c,u`` per slot: balanced
+    work items (one round of resident workgroups for a single 128x128 output
+    tile, two otherwise), per-item partials folded in item order."""
     ops = _backend.ops()
-    chunk = _wgrad_chunk(plan.P_cap, cin, cout)
+    # Rounds of resident workgroups the items are sized for, by output tiles
+    # (tools/bench_slot_gemm.py sweep, 1 / 2 / 3 / 4 / 6 rounds: 128->128
+    # 387 / 407 / 420 / 440 / 467 us, 256->256 178 / 174 / 179 / 184 / 205
+    # us, 1024->256 737 / 720 / 599 / 623 / 573 us; 8 / 12 / 16 rounds: 587
+    # / 623 / 653 us).
+    tiles = (cin // 128) * (cout // 128)
+    rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
+    rounds = int(os.environ.get('DGMC_WG_ROUNDS_%d' % cin, rounds))
     out = None
     for i in range(0, len(xs), MAX_USES):
         part = ops.slot_wgrad_f32(list(xs[i:i + MAX_USES]),
                                   list(dys[i:i + MAX_USES]), plan.src,
-                                  plan.seg, chunk)
+                                  plan.seg, rounds)
         out = part if out is None else out.add_(part)
     return out
 

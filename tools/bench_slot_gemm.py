@@ -86,11 +86,12 @@ def main():
         wt = ops.slot_weight_t(w, r)
         y2 = ops.slot_gemm2(x, plan.src, plan.seg, wt, None, True)
         y2 = y2[:used][valid]
-        ref = (x.double()[plan.src[:used][valid].long()].unsqueeze(1) @ (
-            torch.cat([w, r[None]]).double()[slot_ids(plan, used)[valid]])
-        ).squeeze(1)
-        print('    v1 err %.2e  v2 err %.2e (rel. to max |Y|)' % (
-            rel(y1, ref), rel(y2, ref)))
+        if cin * cout <= 256 * 256:      # (fp64 oracle memory)
+            ref = (x.double()[plan.src[:used][valid].long()].unsqueeze(1) @ (
+                torch.cat([w, r[None]]).double()[slot_ids(plan, used)[valid]])
+            ).squeeze(1)
+            print('    v1 err %.2e  v2 err %.2e (rel. to max |Y|)' % (
+                rel(y1, ref), rel(y2, ref)))
         t = timeit(lambda: ops.slot_gemm2(x, plan.src, plan.seg, wt, None,
                                           True), args.reps)
         print('%4d->%-4d fwd2  %8.1f us  %6.1f TF/s' % (cin, cout, t,
@@ -107,12 +108,14 @@ def main():
                                          True), args.reps)
         print('%4d->%-4d dX    %8.1f us  %6.1f TF/s' % (cin, cout, t,
                                                        flop / t / 1e6))
-        z1 = ops.slot_gemm(dyc, plan.src, plan.seg, w, r, True)[:used]
-        z2 = ops.slot_gemm2(dyc, plan.src, plan.seg, w, r, False)[:used]
-        ref = (dyc[:used].double().unsqueeze(1) @ torch.cat(
-            [w, r[None]]).double()[slot_ids(plan, used)].transpose(1, 2)
-        ).squeeze(1)
-        print('    v1 err %.2e  v2 err %.2e' % (rel(z1, ref), rel(z2, ref)))
+        if cin * cout <= 256 * 256:      # (fp64 oracle memory)
+            z1 = ops.slot_gemm(dyc, plan.src, plan.seg, w, r, True)[:used]
+            z2 = ops.slot_gemm2(dyc, plan.src, plan.seg, w, r, False)[:used]
+            ref = (dyc[:used].double().unsqueeze(1) @ torch.cat(
+                [w, r[None]]).double()[slot_ids(plan, used)].transpose(1, 2)
+            ).squeeze(1)
+            print('    v1 err %.2e  v2 err %.2e' % (rel(z1, ref),
+                                                  rel(z2, ref)))
         t = timeit(lambda: ops.slot_gemm2(dyc, plan.src, plan.seg, w, r,
                                           False), args.reps)
         print('%4d->%-4d dX2   %8.1f us  %6.1f TF/s' % (cin, cout, t,

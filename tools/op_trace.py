@@ -58,19 +58,22 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument('--out', default=None)
     p.add_argument('--batch-size', type=int, default=512)
+    p.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16'])
     args = p.parse_args()
+    bf16 = args.dtype == 'bf16'
     device = parallel.init_distributed()
     torch.manual_seed(0)
     cfg = bench.CONFIGS['pascal']
     groups = make_keypoint_datasets(cfg['categories'], graphs=128,
                                     visible_prob=cfg['visible_prob'], seed=0)
-    store = GraphStore(groups, device, x_dtype=torch.bfloat16,
+    store = GraphStore(groups, device,
+                       x_dtype=torch.bfloat16 if bf16 else torch.float32,
                        valid_pairs=True)
     bargs = bench.parse_args([])
     model = bench.build_model(cfg, bargs, groups[0].num_node_features,
                               groups[0].num_edge_features, device)
     trainer = PairTrainer(model, store, args.batch_size, mode='static',
-                          bf16=device.type == 'cuda', buckets=False)
+                          bf16=bf16 and device.type == 'cuda', buckets=False)
     for _ in range(2):
         trainer.step()
     bucket = trainer._load_next()
