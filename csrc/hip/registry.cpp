@@ -230,6 +230,9 @@ at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
                       const c10::optional<at::Tensor>& broot, bool gather);
 at::Tensor slot_weight_t(const at::Tensor& weight,
                          const c10::optional<at::Tensor>& root);
+at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt);
+at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
+                           at::TensorList gs, const at::Tensor& seg01);
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
@@ -419,6 +422,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm2(Tensor X, Tensor src, Tensor seg, Tensor bt, Tensor? "
       "broot, bool gather) -> Tensor");
   m.def("slot_weight_t(Tensor weight, Tensor? root) -> Tensor");
+  m.def("dense_nt_f32(Tensor[] parts, Tensor bt) -> Tensor");
+  m.def(
+      "dense_wgrad_f32(Tensor[] xparts, int nparts, Tensor[] gs, Tensor "
+      "seg01) -> Tensor");
   m.def(
       "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
       "Tensor g, Tensor? seg=None) -> Tensor");
@@ -496,6 +503,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_gemm2", &dgmc::slot_gemm2);
   m.impl("slot_dx_tiles", &dgmc::slot_dx_tiles);
   m.impl("slot_weight_t", &dgmc::slot_weight_t);
+  m.impl("dense_nt_f32", &dgmc::dense_nt_f32);
+  m.impl("dense_wgrad_f32", &dgmc::dense_wgrad_f32);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);

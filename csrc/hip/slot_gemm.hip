@@ -787,6 +787,197 @@ at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
   return Y;
 }
 
+// ---------------------------------------------------------------------------
+// Dense fp32 NT GEMM on the same LDS-DMA pipeline:
+//   Y[M, Nn] = [A_0 | A_1 | ...] Bt^T,  A_j [M, 128] contiguous (up to 4
+//   parts read in place - psi_2's concatenated features never formed),
+//   Bt [Nn, K] k-contiguous, K = 128 * parts.
+// Rows past M are clamped on load and not stored.
+// ---------------------------------------------------------------------------
+struct DnParts {
+  const float* p[4];
+};
+
+// MB / NB: 32-row blocks per wave along M / N (tile (64 MB) x (64 NB));
+// 64 x 64 tiles for skinny products (the [M, 384] x [384, 128] projection
+// has only M / 128 tiles of 128 x 128).
+template <int MB, int NB>
+__global__ __launch_bounds__(kSgThreads, 2) void dense_nt_f32_kernel(
+    DnParts A, int M, const float* __restrict__ bt, int K, int Nn,
+    float* __restrict__ Y) {
+  constexpr int TM = 64 * MB, TN = 64 * NB;
+  __shared__ __attribute__((aligned(16))) float sA0_[TM * kG2BK];
+  __shared__ __attribute__((aligned(16))) float sA1_[TM * kG2BK];
+  __shared__ __attribute__((aligned(16))) float sB0_[TN * kG2BK];
+  __shared__ __attribute__((aligned(16))) float sB1_[TN * kG2BK];
+  DGMC_LDS float* sA0 = (DGMC_LDS float*)sA0_;
+  DGMC_LDS float* sA1 = (DGMC_LDS float*)sA1_;
+  DGMC_LDS float* sB0 = (DGMC_LDS float*)sB0_;
+  DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int ntn = Nn / TN, nk = K / kG2BK;
+  const int U = ((M + TM - 1) / TM) * ntn;
+  const int G = gridDim.x;
+  int u = xcd_remap(blockIdx.x, G);
+  if (u >= U) return;
+
+  // Staging: wave w's A pieces j < 2 MB cover rows (2 MB) 8 w + 8 j + lane /
+  // 8, its B pieces j < 2 NB rows (2 NB) 8 w + 8 j + lane / 8.
+  const int prow = lane >> 3;
+  auto swz = [&](int row) { return 4 * ((lane & 7) ^ ((row >> 1) & 7)); };
+  int arow[2 * MB];
+  const float* brow;
+  auto tile_ptrs = [&](int uu) {
+    const int m0 = (uu / ntn) * TM, n0 = (uu % ntn) * TN;
+#pragma unroll
+    for (int j = 0; j < 2 * MB; ++j)
+      arow[j] = min(m0 + 16 * MB * wave + 8 * j + prow, M - 1);
+    brow = bt + (size_t)(n0 + 16 * NB * wave + prow) * K;
+  };
+  auto stage = [&](int kc, DGMC_LDS float* da, DGMC_LDS float* db) {
+    const int k0 = kc * kG2BK;
+    const float* part = A.p[k0 >> 7];
+    const int kp = k0 & 127;
+#pragma unroll
+    for (int j = 0; j < 2 * MB; ++j) {
+      const int row = 16 * MB * wave + 8 * j + prow;
+      sg_dma16(part + (size_t)arow[j] * 128 + kp + swz(row),
+               da + (16 * MB * wave + 8 * j) * kG2BK);
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int row = 16 * NB * wave + 8 * j + prow;
+      sg_dma16(brow + (size_t)8 * j * K + k0 + swz(row),
+               db + (16 * NB * wave + 8 * j) * kG2BK);
+    }
+  };
+  const int i = lane & 31, h = lane >> 5, sw = (i >> 1) & 7;
+  int qoff[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) qoff[g] = 4 * ((2 * g + h) ^ sw);
+  const int offN = (wn * 32 * NB + i) * kG2BK;
+  const int offM = (wm * 32 * MB + i) * kG2BK;
+  sg_f32x16 acc[NB][MB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      sg_f32x4 fa[NB], fb[MB];
+#pragma unroll
+      for (int a = 0; a < NB; ++a)
+        fa[a] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+            lb + offN + a * 32 * kG2BK + qoff[g]);
+#pragma unroll
+      for (int b = 0; b < MB; ++b)
+        fb[b] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+            la + offM + b * 32 * kG2BK + qoff[g]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                fa[a][t], fb[b][t], acc[a][b], 0, 0, 0);
+    }
+  };
+  auto epilogue = [&](int uu) {
+    const int m0 = (uu / ntn) * TM + wm * 32 * MB + i;
+    const int n0 = (uu % ntn) * TN + wn * 32 * NB + 4 * h;
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = m0 + 32 * b;
+        float* yrow = Y + (size_t)m * Nn + n0 + 32 * a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (m < M)
+            *reinterpret_cast<float4*>(yrow + 8 * q) =
+                make_float4(acc[a][b][4 * q], acc[a][b][4 * q + 1],
+                            acc[a][b][4 * q + 2], acc[a][b][4 * q + 3]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][4 * q + r] = 0.f;
+        }
+      }
+  };
+  tile_ptrs(u);
+  stage(0, sA0, sB0);
+  int kc = 0;
+  auto step = [&](DGMC_LDS float* ca, DGMC_LDS float* cb, DGMC_LDS float* na,
+                  DGMC_LDS float* nbuf) -> bool {
+    const bool last_chunk = kc + 1 == nk;
+    const int tu = last_chunk ? u + G : u;
+    const int tkc = last_chunk ? 0 : kc + 1;
+    const bool more = tu < U;
+    if (more) {
+      if (last_chunk) tile_ptrs(tu);
+      stage(tkc, na, nbuf);
+      // (this wave's 2 (MB + NB) pieces of the next chunk stay in flight)
+      if constexpr (MB + NB == 4)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr (MB + NB == 3)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    sg_raw_barrier();
+    compute(ca, cb);
+    if (last_chunk) epilogue(u);
+    sg_raw_barrier();
+    u = tu;
+    kc = tkc;
+    return more;
+  };
+  while (step(sA0, sB0, sA1, sB1) && step(sA1, sB1, sA0, sB0)) {
+  }
+}
+
+at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt) {
+  const int64_t np = (int64_t)parts.size();
+  TORCH_CHECK(np >= 1 && np <= 4, "dense_nt_f32: 1..4 parts");
+  const int64_t M = parts[0].size(0);
+  DnParts A{};
+  for (int64_t j = 0; j < np; ++j) {
+    const at::Tensor& p = parts[j];
+    TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat &&
+                    p.is_contiguous() && p.dim() == 2 && p.size(0) == M &&
+                    p.size(1) == 128 && aligned16(p.data_ptr()),
+                "dense_nt_f32: parts contiguous fp32 [M, 128]");
+    A.p[j] = p.data_ptr<float>();
+  }
+  TORCH_CHECK(bt.scalar_type() == at::kFloat && bt.is_contiguous() &&
+                  bt.dim() == 2 && bt.size(1) == 128 * np &&
+                  bt.size(0) % 64 == 0 && aligned16(bt.data_ptr()),
+              "dense_nt_f32: Bt fp32 [Nn % 64, 128 * parts]");
+  const int64_t Nn = bt.size(0), K = bt.size(1);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bt.device());
+  at::Tensor Y = at::empty({M, Nn}, bt.options());
+  if (M == 0) return Y;
+  // 128 x 128 tiles when they fill the chip, else 64 x 64.
+  const int cus = num_cus(bt.device().index());
+  const int64_t big = ((M + 127) / 128) * (Nn / 128);
+  const bool small = big < cus || Nn % 128 != 0;
+  const int64_t tiles =
+      small ? ((M + 63) / 64) * (Nn / 64) : big;
+  const int per_cu = (small || K < 256) ? 2 : 1;     // as slot_gemm2
+  const int64_t blocks = std::min<int64_t>(tiles, per_cu * (int64_t)cus);
+  auto kern = small ? dense_nt_f32_kernel<1, 1> : dense_nt_f32_kernel<2, 2>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kSgThreads), 0, stream(), A,
+                     (int)M, bt.data_ptr<float>(), (int)K, (int)Nn,
+                     Y.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return Y;
+}
+
 // W^T images [S, out, in] of weight [S - 1 or S, in, out] (+ root [in, out]
 // as the last slot): 32x32 tiles through LDS.
 __global__ __launch_bounds__(256) void slot_weight_t_kernel(
@@ -1020,6 +1211,7 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
 struct SgUses {
   const float* x[kSgMaxU];
   const float* g[kSgMaxU];
+  const float* xp[kSgMaxU][4];    // dense mode: X_u as [M, 128] parts
 };
 
 // Item table: item i -> (slot, first step, end step); ib[s] = first item of
@@ -1075,10 +1267,11 @@ __global__ __launch_bounds__(64) void sg_items_kernel(
 constexpr int kW2Rows = 32;                  // p rows per step
 constexpr int kW2MaxRows = 3072;             // gathered rows per item (LDS)
 
+template <bool DENSE>
 __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad2_kernel(
     SgUses U, int nu, const int* __restrict__ src,
     const int* __restrict__ seg, const int* __restrict__ items, int Kin,
-    int C, float* __restrict__ part) {
+    int C, int ldxd, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float sX0_[kW2Rows * 128];
   __shared__ __attribute__((aligned(16))) float sX1_[kW2Rows * 128];
   __shared__ __attribute__((aligned(16))) float sG0_[kW2Rows * 128];
@@ -1101,11 +1294,13 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad2_kernel(
   const int c0 = qb / nu;
   const int pb = seg[s] + c0 * kW2Rows;
   const int nrows = ((qe - 1) / nu - c0 + 1) * kW2Rows;
-  for (int r = tid; r < nrows; r += kSgThreads) {
-    const int j = src[pb + r];
-    sidx[r] = j < 0 ? 0 : j;          // padding rows: dY row is zero
+  if (!DENSE) {
+    for (int r = tid; r < nrows; r += kSgThreads) {
+      const int j = src[pb + r];
+      sidx[r] = j < 0 ? 0 : j;          // padding rows: dY row is zero
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int total = qe - qb;
 
   // Staging: wave w's pieces j = 0..3 cover rows 8 w + 2 j + (lane >> 5),
@@ -1114,13 +1309,14 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_wgrad2_kernel(
   auto stage = [&](int q, DGMC_LDS float* dx, DGMC_LDS float* dg) {
     const int qq = qb + q;
     const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
-    const float* Xu = U.x[u];
+    const float* Xu = DENSE ? U.xp[u][i0 >> 7] + (i0 & 127) : U.x[u] + i0;
+    const int ldx = DENSE ? ldxd : Kin;
     const float* Gu = U.g[u];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = 8 * wave + 2 * j + prow;
       const int row = ch * kW2Rows + r;
-      sg_dma16(Xu + (size_t)sidx[row] * Kin + i0 + pc,
+      sg_dma16(Xu + (size_t)(DENSE ? pb + row : sidx[row]) * ldx + pc,
                dx + (8 * wave + 2 * j) * 128);
       sg_dma16(Gu + (size_t)(pb + row) * C + n0 + pc,
                dg + (8 * wave + 2 * j) * 128);
@@ -1249,16 +1445,82 @@ at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
   DGMC_CHECK_LAUNCH();
   const int64_t per = Kin * C;
   at::Tensor part = at::empty({G_cap, per}, xs[0].options());
-  hipLaunchKernelGGL(slot_wgrad2_kernel, dim3(G_cap * tiles),
+  hipLaunchKernelGGL(slot_wgrad2_kernel<false>, dim3(G_cap * tiles),
                      dim3(kSgThreads), 0, stream(), U, (int)nu,
                      src.data_ptr<int>(), seg.data_ptr<int>(),
-                     items.data_ptr<int>(), (int)Kin, (int)C,
+                     items.data_ptr<int>(), (int)Kin, (int)C, 0,
                      part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   at::Tensor out = at::empty({S, Kin, C}, xs[0].options());
   hipLaunchKernelGGL(sg_fold_kernel, dim3((per / 4 + 255) / 256, S), dim3(256),
                      0, stream(), part.data_ptr<float>(), ib.data_ptr<int>(),
                      (int)S, per, out.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+// Dense weight gradient sum_u [X_u,0 | X_u,1 | ...]^T G_u ([K, C], X parts
+// [M, w] (w % 128, all parts alike) read in place, M % 32 == 0) on the slot
+// kernel's dense mode: one "slot" [0, M), balanced step items, per-item
+// partials folded in order.
+at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
+                           at::TensorList gs, const at::Tensor& seg01) {
+  const int64_t nu = (int64_t)gs.size();
+  TORCH_CHECK(nu >= 1 && nu <= kSgMaxU && nparts >= 1 &&
+                  (int64_t)xparts.size() == nu * nparts,
+              "dense_wgrad_f32: 1..16 uses, nparts parts each");
+  const int64_t M = gs[0].size(0), C = gs[0].size(1);
+  const int64_t w = xparts[0].size(1), sub = w / 128;
+  const int64_t Kin = w * nparts;
+  TORCH_CHECK(w % 128 == 0 && nparts * sub <= 4,
+              "dense_wgrad_f32: part widths % 128, K <= 512");
+  TORCH_CHECK(M % kW2Rows == 0 && C % kSgBN == 0,
+              "dense_wgrad_f32: M % 32, C % 128");
+  TORCH_CHECK(seg01.scalar_type() == at::kInt && seg01.numel() == 2,
+              "dense_wgrad_f32: seg [0, M] (device int32)");
+  SgUses U{};
+  for (int64_t u = 0; u < nu; ++u) {
+    const at::Tensor& g = gs[u];
+    TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat &&
+                    g.is_contiguous() && g.size(0) == M && g.size(1) == C &&
+                    aligned16(g.data_ptr()),
+                "dense_wgrad_f32: G_u contiguous fp32 [M, C]");
+    U.g[u] = g.data_ptr<float>();
+    for (int64_t j = 0; j < nparts; ++j) {
+      const at::Tensor& x = xparts[u * nparts + j];
+      TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() &&
+                      x.dim() == 2 && x.size(0) == M && x.size(1) == w &&
+                      aligned16(x.data_ptr()),
+                  "dense_wgrad_f32: X parts contiguous fp32 [M, w]");
+      for (int64_t q = 0; q < sub; ++q)
+        U.xp[u][j * sub + q] = x.data_ptr<float>() + 128 * q;
+    }
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(seg01.device());
+  const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
+  const int64_t target = std::max<int64_t>(
+      2, 2 * 2 * (int64_t)num_cus(seg01.device().index()) / tiles);
+  const int64_t qcap = (kW2MaxRows / kW2Rows - 2) * nu;
+  const int64_t G_cap = target + (M / kW2Rows * nu + qcap - 1) / qcap + 1;
+  auto i32 = seg01.options();
+  at::Tensor items = at::empty({G_cap, 3}, i32);
+  at::Tensor ib = at::empty({2}, i32);
+  hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
+                     seg01.data_ptr<int>(), 1, (int)nu, (int)target,
+                     (int)qcap, (int)G_cap, items.data_ptr<int>(),
+                     ib.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  const int64_t per = Kin * C;
+  at::Tensor part = at::empty({G_cap, per}, gs[0].options());
+  hipLaunchKernelGGL(slot_wgrad2_kernel<true>, dim3(G_cap * tiles),
+                     dim3(kSgThreads), 0, stream(), U, (int)nu, nullptr,
+                     seg01.data_ptr<int>(), items.data_ptr<int>(), (int)Kin,
+                     (int)C, (int)w, part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  at::Tensor out = at::empty({Kin, C}, gs[0].options());
+  hipLaunchKernelGGL(sg_fold_kernel, dim3((per / 4 + 255) / 256, 1), dim3(256),
+                     0, stream(), part.data_ptr<float>(), ib.data_ptr<int>(),
+                     1, per, out.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return out;
 }

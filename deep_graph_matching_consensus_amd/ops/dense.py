@@ -581,6 +581,93 @@ def cat_matmul(parts, w_t, lp, key, total):
         return _CatMatmul.apply(w_t, w_n, lp['nt'], loop, total, *parts)
 
 
+_SEG01 = {}
+
+
+def _seg01(M, device):
+    """Device int32 ``[0, M]`` (one "slot" covering all rows) for the dense
+    weight-gradient kernel; created outside graph capture (the warm-up
+    steps) and reused by the captured replays."""
+    key = (str(device), int(M))
+    t = _SEG01.get(key)
+    if t is None:
+        t = _SEG01[key] = torch.tensor([0, int(M)], dtype=torch.int32,
+                                       device=device)
+    return t
+
+
+class _CatMatmulF32(torch.autograd.Function):
+    """fp32 ``[X_0 | X_1 | ...] @ W`` (``W = w_t [128 n, 128]``) on the
+    LDS-DMA MFMA GEMM reading psi_2's feature parts in place
+    (``csrc/hip/slot_gemm.hip::dense_nt_f32``: no concatenation); backward
+    ``g W^T`` on the same kernel (part gradients are column views), and
+    inside a consensus loop the weight gradient of all uses as ONE dense TN
+    launch over the kept parts (``dense_wgrad_f32``: no stacked copies)."""
+
+    @staticmethod
+    def forward(ctx, w_t, loop, *parts):
+        ops = _backend.ops()
+        out = ops.dense_nt_f32(list(parts), w_t.detach().t().contiguous())
+        ctx.loop, ctx.np = loop, len(parts)
+        ctx.save_for_backward(w_t)
+        ctx.idx = loop.register() if loop is not None else None
+        ctx.parts = tuple(parts) if ctx.needs_input_grad[0] else None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        w_t, = ctx.saved_tensors
+        ops = _backend.ops()
+        g = g.float().contiguous()
+        gx = ops.dense_nt_f32([g], w_t.detach().contiguous())   # [M, 128 n]
+        grads = tuple(gx[:, 128 * i:128 * (i + 1)]
+                      if ctx.needs_input_grad[2 + i] else None
+                      for i in range(ctx.np))
+        need_w = ctx.needs_input_grad[0]
+        seg = _seg01(g.size(0), g.device)
+        gw, loop = None, ctx.loop
+        if loop is None:
+            if need_w:
+                gw = ops.dense_wgrad_f32(list(ctx.parts), ctx.np, [g], seg)
+        else:
+            if need_w:
+                loop.keep('g', ctx.idx, g)
+                loop.keep('xp', ctx.idx, ctx.parts)
+            ctx.parts = None
+            if loop.arrive():
+                if need_w:
+                    xps, gs = loop.kept_list('xp'), loop.kept_list('g')
+                    for i in range(0, len(gs), 16):
+                        part = ops.dense_wgrad_f32(
+                            [p for t in xps[i:i + 16] for p in t], ctx.np,
+                            gs[i:i + 16], seg)
+                        gw = part if gw is None else gw.add_(part)
+                loop.release()
+        if gw is not None:
+            gw = gw.to(w_t.dtype)
+        return (gw, None) + grads
+
+
+def cat_matmul_f32_supported(parts, w_t):
+    return (1 <= len(parts) <= 4 and w_t.dtype == torch.float32 and
+            tuple(w_t.shape) == (128 * len(parts), 128) and
+            parts[0].size(0) % 32 == 0 and
+            all(_backend.use_hip(p) and p.dtype == torch.float32 and
+                p.dim() == 2 and p.is_contiguous() and p.size(1) == 128 and
+                p.size(0) == parts[0].size(0) and p.data_ptr() % 16 == 0
+                for p in parts))
+
+
+def cat_matmul_f32(parts, w_t, key, total):
+    """``cat(parts, -1) @ w_t`` in fp32 without the concatenation (see
+    :class:`_CatMatmulF32`); ``total`` = uses of ``key``'s loop collector
+    in this forward (the consensus steps)."""
+    loop = loopgrad.group(('catmm32', ) + key + (parts[0].size(0), )) \
+        if total else None
+    with torch.autocast(device_type='cuda', enabled=False):
+        return _CatMatmulF32.apply(w_t, loop, *parts)
+
+
 def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
                      w1_fold=None, next_r_s=None):
     r"""``S_hat + mask * mlp(o_s[:, :, None] - o_t[:, None])`` for packed
@@ -601,6 +688,8 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
         parts = getattr(o_joint, 'parts', None)
         if parts is not None and cat_matmul_supported(parts, w_t):
             PQ = cat_matmul(parts, w_t, lp, key, total)
+        elif parts is not None and cat_matmul_f32_supported(parts, w_t):
+            PQ = cat_matmul_f32(parts, w_t, key, total)
         else:
             if parts is not None:
                 o_joint = o_joint.cat()

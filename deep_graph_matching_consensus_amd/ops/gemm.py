@@ -62,7 +62,14 @@ def matmul_tn_fp32(a, b, out=None, accumulate=False):
         # instead of a skinny split-K library GEMM.
         from .dense import dense_wgrad
         return dense_wgrad([a], [b], out=out, accumulate=accumulate)
-    if not a.is_cuda:
+    if _dense_tn_f32_ok(a, b):
+        # fp32: the LDS-DMA MFMA TN kernel over balanced row ranges (a
+        # batched split-K library GEMM with M x N = 256 x 256 ran as 16
+        # workgroups: 152 us for psi_1's final Linear).
+        from .dense import _seg01
+        res = _backend.ops().dense_wgrad_f32([a], 1, [b],
+                                             _seg01(K, a.device))
+    elif not a.is_cuda:
         res = a.float().t() @ b.float()
     else:
         s = _split_factor(M, N, K)
@@ -98,6 +105,16 @@ def matmul_tn_fp32(a, b, out=None, accumulate=False):
     else:
         out.copy_(res)
     return out
+
+
+def _dense_tn_f32_ok(a, b):
+    return (_backend.use_hip(a) and a.dtype == torch.float32 and
+            b.dtype == torch.float32 and a.dim() == 2 and b.dim() == 2 and
+            a.is_contiguous() and b.is_contiguous() and
+            a.size(0) == b.size(0) and a.size(0) % 32 == 0 and
+            a.size(1) % 128 == 0 and a.size(1) <= 512 and
+            b.size(1) % 128 == 0 and a.data_ptr() % 16 == 0 and
+            b.data_ptr() % 16 == 0)
 
 
 class _MixedMatmul(torch.autograd.Function):

@@ -1418,3 +1418,51 @@ def test_fold_weights_kernel():
     torch.testing.assert_close(w.double(), ref_, atol=1e-3, rtol=1e-4)
     assert torch.equal(wn, w.bfloat16())
     assert torch.equal(wnt, w.t().contiguous().bfloat16())
+
+
+def test_dgmc_fp32_headline_widths_vs_reference_mode():
+    """fp32 at the flagship's layer widths (psi_1 in/out multiples of 128,
+    psi_2 128 -> 128 with cat=True): the step runs the fp32 slot GEMMs,
+    the folded projection on the dense fp32 GEMM, the fused pair-step and
+    objective kernels; outputs, loss and every parameter gradient match the
+    reference-mode expression (``/root/reference/dgmc/models/dgmc.py:
+    163-244``, fp32) to fp32 tolerance (loss 1e-5 relative, gradients 1e-4
+    relative to their largest entry)."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, DevicePairLoader, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    groups = make_keypoint_datasets(graphs=8, feature_dim=256, seed=0)
+    store = GraphStore(groups, DEV)
+    batch = next(iter(DevicePairLoader(store, batch_size=32, seed=0)))
+    torch.manual_seed(3)
+    model = DGMC(SplineCNN(256, 128, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=4).to(DEV)
+    args = (batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+            batch.x_s_batch, batch.x_t, batch.edge_index_t,
+            batch.edge_attr_t, batch.x_t_batch)
+    y = torch.stack([torch.arange(batch.y.numel(), device=DEV), batch.y])
+    params = list(model.parameters())
+
+    torch.manual_seed(5)
+    S_0, S_L = model(*args)
+    loss = model.loss(S_0, y) + model.loss(S_L, y)
+    grads = torch.autograd.grad(loss, params, allow_unused=True)
+    with reference_mode():
+        torch.manual_seed(5)
+        R_0, R_L = model(*args)
+        loss2 = model.loss(R_0, y) + model.loss(R_L, y)
+        grads2 = torch.autograd.grad(loss2, params, allow_unused=True)
+    assert S_L.dtype == torch.float32
+    assert torch.allclose(S_0, R_0, atol=1e-5)
+    assert torch.allclose(S_L, R_L, atol=1e-5)
+    assert abs(loss.item() - loss2.item()) <= 1e-5 * abs(loss2.item())
+    # (floor 1e-5 x the largest gradient: psi_2's final bias and the MLP's
+    # output bias cancel exactly (P_i - Q_j, row softmax) - their exact
+    # gradients are 0 and both paths leave only rounding)
+    G = max(float(b.abs().max()) for b in grads2 if b is not None)
+    for p, a, b in zip(params, grads, grads2):
+        if b is None:
+            continue
+        a = torch.zeros_like(b) if a is None else a
+        err = float((a - b).abs().max())
+        assert err <= 1e-4 * float(b.abs().max()) + 1e-5 * G, p.shape

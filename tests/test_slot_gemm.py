@@ -153,3 +153,59 @@ def test_dx_row0_matches_full_rows(row0):
     assert not part[0][:row0].any()
     for a, bb in zip(part[1:], full[1:]):
         assert torch.equal(a, bb)
+
+
+@pytest.mark.parametrize('M,nparts', [(1088, 3), (512, 1), (96, 2)])
+def test_cat_matmul_f32_matches_fp64(M, nparts):
+    """fp32 ``cat(parts) @ W`` on the dense LDS-DMA GEMM (parts read in
+    place, rows past M clamped) and its backward (g W^T, dense TN weight
+    gradient) against fp64."""
+    from deep_graph_matching_consensus_amd.ops import dense as dops
+    parts = [torch.randn(M, 128, device=DEV, requires_grad=True)
+             for _ in range(nparts)]
+    w_t = (torch.randn(128 * nparts, 128, device=DEV) / 20).requires_grad_()
+    assert dops.cat_matmul_f32_supported(parts, w_t)
+    out = dops.cat_matmul_f32(parts, w_t, ('t', ), 0)
+    ref = torch.cat(parts, -1).double() @ w_t.double()
+    assert _rel(out, ref) < 2e-6
+    g = torch.randn_like(out)
+    grads = torch.autograd.grad(out, parts + [w_t], g)
+    refs = torch.autograd.grad(ref, parts + [w_t], g.double())
+    for a, bb in zip(grads, refs):
+        assert a.dtype == torch.float32
+        assert _rel(a, bb) < 1e-5
+
+
+def test_cat_matmul_f32_loop_weight_grad():
+    """Inside a consensus loop the weight gradient of all uses is one dense
+    TN launch; it equals the per-use autograd sum."""
+    from deep_graph_matching_consensus_amd.ops import dense as dops
+    M, uses = 640, 4
+    w_t = (torch.randn(384, 128, device=DEV) / 20).requires_grad_()
+    xs = [[torch.randn(M, 128, device=DEV) for _ in range(3)]
+          for _ in range(uses)]
+
+    def run(loop):
+        with loopgrad.loop_scope(loop):
+            h = 0
+            for ps in xs:
+                h = h + dops.cat_matmul_f32(ps, w_t, ('L', ),
+                                            uses if loop else 0)
+            return torch.autograd.grad(h.square().sum(), (w_t, ))[0]
+
+    assert _rel(run(True), run(False)) < 1e-6
+
+
+@pytest.mark.parametrize('K,M,N', [(1056, 256, 256), (2048, 128, 384),
+                                   (96, 512, 128)])
+def test_matmul_tn_fp32_dense_kernel(K, M, N):
+    """fp32 ``a^T b`` (weight gradients of Linear layers) on the dense TN
+    MFMA kernel, against fp64, plain and accumulated into ``out``."""
+    from deep_graph_matching_consensus_amd.ops.gemm import matmul_tn_fp32
+    a = torch.randn(K, M, device=DEV)
+    b = torch.randn(K, N, device=DEV)
+    ref = a.double().t() @ b.double()
+    assert _rel(matmul_tn_fp32(a, b), ref) < 2e-6
+    out = torch.ones(M, N, device=DEV)
+    matmul_tn_fp32(a, b, out=out, accumulate=True)
+    assert _rel(out, ref + 1) < 2e-6
