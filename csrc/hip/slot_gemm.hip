@@ -1498,8 +1498,10 @@ at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(seg01.device());
   const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
+  // One round of resident workgroups: the outputs are small (<= 512 x 512)
+  // and every item writes a full partial tile set for the fold.
   const int64_t target = std::max<int64_t>(
-      2, 2 * 2 * (int64_t)num_cus(seg01.device().index()) / tiles);
+      2, 2 * (int64_t)num_cus(seg01.device().index()) / tiles);
   const int64_t qcap = (kW2MaxRows / kW2Rows - 2) * nu;
   const int64_t G_cap = target + (M / kW2Rows * nu + qcap - 1) / qcap + 1;
   auto i32 = seg01.options();

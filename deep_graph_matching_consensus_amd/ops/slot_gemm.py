@@ -91,7 +91,6 @@ def weight_grad(xs, dys, plan, cin, cout):
     # / 623 / 653 us).
     tiles = (cin // 128) * (cout // 128)
     rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
-    rounds = int(os.environ.get('DGMC_WG_ROUNDS_%d' % cin, rounds))
     out = None
     for i in range(0, len(xs), MAX_USES):
         part = ops.slot_wgrad_f32(list(xs[i:i + MAX_USES]),
