@@ -1,6 +1,7 @@
 """Per-step kernel timeline from a rocprofv3 ``kernel_trace.csv``.
 
-Splits the dispatch stream at the optimizer kernel (one fused Adam launch per
+Splits the dispatch stream at the optimizer kernel (one multi-tensor HIP Adam
+launch per
 training step), takes the LAST complete step and prints: wall span, summed
 kernel time, kernel count, idle gaps and a per-kernel-name table.
 
@@ -14,7 +15,7 @@ import sys
 
 def main():
     path = sys.argv[1]
-    marker = sys.argv[2] if len(sys.argv) > 2 else 'FusedOpti'
+    marker = sys.argv[2] if len(sys.argv) > 2 else 'adam_multi_kernel'
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     ends = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
