@@ -42,7 +42,13 @@ class GraphedStep(object):
         torch.cuda.current_stream().wait_stream(stream)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: with data parallelism the process group's watchdog
+        # thread polls collective events while the step is captured; a
+        # global-mode capture would be invalidated by those calls.
+        mode = 'thread_local' if (torch.distributed.is_available() and
+                                  torch.distributed.is_initialized()) \
+            else 'global'
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.fn()
         torch.cuda.synchronize()
         return self
