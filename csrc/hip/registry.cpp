@@ -48,6 +48,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out,
     const c10::optional<at::Tensor>& part, bool accumulate);
 
+at::Tensor train_candidates(const at::Tensor& topk, int64_t n_t, int64_t kr,
+                            const at::Tensor& gt_row,
+                            const at::Tensor& gt_col);
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
                     bool exact);
 
@@ -286,6 +289,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "part=None, bool accumulate=False) -> (Tensor, Tensor, Tensor, "
       "Tensor)");
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k, bool exact=False) -> Tensor");
+  m.def("train_candidates(Tensor topk, int n_t, int kr, Tensor gt_row, "
+        "Tensor gt_col) -> Tensor");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
       "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype, "
@@ -458,6 +463,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_consensus", &dgmc::dense_consensus);
   m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
   m.impl("topk_dot", &dgmc::topk_dot);
+  m.impl("train_candidates", &dgmc::train_candidates);
   m.impl("sddmm", &dgmc::sddmm);
   m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
   m.impl("col_sum", &dgmc::col_sum);

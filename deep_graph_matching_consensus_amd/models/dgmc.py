@@ -459,11 +459,19 @@ class DGMC(torch.nn.Module):
             with trace_range('dgmc.top_k'):
                 S_idx = self.__top_k__(hs, ht)                # [B, N_s, k]
             if self.training and y is not None:
-                rnd_size = (B, N_s, min(self.k, N_t - self.k))
-                S_rnd_idx = torch.randint(N_t, rnd_size, dtype=torch.long,
-                                          device=device)
-                S_idx = torch.cat([S_idx, S_rnd_idx], dim=-1)
-                S_idx = self._include_gt(S_idx, lay_s.index, y)
+                kr = min(self.k, N_t - self.k)
+                if _backend.use_hip(S_idx):
+                    # K12 in two launches: candidates + negatives, then the
+                    # ground-truth patch (csrc/hip/candidates.hip).
+                    S_idx = _backend.ops().train_candidates(
+                        S_idx.contiguous(), N_t, max(kr, 0),
+                        (y[0] if lay_s.identity else lay_s.index[y[0]])
+                        .long().contiguous(), y[1].long().contiguous())
+                else:
+                    S_rnd_idx = torch.randint(N_t, (B, N_s, kr),
+                                              dtype=torch.long, device=device)
+                    S_idx = torch.cat([S_idx, S_rnd_idx], dim=-1)
+                    S_idx = self._include_gt(S_idx, lay_s.index, y)
             k = S_idx.size(-1)
             # CSR/CSC of the candidate set, shared by every op of the loop.
             cand = sparse_corr.CandidateGraph(S_idx, N_t) \

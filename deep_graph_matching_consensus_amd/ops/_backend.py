@@ -81,4 +81,9 @@ def use_hip(*tensors):
 
 
 def ops():
+    # (Loads the libraries on first use: an op looked up before any
+    # use_hip() / hip_available() call still resolves.)
+    if _STATE['hip'] is None or _STATE['host'] is None:
+        _load('hip')
+        _load('host')
     return torch.ops.dgmc_amd

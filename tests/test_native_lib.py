@@ -11,7 +11,8 @@ import deep_graph_matching_consensus_amd as pkg
 OPS = ['spmm_csr', 'spmm_csr_out', 'spline_basis', 'dense_masked_softmax',
        'dense_masked_softmax_bwd', 'dense_softmax_transport',
        'dense_softmax_transport_bwd', 'dense_consensus', 'dense_consensus_bwd',
-       'topk_dot', 'sddmm', 'sparse_consensus_fwd', 'sparse_consensus_bwd',
+       'topk_dot', 'train_candidates', 'sddmm', 'sparse_consensus_fwd',
+       'sparse_consensus_bwd',
        'relu_bias_bwd', 'col_sum', 'reduce_add_rows',
        'gemm_abt', 'piece_plan', 'spmm_pieces_out',
        'sparse_consensus_fwd_prob', 'slot_conv', 'slot_wgrad',
