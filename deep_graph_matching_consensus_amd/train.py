@@ -112,10 +112,21 @@ class PairTrainer(object):
             # datasets/static_batch.py::bucket_capacities).
             self.batcher = StaticPairBatcher(store, batch_size,
                                              sources=sources, seed=data_seed)
+            if self.world > 1:
+                # Every rank must capture the same graphs in the same order
+                # (their in-step collectives pair up across ranks): agree on
+                # the largest capacities (max over the rank shards) and size
+                # the smaller buckets from the whole store, not the shard.
+                agreed = tuple(int(parallel.all_reduce_max(c, self.device))
+                               for c in self.batcher.caps)
+                if agreed != self.batcher.caps:
+                    self.batcher = StaticPairBatcher(
+                        store, batch_size, sources=sources, seed=data_seed,
+                        caps=agreed)
             self.batchers = [self.batcher]
             if mode == 'graph' and buckets:
-                caps = [c for c in bucket_capacities(store, batch_size,
-                                                     sources)
+                probe = sources if self.world == 1 else None
+                caps = [c for c in bucket_capacities(store, batch_size, probe)
                         if all(a < b for a, b in zip(c, self.batcher.caps))]
                 self.batchers = [
                     StaticPairBatcher(store, batch_size, sources=sources,

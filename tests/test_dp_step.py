@@ -46,7 +46,8 @@ def _worker(rank, world, port, mode, device, env, steps, out):
     groups = make_keypoint_datasets(graphs=8, feature_dim=16, seed=2)
     store = GraphStore(groups, device)
     trainer = train_mod.PairTrainer(model, store, 8, mode=mode, bf16=False,
-                                    seed=0, buckets=False,
+                                    seed=0, buckets=env.get(
+                                        'DGMC_TEST_BUCKETS') == '1',
                                     bucket_bytes=16 << 10)
     assert len(trainer.reducer.buckets) > 2      # several all-reduces
     assert trainer.reducer.in_step == (mode == 'static' and
@@ -58,6 +59,7 @@ def _worker(rank, world, port, mode, device, env, steps, out):
         torch.cuda.synchronize()
     out[rank] = torch.cat([p.detach().reshape(-1).cpu()
                            for p in model.parameters()])
+    out['caps%d' % rank] = [b.caps for b in getattr(trainer, 'batchers', [])]
     dist.destroy_process_group()
 
 
@@ -74,6 +76,7 @@ def _run(mode, device, env=None, steps=3, world=2):
     for p in procs:
         p.join(timeout=600)
         assert p.exitcode == 0
+    _run.caps = [out['caps%d' % r] for r in range(world)]
     return [out[r] for r in range(world)]
 
 
@@ -93,3 +96,14 @@ def test_graph_mode_two_ranks_gloo_on_one_gpu():
     s = _run('static', 'cuda', env)
     assert torch.equal(s[0], s[1])
     torch.testing.assert_close(g[0], s[0], atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_graph_mode_size_buckets_agree_across_ranks():
+    """Rank shards differ, yet every rank builds the same static capacities
+    and size buckets (so the captured graphs - and their collectives - pair
+    up across ranks); parameters stay bit-identical."""
+    env = {'DGMC_AMD_DIST_BACKEND': 'gloo', 'DGMC_TEST_BUCKETS': '1'}
+    g = _run('graph', 'cuda', env, steps=4)
+    assert torch.equal(g[0], g[1])
+    assert _run.caps[0] == _run.caps[1] and len(_run.caps[0]) >= 1
