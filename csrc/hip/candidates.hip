@@ -16,6 +16,7 @@
 
 #include <ATen/hip/HIPGeneratorImpl.h>
 #include <ATen/hip/detail/UnpackRaw.cuh>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <mutex>
 
@@ -76,7 +77,83 @@ __global__ __launch_bounds__(256) void include_gt_kernel(
   if (!present) row[kk - 1] = col;
 }
 
+// Candidate CSR / CSC, step 1: global target column of every candidate
+// entry (pair b's targets start at b * N_t), the identity permutation (the
+// sort's values) and the CSR row pointer (k entries per row).
+__global__ __launch_bounds__(256) void csc_prep_kernel(
+    const int64_t* __restrict__ idx, int64_t n, int k, int64_t rows_per_pair,
+    int64_t n_t, int* __restrict__ col, int* __restrict__ iota,
+    int* __restrict__ rowptr, int64_t R) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e <= R) rowptr[e] = (int)(e * k);
+  if (e >= n) return;
+  const int64_t r = e / k;
+  col[e] = (int)(idx[e] + (r / rows_per_pair) * n_t);
+  iota[e] = (int)e;
+}
+
+// Step 3 (after the stable radix sort by column): column pointers from the
+// sorted keys (position i starts every column in (key[i-1], key[i]]) and
+// the source row of every CSC entry.
+__global__ __launch_bounds__(256) void csc_finish_kernel(
+    const int* __restrict__ keys, const int* __restrict__ perm, int64_t n,
+    int k, int64_t C, int* __restrict__ colptr, int* __restrict__ row_of) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  // (keys lie in [0, C); the clamps only keep a corrupt index in bounds)
+  const int64_t lo = i == 0 ? -1 : max((int64_t)keys[i - 1], (int64_t)-1);
+  const int64_t hi = i == n ? C : min((int64_t)keys[i], C);
+  for (int64_t c = lo + 1; c <= hi; ++c) colptr[c] = (int)i;
+  if (i < n) row_of[i] = perm[i] / k;
+}
+
 }  // namespace
+
+// S_idx [B, N_s, k] int64 (targets local to each pair's N_t block) ->
+// (col int32 [nnz] global targets, rowptr int32 [B N_s + 1], colptr int32
+// [B N_t + 1], perm int32 [nnz] CSC -> CSR entry map (stable: row order
+// inside a column), row_of int32 [nnz]).  Five launches (prep, the radix
+// sort's passes, finish) instead of an argsort + histogram + scan chain.
+std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
+  TORCH_CHECK(S_idx.is_cuda() && S_idx.scalar_type() == at::kLong &&
+                  S_idx.is_contiguous() && S_idx.dim() == 3,
+              "candidate_csc: contiguous int64 [B, N_s, k]");
+  const int64_t B = S_idx.size(0), N_s = S_idx.size(1), k = S_idx.size(2);
+  const int64_t R = B * N_s, n = R * k, C = B * n_t;
+  TORCH_CHECK(k >= 1 && n < INT32_MAX && C < INT32_MAX && n_t >= 1,
+              "candidate_csc: sizes");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_idx.device());
+  auto i32 = S_idx.options().dtype(at::kInt);
+  at::Tensor col = at::empty({n}, i32), iota = at::empty({n}, i32);
+  at::Tensor rowptr = at::empty({R + 1}, i32);
+  at::Tensor keys = at::empty({n}, i32), perm = at::empty({n}, i32);
+  at::Tensor colptr = at::empty({C + 1}, i32), row_of = at::empty({n}, i32);
+  const int64_t m = std::max(n, R + 1);
+  hipLaunchKernelGGL(csc_prep_kernel, dim3((unsigned)((m + 255) / 256)),
+                     dim3(256), 0, stream(), S_idx.data_ptr<int64_t>(), n,
+                     (int)k, N_s, n_t, col.data_ptr<int>(),
+                     iota.data_ptr<int>(), rowptr.data_ptr<int>(), R);
+  DGMC_CHECK_LAUNCH();
+  unsigned bits = 1;
+  while (bits < 31 && (int64_t(1) << bits) < C) ++bits;
+  size_t tmp_bytes = 0;
+  DGMC_CHECK_HIP(rocprim::radix_sort_pairs(
+      nullptr, tmp_bytes, col.data_ptr<int>(), keys.data_ptr<int>(),
+      iota.data_ptr<int>(), perm.data_ptr<int>(), (size_t)n, 0, bits,
+      stream()));
+  at::Tensor tmp = at::empty({(int64_t)std::max<size_t>(tmp_bytes, 1)},
+                             S_idx.options().dtype(at::kByte));
+  DGMC_CHECK_HIP(rocprim::radix_sort_pairs(
+      tmp.data_ptr(), tmp_bytes, col.data_ptr<int>(), keys.data_ptr<int>(),
+      iota.data_ptr<int>(), perm.data_ptr<int>(), (size_t)n, 0, bits,
+      stream()));
+  hipLaunchKernelGGL(csc_finish_kernel, dim3((unsigned)((n + 256) / 256)),
+                     dim3(256), 0, stream(), keys.data_ptr<int>(),
+                     perm.data_ptr<int>(), n, (int)k, C,
+                     colptr.data_ptr<int>(), row_of.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  return {col, rowptr, colptr, perm, row_of};
+}
 
 // topk [..., k] int64; gt_row / gt_col int64 [G] (flattened candidate row of
 // each ground-truth source, its target).  Returns [..., k + kr] int64.

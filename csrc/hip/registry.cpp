@@ -48,6 +48,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dense_consensus_bwd(
     const at::Tensor& ptr_t, const c10::optional<at::Tensor>& dpq_out,
     const c10::optional<at::Tensor>& part, bool accumulate);
 
+std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t);
 at::Tensor train_candidates(const at::Tensor& topk, int64_t n_t, int64_t kr,
                             const at::Tensor& gt_row,
                             const at::Tensor& gt_col);
@@ -291,6 +292,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("topk_dot(Tensor h_s, Tensor h_t, int k, bool exact=False) -> Tensor");
   m.def("train_candidates(Tensor topk, int n_t, int kr, Tensor gt_row, "
         "Tensor gt_col) -> Tensor");
+  m.def("candidate_csc(Tensor S_idx, int n_t) -> Tensor[]");
   m.def("sddmm(Tensor rowptr, Tensor col, Tensor A, Tensor B) -> Tensor");
   m.def(
       "relu_bias_bwd(Tensor grad, Tensor out, bool relu, ScalarType g_dtype, "
@@ -464,6 +466,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
   m.impl("topk_dot", &dgmc::topk_dot);
   m.impl("train_candidates", &dgmc::train_candidates);
+  m.impl("candidate_csc", &dgmc::candidate_csc);
   m.impl("sddmm", &dgmc::sddmm);
   m.impl("relu_bias_bwd", &dgmc::relu_bias_bwd);
   m.impl("col_sum", &dgmc::col_sum);

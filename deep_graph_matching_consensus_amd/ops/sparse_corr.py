@@ -62,25 +62,35 @@ class CandidateGraph(object):
         dev = S_idx.device
         self.B, self.N_s, self.N_t, self.k = B, N_s, N_t, k
         self.rows, self.cols = B * N_s, B * N_t
-        offs = (torch.arange(B, device=dev) * N_t).view(B, 1, 1)
-        col = (S_idx + offs).reshape(-1)
-        self.rowptr = (torch.arange(self.rows + 1, device=dev) * k).to(
-            torch.int32)
-        self.col = col.to(torch.int32)
-        self.perm = torch.argsort(col, stable=True)
-        counts = torch.zeros(self.cols, dtype=torch.long, device=dev)
-        counts.index_add_(0, col, torch.ones_like(col))
-        colptr = torch.zeros(self.cols + 1, dtype=torch.long, device=dev)
-        torch.cumsum(counts, 0, out=colptr[1:])
-        self.colptr = colptr.to(torch.int32)
-        self.row_of = (self.perm // k).to(torch.int32)
-        self.perm32 = self.perm.to(torch.int32)
+        if _backend.use_hip(S_idx):
+            # prep + stable radix sort by column + pointers: 5 launches
+            # (csrc/hip/candidates.hip::candidate_csc).
+            (self.col, self.rowptr, self.colptr, self.perm32,
+             self.row_of) = _backend.ops().candidate_csc(
+                 S_idx.contiguous(), N_t)
+            self.perm = self.perm32
+            nnz = self.col.numel()
+        else:
+            offs = (torch.arange(B, device=dev) * N_t).view(B, 1, 1)
+            col = (S_idx + offs).reshape(-1)
+            self.rowptr = (torch.arange(self.rows + 1, device=dev) * k).to(
+                torch.int32)
+            self.col = col.to(torch.int32)
+            self.perm = torch.argsort(col, stable=True)
+            counts = torch.zeros(self.cols, dtype=torch.long, device=dev)
+            counts.index_add_(0, col, torch.ones_like(col))
+            colptr = torch.zeros(self.cols + 1, dtype=torch.long, device=dev)
+            torch.cumsum(counts, 0, out=colptr[1:])
+            self.colptr = colptr.to(torch.int32)
+            self.row_of = (self.perm // k).to(torch.int32)
+            self.perm32 = self.perm.to(torch.int32)
+            nnz = col.numel()
         # Column walks (transport, consensus dQ, gather-dot dB) in pieces of
         # <= sparse.PIECE entries: with random-init embeddings a few
         # targets sit in
         # the top-k of thousands of rows (hubness), which would serialise a
         # column-per-wave kernel.
-        self.col_pieces = piece_plan(self.colptr, col.numel())
+        self.col_pieces = piece_plan(self.colptr, nnz)
 
     def op(self, val):
         """``[rows, cols]`` operator with per-entry values ``val``."""

@@ -92,3 +92,25 @@ def test_train_candidates_fresh_negatives_and_graph_replay():
     g.replay()
     assert not torch.equal(first, static['out'])
     assert torch.equal(first[..., :10], topk)
+
+
+@pytest.mark.parametrize('B,N_s,N_t,k', [(1, 1937, 1960, 20), (4, 50, 70, 7)])
+def test_candidate_csc_matches_stable_argsort(B, N_s, N_t, k):
+    g = torch.Generator().manual_seed(B)
+    # Skewed targets (a few hubs), like top-k of random-init embeddings.
+    w = torch.rand(N_t, generator=g) ** 8
+    S_idx = torch.multinomial(w, B * N_s * k, replacement=True,
+                              generator=g).view(B, N_s, k).cuda()
+    col, rowptr, colptr, perm, row_of = _backend.ops().candidate_csc(
+        S_idx, N_t)
+    offs = (torch.arange(B, device='cuda') * N_t).view(B, 1, 1)
+    ref_col = (S_idx + offs).reshape(-1)
+    ref_perm = torch.argsort(ref_col, stable=True)
+    counts = torch.bincount(ref_col, minlength=B * N_t)
+    ref_colptr = torch.cat([counts.new_zeros(1), counts.cumsum(0)])
+    assert torch.equal(col.long(), ref_col)
+    assert torch.equal(rowptr.long(),
+                       torch.arange(B * N_s + 1, device='cuda') * k)
+    assert torch.equal(perm.long(), ref_perm)
+    assert torch.equal(colptr.long(), ref_colptr)
+    assert torch.equal(row_of.long(), ref_perm // k)

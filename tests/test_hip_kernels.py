@@ -551,8 +551,11 @@ def test_sparse_consensus(R, hub):
         assert torch.allclose(a, b, atol=1e-3, rtol=1e-3)
 
 
-def test_dgmc_sparse_training_hip_vs_reference():
-    """RelCNN + top-k (DBP15K-style) forward/backward: HIP == oracle."""
+def test_dgmc_sparse_training_hip_vs_reference(monkeypatch):
+    """RelCNN + top-k (DBP15K-style) forward/backward: HIP == oracle.  The
+    native path draws its random negatives in the candidate kernel (Philox,
+    csrc/hip/candidates.hip), the oracle with ``torch.randint``: the oracle
+    run is handed the native negatives, so both see one candidate set."""
     from deep_graph_matching_consensus_amd.models import DGMC, RelCNN
     torch.manual_seed(0)
     N, E = 300, 1500
@@ -570,6 +573,14 @@ def test_dgmc_sparse_training_hip_vs_reference():
     loss = model.loss(S_L, y)
     grads = torch.autograd.grad(loss, list(model.parameters()),
                                 allow_unused=True)
+    negs = S_L.__idx__[:, 5:].contiguous()
+    randint = torch.randint
+
+    def native_negatives(high, size, **kw):
+        if tuple(size) == (1, N, negs.size(1)):
+            return negs.view(size).clone()
+        return randint(high, size, **kw)
+    monkeypatch.setattr(torch, 'randint', native_negatives)
     with reference_mode():
         torch.manual_seed(1)
         _, R_L = model(x1, e1, None, None, x2, e2, None, None, y)
