@@ -656,18 +656,26 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm2_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
+  // Fragments double-buffered in registers: group g + 1's four float4
+  // reads are interleaved with group g's 16 MFMAs (one read after every
+  // four MFMAs), so no MFMA waits on a fragment read.
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      sg_f32x4 fa[2], fb[2];
+    sg_f32x4 fa[2][2], fb[2][2];
+    auto frag = [&](int g, int st) {
 #pragma unroll
       for (int a = 0; a < 2; ++a)
-        fa[a] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+        fa[st][a] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
             lb + offN + a * 32 * kG2BK + qoff[g]);
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        fb[b] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
+        fb[st][b] = *reinterpret_cast<const DGMC_LDS sg_f32x4*>(
             la + offM + b * 32 * kG2BK + qoff[g]);
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int st = g & 1;
+      if (g < 3) frag(g + 1, st ^ 1);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -675,8 +683,22 @@ __global__ __launch_bounds__(kSgThreads, 2) void slot_gemm2_kernel(
 #pragma unroll
           for (int b = 0; b < 2; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-                fa[a][t], fb[b][t], acc[a][b], 0, 0, 0);
+                fa[st][a][t], fb[st][b][t], acc[a][b], 0, 0, 0);
     }
+    // Issue order: group 0's reads, then per group 4 x (2 MFMA, 1 read) +
+    // 8 MFMA while a next group exists (its reads land >= 8 MFMAs before
+    // use), then the last group's 16 MFMAs.
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   };
   auto epilogue = [&](int uu) {
     const int m0 = (uu / ntn) * kSgBM + wm * 64 + i;
