@@ -99,6 +99,11 @@ def parse_args(argv=None):
                    help='held-out Hits@1/@10 on this many test pairs per '
                         'evaluation, outside the timed region (reference '
                         'test loop: examples/pascal.py:80-99); 0 skips it')
+    p.add_argument('--normalization', default='softmax',
+                   choices=['softmax', 'sinkhorn'],
+                   help='dense correspondence normalisation: the reference '
+                        'row softmax (headline) or the opt-in masked '
+                        'log-domain Sinkhorn (BASELINE config 3)')
     p.add_argument('--json-out', default=None)
     return p.parse_args(argv)
 
@@ -107,7 +112,8 @@ def build_model(cfg, args, num_node_features, num_edge_features, device):
     psi_1 = SplineCNN(num_node_features, 256, num_edge_features, 2,
                       cat=False, dropout=0.5)
     psi_2 = SplineCNN(128, 128, num_edge_features, 2, cat=True, dropout=0.0)
-    return DGMC(psi_1, psi_2, num_steps=args.num_steps).to(device)
+    return DGMC(psi_1, psi_2, num_steps=args.num_steps,
+                normalization=args.normalization).to(device)
 
 
 def bench_kg(args, cfg, device):
@@ -291,6 +297,7 @@ def main(argv=None):
             'consensus_steps': args.num_steps,
             'hipgraph': bool(use_graph),
             'mode': trainer.mode,
+            'normalization': args.normalization,
         },
         'hits@1_train': round(hits1, 4) if hits1 is not None else None,
         'loss': round(mean_loss, 4),
