@@ -1,8 +1,10 @@
 set -euo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-OUT=gpurun_out/sched
+OUT=gpurun_out/s3
 mkdir -p $OUT
-timeout -k 10 300 python -m pytest -q -x tests/test_slot_gemm.py -m gpu > $OUT/t.txt 2>&1 || { tail -30 $OUT/t.txt; exit 1; }
-tail -1 $OUT/t.txt
-timeout -k 10 300 python tools/bench_slot_gemm.py --reps 20 > $OUT/v2.txt 2>&1
-grep -E "fwd2|dX2|wgrad" $OUT/v2.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python bench.py --normalization sinkhorn --steps 100 --warmup 10 --json-out $OUT/sinkhorn.json > $OUT/sinkhorn.log 2>&1
+tail -1 $OUT/sinkhorn.log | cut -c1-250
+bash tools/prof_quick.sh prof_fp32 > $OUT/prof.txt 2>&1
+head -3 $OUT/prof.txt
