@@ -1091,13 +1091,29 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
         acc.w = fmaf(w[u], v[u].w, acc.w);
       }
     }
-    for (; e < e1; ++e) {
-      const float w = val[e];
-      const float4 v = ld4(g + (size_t)col[e] * C + c0);
-      acc.x = fmaf(w, v.x, acc.x);
-      acc.y = fmaf(w, v.y, acc.y);
-      acc.z = fmaf(w, v.z, acc.z);
-      acc.w = fmaf(w, v.w, acc.w);
+    // Remainder (most compact rows hold 1-3 entries): one predicated batch
+    // - a single (col, val) then g latency round instead of one per entry.
+    const int rem = e1 - e;
+    if (rem > 0) {
+      float w[3];
+      float4 v[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const bool ok = u < rem;
+        const int eu = ok ? e + u : e;     // (clamped: never past the row)
+        const float wv = val[eu];
+        const int cv = col[eu];
+        w[u] = ok ? wv : 0.f;
+        v[u] = ld4(g + (size_t)(ok ? cv : 0) * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (u < rem) {
+          acc.x = fmaf(w[u], v[u].x, acc.x);
+          acc.y = fmaf(w[u], v[u].y, acc.y);
+          acc.z = fmaf(w[u], v[u].z, acc.z);
+          acc.w = fmaf(w[u], v[u].w, acc.w);
+        }
     }
     *reinterpret_cast<float4*>(out + (size_t)p * C + c0) = acc;
   }
@@ -1168,16 +1184,41 @@ __global__ __launch_bounds__(256) void sg_gather_sum_kernel(
           make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
+  // The row's S posmap entries are loaded once, lane-parallel (lane l of
+  // the group holds entries l, l + LPR, ...), and broadcast by shuffles;
+  // the Z rows are then gathered eight slots at a time, branch-free (unused
+  // slots read row 0 and are not added), so a node's gathers are in flight
+  // together instead of one dependent (posmap, Z) round per slot.
+  constexpr int NP = (kSgMaxS + LPR - 1) / LPR;
   const int* pm = posmap + (size_t)j * S;
+  int pl[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int k = q * LPR + lane;
+    const int v = pm[k < S ? k : 0];       // (clamped: never past the row)
+    pl[q] = k < S ? v : -1;
+  }
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
     float4 acc = add ? ld4(add + (size_t)j * lda + c0)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < S; ++k) {
-      const int p = pm[k];
-      if (p >= 0) {
-        const float4 v = ld4(Z + (size_t)p * C + c0);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+#pragma unroll
+    for (int k0 = 0; k0 < kSgMaxS; k0 += 8) {
+      if (k0 >= S) break;
+      int p[8];
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + u;
+        p[u] = __shfl(pl[k / LPR], k % LPR, LPR);
+        p[u] = k < S ? p[u] : -1;
+        v[u] = ld4(Z + (size_t)(p[u] < 0 ? 0 : p[u]) * C + c0);
       }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p[u] >= 0) {          // slot order: the same sums as before
+          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z;
+          acc.w += v[u].w;
+        }
     }
     *reinterpret_cast<float4*>(out + (size_t)j * C + c0) = acc;
   }

@@ -606,20 +606,27 @@ class _CatMatmulF32(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, w_t, loop, *parts):
+        from ..runtime.cache import cached
         ops = _backend.ops()
         out = ops.dense_nt_f32(list(parts), w_t.detach().t().contiguous())
         ctx.loop, ctx.np = loop, len(parts)
-        ctx.save_for_backward(w_t)
+        # The backward's B operand (w_t itself, k-contiguous): one copy per
+        # forward scope, shared by the consensus loop's uses (was a clone
+        # per use in the backward).
+        wc = cached(('cat_f32_w', w_t.data_ptr(), w_t._version,
+                     tuple(w_t.shape), tuple(w_t.stride())),
+                    lambda: w_t.detach().contiguous())
+        ctx.save_for_backward(w_t, wc)
         ctx.idx = loop.register() if loop is not None else None
         ctx.parts = tuple(parts) if ctx.needs_input_grad[0] else None
         return out
 
     @staticmethod
     def backward(ctx, g):
-        w_t, = ctx.saved_tensors
+        w_t, wc = ctx.saved_tensors
         ops = _backend.ops()
         g = g.float().contiguous()
-        gx = ops.dense_nt_f32([g], w_t.detach().contiguous())   # [M, 128 n]
+        gx = ops.dense_nt_f32([g], wc)                          # [M, 128 n]
         grads = tuple(gx[:, 128 * i:128 * (i + 1)]
                       if ctx.needs_input_grad[2 + i] else None
                       for i in range(ctx.np))
