@@ -240,7 +240,10 @@ at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
-                            const c10::optional<at::Tensor>& seg);
+                            const c10::optional<at::Tensor>& seg,
+                            const c10::optional<at::Tensor>& ranges);
+at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
+                              const at::Tensor& cinv);
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t N, int64_t S,
                            const c10::optional<at::Tensor>& add,
@@ -435,7 +438,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "seg01) -> Tensor");
   m.def(
       "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
-      "Tensor g, Tensor? seg=None) -> Tensor");
+      "Tensor g, Tensor? seg=None, Tensor? ranges=None) -> Tensor");
+  m.def("slot_rowmap_ranges(Tensor rowptr, Tensor cinv) -> Tensor");
   m.def(
       "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add, "
       "int row0=0) -> Tensor");
@@ -515,6 +519,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_nt_f32", &dgmc::dense_nt_f32);
   m.impl("dense_wgrad_f32", &dgmc::dense_wgrad_f32);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
+  m.impl("slot_rowmap_ranges", &dgmc::slot_rowmap_ranges);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);
   m.impl("sinkhorn_fwd", &dgmc::sinkhorn_fwd);

@@ -1049,12 +1049,23 @@ at::Tensor slot_weight_t(const at::Tensor& weight,
 // val[e] * g[col[e], :]  (zero for cinv[p] < 0) - dY_c = A_c^T g' straight
 // from the assembled A^T (rows j*S + k) without re-indexing it.
 // ---------------------------------------------------------------------------
+// (start, end) of every compact row's A^T entries (one int2 per row: one
+// dependent load fewer than cinv -> rowptr in each rowmap SpMM of a step).
+__global__ __launch_bounds__(256) void sg_rowmap_ranges_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ cinv, int P,
+    int2* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int c = cinv[p];
+  out[p] = c >= 0 ? make_int2(rowptr[c], rowptr[c + 1]) : make_int2(0, 0);
+}
+
 template <int LPR, bool XL>
 __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ val, const int* __restrict__ cinv,
-    const int* __restrict__ seg, int S, const float* __restrict__ g,
-    float* __restrict__ out, int P, int C) {
+    const int2* __restrict__ ranges, const int* __restrict__ seg, int S,
+    const float* __restrict__ g, float* __restrict__ out, int P, int C) {
   constexpr int RPB = 256 / LPR;
   int p;
   if (XL) {
@@ -1070,8 +1081,16 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
   // Rows past the last slot segment are never read (slot_gemm / wgrad stop
   // at seg[S]); padding rows inside segments are written as zeros.
   if (p >= P || (seg != nullptr && p >= seg[S])) return;
-  const int c = cinv[p];
-  const int e0 = c >= 0 ? rowptr[c] : 0, e1 = c >= 0 ? rowptr[c + 1] : 0;
+  int e0, e1;
+  if (ranges != nullptr) {
+    const int2 r = ranges[p];
+    e0 = r.x;
+    e1 = r.y;
+  } else {
+    const int c = cinv[p];
+    e0 = c >= 0 ? rowptr[c] : 0;
+    e1 = c >= 0 ? rowptr[c + 1] : 0;
+  }
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     int e = e0;
@@ -1122,7 +1141,8 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
-                            const c10::optional<at::Tensor>& seg) {
+                            const c10::optional<at::Tensor>& seg,
+                            const c10::optional<at::Tensor>& ranges) {
   TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat &&
                   g.is_contiguous() && g.dim() == 2 && g.size(1) % 4 == 0 &&
                   aligned16(g.data_ptr()),
@@ -1139,6 +1159,13 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
     segp = seg->data_ptr<int>();
     S = (int)seg->numel() - 1;
   }
+  const int2* rg = nullptr;
+  if (ranges.has_value() && ranges->defined()) {
+    TORCH_CHECK(ranges->scalar_type() == at::kInt && ranges->is_contiguous() &&
+                    ranges->numel() == 2 * P,
+                "slot_spmm_rowmap: int32 ranges [P, 2]");
+    rg = reinterpret_cast<const int2*>(ranges->data_ptr<int>());
+  }
   const bool xl = segp != nullptr;      // XCD-local row groups (above)
   const int lanes = (int)(C / 4);
   auto go = [&](auto lpr) {
@@ -1152,8 +1179,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                    : sg_spmm_rowmap_kernel<L, false>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream(),
                        rowptr.data_ptr<int>(), col.data_ptr<int>(),
-                       val.data_ptr<float>(), cinv.data_ptr<int>(), segp, S,
-                       g.data_ptr<float>(), out.data_ptr<float>(), (int)P,
+                       val.data_ptr<float>(), cinv.data_ptr<int>(), rg, segp,
+                       S, g.data_ptr<float>(), out.data_ptr<float>(), (int)P,
                        (int)C);
   };
   if (lanes <= 8) go(std::integral_constant<int, 8>());
@@ -1222,6 +1249,24 @@ __global__ __launch_bounds__(256) void sg_gather_sum_kernel(
     }
     *reinterpret_cast<float4*>(out + (size_t)j * C + c0) = acc;
   }
+}
+
+at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
+                              const at::Tensor& cinv) {
+  TORCH_CHECK(rowptr.is_cuda() && rowptr.scalar_type() == at::kInt &&
+                  cinv.scalar_type() == at::kInt && cinv.is_contiguous() &&
+                  rowptr.is_contiguous(),
+              "slot_rowmap_ranges: int32 rowptr / cinv");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(cinv.device());
+  const int64_t P = cinv.numel();
+  at::Tensor out = at::empty({P, 2}, cinv.options());
+  if (P == 0) return out;
+  hipLaunchKernelGGL(sg_rowmap_ranges_kernel, dim3((unsigned)((P + 255) / 256)),
+                     dim3(256), 0, stream(), rowptr.data_ptr<int>(),
+                     cinv.data_ptr<int>(), (int)P,
+                     reinterpret_cast<int2*>(out.data_ptr<int>()));
+  DGMC_CHECK_LAUNCH();
+  return out;
 }
 
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,

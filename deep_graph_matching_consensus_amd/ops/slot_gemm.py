@@ -59,6 +59,18 @@ def dx_tiles(plan, row0):
     return t
 
 
+def rowmap_ranges(plan, At):
+    """``[P_cap, 2]`` int32 A^T entry range of every compact row, built once
+    per plan and transposed operator (shared by the step's rowmap SpMMs)."""
+    cache = plan.__dict__.setdefault('_ranges', {})
+    key = At.rowptr.data_ptr()
+    r = cache.get(key)
+    if r is None:
+        r = cache[key] = _backend.ops().slot_rowmap_ranges(At.rowptr,
+                                                           plan.cinv)
+    return r
+
+
 def compact_plan(op, S):
     cache = op.__dict__.setdefault('_compact_plan', {})
     p = cache.get(S)
@@ -145,7 +157,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                   torch.float32, None, False, part)
         At = op.t()
         dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
-                                    plan.seg)
+                                    plan.seg, rowmap_ranges(plan, At))
         gx = None
         if ctx.needs_input_grad[0]:
             # K = 128 (psi_2): the register-staged v1 kernel streams dY_c

@@ -104,6 +104,14 @@ def main():
                                                 plan.cinv, g, plan.seg),
                    args.reps)
         print('%4d->%-4d rowmap %7.1f us' % (cin, cout, t))
+        rg = ops.slot_rowmap_ranges(At.rowptr, plan.cinv)
+        d2 = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
+                                  plan.seg, rg)
+        assert torch.equal(d2[:used], dyc[:used])
+        t = timeit(lambda: ops.slot_spmm_rowmap(At.rowptr, At.col, At.val,
+                                                plan.cinv, g, plan.seg, rg),
+                   args.reps)
+        print('%4d->%-4d rowmap+ranges %7.1f us' % (cin, cout, t))
         t = timeit(lambda: ops.slot_gemm(dyc, plan.src, plan.seg, w, r,
                                          True), args.reps)
         print('%4d->%-4d dX    %8.1f us  %6.1f TF/s' % (cin, cout, t,
