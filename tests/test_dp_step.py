@@ -83,6 +83,8 @@ def _run(mode, device, env=None, steps=3, world=2):
 def test_in_step_allreduce_matches_post_step_cpu():
     a = _run('static', 'cpu')
     assert torch.equal(a[0], a[1])
+    # Shards differ, static capacities agree (max over the ranks).
+    assert _run.caps[0] == _run.caps[1]
     b = _run('static', 'cpu', {'DGMC_AMD_IN_STEP_ALLREDUCE': '0'})
     assert torch.equal(b[0], b[1])
     assert torch.equal(a[0], b[0])
