@@ -16,105 +16,111 @@
 // rebuilds each half-step's output from them and applies the normalisation
 // Jacobians in reverse:  row step  D_ij -= exp(out_ij) sum_k D_ik,
 //                        column step D_ij -= exp(out_ij) sum_k D_kj.
-// The pair tile lives in LDS (N <= 64); rows / columns are reduced one per
-// wave (64 lanes = the other index).  Deterministic, no atomics.
+// The pair tile lives in LDS (N <= 64).  ONE wave per pair: in a row step
+// lane i owns row i and reduces it sequentially (the tile's odd pitch keeps
+// the lanes' reads of one column conflict-free), in a column step lane j
+// owns column j - no cross-lane reductions, no multi-wave barriers (a
+// half-step is ~20 LDS reads + exps per lane; was one wave-wide LSE per row
+// with 4 waves and a block barrier per half-step: 63 -> see
+// docs/performance.md).  Deterministic, no atomics.
 #include "common.h"
 
 namespace dgmc {
 
 namespace {
-constexpr int kShThreads = 256;
-constexpr int kShWaves = kShThreads / kWave;
 constexpr int kShMaxN = 64;
+constexpr int kShPitch = kShMaxN + 1;
 
-// LSE over the valid lanes of a wave (-inf -> empty set -> 0 potential).
-__device__ __forceinline__ float wave_lse(float v, bool valid) {
-  const float x = valid ? v : -INFINITY;
-  const float m = wave_max(x);
+// LSE_k (row[k * stride] - pot[k]) over k < n (0 for an empty set).
+__device__ __forceinline__ float lse_line(const DGMC_LDS float* row,
+                                          int stride,
+                                          const DGMC_LDS float* pot, int n) {
+  float m = -INFINITY;
+  for (int k = 0; k < n; ++k) m = fmaxf(m, row[k * stride] - pot[k]);
   if (m == -INFINITY) return 0.f;
-  const float e = valid ? __expf(x - m) : 0.f;
-  return m + __logf(wave_sum(e));
+  float sum = 0.f;
+  for (int k = 0; k < n; ++k) sum += __expf(row[k * stride] - pot[k] - m);
+  return m + __logf(sum);
 }
 }  // namespace
 
-__global__ __launch_bounds__(kShThreads) void sinkhorn_fwd_kernel(
+__global__ __launch_bounds__(kWave) void sinkhorn_fwd_kernel(
     const float* __restrict__ S_hat, const int* __restrict__ n_s,
     const int* __restrict__ n_t, int Ns, int Nt, int iters, float inv_tau,
     float* __restrict__ P, float* __restrict__ a_hist,
     float* __restrict__ b_hist) {
-  __shared__ float L0[kShMaxN * (kShMaxN + 1)];
-  __shared__ float a[kShMaxN], b[kShMaxN];
+  __shared__ float L0_[kShMaxN * kShPitch];
+  __shared__ float a_[kShMaxN], b_[kShMaxN];
+  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
+  DGMC_LDS float* a = (DGMC_LDS float*)a_;
+  DGMC_LDS float* b = (DGMC_LDS float*)b_;
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x;
   const int ns = n_s[pb], nt = n_t[pb];
-  const int NP = Nt + 1;
+  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
   const float* S = S_hat + (size_t)pb * Ns * Nt;
-  for (int e = tid; e < Ns * Nt; e += kShThreads) {
+  for (int e = lane; e < Ns * Nt; e += kWave) {
     const int i = e / Nt, j = e - i * Nt;
     L0[i * NP + j] = S[e] * inv_tau;
   }
-  for (int j = tid; j < kShMaxN; j += kShThreads) b[j] = 0.f;
+  b[lane] = 0.f;
+  a[lane] = 0.f;
   __syncthreads();
   float* ah = a_hist + (size_t)pb * (iters + 1) * Ns;
   float* bh = b_hist + (size_t)pb * iters * Nt;
   for (int it = 0; it <= iters; ++it) {
-    // Row step.
-    for (int i = wave; i < Ns; i += kShWaves) {
-      const bool v = i < ns && lane < nt;
-      const float x = v ? L0[i * NP + lane] - b[lane] : 0.f;
-      const float r = wave_lse(x, v);
-      if (lane == 0) {
-        a[i] = r;
-        ah[it * Ns + i] = r;
-      }
+    // Row step: lane i.
+    if (lane < Ns) {
+      const float r = lane < ns ? lse_line(L0 + lane * NP, 1, b, nt) : 0.f;
+      a[lane] = r;
+      ah[it * Ns + lane] = r;
     }
     __syncthreads();
     if (it == iters) break;
-    // Column step.
-    for (int j = wave; j < Nt; j += kShWaves) {
-      const bool v = j < nt && lane < ns;
-      const float x = v ? L0[lane * NP + j] - a[lane] : 0.f;
-      const float c = wave_lse(x, v);
-      if (lane == 0) {
-        b[j] = c;
-        bh[it * Nt + j] = c;
-      }
+    // Column step: lane j.
+    if (lane < Nt) {
+      const float c = lane < nt ? lse_line(L0 + lane, NP, a, ns) : 0.f;
+      b[lane] = c;
+      bh[it * Nt + lane] = c;
     }
     __syncthreads();
   }
   float* Pb = P + (size_t)pb * Ns * Nt;
-  for (int e = tid; e < Ns * Nt; e += kShThreads) {
+  for (int e = lane; e < Ns * Nt; e += kWave) {
     const int i = e / Nt, j = e - i * Nt;
     Pb[e] = (i < ns && j < nt) ? __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
   }
 }
 
-__global__ __launch_bounds__(kShThreads) void sinkhorn_bwd_kernel(
+__global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
     const float* __restrict__ G, const float* __restrict__ S_hat,
     const int* __restrict__ n_s, const int* __restrict__ n_t, int Ns, int Nt,
     int iters, float inv_tau, const float* __restrict__ a_hist,
     const float* __restrict__ b_hist, float* __restrict__ dS) {
-  __shared__ float L0[kShMaxN * (kShMaxN + 1)];
-  __shared__ float D[kShMaxN * (kShMaxN + 1)];
-  __shared__ float a[kShMaxN], b[kShMaxN], sums[kShMaxN];
+  __shared__ float L0_[kShMaxN * kShPitch];
+  __shared__ float D_[kShMaxN * kShPitch];
+  __shared__ float a_[kShMaxN], b_[kShMaxN];
+  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
+  DGMC_LDS float* D = (DGMC_LDS float*)D_;
+  DGMC_LDS float* a = (DGMC_LDS float*)a_;
+  DGMC_LDS float* b = (DGMC_LDS float*)b_;
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x;
   const int ns = n_s[pb], nt = n_t[pb];
-  const int NP = Nt + 1;
+  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
   const float* S = S_hat + (size_t)pb * Ns * Nt;
   const float* Gb = G + (size_t)pb * Ns * Nt;
   const float* ah = a_hist + (size_t)pb * (iters + 1) * Ns;
   const float* bh = b_hist + (size_t)pb * iters * Nt;
-  for (int i = tid; i < Ns; i += kShThreads) a[i] = ah[iters * Ns + i];
-  for (int j = tid; j < Nt; j += kShThreads)
-    b[j] = iters > 0 ? bh[(iters - 1) * Nt + j] : 0.f;
-  for (int e = tid; e < Ns * Nt; e += kShThreads) {
+  if (lane < Ns) a[lane] = ah[iters * Ns + lane];
+  if (lane < Nt) b[lane] = iters > 0 ? bh[(iters - 1) * Nt + lane] : 0.f;
+  for (int e = lane; e < Ns * Nt; e += kWave) {
     const int i = e / Nt, j = e - i * Nt;
     L0[i * NP + j] = S[e] * inv_tau;
   }
   __syncthreads();
   // dL of the final output: G * P (P = exp(out of the final row step)).
-  for (int e = tid; e < Ns * Nt; e += kShThreads) {
+  for (int e = lane; e < Ns * Nt; e += kWave) {
     const int i = e / Nt, j = e - i * Nt;
     const bool v = i < ns && j < nt;
     D[i * NP + j] = v ? Gb[e] * __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
@@ -124,40 +130,36 @@ __global__ __launch_bounds__(kShThreads) void sinkhorn_bwd_kernel(
     const bool row = (step & 1) == 0;     // even: row step, odd: column step
     const int it = step >> 1;
     // Potentials defining this half-step's output L0 - a - b.
-    if (row) {
-      for (int i = tid; i < Ns; i += kShThreads) a[i] = ah[it * Ns + i];
-      for (int j = tid; j < Nt; j += kShThreads)
-        b[j] = it > 0 ? bh[(it - 1) * Nt + j] : 0.f;
-    } else {
-      for (int i = tid; i < Ns; i += kShThreads) a[i] = ah[it * Ns + i];
-      for (int j = tid; j < Nt; j += kShThreads) b[j] = bh[it * Nt + j];
-    }
+    if (lane < Ns) a[lane] = ah[it * Ns + lane];
+    if (lane < Nt)
+      b[lane] = row ? (it > 0 ? bh[(it - 1) * Nt + lane] : 0.f)
+                    : bh[it * Nt + lane];
     __syncthreads();
     if (row) {
-      for (int i = wave; i < Ns; i += kShWaves) {
-        const float d = lane < Nt ? D[i * NP + lane] : 0.f;
-        const float s = wave_sum(d);
-        if (lane == 0) sums[i] = s;
+      // Lane i: D_ij -= exp(out_ij) sum_k D_ik over its row.
+      if (lane < ns) {
+        DGMC_LDS float* Dr = D + lane * NP;
+        const DGMC_LDS float* Lr = L0 + lane * NP;
+        float sum = 0.f;
+        for (int j = 0; j < Nt; ++j) sum += Dr[j];
+        const float ai = a[lane];
+        for (int j = 0; j < nt; ++j)
+          Dr[j] -= __expf(Lr[j] - ai - b[j]) * sum;
       }
     } else {
-      for (int j = wave; j < Nt; j += kShWaves) {
-        const float d = lane < Ns ? D[lane * NP + j] : 0.f;
-        const float s = wave_sum(d);
-        if (lane == 0) sums[j] = s;
-      }
-    }
-    __syncthreads();
-    for (int e = tid; e < Ns * Nt; e += kShThreads) {
-      const int i = e / Nt, j = e - i * Nt;
-      if (i < ns && j < nt) {
-        const float p = __expf(L0[i * NP + j] - a[i] - b[j]);
-        D[i * NP + j] -= p * (row ? sums[i] : sums[j]);
+      // Lane j: D_ij -= exp(out_ij) sum_k D_kj over its column.
+      if (lane < nt) {
+        float sum = 0.f;
+        for (int i = 0; i < Ns; ++i) sum += D[i * NP + lane];
+        const float bj = b[lane];
+        for (int i = 0; i < ns; ++i)
+          D[i * NP + lane] -= __expf(L0[i * NP + lane] - a[i] - bj) * sum;
       }
     }
     __syncthreads();
   }
   float* out = dS + (size_t)pb * Ns * Nt;
-  for (int e = tid; e < Ns * Nt; e += kShThreads) {
+  for (int e = lane; e < Ns * Nt; e += kWave) {
     const int i = e / Nt, j = e - i * Nt;
     out[e] = D[i * NP + j] * inv_tau;
   }
@@ -185,7 +187,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
   at::Tensor bh = at::empty({B, std::max<int64_t>(iters, 1), Nt},
                             S_hat.options());
   if (B == 0) return {P, ah, bh};
-  hipLaunchKernelGGL(sinkhorn_fwd_kernel, dim3(B), dim3(kShThreads), 0,
+  hipLaunchKernelGGL(sinkhorn_fwd_kernel, dim3(B), dim3(kWave), 0,
                      stream(), S_hat.data_ptr<float>(), n_s.data_ptr<int>(),
                      n_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
                      (float)(1.0 / tau), P.data_ptr<float>(),
@@ -210,7 +212,7 @@ at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   at::Tensor dS = at::empty_like(S_hat);
   if (B == 0) return dS;
-  hipLaunchKernelGGL(sinkhorn_bwd_kernel, dim3(B), dim3(kShThreads), 0,
+  hipLaunchKernelGGL(sinkhorn_bwd_kernel, dim3(B), dim3(kWave), 0,
                      stream(), G.data_ptr<float>(), S_hat.data_ptr<float>(),
                      n_s.data_ptr<int>(), n_t.data_ptr<int>(), (int)Ns,
                      (int)Nt, (int)iters, (float)(1.0 / tau),
