@@ -67,11 +67,13 @@ __global__ __launch_bounds__(256) void candidates_kernel(
 // candidates, it takes the last slot (rows hold at most one ground truth).
 __global__ __launch_bounds__(256) void include_gt_kernel(
     const int64_t* __restrict__ gt_row, const int64_t* __restrict__ gt_col,
-    int64_t G, int kk, int64_t* __restrict__ out) {
+    int64_t G, int64_t R, int kk, int64_t* __restrict__ out) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
+  const int64_t r = gt_row[g];
+  if (r < 0 || r >= R) return;               // (invalid row: never written)
   const int64_t col = gt_col[g];
-  int64_t* row = out + gt_row[g] * kk;
+  int64_t* row = out + r * kk;
   bool present = false;
   for (int j = 0; j < kk; ++j) present |= row[j] == col;
   if (!present) row[kk - 1] = col;
@@ -197,7 +199,7 @@ at::Tensor train_candidates(const at::Tensor& topk, int64_t n_t, int64_t kr,
   if (G > 0) {
     hipLaunchKernelGGL(include_gt_kernel, dim3((unsigned)((G + 255) / 256)),
                        dim3(256), 0, stream(), gt_row.data_ptr<int64_t>(),
-                       gt_col.data_ptr<int64_t>(), G, (int)kk,
+                       gt_col.data_ptr<int64_t>(), G, R, (int)kk,
                        out.data_ptr<int64_t>());
     DGMC_CHECK_LAUNCH();
   }

@@ -1,4 +1,14 @@
 set -euo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-bash tools/prof_quick.sh prof_sink --normalization sinkhorn > gpurun_out/prof_sink_head.txt 2>&1
-head -30 gpurun_out/prof_sink_head.txt
+OUT=gpurun_out/final
+mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+tail -1 $OUT/smoke.log
+timeout -k 10 300 python bench.py > $OUT/bench_default.log 2>&1
+tail -1 $OUT/bench_default.log | cut -c1-200
+timeout -k 10 300 python bench.py --dtype bf16 --steps 200 --warmup 20 --json-out $OUT/bf16.json > $OUT/bf16.log 2>&1
+tail -1 $OUT/bf16.log | cut -c1-200
+timeout -k 10 600 python bench.py --config dbp15k --steps 20 --warmup 3 --json-out $OUT/dbp.json > $OUT/dbp.log 2>&1
+tail -1 $OUT/dbp.log | cut -c1-200
