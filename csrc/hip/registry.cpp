@@ -78,6 +78,13 @@ sparse_consensus_bwd(
     const c10::optional<at::Tensor>& gS);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
     const at::Tensor& rowptr, int64_t nnz, int64_t T);
+void spmm_split_out(const at::Tensor& rowptr, const at::Tensor& col,
+                    const at::Tensor& val, const at::Tensor& short_rows,
+                    const at::Tensor& long_rows, const at::Tensor& x,
+                    const c10::optional<at::Tensor>& self_x,
+                    const c10::optional<at::Tensor>& self_scale,
+                    const c10::optional<at::Tensor>& bias, bool relu,
+                    at::Tensor out);
 void spmm_pieces_out(const at::Tensor& rowptr, const at::Tensor& col,
                      const at::Tensor& val, const c10::optional<at::Tensor>& perm,
                      const at::Tensor& pptr, const at::Tensor& prow,
@@ -420,6 +427,10 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "self_x, Tensor? self_scale, Tensor? bias, bool relu, Tensor(a!) out) -> "
       "()");
   m.def(
+      "spmm_split_out(Tensor rowptr, Tensor col, Tensor val, Tensor short_rows, "
+      "Tensor long_rows, Tensor x, Tensor? self_x, Tensor? self_scale, "
+      "Tensor? bias, bool relu, Tensor(a!) out) -> ()");
+  m.def(
       "slot_compact_plan(Tensor rowptr, Tensor col, int Nsrc, int S, int "
       "P_cap) -> Tensor[]");
   m.def(
@@ -510,6 +521,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("sparse_consensus_bwd", &dgmc::sparse_consensus_bwd);
   m.impl("sparse_consensus_fwd_prob", &dgmc::sparse_consensus_fwd_prob);
   m.impl("spmm_pieces_out", &dgmc::spmm_pieces_out);
+  m.impl("spmm_split_out", &dgmc::spmm_split_out);
   m.impl("piece_plan", &dgmc::piece_plan);
   m.impl("slot_compact_plan", &dgmc::slot_compact_plan);
   m.impl("slot_gemm", &dgmc::slot_gemm);

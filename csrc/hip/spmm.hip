@@ -391,6 +391,108 @@ __global__ __launch_bounds__(256) void spmm_piece_kernel(
   }
 }
 
+// Static skewed operators (knowledge-graph relational plans): rows split
+// once into SHORT rows (<= T entries: one G-lane group each, PPB per block)
+// and LONG rows (one 256-thread block each: its PPB lane groups take every
+// PPB-th entry, partials reduced in group order through LDS) - one launch,
+// no per-piece partials and no fold pass.  Requires C <= G * VEC.
+template <typename TIn, typename TOut, int VEC, int G>
+__global__ __launch_bounds__(256) void spmm_split_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ val, const int* __restrict__ short_rows,
+    int n_short, const int* __restrict__ long_rows,
+    const TIn* __restrict__ x, const TIn* __restrict__ self_x,
+    const float* __restrict__ self_scale, const float* __restrict__ bias,
+    TOut* __restrict__ out, int C, int relu) {
+  constexpr int PPB = 256 / G;
+  __shared__ float red[PPB * G * VEC];
+  const int nb_short = (n_short + PPB - 1) / PPB;
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  const int q = threadIdx.x / G, gl = threadIdx.x % G;
+  const int c0 = gl * VEC;
+  const float scale = self_x != nullptr ? self_scale[0] : 0.f;
+  float acc[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+  if (b < nb_short) {
+    const int idx = b * PPB + q;
+    if (idx >= n_short || c0 >= C) return;
+    const int r = short_rows[idx];
+    const int beg = rowptr[r], end = rowptr[r + 1];
+    int p = beg;
+    for (; p + 4 <= end; p += 4) {
+      float xv[4][VEC];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w[u] = val[p + u];
+        load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
+    }
+    if (p < end) {
+      float xv[4][VEC];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w[u] = 0.f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xv[u][k] = 0.f;
+        if (p + u < end) {
+          w[u] = val[p + u];
+          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
+    }
+    spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu,
+                                out);
+    return;
+  }
+  // Long row: the whole block (block-uniform branch).
+  const int r = long_rows[b - nb_short];
+  const int beg = rowptr[r], end = rowptr[r + 1];
+  if (c0 < C) {
+    int e = beg + q;
+    for (; e + 3 * PPB < end; e += 4 * PPB) {
+      float xv[4][VEC];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        w[u] = val[e + u * PPB];
+        load_vec<TIn, VEC>(x + (size_t)col[e + u * PPB] * C + c0, xv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
+    }
+    for (; e < end; e += PPB) {
+      float xv[VEC];
+      const float w = val[e];
+      load_vec<TIn, VEC>(x + (size_t)col[e] * C + c0, xv);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[k], acc[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) red[q * G * VEC + c0 + k] = acc[k];
+  __syncthreads();
+  if (q != 0 || c0 >= C) return;
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc[k] = red[c0 + k];
+  for (int qq = 1; qq < PPB; ++qq)
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc[k] += red[qq * G * VEC + c0 + k];
+  spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu, out);
+}
+
 // Pass 2: rows with several pieces.  `colscale` (optional) multiplies channel
 // c by sign * colscale[c] before the epilogue (the -w2 of the consensus
 // backward, sparse_corr.hip).
@@ -543,6 +645,78 @@ void spmm_pieces_out(const at::Tensor& rowptr, const at::Tensor& col,
                          (int)R, (int)C, sp, ssp, bp, relu ? 1 : 0,
                          (const float*)nullptr, 1.f, op);
       DGMC_CHECK_LAUNCH();
+    });
+  });
+}
+
+
+// Static skewed operator, short / long row split (see spmm_split_kernel).
+void spmm_split_out(const at::Tensor& rowptr, const at::Tensor& col,
+                    const at::Tensor& val, const at::Tensor& short_rows,
+                    const at::Tensor& long_rows, const at::Tensor& x,
+                    const c10::optional<at::Tensor>& self_x,
+                    const c10::optional<at::Tensor>& self_scale,
+                    const c10::optional<at::Tensor>& bias, bool relu,
+                    at::Tensor out) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous(),
+              "spmm_split: contiguous x [N, C]");
+  TORCH_CHECK(rowptr.scalar_type() == at::kInt && col.scalar_type() == at::kInt &&
+                  short_rows.scalar_type() == at::kInt &&
+                  long_rows.scalar_type() == at::kInt &&
+                  val.scalar_type() == at::kFloat && val.numel() == col.numel(),
+              "spmm_split: int32 index / fp32 values");
+  const int64_t R = rowptr.numel() - 1, C = x.size(1);
+  TORCH_CHECK(out.is_contiguous() && out.dim() == 2 && out.size(0) == R &&
+                  out.size(1) == C,
+              "spmm_split: out must be a contiguous [R, C] tensor");
+  TORCH_CHECK(short_rows.numel() + long_rows.numel() == R,
+              "spmm_split: every row is short or long");
+  at::Tensor sx_c, ss_c, b_c;
+  if (self_x.has_value() && self_x->defined()) {
+    sx_c = self_x->contiguous();
+    TORCH_CHECK(sx_c.scalar_type() == x.scalar_type() && sx_c.size(0) == R &&
+                    sx_c.size(1) == C && self_scale.has_value() &&
+                    self_scale->defined(),
+                "spmm_split: self_x [R, C] with self_scale");
+    ss_c = self_scale->to(at::kFloat).contiguous();
+  }
+  if (bias.has_value() && bias->defined()) {
+    b_c = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b_c.numel() == C, "spmm_split: bias size");
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  if (R == 0) return;
+  const int n_short = (int)short_rows.numel(), n_long = (int)long_rows.numel();
+  DGMC_DISPATCH_FLOAT(x.scalar_type(), TIn, [&] {
+    constexpr int V = Vec16<TIn>::N;
+    TORCH_CHECK(C % V == 0 && C / V <= 16 && aligned16(x.data_ptr()) &&
+                    aligned16(out.data_ptr()),
+                "spmm_split: C a multiple of the vector width, <= 16 vectors");
+    const TIn* xp = reinterpret_cast<const TIn*>(x.data_ptr());
+    const TIn* sp = sx_c.defined() ? reinterpret_cast<const TIn*>(sx_c.data_ptr())
+                                   : nullptr;
+    const float* ssp = ss_c.defined() ? ss_c.data_ptr<float>() : nullptr;
+    const float* bp = b_c.defined() ? b_c.data_ptr<float>() : nullptr;
+    DGMC_DISPATCH_FLOAT(out.scalar_type(), TOut, [&] {
+      TORCH_CHECK((C * (int64_t)sizeof(TOut)) % 16 == 0,
+                  "spmm_split: output rows of 16-byte multiples");
+      TOut* op = reinterpret_cast<TOut*>(out.data_ptr());
+      auto go = [&](auto gtag) {
+        constexpr int G = decltype(gtag)::value;
+        constexpr int PPB = 256 / G;
+        const int blocks = (n_short + PPB - 1) / PPB + n_long;
+        if (blocks == 0) return;
+        hipLaunchKernelGGL((spmm_split_kernel<TIn, TOut, V, G>), dim3(blocks),
+                           dim3(256), 0, stream(), rowptr.data_ptr<int>(),
+                           col.data_ptr<int>(), val.data_ptr<float>(),
+                           short_rows.data_ptr<int>(), n_short,
+                           long_rows.data_ptr<int>(), xp, sp, ssp, bp, op,
+                           (int)C, relu ? 1 : 0);
+        DGMC_CHECK_LAUNCH();
+      };
+      if (C / V <= 4) go(std::integral_constant<int, 4>());
+      else if (C / V <= 8) go(std::integral_constant<int, 8>());
+      else go(std::integral_constant<int, 16>());
     });
   });
 }

@@ -195,4 +195,5 @@ def relational_plan(edge_index, num_nodes):
     # Knowledge graphs have hub entities (hundreds of neighbours per flow):
     # walk rows in pieces so one hub does not serialise the SpMM.
     plan.balanced = True
+    plan.static = True
     return _CACHE.put((edge_index, ), params, plan)

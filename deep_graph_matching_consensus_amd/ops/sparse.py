@@ -79,13 +79,33 @@ class SparseOperator(object):
         self._row = row
         self._t = None
         self.balanced = balanced
+        # static: the structure outlives one step (e.g. a KG relational
+        # plan), so a once-per-operator host split of its rows pays.
+        self.static = False
         self._pieces = None
+        self._split = None
 
     def pieces(self):
         """``(pptr, prow, pbeg, pend)`` of :func:`piece_plan` (cached)."""
         if self._pieces is None:
             self._pieces = piece_plan(self.rowptr, self.nnz)
         return self._pieces
+
+    def split_rows(self):
+        """``(short_rows, long_rows)`` int32: rows of at most / more than
+        :data:`PIECE` entries (``spmm.hip::spmm_split_kernel``), or None
+        while a graph is being captured before the split exists (it needs
+        one host synchronisation).  Cached."""
+        if self._split is None:
+            if self.rowptr.is_cuda and \
+                    torch.cuda.is_current_stream_capturing():
+                return None
+            counts = self.rowptr[1:] - self.rowptr[:-1]
+            long_ = counts > PIECE
+            self._split = (
+                torch.nonzero(~long_).view(-1).to(torch.int32).contiguous(),
+                torch.nonzero(long_).view(-1).to(torch.int32).contiguous())
+        return self._split
 
     @property
     def nnz(self):
@@ -126,6 +146,7 @@ class SparseOperator(object):
                                               self.num_rows)
             self._t._t = self
             self._t.balanced = self.balanced
+            self._t.static = self.static
         return self._t
 
     def slot_csr(self, num_slots):
@@ -154,10 +175,27 @@ class SparseOperator(object):
             self.num_rows, self.num_cols, self.nnz)
 
 
+def _split_ok(x):
+    """Rows of at most 16 16-byte vectors (spmm_split_kernel's lanes)."""
+    width = 4 if x.dtype == torch.float32 else 8
+    return (x.dim() == 2 and x.size(1) % width == 0 and
+            x.size(1) // width <= 16 and x.is_contiguous() and
+            x.data_ptr() % 16 == 0 and x.dtype in (torch.float32,
+                                                   torch.bfloat16))
+
+
 def spmm_out(op, x, out, self_x=None, self_scale=None, bias=None,
              relu=False):
-    """HIP SpMM into ``out`` (piece-balanced for ``op.balanced``)."""
-    if op.balanced:
+    """HIP SpMM into ``out`` (piece-balanced for ``op.balanced``; for a
+    static balanced operator with narrow rows, the one-launch short / long
+    row split)."""
+    split = op.split_rows() if (op.balanced and op.static and
+                                _split_ok(x)) else None
+    if split is not None:
+        _backend.ops().spmm_split_out(op.rowptr, op.col, op.val, split[0],
+                                      split[1], x, self_x, self_scale, bias,
+                                      relu, out)
+    elif op.balanced:
         _backend.ops().spmm_pieces_out(
             op.rowptr, op.col, op.val, None, *op.pieces(), x, self_x,
             self_scale, bias, relu, out)

@@ -102,6 +102,53 @@ def test_spmm_pieces_skewed_rows(C, dtype):
     assert torch.allclose(gb, gb2, atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize('C,dtype', [(32, torch.float32),
+                                     (64, torch.float32),
+                                     (8, torch.float32),
+                                     (128, torch.bfloat16)])
+def test_spmm_split_static_operator(C, dtype):
+    """Static skewed operators (KG relational plans): the one-launch short /
+    long row split == the piece-balanced path == fp32 oracle, forward (self
+    term, bias, ReLU) and backward (transposed operator), bitwise
+    reproducible."""
+    R, X = 300, 257
+    op = _skewed_op(R, X, DEV, hub=700)
+    op.static = True
+    assert op.split_rows()[1].numel() > 0        # long rows exist
+    x = torch.randn(X, C, device=DEV).to(dtype).requires_grad_()
+    bias = torch.randn(C, device=DEV, requires_grad=True)
+    out = spmm(op, x, bias=bias, relu=True)
+    assert torch.equal(out, spmm(op, x, bias=bias, relu=True))
+    op.static = False
+    op.t().static = False
+    pieces = spmm(op, x, bias=bias, relu=True)
+    op.static = True
+    op.t().static = True
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(out.float(), pieces.float(), atol=tol * 10,
+                          rtol=tol)
+    with reference_mode():
+        x2 = x.detach().clone().requires_grad_()
+        b2 = bias.detach().clone().requires_grad_()
+        out2 = spmm(op, x2, bias=b2, relu=True)
+    assert torch.allclose(out.float(), out2.float(), atol=tol * 10, rtol=tol)
+    g = torch.randn_like(out)
+    gx, gb = torch.autograd.grad(out, (x, bias), g)
+    gx2, gb2 = torch.autograd.grad(out2, (x2, b2), g)
+    assert torch.allclose(gx.float(), gx2.float(), atol=tol * 10, rtol=tol)
+    assert torch.allclose(gb, gb2, atol=1e-3, rtol=1e-4)
+    # Self term (GIN-like (1 + eps) x) through spmm_split_out directly.
+    sx = torch.randn(R, C, device=DEV).to(dtype)
+    scale = torch.tensor([1.5], device=DEV)
+    o3 = torch.empty(R, C, device=DEV, dtype=dtype)
+    sr, lr = op.split_rows()
+    _backend.ops().spmm_split_out(op.rowptr, op.col, op.val, sr, lr,
+                                  x.detach().contiguous(), sx, scale, None,
+                                  False, o3)
+    ref3 = op.to_dense() @ x.detach().float() + 1.5 * sx.float()
+    assert torch.allclose(o3.float(), ref3, atol=tol * 10, rtol=tol)
+
+
 def test_piece_plan_hip_matches_torch():
     from deep_graph_matching_consensus_amd.ops.sparse import piece_plan
     op = _skewed_op(300, 257, DEV)
