@@ -114,8 +114,10 @@ __global__ __launch_bounds__(256) void csc_finish_kernel(
 // S_idx [B, N_s, k] int64 (targets local to each pair's N_t block) ->
 // (col int32 [nnz] global targets, rowptr int32 [B N_s + 1], colptr int32
 // [B N_t + 1], perm int32 [nnz] CSC -> CSR entry map (stable: row order
-// inside a column), row_of int32 [nnz]).  Five launches (prep, the radix
-// sort's passes, finish) instead of an argsort + histogram + scan chain.
+// inside a column), row_of int32 [nnz]).  Prep + rocprim's stable radix
+// sort (default configuration: it merge-sorts up to 1 M keys; forcing
+// onesweep faulted inside the captured step) + finish, instead of an argsort
+// + histogram + scan chain.
 std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
   TORCH_CHECK(S_idx.is_cuda() && S_idx.scalar_type() == at::kLong &&
                   S_idx.is_contiguous() && S_idx.dim() == 3,
