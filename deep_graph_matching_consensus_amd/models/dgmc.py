@@ -87,6 +87,8 @@ class _FoldProduct(torch.autograd.Function):
             w, wn, wnt = _backend.ops().fold_weights(w1.contiguous(),
                                                      wf.contiguous())
             ctx.mark_non_differentiable(wn, wnt)
+            # (no zero-filled gradients for the two bf16 images)
+            ctx.set_materialize_grads(False)
             return w, wn, wnt
         with torch.autocast(w1.device.type, enabled=False):
             return w1.float() @ wf.float(), None, None
