@@ -1,5 +1,8 @@
 set -euo pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-bash tools/prof_quick.sh prof_fp32 > gpurun_out/prof_fp32_head.txt 2>&1
-head -2 gpurun_out/prof_fp32_head.txt
-grep -E "sg_scan|BFloat16|FillFunctor" gpurun_out/prof_fp32/step.txt | cut -c1-120
+OUT=gpurun_out/ex
+mkdir -p $OUT
+timeout -k 10 600 python -u examples/pascal.py --epochs 15 > $OUT/pascal.log 2>&1
+tail -8 $OUT/pascal.log
+timeout -k 10 600 python -u examples/willow.py --runs 3 > $OUT/willow.log 2>&1
+tail -6 $OUT/willow.log
