@@ -29,13 +29,61 @@ host syncs) used as the BASELINE.md denominator.
 """
 import argparse
 import json
+import os
 import os.path as osp
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
 ROOT = osp.dirname(osp.abspath(__file__))
+
+
+def _gpus_arg(argv):
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument('--gpus', type=int, default=1)
+    return p.parse_known_args(argv)[0].gpus
+
+
+def launch_ranks(argv=None):
+    """One process per GPU.  Runs BEFORE torch (or anything else) touches
+    the GPU: a plain ``python bench.py --gpus N`` starts N ranks through
+    ``torch.distributed.run`` as a CHILD process (never an exec) and returns
+    its exit code; under a launcher it checks ``WORLD_SIZE == N``.  Returns
+    None when this process should run the benchmark itself."""
+    argv = sys.argv[1:] if argv is None else list(argv)
+    n = _gpus_arg(argv)
+    if n < 1:
+        sys.stderr.write('bench.py: --gpus must be >= 1\n')
+        return 2
+    if 'WORLD_SIZE' in os.environ:
+        world = int(os.environ['WORLD_SIZE'])
+        if world != n:
+            sys.stderr.write('bench.py: --gpus {} but the launcher started '
+                             'WORLD_SIZE={} ranks\n'.format(n, world))
+            return 2
+        return None
+    if n == 1:
+        return None
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '4')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(n), '--master-addr', '127.0.0.1',
+           '--master-port', str(port), osp.abspath(__file__)] + argv
+    return subprocess.call(cmd, env=env)
+
+
+if __name__ == '__main__':
+    _rc = launch_ranks()
+    if _rc is not None:
+        sys.exit(_rc)
+
+import torch  # noqa: E402
+
 sys.path.insert(0, ROOT)
 
 from deep_graph_matching_consensus_amd import parallel  # noqa: E402
@@ -187,10 +235,26 @@ def bench_kg(args, cfg, device):
 
 def main(argv=None):
     args = parse_args(argv)
+    ngpu = torch.cuda.device_count()    # does not initialise HIP
+    if ngpu and args.gpus > ngpu:
+        sys.stderr.write('bench.py: --gpus {} but only {} GPU(s) visible\n'
+                         .format(args.gpus, ngpu))
+        return 2
     device = parallel.init_distributed()
     rank, world = parallel.rank(), parallel.world_size()
+    if world != args.gpus:
+        sys.stderr.write('bench.py: running {} rank(s) for --gpus {}\n'
+                         .format(world, args.gpus))
+        parallel.shutdown()
+        return 2
     cfg = CONFIGS[args.config]
     if cfg.get('kind') == 'kg':
+        if world > 1:
+            # One full-graph pair per step (B=1, dbp15k.py:37-47): there is
+            # no batch to shard, so this config is single-GPU (BASELINE).
+            sys.stderr.write('bench.py: --config dbp15k runs on one GPU\n')
+            parallel.shutdown()
+            return 2
         out = bench_kg(args, cfg, device)
         if rank == 0:
             line = json.dumps(out)

@@ -1,11 +1,13 @@
 """Data parallelism over RCCL (GPU) / gloo (CPU)."""
 from .dist import (init_distributed, is_distributed, rank, world_size,
-                   barrier, all_reduce_max, all_reduce_sum, shutdown,
+                   barrier, all_reduce_max, all_reduce_sum, all_gather_state,
+                   shutdown,
                    env_rank, env_world_size, env_local_rank)
 from .ddp import GradBucketAllReducer
 
 __all__ = [
     'init_distributed', 'is_distributed', 'rank', 'world_size', 'barrier',
-    'all_reduce_max', 'all_reduce_sum', 'shutdown', 'env_rank',
+    'all_reduce_max', 'all_reduce_sum', 'all_gather_state', 'shutdown',
+    'env_rank',
     'env_world_size', 'env_local_rank', 'GradBucketAllReducer',
 ]

@@ -21,9 +21,11 @@ parameter that completes a bucket packs that bucket into its flat range (one
 multi-tensor kernel) and launches its all-reduce right away, so on RCCL the
 whole data-parallel step - backward, bucketed all-reduces overlapping the
 rest of the backward, the non-finite check and Adam - is ONE captured
-hipGraph.  Gloo (CPU tensors or the multi-rank rehearsal on one GPU) cannot
-be captured: there the step packs all gradients and the trainer runs one
-flat all-reduce after the replay.
+hipGraph (exercised on hardware by ``tests/test_rccl_step.py`` with a
+one-rank RCCL group).  Uncaptured static steps use the same in-step
+buckets on any backend.  A gloo graph step (the multi-rank rehearsal on one
+GPU) cannot capture its collectives: there the step packs all gradients and
+the trainer runs one flat all-reduce after the replay.
 
 With a single process every call is a no-op, so the same training loop runs
 on 1..8 GPUs.

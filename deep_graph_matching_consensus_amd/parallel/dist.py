@@ -96,6 +96,31 @@ def all_reduce_sum(tensor):
     return tensor
 
 
+def all_gather_state(state, device):
+    """Every rank's ``state`` (tensors + Python primitives), gathered on
+    every rank.  Serialised with ``torch.save`` and decoded with
+    ``torch.load(weights_only=True)``, so nothing is unpickled; moved as a
+    padded uint8 tensor (device tensor for RCCL)."""
+    import io
+    if not is_distributed():
+        return [state]
+    buf = io.BytesIO()
+    torch.save(state, buf)
+    raw = torch.frombuffer(bytearray(buf.getvalue()), dtype=torch.uint8)
+    dev = device if dist.get_backend() == 'nccl' else torch.device('cpu')
+    n = torch.tensor([raw.numel()], dtype=torch.long, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(dist.get_world_size())]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    pad = torch.zeros(max(sizes), dtype=torch.uint8, device=dev)
+    pad[:raw.numel()] = raw.to(dev)
+    outs = [torch.empty_like(pad) for _ in sizes]
+    dist.all_gather(outs, pad)
+    return [torch.load(io.BytesIO(o[:s].cpu().numpy().tobytes()),
+                       map_location='cpu', weights_only=True)
+            for o, s in zip(outs, sizes)]
+
+
 def shutdown():
     if is_distributed():
         dist.destroy_process_group()

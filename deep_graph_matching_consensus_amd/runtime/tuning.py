@@ -17,6 +17,7 @@ validates the file against the PyTorch / HIP / hipBLASLt / rocBLAS versions
 and the GPU architecture, so a file from another stack is ignored.
 ``DGMC_AMD_TUNED_GEMMS=0`` disables it.
 """
+import contextlib
 import os
 import os.path as osp
 
@@ -28,8 +29,11 @@ _STATE = {}
 
 
 def use_tuned_gemms(path=None):
-    """Dispatch GEMMs through the tuned solutions in ``path`` (default: the
-    shipped file).  Returns True if the file was loaded."""
+    """Load the tuned solutions in ``path`` (default: the shipped file) into
+    TunableOp's result table.  TunableOp itself is only switched on inside
+    :func:`tuned_gemms` scopes (the trainers' steps), so the process-wide
+    setting outside them is left as the caller had it.  Returns True if the
+    file was loaded."""
     if os.environ.get('DGMC_AMD_TUNED_GEMMS', '1') != '1':
         return False
     if not torch.cuda.is_available():
@@ -40,15 +44,35 @@ def use_tuned_gemms(path=None):
     if _STATE.get('path') == path:
         return _STATE['ok']
     tunable = torch.cuda.tunable
+    prev = (tunable.is_enabled(), tunable.tuning_is_enabled(),
+            tunable.get_filename())
     tunable.enable(True)
     tunable.tuning_enable(False)
-    # Never write results back (the process only reads).
-    tunable.set_filename(os.devnull)
     ok = bool(tunable.read_file(path))
-    if not ok:
-        tunable.enable(False)
+    tunable.enable(prev[0])
+    tunable.tuning_enable(prev[1])
+    tunable.set_filename(prev[2])
     _STATE.update(path=path, ok=ok)
     return ok
+
+
+@contextlib.contextmanager
+def tuned_gemms(active=True):
+    """Dispatch the GEMMs issued inside the scope through the loaded tuned
+    solutions (read-only: tuning stays off, nothing is written), restoring
+    the previous TunableOp settings on exit."""
+    if not (active and _STATE.get('ok')):
+        yield
+        return
+    tunable = torch.cuda.tunable
+    prev = (tunable.is_enabled(), tunable.tuning_is_enabled())
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    try:
+        yield
+    finally:
+        tunable.enable(prev[0])
+        tunable.tuning_enable(prev[1])
 
 
 def start_tuning(out_path, max_duration_ms=15):

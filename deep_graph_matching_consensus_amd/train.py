@@ -31,7 +31,7 @@ from .datasets.device_loader import DevicePairLoader
 from .datasets.static_batch import StaticPairBatcher, bucket_capacities
 from .runtime.graphs import GraphedStep
 from .runtime.profiling import trace_range
-from .runtime.tuning import use_tuned_gemms
+from .runtime.tuning import tuned_gemms, use_tuned_gemms
 
 # Data-parallel gradient all-reduce inside the (captured) step, overlapped
 # with the backward (DGMC_AMD_IN_STEP_ALLREDUCE=0: one flat all-reduce after
@@ -48,7 +48,8 @@ class PairTrainer(object):
         batch_size (int): pairs per step and rank.
         lr (float): Adam learning rate.
         mode (str): ``'eager'``, ``'static'`` or ``'graph'``.
-        bf16 (bool): bf16 autocast for the encoder GEMMs.
+        bf16 (bool): bf16 autocast for the encoder GEMMs (opt-in; the
+            default is fp32, the reference's training precision).
         seed (int): data-order seed (offset by rank).
         overlap (bool): overlap gradient all-reduce with backward (eager).
         bucket_bytes (int): data-parallel all-reduce bucket size.
@@ -59,7 +60,7 @@ class PairTrainer(object):
     """
 
     def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
-                 bf16=True, seed=0, overlap=True, sources=None,
+                 bf16=False, seed=0, overlap=True, sources=None,
                  guard_nonfinite=True, buckets=True, bucket_bytes=8 << 20):
         self.model = model
         self.store = store
@@ -71,14 +72,16 @@ class PairTrainer(object):
         self.bf16 = bf16 and self.device.type == 'cuda'
         if sources is None:
             sources = np.arange(store.num_graphs)[self.rank::self.world]
-        # Data parallel, static / graph modes: bucketed all-reduces from the
-        # backward hooks INSIDE the step (captured with it on RCCL), unless
-        # the backend cannot be captured (gloo: one all-reduce after the
-        # replay) - see parallel/ddp.py.
-        in_step = (mode == 'static' or mode == 'graph' and
-                   parallel.is_distributed() and
-                   torch.distributed.get_backend() == 'nccl') and \
-            IN_STEP_ALLREDUCE
+        # Data parallel: bucketed all-reduces launched from the backward
+        # hooks INSIDE the step body.
+        # * static mode: always (any backend - nothing is captured);
+        # * graph mode: only on RCCL, whose collectives are captured into the
+        #   step's hipGraph; gloo cannot be captured, so a gloo graph step
+        #   packs every gradient and one flat all-reduce runs after the
+        #   replay (parallel/ddp.py).
+        graph_rccl = (mode == 'graph' and parallel.is_distributed() and
+                      torch.distributed.get_backend() == 'nccl')
+        in_step = IN_STEP_ALLREDUCE and (mode == 'static' or graph_rccl)
         self.reducer = parallel.GradBucketAllReducer(
             model, bucket_bytes=bucket_bytes,
             overlap=overlap and mode == 'eager', in_step=in_step)
@@ -304,8 +307,6 @@ class PairTrainer(object):
         warm-up iterations before each capture run real steps; their effect
         on the model, optimizer, RNG and sampler is undone afterwards."""
         snap = self._snapshot()
-        if hasattr(gc, 'unfreeze'):
-            gc.unfreeze()
         for i, b in enumerate(self.batchers):
             for _ in range(10000):
                 s, t = self.batcher.next_ids()
@@ -317,14 +318,21 @@ class PairTrainer(object):
         self._captured = True
         self._restore(snap)
         # The capture phase leaves large autograd graphs behind: collect them
-        # now and move the survivors out of the collector's generations, so
-        # no full collection pauses the host during the replayed steps.
+        # now, not in the middle of a replayed step (steps pause the cyclic
+        # collector themselves, see step()).
         gc.collect()
-        if hasattr(gc, 'freeze'):
-            gc.freeze()
 
     def step(self):
-        """One training step (data, forward, backward, all-reduce, Adam)."""
+        """One training step (data, forward, backward, all-reduce, Adam).
+
+        Process-wide settings are only changed for the duration of the
+        step: the tuned GEMM solutions are active inside it, and the cyclic
+        garbage collector is paused (no collection lands between a step's
+        launches); both are restored on return."""
+        with tuned_gemms(self.device.type == 'cuda'), _gc_paused():
+            self._step()
+
+    def _step(self):
         self.model.train()
         if self.mode == 'eager':
             with trace_range('train.load'):
@@ -378,6 +386,10 @@ class PairTrainer(object):
         ``num_pairs`` random valid pairs of ``store`` (the reference's test
         loop, ``/root/reference/examples/pascal.py:80-99``).  Counts stay on
         the device; one host synchronisation per evaluation."""
+        with tuned_gemms(self.device.type == 'cuda'):
+            return self._evaluate(store, num_pairs, batch_size, seed, k)
+
+    def _evaluate(self, store, num_pairs, batch_size, seed, k):
         model = self.model
         was_training = model.training
         model.eval()
@@ -409,34 +421,48 @@ class PairTrainer(object):
                 for i, kk in enumerate(k)}
 
     # ------------------------------------------------------------------
-    def state_dict(self):
-        """Checkpoint content; every leaf is a tensor or a Python primitive
-        so it loads with ``torch.load(..., weights_only=True)``."""
+    def _rank_state(self):
+        """This rank's private resume state: its sampler (shard order and
+        generator), its share of the running stats and its RNG streams."""
         np_state = np.random.get_state()
         sampler = self.loader if self.mode == 'eager' else self.batcher
-        state = {
+        rng = {
+            'torch': torch.get_rng_state(),
+            'python': random.getstate(),
+            'numpy': (np_state[0], torch.from_numpy(np_state[1].copy()),
+                      int(np_state[2]), int(np_state[3]),
+                      float(np_state[4])),
+        }
+        if self.device.type == 'cuda':
+            rng['cuda'] = torch.cuda.get_rng_state(self.device)
+        return {'sampler': sampler.state_dict(),
+                'stats': self.stats.detach().cpu(), 'rng': rng}
+
+    def state_dict(self, ranks=None):
+        """Checkpoint content; every leaf is a tensor or a Python primitive
+        so it loads with ``torch.load(..., weights_only=True)``.
+
+        ``ranks``: the per-rank states of every rank (gathered by
+        :meth:`save`); defaults to this rank's alone."""
+        if ranks is None:
+            ranks = [self._rank_state()]
+        return {
             'model': self.model.state_dict(),
             'optimizer': self.optimizer.state_dict(),
             'step': self.step_count,
-            'sampler': sampler.state_dict(),
-            'stats': self.stats.detach().cpu(),
-            'rng': {
-                'torch': torch.get_rng_state(),
-                'python': random.getstate(),
-                'numpy': (np_state[0], torch.from_numpy(np_state[1].copy()),
-                          int(np_state[2]), int(np_state[3]),
-                          float(np_state[4])),
-            },
+            'world_size': len(ranks),
+            'ranks': ranks,
         }
-        if torch.cuda.is_available():
-            state['rng']['cuda'] = torch.cuda.get_rng_state_all()
-        return state
 
     def save(self, path):
-        """Rank-0 checkpoint (model in the reference key schema)."""
+        """Checkpoint written by rank 0: the model (reference key schema)
+        and optimizer, which are identical on every rank, plus EVERY rank's
+        sampler / stats / RNG state (gathered), so a data-parallel resume
+        gives each rank back its own shard position."""
+        ranks = parallel.all_gather_state(self._rank_state(), self.device)
         if self.rank == 0:
             tmp = path + '.tmp'
-            torch.save(self.state_dict(), tmp)
+            torch.save(self.state_dict(ranks), tmp)
             os.replace(tmp, path)
         parallel.barrier()
 
@@ -472,17 +498,23 @@ class PairTrainer(object):
         self.model.load_state_dict(state['model'])
         self._load_optimizer(state['optimizer'])
         self.step_count = int(state.get('step', 0))
-        if 'sampler' in state:
-            if self.mode == 'eager':
-                self.loader.load_state_dict(state['sampler'])
-                self._batches = self.loader.forever()
-            else:
-                self.batcher.load_state_dict(state['sampler'])
-        if 'stats' in state:
-            self.stats.copy_(state['stats'].to(self.stats))
         # (Parameters and optimizer tensors were updated in place, so
         # captured graphs stay valid and are replayed as they are.)
-        rng = state.get('rng', {})
+        ranks = state.get('ranks', [])
+        if len(ranks) != self.world:
+            # Different world size: the shards changed, so the saved sampler
+            # positions mean nothing here - keep this rank's freshly seeded
+            # sampler and start the running stats from zero.
+            self.stats.zero_()
+            return state
+        mine = ranks[self.rank]
+        if self.mode == 'eager':
+            self.loader.load_state_dict(mine['sampler'])
+            self._batches = self.loader.forever()
+        else:
+            self.batcher.load_state_dict(mine['sampler'])
+        self.stats.copy_(mine['stats'].to(self.stats))
+        rng = mine.get('rng', {})
         if 'torch' in rng:
             torch.set_rng_state(rng['torch'].cpu())
         if 'python' in rng:
@@ -491,9 +523,23 @@ class PairTrainer(object):
             name, keys, pos, has_gauss, cached = rng['numpy']
             np.random.set_state((name, keys.cpu().numpy().astype(np.uint32),
                                  pos, has_gauss, cached))
-        if 'cuda' in rng and torch.cuda.is_available():
-            torch.cuda.set_rng_state_all([t.cpu() for t in rng['cuda']])
+        if 'cuda' in rng and self.device.type == 'cuda':
+            torch.cuda.set_rng_state(rng['cuda'].cpu(), self.device)
         return state
+
+
+class _gc_paused(object):
+    """Pause the cyclic garbage collector inside the block (restoring the
+    caller's setting)."""
+
+    def __enter__(self):
+        self._was = gc.isenabled()
+        gc.disable()
+
+    def __exit__(self, *exc):
+        if self._was:
+            gc.enable()
+        return False
 
 
 class MetricsLogger(object):
@@ -554,6 +600,10 @@ class KGTrainer(object):
         self.last_loss.copy_(loss.detach())
 
     def step(self):
+        with tuned_gemms(self.device.type == 'cuda'), _gc_paused():
+            self._step()
+
+    def _step(self):
         self.model.train()
         if not self.graph:
             self._body()
@@ -661,6 +711,10 @@ class KGTrainer(object):
 
     @torch.no_grad()
     def evaluate(self, k=10):
+        with tuned_gemms(self.device.type == 'cuda'):
+            return self._evaluate(k)
+
+    def _evaluate(self, k):
         d, model = self.data, self.model
         model.eval()
         with self._autocast():

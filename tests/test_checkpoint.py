@@ -80,6 +80,7 @@ def test_trainer_checkpoint_resume(tmp_path):
 
 
 def _pair_trainer(store, mode, seed_model=0):
+    # (graph mode: the store lives on the GPU)
     torch.manual_seed(seed_model)
     model = DGMC(SplineCNN(16, 16, 2, 2, cat=False, dropout=0.5),
                  SplineCNN(8, 8, 2, 2, cat=True), num_steps=2)
@@ -94,14 +95,17 @@ def _run_trajectory(trainer, steps):
     return losses
 
 
-@pytest.mark.parametrize('mode', ['eager', 'static'])
+@pytest.mark.parametrize('mode', [
+    'eager', 'static', pytest.param('graph', marks=pytest.mark.gpu)])
 def test_interrupted_run_continues_bit_for_bit(tmp_path, mode):
     """Save after 2 of 5 steps, resume in a fresh process-like trainer (other
     init): losses of steps 3-5 and the final weights / Adam moments equal the
     uninterrupted run bit for bit (model, optimizer, RNG AND sampler state
-    are in the checkpoint)."""
+    are in the checkpoint).  Graph mode: the resumed trainer captures its
+    graphs (warm-ups undone by _snapshot/_restore) after the load and then
+    replays them; the trajectory still continues exactly."""
     groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=5)
-    store = GraphStore(groups, 'cpu')
+    store = GraphStore(groups, 'cuda' if mode == 'graph' else 'cpu')
     torch.manual_seed(123)
     full = _pair_trainer(store, mode)
     ref_losses = _run_trajectory(full, 5)
@@ -162,3 +166,58 @@ def test_kg_trainer_checkpoint_resume(tmp_path):
     for (k, v), w in zip(full.model.state_dict().items(),
                          b.model.state_dict().values()):
         assert torch.equal(v, w), k
+
+
+def _dp_resume_worker(rank, world, port, path, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world),
+                      OMP_NUM_THREADS='1')
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=5)
+    store = GraphStore(groups, 'cpu')
+
+    torch.manual_seed(123)
+    full = _pair_trainer(store, 'eager')
+    ref = _run_trajectory(full, 5)
+    torch.manual_seed(123)
+    first = _pair_trainer(store, 'eager')
+    _run_trajectory(first, 2)
+    first.save(path)
+    torch.manual_seed(999)
+    resumed = _pair_trainer(store, 'eager', seed_model=7)
+    state = resumed.load(path)
+    out[rank] = {'ref': ref, 'resumed': _run_trajectory(resumed, 3),
+                 'world': state['world_size'],
+                 'order': [r['sampler']['order'] for r in state['ranks']]}
+    dist.destroy_process_group()
+
+
+def test_data_parallel_resume_restores_each_rank_shard(tmp_path):
+    """Two gloo ranks: the checkpoint holds BOTH ranks' sampler states (their
+    shards differ), each rank resumes its own, and every rank's per-step
+    losses (reduced over ranks by read_stats) continue the uninterrupted
+    run exactly - no rank replays rank 0's batches, no stats inflation."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    out = ctx.Manager().dict()
+    path = str(tmp_path / 'dp.pt')
+    procs = [ctx.Process(target=_dp_resume_worker,
+                         args=(r, 2, port, path, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    for r in range(2):
+        res = out[r]
+        assert res['world'] == 2
+        assert res['resumed'] == res['ref'][2:], r
+    o0, o1 = out[0]['order']
+    assert o0 is not None and o1 is not None and not torch.equal(o0, o1)

@@ -109,7 +109,8 @@ def _bench_worker(rank, world, port, mode, out_path, batch=16):
                       LOCAL_RANK=str(rank), OMP_NUM_THREADS='1')
     torch.set_num_threads(1)
     import bench
-    bench.main(['--steps', '2', '--warmup', '1', '--batch-size', str(batch),
+    bench.main(['--gpus', str(world), '--steps', '2', '--warmup', '1',
+                '--batch-size', str(batch),
                 '--graphs-per-category', '8', '--dtype', 'fp32', '--mode',
                 mode, '--json-out', out_path])
 
