@@ -12,10 +12,17 @@ here, so :func:`make_kg_pair` generates a pair with the same sizes:
   random permutation; aligned relations are kept with probability
   ``edge_keep`` and the target receives extra random triples up to its size;
 * features are a shared latent 300-d embedding per aligned entity plus
-  per-KG noise (``feature_noise``; the default 2.0 gives raw-feature
-  nearest-neighbour Hits@1 / Hits@10 of about 0.34 / 0.60, i.e. the
-  difficulty of the word-embedding initialisation), random for unaligned
-  entities;
+  per-KG noise whose level varies per entity (``feature_noise`` times a
+  log-normal factor of spread ``noise_spread``: some names translate almost
+  verbatim, others barely), random for unaligned entities.  The defaults
+  (1.2, 0.5) give raw-feature nearest-neighbour Hits@1 / Hits@10 of 0.29 /
+  0.77 on the full-size pair (0.48 / 0.89 at ``scale=0.25``).  Calibrated
+  so the task carries an accuracy signal: the reference expression over
+  the two-phase schedule (``dbp15k.py:63-76``) at ``scale=0.25`` reaches
+  test Hits@1 0.41 after phase 1 and 0.62 after the consensus phase - the
+  refinement beats raw matching.  (Round 3's uniform noise 2.0 sat on the
+  other side of a sharp transition: the 900k-parameter psi_1 memorised the
+  4,500 training pairs and test Hits@1 ended at 0.06, below raw NN);
 * ``train_y``/``test_y`` are ``[2, n]`` alignments (source id, target id),
   split ``train_ratio`` / rest.
 
@@ -46,8 +53,8 @@ def _chung_lu_edges(num_nodes, num_edges, exponent, g):
 
 
 def make_kg_pair(category='zh_en', num_aligned=15000, feature_dim=300,
-                 feature_noise=2.0, edge_keep=0.7, train_ratio=0.3,
-                 exponent=2.5, seed=0, scale=1.0):
+                 feature_noise=1.2, edge_keep=0.7, train_ratio=0.3,
+                 exponent=2.5, seed=0, scale=1.0, noise_spread=0.5):
     """Generate a DBP15K-shaped KG pair (``scale`` shrinks it for tests)."""
     n1, n2, e1, e2 = DBP15K_SIZES[category]
     n1, n2 = int(n1 * scale), int(n2 * scale)
@@ -72,10 +79,12 @@ def make_kg_pair(category='zh_en', num_aligned=15000, feature_dim=300,
     latent = torch.randn(na, feature_dim, generator=g)
     x1 = torch.randn(n1, feature_dim, generator=g)
     x2 = torch.randn(n2, feature_dim, generator=g)
-    x1[:na] = latent + feature_noise * torch.randn(na, feature_dim,
-                                                   generator=g)
-    x2[corr] = latent + feature_noise * torch.randn(na, feature_dim,
-                                                    generator=g)
+    # Per-entity noise level (log-normal spread): some names translate
+    # almost verbatim, others barely.
+    sig = feature_noise * torch.exp(noise_spread * torch.randn(
+        na, 1, generator=g)) if noise_spread > 0 else feature_noise
+    x1[:na] = latent + sig * torch.randn(na, feature_dim, generator=g)
+    x2[corr] = latent + sig * torch.randn(na, feature_dim, generator=g)
 
     pairs = torch.stack([torch.arange(na), corr], dim=0)
     pairs = pairs[:, torch.randperm(na, generator=g)]
