@@ -53,7 +53,10 @@ at::Tensor train_candidates(const at::Tensor& topk, int64_t n_t, int64_t kr,
                             const at::Tensor& gt_row,
                             const at::Tensor& gt_col);
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
-                    bool exact);
+                    int64_t mode);
+std::vector<at::Tensor> topk_dot_refined_stats(const at::Tensor& h_s,
+                                               const at::Tensor& h_t,
+                                               int64_t k);
 
 at::Tensor sddmm(const at::Tensor& rowptr, const at::Tensor& col,
                  const at::Tensor& A, const at::Tensor& B);
@@ -299,7 +302,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None, Tensor(b!)? "
       "part=None, bool accumulate=False) -> (Tensor, Tensor, Tensor, "
       "Tensor)");
-  m.def("topk_dot(Tensor h_s, Tensor h_t, int k, bool exact=False) -> Tensor");
+  m.def("topk_dot(Tensor h_s, Tensor h_t, int k, int mode=2) -> Tensor");
+  m.def("topk_dot_refined_stats(Tensor h_s, Tensor h_t, int k) -> Tensor[]");
   m.def("train_candidates(Tensor topk, int n_t, int kr, Tensor gt_row, "
         "Tensor gt_col) -> Tensor");
   m.def("candidate_csc(Tensor S_idx, int n_t) -> Tensor[]");
@@ -480,6 +484,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_consensus", &dgmc::dense_consensus);
   m.impl("dense_consensus_bwd", &dgmc::dense_consensus_bwd);
   m.impl("topk_dot", &dgmc::topk_dot);
+  m.impl("topk_dot_refined_stats", &dgmc::topk_dot_refined_stats);
   m.impl("train_candidates", &dgmc::train_candidates);
   m.impl("candidate_csc", &dgmc::candidate_csc);
   m.impl("sddmm", &dgmc::sddmm);

@@ -212,8 +212,8 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
     const float* __restrict__ h_s, const __bf16* __restrict__ t_hi,
     const __bf16* __restrict__ t_lo,
     float* __restrict__ part_v, int* __restrict__ part_i,
-    int64_t* __restrict__ out, int Ns, int Nt, int C, int k, int span,
-    int dbg) {
+    int64_t* __restrict__ out, float* __restrict__ out_v, int Ns, int Nt,
+    int C, int k, int span, int dbg) {
   constexpr int CP = NKS * 16;              // padded channels
   constexpr int BP = CP + 8;                // LDS row pitch (bf16)
   constexpr int TILE = kX3Tile * BP;        // one hi or lo tile (bf16)
@@ -361,6 +361,7 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
         part_i[o] = li[r];
       } else {
         out[g * k + hl] = (int64_t)li[r];
+        if (out_v) out_v[g * k + hl] = lv[r];
       }
     }
   }
@@ -370,7 +371,8 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
 // among the row's S*k candidates (value desc, index asc) and scatters itself.
 __global__ __launch_bounds__(256) void topk_merge_kernel(
     const float* __restrict__ part_v, const int* __restrict__ part_i,
-    int64_t* __restrict__ out, int64_t rows, int S, int k, int Nt) {
+    int64_t* __restrict__ out, float* __restrict__ out_v, int64_t rows, int S,
+    int k, int Nt) {
   const int n = S * k;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t row = g / n;
@@ -386,7 +388,183 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
     const int oj = ix[e];
     rank += (ov > mv) || (ov == mv && oj < mj);
   }
-  if (rank < k) out[row * k + rank] = mj < Nt ? mj : 0;
+  if (rank < k) {
+    out[row * k + rank] = mj < Nt ? mj : 0;
+    if (out_v) out_v[row * k + rank] = mj < Nt ? mv : -INFINITY;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Exact fp32 top-k at split-bf16 speed: filter + exact re-score.
+//
+// The bf16x3 pass keeps K2 = min(32, N_t) approximate candidates per row
+// (scores s~_j, best first).  Its error against the exact-f32 MFMA score s_j
+// (the k-ordered fmaf chain of topk_dot_kernel) is bounded per product by
+// the dropped lo*lo term and the two split residuals (<= ~3 * 2^-18 |a b|)
+// plus the fp32 accumulation of both (<= ~2^-16 sum |a b| at C = 256), so
+// |s~_j - s_j| <= E = tau * |a| * max_j |b_j| (Cauchy-Schwarz) with
+// tau = 2^-13, a >= 3x margin over the worst case.  Every member of the exact
+// top-k then has s~_j >= T_k - 2E (T_k = the k-th approximate score): if
+// j is in the exact top-k, s_j >= (exact k-th) >= T_k - E.  So
+//   * candidates with s~_j >= T_k - 2E are re-scored with the exact chain
+//     (bit-identical to topk_dot_kernel: k = 8s + t, then 8s + 4 + t) and
+//     the k best by (exact score desc, index asc) are written;
+//   * if the K2-th approximate candidate itself clears T_k - 2E the kept
+//     list may be incomplete: that row (rare; hub-heavy near-ties) is
+//     recomputed exactly over all N_t targets by its wave.
+// One wave per row; the row of h_s is staged in LDS (zero-padded to a
+// multiple of 8 channels) and broadcast to the lanes' chains.
+// ---------------------------------------------------------------------------
+constexpr float kTopkTau = 1.0f / 8192.0f;
+
+static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
+                              int64_t k, at::Tensor* vals = nullptr);
+constexpr int kRefRows = 4;      // rows (waves) per block
+
+// Per-block partial maxima of |h_t[b, j]|^2 (any summation order: the value
+// only feeds the bound, with its own 1 + 2^-10 safety factor below).
+__global__ __launch_bounds__(256) void row_sqnorm_max_kernel(
+    const float* __restrict__ x, int Nt, int C, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  float v = 0.f;
+  if (j < Nt) {
+    const float* r = x + ((size_t)b * Nt + j) * C;
+    for (int c = 0; c < C; c += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(r + c);
+      v += q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+    }
+  }
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[(size_t)b * gridDim.x + blockIdx.x] =
+        fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// Exact chain of topk_dot_kernel for one target row (a: LDS, zero-padded).
+__device__ __forceinline__ float exact_dot(const DGMC_LDS float* a,
+                                           const float* __restrict__ b,
+                                           int C, int C8) {
+  float acc = 0.f;
+  for (int s = 0; s < C8; s += 8) {
+    float bv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = s + e < C ? b[s + e] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc = __builtin_fmaf(a[s + t], bv[t], acc);
+      acc = __builtin_fmaf(a[s + 4 + t], bv[4 + t], acc);
+    }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kRefRows * 64) void topk_refine_kernel(
+    const float* __restrict__ h_s, const float* __restrict__ h_t,
+    const int64_t* __restrict__ cand_i, const float* __restrict__ cand_v,
+    const float* __restrict__ nmax_part, int nparts, int64_t* __restrict__ out,
+    int* __restrict__ n_overflow, int Ns, int Nt, int C, int k, int K2) {
+  __shared__ __attribute__((aligned(16))) float sa[kRefRows][264];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * kRefRows + wave;
+  const int b = blockIdx.y;
+  if (g >= Ns) return;                 // wave-uniform; no block barrier below
+  const int C8 = (C + 7) & ~7;
+  const float* arow = h_s + ((size_t)b * Ns + g) * C;
+  DGMC_LDS float* a = (DGMC_LDS float*)sa[wave];
+  float sq = 0.f;
+  for (int c = lane; c < C8; c += 64) {
+    const float v = c < C ? arow[c] : 0.f;
+    a[c] = v;
+    sq += v * v;
+  }
+  sq = wave_sum(sq);
+  float bm = 0.f;
+  for (int p = lane; p < nparts; p += 64)
+    bm = fmaxf(bm, nmax_part[(size_t)b * nparts + p]);
+  bm = wave_max(bm);
+  // |a| |b|max with a relative safety factor for the (any-order) norms.
+  const float E = kTopkTau * sqrtf(sq * bm) * (1.0f + 1.0f / 1024.0f);
+  const size_t o = ((size_t)b * Ns + g);
+  const int ci = lane < K2 ? (int)cand_i[o * K2 + lane] : 0;
+  const float cv = lane < K2 ? cand_v[o * K2 + lane] : -INFINITY;
+  const float Tk = __shfl(cv, k - 1);
+  const float lim = Tk - 2.0f * E;
+  const bool overflow = K2 < Nt && __shfl(cv, K2 - 1) >= lim;
+  __builtin_amdgcn_wave_barrier();
+  const float* tb = h_t + (size_t)b * Nt * C;
+  int64_t* orow = out + o * k;
+  if (!overflow) {
+    const bool keep = lane < K2 && cv >= lim;
+    const float ev = keep ? exact_dot(a, tb + (size_t)ci * C, C, C8)
+                          : -INFINITY;
+    // rank by (exact desc, index asc) among the kept candidates
+    int rank = 0;
+    for (int l = 0; l < K2; ++l) {
+      const float ov = __shfl(ev, l);
+      const int oj = __shfl(ci, l);
+      const bool ok = __shfl((int)keep, l) != 0;
+      rank += ok && (ov > ev || (ov == ev && oj < ci));
+    }
+    if (keep && rank < k) orow[rank] = ci;
+    return;
+  }
+  // Incomplete list: exact scan of every target (wave-parallel over j),
+  // insertion into a wave list like topk_dot_kernel (lanes 0..k-1).
+  if (lane == 0) atomicAdd(n_overflow, 1);
+  float lv = -INFINITY;
+  int li = 0;
+  for (int j0 = 0; j0 < Nt; j0 += 64) {
+    const int j = j0 + lane;
+    const float v =
+        j < Nt ? exact_dot(a, tb + (size_t)j * C, C, C8) : -INFINITY;
+    float thr = __shfl(lv, k - 1);
+    unsigned long long mask = __ballot(j < Nt && v > thr);
+    while (mask) {
+      const int src = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const float nv = __shfl(v, src);
+      if (!(nv > thr)) continue;
+      const int pos = __popcll(__ballot(lane < k && lv >= nv));
+      const float pv = __shfl_up(lv, 1);
+      const int pi = __shfl_up(li, 1);
+      if (lane > pos && lane < k) { lv = pv; li = pi; }
+      if (lane == pos) { lv = nv; li = j0 + src; }
+      thr = __shfl(lv, k - 1);
+    }
+  }
+  if (lane < k) orow[lane] = li;
+}
+
+static at::Tensor topk_dot_refined(const at::Tensor& h_s,
+                                   const at::Tensor& h_t, int64_t k,
+                                   at::Tensor* n_overflow) {
+  const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
+  const int Nt = h_t.size(1);
+  const int K2 = std::min(32, Nt);
+  at::Tensor cv;
+  at::Tensor ci = topk_dot_x3(h_s, h_t, K2, &cv);
+  at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
+  at::Tensor cnt = at::zeros({1}, h_s.options().dtype(at::kInt));
+  if (n_overflow) *n_overflow = cnt;
+  if (B == 0 || Ns == 0) return out;
+  const int nparts = (Nt + 255) / 256;
+  at::Tensor part = at::empty({B, nparts}, h_s.options());
+  hipLaunchKernelGGL(row_sqnorm_max_kernel, dim3(nparts, B), dim3(256), 0,
+                     stream(), h_t.data_ptr<float>(), Nt, C,
+                     part.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(topk_refine_kernel,
+                     dim3((Ns + kRefRows - 1) / kRefRows, B),
+                     dim3(kRefRows * 64), 0, stream(), h_s.data_ptr<float>(),
+                     h_t.data_ptr<float>(), ci.data_ptr<int64_t>(),
+                     cv.data_ptr<float>(), part.data_ptr<float>(), nparts,
+                     out.data_ptr<int64_t>(), cnt.data_ptr<int>(), Ns, Nt, C,
+                     (int)k, K2);
+  DGMC_CHECK_LAUNCH();
+  return out;
 }
 
 // (The kernels' dbg argument - 1 skip selection, 2 skip MFMA - is a
@@ -412,10 +590,12 @@ static int x3_splits(int64_t row_blocks, int Nt) {
 }
 
 static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
-                              int64_t k) {
+                              int64_t k, at::Tensor* vals) {
   const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
   const int Nt = h_t.size(1);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
+  if (vals) *vals = at::empty({B, Ns, k}, h_s.options());
+  float* out_v = vals ? vals->data_ptr<float>() : nullptr;
   if (B == 0 || Ns == 0) return out;
   const int NKS = (C + 63) / 64 * 4;
   const int CP = NKS * 16;
@@ -454,8 +634,8 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
                        h_s.data_ptr<float>(), t_hi, t_lo,
                        S > 1 ? pv.data_ptr<float>() : nullptr,
                        S > 1 ? pi.data_ptr<int>() : nullptr,
-                       out.data_ptr<int64_t>(), Ns, Nt, C, (int)k, span,
-                       topk_debug());
+                       out.data_ptr<int64_t>(), out_v, Ns, Nt, C, (int)k,
+                       span, topk_debug());
   };
   switch (NKS) {
     case 4: launch(topk_x3_kernel<4>); break;
@@ -469,15 +649,18 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
     const int64_t n = rows * S * k;
     hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)((n + 255) / 256)),
                        dim3(256), 0, stream(), pv.data_ptr<float>(),
-                       pi.data_ptr<int>(), out.data_ptr<int64_t>(), rows, S,
-                       (int)k, Nt);
+                       pi.data_ptr<int>(), out.data_ptr<int64_t>(), out_v,
+                       rows, S, (int)k, Nt);
     DGMC_CHECK_LAUNCH();
   }
   return out;
 }
 
+// mode 0: split-bf16 scores (~2^-16 relative); 1: brute-force exact-f32 MFMA;
+// 2 (default): exact - the split-bf16 filter + exact re-score above, with
+// the brute-force kernel where the filter does not apply (k > 32).
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
-                    bool exact) {
+                    int64_t mode) {
   TORCH_CHECK(h_s.is_cuda() && h_t.is_cuda() && h_s.dim() == 3 &&
                   h_t.dim() == 3 && h_s.scalar_type() == at::kFloat &&
                   h_t.scalar_type() == at::kFloat && h_s.is_contiguous() &&
@@ -489,7 +672,8 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
   TORCH_CHECK(h_t.size(0) == B && h_t.size(2) == C, "topk_dot: shape");
   TORCH_CHECK(k >= 1 && k <= 64 && k <= Nt, "topk_dot: need 1 <= k <= min(64, N_t)");
   TORCH_CHECK(C % 4 == 0 && C <= 256, "topk_dot: C % 4 == 0 and C <= 256");
-  if (!exact && k <= 32) return topk_dot_x3(h_s, h_t, k);
+  if (mode == 0 && k <= 32) return topk_dot_x3(h_s, h_t, k);
+  if (mode == 2 && k <= 16) return topk_dot_refined(h_s, h_t, k, nullptr);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
   if (B == 0 || Ns == 0) return out;
   const int CT = (C + 63) / 64;
@@ -513,6 +697,25 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
   }
   DGMC_CHECK_LAUNCH();
   return out;
+}
+
+// Test hook: the refined result plus the number of rows that took the
+// exhaustive exact path.
+std::vector<at::Tensor> topk_dot_refined_stats(const at::Tensor& h_s,
+                                               const at::Tensor& h_t,
+                                               int64_t k) {
+  TORCH_CHECK(h_s.is_cuda() && h_s.dim() == 3 && h_s.is_contiguous() &&
+                  h_t.is_contiguous() && h_s.scalar_type() == at::kFloat &&
+                  h_t.scalar_type() == at::kFloat && h_t.size(0) == h_s.size(0)
+                  && h_t.size(2) == h_s.size(2),
+              "topk_dot_refined_stats: contiguous fp32 [B, N, C]");
+  TORCH_CHECK(k >= 1 && k <= 16 && k <= h_t.size(1) && h_s.size(2) % 4 == 0 &&
+                  h_s.size(2) <= 256,
+              "topk_dot_refined_stats: 1 <= k <= 16, C % 4 == 0, C <= 256");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(h_s.device());
+  at::Tensor cnt;
+  at::Tensor idx = topk_dot_refined(h_s, h_t, k, &cnt);
+  return {idx, cnt};
 }
 
 }  // namespace dgmc

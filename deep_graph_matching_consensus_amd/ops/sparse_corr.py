@@ -5,9 +5,14 @@
   (``dgmc.py:85-94``; KeOps ``argKmin`` in the reference).  On the GPU a fused
   HIP kernel streams ``h_t`` tiles through LDS, computes the dot tiles on
   MFMA and keeps a per-row register top-k, so the ``N_s x N_t`` score matrix
-  is never materialised.  Default scores use the split-bf16 ("bf16x3",
-  ~2^-16 relative) kernel; ``DGMC_AMD_TOPK_EXACT=1`` (or ``exact=True``)
-  selects the exact-f32 MFMA kernel.
+  is never materialised.  The default is EXACT fp32 selection (the
+  reference's fp32 KeOps ``argKmin``) at split-bf16 speed: a split-bf16
+  ("bf16x3") pass keeps 32 approximate candidates per row, every one within
+  a proven error margin of the k-th is re-scored with the exact fp32 chain,
+  and rows whose margin is not covered are recomputed exhaustively
+  (``csrc/hip/topk.hip::topk_refine_kernel``) - indices identical to the
+  brute-force exact-f32 MFMA kernel.  ``DGMC_AMD_TOPK_EXACT=0`` (or
+  ``exact=False``) returns the unrefined split-bf16 selection.
 * :class:`CandidateGraph`  - the candidate set ``S_idx [B, N_s, k]`` as a CSR
   matrix over flattened source rows (global target columns ``b*N_t + idx``)
   plus its transpose, built once per forward.
@@ -35,22 +40,26 @@ from ..runtime import loopgrad
 from .sparse import SparseOperator, piece_plan
 
 
-TOPK_EXACT = os.environ.get('DGMC_AMD_TOPK_EXACT', '0') == '1'
+TOPK_EXACT = os.environ.get('DGMC_AMD_TOPK_EXACT', '1') == '1'
 
 
-def top_k(h_s, h_t, k, exact=None):
-    """``[B, N_s, k]`` int64 indices of the k best targets per source row.
+def top_k(h_s, h_t, k, exact=None, brute_force=False):
+    """``[B, N_s, k]`` int64 indices of the k best targets per source row
+    (best first, ties to the lower index).
 
-    ``exact`` (default ``DGMC_AMD_TOPK_EXACT``) selects exact-f32 scores on
-    the GPU; otherwise scores are split-bf16 (3 MFMA passes, ~2^-16
-    relative error - only near-exact ties can rank differently)."""
+    ``exact`` (default ``DGMC_AMD_TOPK_EXACT``, on): exact fp32 selection
+    (filter + exact re-score on the GPU); ``exact=False``: split-bf16
+    scores (~2^-16 relative error - near-ties can rank differently).
+    ``brute_force``: the exact-f32 MFMA kernel over every target (the test
+    oracle of the refined path)."""
     B, N_s, C = h_s.shape
     if exact is None:
         exact = TOPK_EXACT
     if _backend.use_hip(h_s) and k <= 64 and C % 4 == 0 and C <= 256 \
             and h_s.dtype == torch.float32:
+        mode = 1 if brute_force else (2 if exact else 0)
         return _backend.ops().topk_dot(h_s.contiguous(), h_t.contiguous(),
-                                       int(k), bool(exact))
+                                       int(k), mode)
     return ref.top_k(h_s, h_t, k)
 
 

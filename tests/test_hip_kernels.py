@@ -336,6 +336,49 @@ def test_topk_dot(shape, k, exact):
     assert same > (0.999 if exact else 0.98)
 
 
+def _hub_case(B, Ns, Nt, C, seed):
+    """Hub-heavy scores with near-ties: low-rank sources, a few large-norm
+    hub targets that rank first for most rows, exact duplicates and
+    near-duplicates (differences at the last fp32 bits)."""
+    g = torch.Generator().manual_seed(seed)
+    basis = torch.randn(B, 4, C, generator=g)
+    h_s = torch.randn(B, Ns, 4, generator=g) @ basis + \
+        1e-3 * torch.randn(B, Ns, C, generator=g)
+    h_t = torch.randn(B, Nt, C, generator=g)
+    h_t[:, :8] *= 6.0                                   # hubs
+    h_t[:, Nt - 40:Nt - 20] = h_t[:, 100:120]          # exact ties
+    h_t[:, Nt - 20:] = h_t[:, 200:220] * (1 + 2e-7)     # near-ties
+    return h_s.to(DEV), h_t.to(DEV)
+
+
+@pytest.mark.parametrize('case', ['random', 'hub', 'clustered'])
+@pytest.mark.parametrize('k', [1, 10, 16])
+def test_topk_exact_refined_equals_brute_force(case, k):
+    """The default exact selection (split-bf16 filter + exact fp32
+    re-score, exhaustive fallback) returns exactly the brute-force exact-f32
+    MFMA kernel's indices (order included: score desc, index asc)."""
+    from deep_graph_matching_consensus_amd.ops import _backend
+    if case == 'random':
+        torch.manual_seed(1)
+        h_s = torch.randn(2, 700, 256, device=DEV)
+        h_t = torch.randn(2, 1500, 256, device=DEV)
+    elif case == 'hub':
+        h_s, h_t = _hub_case(1, 2000, 3000, 256, seed=3)
+    else:   # every target a near-copy of one of 5 centres: many near-ties
+        g = torch.Generator().manual_seed(5)
+        cent = torch.randn(5, 64, generator=g)
+        h_t = (cent[torch.randint(0, 5, (2500, ), generator=g)] +
+               1e-6 * torch.randn(2500, 64, generator=g))[None].to(DEV)
+        h_s = torch.randn(1, 900, 64, generator=g).to(DEV)
+    want = sparse_corr.top_k(h_s, h_t, k, brute_force=True)
+    got, n_over = _backend.ops().topk_dot_refined_stats(
+        h_s.contiguous(), h_t.contiguous(), k)
+    assert torch.equal(got, want)
+    assert torch.equal(sparse_corr.top_k(h_s, h_t, k), want)  # the default
+    if case == 'random':
+        assert int(n_over) == 0      # the margin covers random inputs
+
+
 @pytest.mark.parametrize('Ns,Nt', [(4000, 3000), (200, 5000)])
 def test_topk_dot_split_merge(Ns, Nt):
     """Few source rows -> the target range is split over blocks and the
@@ -346,7 +389,8 @@ def test_topk_dot_split_merge(Ns, Nt):
     # duplicated targets -> exact ties must resolve to the lower index
     h_t[0, Nt // 2:Nt // 2 + 7] = h_t[0, 3:10]
     a = sparse_corr.top_k(h_s, h_t, 10, exact=False)
-    b = sparse_corr.top_k(h_s, h_t, 10, exact=True)
+    b = sparse_corr.top_k(h_s, h_t, 10, brute_force=True)
+    assert torch.equal(sparse_corr.top_k(h_s, h_t, 10, exact=True), b)
     scores = h_s @ h_t.transpose(-1, -2)
     va, vb = torch.gather(scores, -1, a), torch.gather(scores, -1, b)
     assert torch.allclose(va, vb, atol=1e-3)
