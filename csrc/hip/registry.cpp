@@ -238,10 +238,21 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
                      const c10::optional<at::Tensor>& root, bool trans_w,
                      const c10::optional<at::Tensor>& tiles);
 at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
-                         int64_t N, int64_t row0, int64_t P_cap);
+                         int64_t N, int64_t row0, int64_t P_cap,
+                         int64_t unit);
 at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
                       const at::Tensor& seg, const at::Tensor& bt,
                       const c10::optional<at::Tensor>& broot, bool gather);
+at::Tensor split3(const at::Tensor& x);
+at::Tensor slot_weight_x3(const at::Tensor& weight,
+                          const c10::optional<at::Tensor>& root,
+                          bool transpose);
+at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
+                        const at::Tensor& seg, const at::Tensor& b3,
+                        bool gather, const c10::optional<at::Tensor>& tiles);
+at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
+                         const at::Tensor& src, const at::Tensor& seg,
+                         int64_t rounds);
 at::Tensor slot_weight_t(const at::Tensor& weight,
                          const c10::optional<at::Tensor>& root);
 at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt);
@@ -251,7 +262,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
                             const c10::optional<at::Tensor>& seg,
-                            const c10::optional<at::Tensor>& ranges);
+                            const c10::optional<at::Tensor>& ranges,
+                            bool planes);
 at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
                               const at::Tensor& cinv);
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
@@ -441,19 +453,28 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm(Tensor X, Tensor src, Tensor seg, Tensor weight, Tensor? "
       "root, bool trans_w, Tensor? tiles=None) -> Tensor");
   m.def(
-      "slot_dx_tiles(Tensor posmap, Tensor seg, int N, int row0, int P_cap) "
-      "-> Tensor");
+      "slot_dx_tiles(Tensor posmap, Tensor seg, int N, int row0, int P_cap, "
+      "int unit=128) -> Tensor");
   m.def(
       "slot_gemm2(Tensor X, Tensor src, Tensor seg, Tensor bt, Tensor? "
       "broot, bool gather) -> Tensor");
   m.def("slot_weight_t(Tensor weight, Tensor? root) -> Tensor");
+  m.def("split3(Tensor x) -> Tensor");
+  m.def(
+      "slot_wgrad_x6(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
+      "rounds) -> Tensor");
+  m.def("slot_weight_x3(Tensor weight, Tensor? root, bool transpose) -> Tensor");
+  m.def(
+      "slot_gemm_x6(Tensor a3, Tensor src, Tensor seg, Tensor b3, bool gather, "
+      "Tensor? tiles=None) -> Tensor");
   m.def("dense_nt_f32(Tensor[] parts, Tensor bt) -> Tensor");
   m.def(
       "dense_wgrad_f32(Tensor[] xparts, int nparts, Tensor[] gs, Tensor "
       "seg01) -> Tensor");
   m.def(
       "slot_spmm_rowmap(Tensor rowptr, Tensor col, Tensor val, Tensor cinv, "
-      "Tensor g, Tensor? seg=None, Tensor? ranges=None) -> Tensor");
+      "Tensor g, Tensor? seg=None, Tensor? ranges=None, bool planes=False) -> "
+      "Tensor");
   m.def("slot_rowmap_ranges(Tensor rowptr, Tensor cinv) -> Tensor");
   m.def(
       "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add, "
@@ -533,6 +554,10 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_gemm2", &dgmc::slot_gemm2);
   m.impl("slot_dx_tiles", &dgmc::slot_dx_tiles);
   m.impl("slot_weight_t", &dgmc::slot_weight_t);
+  m.impl("split3", &dgmc::split3);
+  m.impl("slot_wgrad_x6", &dgmc::slot_wgrad_x6);
+  m.impl("slot_weight_x3", &dgmc::slot_weight_x3);
+  m.impl("slot_gemm_x6", &dgmc::slot_gemm_x6);
   m.impl("dense_nt_f32", &dgmc::dense_nt_f32);
   m.impl("dense_wgrad_f32", &dgmc::dense_wgrad_f32);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);

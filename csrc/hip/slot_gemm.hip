@@ -38,7 +38,9 @@ namespace {
 typedef float sg_f32x16 __attribute__((ext_vector_type(16)));
 typedef float sg_f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kSgBM = 128;               // compact rows per tile / segment unit
+constexpr int kSgBM = 128;               // compact rows per tile
+constexpr int kSgSeg = 256;              // slot segment alignment (the bf16x6
+                                         // kernels' 256-row tiles)
 constexpr int kSgBN = 128;
 constexpr int kSgBK = 32;
 constexpr int kSgThreads = 256;          // 4 waves, 2 x 2 wave grid of 64x64
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(256) void sg_fill_kernel(
     int run = 0;
     for (int k = 0; k < S; ++k) {
       sseg[k] = run;
-      run += (cnt[k] + kSgBM - 1) / kSgBM * kSgBM;
+      run += (cnt[k] + kSgSeg - 1) / kSgSeg * kSgSeg;
     }
     sseg[S] = run;
   }
@@ -211,7 +213,7 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
                   col.scalar_type() == at::kInt,
               "slot_compact_plan: int32 CSR expected");
   TORCH_CHECK(S >= 1 && S <= kSgMaxS, "slot_compact_plan: 1 <= S <= 64");
-  TORCH_CHECK(P_cap % kSgBM == 0, "slot_compact_plan: P_cap % 128");
+  TORCH_CHECK(P_cap % kSgSeg == 0, "slot_compact_plan: P_cap % 256");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(rowptr.device());
   const int R = (int)rowptr.numel() - 1;
   const int cap = (int)col.numel();
@@ -477,7 +479,7 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
 // listed in slot order; out[tcap] = count.
 __global__ __launch_bounds__(64) void sg_dx_tiles_kernel(
     const int* __restrict__ posmap, const int* __restrict__ seg, int N, int S,
-    int row0, int tcap, int* __restrict__ out) {
+    int row0, int tcap, int unit, int* __restrict__ out) {
   const int k = threadIdx.x;
   int first = 0, last = 0;
   if (k < S) {
@@ -489,8 +491,8 @@ __global__ __launch_bounds__(64) void sg_dx_tiles_kernel(
         break;
       }
     }
-    first = p / kSgBM;
-    last = seg[k + 1] / kSgBM;
+    first = p / unit;
+    last = seg[k + 1] / unit;
     if (first > last) first = last;
   }
   const int n = last - first;
@@ -506,19 +508,22 @@ __global__ __launch_bounds__(64) void sg_dx_tiles_kernel(
 }
 
 at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
-                         int64_t N, int64_t row0, int64_t P_cap) {
+                         int64_t N, int64_t row0, int64_t P_cap,
+                         int64_t unit) {
   TORCH_CHECK(posmap.is_cuda() && posmap.scalar_type() == at::kInt &&
                   seg.scalar_type() == at::kInt,
               "slot_dx_tiles: int32 plan");
   const int64_t S = seg.numel() - 1;
-  TORCH_CHECK(S <= 64 && posmap.numel() == N * S && P_cap % kSgBM == 0,
-              "slot_dx_tiles: plan shapes");
+  TORCH_CHECK(S <= 64 && posmap.numel() == N * S && (unit == 128 ||
+              unit == 256) && P_cap % unit == 0,
+              "slot_dx_tiles: plan shapes, unit 128 / 256");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(posmap.device());
-  const int64_t tcap = P_cap / kSgBM;
+  const int64_t tcap = P_cap / unit;
   at::Tensor out = at::empty({tcap + 1}, posmap.options());
   hipLaunchKernelGGL(sg_dx_tiles_kernel, dim3(1), dim3(64), 0, stream(),
                      posmap.data_ptr<int>(), seg.data_ptr<int>(), (int)N,
-                     (int)S, (int)row0, (int)tcap, out.data_ptr<int>());
+                     (int)S, (int)row0, (int)tcap, (int)unit,
+                     out.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
   return out;
 }
@@ -1060,12 +1065,31 @@ __global__ __launch_bounds__(256) void sg_rowmap_ranges_kernel(
   out[p] = c >= 0 ? make_int2(rowptr[c], rowptr[c + 1]) : make_int2(0, 0);
 }
 
+typedef __bf16 sg_bf16x4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> three bf16 terms hi + mid + lo (round-to-nearest at each stage;
+// the operand format of slot_gemm_x6.hip).
+__device__ __forceinline__ void sg_split4(const float4 v, sg_bf16x4& h,
+                                          sg_bf16x4& m, sg_bf16x4& l) {
+  const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 he = (__bf16)f[e];
+    const float r1 = f[e] - (float)he;
+    const __bf16 me = (__bf16)r1;
+    h[e] = he;
+    m[e] = me;
+    l[e] = (__bf16)(r1 - (float)me);
+  }
+}
+
 template <int LPR, bool XL>
 __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ val, const int* __restrict__ cinv,
     const int2* __restrict__ ranges, const int* __restrict__ seg, int S,
-    const float* __restrict__ g, float* __restrict__ out, int P, int C) {
+    const float* __restrict__ g, float* __restrict__ out,
+    __bf16* __restrict__ out3, int P, int C) {
   constexpr int RPB = 256 / LPR;
   int p;
   if (XL) {
@@ -1134,7 +1158,16 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
           acc.w = fmaf(w[u], v[u].w, acc.w);
         }
     }
-    *reinterpret_cast<float4*>(out + (size_t)p * C + c0) = acc;
+    if (out3 != nullptr) {     // bf16x6 operand planes [3][P][C]
+      sg_bf16x4 h, m, l;
+      sg_split4(acc, h, m, l);
+      const size_t o = (size_t)p * C + c0, plane = (size_t)P * C;
+      *reinterpret_cast<sg_bf16x4*>(out3 + o) = h;
+      *reinterpret_cast<sg_bf16x4*>(out3 + o + plane) = m;
+      *reinterpret_cast<sg_bf16x4*>(out3 + o + 2 * plane) = l;
+    } else {
+      *reinterpret_cast<float4*>(out + (size_t)p * C + c0) = acc;
+    }
   }
 }
 
@@ -1142,7 +1175,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
                             const c10::optional<at::Tensor>& seg,
-                            const c10::optional<at::Tensor>& ranges) {
+                            const c10::optional<at::Tensor>& ranges,
+                            bool planes) {
   TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kFloat &&
                   g.is_contiguous() && g.dim() == 2 && g.size(1) % 4 == 0 &&
                   aligned16(g.data_ptr()),
@@ -1151,8 +1185,14 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
               "slot_spmm_rowmap: dtypes");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
   const int64_t P = cinv.numel(), C = g.size(1);
-  at::Tensor out = at::empty({P, C}, g.options());
+  at::Tensor out = planes ? at::empty({3, P, C}, g.options().dtype(at::kBFloat16))
+                          : at::empty({P, C}, g.options());
   if (P == 0) return out;
+  // (Rows past seg[S] are left unwritten in both formats: no consumer -
+  // the GEMMs stop at seg[S], the weight gradient at its segments - reads
+  // them.)
+  float* op = planes ? nullptr : out.data_ptr<float>();
+  __bf16* op3 = planes ? reinterpret_cast<__bf16*>(out.data_ptr()) : nullptr;
   const int* segp = nullptr;
   int S = 0;
   if (seg.has_value() && seg->defined()) {
@@ -1180,8 +1220,7 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream(),
                        rowptr.data_ptr<int>(), col.data_ptr<int>(),
                        val.data_ptr<float>(), cinv.data_ptr<int>(), rg, segp,
-                       S, g.data_ptr<float>(), out.data_ptr<float>(), (int)P,
-                       (int)C);
+                       S, g.data_ptr<float>(), op, op3, (int)P, (int)C);
   };
   if (lanes <= 8) go(std::integral_constant<int, 8>());
   else if (lanes <= 16) go(std::integral_constant<int, 16>());
@@ -1330,12 +1369,12 @@ struct SgUses {
 // by the LDS index buffer (qcap steps).  One wave: lane s owns slot s.
 __global__ __launch_bounds__(64) void sg_items_kernel(
     const int* __restrict__ seg, int S, int nu, int target, int qcap,
-    int G_cap, int* __restrict__ items, int* __restrict__ ib) {
+    int G_cap, int* __restrict__ items, int* __restrict__ ib, int rows) {
   const int lane = threadIdx.x;
   int b = 0, steps = 0;
   if (lane < S) {
     b = seg[lane];
-    steps = (seg[lane + 1] - b) / 32 * nu;
+    steps = (seg[lane + 1] - b) / rows * nu;
   }
   int tot = steps;
 #pragma unroll
@@ -1509,6 +1548,36 @@ __global__ __launch_bounds__(256) void sg_fold_kernel(
   *reinterpret_cast<float4*>(out + (size_t)s * per + i) = acc;
 }
 
+// Work items (slot, step range) of `rows`-row steps for an external weight
+// gradient kernel (slot_gemm_x6.hip) + the per-slot fold of its partials.
+std::vector<at::Tensor> slot_wgrad_items(const at::Tensor& seg, int64_t nu,
+                                         int64_t target, int64_t qcap,
+                                         int64_t G_cap, int64_t rows) {
+  const int64_t S = seg.numel() - 1;
+  auto i32 = seg.options();
+  at::Tensor items = at::empty({G_cap, 3}, i32);
+  at::Tensor ib = at::empty({S + 1}, i32);
+  hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
+                     seg.data_ptr<int>(), (int)S, (int)nu, (int)target,
+                     (int)qcap, (int)G_cap, items.data_ptr<int>(),
+                     ib.data_ptr<int>(), (int)rows);
+  DGMC_CHECK_LAUNCH();
+  return {items, ib};
+}
+
+at::Tensor slot_fold_parts(const at::Tensor& part, const at::Tensor& ib,
+                           int64_t S, int64_t Kin, int64_t C) {
+  const int64_t per = Kin * C;
+  at::Tensor out = at::empty({S, Kin, C}, part.options());
+  hipLaunchKernelGGL(sg_fold_kernel, dim3((per / 4 + 255) / 256, S), dim3(256),
+                     0, stream(), part.data_ptr<float>(), ib.data_ptr<int>(),
+                     (int)S, per, out.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+int slot_num_cus(int dev) { return num_cus(dev); }
+
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
                           int64_t rounds) {
@@ -1549,7 +1618,7 @@ at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
   hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
                      seg.data_ptr<int>(), (int)S, (int)nu, (int)target,
                      (int)qcap, (int)G_cap, items.data_ptr<int>(),
-                     ib.data_ptr<int>());
+                     ib.data_ptr<int>(), kW2Rows);
   DGMC_CHECK_LAUNCH();
   const int64_t per = Kin * C;
   at::Tensor part = at::empty({G_cap, per}, xs[0].options());
@@ -1618,7 +1687,7 @@ at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
   hipLaunchKernelGGL(sg_items_kernel, dim3(1), dim3(64), 0, stream(),
                      seg01.data_ptr<int>(), 1, (int)nu, (int)target,
                      (int)qcap, (int)G_cap, items.data_ptr<int>(),
-                     ib.data_ptr<int>());
+                     ib.data_ptr<int>(), kW2Rows);
   DGMC_CHECK_LAUNCH();
   const int64_t per = Kin * C;
   at::Tensor part = at::empty({G_cap, per}, gs[0].options());

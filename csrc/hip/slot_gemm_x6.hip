@@ -1,0 +1,769 @@
+// fp32-accurate slot GEMM on the bf16 matrix cores ("bf16x6").
+//
+// Same products as slot_gemm.hip (reference: /root/reference/dgmc/models/
+// spline.py:21,49 - PyG SplineConv, fp32):
+//
+//   Y[m, :] = A_m Bt_s^T    forward: A_m = X[src[m]], Bt_s = W_s^T images
+//                           dX:      A_m = dY_c[m],   Bt_s = W_s ([in, out])
+//
+// but on v_mfma_f32_32x32x16_bf16 (16x the f32-MFMA rate) instead of the
+// exact-f32 v_mfma_f32_32x32x2_f32.  Every fp32 operand is split once into
+// three bf16 terms x = hi + mid + lo (round-to-nearest at each stage, so the
+// residual is < 2^-26 |x|: 24 mantissa bits in three 8-bit pieces), and the
+// six products whose order is >= 2^-16 are accumulated in fp32:
+//
+//   acc_hi += hi*hi,   acc_lo += lo*hi + hi*lo + mid*mid + mid*hi + hi*mid
+//
+// The three dropped terms (mid*lo, lo*mid, lo*lo) are < 2^-26 relative per
+// product - below fp32's own rounding - and keeping the large and small
+// partial sums in separate accumulators halves the accumulation error:
+// measured on MI355X against an fp64 oracle (tools/micro/
+// split_bf16_numerics.hip, profiles/split_bf16_numerics_r4.jsonl) the max
+// error is 2.2-2.9x BELOW the exact-f32 MFMA chain at K = 128 ... 16384.
+// Cost: 6 bf16 MFMAs (6 x 32 cycles) per 16-deep k step of a 32x32 block vs
+// 8 f32 MFMAs (8 x 64 cycles): 2.7x fewer matrix-core cycles.
+//
+// Kernel: persistent grid over 256x128 output tiles (each inside one slot
+// segment), 8 waves of 64x64, one workgroup per CU.  Operand planes are
+// bf16 [3][rows][K]; each 16-deep k chunk of a tile is staged global -> LDS
+// by global_load_lds_dwordx4 through a four-stage ring (raw s_barrier,
+// hand-counted vmcnt), into [rows][32 B] images whose two 16-byte k-halves
+// are XOR-swizzled by row bit 3 so every fragment read (ds_read_b128, 8
+// consecutive k of one row) is bank-conflict free.  The weights are the
+// MFMA A operand, so the accumulator holds Y^T: the epilogue writes float4
+// rows (acc_hi + acc_lo).
+#include "common.h"
+
+namespace dgmc {
+
+namespace {
+
+typedef __bf16 x6_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 x6_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float x6_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kX6BN = 128;                 // output columns per tile
+constexpr int kX6BK = 16;                  // k per staged chunk
+constexpr int kX6MaxS = 64;
+
+int x6_num_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    hipDeviceProp_t prop;
+    DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
+    cached[dev] = prop.multiProcessorCount;
+  }
+  return cached[dev];
+}
+
+// 16 bytes per lane global -> LDS (destination M0 + 16 * lane), issued as
+// inline asm so the compiler does not model it as an LDS write (it would
+// otherwise drain vmcnt before every fragment read); counted by hand below.
+__device__ __forceinline__ void x6_dma16(const __bf16* g, DGMC_LDS __bf16* l) {
+  const unsigned m0 =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :: "v"(g), "s"(m0) : "memory", "m0");
+}
+
+// s_barrier without __syncthreads' fence (which would drain vmcnt and
+// serialise the next chunk's DMA with this chunk's MFMAs).
+__device__ __forceinline__ void x6_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void x6_split(float x, __bf16& h, __bf16& m,
+                                         __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;      // exact
+  m = (__bf16)r1;
+  const float r2 = r1 - (float)m;     // exact
+  l = (__bf16)r2;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Splits: fp32 [R, K] (row stride lda) -> bf16 planes [3][R][K].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void split3_kernel(
+    const float* __restrict__ x, int64_t R, int K, int64_t lda,
+    __bf16* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int vpr = K / 4;
+  const int64_t r = t / vpr;
+  if (r >= R) return;
+  const int c = (int)(t - r * vpr) * 4;
+  const float4 v = *reinterpret_cast<const float4*>(x + r * lda + c);
+  const float f[4] = {v.x, v.y, v.z, v.w};
+  x6_bf16x4 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __bf16 he, me, le;
+    x6_split(f[e], he, me, le);
+    h[e] = he;
+    m[e] = me;
+    l[e] = le;
+  }
+  const int64_t plane = R * K;
+  __bf16* o = out + r * K + c;
+  *reinterpret_cast<x6_bf16x4*>(o) = h;
+  *reinterpret_cast<x6_bf16x4*>(o + plane) = m;
+  *reinterpret_cast<x6_bf16x4*>(o + 2 * plane) = l;
+}
+
+// Weight images: slot s < nw is weight[s] ([in, out]), slot nw the root.
+// TRANS: out[p][s][n][k] = W_s[k][n] (forward Bt = W^T, K = in, Nn = out);
+// else   out[p][s][n][k] = W_s[n][k] (dX Bt = W, Nn = in, K = out).
+template <bool TRANS>
+__global__ __launch_bounds__(256) void weight_x3_kernel(
+    const float* __restrict__ weight, const float* __restrict__ root, int nw,
+    int in, int out, __bf16* __restrict__ img, int64_t plane) {
+  const int Nn = TRANS ? out : in, K = TRANS ? in : out;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int vpr = K / 4;
+  const int64_t per_slot = (int64_t)Nn * vpr;
+  const int s = (int)(t / per_slot);
+  const int64_t rem = t - (int64_t)s * per_slot;
+  const int n = (int)(rem / vpr), k = (int)(rem - (int64_t)n * vpr) * 4;
+  if (s > nw || (s == nw && root == nullptr)) return;
+  const float* w = s < nw ? weight + (size_t)s * in * out : root;
+  float f[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    f[e] = TRANS ? w[(size_t)(k + e) * out + n] : w[(size_t)n * out + k + e];
+  x6_bf16x4 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __bf16 he, me, le;
+    x6_split(f[e], he, me, le);
+    h[e] = he;
+    m[e] = me;
+    l[e] = le;
+  }
+  __bf16* o = img + ((size_t)s * Nn + n) * K + k;
+  *reinterpret_cast<x6_bf16x4*>(o) = h;
+  *reinterpret_cast<x6_bf16x4*>(o + plane) = m;
+  *reinterpret_cast<x6_bf16x4*>(o + 2 * plane) = l;
+}
+
+// ---------------------------------------------------------------------------
+// The GEMM.  A planes [3][*][K] (plane stride a_plane), B planes
+// [3][S][Nn][K] (plane stride b_plane).  tiles (optional): 256-row tile list
+// with its count at tiles[tcap] (dX of psi_2: only the target-source tiles).
+//
+// One workgroup per CU (8 waves = 2 per SIMD, 4 (rows) x 2 (cols) waves of
+// 64 x 64), output tiles of 256 compact rows x 128 columns (slot segments
+// are 256-aligned, so a tile is inside one slot), k consumed 32 at a time
+// (48 MFMAs per wave between barriers) through two 72 KB LDS stages with
+// ONE barrier per chunk: after it, the next chunk is staged into the buffer
+// every wave has just finished reading.  Row segments are 64 B per plane
+// (16 rows per 1 KB DMA instruction).  The 16-byte quads of a row are
+// XOR-swizzled by f(row bits 2-4) so the ds_read_b128 fragment reads are
+// bank-conflict free.  The next tile's gather indices are DMA'd into LDS
+// (global_load_lds_dword): no compiler-visible vector load sits inside the
+// hand-counted DMA pipeline.
+// ---------------------------------------------------------------------------
+constexpr int kXBM = 256;                        // rows per tile
+constexpr int kXBK = 32;                         // k per chunk
+constexpr int kXThreads = 512;
+constexpr int kXAPlane = kXBM * kXBK;            // 8192 bf16 (16 KB)
+constexpr int kXBPlane = kX6BN * kXBK;           // 4096 bf16 (8 KB)
+constexpr int kXStage = 3 * kXAPlane + 3 * kXBPlane;   // bf16 per stage
+constexpr size_t kXLds = (size_t)2 * kXStage * 2 + 2 * kXBM * 4;
+
+__device__ __forceinline__ void x6_dma4(const int* g, DGMC_LDS int* l) {
+  const unsigned m0 =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %0, off"
+      :: "v"(g), "s"(m0) : "memory", "m0");
+}
+
+// Quad swizzle of a 64-B row image: bits (2 ^ 4, 3 ^ 4) of the row.
+__device__ __forceinline__ int x6_qswz(int r) {
+  const int b4 = (r >> 4) & 1;
+  return (((r >> 2) & 1) ^ b4) | ((((r >> 3) & 1) ^ b4) << 1);
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
+    const __bf16* __restrict__ A, int64_t a_plane, const int* __restrict__ src,
+    const int* __restrict__ seg, int S, const __bf16* __restrict__ B,
+    int64_t b_plane, int K, int Nn, const int* __restrict__ tiles, int tcap,
+    float* __restrict__ Y, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) char x6_smem[];
+  DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)x6_smem;
+  DGMC_LDS int* sidx =
+      (DGMC_LDS int*)(x6_smem + (size_t)2 * kXStage * 2);   // [2][256]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int ntn = Nn / kX6BN, nk = K / kXBK;
+  // Segment starts in lane registers: slot(m) = #{1 <= s < S: seg[s] <= m}.
+  const int segv = lane <= S ? seg[lane] : 0x7fffffff;
+  const int nrt = tiles != nullptr
+                      ? tiles[tcap]
+                      : __builtin_amdgcn_readlane(segv, S) / kXBM;
+  const int U = nrt * ntn;
+  const int G = gridDim.x;
+  const int u0 = xcd_remap(blockIdx.x, G);
+  if (u0 >= U) return;
+  const int my_tiles = (U - u0 + G - 1) / G;
+  const int total = my_tiles * nk;
+  auto slot_of = [&](int m) {
+    return __popcll(__ballot(lane >= 1 && lane < S && segv <= m));
+  };
+  auto row_tile = [&](int j) {          // j-th tile of this workgroup
+    const int q = (u0 + j * G) / ntn;
+    return tiles != nullptr ? tiles[q] : q;
+  };
+  auto col_tile = [&](int j) { return (u0 + j * G) % ntn; };
+
+  // Staging.  A: wave w fills rows 32 w + 16 e + L / 4 (e = 0, 1) of the
+  // three plane images; B: DMA t = 3 w + e (e = 0..2) fills plane t / 8,
+  // rows 16 (t % 8) + L / 4.  Lane L holds physical quad L % 4 of its row,
+  // i.e. logical quad (L % 4) ^ swz(row).
+  const int lr = lane >> 2;
+  int ar[2], aq[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    ar[e] = 32 * wave + 16 * e + lr;
+    aq[e] = 8 * ((lane & 3) ^ x6_qswz(ar[e]));
+  }
+  int bp[3], br[3], bq[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int t = 3 * wave + e;
+    bp[e] = t >> 3;
+    br[e] = 16 * (t & 7) + lr;
+    bq[e] = 8 * ((lane & 3) ^ x6_qswz(br[e]));
+  }
+  const bool bhi = wave >= 4;
+  const __bf16* arow[2] = {A, A};
+  const __bf16* brow = B;
+  int bslot = 0;
+  auto set_tile = [&](int j) {
+    const int m0 = row_tile(j) * kXBM;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      int ix = m0 + ar[e];
+      if (GATHER) ix = sidx[(j & 1) * kXBM + ar[e]];
+      arow[e] = A + (size_t)(ix < 0 ? 0 : ix) * K + aq[e];   // padding: row 0
+    }
+    bslot = slot_of(m0);
+    brow = B + ((size_t)bslot * Nn + col_tile(j) * kX6BN) * K;
+  };
+  // Gather indices of tile j into sidx[j & 1] (waves 4-7, one dword each).
+  auto idx_dma = [&](int j) {
+    if (GATHER && bhi && j < my_tiles)
+      x6_dma4(src + row_tile(j) * kXBM + (tid - 256),
+              sidx + (j & 1) * kXBM + 64 * (wave - 4));
+  };
+  auto stage = [&](int it) {
+    const int j = it / nk, kc = it - j * nk;
+    if (kc == 0) {
+      set_tile(j);
+      idx_dma(j + 1);
+    }
+    if (dbg & 2) return;
+    DGMC_LDS __bf16* buf = ring + (it & 1) * kXStage;
+    const int k0 = kc * kXBK;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        x6_dma16(arow[e] + p * a_plane + k0,
+                 buf + p * kXAPlane + (32 * wave + 16 * e) * kXBK);
+    DGMC_LDS __bf16* bb = buf + 3 * kXAPlane;
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      x6_dma16(brow + bp[e] * b_plane + (size_t)br[e] * K + k0 + bq[e],
+               bb + bp[e] * kXBPlane + (br[e] - lr) * kXBK);
+  };
+
+  // Fragment offsets: row (block base + i), logical quad 2 s + h at physical
+  // quad (2 s + h) ^ swz(i) (block bases are multiples of 32: swz of i).
+  const int i = lane & 31, h = lane >> 5;
+  const int fs = x6_qswz(i);
+  const int offX = (wm * 64 + i) * kXBK;
+  const int offW = (wn * 64 + i) * kXBK;
+
+  x6_f32x16 acc[2][2], acs[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
+
+  auto compute = [&](const DGMC_LDS __bf16* buf) {
+    if (dbg & 1) return;
+    const DGMC_LDS __bf16* la = buf;
+    const DGMC_LDS __bf16* lb = buf + 3 * kXAPlane;
+    x6_bf16x8 w[2][3][2], x[2][3][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int qo = 8 * ((2 * st + h) ^ fs);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          w[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
+              lb + p * kXBPlane + offW + a * 32 * kXBK + qo);
+          x[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
+              la + p * kXAPlane + offX + a * 32 * kXBK + qo);
+        }
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          x6_f32x16 sm = acs[a][b];
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][2][a], x[st][0][b], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][0][a], x[st][2][b], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][1][a], x[st][1][b], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][1][a], x[st][0][b], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][0][a], x[st][1][b], sm, 0, 0, 0);
+          acs[a][b] = sm;
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              w[st][0][a], x[st][0][b], acc[a][b], 0, 0, 0);
+        }
+  };
+  auto epilogue = [&](int j) {
+    const int m0 = row_tile(j) * kXBM + wm * 64 + i;
+    const int n0 = col_tile(j) * kX6BN + wn * 64 + 4 * h;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* yrow = Y + (size_t)(m0 + 32 * b) * Nn + n0 + 32 * a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          *reinterpret_cast<float4*>(yrow + 8 * q) = make_float4(
+              acc[a][b][4 * q] + acs[a][b][4 * q],
+              acc[a][b][4 * q + 1] + acs[a][b][4 * q + 1],
+              acc[a][b][4 * q + 2] + acs[a][b][4 * q + 2],
+              acc[a][b][4 * q + 3] + acs[a][b][4 * q + 3]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[a][b][4 * q + r] = acs[a][b][4 * q + r] = 0.f;
+        }
+      }
+  };
+
+  if (GATHER) {                 // the first tile's gather indices
+    idx_dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  stage(0);
+  for (int it = 0; it < total; ++it) {
+    // Item `it` (staged during the previous iteration) must have landed;
+    // the previous tile's 16 epilogue stores, issued after it, need not.
+    if (it > 0 && it % nk == 0)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x6_barrier();
+    if (it + 1 < total) stage(it + 1);
+    compute(ring + (it & 1) * kXStage);
+    const int j = it / nk;
+    if (it - j * nk == nk - 1) epilogue(j);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient (TN) on bf16x6:
+//   dW_s[i, c] = sum_u sum_{p in slot s} X_u[src p][i] * dY_u[p][c]
+// Same work decomposition as slot_gemm.hip's slot_wgrad2_kernel - items =
+// (slot, range of (16-row step, use) pairs, chunk-major) x 128 x 128 output
+// tiles, per-item fp32 partials folded per slot in item order
+// (deterministic) - with the contraction over compact rows p on
+// v_mfma_f32_32x32x16_bf16: both operands are needed k(=p)-major per lane,
+// so the row-major [16 p][128 ch] bf16 plane images are read with the
+// gfx950 transposing ds_read_b64_tr_b16 (two per 8-row half fragment).  The
+// images' 16-byte chunks are XOR-swizzled by ((row & 3) << 2 | (row >> 2) &
+// 3), which makes the transposed reads bank-conflict free (guide T10 (b));
+// the lane-linear LDS-DMA fill applies the same XOR to the global chunk each
+// lane fetches.  Three-stage ring (2 x 24 KB in flight), two workgroups per
+// CU, dual accumulators as in the forward kernel.
+// ---------------------------------------------------------------------------
+constexpr int kWXRows = 16;                      // rows per step
+constexpr int kWXNst = 3;
+constexpr int kWXPlane = kWXRows * 128;          // bf16 per plane image
+constexpr int kWXStage = 6 * kWXPlane;           // X (3) + dY (3) planes
+constexpr int kWXMaxRows = 1536;                 // gathered rows per item
+constexpr int kWXMaxU = 16;
+constexpr size_t kWXLds = (size_t)kWXNst * kWXStage * 2 + kWXMaxRows * 4;
+
+struct X6Uses {
+  const __bf16* x[kWXMaxU];     // X_u planes [3][N][Kin]
+  const __bf16* g[kWXMaxU];     // dY_u planes [3][P][C]
+};
+
+typedef short x6_i16x4 __attribute__((ext_vector_type(4)));
+typedef short x6_i16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int wx_swz(int r) {
+#ifdef DGMC_WX_NOSWZ
+  return 0;
+#else
+  return ((r & 3) << 2) | ((r >> 2) & 3);
+#endif
+}
+
+__global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
+    X6Uses U, int nu, int64_t xplane, int64_t gplane,
+    const int* __restrict__ src, const int* __restrict__ seg,
+    const int* __restrict__ items, int Kin, int C, float* __restrict__ part,
+    int dbg) {
+  extern __shared__ __attribute__((aligned(16))) char wx_smem[];
+  DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)wx_smem;
+  DGMC_LDS int* sidx =
+      (DGMC_LDS int*)(wx_smem + (size_t)kWXNst * kWXStage * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int tiles_n = C / 128, tiles = (Kin / 128) * tiles_n;
+  const int item = blockIdx.x / tiles, t = blockIdx.x % tiles;
+  const int i0 = (t / tiles_n) * 128, n0 = (t % tiles_n) * 128;
+  const int s = items[3 * item];
+  if (s < 0) return;
+  const int qb = items[3 * item + 1], qe = items[3 * item + 2];
+  const int c0 = qb / nu;
+  const int pb = seg[s] + c0 * kWXRows;
+  const int nrows = ((qe - 1) / nu - c0 + 1) * kWXRows;
+  for (int r = tid; r < nrows; r += 256) {
+    const int j = src[pb + r];
+    sidx[r] = j < 0 ? 0 : j;            // padding rows: their dY row is zero
+  }
+  __syncthreads();
+  const int total = qe - qb;
+
+  // Staging: wave w fills rows 4 w .. 4 w + 3 of each plane image (1 KB per
+  // DMA); lane L -> row 4 w + L / 16, physical chunk L % 16, which holds the
+  // logical chunk (L % 16) ^ swz(row).
+  const int srow = 4 * wave + (lane >> 4);
+  const int schunk = (lane & 15) ^ wx_swz(srow);
+  auto stage = [&](int q, DGMC_LDS __bf16* buf) {
+    const int qq = qb + q;
+    const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
+    const int row = ch * kWXRows + srow;
+    const __bf16* xr = U.x[u] + (size_t)sidx[row] * Kin + i0 + 8 * schunk;
+    const __bf16* gr = U.g[u] + (size_t)(pb + row) * C + n0 + 8 * schunk;
+    DGMC_LDS __bf16* d = buf + 4 * wave * 128;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x6_dma16(xr + p * xplane, d + p * kWXPlane);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      x6_dma16(gr + p * gplane, d + (3 + p) * kWXPlane);
+  };
+
+  // Transposed fragment reads: 16-lane group g = lane / 16 covers columns
+  // 16 (g & 1) .. + 15 of the 32-column block and rows 8 (g >> 1) .. + 7;
+  // lane 4 q + p (of the group) addresses row q (+ 4 for the second read),
+  // columns 4 p .. 4 p + 3.
+  const int gq = (lane & 15) >> 2, gp = lane & 3, grp = lane >> 4;
+  const int kb = 8 * (grp >> 1), cb = 16 * (grp & 1);
+  auto tr_off = [&](int col0, int rr) {   // element offset in a plane image
+    const int row = kb + rr + gq;
+    const int chunk = (col0 + cb) / 8 + (gp >> 1);
+    return row * 128 + 8 * (chunk ^ wx_swz(row)) + 4 * (gp & 1);
+  };
+  int offG[2][2], offX[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      offG[a][rr] = tr_off(wn * 64 + a * 32, 4 * rr);
+      offX[a][rr] = tr_off(wm * 64 + a * 32, 4 * rr);
+    }
+
+  x6_f32x16 acc[2][2], acs[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
+
+  // Two transposing reads (rows kb .. kb + 3 and kb + 4 .. kb + 7) make one
+  // 8-element fragment.
+  auto frag = [&](const DGMC_LDS __bf16* img, int o0, int o1) {
+    const x6_i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (DGMC_LDS x6_i16x4*)(img + o0));
+    const x6_i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (DGMC_LDS x6_i16x4*)(img + o1));
+    // Whole-vector reinterpretation (a per-element bit_cast of the short
+    // vector's lanes miscompiled to element 0 on this toolchain).
+    const x6_i16x8 both = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5,
+                                                  6, 7);
+    return __builtin_bit_cast(x6_bf16x8, both);
+  };
+  auto compute = [&](const DGMC_LDS __bf16* buf) {
+    x6_bf16x8 gv[3][2], xv[3][2];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        gv[p][a] = frag(buf + (3 + p) * kWXPlane, offG[a][0], offG[a][1]);
+        xv[p][a] = frag(buf + p * kWXPlane, offX[a][0], offX[a][1]);
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        x6_f32x16 sm = acs[a][b];
+        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[2][a], xv[0][b], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[0][a], xv[2][b], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[1][a], xv[1][b], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[1][a], xv[0][b], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[0][a], xv[1][b], sm, 0, 0, 0);
+        acs[a][b] = sm;
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            gv[0][a], xv[0][b], acc[a][b], 0, 0, 0);
+      }
+  };
+
+  const int pro = total < kWXNst - 1 ? total : kWXNst - 1;
+  for (int q = 0; q < pro; ++q) stage(q, ring + (q % kWXNst) * kWXStage);
+  if (dbg & 8) {        // diagnostic: dump lane fragments of stage 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (dbg & 16) {      // settle: long pause before the transposed reads
+      for (int w = 0; w < 200; ++w) __builtin_amdgcn_s_sleep(100);
+      __syncthreads();
+    }
+    const x6_bf16x8 gv = frag(ring + 3 * kWXPlane, offG[0][0], offG[0][1]);
+    const x6_bf16x8 xv = frag(ring, offX[0][0], offX[0][1]);
+    if (blockIdx.x == 0 && tid < 64) {
+      for (int e = 0; e < 8; ++e) {
+        reinterpret_cast<__bf16*>(part)[tid * 16 + e] = gv[e];
+        reinterpret_cast<__bf16*>(part)[tid * 16 + 8 + e] = xv[e];
+      }
+      part[1024 + tid] = (float)offX[0][0];
+      part[1088 + tid] = (float)offX[0][1];
+      part[1152 + tid] = (float)(unsigned)(uintptr_t)(ring + offX[0][0]);
+      part[1216 + tid] = (float)(unsigned)(uintptr_t)(ring);
+      const x6_bf16x4 pl = *reinterpret_cast<const DGMC_LDS x6_bf16x4*>(
+          ring + offX[0][0]);
+      for (int e = 0; e < 4; ++e) part[1280 + 4 * tid + e] = (float)pl[e];
+    }
+    return;
+  }
+  if (dbg & 4) {        // diagnostic: dump stage 0 (6 plane images) + exit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (blockIdx.x == 0)
+      for (int e = tid; e < kWXStage; e += 256)
+        reinterpret_cast<__bf16*>(part)[e] = ring[e];
+    return;
+  }
+  for (int q = 0; q < total; ++q) {
+    if (q + kWXNst - 1 < total) {
+      stage(q + kWXNst - 1, ring + ((q + kWXNst - 1) % kWXNst) * kWXStage);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    x6_barrier();
+    compute(ring + (q % kWXNst) * kWXStage);
+    x6_barrier();
+  }
+  // acc[a][b]: rows c = wn 64 + 32 a + 8 qd + 4 h + e, column i = wm 64 +
+  // 32 b + l32 (the dW^T layout of slot_wgrad2_kernel).
+  const int l32 = lane & 31, h = lane >> 5;
+  float* outp = part + (size_t)item * Kin * C;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float* row = outp + (size_t)(i0 + wm * 64 + b * 32 + l32) * C + n0 +
+                   wn * 64 + a * 32 + 4 * h;
+#pragma unroll
+      for (int qd = 0; qd < 4; ++qd)
+        *reinterpret_cast<float4*>(row + 8 * qd) = make_float4(
+            acc[a][b][4 * qd] + acs[a][b][4 * qd],
+            acc[a][b][4 * qd + 1] + acs[a][b][4 * qd + 1],
+            acc[a][b][4 * qd + 2] + acs[a][b][4 * qd + 2],
+            acc[a][b][4 * qd + 3] + acs[a][b][4 * qd + 3]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host wrappers
+// ---------------------------------------------------------------------------
+at::Tensor split3(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 2 &&
+                  x.stride(1) == 1 && x.size(1) % 4 == 0 &&
+                  x.stride(0) % 4 == 0 && aligned16(x.data_ptr()),
+              "split3: fp32 [R, K % 4] with 16-B aligned rows");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t R = x.size(0), K = x.size(1);
+  at::Tensor out = at::empty({3, R, K}, x.options().dtype(at::kBFloat16));
+  const int64_t n = R * (K / 4);
+  if (n == 0) return out;
+  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, stream(), x.data_ptr<float>(), R, (int)K,
+                     x.stride(0),
+                     reinterpret_cast<__bf16*>(out.data_ptr()));
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+at::Tensor slot_weight_x3(const at::Tensor& weight,
+                          const c10::optional<at::Tensor>& root,
+                          bool transpose) {
+  TORCH_CHECK(weight.is_cuda() && weight.scalar_type() == at::kFloat &&
+                  weight.is_contiguous() && weight.dim() == 3,
+              "slot_weight_x3: fp32 weight [K, in, out]");
+  const bool has_root = root.has_value() && root->defined();
+  const int64_t nw = weight.size(0), in = weight.size(1), out = weight.size(2);
+  if (has_root)
+    TORCH_CHECK(root->scalar_type() == at::kFloat && root->is_contiguous() &&
+                    root->size(0) == in && root->size(1) == out,
+                "slot_weight_x3: root [in, out]");
+  TORCH_CHECK(in % 4 == 0 && out % 4 == 0, "slot_weight_x3: in/out % 4");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(weight.device());
+  const int64_t S = nw + (has_root ? 1 : 0);
+  const int64_t Nn = transpose ? out : in, K = transpose ? in : out;
+  at::Tensor img =
+      at::empty({3, S, Nn, K}, weight.options().dtype(at::kBFloat16));
+  const int64_t n = S * Nn * (K / 4);
+  if (n == 0) return img;
+  const float* rp = has_root ? root->data_ptr<float>() : nullptr;
+  auto kern = transpose ? weight_x3_kernel<true> : weight_x3_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     stream(), weight.data_ptr<float>(), rp, (int)nw, (int)in,
+                     (int)out, reinterpret_cast<__bf16*>(img.data_ptr()),
+                     S * Nn * K);
+  DGMC_CHECK_LAUNCH();
+  return img;
+}
+
+// DGMC_X6_DEBUG (diagnostic ablations, never set in production runs):
+// bit 0 skips the MFMAs, bit 1 the operand DMAs.
+static int x6_debug() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGMC_X6_DEBUG");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
+                        const at::Tensor& seg, const at::Tensor& b3,
+                        bool gather, const c10::optional<at::Tensor>& tiles) {
+  TORCH_CHECK(a3.is_cuda() && a3.scalar_type() == at::kBFloat16 &&
+                  a3.is_contiguous() && a3.dim() == 3 && a3.size(0) == 3,
+              "slot_gemm_x6: bf16 A planes [3, R, K]");
+  TORCH_CHECK(b3.scalar_type() == at::kBFloat16 && b3.is_contiguous() &&
+                  b3.dim() == 4 && b3.size(0) == 3,
+              "slot_gemm_x6: bf16 B planes [3, S, Nn, K]");
+  const int64_t S = seg.numel() - 1;
+  const int64_t Nn = b3.size(2), K = b3.size(3);
+  TORCH_CHECK(b3.size(1) == S && S <= kX6MaxS, "slot_gemm_x6: slot count");
+  TORCH_CHECK(a3.size(2) == K, "slot_gemm_x6: A [*, K]");
+  TORCH_CHECK(K % 128 == 0 && Nn % kX6BN == 0,
+              "slot_gemm_x6: K, Nn multiples of 128");
+  const int64_t P = src.numel();
+  TORCH_CHECK(P % kXBM == 0 && src.scalar_type() == at::kInt &&
+                  seg.scalar_type() == at::kInt,
+              "slot_gemm_x6: int32 src [P_cap % 256], seg");
+  if (!gather) TORCH_CHECK(a3.size(1) == P, "slot_gemm_x6: rows == P_cap");
+  const bool listed = tiles.has_value() && tiles->defined();
+  if (listed)
+    TORCH_CHECK(tiles->scalar_type() == at::kInt &&
+                    tiles->numel() == P / kXBM + 1,
+                "slot_gemm_x6: 256-row tile list [P_cap / 256 + 1] (count "
+                "last)");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(a3.device());
+  at::Tensor Y = at::empty({P, Nn}, a3.options().dtype(at::kFloat));
+  const int64_t tiles_max = (P / kXBM) * (Nn / kX6BN);
+  const int64_t blocks = std::min<int64_t>(
+      tiles_max, (int64_t)x6_num_cus(a3.device().index()));
+  if (blocks == 0) return Y;
+  const __bf16* ap = reinterpret_cast<const __bf16*>(a3.data_ptr());
+  const __bf16* bp = reinterpret_cast<const __bf16*>(b3.data_ptr());
+  const int* tl = listed ? tiles->data_ptr<int>() : nullptr;
+  auto kern = gather ? slot_gemm_x6_kernel<true> : slot_gemm_x6_kernel<false>;
+  DGMC_CHECK_HIP(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(kern),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kXThreads), kXLds, stream(), ap,
+                     a3.size(1) * K, src.data_ptr<int>(), seg.data_ptr<int>(),
+                     (int)S, bp, S * Nn * K, (int)K, (int)Nn, tl,
+                     (int)(P / kXBM), Y.data_ptr<float>(), x6_debug());
+  DGMC_CHECK_LAUNCH();
+  return Y;
+}
+
+std::vector<at::Tensor> slot_wgrad_items(const at::Tensor& seg, int64_t nu,
+                                         int64_t target, int64_t qcap,
+                                         int64_t G_cap, int64_t rows);
+at::Tensor slot_fold_parts(const at::Tensor& part, const at::Tensor& ib,
+                           int64_t S, int64_t Kin, int64_t C);
+
+// dW [S, Kin, C] = sum_u X_u[src]^T dY_u per slot, operands as bf16 planes:
+// xs[u] [3, N, Kin], gs[u] [3, P_cap, C].  `rounds`: rounds of resident
+// workgroups the items are sized for (as slot_wgrad_f32).
+at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
+                         const at::Tensor& src, const at::Tensor& seg,
+                         int64_t rounds) {
+  const int64_t nu = (int64_t)xs.size();
+  TORCH_CHECK(nu >= 1 && nu <= kWXMaxU && (int64_t)gs.size() == nu,
+              "slot_wgrad_x6: 1 <= uses <= 16, one dY per X");
+  const int64_t N = xs[0].size(1), Kin = xs[0].size(2), C = gs[0].size(2);
+  const int64_t P = src.numel(), S = seg.numel() - 1;
+  TORCH_CHECK(Kin % 128 == 0 && C % 128 == 0 && P % kWXRows == 0 &&
+                  rounds >= 1 && S <= kX6MaxS && src.scalar_type() == at::kInt,
+              "slot_wgrad_x6: in / out multiples of 128");
+  X6Uses U{};
+  for (int64_t u = 0; u < nu; ++u) {
+    const at::Tensor& x = xs[u];
+    const at::Tensor& g = gs[u];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 &&
+                    x.is_contiguous() && x.dim() == 3 && x.size(0) == 3 &&
+                    x.size(1) == N && x.size(2) == Kin,
+                "slot_wgrad_x6: X_u bf16 planes [3, N, in]");
+    TORCH_CHECK(g.scalar_type() == at::kBFloat16 && g.is_contiguous() &&
+                    g.dim() == 3 && g.size(0) == 3 && g.size(1) == P &&
+                    g.size(2) == C,
+                "slot_wgrad_x6: dY_u bf16 planes [3, P_cap, out]");
+    U.x[u] = reinterpret_cast<const __bf16*>(x.data_ptr());
+    U.g[u] = reinterpret_cast<const __bf16*>(g.data_ptr());
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  const int64_t tiles = (Kin / 128) * (C / 128);
+  const int64_t target = std::max<int64_t>(
+      1, rounds * 2 * (int64_t)x6_num_cus(src.device().index()) / tiles);
+  const int64_t qcap = (kWXMaxRows / kWXRows - 2) * nu;
+  const int64_t G_cap = target + (P / kWXRows * nu + qcap - 1) / qcap + S;
+  auto it = slot_wgrad_items(seg, nu, target, qcap, G_cap, kWXRows);
+  const int64_t per = Kin * C;
+  at::Tensor part =
+      at::empty({G_cap, per}, xs[0].options().dtype(at::kFloat));
+  DGMC_CHECK_HIP(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(slot_wgrad_x6_kernel),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWXLds));
+  hipLaunchKernelGGL(slot_wgrad_x6_kernel, dim3(G_cap * tiles), dim3(256),
+                     kWXLds, stream(), U, (int)nu, N * Kin, P * C,
+                     src.data_ptr<int>(), seg.data_ptr<int>(),
+                     it[0].data_ptr<int>(), (int)Kin, (int)C,
+                     part.data_ptr<float>(), x6_debug());
+  if (x6_debug() & 12) return part;
+  DGMC_CHECK_LAUNCH();
+  return slot_fold_parts(part, it[1], S, Kin, C);
+}
+
+}  // namespace dgmc

@@ -30,9 +30,15 @@ from . import _backend
 from ..runtime.cache import cached
 from .gemm import col_partial_rows, loop_col_total
 
-BM = 128                      # compact segment / tile unit (slot_gemm.hip)
+BM = 128                      # compact tile unit (slot_gemm.hip)
+SEG = 256                     # slot segment alignment (256-row x6 tiles)
 MAX_USES = 16                 # pointer table of slot_wgrad_f32
 ENABLED = os.environ.get('DGMC_AMD_SLOT_GEMM', '1') == '1'
+# fp32 products on the bf16 matrix cores ("bf16x6", csrc/hip/slot_gemm_x6.hip):
+# every operand split into three bf16 terms, six products, two fp32
+# accumulators - max error vs fp64 BELOW the exact-f32 MFMA kernels on every
+# headline shape (tests/test_slot_gemm_x6.py).
+X6 = os.environ.get('DGMC_AMD_X6', '0') == '1'
 
 
 class CompactPlan(object):
@@ -42,20 +48,21 @@ class CompactPlan(object):
         N = op.num_cols // S
         ncols = op.num_cols
         cap = op.col.numel()
-        P_cap = (min(cap, ncols) + S * BM + BM - 1) // BM * BM
+        P_cap = (min(cap, ncols) + S * SEG + SEG - 1) // SEG * SEG
         (self.src, self.seg, self.col_c, self.posmap, self.cinv,
          self.counts) = _backend.ops().slot_compact_plan(
              op.rowptr, op.col, N, S, P_cap)
         self.S, self.N, self.P_cap = S, N, P_cap
 
 
-def dx_tiles(plan, row0):
-    """Row-tile list of the dX pass for sources ``j >= row0`` (cached)."""
+def dx_tiles(plan, row0, unit=BM):
+    """Row-tile list (``unit``-row tiles) of the dX pass for sources
+    ``j >= row0`` (cached)."""
     cache = plan.__dict__.setdefault('_dx_tiles', {})
-    t = cache.get(row0)
+    t = cache.get((row0, unit))
     if t is None:
-        t = cache[row0] = _backend.ops().slot_dx_tiles(
-            plan.posmap, plan.seg, plan.N, row0, plan.P_cap)
+        t = cache[(row0, unit)] = _backend.ops().slot_dx_tiles(
+            plan.posmap, plan.seg, plan.N, row0, plan.P_cap, unit)
     return t
 
 
@@ -112,6 +119,33 @@ def weight_grad(xs, dys, plan, cin, cout):
     return out
 
 
+def weight_grad_x6(x3s, dy3s, plan, cin, cout):
+    """:func:`weight_grad` on bf16x6 operand planes (``[3, N, in]`` /
+    ``[3, P_cap, out]``)."""
+    ops = _backend.ops()
+    tiles = (cin // 128) * (cout // 128)
+    rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
+    out = None
+    for i in range(0, len(x3s), MAX_USES):
+        part = ops.slot_wgrad_x6(list(x3s[i:i + MAX_USES]),
+                                 list(dy3s[i:i + MAX_USES]), plan.src,
+                                 plan.seg, rounds)
+        out = part if out is None else out.add_(part)
+    return out
+
+
+def _x6_images(weight, root):
+    """bf16x6 weight images of the forward (W^T) and the input gradient (W),
+    built once per forward scope and shared by the consensus loop's uses."""
+    ops = _backend.ops()
+    w = weight.detach().contiguous()
+    r = root.detach().contiguous() if root is not None else None
+    return (cached(('slot_wt3', id(weight)),
+                   lambda: ops.slot_weight_x3(w, r, True)),
+            cached(('slot_w3', id(weight)),
+                   lambda: ops.slot_weight_x3(w, r, False)))
+
+
 class _SlotGemmSpMM(torch.autograd.Function):
 
     @staticmethod
@@ -121,12 +155,20 @@ class _SlotGemmSpMM(torch.autograd.Function):
         plan = compact_plan(op, S)
         xc = x.contiguous()
         ops = _backend.ops()
-        # W^T images [S, out, in] (k-contiguous B operand), built once per
-        # forward scope and shared by the consensus loop's uses.
-        wt = cached(('slot_wt', id(weight)), lambda: ops.slot_weight_t(
-            weight.detach().contiguous(),
-            root.detach().contiguous() if root is not None else None))
-        Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
+        ctx.x6 = X6
+        if X6:
+            # bf16x6: X split once (the planes are also the weight
+            # gradient's operand), weight images once per forward scope.
+            wt3, ctx.w3 = _x6_images(weight, root)
+            xc = ops.split3(xc)
+            Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
+        else:
+            # W^T images [S, out, in] (k-contiguous B operand), built once
+            # per forward scope and shared by the consensus loop's uses.
+            wt = cached(('slot_wt', id(weight)), lambda: ops.slot_weight_t(
+                weight.detach().contiguous(),
+                root.detach().contiguous() if root is not None else None))
+            Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
         out = ops.spmm_csr(op.rowptr, plan.col_c, op.val, Y, None, None,
                            bias, relu, torch.float32)
         ctx.save_for_backward(xc, weight, root, out if relu else None)
@@ -157,9 +199,26 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                   torch.float32, None, False, part)
         At = op.t()
         dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
-                                    plan.seg, rowmap_ranges(plan, At))
+                                    plan.seg, rowmap_ranges(plan, At),
+                                    ctx.x6)
         gx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and ctx.x6:
+            # dY_c planes straight from the rowmap SpMM; 256-row tiles of
+            # the sources >= dx_row0 only.
+            row0 = ctx.dx_row0
+            Z = ops.slot_gemm_x6(dyc, plan.src, plan.seg, ctx.w3, False,
+                                 dx_tiles(plan, row0, SEG) if row0 > 0
+                                 else None)
+            add = gpass if (gpass is not None and
+                            gpass.dtype == torch.float32 and gpass.dim() == 2
+                            and gpass.stride(1) == 1 and
+                            gpass.stride(0) % 4 == 0 and
+                            gpass.data_ptr() % 16 == 0) else None
+            gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add,
+                                     row0)
+            if gpass is not None and add is None:
+                gx = gx + gpass
+        elif ctx.needs_input_grad[0]:
             # K = 128 (psi_2): the register-staged v1 kernel streams dY_c
             # faster than the LDS-DMA one (51 vs 57 us per call,
             # tools/bench_slot_gemm.py); longer K: v2.  Rows below
@@ -188,9 +247,10 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                              ctx.needs_input_grad[2])
         cin, cout = weight.size(1), weight.size(2)
         gw = gr = gb = None
+        wgrad = weight_grad_x6 if ctx.x6 else weight_grad
         if loop is None:
             if need_w:
-                dW = weight_grad([x], [dyc], plan, cin, cout)
+                dW = wgrad([x], [dyc], plan, cin, cout)
             if need_b:
                 gb = db.to(ctx.bias_dtype)
         else:
@@ -200,8 +260,8 @@ class _SlotGemmSpMM(torch.autograd.Function):
             if not loop.arrive():
                 return (gx, None, None, None) + nones
             if need_w:
-                dW = weight_grad(loop.kept_list('x'), loop.kept_list('dy'),
-                                 plan, cin, cout)
+                dW = wgrad(loop.kept_list('x'), loop.kept_list('dy'), plan,
+                           cin, cout)
             if need_b:
                 gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
             loop.release()

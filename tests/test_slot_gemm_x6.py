@@ -1,0 +1,216 @@
+"""bf16x6 slot GEMM (csrc/hip/slot_gemm_x6.hip) at the headline shapes.
+
+The gate for making it the default fp32 path ("bf16x6"): on
+every headline GEMM shape - psi_1 1024->256 and 256->256, psi_2 128->128,
+forward (gathered X W_s) and input gradient (dY_c W_s^T) - the max error
+against an fp64 oracle must not exceed that of the exact-f32 MFMA kernel
+(``slot_gemm2`` / ``slot_gemm``, a k-ordered fmaf chain) on the same
+inputs.  The operator is the PascalVOC-shaped static training batch of the
+benchmark (512 pairs, union of source and target graphs, ~10k nodes).
+"""
+import pytest
+import torch
+
+from deep_graph_matching_consensus_amd.ops import _backend
+from deep_graph_matching_consensus_amd.ops import slot_gemm as sg
+from deep_graph_matching_consensus_amd.ops.plans import spline_plan
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def headline_plan():
+    from deep_graph_matching_consensus_amd.datasets import (
+        PASCAL_VOC_CATEGORIES, GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    assert _backend.hip_available()
+    groups = make_keypoint_datasets(PASCAL_VOC_CATEGORIES, graphs=64,
+                                    feature_dim=16, seed=0)
+    store = GraphStore(groups, DEV, valid_pairs=True)
+    b = StaticPairBatcher(store, 512, seed=0)
+    assert b.load()
+    b.materialize()
+    N = b.cap_s + b.cap_t
+    op = spline_plan(b.v['ei'], b.v['ea_val'], N, (5, 5), (1, 1), 1,
+                     root=True)
+    plan = sg.compact_plan(op, 26)
+    return N, plan
+
+
+def _slot_rows(plan):
+    seg = plan.seg.cpu().tolist()
+    src = plan.src.long()
+    return [(s, seg[s], seg[s + 1]) for s in range(len(seg) - 1)], src
+
+
+def _oracle_fwd(plan, x, w, r):
+    """fp64 Y[p] = x[src p] W_{slot p} (rows with src < 0: left at 0)."""
+    W = torch.cat([w, r[None]], 0).double()
+    Y = torch.zeros(plan.src.numel(), w.size(2), dtype=torch.float64,
+                    device=DEV)
+    slots, src = _slot_rows(plan)
+    for s, a, b in slots:
+        rows = src[a:b]
+        ok = rows >= 0
+        Y[a:b][ok] = x.double()[rows[ok]] @ W[s]
+    return Y
+
+
+def _oracle_dx(plan, dy, w, r):
+    """fp64 Z[p] = dY[p] W_{slot p}^T."""
+    W = torch.cat([w, r[None]], 0).double()
+    Z = torch.zeros(dy.size(0), w.size(1), dtype=torch.float64, device=DEV)
+    slots, src = _slot_rows(plan)
+    for s, a, b in slots:
+        Z[a:b] = dy.double()[a:b] @ W[s].t()
+    return Z
+
+
+def _valid(plan):
+    return plan.src.long() >= 0
+
+
+def _err(a, ref, rows):
+    return float((a.double() - ref)[rows].abs().max())
+
+
+@pytest.mark.parametrize('cin,cout', [(128, 128), (256, 256), (1024, 256)])
+def test_x6_forward_error_not_above_exact_f32(headline_plan, cin, cout):
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(cin)
+    x = torch.randn(N, cin, device=DEV, generator=g)
+    w = torch.randn(25, cin, cout, device=DEV, generator=g) / cin ** 0.5
+    r = torch.randn(cin, cout, device=DEV, generator=g) / cin ** 0.5
+    y6 = ops.slot_gemm_x6(ops.split3(x), plan.src, plan.seg,
+                          ops.slot_weight_x3(w, r, True), True, None)
+    y32 = ops.slot_gemm2(x, plan.src, plan.seg, ops.slot_weight_t(w, r),
+                         None, True)
+    ref = _oracle_fwd(plan, x, w, r)
+    rows = _valid(plan)
+    e6, e32 = _err(y6, ref, rows), _err(y32, ref, rows)
+    assert e6 <= e32, (e6, e32)
+    assert e6 < 1e-5 * float(ref[rows].abs().max())
+
+
+@pytest.mark.parametrize('cin,cout', [(128, 128), (256, 256), (1024, 256)])
+def test_x6_input_grad_error_not_above_exact_f32(headline_plan, cin, cout):
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(7 + cin)
+    P = plan.src.numel()
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    w = torch.randn(25, cin, cout, device=DEV, generator=g) / cout ** 0.5
+    r = torch.randn(cin, cout, device=DEV, generator=g) / cout ** 0.5
+    z6 = ops.slot_gemm_x6(ops.split3(dy), plan.src, plan.seg,
+                          ops.slot_weight_x3(w, r, False), False, None)
+    if cout >= 256:
+        z32 = ops.slot_gemm2(dy, plan.src, plan.seg, w.contiguous(),
+                             r.contiguous(), False)
+    else:
+        z32 = ops.slot_gemm(dy, plan.src, plan.seg, w.contiguous(),
+                            r.contiguous(), True, None)
+    ref = _oracle_dx(plan, dy, w, r)
+    rows = torch.zeros(P, dtype=torch.bool, device=DEV)
+    rows[:int(plan.seg[-1])] = True
+    e6, e32 = _err(z6, ref, rows), _err(z32, ref, rows)
+    assert e6 <= e32, (e6, e32)
+
+
+def test_x6_dx_tile_list(headline_plan):
+    """With a row-tile list (psi_2's target-source rows) exactly the listed
+    tiles are computed, equal to the full pass on those rows."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    P = plan.src.numel()
+    dy = torch.randn(P, 128, device=DEV)
+    w = torch.randn(25, 128, 128, device=DEV) / 12
+    r = torch.randn(128, 128, device=DEV) / 12
+    b3 = ops.slot_weight_x3(w, r, False)
+    full = ops.slot_gemm_x6(ops.split3(dy), plan.src, plan.seg, b3, False,
+                            None)
+    tiles = sg.dx_tiles(plan, N // 2, unit=256)
+    part = ops.slot_gemm_x6(ops.split3(dy), plan.src, plan.seg, b3, False,
+                            tiles)
+    cnt = int(tiles[-1])
+    assert 0 < cnt < P // 256
+    for t in tiles[:cnt].tolist():
+        assert torch.equal(part[t * 256:(t + 1) * 256],
+                           full[t * 256:(t + 1) * 256])
+
+
+def test_split3_reconstructs_fp32():
+    ops = _backend.ops()
+    x = torch.randn(1000, 64, device=DEV) * torch.logspace(
+        -20, 20, 64, device=DEV)
+    p = ops.split3(x).double()
+    rec = p[0] + p[1] + p[2]
+    assert float(((rec - x.double()).abs() / x.double().abs()).max()) < 2 ** -24
+
+
+def _oracle_wgrad(plan, xs, dys, S):
+    """fp64 dW[s] = sum_u X_u[src]^T dY_u over slot s's compact rows."""
+    slots, src = _slot_rows(plan)
+    out = []
+    for s, a, b in slots:
+        rows = src[a:b]
+        ok = rows >= 0
+        acc = 0
+        for x, dy in zip(xs, dys):
+            acc = acc + x.double()[rows[ok]].t() @ dy.double()[a:b][ok]
+        out.append(acc)
+    return torch.stack(out)
+
+
+@pytest.mark.parametrize('cin,cout,uses', [(128, 128, 10), (256, 256, 1),
+                                           (1024, 256, 1)])
+def test_x6_weight_grad_error_not_above_exact_f32(headline_plan, cin, cout,
+                                                  uses):
+    """psi_2's 10-use loop gradient and psi_1's two layers."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(11 + cin)
+    P = plan.src.numel()
+    used = int(plan.seg[-1])
+    xs = [torch.randn(N, cin, device=DEV, generator=g) for _ in range(uses)]
+    dys = []
+    for _ in range(uses):
+        d = torch.randn(P, cout, device=DEV, generator=g)
+        d[used:] = 0
+        d[plan.src.long() < 0] = 0           # padding rows carry no gradient
+        dys.append(d)
+    rounds = 1 if cin == 128 else (2 if cin == 256 else 6)
+    w6 = ops.slot_wgrad_x6([ops.split3(x) for x in xs],
+                           [ops.split3(d) for d in dys], plan.src, plan.seg,
+                           rounds)
+    w32 = ops.slot_wgrad_f32(xs, dys, plan.src, plan.seg, rounds)
+    ref = _oracle_wgrad(plan, xs, dys, 26)
+    e6 = float((w6.double() - ref).abs().max())
+    e32 = float((w32.double() - ref).abs().max())
+    assert e6 <= e32, (e6, e32)
+
+
+def test_rowmap_planes_equal_split_of_fp32(headline_plan):
+    """The row-mapped SpMM's bf16x6 plane output is exactly split3 of its
+    fp32 output on every row the consumers read (rows < seg[S])."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.randn(N, 128, device=DEV)
+    # any CSR over N*S columns works for the kernel: a random sparse A^T
+    R = N * 26
+    gen = torch.Generator().manual_seed(3)
+    nnz = 4 * N
+    rows = torch.randint(R, (nnz, ), generator=gen).sort()[0]
+    rowptr = torch.zeros(R + 1, dtype=torch.long)
+    rowptr[1:] = torch.bincount(rows, minlength=R).cumsum(0)
+    col = torch.randint(N, (nnz, ), generator=gen).int()
+    val = torch.rand(nnz, generator=gen)
+    rowptr, col, val = rowptr.int().to(DEV), col.to(DEV), val.to(DEV)
+    f32 = ops.slot_spmm_rowmap(rowptr, col, val, plan.cinv, g, plan.seg,
+                               None, False)
+    p3 = ops.slot_spmm_rowmap(rowptr, col, val, plan.cinv, g, plan.seg,
+                              None, True)
+    used = int(plan.seg[-1])
+    assert torch.equal(p3[:, :used], ops.split3(f32)[:, :used])
