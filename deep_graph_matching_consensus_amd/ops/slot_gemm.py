@@ -38,7 +38,7 @@ ENABLED = os.environ.get('DGMC_AMD_SLOT_GEMM', '1') == '1'
 # every operand split into three bf16 terms, six products, two fp32
 # accumulators - max error vs fp64 BELOW the exact-f32 MFMA kernels on every
 # headline shape (tests/test_slot_gemm_x6.py).
-X6 = os.environ.get('DGMC_AMD_X6', '0') == '1'
+X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
 
 
 class CompactPlan(object):

@@ -83,7 +83,7 @@ def _pair_trainer(store, mode, seed_model=0):
     # (graph mode: the store lives on the GPU)
     torch.manual_seed(seed_model)
     model = DGMC(SplineCNN(16, 16, 2, 2, cat=False, dropout=0.5),
-                 SplineCNN(8, 8, 2, 2, cat=True), num_steps=2)
+                 SplineCNN(8, 8, 2, 2, cat=True), num_steps=2).to(store.device)
     return PairTrainer(model, store, 8, mode=mode, bf16=False, seed=3)
 
 

@@ -77,12 +77,10 @@ def main():
         rec['fwd_x6_us'] = timeit(lambda: ops.slot_gemm_x6(
             x3, plan.src, plan.seg, wt3, True, None), args.reps)
         rec['split_x_us'] = timeit(lambda: ops.split3(x), args.reps)
-        if cout >= 256:
-            f32dx = lambda: ops.slot_gemm2(dy, plan.src, plan.seg, w, r,  # noqa
-                                           False)
-        else:
-            f32dx = lambda: ops.slot_gemm(dy, plan.src, plan.seg, w, r,  # noqa
-                                          True, None)
+        def f32dx():
+            if cout >= 256:
+                return ops.slot_gemm2(dy, plan.src, plan.seg, w, r, False)
+            return ops.slot_gemm(dy, plan.src, plan.seg, w, r, True, None)
         rec['dx_f32_us'] = timeit(f32dx, args.reps)
         rec['dx_x6_us'] = timeit(lambda: ops.slot_gemm_x6(
             dy3, plan.src, plan.seg, w3, False, None), args.reps)

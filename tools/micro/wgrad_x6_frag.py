@@ -28,7 +28,8 @@ for l in (0, 1, 4, 5, 8, 12, 16, 31, 32, 48):
                                        out['col'][l].int().tolist()))
 print('offX[0][0] lanes 0..15:', part.view(-1)[1024:1040].int().tolist())
 print('offX[0][1] lanes 0..15:', part.view(-1)[1088:1104].int().tolist())
-print('tr address bytes lanes 0..15:', part.view(-1)[1152:1168].long().tolist())
+flat = part.view(-1)
+print('tr address bytes lanes 0..15:', flat[1152:1168].long().tolist())
 print('ring base bytes lane 0:', int(part.view(-1)[1216]))
 pl = part.view(-1)[1280:1280 + 256].view(64, 4)
 print('plain 8-B read at each lane address (last run), lanes 0..7:',
