@@ -273,6 +273,22 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
                           int64_t rounds);
+std::vector<at::Tensor> sinkhorn_transport(const at::Tensor& S_hat,
+                                           const at::Tensor& r_s,
+                                           const at::Tensor& ptr_s,
+                                           const at::Tensor& ptr_t,
+                                           int64_t rows_t, int64_t iters,
+                                           double tau, bool with_prob);
+at::Tensor sinkhorn_transport_bwd(const c10::optional<at::Tensor>& G,
+                                  const at::Tensor& g_joint,
+                                  const at::Tensor& r_s,
+                                  const at::Tensor& S_hat,
+                                  const at::Tensor& ptr_s,
+                                  const at::Tensor& ptr_t,
+                                  const at::Tensor& a_hist,
+                                  const at::Tensor& b_hist, int64_t iters,
+                                  double tau,
+                                  const c10::optional<at::Tensor>& add);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
     const at::Tensor& S_hat, const at::Tensor& n_s, const at::Tensor& n_t,
     int64_t iters, double tau);
@@ -488,6 +504,13 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "sinkhorn_bwd(Tensor grad, Tensor S_hat, Tensor n_s, Tensor n_t, Tensor "
       "a_hist, Tensor b_hist, int iters, float tau) -> Tensor");
+  m.def(
+      "sinkhorn_transport(Tensor S_hat, Tensor r_s, Tensor ptr_s, Tensor "
+      "ptr_t, int rows_t, int iters, float tau, bool with_prob) -> Tensor[]");
+  m.def(
+      "sinkhorn_transport_bwd(Tensor? grad_P, Tensor grad_joint, Tensor r_s, "
+      "Tensor S_hat, Tensor ptr_s, Tensor ptr_t, Tensor a_hist, Tensor "
+      "b_hist, int iters, float tau, Tensor? add) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
@@ -566,4 +589,6 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);
   m.impl("sinkhorn_fwd", &dgmc::sinkhorn_fwd);
   m.impl("sinkhorn_bwd", &dgmc::sinkhorn_bwd);
+  m.impl("sinkhorn_transport", &dgmc::sinkhorn_transport);
+  m.impl("sinkhorn_transport_bwd", &dgmc::sinkhorn_transport_bwd);
 }

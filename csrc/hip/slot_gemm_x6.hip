@@ -194,7 +194,41 @@ __device__ __forceinline__ int x6_qswz(int r) {
   return (((r >> 2) & 1) ^ b4) | ((((r >> 3) & 1) ^ b4) << 1);
 }
 
-template <bool GATHER>
+// XCD-local 256-row units of the compact row space (as slot_gemm.hip's
+// sg_xcd_unit): slot segments list their rows in source-node order, so the
+// x-th eighth of every segment covers about the x-th eighth of the nodes.
+// Returns the first row of XCD x's i-th unit (-1 past the end) and, in
+// *total, XCD x's unit count.  Wave-wide (lane s holds slot s).
+__device__ __forceinline__ int x6_xcd_unit(const int* __restrict__ seg, int S,
+                                           int x, int i, int* total) {
+  const int lane = threadIdx.x & 63;
+  const int sv = lane <= S ? seg[lane] : 0;
+  const int sn = __shfl_down(sv, 1);
+  int lo = 0, cnt = 0;
+  if (lane < S) {
+    const int q = (sn - sv) / kXBM;
+    lo = q * x / kNumXcd;
+    cnt = q * (x + 1) / kNumXcd - lo;
+  }
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  *total = __shfl(incl, S - 1);
+  const unsigned long long hit = __ballot(lane < S && incl > i);
+  if (hit == 0ull) return -1;
+  const int sl = __ffsll((long long)hit) - 1;
+  const int base = __shfl(sv, sl), first = __shfl(lo, sl),
+            before = __shfl(incl - cnt, sl);
+  return base + (first + i - before) * kXBM;
+}
+
+// XL (forward, K <= 256): workgroup b works on XCD b % 8's node eighth of
+// every slot, so the X rows it gathers (<= 1 / 8 of X) stay in that XCD's
+// L2 (grid = a multiple of 8, dispatched round-robin over the XCDs).
+template <bool GATHER, bool XL>
 __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     const __bf16* __restrict__ A, int64_t a_plane, const int* __restrict__ src,
     const int* __restrict__ seg, int S, const __bf16* __restrict__ B,
@@ -209,12 +243,13 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   const int ntn = Nn / kX6BN, nk = K / kXBK;
   // Segment starts in lane registers: slot(m) = #{1 <= s < S: seg[s] <= m}.
   const int segv = lane <= S ? seg[lane] : 0x7fffffff;
-  const int nrt = tiles != nullptr
-                      ? tiles[tcap]
-                      : __builtin_amdgcn_readlane(segv, S) / kXBM;
+  int nrt = tiles != nullptr ? tiles[tcap]
+                              : __builtin_amdgcn_readlane(segv, S) / kXBM;
+  const int xcd = blockIdx.x % kNumXcd;
+  if (XL) x6_xcd_unit(seg, S, xcd, 0, &nrt);     // this XCD's unit count
   const int U = nrt * ntn;
-  const int G = gridDim.x;
-  const int u0 = xcd_remap(blockIdx.x, G);
+  const int G = XL ? gridDim.x / kNumXcd : gridDim.x;
+  const int u0 = XL ? blockIdx.x / kNumXcd : xcd_remap(blockIdx.x, G);
   if (u0 >= U) return;
   const int my_tiles = (U - u0 + G - 1) / G;
   const int total = my_tiles * nk;
@@ -223,6 +258,10 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   };
   auto row_tile = [&](int j) {          // j-th tile of this workgroup
     const int q = (u0 + j * G) / ntn;
+    if (XL) {
+      int dummy;
+      return x6_xcd_unit(seg, S, xcd, q, &dummy) / kXBM;
+    }
     return tiles != nullptr ? tiles[q] : q;
   };
   auto col_tile = [&](int j) { return (u0 + j * G) % ntn; };
@@ -650,6 +689,17 @@ at::Tensor slot_weight_x3(const at::Tensor& weight,
   return img;
 }
 
+// Largest K of the XCD-local forward mapping (DGMC_X6_XL_KMAX, default 256;
+// 0 disables it).
+static int x6_xl_kmax() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGMC_X6_XL_KMAX");
+    v = e ? atoi(e) : 256;
+  }
+  return v;
+}
+
 // DGMC_X6_DEBUG (diagnostic ablations, never set in production runs):
 // bit 0 skips the MFMAs, bit 1 the operand DMAs.
 static int x6_debug() {
@@ -696,11 +746,17 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   const __bf16* ap = reinterpret_cast<const __bf16*>(a3.data_ptr());
   const __bf16* bp = reinterpret_cast<const __bf16*>(b3.data_ptr());
   const int* tl = listed ? tiles->data_ptr<int>() : nullptr;
-  auto kern = gather ? slot_gemm_x6_kernel<true> : slot_gemm_x6_kernel<false>;
+  // XCD-local forward tiles where the gathered X (and the weights) fit the
+  // XCDs' L2s (K <= 256); the 1024-wide psi_1 layer streams.
+  const bool xl = gather && !listed && K <= x6_xl_kmax() && blocks >= 64;
+  auto kern = gather ? (xl ? slot_gemm_x6_kernel<true, true>
+                           : slot_gemm_x6_kernel<true, false>)
+                     : slot_gemm_x6_kernel<false, false>;
+  const int64_t grid = xl ? blocks / kNumXcd * kNumXcd : blocks;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kXThreads), kXLds, stream(), ap,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kXThreads), kXLds, stream(), ap,
                      a3.size(1) * K, src.data_ptr<int>(), seg.data_ptr<int>(),
                      (int)S, bp, S * Nn * K, (int)K, (int)Nn, tl,
                      (int)(P / kXBM), Y.data_ptr<float>(), x6_debug());

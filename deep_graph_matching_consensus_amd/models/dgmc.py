@@ -45,6 +45,9 @@ from .encoder import CatParts, StackedEncoder
 
 # DGMC_AMD_FOLD_PROJECTION=0 keeps psi_2's final Linear as its own GEMM.
 FOLD_PROJECTION = os.environ.get('DGMC_AMD_FOLD_PROJECTION', '1') == '1'
+# DGMC_AMD_SINKHORN_FUSED=0 runs the Sinkhorn consensus loop unfused
+# (separate normalisation kernel + batched-GEMM transport).
+SINKHORN_FUSED = os.environ.get('DGMC_AMD_SINKHORN_FUSED', '1') == '1'
 
 EPS = 1e-8
 _PAIR_CACHE = _IdentityCache(max_entries=8)
@@ -312,8 +315,7 @@ class DGMC(torch.nn.Module):
                 else torch.float32
             # Dense path on the GPU: S_hat straight from the packed joint
             # encoder output (one per-pair kernel, no padded copies).
-            h_joint = _cat_rows(h_s, h_t) if self.k < 1 and \
-                self.normalization == 'softmax' else None
+            h_joint = _cat_rows(h_s, h_t) if self.k < 1 else None
             direct = h_joint is not None and h_joint.data_ptr() == \
                 h_s.data_ptr() and dense_ops.pair_scores_supported(
                     h_joint, lay_s, lay_t)
@@ -363,8 +365,13 @@ class DGMC(torch.nn.Module):
 
             if self.k < 1 and self.normalization == 'sinkhorn':
                 # ---------- dense variant, Sinkhorn (extension) ---------- #
-                return self._dense_sinkhorn(hs, ht, r_all, steps, lay_s,
-                                            lay_t, refine)
+                if direct:
+                    S_hat = dense_ops.pair_scores(h_joint, h_s.size(0),
+                                                  lay_s, lay_t)
+                else:
+                    S_hat = hs @ ht.transpose(-1, -2)
+                return self._dense_sinkhorn(S_hat, r_all, steps, lay_s,
+                                            lay_t, refine, pair)
             assert self.normalization == 'softmax', \
                 'Sinkhorn normalisation is only defined for k=-1 (dense)'
             if self.k < 1:
@@ -400,20 +407,7 @@ class DGMC(torch.nn.Module):
                 # node-level GEMM per step instead of two (forward and
                 # backward); the fold's weight gradient flows through the
                 # tiny W1 W_f product once per step.
-                fold = None
-                if joint and self._foldable():
-                    # (b_f's exact gradient is zero; it stays in the graph
-                    # for autograd.grad / DDP.)
-                    lp = {}
-                    w_fold, wn, wnt = _FoldProduct.apply(
-                        self.mlp[0].weight, self.psi_2.final.weight,
-                        self.psi_2.final.bias)
-                    if wn is not None:
-                        # bf16 operand images from the same kernel
-                        # (ops/dense.py::cat_matmul reads them here).
-                        lp = {'n': wn, 'nt': wnt}
-                    fold = (w_fold.t(), lp, ('fold', id(self.mlp[0].weight)),
-                            steps)
+                fold = self._dense_fold(steps) if joint else None
                 pending = None    # (joint, S_hat) from a fused step boundary
                 for step in range(steps):
                     mark('dgmc.consensus_step')
@@ -541,26 +535,82 @@ class DGMC(torch.nn.Module):
             out.append(S)
         return tuple(out)
 
-    def _dense_sinkhorn(self, hs, ht, r_all, steps, lay_s, lay_t, refine):
+    def _dense_fold(self, steps):
+        """psi_2's final Linear folded into the MLP's first layer (dense
+        path): ``(W1 W_f)^T``, its bf16 operand images, loop key, uses - or
+        None when not foldable."""
+        if not self._foldable():
+            return None
+        # (b_f's exact gradient is zero; it stays in the graph for
+        # autograd.grad / DDP.)
+        lp = {}
+        w_fold, wn, wnt = _FoldProduct.apply(
+            self.mlp[0].weight, self.psi_2.final.weight,
+            self.psi_2.final.bias)
+        if wn is not None:
+            # bf16 operand images from the same kernel
+            # (ops/dense.py::cat_matmul reads them here).
+            lp = {'n': wn, 'nt': wnt}
+        return (w_fold.t(), lp, ('fold', id(self.mlp[0].weight)), steps)
+
+    def _dense_sinkhorn(self, S_hat, r_all, steps, lay_s, lay_t, refine,
+                        pair):
         """Dense path with Sinkhorn normalisation (opt-in extension): the
         same consensus loop with a masked log-domain Sinkhorn (HIP kernel
-        per pair, ``csrc/hip/sinkhorn.hip``) in place of the row softmax;
-        transport ``r_t = S^T r_s`` as a batched GEMM."""
-        def norm(S_hat):
-            return dense_ops.masked_sinkhorn(S_hat, lay_s, lay_t,
-                                             self.sinkhorn_iters)
+        per pair, ``csrc/hip/sinkhorn.hip``) in place of the row softmax.
 
-        S_hat = hs @ ht.transpose(-1, -2)
-        S_0 = lay_s.to_sparse(norm(S_hat))
-        for step in range(steps):
-            r_s = r_all[step]
+        On the GPU each step's normalisation and transport ``r_t = S^T r_s``
+        run as ONE per-pair kernel writing psi_2's joint input ``[r_s; r_t]``
+        (step 0's also emits ``S_0``), whose backward forms
+        ``dL/dS = r_s g_t^T`` itself; psi_2's final Linear is folded into the
+        consensus MLP as on the softmax path.  Elsewhere: the normalisation
+        kernel / oracle and a batched-GEMM transport."""
+        iters = self.sinkhorn_iters
+
+        def norm(S_hat):
+            return dense_ops.masked_sinkhorn(S_hat, lay_s, lay_t, iters)
+
+        fused = (SINKHORN_FUSED and steps > 0 and pair is not None and
+                 self._fusable(self.psi_2) and not is_reference_mode() and
+                 r_all.dtype == torch.float32 and
+                 dense_ops.sinkhorn_transport_supported(S_hat, r_all[0],
+                                                        lay_s, lay_t))
+        if not fused:
             S = norm(S_hat)
-            r_t = lay_t.to_sparse(S.transpose(-1, -2) @
-                                  lay_s.to_dense(r_s.to(S.dtype)))
-            o_s, o_t, o = refine(r_s, r_t.to(r_s.dtype))
-            S_hat = dense_ops.consensus_update(S_hat, o_s, o_t, self.mlp,
-                                               lay_s, lay_t, o_joint=o)
-        return S_0, lay_s.to_sparse(norm(S_hat))
+            S_0 = lay_s.to_sparse(S)
+            for step in range(steps):
+                r_s = r_all[step]
+                if step > 0:
+                    S = norm(S_hat)
+                r_t = lay_t.to_sparse(S.transpose(-1, -2) @
+                                      lay_s.to_dense(r_s.to(S.dtype)))
+                o_s, o_t, o = refine(r_s, r_t.to(r_s.dtype))
+                S_hat = dense_ops.consensus_update(S_hat, o_s, o_t, self.mlp,
+                                                   lay_s, lay_t, o_joint=o)
+            return S_0, lay_s.to_sparse(norm(S_hat))
+
+        fold = self._dense_fold(steps)
+        P0 = None
+        for step in range(steps):
+            mark('dgmc.consensus_step')
+            grad = S_hat.requires_grad and torch.is_grad_enabled()
+            res = dense_ops.sinkhorn_transport_joint(
+                S_hat, r_all[step], lay_s, lay_t, iters,
+                with_prob=step == 0, passthrough=grad)
+            if step == 0 and grad:
+                r_joint, P0, S_hat = res
+            elif step == 0:
+                r_joint, P0 = res
+            elif grad:
+                r_joint, S_hat = res
+            else:
+                r_joint = res
+            o_s, o_t, o = refine(None, None, r_joint,
+                                 features=fold is not None)
+            S_hat = dense_ops.consensus_update(
+                S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o,
+                w1_fold=fold)
+        return lay_s.to_sparse(P0), lay_s.to_sparse(norm(S_hat))
 
     # ------------------------------------------------------------------
     # Objectives and metrics (dgmc.py:246-311)

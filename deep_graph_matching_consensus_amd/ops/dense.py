@@ -239,6 +239,70 @@ def masked_sinkhorn(S_hat, lay_s, lay_t, iters=10, tau=1.0):
     return ref.masked_sinkhorn(S_hat, _count_mask(lay_s, lay_t), iters, tau)
 
 
+class _SinkhornTransportJoint(torch.autograd.Function):
+    """``[r_s; sinkhorn(S_hat)^T r_s]`` (and optionally the normalised
+    ``P`` itself) from one per-pair kernel (csrc/hip/sinkhorn.hip::
+    sinkhorn_transport); the backward forms ``dL/dP = G_P + r_s g_t^T``
+    inside the Sinkhorn backward kernel (plus ``S_hat``'s passthrough
+    gradient) - no batched GEMMs, pack / unpack or gradient adds."""
+
+    @staticmethod
+    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t, iters, tau, with_prob,
+                passthrough):
+        S_hat = S_hat.float().contiguous()
+        r_s = r_s.float().contiguous()
+        joint, P, ah, bh = _backend.ops().sinkhorn_transport(
+            S_hat, r_s, ptr_s, ptr_t, int(rows_t), int(iters), float(tau),
+            bool(with_prob))
+        ctx.save_for_backward(S_hat, r_s, ptr_s, ptr_t, ah, bh)
+        ctx.iters, ctx.tau = int(iters), float(tau)
+        ctx.with_prob, ctx.passthrough = bool(with_prob), bool(passthrough)
+        ctx.joint_shape = tuple(joint.shape)
+        ctx.set_materialize_grads(False)
+        out = (joint, )
+        if with_prob:
+            out = out + (P, )
+        if passthrough:
+            out = out + (S_hat.view_as(S_hat), )
+        return out if len(out) > 1 else joint
+
+    @staticmethod
+    def backward(ctx, gj, *rest):
+        S_hat, r_s, ptr_s, ptr_t, ah, bh = ctx.saved_tensors
+        rest = list(rest)
+        gP = rest.pop(0) if ctx.with_prob else None
+        gpass = rest.pop(0) if ctx.passthrough else None
+        if gj is None:
+            gj = torch.zeros(ctx.joint_shape, device=S_hat.device)
+        dS = _backend.ops().sinkhorn_transport_bwd(
+            None if gP is None else gP.float().contiguous(),
+            gj.float().contiguous(), r_s, S_hat, ptr_s, ptr_t, ah, bh,
+            ctx.iters, ctx.tau,
+            None if gpass is None else gpass.float().contiguous())
+        return (dS, ) + (None, ) * 8
+
+
+def sinkhorn_transport_supported(S_hat, r_s, lay_s, lay_t):
+    B, N_s, N_t = S_hat.shape
+    return (_hip_ok(S_hat, N_s, N_t) and r_s.dim() == 2 and
+            r_s.size(1) in (64, 128, 256) and
+            torch.is_tensor(getattr(lay_s, 'ptr', None)) and
+            torch.is_tensor(getattr(lay_t, 'ptr', None)))
+
+
+def sinkhorn_transport_joint(S_hat, r_s, lay_s, lay_t, iters=10, tau=1.0,
+                             with_prob=False, passthrough=False):
+    r"""``joint = [r_s; masked_sinkhorn(S_hat)^T r_s]`` packed
+    ``[sum N_s + sum N_t, R]`` fp32 (psi_2's fused input), differentiable
+    w.r.t. ``S_hat``.  ``with_prob`` also returns the dense normalised
+    ``P`` (``masked_sinkhorn(S_hat)``); ``passthrough`` an alias of
+    ``S_hat`` whose gradient is summed inside the backward kernel.
+    Returns ``joint`` or the tuple ``(joint[, P][, S_hat'])``."""
+    return _SinkhornTransportJoint.apply(S_hat, r_s, lay_s.ptr, lay_t.ptr,
+                                         lay_t.num_nodes, iters, tau,
+                                         with_prob, passthrough)
+
+
 # ---------------------------------------------------------------------------
 class _SoftmaxTransport(torch.autograd.Function):
     @staticmethod

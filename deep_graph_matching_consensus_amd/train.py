@@ -567,7 +567,8 @@ class KGTrainer(object):
     (``num_steps``/``detach`` setting) is captured once into a hipGraph.
     """
 
-    def __init__(self, model, data, lr=1e-3, graph=True, bf16=False):
+    def __init__(self, model, data, lr=1e-3, graph=True, bf16=False,
+                 guard_nonfinite=True):
         self.model = model
         self.data = data
         self.device = data.x1.device
@@ -579,6 +580,16 @@ class KGTrainer(object):
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda, capturable=self.graph)
         self.last_loss = torch.zeros((), device=self.device)
+        # Non-finite guard as in PairTrainer: a step whose gradients hold a
+        # NaN / Inf skips its update (and step counters) on the device;
+        # ``skipped`` counts them (no host sync, capturable).
+        self.guard = guard_nonfinite
+        self._found_inf = torch.zeros((), dtype=torch.float32,
+                                      device=self.device)
+        self._unit = torch.ones((), dtype=torch.float32, device=self.device)
+        self.skipped = torch.zeros((), dtype=torch.float64, device=self.device)
+        if self.guard and cuda:
+            self.optimizer.found_inf = self._found_inf
         self._graphs = {}
         self.step_count = 0
 
@@ -596,8 +607,28 @@ class KGTrainer(object):
                            d.edge_index2, None, None, d.train_y)
         loss = model.loss(S_L, d.train_y)
         loss.backward()
-        self.optimizer.step()
+        self._update()
         self.last_loss.copy_(loss.detach())
+
+    def _update(self):
+        """Non-finite check over the gradients this phase produced (one
+        multi-tensor kernel) + the HIP multi-tensor Adam reading the flag
+        (runtime/optim.py); stock Adam where that is unsupported."""
+        from .runtime import optim as hip_optim
+        grads = [p.grad for p in self.model.parameters()
+                 if p.grad is not None]
+        if self.guard and grads:
+            self._found_inf.zero_()
+            torch._amp_foreach_non_finite_check_and_unscale_(
+                grads, self._found_inf, self._unit)
+            self.skipped += self._found_inf.double()
+            if self.device.type != 'cuda' and self._found_inf.item() != 0:
+                return                   # CPU Adam has no found_inf input
+        if hip_optim.supported(self.optimizer):
+            hip_optim.hip_adam_step(self.optimizer,
+                                    self._found_inf if self.guard else None)
+            return
+        self.optimizer.step()
 
     def step(self):
         with tuned_gemms(self.device.type == 'cuda'), _gc_paused():
@@ -630,6 +661,7 @@ class KGTrainer(object):
                                     if torch.is_tensor(v)}
                             for p, st in self.optimizer.state.items()},
                     'loss': self.last_loss.clone(),
+                    'skipped': self.skipped.clone(),
                     'cpu_rng': torch.get_rng_state()}
         if self.device.type == 'cuda':
             snap['cuda_rng'] = torch.cuda.get_rng_state(self.device)
@@ -648,6 +680,7 @@ class KGTrainer(object):
                         else:
                             v.zero_()
             self.last_loss.copy_(snap['loss'])
+            self.skipped.copy_(snap['skipped'])
         torch.set_rng_state(snap['cpu_rng'])
         if 'cuda_rng' in snap:
             torch.cuda.set_rng_state(snap['cuda_rng'], self.device)
@@ -706,7 +739,7 @@ class KGTrainer(object):
                            d.edge_index2, None, None, d.train_y)
         loss = model.loss(S_L, d.train_y)
         loss.backward()
-        self.optimizer.step()
+        self._update()
         self.last_loss.copy_(loss.detach())
 
     @torch.no_grad()

@@ -59,3 +59,55 @@ def test_kg_trainer_two_phase_graph_captured_gpu():
     from deep_graph_matching_consensus_amd.ops import _backend
     assert _backend.hip_available()
     _run_schedule(torch.device('cuda'), graph=True)
+
+
+def _guard_case(device, graph):
+    data, model = _setup(device)
+    trainer = KGTrainer(model, data, lr=1e-2, graph=graph)
+    model.num_steps, model.detach = 0, False
+    trainer.step()
+    before = [p.detach().clone() for p in model.parameters()]
+    x = data.x1.clone()
+    data.x1[0, 0] = float("nan")     # in place: the captured step reads it
+    trainer.step()
+    assert float(trainer.skipped) == 1.0
+    for p, q in zip(model.parameters(), before):
+        assert torch.equal(p.detach(), q), 'a non-finite step must not update'
+    data.x1.copy_(x)
+    trainer.step()
+    assert float(trainer.skipped) == 1.0
+    assert any(not torch.equal(p.detach(), q)
+               for p, q in zip(model.parameters(), before))
+
+
+def test_kg_trainer_nonfinite_guard_cpu():
+    _guard_case(torch.device('cpu'), graph=False)
+
+
+@pytest.mark.gpu
+def test_kg_trainer_nonfinite_guard_graph_gpu():
+    from deep_graph_matching_consensus_amd.runtime import optim as hip_optim
+    data, model = _setup(torch.device('cuda'))
+    trainer = KGTrainer(model, data, lr=1e-2, graph=True)
+    assert hip_optim.supported(trainer.optimizer)
+    _guard_case(torch.device('cuda'), graph=True)
+
+
+@pytest.mark.gpu
+def test_kg_trainer_hip_adam_matches_torch_adam():
+    """KGTrainer's HIP multi-tensor Adam follows torch's Adam (eager)."""
+    from deep_graph_matching_consensus_amd.runtime import optim as hip_optim
+    params = {}
+    for enabled in (True, False):
+        hip_optim.ENABLED = enabled
+        try:
+            data, model = _setup(torch.device('cuda'))
+            trainer = KGTrainer(model, data, lr=1e-2, graph=False)
+            model.num_steps, model.detach = 0, False
+            for _ in range(3):
+                trainer.step()
+        finally:
+            hip_optim.ENABLED = True
+        params[enabled] = [p.detach().cpu() for p in model.parameters()]
+    for a, b in zip(params[True], params[False]):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-4)

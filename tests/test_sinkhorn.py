@@ -112,3 +112,102 @@ def test_dgmc_sinkhorn_gpu_matches_cpu():
                                rtol=1e-3)
     for a, b in zip(out['cuda'][1], out['cpu'][1]):
         torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('R,iters', [(64, 10), (128, 5), (256, 0)])
+def test_sinkhorn_transport_kernel_matches_fp64(R, iters):
+    """The fused Sinkhorn + transport kernel (joint ``[r_s; P^T r_s]``,
+    optional ``P``) and its backward (``dL/dP = G_P + r_s g_t^T`` through
+    the Sinkhorn Jacobians, plus a passthrough addend) against fp64
+    autograd of the oracle."""
+    from deep_graph_matching_consensus_amd.ops import _backend
+    assert _backend.hip_available()
+    S_hat, n_s, n_t = _sinkhorn_case(seed=R)
+    B, Ns, Nt = S_hat.shape
+    mask = ref.count_mask(n_s, n_t, Ns, Nt)
+    g = torch.Generator().manual_seed(1)
+    ptr_s = torch.cat([torch.zeros(1, dtype=torch.long), n_s.cumsum(0)])
+    ptr_t = torch.cat([torch.zeros(1, dtype=torch.long), n_t.cumsum(0)])
+    rows_s, rows_t = int(ptr_s[-1]), int(ptr_t[-1])
+    r_s = torch.randn(rows_s, R, generator=g, dtype=torch.float64)
+    Sd = S_hat.double().requires_grad_()
+    P = ref.masked_sinkhorn(Sd, mask, iters, 1.0)
+    r_t = []
+    for b in range(B):
+        blk = P[b, :n_s[b], :n_t[b]]
+        r_t.append(blk.t() @ r_s[ptr_s[b]:ptr_s[b + 1]])
+    joint = torch.cat([r_s] + r_t)
+    gj = torch.randn(rows_s + rows_t, R, generator=g, dtype=torch.float64)
+    gP = torch.randn(B, Ns, Nt, generator=g, dtype=torch.float64)
+    add = torch.randn(B, Ns, Nt, generator=g, dtype=torch.float64)
+    dS_ref, = torch.autograd.grad((joint * gj).sum() + (P * gP).sum(), Sd)
+    dS_ref = dS_ref + add
+    ops = _backend.ops()
+    dev = 'cuda'
+    S = S_hat.to(dev)
+    ps, pt = ptr_s.int().to(dev), ptr_t.int().to(dev)
+    rs = r_s.float().to(dev)
+    out = ops.sinkhorn_transport(S, rs, ps, pt, rows_t, iters, 1.0, True)
+    torch.testing.assert_close(out[0].cpu().double(), joint.detach(),
+                               atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(out[1].cpu().double(), P.detach(), atol=2e-6,
+                               rtol=1e-5)
+    dS = ops.sinkhorn_transport_bwd(gP.float().to(dev), gj.float().to(dev),
+                                    rs, S, ps, pt, out[2], out[3], iters,
+                                    1.0, add.float().to(dev))
+    torch.testing.assert_close(dS.cpu().double(), dS_ref, atol=1e-4,
+                               rtol=1e-4)
+    # without P / addend
+    out2 = ops.sinkhorn_transport(S, rs, ps, pt, rows_t, iters, 1.0, False)
+    assert torch.equal(out2[0], out[0])
+    dS2 = ops.sinkhorn_transport_bwd(None, gj.float().to(dev), rs, S, ps, pt,
+                                     out[2], out[3], iters, 1.0, None)
+    dS2_ref, = torch.autograd.grad((joint * gj).sum(), Sd)
+    torch.testing.assert_close(dS2.cpu().double(), dS2_ref, atol=1e-4,
+                               rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_dgmc_sinkhorn_fused_gpu_matches_cpu():
+    """The fused Sinkhorn consensus loop (R = 64: one kernel per step for
+    normalisation + transport, psi_2's final Linear folded) equals the CPU
+    oracle path: outputs and every parameter gradient."""
+    from deep_graph_matching_consensus_amd.models import dgmc as dgmc_mod
+    assert dgmc_mod.SINKHORN_FUSED
+    groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=1)
+    out = {}
+    for dev in ('cpu', 'cuda'):
+        store = GraphStore(groups, dev)
+        b = next(iter(DevicePairLoader(store, batch_size=6, seed=0)))
+        torch.manual_seed(0)
+        model = DGMC(SplineCNN(16, 32, 2, 2, cat=False),
+                     SplineCNN(64, 32, 2, 2, cat=True), num_steps=3,
+                     normalization='sinkhorn', sinkhorn_iters=6).to(dev)
+        r = torch.randn(3, b.x_s.size(0), 64).to(dev)
+
+        def fake_randn(*a, **k):
+            return r.to(k.get('dtype', r.dtype))
+        orig = torch.randn
+        torch.randn = fake_randn
+        try:
+            S_0, S_L = model(b.x_s, b.edge_index_s, b.edge_attr_s,
+                             b.x_s_batch, b.x_t, b.edge_index_t,
+                             b.edge_attr_t, b.x_t_batch)
+        finally:
+            torch.randn = orig
+        y = torch.stack([torch.arange(b.y.numel(), device=dev), b.y])
+        loss = model.loss(S_0, y) + model.loss(S_L, y)
+        params = [p for p in model.parameters() if p.requires_grad]
+        grads = torch.autograd.grad(loss, params, allow_unused=True)
+        out[dev] = (S_0.detach().cpu(), S_L.detach().cpu(),
+                    [None if g is None else g.cpu() for g in grads])
+    torch.testing.assert_close(out['cuda'][0], out['cpu'][0], atol=1e-4,
+                               rtol=1e-3)
+    torch.testing.assert_close(out['cuda'][1], out['cpu'][1], atol=1e-4,
+                               rtol=1e-3)
+    for a, b in zip(out['cuda'][2], out['cpu'][2]):
+        if a is None or b is None:
+            assert a is None or float(a.abs().max()) == 0
+            continue
+        torch.testing.assert_close(a, b, atol=2e-4, rtol=2e-3)

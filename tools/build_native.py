@@ -108,13 +108,44 @@ def write_ninja(debug=False):
 
 
 def build(jobs=None, debug=False, verbose=False):
+    """Incremental ninja build (gcc-style depfiles track every included
+    header; ninja also rebuilds an object whose command line changed), then
+    a dry run that must report nothing left to do, and a manifest
+    (``build/native/manifest.json``: sha256 of every source and library) of
+    what the libraries were built from."""
     targets = write_ninja(debug)
     jobs = jobs or min(16, os.cpu_count() or 4)
     cmd = ['ninja', '-C', BUILD, '-j', str(jobs)]
     if verbose:
         cmd.append('-v')
     subprocess.check_call(cmd)
+    dry = subprocess.run(['ninja', '-C', BUILD, '-n'], check=True,
+                         capture_output=True, text=True).stdout
+    if 'no work to do' not in dry:
+        raise RuntimeError('native build not up to date after ninja:\n' +
+                           dry)
+    _write_manifest(targets)
     return targets
+
+
+def _sha256(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, 'rb') as f:
+        for chunk in iter(lambda: f.read(1 << 20), b''):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def _write_manifest(targets):
+    import json
+    srcs = sorted(glob.glob(osp.join(ROOT, 'csrc', '*', '*')))
+    man = {'arch': ARCH,
+           'sources': {osp.relpath(p, ROOT): _sha256(p) for p in srcs
+                       if osp.isfile(p)},
+           'libraries': {osp.relpath(t, ROOT): _sha256(t) for t in targets}}
+    with open(osp.join(BUILD, 'manifest.json'), 'w') as f:
+        json.dump(man, f, indent=1, sort_keys=True)
 
 
 def clean():
