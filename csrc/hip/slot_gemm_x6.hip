@@ -689,13 +689,15 @@ at::Tensor slot_weight_x3(const at::Tensor& weight,
   return img;
 }
 
-// Largest K of the XCD-local forward mapping (DGMC_X6_XL_KMAX, default 256;
-// 0 disables it).
+// Largest K of the XCD-local forward mapping (DGMC_X6_XL_KMAX; default 0 =
+// off: measured SLOWER on the headline plan - 128->128 50.5 vs 44.3 us,
+// 256->256 130 vs 111 us, 1024->256 equal; profiles/bench_slot_gemm_x6_xl_r4
+// .json.  The slot-segment order already keeps a W_s image hot in L2).
 static int x6_xl_kmax() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("DGMC_X6_XL_KMAX");
-    v = e ? atoi(e) : 256;
+    v = e ? atoi(e) : 0;
   }
   return v;
 }

@@ -492,12 +492,16 @@ __global__ __launch_bounds__(kRefRows * 64) void topk_refine_kernel(
   const float cv = lane < K2 ? cand_v[o * K2 + lane] : -INFINITY;
   const float Tk = __shfl(cv, k - 1);
   const float lim = Tk - 2.0f * E;
-  const bool overflow = K2 < Nt && __shfl(cv, K2 - 1) >= lim;
+  const bool keep = lane < K2 && cv >= lim;
+  // Fewer than k kept (non-finite scores: NaN compares false) or a possibly
+  // incomplete list -> the exhaustive scan, which always writes k valid
+  // indices.
+  const bool overflow = (K2 < Nt && __shfl(cv, K2 - 1) >= lim) ||
+                        __popcll(__ballot(keep)) < k;
   __builtin_amdgcn_wave_barrier();
   const float* tb = h_t + (size_t)b * Nt * C;
   int64_t* orow = out + o * k;
   if (!overflow) {
-    const bool keep = lane < K2 && cv >= lim;
     const float ev = keep ? exact_dot(a, tb + (size_t)ci * C, C, C8)
                           : -INFINITY;
     // rank by (exact desc, index asc) among the kept candidates

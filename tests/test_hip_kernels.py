@@ -379,6 +379,30 @@ def test_topk_exact_refined_equals_brute_force(case, k):
         assert int(n_over) == 0      # the margin covers random inputs
 
 
+@pytest.mark.parametrize('exact', [True, False])
+def test_topk_nonfinite_rows_give_valid_indices(exact):
+    """Rows (or targets) holding NaN / Inf still produce k in-range indices
+    (the consumers gather with them); finite rows are unaffected."""
+    torch.manual_seed(2)
+    h_s = torch.randn(1, 300, 64, device=DEV)
+    h_t = torch.randn(1, 900, 64, device=DEV)
+    want = sparse_corr.top_k(h_s, h_t, 10, brute_force=True)
+    h_s[0, 5, 0] = float('nan')
+    h_s[0, 6, :] = float('nan')
+    h_s[0, 7, 3] = float('inf')
+    idx = sparse_corr.top_k(h_s, h_t, 10, exact=exact)
+    torch.cuda.synchronize()
+    assert (idx >= 0).all() and (idx < 900).all()
+    ok = torch.ones(300, dtype=torch.bool)
+    ok[5:8] = False
+    if exact:
+        assert torch.equal(idx[0, ok], want[0, ok])
+    h_t[0, 11, 0] = float('nan')
+    idx = sparse_corr.top_k(h_s, h_t, 10, exact=exact)
+    torch.cuda.synchronize()
+    assert (idx >= 0).all() and (idx < 900).all()
+
+
 @pytest.mark.parametrize('Ns,Nt', [(4000, 3000), (200, 5000)])
 def test_topk_dot_split_merge(Ns, Nt):
     """Few source rows -> the target range is split over blocks and the

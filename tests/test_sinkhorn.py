@@ -141,7 +141,8 @@ def test_sinkhorn_transport_kernel_matches_fp64(R, iters):
     gj = torch.randn(rows_s + rows_t, R, generator=g, dtype=torch.float64)
     gP = torch.randn(B, Ns, Nt, generator=g, dtype=torch.float64)
     add = torch.randn(B, Ns, Nt, generator=g, dtype=torch.float64)
-    dS_ref, = torch.autograd.grad((joint * gj).sum() + (P * gP).sum(), Sd)
+    dS_ref, = torch.autograd.grad((joint * gj).sum() + (P * gP).sum(), Sd,
+                                  retain_graph=True)
     dS_ref = dS_ref + add
     ops = _backend.ops()
     dev = 'cuda'
