@@ -61,8 +61,9 @@ def run(impl, args, device):
                               'hits@1': round(h1, 4),
                               'hits@10': round(h10, 4)})
                 print(impl, curve[-1], flush=True)
-    return {'impl': impl, 'dtype': 'fp32', 'wall_s': round(time.time() - t0, 1),
-            'curve': curve, 'hits@1': curve[-1]['hits@1'],
+    return {'impl': impl, 'dtype': 'fp32',
+            'wall_s': round(time.time() - t0, 1), 'curve': curve,
+            'hits@1': curve[-1]['hits@1'],
             'hits@10': curve[-1]['hits@10'], 'raw_nn_hits@1': round(
                 raw_nn_hits1(data), 4)}
 
