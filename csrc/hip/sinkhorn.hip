@@ -1,6 +1,6 @@
 // Masked log-domain Sinkhorn normalisation of the dense correspondence
-// scores, one workgroup per graph pair (opt-in `normalization='sinkhorn'`
-// of DGMC; the reference itself only row-normalises with a masked softmax,
+// scores, one wave per graph pair (opt-in `normalization='sinkhorn'` of
+// DGMC; the reference itself only row-normalises with a masked softmax,
 // /root/reference/dgmc/models/dgmc.py:15-19 - BASELINE.json config 3 names
 // the dense Sinkhorn variant).
 //
@@ -16,187 +16,150 @@
 // rebuilds each half-step's output from them and applies the normalisation
 // Jacobians in reverse:  row step  D_ij -= exp(out_ij) sum_k D_ik,
 //                        column step D_ij -= exp(out_ij) sum_k D_kj.
-// The pair tile lives in LDS (N <= 64).  ONE wave per pair: in a row step
-// lane i owns row i and reduces it sequentially (the tile's odd pitch keeps
-// the lanes' reads of one column conflict-free), in a column step lane j
-// owns column j - no cross-lane reductions, no multi-wave barriers (a
-// half-step is ~20 LDS reads + exps per lane; was one wave-wide LSE per row
-// with 4 waves and a block barrier per half-step: 63 -> see
-// docs/performance.md).  Deterministic, no atomics.
+//
+// Register-resident (N <= 64, compile-time bucket NM in {16, 32, 64}): lane
+// i holds row i of L0 (r[]) and lane j column j (c[]) in VGPRs; the
+// potentials live one per lane (a in lane i, b in lane j) and reach the
+// other lanes by v_readlane (scalar broadcast) - a half-step is NM
+// unrolled sub / max / exp per lane with no LDS traffic and no barrier.
+// The backward keeps D in registers too and switches it between the row and
+// the column layout through a conflict-free LDS transpose (odd pitch).
+// Was: the tile in LDS with a sequential LSE loop per lane (~20 dependent
+// LDS reads per half-step); before that one wave-wide LSE per row with a
+// block barrier per half-step (docs/performance.md).  Deterministic, no
+// atomics.
 #include "common.h"
 
 namespace dgmc {
 
 namespace {
 constexpr int kShMaxN = 64;
-constexpr int kShPitch = kShMaxN + 1;
 
-// LSE_k (row[k * stride] - pot[k]) over k < n (0 for an empty set).
-__device__ __forceinline__ float lse_line(const DGMC_LDS float* row,
-                                          int stride,
-                                          const DGMC_LDS float* pot, int n) {
+__device__ __forceinline__ float sk_rl(float v, int l) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// LSE_k (x[k] - pot of lane k) over k < NM (x = -inf excluded); 0 if empty.
+// n: the wave-uniform valid count (the unrolled loops stop there: the
+// pair's own size, not the bucket's).
+template <int NM>
+__device__ __forceinline__ float sk_lse(const float (&x)[NM], float pot,
+                                        int n) {
+  float t[NM];
   float m = -INFINITY;
-  for (int k = 0; k < n; ++k) m = fmaxf(m, row[k * stride] - pot[k]);
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    if (k >= n) break;
+    t[k] = x[k] - sk_rl(pot, k);
+    m = fmaxf(m, t[k]);
+  }
   if (m == -INFINITY) return 0.f;
-  float sum = 0.f;
-  for (int k = 0; k < n; ++k) sum += __expf(row[k * stride] - pot[k] - m);
-  return m + __logf(sum);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    if (k >= n) break;
+    s += __expf(t[k] - m);
+  }
+  return m + __logf(s);
 }
 
-
-// Loads L0 = S_hat / tau of pair tile S (row pitch NP) into LDS.
-__device__ __forceinline__ void sk_load(DGMC_LDS float* L0, const float* S,
-                                        int Ns, int Nt, int NP, float inv_tau,
-                                        int lane) {
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    L0[i * NP + j] = S[e] * inv_tau;
+// Row copy (lane i: r[j] = L0_ij) and column copy (lane j: c[i] = L0_ij) of
+// a pair tile S [Ns, Nt]; -inf outside the valid n_s x n_t block.
+template <int NM>
+__device__ __forceinline__ void sk_load_regs(const float* S, int Nt, int ns,
+                                             int nt, float inv_tau, int lane,
+                                             float (&r)[NM], float (&c)[NM]) {
+  const bool rv = lane < ns, cv = lane < nt;
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    r[k] = (rv && k < nt) ? S[lane * Nt + k] * inv_tau : -INFINITY;
+    c[k] = (cv && k < ns) ? S[k * Nt + lane] * inv_tau : -INFINITY;
   }
 }
 
-// The forward iterations on the LDS tile: leaves the final potentials in
-// a / b and records every half-step's in ah ([iters + 1, Ns]) / bh
-// ([iters, Nt]).  Ends with a barrier.
-__device__ __forceinline__ void sk_iterate(const DGMC_LDS float* L0,
-                                           DGMC_LDS float* a,
-                                           DGMC_LDS float* b, int ns, int nt,
-                                           int Ns, int Nt, int NP, int iters,
-                                           float* ah, float* bh, int lane) {
-  b[lane] = 0.f;
-  a[lane] = 0.f;
-  __syncthreads();
+// The forward iterations: final potentials in a (lane i) / b (lane j),
+// every half-step's recorded in ah ([iters + 1, Ns]) / bh ([iters, Nt]).
+template <int NM>
+__device__ __forceinline__ void sk_iterate(const float (&r)[NM],
+                                           const float (&c)[NM], int ns,
+                                           int nt, int Ns, int Nt, int iters,
+                                           float* ah, float* bh, int lane,
+                                           float& a, float& b) {
+  a = 0.f;
+  b = 0.f;
   for (int it = 0; it <= iters; ++it) {
-    // Row step: lane i.
-    if (lane < Ns) {
-      const float r = lane < ns ? lse_line(L0 + lane * NP, 1, b, nt) : 0.f;
-      a[lane] = r;
-      ah[it * Ns + lane] = r;
-    }
-    __syncthreads();
+    const float x = sk_lse<NM>(r, b, nt);   // row step: lane i
+    a = lane < ns ? x : 0.f;
+    if (lane < Ns) ah[it * Ns + lane] = a;
     if (it == iters) break;
-    // Column step: lane j.
-    if (lane < Nt) {
-      const float c = lane < nt ? lse_line(L0 + lane, NP, a, ns) : 0.f;
-      b[lane] = c;
-      bh[it * Nt + lane] = c;
-    }
-    __syncthreads();
+    const float y = sk_lse<NM>(c, a, ns);   // column step: lane j
+    b = lane < nt ? y : 0.f;
+    if (lane < Nt) bh[it * Nt + lane] = b;
   }
 }
 
-// The backward half-steps in reverse on D (holding dL/d(final row-step
-// output) on entry, dL/dL0 on exit).  Ends with a barrier.
-__device__ __forceinline__ void sk_reverse(const DGMC_LDS float* L0,
-                                           DGMC_LDS float* D,
-                                           DGMC_LDS float* a,
-                                           DGMC_LDS float* b, int ns, int nt,
-                                           int Ns, int Nt, int NP, int iters,
-                                           const float* ah, const float* bh,
-                                           int lane) {
-  for (int step = 2 * iters; step >= 0; --step) {
-    const bool row = (step & 1) == 0;     // even: row step, odd: column step
-    const int it = step >> 1;
-    // Potentials defining this half-step's output L0 - a - b.
-    if (lane < Ns) a[lane] = ah[it * Ns + lane];
-    if (lane < Nt)
-      b[lane] = row ? (it > 0 ? bh[(it - 1) * Nt + lane] : 0.f)
-                    : bh[it * Nt + lane];
-    __syncthreads();
-    if (row) {
-      // Lane i: D_ij -= exp(out_ij) sum_k D_ik over its row.
-      if (lane < ns) {
-        DGMC_LDS float* Dr = D + lane * NP;
-        const DGMC_LDS float* Lr = L0 + lane * NP;
-        float sum = 0.f;
-        for (int j = 0; j < Nt; ++j) sum += Dr[j];
-        const float ai = a[lane];
-        for (int j = 0; j < nt; ++j)
-          Dr[j] -= __expf(Lr[j] - ai - b[j]) * sum;
-      }
-    } else {
-      // Lane j: D_ij -= exp(out_ij) sum_k D_kj over its column.
-      if (lane < nt) {
-        float sum = 0.f;
-        for (int i = 0; i < Ns; ++i) sum += D[i * NP + lane];
-        const float bj = b[lane];
-        for (int i = 0; i < ns; ++i)
-          D[i * NP + lane] -= __expf(L0[i * NP + lane] - a[i] - bj) * sum;
-      }
-    }
-    __syncthreads();
+// r[] <- row of P = exp(L0 - a - b) (0 outside the valid block).
+template <int NM>
+__device__ __forceinline__ void sk_prob_row(float (&r)[NM], float a, float b,
+                                            int ns, int nt, int lane) {
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const float p = __expf(r[k] - a - sk_rl(b, k));
+    r[k] = (lane < ns && k < nt) ? p : 0.f;
   }
 }
 
-// Loads the final potentials (row step iters, column step iters - 1).
-__device__ __forceinline__ void sk_final_pot(DGMC_LDS float* a,
-                                             DGMC_LDS float* b, int Ns,
-                                             int Nt, int iters,
-                                             const float* ah, const float* bh,
-                                             int lane) {
-  if (lane < Ns) a[lane] = ah[iters * Ns + lane];
-  if (lane < Nt) b[lane] = iters > 0 ? bh[(iters - 1) * Nt + lane] : 0.f;
+// D between the row layout (lane i: d[j] = D_ij) and the column layout
+// (lane j: d[i] = D_ij) through the LDS tile Dl [NM][NM + 1].
+// Only the valid block moves: n_from entries per lane out (the current
+// layout's valid count), n_to in (the new one's); entries past the valid
+// count are never read (every loop stops at it).
+template <int NM>
+__device__ __forceinline__ void sk_transpose(float (&d)[NM], DGMC_LDS float* Dl,
+                                             int lane, bool row_to_col,
+                                             int n_from, int n_to) {
+  constexpr int DP = NM + 1;
+  if (lane < NM) {
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      if (k >= n_from) break;
+      Dl[row_to_col ? lane * DP + k : k * DP + lane] = d[k];
+    }
+  }
+  __syncthreads();
+  if (lane < NM) {
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      if (k >= n_to) break;
+      d[k] = Dl[row_to_col ? k * DP + lane : lane * DP + k];
+    }
+  }
+  __syncthreads();
 }
 }  // namespace
 
+template <int NM>
 __global__ __launch_bounds__(kWave) void sinkhorn_fwd_kernel(
     const float* __restrict__ S_hat, const int* __restrict__ n_s,
     const int* __restrict__ n_t, int Ns, int Nt, int iters, float inv_tau,
     float* __restrict__ P, float* __restrict__ a_hist,
     float* __restrict__ b_hist) {
-  __shared__ float L0_[kShMaxN * kShPitch];
-  __shared__ float a_[kShMaxN], b_[kShMaxN];
-  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
-  DGMC_LDS float* a = (DGMC_LDS float*)a_;
-  DGMC_LDS float* b = (DGMC_LDS float*)b_;
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int ns = n_s[pb], nt = n_t[pb];
-  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
-  sk_load(L0, S_hat + (size_t)pb * Ns * Nt, Ns, Nt, NP, inv_tau, lane);
-  sk_iterate(L0, a, b, ns, nt, Ns, Nt, NP, iters,
-             a_hist + (size_t)pb * (iters + 1) * Ns,
-             b_hist + (size_t)pb * iters * Nt, lane);
-  float* Pb = P + (size_t)pb * Ns * Nt;
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    Pb[e] = (i < ns && j < nt) ? __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
-  }
-}
-
-__global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
-    const float* __restrict__ G, const float* __restrict__ S_hat,
-    const int* __restrict__ n_s, const int* __restrict__ n_t, int Ns, int Nt,
-    int iters, float inv_tau, const float* __restrict__ a_hist,
-    const float* __restrict__ b_hist, float* __restrict__ dS) {
-  __shared__ float L0_[kShMaxN * kShPitch];
-  __shared__ float D_[kShMaxN * kShPitch];
-  __shared__ float a_[kShMaxN], b_[kShMaxN];
-  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
-  DGMC_LDS float* D = (DGMC_LDS float*)D_;
-  DGMC_LDS float* a = (DGMC_LDS float*)a_;
-  DGMC_LDS float* b = (DGMC_LDS float*)b_;
-  const int pb = xcd_remap(blockIdx.x, gridDim.x);
-  const int lane = threadIdx.x;
-  const int ns = n_s[pb], nt = n_t[pb];
-  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
-  const float* Gb = G + (size_t)pb * Ns * Nt;
-  const float* ah = a_hist + (size_t)pb * (iters + 1) * Ns;
-  const float* bh = b_hist + (size_t)pb * iters * Nt;
-  sk_final_pot(a, b, Ns, Nt, iters, ah, bh, lane);
-  sk_load(L0, S_hat + (size_t)pb * Ns * Nt, Ns, Nt, NP, inv_tau, lane);
-  __syncthreads();
-  // dL of the final output: G * P (P = exp(out of the final row step)).
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    const bool v = i < ns && j < nt;
-    D[i * NP + j] = v ? Gb[e] * __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
-  }
-  __syncthreads();
-  sk_reverse(L0, D, a, b, ns, nt, Ns, Nt, NP, iters, ah, bh, lane);
-  float* out = dS + (size_t)pb * Ns * Nt;
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    out[e] = D[i * NP + j] * inv_tau;
+  const size_t off = (size_t)pb * Ns * Nt;
+  float r[NM], c[NM], a, b;
+  sk_load_regs<NM>(S_hat + off, Nt, ns, nt, inv_tau, lane, r, c);
+  sk_iterate<NM>(r, c, ns, nt, Ns, Nt, iters,
+                 a_hist + (size_t)pb * (iters + 1) * Ns,
+                 b_hist + (size_t)pb * iters * Nt, lane, a, b);
+  sk_prob_row<NM>(r, a, b, ns, nt, lane);
+  if (lane < Ns) {
+    float* Pr = P + off + (size_t)lane * Nt;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < Nt) Pr[k] = r[k];
   }
 }
 
@@ -206,12 +169,13 @@ __global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
 // with the normaliser swapped):
 //   joint[ps + i]          = r_s[ps + i]                  (i < n_s)
 //   joint[rows_s + pt + j] = sum_i P_ij r_s[ps + i]       (j < n_t)
-// P is formed in place of L0 (and optionally written out, step 0's S_0).
-// Lane c owns channels c + 64 q, q < CPL (R = 64 CPL); the target rows run
-// in chunks of kSkJ with the P column entries read as LDS broadcasts.
-constexpr int kSkJ = 8;
+// P is formed in place of the row copy (and optionally written out, step
+// 0's S_0).  Lane c owns channels c + 64 q, q < CPL (R = 64 CPL); P_ij
+// reaches the channel lanes by v_readlane from lane i, kSkJ target rows of
+// accumulators at a time.
+constexpr int kSkJ = 16;
 
-template <int CPL>
+template <int NM, int CPL>
 __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
     const float* __restrict__ S_hat, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, int Ns, int Nt, int iters, float inv_tau,
@@ -219,55 +183,51 @@ __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
     float* __restrict__ P, float* __restrict__ a_hist,
     float* __restrict__ b_hist) {
   constexpr int R = kWave * CPL;
-  __shared__ float L0_[kShMaxN * kShPitch];
-  __shared__ float a_[kShMaxN], b_[kShMaxN];
-  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
-  DGMC_LDS float* a = (DGMC_LDS float*)a_;
-  DGMC_LDS float* b = (DGMC_LDS float*)b_;
+  constexpr int JC = NM < kSkJ ? NM : kSkJ;
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int ps = ptr_s[pb], ns = ptr_s[pb + 1] - ps;
   const int pt = ptr_t[pb], nt = ptr_t[pb + 1] - pt;
-  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
-  sk_load(L0, S_hat + (size_t)pb * Ns * Nt, Ns, Nt, NP, inv_tau, lane);
-  sk_iterate(L0, a, b, ns, nt, Ns, Nt, NP, iters,
-             a_hist + (size_t)pb * (iters + 1) * Ns,
-             b_hist + (size_t)pb * iters * Nt, lane);
-  float* Pb = P ? P + (size_t)pb * Ns * Nt : nullptr;
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    const float v =
-        (i < ns && j < nt) ? __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
-    L0[i * NP + j] = v;      // each entry read and rewritten by one lane
-    if (Pb) Pb[e] = v;
+  const size_t off = (size_t)pb * Ns * Nt;
+  float r[NM], c[NM], a, b;
+  sk_load_regs<NM>(S_hat + off, Nt, ns, nt, inv_tau, lane, r, c);
+  sk_iterate<NM>(r, c, ns, nt, Ns, Nt, iters,
+                 a_hist + (size_t)pb * (iters + 1) * Ns,
+                 b_hist + (size_t)pb * iters * Nt, lane, a, b);
+  sk_prob_row<NM>(r, a, b, ns, nt, lane);
+  if (P && lane < Ns) {
+    float* Pr = P + off + (size_t)lane * Nt;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < Nt) Pr[k] = r[k];
   }
-  __syncthreads();
   const float* rs = r_s + (size_t)ps * R + lane;
   float* js = joint + (size_t)ps * R + lane;
   for (int i = 0; i < ns; ++i)
 #pragma unroll
     for (int q = 0; q < CPL; ++q) js[i * R + q * kWave] = rs[i * R + q * kWave];
   float* jt = joint + ((size_t)rows_s + pt) * R + lane;
-  for (int j0 = 0; j0 < nt; j0 += kSkJ) {
-    float acc[kSkJ][CPL];
 #pragma unroll
-    for (int jj = 0; jj < kSkJ; ++jj)
+  for (int j0 = 0; j0 < NM; j0 += JC) {
+    if (j0 >= nt) break;
+    float acc[JC][CPL];
+#pragma unroll
+    for (int jj = 0; jj < JC; ++jj)
 #pragma unroll
       for (int q = 0; q < CPL; ++q) acc[jj][q] = 0.f;
     for (int i = 0; i < ns; ++i) {
       float rv[CPL];
 #pragma unroll
       for (int q = 0; q < CPL; ++q) rv[q] = rs[i * R + q * kWave];
-      const DGMC_LDS float* Pr = L0 + i * NP + j0;
 #pragma unroll
-      for (int jj = 0; jj < kSkJ; ++jj) {
-        const float p = j0 + jj < nt ? Pr[jj] : 0.f;
+      for (int jj = 0; jj < JC; ++jj) {
+        const float p = sk_rl(r[j0 + jj], i);
 #pragma unroll
         for (int q = 0; q < CPL; ++q) acc[jj][q] = fmaf(p, rv[q], acc[jj][q]);
       }
     }
 #pragma unroll
-    for (int jj = 0; jj < kSkJ; ++jj)
+    for (int jj = 0; jj < JC; ++jj)
       if (j0 + jj < nt)
 #pragma unroll
         for (int q = 0; q < CPL; ++q)
@@ -275,100 +235,201 @@ __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
   }
 }
 
-// Backward of sinkhorn_transport: with g_t = d joint[rows_s + pt + j] and
-// G_P = dL/dP (optional: step 0's S_0 loss),
-//   dL/dP_ij = G_P_ij + <r_s[ps + i], g_t[j]>,
-// then the Sinkhorn Jacobians as in sinkhorn_bwd_kernel; dS = D / tau
-// (+ add, the gradient of S_hat's other consumer).  The inner products run
-// over kSkC-channel chunks of r_s / g_t staged in LDS, lane per (i, j).
+// Backward, plain (TR = false: G = dL/dP, counts n_s / n_t) or of
+// sinkhorn_transport (TR = true: ptr_s / ptr_t, g_t = d joint[rows_s + pt +
+// j], optional G_P):
+//   dL/dP_ij = G_P_ij + <r_s[ps + i], g_t[j]>
+// (inner products over kSkC-channel chunks staged in LDS, lane per (i, j)),
+// then the Sinkhorn Jacobians in reverse; dS = D / tau (+ add, the gradient
+// of S_hat's other consumer).  The potentials of every half-step are staged
+// in LDS once (dynamic, (iters + 1) Ns + iters Nt floats).
 constexpr int kSkC = 32;
 constexpr int kSkCP = kSkC + 4;       // 16-byte rows, bank-shifted
 typedef float sk_f4 __attribute__((ext_vector_type(4)));
 
-template <int CPL>
-__global__ __launch_bounds__(kWave) void sinkhorn_transport_bwd_kernel(
+template <int NM, bool TR, int CPL>
+__global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
     const float* __restrict__ G, const float* __restrict__ g_joint,
     const float* __restrict__ r_s, const float* __restrict__ S_hat,
-    const int* __restrict__ ptr_s, const int* __restrict__ ptr_t, int Ns,
+    const int* __restrict__ cnt_s, const int* __restrict__ cnt_t, int Ns,
     int Nt, int iters, float inv_tau, int rows_s,
     const float* __restrict__ a_hist, const float* __restrict__ b_hist,
     const float* __restrict__ add, float* __restrict__ dS) {
   constexpr int R = kWave * CPL;
-  __shared__ float L0_[kShMaxN * kShPitch];
-  __shared__ float D_[kShMaxN * kShPitch];
-  __shared__ __attribute__((aligned(16))) float rc_[kShMaxN * kSkCP];
-  __shared__ __attribute__((aligned(16))) float gc_[kShMaxN * kSkCP];
-  __shared__ float a_[kShMaxN], b_[kShMaxN];
-  DGMC_LDS float* L0 = (DGMC_LDS float*)L0_;
-  DGMC_LDS float* D = (DGMC_LDS float*)D_;
-  DGMC_LDS float* rc = (DGMC_LDS float*)rc_;
-  DGMC_LDS float* gc = (DGMC_LDS float*)gc_;
-  DGMC_LDS float* a = (DGMC_LDS float*)a_;
-  DGMC_LDS float* b = (DGMC_LDS float*)b_;
+  constexpr int DP = NM + 1;
+  constexpr int CH = TR ? NM * kSkCP : 1;
+  __shared__ float Dl_[NM * DP];
+  __shared__ __attribute__((aligned(16))) float rc_[CH];
+  __shared__ __attribute__((aligned(16))) float gc_[CH];
+  extern __shared__ float hist_[];
+  DGMC_LDS float* Dl = (DGMC_LDS float*)Dl_;
+  DGMC_LDS float* ahs = (DGMC_LDS float*)hist_;
+  DGMC_LDS float* bhs = ahs + (iters + 1) * Ns;
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
-  const int ps = ptr_s[pb], ns = ptr_s[pb + 1] - ps;
-  const int pt = ptr_t[pb], nt = ptr_t[pb + 1] - pt;
-  const int NP = Nt + 1 + (Nt & 1);      // odd pitch (<= 65)
-  const size_t off = (size_t)pb * Ns * Nt;
-  const float* ah = a_hist + (size_t)pb * (iters + 1) * Ns;
-  const float* bh = b_hist + (size_t)pb * iters * Nt;
-  sk_final_pot(a, b, Ns, Nt, iters, ah, bh, lane);
-  sk_load(L0, S_hat + off, Ns, Nt, NP, inv_tau, lane);
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    D[i * NP + j] = G ? G[off + e] : 0.f;
+  int ns, nt, ps = 0, pt = 0;
+  if (TR) {   // cnt_* are the pair offsets
+    ps = cnt_s[pb];
+    ns = cnt_s[pb + 1] - ps;
+    pt = cnt_t[pb];
+    nt = cnt_t[pb + 1] - pt;
+  } else {
+    ns = cnt_s[pb];
+    nt = cnt_t[pb];
   }
-  // <r_s[i], g_t[j]> over channel chunks: 8 lanes stage one 32-float row.
-  const float* rs = r_s + (size_t)ps * R;
-  const float* gt = g_joint + ((size_t)rows_s + pt) * R;
-  const int sr = lane >> 3, sc = (lane & 7) * 4;
-  for (int c0 = 0; c0 < R; c0 += kSkC) {
-    __syncthreads();                     // previous chunk's readers done
-    for (int i = sr; i < ns; i += kWave / 8)
-      *(DGMC_LDS sk_f4*)(rc + i * kSkCP + sc) =
-          *(const sk_f4*)(rs + (size_t)i * R + c0 + sc);
-    for (int j = sr; j < nt; j += kWave / 8)
-      *(DGMC_LDS sk_f4*)(gc + j * kSkCP + sc) =
-          *(const sk_f4*)(gt + (size_t)j * R + c0 + sc);
-    __syncthreads();
-    for (int e = lane; e < ns * nt; e += kWave) {
-      const int i = e / nt, j = e - i * nt;
-      const DGMC_LDS sk_f4* x = (const DGMC_LDS sk_f4*)(rc + i * kSkCP);
-      const DGMC_LDS sk_f4* y = (const DGMC_LDS sk_f4*)(gc + j * kSkCP);
-      float s = 0.f;
+  const size_t off = (size_t)pb * Ns * Nt;
+  {
+    const float* ah = a_hist + (size_t)pb * (iters + 1) * Ns;
+    const float* bh = b_hist + (size_t)pb * iters * Nt;
+    for (int e = lane; e < (iters + 1) * Ns; e += kWave) ahs[e] = ah[e];
+    for (int e = lane; e < iters * Nt; e += kWave) bhs[e] = bh[e];
+  }
+  float r[NM], c[NM], d[NM];
+  sk_load_regs<NM>(S_hat + off, Nt, ns, nt, inv_tau, lane, r, c);
+  if (TR) {
+    // D = G_P + <r_s[i], g_t[j]> in the LDS tile (8 lanes stage one row).
+    DGMC_LDS float* rc = (DGMC_LDS float*)rc_;
+    DGMC_LDS float* gc = (DGMC_LDS float*)gc_;
+    for (int e = lane; e < Ns * Nt; e += kWave) {
+      const int i = e / Nt, j = e - i * Nt;
+      Dl[i * DP + j] = G ? G[off + e] : 0.f;
+    }
+    const float* rs = r_s + (size_t)ps * R;
+    const float* gt = g_joint + ((size_t)rows_s + pt) * R;
+    const int sr = lane >> 3, sc = (lane & 7) * 4;
+    for (int c0 = 0; c0 < R; c0 += kSkC) {
+      __syncthreads();                   // previous chunk's readers done
+      for (int i = sr; i < ns; i += kWave / 8)
+        *(DGMC_LDS sk_f4*)(rc + i * kSkCP + sc) =
+            *(const sk_f4*)(rs + (size_t)i * R + c0 + sc);
+      for (int j = sr; j < nt; j += kWave / 8)
+        *(DGMC_LDS sk_f4*)(gc + j * kSkCP + sc) =
+            *(const sk_f4*)(gt + (size_t)j * R + c0 + sc);
+      __syncthreads();
+      for (int e = lane; e < ns * nt; e += kWave) {
+        const int i = e / nt, j = e - i * nt;
+        const DGMC_LDS sk_f4* x = (const DGMC_LDS sk_f4*)(rc + i * kSkCP);
+        const DGMC_LDS sk_f4* y = (const DGMC_LDS sk_f4*)(gc + j * kSkCP);
+        float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < kSkC / 4; ++k) {
-        const sk_f4 u = x[k], v = y[k];
-        s = fmaf(u.x, v.x, s);
-        s = fmaf(u.y, v.y, s);
-        s = fmaf(u.z, v.z, s);
-        s = fmaf(u.w, v.w, s);
+        for (int k = 0; k < kSkC / 4; ++k) {
+          const sk_f4 u = x[k], v = y[k];
+          s = fmaf(u.x, v.x, s);
+          s = fmaf(u.y, v.y, s);
+          s = fmaf(u.z, v.z, s);
+          s = fmaf(u.w, v.w, s);
+        }
+        Dl[i * DP + j] += s;
       }
-      D[i * NP + j] += s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      d[k] = (lane < Ns && k < Nt) ? Dl[lane * DP + k] : 0.f;
+    __syncthreads();
+  } else {
+    __syncthreads();
+    const float* Gr = G + off + (size_t)lane * Nt;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) d[k] = (lane < Ns && k < Nt) ? Gr[k] : 0.f;
+  }
+  // dL of the final output -> times P (final row step's potentials).
+  float a = lane < Ns ? ahs[iters * Ns + lane] : 0.f;
+  float b = (lane < Nt && iters > 0) ? bhs[(iters - 1) * Nt + lane] : 0.f;
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const float p = __expf(r[k] - a - sk_rl(b, k));
+    d[k] = (lane < ns && k < nt) ? d[k] * p : 0.f;
+  }
+  for (int step = 2 * iters; step >= 0; --step) {
+    const bool row = (step & 1) == 0;     // even: row step, odd: column step
+    const int it = step >> 1;
+    a = lane < Ns ? ahs[it * Ns + lane] : 0.f;
+    b = lane < Nt ? (row ? (it > 0 ? bhs[(it - 1) * Nt + lane] : 0.f)
+                         : bhs[it * Nt + lane])
+                  : 0.f;
+    // (d: row layout, valid k < nt, in a row step; column layout, valid
+    // k < ns, in a column step)
+    const int n = row ? nt : ns;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NM; ++k) {
+      if (k >= n) break;
+      s += d[k];
+    }
+    if (row) {
+      // lane i: D_ij -= exp(out_ij) sum_k D_ik
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        if (k >= nt) break;
+        const float e = __expf(r[k] - a - sk_rl(b, k));
+        d[k] = lane < ns ? fmaf(-e, s, d[k]) : d[k];
+      }
+      if (step > 0) sk_transpose<NM>(d, Dl, lane, true, nt, ns);
+    } else {
+      // lane j: D_ij -= exp(out_ij) sum_k D_kj
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        if (k >= ns) break;
+        const float e = __expf(c[k] - sk_rl(a, k) - b);
+        d[k] = lane < nt ? fmaf(-e, s, d[k]) : d[k];
+      }
+      sk_transpose<NM>(d, Dl, lane, false, ns, nt);
     }
   }
-  __syncthreads();
-  // dL of the final output -> times P.
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    const bool v = i < ns && j < nt;
-    D[i * NP + j] =
-        v ? D[i * NP + j] * __expf(L0[i * NP + j] - a[i] - b[j]) : 0.f;
-  }
-  __syncthreads();
-  sk_reverse(L0, D, a, b, ns, nt, Ns, Nt, NP, iters, ah, bh, lane);
-  float* out = dS + off;
-  for (int e = lane; e < Ns * Nt; e += kWave) {
-    const int i = e / Nt, j = e - i * Nt;
-    out[e] = D[i * NP + j] * inv_tau + (add ? add[off + e] : 0.f);
+  if (lane < Ns) {
+    float* out = dS + off + (size_t)lane * Nt;
+    const float* ad = add ? add + off + (size_t)lane * Nt : nullptr;
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      if (k < Nt)
+        out[k] = (lane < ns && k < nt ? d[k] * inv_tau : 0.f) +
+                 (ad ? ad[k] : 0.f);
   }
 }
 
+// ---------------------------------------------------------------------------
 static void sh_check(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat &&
                   t.is_contiguous() && t.dim() == 3,
               name, " must be a contiguous fp32 [B, Ns, Nt] GPU tensor");
+}
+
+// Compile-time tile bucket of the register-resident kernels.
+template <typename F>
+static void sk_dispatch_nm(int64_t Ns, int64_t Nt, F&& f) {
+  const int64_t n = std::max(Ns, Nt);
+  TORCH_CHECK(n <= kShMaxN, "sinkhorn: pair tile > 64");
+  if (n <= 16)
+    f(std::integral_constant<int, 16>());
+  else if (n <= 32)
+    f(std::integral_constant<int, 32>());
+  else
+    f(std::integral_constant<int, 64>());
+}
+
+template <typename F>
+static void sk_dispatch_cpl(int64_t R, F&& f) {
+  switch (R) {
+    case 64: f(std::integral_constant<int, 1>()); break;
+    case 128: f(std::integral_constant<int, 2>()); break;
+    case 256: f(std::integral_constant<int, 4>()); break;
+    default: TORCH_CHECK(false, "sinkhorn_transport: R in {64, 128, 256}");
+  }
+}
+
+// Dynamic LDS of the backward (the potentials of every half-step).
+template <typename K>
+static size_t sk_hist_lds(K kern, int64_t iters, int64_t Ns, int64_t Nt) {
+  const size_t bytes =
+      (size_t)((iters + 1) * Ns + iters * Nt) * sizeof(float);
+  TORCH_CHECK(bytes <= 96 * 1024, "sinkhorn_bwd: too many iterations (",
+              iters, ") for the LDS-staged potentials");
+  if (bytes > 48 * 1024)
+    DGMC_CHECK_HIP(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(kern),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return bytes;
 }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
@@ -387,11 +448,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> sinkhorn_fwd(
   at::Tensor bh = at::empty({B, std::max<int64_t>(iters, 1), Nt},
                             S_hat.options());
   if (B == 0) return {P, ah, bh};
-  hipLaunchKernelGGL(sinkhorn_fwd_kernel, dim3(B), dim3(kWave), 0,
-                     stream(), S_hat.data_ptr<float>(), n_s.data_ptr<int>(),
-                     n_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
-                     (float)(1.0 / tau), P.data_ptr<float>(),
-                     ah.data_ptr<float>(), bh.data_ptr<float>());
+  sk_dispatch_nm(Ns, Nt, [&](auto nm) {
+    hipLaunchKernelGGL(sinkhorn_fwd_kernel<decltype(nm)::value>, dim3(B),
+                       dim3(kWave), 0, stream(), S_hat.data_ptr<float>(),
+                       n_s.data_ptr<int>(), n_t.data_ptr<int>(), (int)Ns,
+                       (int)Nt, (int)iters, (float)(1.0 / tau),
+                       P.data_ptr<float>(), ah.data_ptr<float>(),
+                       bh.data_ptr<float>());
+  });
   DGMC_CHECK_LAUNCH();
   return {P, ah, bh};
 }
@@ -405,6 +469,9 @@ at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
   TORCH_CHECK(G.sizes() == S_hat.sizes(), "sinkhorn_bwd: grad shape");
   const int64_t B = S_hat.size(0), Ns = S_hat.size(1), Nt = S_hat.size(2);
   TORCH_CHECK(Ns <= kShMaxN && Nt <= kShMaxN, "sinkhorn: pair tile > 64");
+  TORCH_CHECK(n_s.scalar_type() == at::kInt && n_t.scalar_type() == at::kInt &&
+                  n_s.numel() == B && n_t.numel() == B,
+              "sinkhorn: int32 node counts [B]");
   TORCH_CHECK(a_hist.is_contiguous() && b_hist.is_contiguous() &&
                   a_hist.numel() == B * (iters + 1) * Ns &&
                   b_hist.numel() >= B * iters * Nt,
@@ -412,12 +479,17 @@ at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   at::Tensor dS = at::empty_like(S_hat);
   if (B == 0) return dS;
-  hipLaunchKernelGGL(sinkhorn_bwd_kernel, dim3(B), dim3(kWave), 0,
-                     stream(), G.data_ptr<float>(), S_hat.data_ptr<float>(),
-                     n_s.data_ptr<int>(), n_t.data_ptr<int>(), (int)Ns,
-                     (int)Nt, (int)iters, (float)(1.0 / tau),
-                     a_hist.data_ptr<float>(), b_hist.data_ptr<float>(),
-                     dS.data_ptr<float>());
+  sk_dispatch_nm(Ns, Nt, [&](auto nm) {
+    auto kern = sinkhorn_bwd_kernel<decltype(nm)::value, false, 1>;
+    const size_t lds = sk_hist_lds(kern, iters, Ns, Nt);
+    hipLaunchKernelGGL(kern, dim3(B), dim3(kWave), lds, stream(),
+                       G.data_ptr<float>(), nullptr, nullptr,
+                       S_hat.data_ptr<float>(), n_s.data_ptr<int>(),
+                       n_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
+                       (float)(1.0 / tau), 0, a_hist.data_ptr<float>(),
+                       b_hist.data_ptr<float>(), nullptr,
+                       dS.data_ptr<float>());
+  });
   DGMC_CHECK_LAUNCH();
   return dS;
 }
@@ -434,16 +506,6 @@ static void sk_rows_check(const at::Tensor& t, const char* name) {
                   t.data_ptr() != nullptr &&
                   reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
               name, " must be a contiguous 16-byte aligned fp32 [rows, R]");
-}
-
-template <typename F>
-static void sk_dispatch_cpl(int64_t R, F&& f) {
-  switch (R) {
-    case 64: f(std::integral_constant<int, 1>()); break;
-    case 128: f(std::integral_constant<int, 2>()); break;
-    case 256: f(std::integral_constant<int, 4>()); break;
-    default: TORCH_CHECK(false, "sinkhorn_transport: R in {64, 128, 256}");
-  }
 }
 
 std::vector<at::Tensor> sinkhorn_transport(const at::Tensor& S_hat,
@@ -467,15 +529,17 @@ std::vector<at::Tensor> sinkhorn_transport(const at::Tensor& S_hat,
   at::Tensor bh = at::empty({B, std::max<int64_t>(iters, 1), Nt},
                             S_hat.options());
   if (B == 0) return {joint, P, ah, bh};
-  sk_dispatch_cpl(R, [&](auto cpl) {
-    hipLaunchKernelGGL(sinkhorn_transport_kernel<decltype(cpl)::value>,
-                       dim3(B), dim3(kWave), 0, stream(),
-                       S_hat.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                       ptr_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
-                       (float)(1.0 / tau), r_s.data_ptr<float>(), (int)rows_s,
-                       joint.data_ptr<float>(),
-                       with_prob ? P.data_ptr<float>() : nullptr,
-                       ah.data_ptr<float>(), bh.data_ptr<float>());
+  sk_dispatch_nm(Ns, Nt, [&](auto nm) {
+    sk_dispatch_cpl(R, [&](auto cpl) {
+      hipLaunchKernelGGL(
+          (sinkhorn_transport_kernel<decltype(nm)::value,
+                                     decltype(cpl)::value>),
+          dim3(B), dim3(kWave), 0, stream(), S_hat.data_ptr<float>(),
+          ptr_s.data_ptr<int>(), ptr_t.data_ptr<int>(), (int)Ns, (int)Nt,
+          (int)iters, (float)(1.0 / tau), r_s.data_ptr<float>(), (int)rows_s,
+          joint.data_ptr<float>(), with_prob ? P.data_ptr<float>() : nullptr,
+          ah.data_ptr<float>(), bh.data_ptr<float>());
+    });
   });
   DGMC_CHECK_LAUNCH();
   return {joint, P, ah, bh};
@@ -520,15 +584,19 @@ at::Tensor sinkhorn_transport_bwd(const c10::optional<at::Tensor>& G,
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
   at::Tensor dS = at::empty_like(S_hat);
   if (B == 0) return dS;
-  sk_dispatch_cpl(R, [&](auto cpl) {
-    hipLaunchKernelGGL(sinkhorn_transport_bwd_kernel<decltype(cpl)::value>,
-                       dim3(B), dim3(kWave), 0, stream(), gp,
-                       g_joint.data_ptr<float>(), r_s.data_ptr<float>(),
-                       S_hat.data_ptr<float>(), ptr_s.data_ptr<int>(),
-                       ptr_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
-                       (float)(1.0 / tau), (int)rows_s,
-                       a_hist.data_ptr<float>(), b_hist.data_ptr<float>(), ad,
-                       dS.data_ptr<float>());
+  sk_dispatch_nm(Ns, Nt, [&](auto nm) {
+    sk_dispatch_cpl(R, [&](auto cpl) {
+      auto kern = sinkhorn_bwd_kernel<decltype(nm)::value, true,
+                                      decltype(cpl)::value>;
+      const size_t lds = sk_hist_lds(kern, iters, Ns, Nt);
+      hipLaunchKernelGGL(kern, dim3(B), dim3(kWave), lds, stream(), gp,
+                         g_joint.data_ptr<float>(), r_s.data_ptr<float>(),
+                         S_hat.data_ptr<float>(), ptr_s.data_ptr<int>(),
+                         ptr_t.data_ptr<int>(), (int)Ns, (int)Nt, (int)iters,
+                         (float)(1.0 / tau), (int)rows_s,
+                         a_hist.data_ptr<float>(), b_hist.data_ptr<float>(),
+                         ad, dS.data_ptr<float>());
+    });
   });
   DGMC_CHECK_LAUNCH();
   return dS;

@@ -397,7 +397,8 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 // ---------------------------------------------------------------------------
 // Exact fp32 top-k at split-bf16 speed: filter + exact re-score.
 //
-// The bf16x3 pass keeps K2 = min(32, N_t) approximate candidates per row
+// The bf16x3 pass keeps K2 = min(32, N_t, max(16, k + 6)) approximate
+// candidates per row
 // (scores s~_j, best first).  Its error against the exact-f32 MFMA score s_j
 // (the k-ordered fmaf chain of topk_dot_kernel) is bounded per product by
 // the dropped lo*lo term and the two split residuals (<= ~3 * 2^-18 |a b|)
@@ -547,7 +548,17 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
                                    at::Tensor* n_overflow) {
   const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
   const int Nt = h_t.size(1);
-  const int K2 = std::min(32, Nt);
+  // Candidates kept by the filter pass: k + 6 (>= 16), at most 32.  The
+  // pass's insertion work grows ~K2 ln(Nt / K2); a row whose K2-th
+  // candidate still clears the margin is recomputed exhaustively, so K2
+  // only trades filter time against (rare) fallbacks.  DGMC_TOPK_K2
+  // overrides (diagnostics).
+  static const int k2_env = [] {
+    const char* e = getenv("DGMC_TOPK_K2");
+    return e ? atoi(e) : 0;
+  }();
+  int K2 = k2_env > 0 ? k2_env : std::max<int>(16, (int)k + 6);
+  K2 = std::min(std::min(32, Nt), std::max<int>(K2, (int)k));
   at::Tensor cv;
   at::Tensor ci = topk_dot_x3(h_s, h_t, K2, &cv);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));

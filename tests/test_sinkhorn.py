@@ -52,14 +52,19 @@ def _sinkhorn_case(B=37, Ns=19, Nt=23, seed=0):
     return S_hat, n_s, n_t
 
 
+# pair tiles of the three register buckets (NM = 16, 32, 64)
+SHAPES = [(20, 12, 9), (37, 19, 23), (9, 64, 50)]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape', SHAPES)
 @pytest.mark.parametrize('iters,tau', [(10, 1.0), (0, 1.0), (25, 0.5)])
-def test_sinkhorn_kernel_matches_fp64_reference(iters, tau):
+def test_sinkhorn_kernel_matches_fp64_reference(iters, tau, shape):
     """csrc/hip/sinkhorn.hip forward + backward against the log-domain
     oracle (ops/reference.py::masked_sinkhorn) under fp64 autograd."""
     from deep_graph_matching_consensus_amd.ops import _backend
     assert _backend.hip_available()
-    S_hat, n_s, n_t = _sinkhorn_case()
+    S_hat, n_s, n_t = _sinkhorn_case(*shape)
     B, Ns, Nt = S_hat.shape
     mask = ref.count_mask(n_s, n_t, Ns, Nt)
     Sd = S_hat.double().requires_grad_()
@@ -115,15 +120,16 @@ def test_dgmc_sinkhorn_gpu_matches_cpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('shape', SHAPES)
 @pytest.mark.parametrize('R,iters', [(64, 10), (128, 5), (256, 0)])
-def test_sinkhorn_transport_kernel_matches_fp64(R, iters):
+def test_sinkhorn_transport_kernel_matches_fp64(R, iters, shape):
     """The fused Sinkhorn + transport kernel (joint ``[r_s; P^T r_s]``,
     optional ``P``) and its backward (``dL/dP = G_P + r_s g_t^T`` through
     the Sinkhorn Jacobians, plus a passthrough addend) against fp64
     autograd of the oracle."""
     from deep_graph_matching_consensus_amd.ops import _backend
     assert _backend.hip_available()
-    S_hat, n_s, n_t = _sinkhorn_case(seed=R)
+    S_hat, n_s, n_t = _sinkhorn_case(*shape, seed=R)
     B, Ns, Nt = S_hat.shape
     mask = ref.count_mask(n_s, n_t, Ns, Nt)
     g = torch.Generator().manual_seed(1)
