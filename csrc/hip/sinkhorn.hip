@@ -17,8 +17,8 @@
 // Jacobians in reverse:  row step  D_ij -= exp(out_ij) sum_k D_ik,
 //                        column step D_ij -= exp(out_ij) sum_k D_kj.
 //
-// Register-resident (N <= 64, compile-time bucket NM in {16, 32, 64}): lane
-// i holds row i of L0 (r[]) and lane j column j (c[]) in VGPRs; the
+// Register-resident (N <= 64, compile-time bucket NM in {16, 24, 32, 48, 64}):
+// lane i holds row i of L0 (r[]) and lane j column j (c[]) in VGPRs; the
 // potentials live one per lane (a in lane i, b in lane j) and reach the
 // other lanes by v_readlane (scalar broadcast) - a half-step is NM
 // unrolled sub / max / exp per lane with no LDS traffic and no barrier.
@@ -41,26 +41,22 @@ __device__ __forceinline__ float sk_rl(float v, int l) {
 }
 
 // LSE_k (x[k] - pot of lane k) over k < NM (x = -inf excluded); 0 if empty.
-// n: the wave-uniform valid count (the unrolled loops stop there: the
-// pair's own size, not the bucket's).
+// (Fully unrolled over the bucket: wave-uniform early exits at the pair's
+// own size measured SLOWER - 50 -> 77 us per backward - the per-k branch
+// serialises the readlane / exp chains.)
 template <int NM>
-__device__ __forceinline__ float sk_lse(const float (&x)[NM], float pot,
-                                        int n) {
+__device__ __forceinline__ float sk_lse(const float (&x)[NM], float pot) {
   float t[NM];
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < NM; ++k) {
-    if (k >= n) break;
     t[k] = x[k] - sk_rl(pot, k);
     m = fmaxf(m, t[k]);
   }
   if (m == -INFINITY) return 0.f;
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < NM; ++k) {
-    if (k >= n) break;
-    s += __expf(t[k] - m);
-  }
+  for (int k = 0; k < NM; ++k) s += __expf(t[k] - m);
   return m + __logf(s);
 }
 
@@ -89,11 +85,11 @@ __device__ __forceinline__ void sk_iterate(const float (&r)[NM],
   a = 0.f;
   b = 0.f;
   for (int it = 0; it <= iters; ++it) {
-    const float x = sk_lse<NM>(r, b, nt);   // row step: lane i
+    const float x = sk_lse<NM>(r, b);       // row step: lane i
     a = lane < ns ? x : 0.f;
     if (lane < Ns) ah[it * Ns + lane] = a;
     if (it == iters) break;
-    const float y = sk_lse<NM>(c, a, ns);   // column step: lane j
+    const float y = sk_lse<NM>(c, a);       // column step: lane j
     b = lane < nt ? y : 0.f;
     if (lane < Nt) bh[it * Nt + lane] = b;
   }
@@ -112,28 +108,20 @@ __device__ __forceinline__ void sk_prob_row(float (&r)[NM], float a, float b,
 
 // D between the row layout (lane i: d[j] = D_ij) and the column layout
 // (lane j: d[i] = D_ij) through the LDS tile Dl [NM][NM + 1].
-// Only the valid block moves: n_from entries per lane out (the current
-// layout's valid count), n_to in (the new one's); entries past the valid
-// count are never read (every loop stops at it).
 template <int NM>
 __device__ __forceinline__ void sk_transpose(float (&d)[NM], DGMC_LDS float* Dl,
-                                             int lane, bool row_to_col,
-                                             int n_from, int n_to) {
+                                             int lane, bool row_to_col) {
   constexpr int DP = NM + 1;
   if (lane < NM) {
 #pragma unroll
-    for (int k = 0; k < NM; ++k) {
-      if (k >= n_from) break;
+    for (int k = 0; k < NM; ++k)
       Dl[row_to_col ? lane * DP + k : k * DP + lane] = d[k];
-    }
   }
   __syncthreads();
   if (lane < NM) {
 #pragma unroll
-    for (int k = 0; k < NM; ++k) {
-      if (k >= n_to) break;
+    for (int k = 0; k < NM; ++k)
       d[k] = Dl[row_to_col ? k * DP + lane : lane * DP + k];
-    }
   }
   __syncthreads();
 }
@@ -183,7 +171,7 @@ __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
     float* __restrict__ P, float* __restrict__ a_hist,
     float* __restrict__ b_hist) {
   constexpr int R = kWave * CPL;
-  constexpr int JC = NM < kSkJ ? NM : kSkJ;
+  constexpr int JC = NM % kSkJ == 0 ? kSkJ : 8;     // divides NM
   const int pb = xcd_remap(blockIdx.x, gridDim.x);
   const int lane = threadIdx.x;
   const int ps = ptr_s[pb], ns = ptr_s[pb + 1] - ps;
@@ -348,33 +336,27 @@ __global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
     b = lane < Nt ? (row ? (it > 0 ? bhs[(it - 1) * Nt + lane] : 0.f)
                          : bhs[it * Nt + lane])
                   : 0.f;
-    // (d: row layout, valid k < nt, in a row step; column layout, valid
-    // k < ns, in a column step)
-    const int n = row ? nt : ns;
+    // (d: row layout in a row step, column layout in a column step; zero
+    // outside the valid block)
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < NM; ++k) {
-      if (k >= n) break;
-      s += d[k];
-    }
+    for (int k = 0; k < NM; ++k) s += d[k];
     if (row) {
       // lane i: D_ij -= exp(out_ij) sum_k D_ik
 #pragma unroll
       for (int k = 0; k < NM; ++k) {
-        if (k >= nt) break;
         const float e = __expf(r[k] - a - sk_rl(b, k));
         d[k] = lane < ns ? fmaf(-e, s, d[k]) : d[k];
       }
-      if (step > 0) sk_transpose<NM>(d, Dl, lane, true, nt, ns);
+      if (step > 0) sk_transpose<NM>(d, Dl, lane, true);
     } else {
       // lane j: D_ij -= exp(out_ij) sum_k D_kj
 #pragma unroll
       for (int k = 0; k < NM; ++k) {
-        if (k >= ns) break;
         const float e = __expf(c[k] - sk_rl(a, k) - b);
         d[k] = lane < nt ? fmaf(-e, s, d[k]) : d[k];
       }
-      sk_transpose<NM>(d, Dl, lane, false, ns, nt);
+      sk_transpose<NM>(d, Dl, lane, false);
     }
   }
   if (lane < Ns) {
@@ -402,8 +384,12 @@ static void sk_dispatch_nm(int64_t Ns, int64_t Nt, F&& f) {
   TORCH_CHECK(n <= kShMaxN, "sinkhorn: pair tile > 64");
   if (n <= 16)
     f(std::integral_constant<int, 16>());
+  else if (n <= 24)
+    f(std::integral_constant<int, 24>());
   else if (n <= 32)
     f(std::integral_constant<int, 32>());
+  else if (n <= 48)
+    f(std::integral_constant<int, 48>());
   else
     f(std::integral_constant<int, 64>());
 }

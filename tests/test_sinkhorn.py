@@ -52,8 +52,8 @@ def _sinkhorn_case(B=37, Ns=19, Nt=23, seed=0):
     return S_hat, n_s, n_t
 
 
-# pair tiles of the three register buckets (NM = 16, 32, 64)
-SHAPES = [(20, 12, 9), (37, 19, 23), (9, 64, 50)]
+# pair tiles of the register buckets (NM = 16, 24, 32, 48, 64)
+SHAPES = [(20, 12, 9), (37, 19, 23), (8, 30, 28), (6, 40, 45), (9, 64, 50)]
 
 
 @pytest.mark.gpu
