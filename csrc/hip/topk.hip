@@ -168,7 +168,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kX3Rows = 128;   // source rows per workgroup (4 waves x 32)
+// Source rows per workgroup: W waves x 32.  W = 8 (one 512-thread workgroup
+// per CU) at C = 128 / 256: every streamed target tile serves 256 source rows
+// - the kernel is bound by the target-plane stream (MALL / HBM), not the
+// matrix cores, at 128 rows per tile load.
 constexpr int kX3Tile = 32;    // targets per streamed tile
 
 __device__ __forceinline__ float lane_f(float v, int l) {
@@ -207,8 +210,8 @@ __global__ __launch_bounds__(256) void split_bf16_kernel(
   *reinterpret_cast<bf16x4*>(lo + r * CP + c) = vl;
 }
 
-template <int NKS>
-__global__ __launch_bounds__(256, 2) void topk_x3_kernel(
+template <int NKS, int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     const float* __restrict__ h_s, const __bf16* __restrict__ t_hi,
     const __bf16* __restrict__ t_lo,
     float* __restrict__ part_v, int* __restrict__ part_i,
@@ -218,15 +221,16 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
   constexpr int BP = CP + 8;                // LDS row pitch (bf16)
   constexpr int TILE = kX3Tile * BP;        // one hi or lo tile (bf16)
   constexpr int V_ROW = CP / 8;             // 16-byte vectors per plane row
-  constexpr int PRE = kX3Tile * V_ROW / 256;    // vectors per thread per plane
-  static_assert(PRE >= 1 && kX3Tile * V_ROW % 256 == 0, "tile split");
+  constexpr int NT = 64 * W;                // threads
+  constexpr int PRE = kX3Tile * V_ROW / NT;     // vectors per thread per plane
+  static_assert(PRE >= 1 && kX3Tile * V_ROW % NT == 0, "tile split");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS __bf16* sB = (DGMC_LDS __bf16*)smem_raw;   // [2 buf][hi, lo][TILE]
 
   const int b = blockIdx.z, split = blockIdx.y;
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int h = lane >> 5, hl = lane & 31, hb = lane & 32;
-  const int row0 = blockIdx.x * kX3Rows + wave * 32;
+  const int row0 = blockIdx.x * (32 * W) + wave * 32;
   const int j_begin = split * span;
   const int j_end = min(Nt, j_begin + span);
   const float* hs = h_s + (size_t)b * Ns * C;
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
   auto load_tile = [&](int j0, u32x4* regs) {
 #pragma unroll
     for (int u = 0; u < PRE; ++u) {
-      const int f = tid + 256 * u;
+      const int f = tid + NT * u;
       const int r = f / V_ROW, c = (f % V_ROW) * 8;
       u32x4 h = {0u, 0u, 0u, 0u}, l = h;
       if (j0 + r < j_end) {
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
     DGMC_LDS __bf16* lo_t = hi_t + TILE;
 #pragma unroll
     for (int u = 0; u < PRE; ++u) {
-      const int f = tid + 256 * u;
+      const int f = tid + NT * u;
       const int r = f / V_ROW, c = (f % V_ROW) * 8;
       *reinterpret_cast<DGMC_LDS u32x4*>(hi_t + r * BP + c) = regs[u];
       *reinterpret_cast<DGMC_LDS u32x4*>(lo_t + r * BP + c) = regs[PRE + u];
@@ -323,8 +327,16 @@ __global__ __launch_bounds__(256, 2) void topk_x3_kernel(
     if (t + 1 < ntiles) store_tile((t + 1) & 1, pre);
 
     const bool col_ok = j0 + hl < j_end && !(dbg & 1);
+    // One wave vote for the whole tile first: once the lists have filled,
+    // most tiles hold no candidate beating any row's k-th score, and the
+    // 16 per-row votes below are skipped.
+    bool hit = false;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hit |= col_ok && acc[r] > thr[r];
+    const bool any = __ballot(hit) != 0ull;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
+      if (!any) break;
       const float v = col_ok ? acc[r] : -INFINITY;
       unsigned long long mask = __ballot(v > thr[r]);
       while (mask) {
@@ -587,10 +599,10 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
 static int topk_debug() { return 0; }
 
 // Target splits for the bf16x3 kernel: the smallest S whose blocks fill the
-// 2-blocks-per-CU slots of the chip to >= 85% (a partial last wave of blocks
+// per_cu-blocks-per-CU slots of the chip to >= 85% (a partial last wave of blocks
 // idles CUs), keeping every split >= 2 tiles.
-static int x3_splits(int64_t row_blocks, int Nt) {
-  const int64_t slots = 2 * 256;
+static int x3_splits(int64_t row_blocks, int Nt, int per_cu) {
+  const int64_t slots = (int64_t)per_cu * 256;
   int best = 1;
   double best_eff = 0.0;
   for (int S = 1; S <= 16; ++S) {
@@ -615,8 +627,9 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
   const int NKS = (C + 63) / 64 * 4;
   const int CP = NKS * 16;
   const size_t lds = (size_t)4 * kX3Tile * (CP + 8) * sizeof(__bf16);
-  const int row_blocks = (Ns + kX3Rows - 1) / kX3Rows;
-  int S = x3_splits((int64_t)row_blocks * B, Nt);
+  const int W = (NKS == 8 || NKS == 16) ? 8 : 4;
+  const int row_blocks = (Ns + 32 * W - 1) / (32 * W);
+  int S = x3_splits((int64_t)row_blocks * B, Nt, W == 8 ? 1 : 2);
   int span = (Nt + S - 1) / S;
   span = (span + kX3Tile - 1) / kX3Tile * kX3Tile;
   S = (Nt + span - 1) / span;
@@ -645,7 +658,7 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
     DGMC_CHECK_HIP(hipFuncSetAttribute(
         reinterpret_cast<const void*>(kernel),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(kernel, grid, dim3(256), lds, stream(),
+    hipLaunchKernelGGL(kernel, grid, dim3(64 * W), lds, stream(),
                        h_s.data_ptr<float>(), t_hi, t_lo,
                        S > 1 ? pv.data_ptr<float>() : nullptr,
                        S > 1 ? pi.data_ptr<int>() : nullptr,
@@ -653,10 +666,10 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
                        span, topk_debug());
   };
   switch (NKS) {
-    case 4: launch(topk_x3_kernel<4>); break;
-    case 8: launch(topk_x3_kernel<8>); break;
-    case 12: launch(topk_x3_kernel<12>); break;
-    default: launch(topk_x3_kernel<16>); break;
+    case 4: launch(topk_x3_kernel<4, 4>); break;
+    case 8: launch(topk_x3_kernel<8, 8>); break;
+    case 12: launch(topk_x3_kernel<12, 4>); break;
+    default: launch(topk_x3_kernel<16, 8>); break;
   }
   DGMC_CHECK_LAUNCH();
   if (S > 1) {
