@@ -149,6 +149,16 @@ __device__ __forceinline__ void store_vec(T* __restrict__ p, const float* v) {
   }
 }
 
+// fp32 -> three bf16 terms x = hi + mid + lo (round-to-nearest per stage;
+// the bf16x6 operand planes of slot_gemm_x6.hip).
+__device__ __forceinline__ void split3_bf16(float x, __bf16& h, __bf16& m,
+                                            __bf16& l) {
+  h = (__bf16)x;
+  const float r1 = x - (float)h;      // exact
+  m = (__bf16)r1;
+  l = (__bf16)(r1 - (float)m);        // exact residual, rounded
+}
+
 __host__ __device__ inline bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }

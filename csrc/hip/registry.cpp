@@ -12,6 +12,12 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                     const c10::optional<at::Tensor>& self_scale,
                     const c10::optional<at::Tensor>& bias, bool relu,
                     at::ScalarType out_dtype);
+std::vector<at::Tensor> spmm_csr_planes(const at::Tensor& rowptr,
+                                        const at::Tensor& col,
+                                        const at::Tensor& val,
+                                        const at::Tensor& x,
+                                        const c10::optional<at::Tensor>& bias,
+                                        bool relu);
 void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
                   const at::Tensor& val, const at::Tensor& x,
                   const c10::optional<at::Tensor>& self_x,
@@ -306,6 +312,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "out_dtype) -> "
       "Tensor");
   m.def(
+      "spmm_csr_planes(Tensor rowptr, Tensor col, Tensor val, Tensor x, "
+      "Tensor? bias, bool relu) -> Tensor[]");
+  m.def(
       "spmm_csr_out(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
       "self_x, Tensor? self_scale, Tensor? bias, bool relu, Tensor(a!) out) "
       "-> ()");
@@ -519,6 +528,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("spmm_csr", &dgmc::spmm_csr);
+  m.impl("spmm_csr_planes", &dgmc::spmm_csr_planes);
   m.impl("spmm_csr_out", &dgmc::spmm_csr_out);
   m.impl("spline_basis", &dgmc::spline_basis);
   m.impl("dense_masked_softmax", &dgmc::dense_masked_softmax);

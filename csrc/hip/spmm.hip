@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const float* __restrict__ val, const TIn* __restrict__ x,
     const TIn* __restrict__ self_x, const float* __restrict__ self_scale,
     const float* __restrict__ bias, TOut* __restrict__ out, int R, int C,
-    int relu) {
+    int relu, __bf16* __restrict__ planes) {
   constexpr int RPB = 256 / LPR;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int r = blk * RPB + threadIdx.x / LPR;
@@ -102,19 +102,48 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
       for (int k = 0; k < VEC; ++k) acc[k] = fmaxf(acc[k], 0.f);
     }
     store_row<TOut, VEC>(out + (size_t)r * C + c0, acc);
+    if (planes != nullptr) {
+      // bf16x6 operand planes [3][R][C] of the output (the next slot GEMM's
+      // A operand: no separate split pass).
+      typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+      const size_t o = (size_t)r * C + c0, plane = (size_t)R * C;
+      if constexpr (VEC % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < VEC; k += 4) {
+          b4 h, m, l;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            __bf16 he, me, le;
+            split3_bf16(acc[k + e], he, me, le);
+            h[e] = he;
+            m[e] = me;
+            l[e] = le;
+          }
+          *reinterpret_cast<b4*>(planes + o + k) = h;
+          *reinterpret_cast<b4*>(planes + o + plane + k) = m;
+          *reinterpret_cast<b4*>(planes + o + 2 * plane + k) = l;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+          split3_bf16(acc[k], planes[o + k], planes[o + plane + k],
+                      planes[o + 2 * plane + k]);
+      }
+    }
   }
 }
 
 template <typename TIn, typename TOut, int VEC, int LPR>
 void launch_spmm(const int* rowptr, const int* col, const float* val,
                  const TIn* x, const TIn* self_x, const float* self_scale,
-                 const float* bias, TOut* out, int R, int C, bool relu) {
+                 const float* bias, TOut* out, int R, int C, bool relu,
+                 __bf16* planes) {
   constexpr int RPB = 256 / LPR;
   const int blocks = (R + RPB - 1) / RPB;
   if (blocks == 0) return;
   hipLaunchKernelGGL((spmm_csr_kernel<TIn, TOut, VEC, LPR, 4>), dim3(blocks),
                      dim3(256), 0, stream(), rowptr, col, val, x, self_x,
-                     self_scale, bias, out, R, C, relu ? 1 : 0);
+                     self_scale, bias, out, R, C, relu ? 1 : 0, planes);
   DGMC_CHECK_LAUNCH();
 }
 
@@ -122,27 +151,32 @@ template <typename TIn, typename TOut>
 void spmm_dispatch(const int* rowptr, const int* col, const float* val,
                    const TIn* x, const TIn* self_x, const float* self_scale,
                    const float* bias, TOut* out, int R, int C, bool relu,
-                   bool vec_ok) {
+                   bool vec_ok, __bf16* planes = nullptr) {
   constexpr int V = Vec16<TIn>::N;
   if (vec_ok && C % V == 0) {
     const int lanes = C / V;
     if (lanes <= 4)
       return launch_spmm<TIn, TOut, V, 4>(rowptr, col, val, x, self_x,
-                                          self_scale, bias, out, R, C, relu);
+                                          self_scale, bias, out, R, C, relu,
+                                          planes);
     if (lanes <= 8)
       return launch_spmm<TIn, TOut, V, 8>(rowptr, col, val, x, self_x,
-                                          self_scale, bias, out, R, C, relu);
+                                          self_scale, bias, out, R, C, relu,
+                                          planes);
     if (lanes <= 16)
       return launch_spmm<TIn, TOut, V, 16>(rowptr, col, val, x, self_x,
-                                           self_scale, bias, out, R, C, relu);
+                                           self_scale, bias, out, R, C, relu,
+                                           planes);
     if (lanes <= 32)
       return launch_spmm<TIn, TOut, V, 32>(rowptr, col, val, x, self_x,
-                                           self_scale, bias, out, R, C, relu);
+                                           self_scale, bias, out, R, C, relu,
+                                           planes);
     return launch_spmm<TIn, TOut, V, 64>(rowptr, col, val, x, self_x,
-                                         self_scale, bias, out, R, C, relu);
+                                         self_scale, bias, out, R, C, relu,
+                                         planes);
   }
   launch_spmm<TIn, TOut, 1, 64>(rowptr, col, val, x, self_x, self_scale, bias,
-                                out, R, C, relu);
+                                out, R, C, relu, planes);
 }
 
 static void spmm_into(const at::Tensor& rowptr, const at::Tensor& col,
@@ -211,6 +245,42 @@ at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
       at::empty({rowptr.numel() - 1, x.size(1)}, x.options().dtype(out_dtype));
   spmm_into(rowptr, col, val, x, self_x, self_scale, bias, relu, out);
   return out;
+}
+
+// fp32 SpMM that also writes the bf16x6 operand planes [3, R, C] of its
+// output (bias + ReLU applied first).
+std::vector<at::Tensor> spmm_csr_planes(const at::Tensor& rowptr,
+                                        const at::Tensor& col,
+                                        const at::Tensor& val,
+                                        const at::Tensor& x,
+                                        const c10::optional<at::Tensor>& bias,
+                                        bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.is_contiguous() &&
+                  x.scalar_type() == at::kFloat && x.size(1) % 4 == 0 &&
+                  aligned16(x.data_ptr()),
+              "spmm_csr_planes: contiguous aligned fp32 x, C % 4 == 0");
+  TORCH_CHECK(rowptr.scalar_type() == at::kInt && col.scalar_type() == at::kInt &&
+                  val.scalar_type() == at::kFloat && col.numel() == val.numel(),
+              "spmm_csr_planes: int32 CSR with fp32 values");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int64_t R = rowptr.numel() - 1, C = x.size(1);
+  TORCH_CHECK(R >= 0 && R * C < INT32_MAX * 4LL, "spmm_csr_planes: size");
+  at::Tensor out = at::empty({R, C}, x.options());
+  at::Tensor planes = at::empty({3, R, C}, x.options().dtype(at::kBFloat16));
+  if (R == 0 || C == 0) return {out, planes};
+  at::Tensor b_c;
+  if (bias.has_value() && bias->defined()) {
+    b_c = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b_c.numel() == C, "spmm_csr_planes: bias size");
+  }
+  spmm_dispatch<float, float>(
+      rowptr.data_ptr<int>(), col.data_ptr<int>(), val.data_ptr<float>(),
+      x.data_ptr<float>(), nullptr, nullptr,
+      b_c.defined() ? b_c.data_ptr<float>() : nullptr, out.data_ptr<float>(),
+      (int)R, (int)C, relu, aligned16(out.data_ptr()),
+      reinterpret_cast<__bf16*>(planes.data_ptr()));
+  DGMC_CHECK_LAUNCH();
+  return {out, planes};
 }
 
 // Writes into a caller-owned buffer (e.g. a slot of a loop-gradient stack,

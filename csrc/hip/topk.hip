@@ -594,9 +594,15 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
   return out;
 }
 
-// (The kernels' dbg argument - 1 skip selection, 2 skip MFMA - is a
-// diagnostic-build ablation knob; production launches pass 0.)
-static int topk_debug() { return 0; }
+// (The kernels' dbg argument - 1 skip selection, 2 skip MFMA - is an
+// ablation knob: DGMC_TOPK_DEBUG, never set in production runs.)
+static int topk_debug() {
+  static const int v = [] {
+    const char* e = getenv("DGMC_TOPK_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 
 // Target splits for the bf16x3 kernel: the smallest S whose blocks fill the
 // per_cu-blocks-per-CU slots of the chip to >= 85% (a partial last wave of blocks
@@ -630,6 +636,13 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
   const int W = (NKS == 8 || NKS == 16) ? 8 : 4;
   const int row_blocks = (Ns + 32 * W - 1) / (32 * W);
   int S = x3_splits((int64_t)row_blocks * B, Nt, W == 8 ? 1 : 2);
+  {
+    static const int s_env = [] {     // DGMC_TOPK_SPLITS: diagnostics only
+      const char* e = getenv("DGMC_TOPK_SPLITS");
+      return e ? atoi(e) : 0;
+    }();
+    if (s_env > 0) S = s_env;
+  }
   int span = (Nt + S - 1) / S;
   span = (span + kX3Tile - 1) / kX3Tile * kX3Tile;
   S = (Nt + span - 1) / span;

@@ -35,16 +35,20 @@ class SplineCNN(StackedEncoder):
 
     def forward(self, x, edge_index, edge_attr, *args):
         xs = [x]
-        for conv in self.convs:
+        last = len(self.convs) - 1
+        for i, conv in enumerate(self.convs):
+            # (a non-last layer's output feeds the next conv: on the fp32
+            # bf16x6 path its aggregation also writes the operand planes)
+            kw = {'planes_out': True} if i < last else {}
             if (self.cat and xs[-1].requires_grad and
                     torch.is_grad_enabled()):
                 # xs[-1] also feeds the concatenation: route that consumer
                 # through the conv's alias so both gradients meet inside
                 # the conv backward (no separate add kernel).
                 out, xs[-1] = conv(xs[-1], edge_index, edge_attr, act='relu',
-                                   passthrough=True)
+                                   passthrough=True, **kw)
             else:
-                out = conv(xs[-1], edge_index, edge_attr, act='relu')
+                out = conv(xs[-1], edge_index, edge_attr, act='relu', **kw)
             xs.append(out)
         parts = self._parts_out(xs)
         if parts is not None:

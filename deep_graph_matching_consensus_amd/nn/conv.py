@@ -163,7 +163,8 @@ class SplineConv(torch.nn.Module):
         return w, cached(('spline_w_lp', id(self), dtype),
                          lambda: w.detach().to(dtype))
 
-    def forward(self, x, edge_index, pseudo, act=None, passthrough=False):
+    def forward(self, x, edge_index, pseudo, act=None, passthrough=False,
+                planes_out=False):
         x = x.unsqueeze(-1) if x.dim() == 1 else x
         pseudo = pseudo.unsqueeze(-1) if pseudo.dim() == 1 else pseudo
         N = x.size(0)
@@ -180,7 +181,8 @@ class SplineConv(torch.nn.Module):
                 plan, x, self.weight, self.root, self.bias,
                 relu=(act == 'relu'), loop_key=(id(self), N, plan.num_cols),
                 passthrough=passthrough,
-                dx_row0=getattr(x, '_dgmc_dx_row0', 0))
+                dx_row0=getattr(x, '_dgmc_dx_row0', 0),
+                planes_out=planes_out)
         w, w_lp = self.stacked_operands(dtype, x, plan)
         return gemm_spmm(plan, x, w, w_lp, self.out_channels, bias=self.bias,
                          relu=(act == 'relu'),

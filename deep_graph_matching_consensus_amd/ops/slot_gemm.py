@@ -150,7 +150,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, root, bias, op, relu, loop, passthrough,
-                dx_row0=0):
+                dx_row0=0, planes_out=False):
         S = weight.size(0) + (1 if root is not None else 0)
         plan = compact_plan(op, S)
         xc = x.contiguous()
@@ -160,7 +160,14 @@ class _SlotGemmSpMM(torch.autograd.Function):
             # bf16x6: X split once (the planes are also the weight
             # gradient's operand), weight images once per forward scope.
             wt3, ctx.w3 = _x6_images(weight, root)
-            xc = ops.split3(xc)
+            # (planes written by the producing SpMM when it was another
+            # slot conv; valid while x is unmodified)
+            pl = getattr(x, '_dgmc_x6', None)
+            if pl is not None and pl[1] == x._version and \
+                    tuple(pl[0].shape) == (3, ) + tuple(x.shape):
+                xc = pl[0]
+            else:
+                xc = ops.split3(xc)
             Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
         else:
             # W^T images [S, out, in] (k-contiguous B operand), built once
@@ -169,8 +176,15 @@ class _SlotGemmSpMM(torch.autograd.Function):
                 weight.detach().contiguous(),
                 root.detach().contiguous() if root is not None else None))
             Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
-        out = ops.spmm_csr(op.rowptr, plan.col_c, op.val, Y, None, None,
-                           bias, relu, torch.float32)
+        if X6 and planes_out:
+            # The consumer is another bf16x6 slot conv: the SpMM also
+            # writes its operand planes (no split pass there).
+            out, planes = ops.spmm_csr_planes(op.rowptr, plan.col_c, op.val,
+                                              Y, bias, relu)
+            out._dgmc_x6 = (planes, out._version)
+        else:
+            out = ops.spmm_csr(op.rowptr, plan.col_c, op.val, Y, None, None,
+                               bias, relu, torch.float32)
         ctx.save_for_backward(xc, weight, root, out if relu else None)
         ctx.op, ctx.plan, ctx.relu, ctx.loop = op, plan, relu, loop
         ctx.dx_row0 = int(dx_row0)
@@ -184,7 +198,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad, gpass=None):
         x, weight, root, out = ctx.saved_tensors
-        nones = (None, ) * 5
+        nones = (None, ) * 6
         op, plan, loop, idx = ctx.op, ctx.plan, ctx.loop, ctx.idx
         ops = _backend.ops()
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
@@ -275,16 +289,18 @@ class _SlotGemmSpMM(torch.autograd.Function):
 
 
 def slot_gemm_spmm(op, x, weight, root, bias=None, relu=False, loop_key=None,
-                   passthrough=False, dx_row0=0):
+                   passthrough=False, dx_row0=0, planes_out=False):
     r"""``act(A (x @ [W_0 | .. | W_{K-1} | root]).view(-1, C) + bias)`` in
     fp32 on the used ``(node, slot)`` pairs only; ``weight [K, in, out]``,
     ``root [in, out]`` are read in place (reference checkpoint layout).
     ``passthrough`` returns ``(out, x')`` (``x'`` aliases ``x``; its
     gradient is added inside this op's dX kernel).  ``dx_row0``: the input
-    gradient of rows ``< dx_row0`` is not needed (returned as zeros)."""
+    gradient of rows ``< dx_row0`` is not needed (returned as zeros).
+    ``planes_out``: the output feeds another slot conv - on the bf16x6 path
+    the aggregation also writes its operand planes."""
     from ..runtime import loopgrad
     loop = loopgrad.group(('slot_gemm', ) + tuple(loop_key)) \
         if loop_key is not None else None
     with torch.autocast(device_type='cuda', enabled=False):
         return _SlotGemmSpMM.apply(x, weight, root, bias, op, relu, loop,
-                                   passthrough, dx_row0)
+                                   passthrough, dx_row0, planes_out)

@@ -215,3 +215,31 @@ def test_rowmap_planes_equal_split_of_fp32(headline_plan):
                               None, True)
     used = int(plan.seg[-1])
     assert torch.equal(p3[:, :used], ops.split3(f32)[:, :used])
+
+
+def test_spmm_planes_feed_next_conv():
+    """A non-last fp32 SplineConv's aggregation also writes the bf16x6
+    planes of its output (== split3 of it, bitwise); the next conv consumes
+    them instead of splitting, with an identical result."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, DevicePairLoader, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.nn.conv import SplineConv
+    assert sg.X6
+    ops = _backend.ops()
+    torch.manual_seed(0)
+    groups = make_keypoint_datasets(graphs=8, feature_dim=128, seed=0)
+    store = GraphStore(groups, DEV)
+    b = next(iter(DevicePairLoader(store, batch_size=16, seed=0)))
+    c0 = SplineConv(128, 128, dim=2, kernel_size=5).to(DEV)
+    c1 = SplineConv(128, 128, dim=2, kernel_size=5).to(DEV)
+    x = b.x_s.float()
+    h = c0(x, b.edge_index_s, b.edge_attr_s, act='relu', planes_out=True)
+    pl = getattr(h, '_dgmc_x6', None)
+    assert pl is not None and pl[1] == h._version
+    assert torch.equal(pl[0], ops.split3(h.detach().contiguous()))
+    y1 = c1(h, b.edge_index_s, b.edge_attr_s, act='relu')
+    y2 = c1(h.detach().clone(), b.edge_index_s, b.edge_attr_s, act='relu')
+    assert torch.equal(y1, y2)
+    with torch.no_grad():
+        h.add_(0)             # an in-place write bumps the version: stale
+    assert h._dgmc_x6[1] != h._version
