@@ -55,10 +55,15 @@ __global__ __launch_bounds__(256) void candidates_kernel(
   }
   const auto so = at::cuda::philox::unpack(rng);
   const uint64_t seed = std::get<0>(so), off = std::get<1>(so);
-  const uint64_t ctr = (uint64_t)(r * kr + (j - k));
+  // ATen's Philox layout (curand_init(seed, subsequence, offset)): the low
+  // 64 counter bits are the 128-bit block (offset / 4), the high 64 the
+  // subsequence (this entry) - so another op drawing from the generator
+  // after this one (offset advanced by 4 below) never reuses these blocks.
+  const uint64_t sub = (uint64_t)(r * kr + (j - k));
+  const uint64_t blk = off / 4;
   const uint4 v = philox4x32_10(
-      make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)off,
-                 (uint32_t)(off >> 32)),
+      make_uint4((uint32_t)blk, (uint32_t)(blk >> 32), (uint32_t)sub,
+                 (uint32_t)(sub >> 32)),
       make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
   out[e] = (int64_t)(((uint64_t)v.x * (uint64_t)n_t) >> 32);
 }

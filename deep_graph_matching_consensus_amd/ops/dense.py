@@ -680,14 +680,17 @@ class _CatMatmulF32(torch.autograd.Function):
         wc = cached(('cat_f32_w', w_t.data_ptr(), w_t._version,
                      tuple(w_t.shape), tuple(w_t.stride())),
                     lambda: w_t.detach().contiguous())
-        ctx.save_for_backward(w_t, wc)
+        # The parts go through save_for_backward (autograd's version check
+        # catches an in-place write to a part before the weight gradient).
+        keep = tuple(parts) if ctx.needs_input_grad[0] else ()
+        ctx.save_for_backward(w_t, wc, *keep)
         ctx.idx = loop.register() if loop is not None else None
-        ctx.parts = tuple(parts) if ctx.needs_input_grad[0] else None
         return out
 
     @staticmethod
     def backward(ctx, g):
-        w_t, wc = ctx.saved_tensors
+        w_t, wc, *kept = ctx.saved_tensors
+        ctx.parts = tuple(kept) if kept else None
         ops = _backend.ops()
         g = g.float().contiguous()
         gx = ops.dense_nt_f32([g], wc)                          # [M, 128 n]
