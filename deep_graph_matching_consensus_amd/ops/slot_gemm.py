@@ -39,6 +39,16 @@ ENABLED = os.environ.get('DGMC_AMD_SLOT_GEMM', '1') == '1'
 # accumulators - max error vs fp64 BELOW the exact-f32 MFMA kernels on every
 # headline shape (tests/test_slot_gemm_x6.py).
 X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
+# Under in-step data parallelism a single-use weight gradient of at least
+# PIECE_BYTES (psi_1 layer 0: 25 MiB, the last gradient of the backward) is
+# produced in PIECES slot ranges and each piece's all-reduce starts as soon
+# as it is written (parallel/ddp.py::grad_sink), instead of the whole bucket
+# waiting for the last launch.  Without a reducer one launch is cheaper
+# (+0.03 ms per PascalVOC step for the extra fold); PIECES_ALWAYS=1 pieces
+# regardless (tests compare a one-rank RCCL run bit-for-bit with that).
+PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
+PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
+PIECE_BYTES = 8 << 20
 
 
 class CompactPlan(object):
@@ -263,7 +273,15 @@ class _SlotGemmSpMM(torch.autograd.Function):
         gw = gr = gb = None
         wgrad = weight_grad_x6 if ctx.x6 else weight_grad
         if loop is None:
-            if need_w:
+            if need_w and ctx.x6 and PIECES > 1 and \
+                    weight.numel() * 4 >= PIECE_BYTES and \
+                    ctx.needs_input_grad[1] and (PIECES_ALWAYS or
+                                                 _has_sink(weight)):
+                gw, gr = _weight_grad_pieces(x, dyc, plan, weight, root,
+                                             ctx.has_root and
+                                             ctx.needs_input_grad[2])
+                need_w = False
+            elif need_w:
                 dW = wgrad([x], [dyc], plan, cin, cout)
             if need_b:
                 gb = db.to(ctx.bias_dtype)
@@ -286,6 +304,42 @@ class _SlotGemmSpMM(torch.autograd.Function):
             if ctx.has_root and ctx.needs_input_grad[2]:
                 gr = dW[nw]
         return (gx, gw, gr, gb) + nones
+
+
+def _has_sink(weight):
+    from ..parallel.ddp import grad_sink
+    return grad_sink(weight) is not None
+
+
+def _weight_grad_pieces(x3, dy3, plan, weight, root, need_root):
+    """``dW`` of one use in ``PIECES`` slot ranges, each written into the
+    weight's flat DP gradient view (when an in-step reducer owns it) and
+    all-reduced right away; returns ``(gw, gr)``."""
+    from ..parallel.ddp import grad_sink
+    ops = _backend.ops()
+    nw, cin, cout = weight.shape
+    S = plan.S
+    tiles = (cin // 128) * (cout // 128)
+    rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
+    sink = grad_sink(weight)
+    gw = sink.grad_view(weight) if sink is not None else \
+        torch.empty_like(weight)
+    gr = None
+    per = cin * cout
+    bounds = [nw * i // PIECES for i in range(PIECES)] + [S]
+    for c in range(PIECES):
+        s0, s1 = bounds[c], bounds[c + 1]
+        part = ops.slot_wgrad_x6([x3], [dy3], plan.src, plan.seg[s0:s1 + 1],
+                                 rounds)
+        w1 = min(s1, nw)
+        gw[s0:w1].copy_(part[:w1 - s0])
+        if sink is not None:
+            sink.reduce_piece(weight, s0 * per, w1 * per)
+        if s1 > nw and need_root:
+            gr = part[nw - s0]
+    if sink is not None:
+        sink.mark_reduced(weight)
+    return gw, gr
 
 
 def slot_gemm_spmm(op, x, weight, root, bias=None, relu=False, loop_key=None,

@@ -30,10 +30,26 @@ the trainer runs one flat all-reduce after the replay.
 With a single process every call is a no-op, so the same training loop runs
 on 1..8 GPUs.
 """
+import weakref
+
 import torch
 import torch.distributed as dist
+from torch.utils.weak import WeakIdKeyDictionary
 
 from .dist import is_distributed
+
+# Gradient sinks: parameter -> the in-step reducer that owns its flat
+# gradient view.  A backward op that produces a large weight gradient in
+# pieces (ops/slot_gemm.py: psi_1 layer 0) writes each piece into the view
+# and starts its all-reduce at once, so the last - largest - gradient of the
+# backward does not leave its whole bucket exposed.
+_SINKS = WeakIdKeyDictionary()          # (tensor keys: by identity)
+
+
+def grad_sink(param):
+    """The in-step reducer collecting ``param``'s gradient, or None."""
+    r = _SINKS.get(param)
+    return r() if r is not None else None
 
 
 def _pad4(n):
@@ -99,6 +115,11 @@ class GradBucketAllReducer(object):
         if self.overlap:
             self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad)
                            for p in self.params]
+        self._pre = set()          # params whose gradient was pre-reduced
+        if self.in_step:
+            me = weakref.ref(self)
+            for p in self.params:
+                _SINKS[p] = me
         self._reset_counts()
 
     # ------------------------------------------------------------------
@@ -169,9 +190,45 @@ class GradBucketAllReducer(object):
     def _reset_counts(self):
         self._pending = [len(b) for b in self.buckets]
         self._works = []
+        self._pre = set()
+
+    # ------------------------------------------------------------------
+    # Pieces of one parameter's gradient reduced as they are produced.
+    def grad_view(self, p):
+        """``p``'s view of the flat gradient buffer (write pieces here)."""
+        off, n = self._slot[p]
+        return self.flat[off:off + n].view_as(p)
+
+    def reduce_piece(self, p, lo, hi):
+        """All-reduce elements ``[lo, hi)`` of ``p``'s flat gradient view
+        now (asynchronously); call :meth:`mark_reduced` once every piece of
+        ``p`` has been launched, before ``p``'s gradient is accumulated."""
+        off, n = self._slot[p]
+        assert 0 <= lo <= hi <= n
+        if hi > lo:
+            self._launch_range(off + lo, off + hi)
+
+    def mark_reduced(self, p):
+        """``p``'s whole gradient is in its flat view and being reduced:
+        its bucket skips it."""
+        self._pre.add(p)
 
     def _launch(self, bi):
-        self._launch_range(*self._bucket_range[bi])
+        if not self._pre:
+            self._launch_range(*self._bucket_range[bi])
+            return
+        # Contiguous runs of the bucket's parameters not already reduced.
+        run = None
+        for p in self.buckets[bi]:
+            off, n = self._slot[p]
+            if p in self._pre:
+                if run is not None:
+                    self._launch_range(*run)
+                    run = None
+                continue
+            run = (off, off + n) if run is None else (run[0], off + n)
+        if run is not None:
+            self._launch_range(*run)
 
     def _launch_range(self, lo, hi):
         buf = self.flat[lo:hi]
@@ -189,7 +246,10 @@ class GradBucketAllReducer(object):
         kernel; zeros for parameters without a gradient) and re-bind their
         ``p.grad`` to the flat views."""
         from ..ops import _backend
-        bucket = self.buckets[bi]
+        # (pre-reduced parameters already hold their flat view)
+        bucket = [p for p in self.buckets[bi] if p not in self._pre]
+        if not bucket:
+            return
         views = [self.flat[o:o + n].view_as(p)
                  for p, (o, n) in ((p, self._slot[p]) for p in bucket)]
         grads = [p.grad for p in bucket]
@@ -208,6 +268,10 @@ class GradBucketAllReducer(object):
             p.grad = v
 
     def _on_grad(self, p):
+        if p in self._pre:
+            # Accumulation may have copied the view: the update must read
+            # the (reduced in place) flat view itself.
+            p.grad = self.grad_view(p)
         bi = self._bucket_of[p]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:

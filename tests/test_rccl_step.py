@@ -60,10 +60,13 @@ def test_bench_rejects_world_size_mismatch():
 @pytest.mark.gpu
 def test_rccl_world1_captured_step_bit_identical(tmp_path):
     out = tmp_path / 'rccl.json'
+    # Both runs produce psi_1 layer 0's weight gradient in pieces (the RCCL
+    # run all-reduces each piece from inside the captured backward).
+    env = dict(os.environ, DGMC_AMD_WGRAD_PIECES_ALWAYS='1')
     r = subprocess.run([sys.executable, '-u',
                         osp.join(ROOT, 'tests', 'rccl_world1_worker.py'),
                         '--steps', '6', '--json', str(out)],
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=env)
     assert out.exists(), r.stdout[-2000:] + r.stderr[-4000:]
     res = json.loads(out.read_text())
     assert res['rccl']['distributed'] and res['rccl']['in_step']
