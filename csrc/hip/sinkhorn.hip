@@ -34,6 +34,8 @@ namespace dgmc {
 
 namespace {
 constexpr int kShMaxN = 64;
+typedef float sk_f4 __attribute__((ext_vector_type(4)));
+typedef float sk_f16v __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float sk_rl(float v, int l) {
   return __builtin_bit_cast(
@@ -194,32 +196,74 @@ __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
   for (int i = 0; i < ns; ++i)
 #pragma unroll
     for (int q = 0; q < CPL; ++q) js[i * R + q * kWave] = rs[i * R + q * kWave];
-  float* jt = joint + ((size_t)rows_s + pt) * R + lane;
+  if constexpr (NM <= 32) {
+    // r_t^T blocks on the matrix cores (v_mfma_f32_32x32x2_f32): A = P^T
+    // (lane l: row j = l % 32, k = i of the pair 2 t + l / 32, read from the
+    // transposed P tile), B = r_s (k = i, 32 channels), one 32 x 32 output
+    // block per 32 channels.
+    constexpr int DP = NM + 1;
+    __shared__ float Pt_[NM * DP];
+    DGMC_LDS float* Pt = (DGMC_LDS float*)Pt_;
+    if (lane < NM) {
 #pragma unroll
-  for (int j0 = 0; j0 < NM; j0 += JC) {
-    if (j0 >= nt) break;
-    float acc[JC][CPL];
+      for (int k = 0; k < NM; ++k) Pt[lane * DP + k] = r[k];   // P[i][j]
+    }
+    __syncthreads();
+    const int lj = lane & 31, hh = lane >> 5;
+    const float* rb = r_s + (size_t)ps * R + lj;
+    sk_f16v acc[CPL * 2];
 #pragma unroll
-    for (int jj = 0; jj < JC; ++jj)
+    for (int b = 0; b < 2 * CPL; ++b)
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) acc[jj][q] = 0.f;
-    for (int i = 0; i < ns; ++i) {
-      float rv[CPL];
+      for (int q = 0; q < 16; ++q) acc[b][q] = 0.f;
+    for (int i0 = 0; i0 < ns; i0 += 2) {
+      const int i = i0 + hh;
+      const bool vi = i < ns;
+      const float a = (vi && lj < NM) ? Pt[i * DP + lj] : 0.f;
 #pragma unroll
-      for (int q = 0; q < CPL; ++q) rv[q] = rs[i * R + q * kWave];
-#pragma unroll
-      for (int jj = 0; jj < JC; ++jj) {
-        const float p = sk_rl(r[j0 + jj], i);
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) acc[jj][q] = fmaf(p, rv[q], acc[jj][q]);
+      for (int b = 0; b < 2 * CPL; ++b) {
+        const float bv = vi ? rb[(size_t)i * R + 32 * b] : 0.f;
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[b], 0, 0,
+                                                      0);
       }
     }
+    float* jt = joint + ((size_t)rows_s + pt) * R + lj;
 #pragma unroll
-    for (int jj = 0; jj < JC; ++jj)
-      if (j0 + jj < nt)
+    for (int q = 0; q < 16; ++q) {
+      const int j = 8 * (q >> 2) + 4 * hh + (q & 3);
+      if (j < nt)
 #pragma unroll
-        for (int q = 0; q < CPL; ++q)
-          jt[(j0 + jj) * R + q * kWave] = acc[jj][q];
+        for (int b = 0; b < 2 * CPL; ++b) jt[(size_t)j * R + 32 * b] = acc[b][q];
+    }
+  } else {
+    float* jt = joint + ((size_t)rows_s + pt) * R + lane;
+#pragma unroll
+    for (int j0 = 0; j0 < NM; j0 += JC) {
+      if (j0 >= nt) break;
+      float acc[JC][CPL];
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj)
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) acc[jj][q] = 0.f;
+      for (int i = 0; i < ns; ++i) {
+        float rv[CPL];
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) rv[q] = rs[i * R + q * kWave];
+#pragma unroll
+        for (int jj = 0; jj < JC; ++jj) {
+          const float p = sk_rl(r[j0 + jj], i);
+#pragma unroll
+          for (int q = 0; q < CPL; ++q)
+            acc[jj][q] = fmaf(p, rv[q], acc[jj][q]);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < JC; ++jj)
+        if (j0 + jj < nt)
+#pragma unroll
+          for (int q = 0; q < CPL; ++q)
+            jt[(j0 + jj) * R + q * kWave] = acc[jj][q];
+    }
   }
 }
 
@@ -233,7 +277,6 @@ __global__ __launch_bounds__(kWave) void sinkhorn_transport_kernel(
 // in LDS once (dynamic, (iters + 1) Ns + iters Nt floats).
 constexpr int kSkC = 32;
 constexpr int kSkCP = kSkC + 4;       // 16-byte rows, bank-shifted
-typedef float sk_f4 __attribute__((ext_vector_type(4)));
 
 template <int NM, bool TR, int CPL>
 __global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
@@ -245,7 +288,7 @@ __global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
     const float* __restrict__ add, float* __restrict__ dS) {
   constexpr int R = kWave * CPL;
   constexpr int DP = NM + 1;
-  constexpr int CH = TR ? NM * kSkCP : 1;
+  constexpr int CH = (TR && NM > 32) ? NM * kSkCP : 1;
   __shared__ float Dl_[NM * DP];
   __shared__ __attribute__((aligned(16))) float rc_[CH];
   __shared__ __attribute__((aligned(16))) float gc_[CH];
@@ -274,7 +317,47 @@ __global__ __launch_bounds__(kWave) void sinkhorn_bwd_kernel(
   }
   float r[NM], c[NM], d[NM];
   sk_load_regs<NM>(S_hat + off, Nt, ns, nt, inv_tau, lane, r, c);
-  if (TR) {
+  if (TR && NM <= 32) {
+    // D = G_P + <r_s[i], g_t[j]>: the 32 x 32 product block on the matrix
+    // cores (v_mfma_f32_32x32x2_f32; lane l feeds row l % 32 of r_s and of
+    // g_t, channel half l / 32 of each k pair).
+    for (int e = lane; e < Ns * Nt; e += kWave) {
+      const int i = e / Nt, j = e - i * Nt;
+      Dl[i * DP + j] = G ? G[off + e] : 0.f;
+    }
+    const int li = lane & 31, hh = lane >> 5;
+    const bool va = li < ns, vb = li < nt;
+    const float* ra = r_s + ((size_t)ps + li) * R + hh * (R / 2);
+    const float* gb = g_joint + ((size_t)rows_s + pt + li) * R + hh * (R / 2);
+    sk_f16v acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    for (int c0 = 0; c0 < R / 2; c0 += 16) {
+      sk_f4 av[4], bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        av[q] = va ? *(const sk_f4*)(ra + c0 + 4 * q) : sk_f4{0.f, 0.f, 0.f, 0.f};
+        bv[q] = vb ? *(const sk_f4*)(gb + c0 + 4 * q) : sk_f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q][t], bv[q][t], acc,
+                                                     0, 0, 0);
+    }
+    __syncthreads();                     // G staged
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = 8 * (q >> 2) + 4 * hh + (q & 3);
+      if (i < NM && li < NM) Dl[i * DP + li] += acc[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      d[k] = (lane < Ns && k < Nt) ? Dl[lane * DP + k] : 0.f;
+    __syncthreads();
+  } else if (TR) {
     // D = G_P + <r_s[i], g_t[j]> in the LDS tile (8 lanes stage one row).
     DGMC_LDS float* rc = (DGMC_LDS float*)rc_;
     DGMC_LDS float* gc = (DGMC_LDS float*)gc_;
