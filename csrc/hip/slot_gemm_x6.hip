@@ -454,18 +454,13 @@ typedef short x6_i16x4 __attribute__((ext_vector_type(4)));
 typedef short x6_i16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int wx_swz(int r) {
-#ifdef DGMC_WX_NOSWZ
-  return 0;
-#else
   return ((r & 3) << 2) | ((r >> 2) & 3);
-#endif
 }
 
 __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     X6Uses U, int nu, int64_t xplane, int64_t gplane,
     const int* __restrict__ src, const int* __restrict__ seg,
-    const int* __restrict__ items, int Kin, int C, float* __restrict__ part,
-    int dbg) {
+    const int* __restrict__ items, int Kin, int C, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char wx_smem[];
   DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)wx_smem;
   DGMC_LDS int* sidx =
@@ -575,38 +570,6 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
 
   const int pro = total < kWXNst - 1 ? total : kWXNst - 1;
   for (int q = 0; q < pro; ++q) stage(q, ring + (q % kWXNst) * kWXStage);
-  if (dbg & 8) {        // diagnostic: dump lane fragments of stage 0
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (dbg & 16) {      // settle: long pause before the transposed reads
-      for (int w = 0; w < 200; ++w) __builtin_amdgcn_s_sleep(100);
-      __syncthreads();
-    }
-    const x6_bf16x8 gv = frag(ring + 3 * kWXPlane, offG[0][0], offG[0][1]);
-    const x6_bf16x8 xv = frag(ring, offX[0][0], offX[0][1]);
-    if (blockIdx.x == 0 && tid < 64) {
-      for (int e = 0; e < 8; ++e) {
-        reinterpret_cast<__bf16*>(part)[tid * 16 + e] = gv[e];
-        reinterpret_cast<__bf16*>(part)[tid * 16 + 8 + e] = xv[e];
-      }
-      part[1024 + tid] = (float)offX[0][0];
-      part[1088 + tid] = (float)offX[0][1];
-      part[1152 + tid] = (float)(unsigned)(uintptr_t)(ring + offX[0][0]);
-      part[1216 + tid] = (float)(unsigned)(uintptr_t)(ring);
-      const x6_bf16x4 pl = *reinterpret_cast<const DGMC_LDS x6_bf16x4*>(
-          ring + offX[0][0]);
-      for (int e = 0; e < 4; ++e) part[1280 + 4 * tid + e] = (float)pl[e];
-    }
-    return;
-  }
-  if (dbg & 4) {        // diagnostic: dump stage 0 (6 plane images) + exit
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (blockIdx.x == 0)
-      for (int e = tid; e < kWXStage; e += 256)
-        reinterpret_cast<__bf16*>(part)[e] = ring[e];
-    return;
-  }
   for (int q = 0; q < total; ++q) {
     if (q + kWXNst - 1 < total) {
       stage(q + kWXNst - 1, ring + ((q + kWXNst - 1) % kWXNst) * kWXStage);
@@ -818,8 +781,7 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                      kWXLds, stream(), U, (int)nu, N * Kin, P * C,
                      src.data_ptr<int>(), seg.data_ptr<int>(),
                      it[0].data_ptr<int>(), (int)Kin, (int)C,
-                     part.data_ptr<float>(), x6_debug());
-  if (x6_debug() & 12) return part;
+                     part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return slot_fold_parts(part, it[1], S, Kin, C);
 }

@@ -429,6 +429,14 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 // multiple of 8 channels) and broadcast to the lanes' chains.
 // ---------------------------------------------------------------------------
 constexpr float kTopkTau = 1.0f / 8192.0f;
+// DGMC_TOPK_TAU_LOG2 (diagnostics): tau = 2^-value.
+static float topk_tau() {
+  static const float v = [] {
+    const char* e = getenv("DGMC_TOPK_TAU_LOG2");
+    return e ? ldexpf(1.0f, -atoi(e)) : kTopkTau;
+  }();
+  return v;
+}
 
 static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
                               int64_t k, at::Tensor* vals = nullptr);
@@ -478,7 +486,8 @@ __global__ __launch_bounds__(kRefRows * 64) void topk_refine_kernel(
     const float* __restrict__ h_s, const float* __restrict__ h_t,
     const int64_t* __restrict__ cand_i, const float* __restrict__ cand_v,
     const float* __restrict__ nmax_part, int nparts, int64_t* __restrict__ out,
-    int* __restrict__ n_overflow, int Ns, int Nt, int C, int k, int K2) {
+    int* __restrict__ n_overflow, int Ns, int Nt, int C, int k, int K2,
+    float tau) {
   __shared__ __attribute__((aligned(16))) float sa[kRefRows][264];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t g = (int64_t)blockIdx.x * kRefRows + wave;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(kRefRows * 64) void topk_refine_kernel(
     bm = fmaxf(bm, nmax_part[(size_t)b * nparts + p]);
   bm = wave_max(bm);
   // |a| |b|max with a relative safety factor for the (any-order) norms.
-  const float E = kTopkTau * sqrtf(sq * bm) * (1.0f + 1.0f / 1024.0f);
+  const float E = tau * sqrtf(sq * bm) * (1.0f + 1.0f / 1024.0f);
   const size_t o = ((size_t)b * Ns + g);
   const int ci = lane < K2 ? (int)cand_i[o * K2 + lane] : 0;
   const float cv = lane < K2 ? cand_v[o * K2 + lane] : -INFINITY;
@@ -589,7 +598,7 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
                      h_t.data_ptr<float>(), ci.data_ptr<int64_t>(),
                      cv.data_ptr<float>(), part.data_ptr<float>(), nparts,
                      out.data_ptr<int64_t>(), cnt.data_ptr<int>(), Ns, Nt, C,
-                     (int)k, K2);
+                     (int)k, K2, topk_tau());
   DGMC_CHECK_LAUNCH();
   return out;
 }
