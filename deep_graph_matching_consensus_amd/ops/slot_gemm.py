@@ -144,16 +144,18 @@ def weight_grad_x6(x3s, dy3s, plan, cin, cout):
     return out
 
 
-def _x6_images(weight, root):
-    """bf16x6 weight images of the forward (W^T) and the input gradient (W),
-    built once per forward scope and shared by the consensus loop's uses."""
+def _x6_images(weight, root, need_dx=True):
+    """bf16x6 weight images of the forward (W^T) and the input gradient (W,
+    only when ``need_dx``: psi_1 layer 0's input needs no gradient), built
+    once per forward scope and shared by the consensus loop's uses."""
     ops = _backend.ops()
     w = weight.detach().contiguous()
     r = root.detach().contiguous() if root is not None else None
     return (cached(('slot_wt3', id(weight)),
                    lambda: ops.slot_weight_x3(w, r, True)),
             cached(('slot_w3', id(weight)),
-                   lambda: ops.slot_weight_x3(w, r, False)))
+                   lambda: ops.slot_weight_x3(w, r, False))
+            if need_dx else None)
 
 
 class _SlotGemmSpMM(torch.autograd.Function):
@@ -169,7 +171,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
         if X6:
             # bf16x6: X split once (the planes are also the weight
             # gradient's operand), weight images once per forward scope.
-            wt3, ctx.w3 = _x6_images(weight, root)
+            wt3, ctx.w3 = _x6_images(weight, root, ctx.needs_input_grad[0])
             # (planes written by the producing SpMM when it was another
             # slot conv; valid while x is unmodified)
             pl = getattr(x, '_dgmc_x6', None)
