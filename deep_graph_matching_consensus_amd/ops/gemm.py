@@ -16,11 +16,49 @@ in ~33 us (s=16) and accumulates directly in fp32 for the fp32 master weight
 :func:`~..runtime.loopgrad.loop_scope` the weight/bias gradients of repeated
 uses are accumulated in place by the split-K combine / column-sum kernels.
 """
+import os
+
 import torch
 
 from . import _backend
 from ..runtime import loopgrad
 from ..runtime.cache import cached
+
+# fp32 node GEMMs (RelConv's stacked maps, encoder projections) as bf16x6 on
+# the matrix cores (csrc/hip/slot_gemm_x6.hip::dense_gemm_x6: three bf16
+# terms per operand, six products, two fp32 accumulators - error below the
+# exact fp32 MFMA chain).  Opt-in (DGMC_AMD_X6_DENSE=1): measured slower
+# than hipBLASLt fp32 on these shapes - DBP15K refinement step 6.75 ->
+# 6.99 ms (the [39k, 256] x [256, 768] maps: 142 us + 32 us operand split
+# vs ~140 us), PascalVOC neutral.
+X6_DENSE = os.environ.get('DGMC_AMD_X6_DENSE', '0') == '1'
+X6_DENSE_MIN_ROWS = 4096
+
+
+def dense_x6_supported(x, w):
+    """``x [M, K] @ w [K, N]`` in fp32 on the bf16x6 dense kernel."""
+    return (X6_DENSE and _backend.use_hip(x) and x.dtype == torch.float32
+            and w.dtype == torch.float32 and x.dim() == 2 and w.dim() == 2
+            and x.stride(1) == 1 and x.size(0) >= X6_DENSE_MIN_ROWS and
+            x.size(1) >= 64 and w.size(1) % 128 == 0)
+
+
+def dense_x6(x, w, bias=None):
+    """``x @ w (+ bias)`` (fp32 in, fp32 out) via bf16x6; the weight's bf16
+    planes are built once per forward scope."""
+    ops = _backend.ops()
+    K = w.size(0)
+    Kp = (K + 127) // 128 * 128
+    wd = w.detach()
+    w3 = cached(('dense_w3', wd.data_ptr(), wd._version, tuple(wd.shape),
+                 tuple(wd.stride()), Kp),
+                lambda: ops.dense_weight_x3(wd, Kp))
+    b = None
+    if bias is not None:
+        b = bias.detach()
+        if b.dtype != torch.float32 or not b.is_contiguous():
+            b = b.float().contiguous()
+    return ops.dense_gemm_x6(x, w3, b)
 
 
 def _split_factor(m, n, k):
@@ -121,7 +159,9 @@ class _MixedMatmul(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w_lp, bias, loop):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
-        if bias is not None:
+        if dense_x6_supported(xc, w_lp):
+            out = dense_x6(xc, w_lp, bias)
+        elif bias is not None:
             # Bias in the GEMM epilogue (hipBLASLt), cast once per forward.
             b_lp = bias if bias.dtype == w_lp.dtype else cached(
                 ('bias_lp', id(bias), w_lp.dtype),

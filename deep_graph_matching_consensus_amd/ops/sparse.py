@@ -313,7 +313,11 @@ class _GemmSpMM(torch.autograd.Function):
                 xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
                 relu, xc.dtype, None)
         else:
-            y = (xc @ w_lp).view(-1, C)
+            from .gemm import dense_x6, dense_x6_supported
+            if dense_x6_supported(xc, w_lp):
+                y = dense_x6(xc, w_lp).view(-1, C)      # fp32 as bf16x6
+            else:
+                y = (xc @ w_lp).view(-1, C)
             out_dtype = y.dtype if y.dtype in (torch.bfloat16,
                                                torch.float16) \
                 else torch.float32
