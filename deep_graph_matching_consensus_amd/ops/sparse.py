@@ -488,7 +488,16 @@ class _GemmSpMM(torch.autograd.Function):
             if gpass is not None and gpass.dtype == dY.dtype == \
                     ctx.x_dtype and gpass.shape == (dY.size(0),
                                                     w_lp.size(0)):
-                gx = torch.addmm(gpass, dY, w_lp.t())
+                if gpass.dim() == 2 and gpass.stride(1) == 1 and \
+                        gpass.stride(0) >= gpass.size(1):
+                    # In place: gpass is this op's own slice of the
+                    # concatenation's gradient (CatBackward hands out
+                    # disjoint column views nothing else reads), so the
+                    # GEMM accumulates into it with beta = 1 - no copy of
+                    # gpass into a fresh output first.
+                    gx = gpass.addmm_(dY, w_lp.t())
+                else:
+                    gx = torch.addmm(gpass, dY, w_lp.t())
                 gpass = None
             else:
                 gx = (dY @ w_lp.t()).to(ctx.x_dtype)
