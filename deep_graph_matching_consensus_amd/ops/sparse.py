@@ -325,6 +325,8 @@ class _GemmSpMM(torch.autograd.Function):
         ctx.save_for_backward(xc, w_lp, out if relu else None)
         ctx.op, ctx.relu, ctx.C, ctx.loop = op, relu, C, loop
         ctx.x_dtype, ctx.w_dtype = x.dtype, w.dtype
+        ctx.w_transposed = w.dim() == 2 and w.size(0) > 1 and \
+            w.size(1) > 1 and w.stride(0) == 1 and w.stride(1) == w.size(0)
         # Gradient carrier token of nn/conv.py::_StackedSplineWeight (an
         # expanded 1-element tensor): its node can take the loop-folded
         # weight gradient in slot-major layout directly (no permute copy, no
@@ -501,15 +503,23 @@ class _GemmSpMM(torch.autograd.Function):
                 gpass = None
             else:
                 gx = (dY @ w_lp.t()).to(ctx.x_dtype)
+        # w = (stacked weights).t() (RelConv): the gradient is produced in
+        # the stacked [3C, K] layout and handed back transposed, so the
+        # concatenation's backward gives each Linear a contiguous slice that
+        # AccumulateGrad keeps without a layout copy.
+        wt = ctx.w_transposed
         if loop is None:
             if ctx.needs_input_grad[1]:
-                gw = matmul_tn_fp32(xc.contiguous(), dY).to(ctx.w_dtype)
+                gw = (matmul_tn_fp32(dY, xc.contiguous()).t() if wt else
+                      matmul_tn_fp32(xc.contiguous(), dY)).to(ctx.w_dtype)
             if need_b:
                 gb = db.to(ctx.bias_dtype)
         elif loop.arrive():
             if ctx.needs_input_grad[1]:
                 X = loop.kept('x').contiguous()
-                gw = matmul_tn_fp32(X, loop.stack('dy').view(X.size(0), -1))
+                dYs = loop.stack('dy').view(X.size(0), -1)
+                gw = matmul_tn_fp32(dYs, X).t() if wt else \
+                    matmul_tn_fp32(X, dYs)
                 gw = gw.to(ctx.w_dtype)
             if need_b:
                 gb = loop_col_total(loop, 'b').to(ctx.bias_dtype)
