@@ -41,6 +41,7 @@ namespace {
 typedef __bf16 x6_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 x6_bf16x4 __attribute__((ext_vector_type(4)));
 typedef float x6_f32x16 __attribute__((ext_vector_type(16)));
+typedef float x6_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kX6BN = 128;                 // output columns per tile
 constexpr int kX6BK = 16;                  // k per staged chunk
@@ -228,17 +229,24 @@ __device__ __forceinline__ int x6_xcd_unit(const int* __restrict__ seg, int S,
 // XL (forward, K <= 256): workgroup b works on XCD b % 8's node eighth of
 // every slot, so the X rows it gathers (<= 1 / 8 of X) stay in that XCD's
 // L2 (grid = a multiple of 8, dispatched round-robin over the XCDs).
-template <bool GATHER, bool XL>
+// AF32 (input gradient from fp32 dY_c, no gather): the A operand is staged
+// as fp32 row images ([256][32] floats, 16-byte chunks XOR-swizzled by row
+// bits 1-3 - conflict-free ds_read_b128) and split into the three bf16
+// terms in registers: dY_c is stored at 4 instead of 6 bytes per element.
+template <bool GATHER, bool XL, bool AF32 = false>
 __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     const __bf16* __restrict__ A, int64_t a_plane, const int* __restrict__ src,
     const int* __restrict__ seg, int S, const __bf16* __restrict__ B,
     int64_t b_plane, int K, int Nn, const int* __restrict__ tiles, int tcap,
     float* __restrict__ Y, const float* __restrict__ bias, int m_lim,
     int dbg) {
+  // (stage sizes in bf16 units: A planes or the fp32 A image, then B)
+  constexpr int AREG = AF32 ? 2 * kXBM * kXBK : 3 * kXAPlane;
+  constexpr int STG = AREG + 3 * kXBPlane;
   extern __shared__ __attribute__((aligned(16))) char x6_smem[];
   DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)x6_smem;
   DGMC_LDS int* sidx =
-      (DGMC_LDS int*)(x6_smem + (size_t)2 * kXStage * 2);   // [2][256]
+      (DGMC_LDS int*)(x6_smem + (size_t)2 * STG * 2);   // [2][256]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
   const int ntn = Nn / kX6BN, nk = K / kXBK;
@@ -286,12 +294,27 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     br[e] = 16 * (t & 7) + lr;
     bq[e] = 8 * ((lane & 3) ^ x6_qswz(br[e]));
   }
+  // AF32 staging: wave w fills rows 32 w + 8 e + L / 8 (e < 4), lane L
+  // holds physical chunk L % 8 (4 floats) = logical (L % 8) ^ ((row >> 1) & 7).
+  int fr[4], fq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    fr[e] = 32 * wave + 8 * e + (lane >> 3);
+    fq[e] = 4 * ((lane & 7) ^ ((fr[e] >> 1) & 7));
+  }
+  const float* Af = reinterpret_cast<const float*>(A);
+  const float* frow[4] = {Af, Af, Af, Af};
   const bool bhi = wave >= 4;
   const __bf16* arow[2] = {A, A};
   const __bf16* brow = B;
   int bslot = 0;
   auto set_tile = [&](int j) {
     const int m0 = row_tile(j) * kXBM;
+    if (AF32) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        frow[e] = Af + (size_t)(m0 + fr[e]) * K + fq[e];
+    }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       int ix = m0 + ar[e];
@@ -314,15 +337,22 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
       idx_dma(j + 1);
     }
     if (dbg & 2) return;
-    DGMC_LDS __bf16* buf = ring + (it & 1) * kXStage;
+    DGMC_LDS __bf16* buf = ring + (it & 1) * STG;
     const int k0 = kc * kXBK;
+    if (AF32) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+      for (int e = 0; e < 4; ++e)
+        x6_dma16(reinterpret_cast<const __bf16*>(frow[e] + k0),
+                 buf + 2 * (32 * wave + 8 * e) * kXBK);
+    } else {
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-        x6_dma16(arow[e] + p * a_plane + k0,
-                 buf + p * kXAPlane + (32 * wave + 16 * e) * kXBK);
-    DGMC_LDS __bf16* bb = buf + 3 * kXAPlane;
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          x6_dma16(arow[e] + p * a_plane + k0,
+                   buf + p * kXAPlane + (32 * wave + 16 * e) * kXBK);
+    }
+    DGMC_LDS __bf16* bb = buf + AREG;
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       x6_dma16(brow + bp[e] * b_plane + (size_t)br[e] * K + k0 + bq[e],
@@ -347,7 +377,7 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   auto compute = [&](const DGMC_LDS __bf16* buf) {
     if (dbg & 1) return;
     const DGMC_LDS __bf16* la = buf;
-    const DGMC_LDS __bf16* lb = buf + 3 * kXAPlane;
+    const DGMC_LDS __bf16* lb = buf + AREG;
     x6_bf16x8 w[2][3][2], x[2][3][2];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
@@ -358,9 +388,31 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
         for (int a = 0; a < 2; ++a) {
           w[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
               lb + p * kXBPlane + offW + a * 32 * kXBK + qo);
-          x[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
-              la + p * kXAPlane + offX + a * 32 * kXBK + qo);
+          if (!AF32)
+            x[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
+                la + p * kXAPlane + offX + a * 32 * kXBK + qo);
         }
+      if (AF32) {
+        // 8 consecutive k of row r: logical chunks 4 st + 2 h, + 1.
+        const DGMC_LDS float* lf = reinterpret_cast<const DGMC_LDS float*>(la);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int r = wm * 64 + a * 32 + i;
+          const int sw = (r >> 1) & 7, c0 = 4 * st + 2 * h;
+          const x6_f32x4 u0 = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+              lf + r * kXBK + 4 * (c0 ^ sw));
+          const x6_f32x4 u1 = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+              lf + r * kXBK + 4 * ((c0 + 1) ^ sw));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            __bf16 hh, mm, ll;
+            x6_split(e < 4 ? u0[e] : u1[e - 4], hh, mm, ll);
+            x[st][0][a][e] = hh;
+            x[st][1][a][e] = mm;
+            x[st][2][a][e] = ll;
+          }
+        }
+      }
     }
 #pragma unroll
     for (int st = 0; st < 2; ++st)
@@ -421,7 +473,7 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     x6_barrier();
     if (it + 1 < total) stage(it + 1);
-    compute(ring + (it & 1) * kXStage);
+    compute(ring + (it & 1) * STG);
     const int j = it / nk;
     if (it - j * nk == nk - 1) epilogue(j);
   }
@@ -463,14 +515,22 @@ __device__ __forceinline__ int wx_swz(int r) {
   return ((r & 3) << 2) | ((r >> 2) & 3);
 }
 
+// GF32: dY_u is fp32 [P][C] (4 instead of 6 bytes per element): staged as
+// [16 rows][128 floats] images (16-byte chunks XOR 8 for rows 8-15, so the
+// two half-waves' column reads hit disjoint banks), read column-wise
+// (8 x ds_read_b32 per fragment) and split into bf16 terms in registers.
+constexpr int kWXStageF = 3 * kWXPlane + 2 * kWXPlane;   // X planes + fp32 dY
+
+template <bool GF32>
 __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     X6Uses U, int nu, int64_t xplane, int64_t gplane,
     const int* __restrict__ src, const int* __restrict__ seg,
     const int* __restrict__ items, int Kin, int C, float* __restrict__ part) {
+  constexpr int STG = GF32 ? kWXStageF : kWXStage;
   extern __shared__ __attribute__((aligned(16))) char wx_smem[];
   DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)wx_smem;
   DGMC_LDS int* sidx =
-      (DGMC_LDS int*)(wx_smem + (size_t)kWXNst * kWXStage * 2);
+      (DGMC_LDS int*)(wx_smem + (size_t)kWXNst * STG * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
   const int tiles_n = C / 128, tiles = (Kin / 128) * tiles_n;
@@ -494,18 +554,37 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
   // logical chunk (L % 16) ^ swz(row).
   const int srow = 4 * wave + (lane >> 4);
   const int schunk = (lane & 15) ^ wx_swz(srow);
+  // GF32 dY staging: wave w fills rows 4 w + 2 e + L / 32 (e < 2); lane L
+  // holds physical chunk L % 32 = logical (L % 32) ^ (8 (row >> 3 & 1)).
+  int gfr[2], gfq[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    gfr[e] = 4 * wave + 2 * e + (lane >> 5);
+    gfq[e] = 4 * ((lane & 31) ^ (8 * ((gfr[e] >> 3) & 1)));
+  }
   auto stage = [&](int q, DGMC_LDS __bf16* buf) {
     const int qq = qb + q;
     const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
     const int row = ch * kWXRows + srow;
     const __bf16* xr = U.x[u] + (size_t)sidx[row] * Kin + i0 + 8 * schunk;
-    const __bf16* gr = U.g[u] + (size_t)(pb + row) * C + n0 + 8 * schunk;
     DGMC_LDS __bf16* d = buf + 4 * wave * 128;
 #pragma unroll
     for (int p = 0; p < 3; ++p) x6_dma16(xr + p * xplane, d + p * kWXPlane);
+    if (GF32) {
+      const float* gf = reinterpret_cast<const float*>(U.g[u]) +
+                        (size_t)(pb + ch * kWXRows) * C + n0;
+      DGMC_LDS __bf16* dg = buf + 3 * kWXPlane;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      x6_dma16(gr + p * gplane, d + (3 + p) * kWXPlane);
+      for (int e = 0; e < 2; ++e)
+        x6_dma16(reinterpret_cast<const __bf16*>(gf + (size_t)gfr[e] * C +
+                                                 gfq[e]),
+                 dg + 2 * (4 * wave + 2 * e) * 128);
+    } else {
+      const __bf16* gr = U.g[u] + (size_t)(pb + row) * C + n0 + 8 * schunk;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        x6_dma16(gr + p * gplane, d + (3 + p) * kWXPlane);
+    }
   };
 
   // Transposed fragment reads: 16-lane group g = lane / 16 covers columns
@@ -555,9 +634,30 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     for (int p = 0; p < 3; ++p)
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        gv[p][a] = frag(buf + (3 + p) * kWXPlane, offG[a][0], offG[a][1]);
+        if (!GF32)
+          gv[p][a] = frag(buf + (3 + p) * kWXPlane, offG[a][0], offG[a][1]);
         xv[p][a] = frag(buf + p * kWXPlane, offX[a][0], offX[a][1]);
       }
+    if (GF32) {
+      // A operand dY^T: lane l -> column c = wn 64 + 32 a + l % 32, rows
+      // 8 (l / 32) + j, j < 8.
+      const DGMC_LDS float* gf =
+          reinterpret_cast<const DGMC_LDS float*>(buf + 3 * kWXPlane);
+      const int hl = lane >> 5;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int c = wn * 64 + a * 32 + (lane & 31);
+        const int pc = 4 * ((c >> 2) ^ (8 * hl)) + (c & 3);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 hh, mm, ll;
+          x6_split(gf[(8 * hl + j) * 128 + pc], hh, mm, ll);
+          gv[0][a][j] = hh;
+          gv[1][a][j] = mm;
+          gv[2][a][j] = ll;
+        }
+      }
+    }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -575,16 +675,20 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
   };
 
   const int pro = total < kWXNst - 1 ? total : kWXNst - 1;
-  for (int q = 0; q < pro; ++q) stage(q, ring + (q % kWXNst) * kWXStage);
+  for (int q = 0; q < pro; ++q) stage(q, ring + (q % kWXNst) * STG);
   for (int q = 0; q < total; ++q) {
     if (q + kWXNst - 1 < total) {
-      stage(q + kWXNst - 1, ring + ((q + kWXNst - 1) % kWXNst) * kWXStage);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      stage(q + kWXNst - 1, ring + ((q + kWXNst - 1) % kWXNst) * STG);
+      // (this thread's DMAs of the two stages still in flight)
+      if (GF32)
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     x6_barrier();
-    compute(ring + (q % kWXNst) * kWXStage);
+    compute(ring + (q % kWXNst) * STG);
     x6_barrier();
   }
   // acc[a][b]: rows c = wn 64 + 32 a + 8 qd + 4 h + e, column i = wm 64 +
@@ -685,23 +789,32 @@ static int x6_debug() {
 at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
                         const at::Tensor& seg, const at::Tensor& b3,
                         bool gather, const c10::optional<at::Tensor>& tiles) {
-  TORCH_CHECK(a3.is_cuda() && a3.scalar_type() == at::kBFloat16 &&
-                  a3.is_contiguous() && a3.dim() == 3 && a3.size(0) == 3,
-              "slot_gemm_x6: bf16 A planes [3, R, K]");
+  // A: bf16 planes [3, R, K], or (input gradient, no gather) fp32 [R, K]
+  // split in the kernel.
+  const bool af32 = a3.scalar_type() == at::kFloat;
+  TORCH_CHECK(a3.is_cuda() && a3.is_contiguous() &&
+                  (af32 ? (a3.dim() == 2 && !gather &&
+                           aligned16(a3.data_ptr()))
+                        : (a3.scalar_type() == at::kBFloat16 &&
+                           a3.dim() == 3 && a3.size(0) == 3)),
+              "slot_gemm_x6: bf16 A planes [3, R, K] or fp32 A [R, K] "
+              "(no gather)");
   TORCH_CHECK(b3.scalar_type() == at::kBFloat16 && b3.is_contiguous() &&
                   b3.dim() == 4 && b3.size(0) == 3,
               "slot_gemm_x6: bf16 B planes [3, S, Nn, K]");
   const int64_t S = seg.numel() - 1;
   const int64_t Nn = b3.size(2), K = b3.size(3);
   TORCH_CHECK(b3.size(1) == S && S <= kX6MaxS, "slot_gemm_x6: slot count");
-  TORCH_CHECK(a3.size(2) == K, "slot_gemm_x6: A [*, K]");
+  TORCH_CHECK(a3.size(a3.dim() - 1) == K, "slot_gemm_x6: A [*, K]");
   TORCH_CHECK(K % 128 == 0 && Nn % kX6BN == 0,
               "slot_gemm_x6: K, Nn multiples of 128");
   const int64_t P = src.numel();
   TORCH_CHECK(P % kXBM == 0 && src.scalar_type() == at::kInt &&
                   seg.scalar_type() == at::kInt,
               "slot_gemm_x6: int32 src [P_cap % 256], seg");
-  if (!gather) TORCH_CHECK(a3.size(1) == P, "slot_gemm_x6: rows == P_cap");
+  if (!gather) {
+    TORCH_CHECK(a3.size(a3.dim() - 2) == P, "slot_gemm_x6: rows == P_cap");
+  }
   const bool listed = tiles.has_value() && tiles->defined();
   if (listed)
     TORCH_CHECK(tiles->scalar_type() == at::kInt &&
@@ -720,15 +833,20 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   // XCD-local forward tiles where the gathered X (and the weights) fit the
   // XCDs' L2s (K <= 256); the 1024-wide psi_1 layer streams.
   const bool xl = gather && !listed && K <= x6_xl_kmax() && blocks >= 64;
-  auto kern = gather ? (xl ? slot_gemm_x6_kernel<true, true>
-                           : slot_gemm_x6_kernel<true, false>)
-                     : slot_gemm_x6_kernel<false, false>;
+  auto kern = af32 ? slot_gemm_x6_kernel<false, false, true>
+              : gather ? (xl ? slot_gemm_x6_kernel<true, true>
+                             : slot_gemm_x6_kernel<true, false>)
+                       : slot_gemm_x6_kernel<false, false>;
   const int64_t grid = xl ? blocks / kNumXcd * kNumXcd : blocks;
+  const size_t lds = af32 ? (size_t)2 * (2 * kXBM * kXBK + 3 * kXBPlane) * 2 +
+                                2 * kXBM * 4
+                          : kXLds;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kXThreads), kXLds, stream(), ap,
-                     a3.size(1) * K, src.data_ptr<int>(), seg.data_ptr<int>(),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kXThreads), lds, stream(), ap,
+                     af32 ? 0 : a3.size(1) * K, src.data_ptr<int>(),
+                     seg.data_ptr<int>(),
                      (int)S, bp, S * Nn * K, (int)K, (int)Nn, tl,
                      (int)(P / kXBM), Y.data_ptr<float>(), nullptr,
                      (int)P, x6_debug());
@@ -874,7 +992,11 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const int64_t nu = (int64_t)xs.size();
   TORCH_CHECK(nu >= 1 && nu <= kWXMaxU && (int64_t)gs.size() == nu,
               "slot_wgrad_x6: 1 <= uses <= 16, one dY per X");
-  const int64_t N = xs[0].size(1), Kin = xs[0].size(2), C = gs[0].size(2);
+  // dY_u: bf16 planes [3, P_cap, out] or fp32 [P_cap, out] (split in
+  // the kernel).
+  const bool gf32 = gs[0].scalar_type() == at::kFloat;
+  const int64_t N = xs[0].size(1), Kin = xs[0].size(2);
+  const int64_t C = gf32 ? gs[0].size(1) : gs[0].size(2);
   const int64_t P = src.numel(), S = seg.numel() - 1;
   TORCH_CHECK(Kin % 128 == 0 && C % 128 == 0 && P % kWXRows == 0 &&
                   rounds >= 1 && S <= kX6MaxS && src.scalar_type() == at::kInt,
@@ -887,10 +1009,17 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                     x.is_contiguous() && x.dim() == 3 && x.size(0) == 3 &&
                     x.size(1) == N && x.size(2) == Kin,
                 "slot_wgrad_x6: X_u bf16 planes [3, N, in]");
-    TORCH_CHECK(g.scalar_type() == at::kBFloat16 && g.is_contiguous() &&
-                    g.dim() == 3 && g.size(0) == 3 && g.size(1) == P &&
-                    g.size(2) == C,
-                "slot_wgrad_x6: dY_u bf16 planes [3, P_cap, out]");
+    if (gf32) {
+      TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous() &&
+                      g.dim() == 2 && g.size(0) == P && g.size(1) == C &&
+                      aligned16(g.data_ptr()),
+                  "slot_wgrad_x6: dY_u fp32 [P_cap, out] (all uses alike)");
+    } else {
+      TORCH_CHECK(g.scalar_type() == at::kBFloat16 && g.is_contiguous() &&
+                      g.dim() == 3 && g.size(0) == 3 && g.size(1) == P &&
+                      g.size(2) == C,
+                  "slot_wgrad_x6: dY_u bf16 planes [3, P_cap, out]");
+    }
     U.x[u] = reinterpret_cast<const __bf16*>(x.data_ptr());
     U.g[u] = reinterpret_cast<const __bf16*>(g.data_ptr());
   }
@@ -904,14 +1033,16 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const int64_t per = Kin * C;
   at::Tensor part =
       at::empty({G_cap, per}, xs[0].options().dtype(at::kFloat));
+  auto kern = gf32 ? slot_wgrad_x6_kernel<true> : slot_wgrad_x6_kernel<false>;
+  const size_t lds = (size_t)kWXNst * (gf32 ? kWXStageF : kWXStage) * 2 +
+                     kWXMaxRows * 4;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
-      reinterpret_cast<const void*>(slot_wgrad_x6_kernel),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWXLds));
-  hipLaunchKernelGGL(slot_wgrad_x6_kernel, dim3(G_cap * tiles), dim3(256),
-                     kWXLds, stream(), U, (int)nu, N * Kin, P * C,
-                     src.data_ptr<int>(), seg.data_ptr<int>(),
-                     it[0].data_ptr<int>(), (int)Kin, (int)C,
-                     part.data_ptr<float>());
+      reinterpret_cast<const void*>(kern),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, dim3(G_cap * tiles), dim3(256), lds, stream(), U,
+                     (int)nu, N * Kin, P * C, src.data_ptr<int>(),
+                     seg.data_ptr<int>(), it[0].data_ptr<int>(), (int)Kin,
+                     (int)C, part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return slot_fold_parts(part, it[1], S, Kin, C);
 }

@@ -47,6 +47,9 @@ X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
 # (+0.03 ms per PascalVOC step for the extra fold); PIECES_ALWAYS=1 pieces
 # regardless (tests compare a one-rank RCCL run bit-for-bit with that).
 PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
+# bf16x6 backward on fp32 dY_c (split inside the dX / dW kernels' LDS
+# staging) instead of the rowmap SpMM writing three bf16 planes.
+F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
 PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
 PIECE_BYTES = 8 << 20
 
@@ -226,7 +229,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
         At = op.t()
         dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
                                     plan.seg, rowmap_ranges(plan, At),
-                                    ctx.x6)
+                                    ctx.x6 and not F32DY)
         gx = None
         if ctx.needs_input_grad[0] and ctx.x6:
             # dY_c planes straight from the rowmap SpMM; 256-row tiles of

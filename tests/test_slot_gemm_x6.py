@@ -141,6 +141,78 @@ def test_x6_dx_tile_list(headline_plan):
                            full[t * 256:(t + 1) * 256])
 
 
+@pytest.mark.parametrize('cin,cout', [(128, 128), (256, 256), (1024, 256)])
+def test_x6_input_grad_fp32_operand_equals_planes(headline_plan, cin, cout):
+    """fp32 dY_c split inside the dX kernel's LDS staging gives bit-for-bit
+    the planes path's result (same split, same MFMA order), full and with
+    a row-tile list."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(5 + cin)
+    P = plan.src.numel()
+    dy = torch.randn(P, cout, device=DEV, generator=g)
+    w = torch.randn(25, cin, cout, device=DEV, generator=g) / cout ** 0.5
+    r = torch.randn(cin, cout, device=DEV, generator=g) / cout ** 0.5
+    b3 = ops.slot_weight_x3(w, r, False)
+    for tiles in (None, sg.dx_tiles(plan, N // 2, unit=256)):
+        zp = ops.slot_gemm_x6(ops.split3(dy), plan.src, plan.seg, b3, False,
+                              tiles)
+        zf = ops.slot_gemm_x6(dy, plan.src, plan.seg, b3, False, tiles)
+        if tiles is None:
+            used = int(plan.seg[-1])      # rows past seg[S] are not written
+            assert torch.equal(zf[:used], zp[:used]), float(
+                (zf[:used] - zp[:used]).abs().max())
+        else:
+            for t in tiles[:int(tiles[-1])].tolist():
+                assert torch.equal(zf[t * 256:(t + 1) * 256],
+                                   zp[t * 256:(t + 1) * 256])
+
+
+@pytest.mark.parametrize('cin,cout,uses', [(128, 128, 10), (256, 256, 1),
+                                           (1024, 256, 1)])
+def test_x6_weight_grad_fp32_dy_equals_planes(headline_plan, cin, cout,
+                                              uses):
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(13 + cin)
+    P = plan.src.numel()
+    used = int(plan.seg[-1])
+    xs = [ops.split3(torch.randn(N, cin, device=DEV, generator=g))
+          for _ in range(uses)]
+    dys = []
+    for _ in range(uses):
+        d = torch.randn(P, cout, device=DEV, generator=g)
+        d[used:] = 0
+        d[plan.src.long() < 0] = 0
+        dys.append(d)
+    rounds = 1 if cin == 128 else (2 if cin == 256 else 6)
+    wp = ops.slot_wgrad_x6(xs, [ops.split3(d) for d in dys], plan.src,
+                           plan.seg, rounds)
+    wf = ops.slot_wgrad_x6(xs, dys, plan.src, plan.seg, rounds)
+    assert torch.equal(wf, wp), float((wf - wp).abs().max())
+
+
+def test_x6_f32dy_training_step_matches_planes(monkeypatch):
+    """The gated fp32-dY backward gives the planes backward's gradients."""
+    from deep_graph_matching_consensus_amd.nn.conv import SplineConv
+    torch.manual_seed(0)
+    N = 600
+    ei = torch.randint(N, (2, 4 * N), device=DEV)
+    ea = torch.rand(ei.size(1), 2, device=DEV)
+    conv = SplineConv(128, 128, 2, kernel_size=5).to(DEV)
+    x = torch.randn(N, 128, device=DEV, requires_grad=True)
+    grads = []
+    for flag in (False, True):
+        monkeypatch.setattr(sg, 'F32DY', flag)
+        conv.zero_grad()
+        x.grad = None
+        conv(x, ei, ea).square().sum().backward()
+        grads.append([x.grad.clone()] +
+                     [p.grad.clone() for p in conv.parameters()])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
 def test_split3_reconstructs_fp32():
     ops = _backend.ops()
     x = torch.randn(1000, 64, device=DEV) * torch.logspace(
