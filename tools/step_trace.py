@@ -7,6 +7,8 @@ kernel time, kernel count, idle gaps and a per-kernel-name table.
 
     python tools/step_trace.py \
         gpurun_out/prof/.../run_kernel_trace.csv [marker]
+
+(or the ``run_results.db`` rocprofv3 writes by default.)
 """
 import collections
 import csv
@@ -16,7 +18,14 @@ import sys
 def main():
     path = sys.argv[1]
     marker = sys.argv[2] if len(sys.argv) > 2 else 'adam_multi_kernel'
-    rows = list(csv.DictReader(open(path)))
+    if path.endswith('.db'):
+        import sqlite3
+        con = sqlite3.connect(path)
+        rows = [{'Kernel_Name': n, 'Start_Timestamp': a, 'End_Timestamp': b}
+                for n, a, b in con.execute(
+                    'select name, start, end from kernels')]
+    else:
+        rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     ends = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
     if len(ends) < 2:
