@@ -273,6 +273,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const c10::optional<at::Tensor>& seg,
                             const c10::optional<at::Tensor>& ranges,
                             bool planes);
+at::Tensor slot_rowmap_ell(const at::Tensor& rowptr, const at::Tensor& col,
+                           const at::Tensor& val, const at::Tensor& cinv);
 at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
                               const at::Tensor& cinv);
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
@@ -506,6 +508,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "Tensor g, Tensor? seg=None, Tensor? ranges=None, bool planes=False) -> "
       "Tensor");
   m.def("slot_rowmap_ranges(Tensor rowptr, Tensor cinv) -> Tensor");
+  m.def("slot_rowmap_ell(Tensor rowptr, Tensor col, Tensor val, Tensor cinv) "
+        "-> Tensor");
   m.def(
       "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add, "
       "int row0=0) -> Tensor");
@@ -602,6 +606,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("dense_wgrad_f32", &dgmc::dense_wgrad_f32);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_rowmap_ranges", &dgmc::slot_rowmap_ranges);
+  m.impl("slot_rowmap_ell", &dgmc::slot_rowmap_ell);
   m.impl("slot_gather_sum", &dgmc::slot_gather_sum);
   m.impl("slot_wgrad_f32", &dgmc::slot_wgrad_f32);
   m.impl("sinkhorn_fwd", &dgmc::sinkhorn_fwd);

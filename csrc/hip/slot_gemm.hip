@@ -1065,6 +1065,33 @@ __global__ __launch_bounds__(256) void sg_rowmap_ranges_kernel(
   out[p] = c >= 0 ? make_int2(rowptr[c], rowptr[c + 1]) : make_int2(0, 0);
 }
 
+// Inline entry table ("ELL"), 32 bytes per compact row: {c0, c1, c2, n} and
+// {v0, v1, v2, e0} (values as float bits).  Rows with n <= 3 entries (nearly
+// all) need no (col, val) round after the table load; longer rows walk
+// col / val from e0.
+__global__ __launch_bounds__(256) void sg_rowmap_ell_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col,
+    const float* __restrict__ val, const int* __restrict__ cinv, int P,
+    int4* __restrict__ out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int c = cinv[p];
+  const int e0 = c >= 0 ? rowptr[c] : 0, n = c >= 0 ? rowptr[c + 1] - e0 : 0;
+  int cc[3] = {0, 0, 0};
+  float vv[3] = {0.f, 0.f, 0.f};
+  if (n <= 3) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (u < n) {
+        cc[u] = col[e0 + u];
+        vv[u] = val[e0 + u];
+      }
+  }
+  out[2 * p] = make_int4(cc[0], cc[1], cc[2], n);
+  out[2 * p + 1] = make_int4(__float_as_int(vv[0]), __float_as_int(vv[1]),
+                             __float_as_int(vv[2]), e0);
+}
+
 typedef __bf16 sg_bf16x4 __attribute__((ext_vector_type(4)));
 
 // fp32 -> three bf16 terms hi + mid + lo (round-to-nearest at each stage;
@@ -1087,7 +1114,8 @@ template <int LPR, bool XL>
 __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col,
     const float* __restrict__ val, const int* __restrict__ cinv,
-    const int2* __restrict__ ranges, const int* __restrict__ seg, int S,
+    const int2* __restrict__ ranges, const int4* __restrict__ ell,
+    const int* __restrict__ seg, int S,
     const float* __restrict__ g, float* __restrict__ out,
     __bf16* __restrict__ out3, int P, int C) {
   constexpr int RPB = 256 / LPR;
@@ -1106,7 +1134,15 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
   // at seg[S]); padding rows inside segments are written as zeros.
   if (p >= P || (seg != nullptr && p >= seg[S])) return;
   int e0, e1;
-  if (ranges != nullptr) {
+  int4 ec = make_int4(0, 0, 0, 0), ev = make_int4(0, 0, 0, 0);
+  bool inl = false;
+  if (ell != nullptr) {
+    ec = ell[2 * p];
+    ev = ell[2 * p + 1];
+    inl = ec.w <= 3;
+    e0 = ev.w;
+    e1 = inl ? e0 : e0 + ec.w;
+  } else if (ranges != nullptr) {
     const int2 r = ranges[p];
     e0 = r.x;
     e1 = r.y;
@@ -1117,6 +1153,25 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
   }
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (inl) {     // entries from the table: one g round
+      const int n = ec.w;
+      const int cs[3] = {ec.x, ec.y, ec.z};
+      const int vs[3] = {ev.x, ev.y, ev.z};
+      float4 v[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        v[u] = u < n ? ld4(g + (size_t)cs[u] * C + c0)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (u < n) {
+          const float w = __int_as_float(vs[u]);
+          acc.x = fmaf(w, v[u].x, acc.x);
+          acc.y = fmaf(w, v[u].y, acc.y);
+          acc.z = fmaf(w, v[u].z, acc.z);
+          acc.w = fmaf(w, v[u].w, acc.w);
+        }
+    }
     int e = e0;
     for (; e + 4 <= e1; e += 4) {
       float4 v[4];
@@ -1200,11 +1255,15 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
     S = (int)seg->numel() - 1;
   }
   const int2* rg = nullptr;
+  const int4* el = nullptr;
   if (ranges.has_value() && ranges->defined()) {
     TORCH_CHECK(ranges->scalar_type() == at::kInt && ranges->is_contiguous() &&
-                    ranges->numel() == 2 * P,
-                "slot_spmm_rowmap: int32 ranges [P, 2]");
-    rg = reinterpret_cast<const int2*>(ranges->data_ptr<int>());
+                    (ranges->numel() == 2 * P || ranges->numel() == 8 * P),
+                "slot_spmm_rowmap: int32 ranges [P, 2] or entry table [P, 8]");
+    if (ranges->numel() == 8 * P)
+      el = reinterpret_cast<const int4*>(ranges->data_ptr<int>());
+    else
+      rg = reinterpret_cast<const int2*>(ranges->data_ptr<int>());
   }
   const bool xl = segp != nullptr;      // XCD-local row groups (above)
   const int lanes = (int)(C / 4);
@@ -1219,7 +1278,8 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                    : sg_spmm_rowmap_kernel<L, false>;
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, stream(),
                        rowptr.data_ptr<int>(), col.data_ptr<int>(),
-                       val.data_ptr<float>(), cinv.data_ptr<int>(), rg, segp,
+                       val.data_ptr<float>(), cinv.data_ptr<int>(), rg, el,
+                       segp,
                        S, g.data_ptr<float>(), op, op3, (int)P, (int)C);
   };
   if (lanes <= 8) go(std::integral_constant<int, 8>());
@@ -1304,6 +1364,28 @@ at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
                      dim3(256), 0, stream(), rowptr.data_ptr<int>(),
                      cinv.data_ptr<int>(), (int)P,
                      reinterpret_cast<int2*>(out.data_ptr<int>()));
+  DGMC_CHECK_LAUNCH();
+  return out;
+}
+
+at::Tensor slot_rowmap_ell(const at::Tensor& rowptr, const at::Tensor& col,
+                           const at::Tensor& val, const at::Tensor& cinv) {
+  TORCH_CHECK(rowptr.is_cuda() && rowptr.scalar_type() == at::kInt &&
+                  col.scalar_type() == at::kInt &&
+                  val.scalar_type() == at::kFloat &&
+                  cinv.scalar_type() == at::kInt && cinv.is_contiguous() &&
+                  rowptr.is_contiguous() && col.is_contiguous() &&
+                  val.is_contiguous(),
+              "slot_rowmap_ell: int32 rowptr / col / cinv, fp32 val");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(cinv.device());
+  const int64_t P = cinv.numel();
+  at::Tensor out = at::empty({P, 8}, cinv.options());
+  if (P == 0) return out;
+  hipLaunchKernelGGL(sg_rowmap_ell_kernel, dim3((unsigned)((P + 255) / 256)),
+                     dim3(256), 0, stream(), rowptr.data_ptr<int>(),
+                     col.data_ptr<int>(), val.data_ptr<float>(),
+                     cinv.data_ptr<int>(), (int)P,
+                     reinterpret_cast<int4*>(out.data_ptr<int>()));
   DGMC_CHECK_LAUNCH();
   return out;
 }

@@ -50,6 +50,7 @@ PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
 # bf16x6 backward on fp32 dY_c (split inside the dX / dW kernels' LDS
 # staging) instead of the rowmap SpMM writing three bf16 planes.
 F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
+ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
 PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
 PIECE_BYTES = 8 << 20
 
@@ -80,14 +81,19 @@ def dx_tiles(plan, row0, unit=BM):
 
 
 def rowmap_ranges(plan, At):
-    """``[P_cap, 2]`` int32 A^T entry range of every compact row, built once
-    per plan and transposed operator (shared by the step's rowmap SpMMs)."""
+    """A^T entries of every compact row, built once per plan and transposed
+    operator (shared by the step's rowmap SpMMs): the ``[P_cap, 8]`` inline
+    entry table (``ROWMAP_ELL``: up to three (col, val) pairs per row, one
+    dependent load round fewer) or ``[P_cap, 2]`` int32 ranges."""
     cache = plan.__dict__.setdefault('_ranges', {})
-    key = At.rowptr.data_ptr()
+    key = (At.rowptr.data_ptr(), At.col.data_ptr(), At.val.data_ptr(),
+           ROWMAP_ELL)
     r = cache.get(key)
     if r is None:
-        r = cache[key] = _backend.ops().slot_rowmap_ranges(At.rowptr,
-                                                           plan.cinv)
+        ops = _backend.ops()
+        r = cache[key] = ops.slot_rowmap_ell(
+            At.rowptr, At.col, At.val, plan.cinv) if ROWMAP_ELL else \
+            ops.slot_rowmap_ranges(At.rowptr, plan.cinv)
     return r
 
 

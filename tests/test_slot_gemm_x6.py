@@ -289,6 +289,37 @@ def test_rowmap_planes_equal_split_of_fp32(headline_plan):
     assert torch.equal(p3[:, :used], ops.split3(f32)[:, :used])
 
 
+def test_rowmap_entry_table_equals_ranges(headline_plan):
+    """The inline (col, val) entry table gives the range walk's rows bit for
+    bit, including rows with more than three entries (table fallback)."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.randn(N, 128, device=DEV)
+    R = N * 26
+    gen = torch.Generator().manual_seed(4)
+    rows = torch.randint(R, (4 * N, ), generator=gen)
+    heavy = plan.cinv[plan.cinv >= 0][:64].cpu().long()
+    rows = torch.cat([rows, heavy.repeat_interleave(7)]).sort()[0]
+    rowptr = torch.zeros(R + 1, dtype=torch.long)
+    rowptr[1:] = torch.bincount(rows, minlength=R).cumsum(0)
+    col = torch.randint(N, (rows.numel(), ), generator=gen).int()
+    val = torch.rand(rows.numel(), generator=gen)
+    rowptr, col, val = rowptr.int().to(DEV), col.to(DEV), val.to(DEV)
+    rg = ops.slot_rowmap_ranges(rowptr, plan.cinv)
+    ell = ops.slot_rowmap_ell(rowptr, col, val, plan.cinv)
+    assert int((ell[:, 3] > 3).sum()) >= 64
+    used = int(plan.seg[-1])
+    for planes in (False, True):
+        a = ops.slot_spmm_rowmap(rowptr, col, val, plan.cinv, g, plan.seg,
+                                 rg, planes)
+        b = ops.slot_spmm_rowmap(rowptr, col, val, plan.cinv, g, plan.seg,
+                                 ell, planes)
+        if planes:
+            assert torch.equal(a[:, :used], b[:, :used])
+        else:
+            assert torch.equal(a[:used], b[:used])
+
+
 def test_spmm_planes_feed_next_conv():
     """A non-last fp32 SplineConv's aggregation also writes the bf16x6
     planes of its output (== split3 of it, bitwise); the next conv consumes
