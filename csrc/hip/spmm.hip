@@ -486,69 +486,76 @@ __global__ __launch_bounds__(256) void spmm_split_kernel(
   for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
   if (b < nb_short) {
     const int idx = b * PPB + q;
-    if (idx >= n_short || c0 >= C) return;
+    if (idx >= n_short) return;      // (whole lane groups: shuffles below)
     const int r = short_rows[idx];
     const int beg = rowptr[r], end = rowptr[r + 1];
-    int p = beg;
-    for (; p + 4 <= end; p += 4) {
-      float xv[4][VEC];
-      float w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        w[u] = val[p + u];
-        load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
+    // The group's G lanes load G (col, val) entries at once and broadcast
+    // them by shuffles, so every gather of a G-entry batch is in flight
+    // together: rowptr -> (col, val) -> x is three latency rounds per batch
+    // instead of two per 4 entries.  Entries are summed in row order.
+    const int gbase = threadIdx.x & 63 & ~(G - 1);
+    for (int p = beg; p < end; p += G) {
+      const int cnt = min(G, end - p);
+      int mc = 0;
+      float mv = 0.f;
+      if (gl < cnt) {
+        mc = col[p + gl];
+        mv = val[p + gl];
       }
+      float xv[G][VEC];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
-    }
-    if (p < end) {
-      float xv[4][VEC];
-      float w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        w[u] = 0.f;
+      for (int u = 0; u < G; ++u) {
+        const int cu = __shfl(mc, gbase + u);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) xv[u][k] = 0.f;
-        if (p + u < end) {
-          w[u] = val[p + u];
-          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
-        }
+        if (u < cnt && c0 < C)
+          load_vec<TIn, VEC>(x + (size_t)cu * C + c0, xv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < G; ++u) {
+        const float w = __shfl(mv, gbase + u);
+        if (u < cnt)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
+          for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[u][k], acc[k]);
+      }
     }
-    spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu,
-                                out);
+    if (c0 < C)
+      spmm_finish<TIn, TOut, VEC>(acc, r, c0, C, self_x, scale, bias, relu,
+                                  out);
     return;
   }
   // Long row: the whole block (block-uniform branch).
   const int r = long_rows[b - nb_short];
   const int beg = rowptr[r], end = rowptr[r + 1];
-  if (c0 < C) {
-    int e = beg + q;
-    for (; e + 3 * PPB < end; e += 4 * PPB) {
-      float xv[4][VEC];
-      float w[4];
+  {
+    // Chunks of 256 entries: every thread loads one (col, val), group q
+    // takes entries q G .. q G + G - 1 of the chunk (broadcast by shuffles,
+    // G gathers in flight per lane).
+    const int gbase = threadIdx.x & 63 & ~(G - 1);
+    for (int p = beg + q * G; p < end; p += 256) {
+      const int cnt = min(G, end - p);
+      int mc = 0;
+      float mv = 0.f;
+      if (gl < cnt) {
+        mc = col[p + gl];
+        mv = val[p + gl];
+      }
+      float xv[G][VEC];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        w[u] = val[e + u * PPB];
-        load_vec<TIn, VEC>(x + (size_t)col[e + u * PPB] * C + c0, xv[u]);
+      for (int u = 0; u < G; ++u) {
+        const int cu = __shfl(mc, gbase + u);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) xv[u][k] = 0.f;
+        if (u < cnt && c0 < C)
+          load_vec<TIn, VEC>(x + (size_t)cu * C + c0, xv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < G; ++u) {
+        const float w = __shfl(mv, gbase + u);
+        if (u < cnt)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
-    }
-    for (; e < end; e += PPB) {
-      float xv[VEC];
-      const float w = val[e];
-      load_vec<TIn, VEC>(x + (size_t)col[e] * C + c0, xv);
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[k], acc[k]);
+          for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, xv[u][k], acc[k]);
+      }
     }
   }
 #pragma unroll
