@@ -229,7 +229,8 @@ __device__ __forceinline__ int x6_xcd_unit(const int* __restrict__ seg, int S,
 // XL (forward, K <= 256): workgroup b works on XCD b % 8's node eighth of
 // every slot, so the X rows it gathers (<= 1 / 8 of X) stay in that XCD's
 // L2 (grid = a multiple of 8, dispatched round-robin over the XCDs).
-// AF32 (input gradient from fp32 dY_c, no gather): the A operand is staged
+// AF32 (fp32 A: the input gradient's dY_c, or the forward's gathered X):
+// the A operand is staged
 // as fp32 row images ([256][32] floats, 16-byte chunks XOR-swizzled by row
 // bits 1-3 - conflict-free ds_read_b128) and split into the three bf16
 // terms in registers: dY_c is stored at 4 instead of 6 bytes per element.
@@ -312,8 +313,11 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     const int m0 = row_tile(j) * kXBM;
     if (AF32) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        frow[e] = Af + (size_t)(m0 + fr[e]) * K + fq[e];
+      for (int e = 0; e < 4; ++e) {
+        int ix = m0 + fr[e];
+        if (GATHER) ix = sidx[(j & 1) * kXBM + fr[e]];
+        frow[e] = Af + (size_t)(ix < 0 ? 0 : ix) * K + fq[e];   // padding: row 0
+      }
     }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -793,12 +797,10 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   // split in the kernel.
   const bool af32 = a3.scalar_type() == at::kFloat;
   TORCH_CHECK(a3.is_cuda() && a3.is_contiguous() &&
-                  (af32 ? (a3.dim() == 2 && !gather &&
-                           aligned16(a3.data_ptr()))
+                  (af32 ? (a3.dim() == 2 && aligned16(a3.data_ptr()))
                         : (a3.scalar_type() == at::kBFloat16 &&
                            a3.dim() == 3 && a3.size(0) == 3)),
-              "slot_gemm_x6: bf16 A planes [3, R, K] or fp32 A [R, K] "
-              "(no gather)");
+              "slot_gemm_x6: bf16 A planes [3, R, K] or fp32 A [R, K]");
   TORCH_CHECK(b3.scalar_type() == at::kBFloat16 && b3.is_contiguous() &&
                   b3.dim() == 4 && b3.size(0) == 3,
               "slot_gemm_x6: bf16 B planes [3, S, Nn, K]");
@@ -832,8 +834,10 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   const int* tl = listed ? tiles->data_ptr<int>() : nullptr;
   // XCD-local forward tiles where the gathered X (and the weights) fit the
   // XCDs' L2s (K <= 256); the 1024-wide psi_1 layer streams.
-  const bool xl = gather && !listed && K <= x6_xl_kmax() && blocks >= 64;
-  auto kern = af32 ? slot_gemm_x6_kernel<false, false, true>
+  const bool xl = gather && !af32 && !listed && K <= x6_xl_kmax() &&
+                  blocks >= 64;
+  auto kern = af32 ? (gather ? slot_gemm_x6_kernel<true, false, true>
+                             : slot_gemm_x6_kernel<false, false, true>)
               : gather ? (xl ? slot_gemm_x6_kernel<true, true>
                              : slot_gemm_x6_kernel<true, false>)
                        : slot_gemm_x6_kernel<false, false>;

@@ -51,6 +51,8 @@ PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
 # staging) instead of the rowmap SpMM writing three bf16 planes.
 F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
 ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
+# bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging).
+F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
 PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
 PIECE_BYTES = 8 << 20
 
@@ -184,12 +186,22 @@ class _SlotGemmSpMM(torch.autograd.Function):
             # (planes written by the producing SpMM when it was another
             # slot conv; valid while x is unmodified)
             pl = getattr(x, '_dgmc_x6', None)
-            if pl is not None and pl[1] == x._version and \
-                    tuple(pl[0].shape) == (3, ) + tuple(x.shape):
-                xc = pl[0]
+            planes = pl[0] if (pl is not None and pl[1] == x._version and
+                               tuple(pl[0].shape) == (3, ) + tuple(x.shape)) \
+                else None
+            if F32X and xc.data_ptr() % 16 == 0:
+                # The GEMM gathers fp32 X rows and splits them in its LDS
+                # staging (4 instead of 6 bytes per gathered element); the
+                # planes are kept for the weight gradient only.
+                Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
+                if planes is None and (ctx.needs_input_grad[1] or (
+                        root is not None and ctx.needs_input_grad[2])):
+                    planes = ops.split3(xc)
+                xc = planes
             else:
-                xc = ops.split3(xc)
-            Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
+                xc = planes if planes is not None else ops.split3(xc)
+                Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True,
+                                     None)
         else:
             # W^T images [S, out, in] (k-contiguous B operand), built once
             # per forward scope and shared by the consensus loop's uses.

@@ -193,7 +193,8 @@ def test_x6_weight_grad_fp32_dy_equals_planes(headline_plan, cin, cout,
 
 
 def test_x6_f32dy_training_step_matches_planes(monkeypatch):
-    """The gated fp32-dY backward gives the planes backward's gradients."""
+    """The fp32-X forward and fp32-dY backward give the plane path's
+    output and gradients."""
     from deep_graph_matching_consensus_amd.nn.conv import SplineConv
     torch.manual_seed(0)
     N = 600
@@ -204,6 +205,7 @@ def test_x6_f32dy_training_step_matches_planes(monkeypatch):
     grads = []
     for flag in (False, True):
         monkeypatch.setattr(sg, 'F32DY', flag)
+        monkeypatch.setattr(sg, 'F32X', flag)
         conv.zero_grad()
         x.grad = None
         conv(x, ei, ea).square().sum().backward()
@@ -211,6 +213,24 @@ def test_x6_f32dy_training_step_matches_planes(monkeypatch):
                      [p.grad.clone() for p in conv.parameters()])
     for a, b in zip(*grads):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('cin,cout', [(128, 128), (256, 256), (1024, 256)])
+def test_x6_forward_fp32_gather_equals_planes(headline_plan, cin, cout):
+    """Gathered fp32 X rows split in the forward kernel's staging give bit
+    for bit the plane path's Y."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(3 + cin)
+    x = torch.randn(N, cin, device=DEV, generator=g)
+    w = torch.randn(25, cin, cout, device=DEV, generator=g) / cin ** 0.5
+    r = torch.randn(cin, cout, device=DEV, generator=g) / cin ** 0.5
+    wt3 = ops.slot_weight_x3(w, r, True)
+    yp = ops.slot_gemm_x6(ops.split3(x), plan.src, plan.seg, wt3, True, None)
+    yf = ops.slot_gemm_x6(x, plan.src, plan.seg, wt3, True, None)
+    used = int(plan.seg[-1])
+    assert torch.equal(yf[:used], yp[:used]), float(
+        (yf[:used] - yp[:used]).abs().max())
 
 
 def test_split3_reconstructs_fp32():
