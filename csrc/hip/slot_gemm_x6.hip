@@ -523,14 +523,19 @@ __device__ __forceinline__ int wx_swz(int r) {
 // [16 rows][128 floats] images (16-byte chunks XOR 8 for rows 8-15, so the
 // two half-waves' column reads hit disjoint banks), read column-wise
 // (8 x ds_read_b32 per fragment) and split into bf16 terms in registers.
+// XF32 (with GF32): X_u is fp32 [N][Kin] too - gathered rows staged as the
+// same [16][128]-float images, B-operand columns read and split alike.
 constexpr int kWXStageF = 3 * kWXPlane + 2 * kWXPlane;   // X planes + fp32 dY
+constexpr int kWXStageFF = 2 * kWXPlane + 2 * kWXPlane;  // fp32 X + fp32 dY
 
-template <bool GF32>
+template <bool GF32, bool XF32 = false>
 __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     X6Uses U, int nu, int64_t xplane, int64_t gplane,
     const int* __restrict__ src, const int* __restrict__ seg,
     const int* __restrict__ items, int Kin, int C, float* __restrict__ part) {
-  constexpr int STG = GF32 ? kWXStageF : kWXStage;
+  static_assert(GF32 || !XF32, "fp32 X only with fp32 dY");
+  constexpr int STG = XF32 ? kWXStageFF : GF32 ? kWXStageF : kWXStage;
+  constexpr int XREG = XF32 ? 2 * kWXPlane : 3 * kWXPlane;   // X image size
   extern __shared__ __attribute__((aligned(16))) char wx_smem[];
   DGMC_LDS __bf16* ring = (DGMC_LDS __bf16*)wx_smem;
   DGMC_LDS int* sidx =
@@ -570,14 +575,24 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     const int qq = qb + q;
     const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
     const int row = ch * kWXRows + srow;
-    const __bf16* xr = U.x[u] + (size_t)sidx[row] * Kin + i0 + 8 * schunk;
     DGMC_LDS __bf16* d = buf + 4 * wave * 128;
+    if (XF32) {
+      const float* xf = reinterpret_cast<const float*>(U.x[u]);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) x6_dma16(xr + p * xplane, d + p * kWXPlane);
+      for (int e = 0; e < 2; ++e)
+        x6_dma16(reinterpret_cast<const __bf16*>(
+                     xf + (size_t)sidx[ch * kWXRows + gfr[e]] * Kin + i0 +
+                     gfq[e]),
+                 buf + 2 * (4 * wave + 2 * e) * 128);
+    } else {
+      const __bf16* xr = U.x[u] + (size_t)sidx[row] * Kin + i0 + 8 * schunk;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) x6_dma16(xr + p * xplane, d + p * kWXPlane);
+    }
     if (GF32) {
       const float* gf = reinterpret_cast<const float*>(U.g[u]) +
                         (size_t)(pb + ch * kWXRows) * C + n0;
-      DGMC_LDS __bf16* dg = buf + 3 * kWXPlane;
+      DGMC_LDS __bf16* dg = buf + XREG;
 #pragma unroll
       for (int e = 0; e < 2; ++e)
         x6_dma16(reinterpret_cast<const __bf16*>(gf + (size_t)gfr[e] * C +
@@ -640,13 +655,33 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
       for (int a = 0; a < 2; ++a) {
         if (!GF32)
           gv[p][a] = frag(buf + (3 + p) * kWXPlane, offG[a][0], offG[a][1]);
-        xv[p][a] = frag(buf + p * kWXPlane, offX[a][0], offX[a][1]);
+        if (!XF32)
+          xv[p][a] = frag(buf + p * kWXPlane, offX[a][0], offX[a][1]);
       }
+    if (XF32) {
+      // B operand X: lane l -> column i = wm 64 + 32 b + l % 32, rows
+      // 8 (l / 32) + j, j < 8.
+      const DGMC_LDS float* xf = reinterpret_cast<const DGMC_LDS float*>(buf);
+      const int hl = lane >> 5;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int c = wm * 64 + b * 32 + (lane & 31);
+        const int pc = 4 * ((c >> 2) ^ (8 * hl)) + (c & 3);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 hh, mm, ll;
+          x6_split(xf[(8 * hl + j) * 128 + pc], hh, mm, ll);
+          xv[0][b][j] = hh;
+          xv[1][b][j] = mm;
+          xv[2][b][j] = ll;
+        }
+      }
+    }
     if (GF32) {
       // A operand dY^T: lane l -> column c = wn 64 + 32 a + l % 32, rows
       // 8 (l / 32) + j, j < 8.
       const DGMC_LDS float* gf =
-          reinterpret_cast<const DGMC_LDS float*>(buf + 3 * kWXPlane);
+          reinterpret_cast<const DGMC_LDS float*>(buf + XREG);
       const int hl = lane >> 5;
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
@@ -684,7 +719,9 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     if (q + kWXNst - 1 < total) {
       stage(q + kWXNst - 1, ring + ((q + kWXNst - 1) % kWXNst) * STG);
       // (this thread's DMAs of the two stages still in flight)
-      if (GF32)
+      if (XF32)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (GF32)
         asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -999,7 +1036,10 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   // dY_u: bf16 planes [3, P_cap, out] or fp32 [P_cap, out] (split in
   // the kernel).
   const bool gf32 = gs[0].scalar_type() == at::kFloat;
-  const int64_t N = xs[0].size(1), Kin = xs[0].size(2);
+  const bool xf32 = xs[0].scalar_type() == at::kFloat;
+  TORCH_CHECK(gf32 || !xf32, "slot_wgrad_x6: fp32 X needs fp32 dY");
+  const int64_t N = xf32 ? xs[0].size(0) : xs[0].size(1);
+  const int64_t Kin = xf32 ? xs[0].size(1) : xs[0].size(2);
   const int64_t C = gf32 ? gs[0].size(1) : gs[0].size(2);
   const int64_t P = src.numel(), S = seg.numel() - 1;
   TORCH_CHECK(Kin % 128 == 0 && C % 128 == 0 && P % kWXRows == 0 &&
@@ -1009,10 +1049,17 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   for (int64_t u = 0; u < nu; ++u) {
     const at::Tensor& x = xs[u];
     const at::Tensor& g = gs[u];
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 &&
-                    x.is_contiguous() && x.dim() == 3 && x.size(0) == 3 &&
-                    x.size(1) == N && x.size(2) == Kin,
-                "slot_wgrad_x6: X_u bf16 planes [3, N, in]");
+    if (xf32) {
+      TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat &&
+                      x.is_contiguous() && x.dim() == 2 && x.size(0) == N &&
+                      x.size(1) == Kin && aligned16(x.data_ptr()),
+                  "slot_wgrad_x6: X_u fp32 [N, in] (all uses alike)");
+    } else {
+      TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 &&
+                      x.is_contiguous() && x.dim() == 3 && x.size(0) == 3 &&
+                      x.size(1) == N && x.size(2) == Kin,
+                  "slot_wgrad_x6: X_u bf16 planes [3, N, in]");
+    }
     if (gf32) {
       TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous() &&
                       g.dim() == 2 && g.size(0) == P && g.size(1) == C &&
@@ -1037,9 +1084,11 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const int64_t per = Kin * C;
   at::Tensor part =
       at::empty({G_cap, per}, xs[0].options().dtype(at::kFloat));
-  auto kern = gf32 ? slot_wgrad_x6_kernel<true> : slot_wgrad_x6_kernel<false>;
-  const size_t lds = (size_t)kWXNst * (gf32 ? kWXStageF : kWXStage) * 2 +
-                     kWXMaxRows * 4;
+  auto kern = xf32 ? slot_wgrad_x6_kernel<true, true>
+              : gf32 ? slot_wgrad_x6_kernel<true> : slot_wgrad_x6_kernel<false>;
+  const size_t lds =
+      (size_t)kWXNst * (xf32 ? kWXStageFF : gf32 ? kWXStageF : kWXStage) * 2 +
+      kWXMaxRows * 4;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -53,6 +53,15 @@ F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
 ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
 # bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging).
 F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
+# ... and the weight gradient reads fp32 X rows too (with F32DY: no operand
+# planes of X at all - no split pass, no plane output of the producing SpMM).
+# Off: measured slower (PascalVOC 5.57 -> 5.66 ms: both operands' column
+# reads + splits cost more than the 1/3 of X traffic they save).
+F32X_WGRAD = os.environ.get('DGMC_AMD_X6_F32X_WGRAD', '0') == '1'
+
+
+def _x_planes_free():
+    return F32X and F32DY and F32X_WGRAD
 PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
 PIECE_BYTES = 8 << 20
 
@@ -189,15 +198,18 @@ class _SlotGemmSpMM(torch.autograd.Function):
             planes = pl[0] if (pl is not None and pl[1] == x._version and
                                tuple(pl[0].shape) == (3, ) + tuple(x.shape)) \
                 else None
-            if F32X and xc.data_ptr() % 16 == 0:
+            if F32X:
+                if xc.data_ptr() % 16 != 0:
+                    xc = xc.clone()          # (16-byte row DMA)
                 # The GEMM gathers fp32 X rows and splits them in its LDS
-                # staging (4 instead of 6 bytes per gathered element); the
-                # planes are kept for the weight gradient only.
+                # staging (4 instead of 6 bytes per gathered element); with
+                # the fp32-X weight gradient no X planes are formed at all.
                 Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
-                if planes is None and (ctx.needs_input_grad[1] or (
-                        root is not None and ctx.needs_input_grad[2])):
-                    planes = ops.split3(xc)
-                xc = planes
+                if not _x_planes_free():
+                    if planes is None and (ctx.needs_input_grad[1] or (
+                            root is not None and ctx.needs_input_grad[2])):
+                        planes = ops.split3(xc)
+                    xc = planes
             else:
                 xc = planes if planes is not None else ops.split3(xc)
                 Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True,
@@ -209,7 +221,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
                 weight.detach().contiguous(),
                 root.detach().contiguous() if root is not None else None))
             Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
-        if X6 and planes_out:
+        if X6 and planes_out and not _x_planes_free():
             # The consumer is another bf16x6 slot conv: the SpMM also
             # writes its operand planes (no split pass there).
             out, planes = ops.spmm_csr_planes(op.rowptr, plan.col_c, op.val,

@@ -177,8 +177,8 @@ def test_x6_weight_grad_fp32_dy_equals_planes(headline_plan, cin, cout,
     g = torch.Generator(device=DEV).manual_seed(13 + cin)
     P = plan.src.numel()
     used = int(plan.seg[-1])
-    xs = [ops.split3(torch.randn(N, cin, device=DEV, generator=g))
-          for _ in range(uses)]
+    xf = [torch.randn(N, cin, device=DEV, generator=g) for _ in range(uses)]
+    xs = [ops.split3(x) for x in xf]
     dys = []
     for _ in range(uses):
         d = torch.randn(P, cout, device=DEV, generator=g)
@@ -190,6 +190,9 @@ def test_x6_weight_grad_fp32_dy_equals_planes(headline_plan, cin, cout,
                            plan.seg, rounds)
     wf = ops.slot_wgrad_x6(xs, dys, plan.src, plan.seg, rounds)
     assert torch.equal(wf, wp), float((wf - wp).abs().max())
+    # fp32 X rows as well (split in the kernel)
+    wff = ops.slot_wgrad_x6(xf, dys, plan.src, plan.seg, rounds)
+    assert torch.equal(wff, wp), float((wff - wp).abs().max())
 
 
 def test_x6_f32dy_training_step_matches_planes(monkeypatch):
@@ -206,6 +209,7 @@ def test_x6_f32dy_training_step_matches_planes(monkeypatch):
     for flag in (False, True):
         monkeypatch.setattr(sg, 'F32DY', flag)
         monkeypatch.setattr(sg, 'F32X', flag)
+        monkeypatch.setattr(sg, 'F32X_WGRAD', flag)
         conv.zero_grad()
         x.grad = None
         conv(x, ei, ea).square().sum().backward()
@@ -340,10 +344,12 @@ def test_rowmap_entry_table_equals_ranges(headline_plan):
             assert torch.equal(a[:used], b[:used])
 
 
-def test_spmm_planes_feed_next_conv():
-    """A non-last fp32 SplineConv's aggregation also writes the bf16x6
-    planes of its output (== split3 of it, bitwise); the next conv consumes
-    them instead of splitting, with an identical result."""
+def test_spmm_planes_feed_next_conv(monkeypatch):
+    """Plane path (``F32X_WGRAD=0``): a non-last fp32 SplineConv's
+    aggregation also writes the bf16x6 planes of its output (== split3 of
+    it, bitwise); the next conv consumes them instead of splitting, with an
+    identical result."""
+    monkeypatch.setattr(sg, 'F32X_WGRAD', False)
     from deep_graph_matching_consensus_amd.datasets import (
         GraphStore, DevicePairLoader, make_keypoint_datasets)
     from deep_graph_matching_consensus_amd.nn.conv import SplineConv
