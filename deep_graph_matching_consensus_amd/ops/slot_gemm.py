@@ -149,12 +149,24 @@ def weight_grad(xs, dys, plan, cin, cout):
     return out
 
 
+def _x6_rounds(tiles):
+    """Rounds of resident workgroups the bf16x6 weight gradient's slot-range
+    items are sized for (more items: better balance, more partial bytes
+    for the fold)."""
+    if tiles == 1:
+        return 1
+    return 2 if tiles <= 4 else X6_WGRAD_ROUNDS_BIG
+
+
+X6_WGRAD_ROUNDS_BIG = int(os.environ.get('DGMC_AMD_X6_WGRAD_ROUNDS', '6'))
+
+
 def weight_grad_x6(x3s, dy3s, plan, cin, cout):
     """:func:`weight_grad` on bf16x6 operand planes (``[3, N, in]`` /
     ``[3, P_cap, out]``)."""
     ops = _backend.ops()
     tiles = (cin // 128) * (cout // 128)
-    rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
+    rounds = _x6_rounds(tiles)
     out = None
     for i in range(0, len(x3s), MAX_USES):
         part = ops.slot_wgrad_x6(list(x3s[i:i + MAX_USES]),
@@ -355,7 +367,7 @@ def _weight_grad_pieces(x3, dy3, plan, weight, root, need_root):
     nw, cin, cout = weight.shape
     S = plan.S
     tiles = (cin // 128) * (cout // 128)
-    rounds = 1 if tiles == 1 else (2 if tiles <= 4 else 6)
+    rounds = _x6_rounds(tiles)
     sink = grad_sink(weight)
     gw = sink.grad_view(weight) if sink is not None else \
         torch.empty_like(weight)
