@@ -53,6 +53,9 @@ F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
 ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
 # bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging).
 F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
+# (only for in <= 128: tools/bench_slot_gemm_x6.py, 128->128 43.4 -> 39.5 us,
+# but 256->256 117 -> 120 and 1024->256 360 -> 369 us)
+F32X_KMAX = int(os.environ.get('DGMC_AMD_X6_F32X_KMAX', '128'))
 # ... and the weight gradient reads fp32 X rows too (with F32DY: no operand
 # planes of X at all - no split pass, no plane output of the producing SpMM).
 # Off: measured slower (PascalVOC 5.57 -> 5.66 ms: both operands' column
@@ -210,7 +213,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
             planes = pl[0] if (pl is not None and pl[1] == x._version and
                                tuple(pl[0].shape) == (3, ) + tuple(x.shape)) \
                 else None
-            if F32X:
+            if F32X and (x.size(1) <= F32X_KMAX or _x_planes_free()):
                 if xc.data_ptr() % 16 != 0:
                     xc = xc.clone()          # (16-byte row DMA)
                 # The GEMM gathers fp32 X rows and splits them in its LDS

@@ -4,8 +4,9 @@ the exact-f32 MFMA kernels on the PascalVOC-shaped static batch operator.
     python tools/bench_slot_gemm_x6.py [--reps 20] [--json out.json]
 
 Per shape (psi_2 128->128, psi_1 256->256 and 1024->256): forward (gathered
-X W_s) and input gradient (dY_c W_s^T) in us per call, plus the split
-kernels' cost, and the max error of both against fp64.
+X W_s) and input gradient (dY_c W_s^T) in us per call - operands as bf16
+planes or fp32 (split in the kernel) - plus the split kernels' cost, the
+weight gradient, and the max error of both against fp64.
 """
 import argparse
 import json
@@ -76,6 +77,8 @@ def main():
             x, plan.src, plan.seg, wt, None, True), args.reps)
         rec['fwd_x6_us'] = timeit(lambda: ops.slot_gemm_x6(
             x3, plan.src, plan.seg, wt3, True, None), args.reps)
+        rec['fwd_x6_f32x_us'] = timeit(lambda: ops.slot_gemm_x6(
+            x, plan.src, plan.seg, wt3, True, None), args.reps)
         rec['split_x_us'] = timeit(lambda: ops.split3(x), args.reps)
         def f32dx():
             if cout >= 256:
@@ -84,6 +87,8 @@ def main():
         rec['dx_f32_us'] = timeit(f32dx, args.reps)
         rec['dx_x6_us'] = timeit(lambda: ops.slot_gemm_x6(
             dy3, plan.src, plan.seg, w3, False, None), args.reps)
+        rec['dx_x6_f32dy_us'] = timeit(lambda: ops.slot_gemm_x6(
+            dy, plan.src, plan.seg, w3, False, None), args.reps)
         rec['split_dy_us'] = timeit(lambda: ops.split3(dy), args.reps)
         rec['weight_x3_us'] = timeit(lambda: ops.slot_weight_x3(w, r, True),
                                      args.reps)
@@ -98,6 +103,10 @@ def main():
             xs, dys, plan.src, plan.seg, rounds), args.reps)
         rec['wgrad_x6_us'] = timeit(lambda: ops.slot_wgrad_x6(
             x3s, dy3s, plan.src, plan.seg, rounds), args.reps)
+        rec['wgrad_x6_f32dy_us'] = timeit(lambda: ops.slot_wgrad_x6(
+            x3s, dys, plan.src, plan.seg, rounds), args.reps)
+        rec['wgrad_x6_f32xdy_us'] = timeit(lambda: ops.slot_wgrad_x6(
+            xs, dys, plan.src, plan.seg, rounds), args.reps)
         rec['fwd_x6_tflops'] = round(flop / rec['fwd_x6_us'] / 1e6, 1)
         rec['fwd_f32_tflops'] = round(flop / rec['fwd_f32_us'] / 1e6, 1)
         # errors vs fp64
