@@ -265,6 +265,7 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
 at::Tensor slot_weight_t(const at::Tensor& weight,
                          const c10::optional<at::Tensor>& root);
 at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt);
+at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt);
 at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
                            at::TensorList gs, const at::Tensor& seg01);
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
@@ -500,6 +501,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm_x6(Tensor a3, Tensor src, Tensor seg, Tensor b3, bool gather, "
       "Tensor? tiles=None) -> Tensor");
   m.def("dense_nt_f32(Tensor[] parts, Tensor bt) -> Tensor");
+  m.def("dense_nt_x6(Tensor[] parts, Tensor bt) -> Tensor");
   m.def(
       "dense_wgrad_f32(Tensor[] xparts, int nparts, Tensor[] gs, Tensor "
       "seg01) -> Tensor");
@@ -603,6 +605,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_weight_x3", &dgmc::slot_weight_x3);
   m.impl("slot_gemm_x6", &dgmc::slot_gemm_x6);
   m.impl("dense_nt_f32", &dgmc::dense_nt_f32);
+  m.impl("dense_nt_x6", &dgmc::dense_nt_x6);
   m.impl("dense_wgrad_f32", &dgmc::dense_wgrad_f32);
   m.impl("slot_spmm_rowmap", &dgmc::slot_spmm_rowmap);
   m.impl("slot_rowmap_ranges", &dgmc::slot_rowmap_ranges);

@@ -753,6 +753,116 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Dense NT GEMM on bf16x6, fp32 operands split in registers:
+//   Y[M, Nn] = [A_0 | A_1 | ...] Bt^T,  A_j fp32 [M, 128] read in place,
+//   Bt fp32 [Nn, K] k-contiguous, K = 128 * parts.
+// The consensus loop's folded projection (ops/dense.py::_CatMatmulF32) and
+// its input gradient: skinny (M ~ 11k, K = 384 / 128) products that the
+// 256x128 slot-GEMM tiles cannot spread over the chip.  One 64x64 tile per
+// workgroup (4 waves of 32x32), k consumed 32 at a time through two LDS
+// stages of fp32 row images ([64][32] floats, 16-byte chunks XOR-swizzled by
+// row bits 1-3: conflict-free ds_read_b128), each fragment split into its
+// three bf16 terms in registers.  Rows past M are clamped on load and not
+// stored.  tools/micro/bench_dense_nt.py: [10944, 128] x [128, 384] 24.1 ->
+// 15.6 us vs the exact-f32 kernel, [10944, 384] x [384, 128] 18.7 -> 18.1 us
+// (a four-stage ring, three chunks in flight, changed nothing: 18.8 us).
+// ---------------------------------------------------------------------------
+struct NtParts {
+  const float* p[4];
+};
+
+constexpr int kNtT = 64;                    // tile rows / columns
+constexpr int kNtK = 32;                    // k per chunk
+constexpr int kNtImg = kNtT * kNtK;         // floats per operand image
+
+__global__ __launch_bounds__(256, 4) void dense_nt_x6_kernel(
+    NtParts A, int M, const float* __restrict__ bt, int K, int Nn,
+    float* __restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) float lds_[2 * 2 * kNtImg];
+  DGMC_LDS float* lds = (DGMC_LDS float*)lds_;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int ntn = Nn / kNtT, nk = K / kNtK;
+  const int m0 = (blockIdx.x / ntn) * kNtT, n0 = (blockIdx.x % ntn) * kNtT;
+  // Staging: wave w fills rows 16 w + 8 e + L / 8 (e < 2) of both images;
+  // lane L holds physical chunk L % 8 = logical (L % 8) ^ ((row >> 1) & 7).
+  int srow[2], sq[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    srow[e] = 16 * wave + 8 * e + (lane >> 3);
+    sq[e] = 4 * ((lane & 7) ^ ((srow[e] >> 1) & 7));
+  }
+  auto stage = [&](int kc, DGMC_LDS float* buf) {
+    const int k0 = kc * kNtK;
+    const float* part = A.p[k0 >> 7];
+    const int kp = k0 & 127;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int m = min(m0 + srow[e], M - 1);
+      x6_dma16(reinterpret_cast<const __bf16*>(part + (size_t)m * 128 + kp +
+                                               sq[e]),
+               reinterpret_cast<DGMC_LDS __bf16*>(
+                   buf + (16 * wave + 8 * e) * kNtK));
+      x6_dma16(reinterpret_cast<const __bf16*>(
+                   bt + (size_t)(n0 + srow[e]) * K + k0 + sq[e]),
+               reinterpret_cast<DGMC_LDS __bf16*>(
+                   buf + kNtImg + (16 * wave + 8 * e) * kNtK));
+    }
+  };
+  const int i = lane & 31, h = lane >> 5;
+  const int ra = wm * 32 + i, rb = wn * 32 + i;   // A (m) / Bt (n) rows
+  x6_f32x16 acc, acs;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = acs[r] = 0.f;
+  auto frag = [&](const DGMC_LDS float* img, int row, int st,
+                  x6_bf16x8 (&v)[3]) {
+    const int sw = (row >> 1) & 7, c0 = 4 * st + 2 * h;
+    const x6_f32x4 u0 = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+        img + row * kNtK + 4 * (c0 ^ sw));
+    const x6_f32x4 u1 = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+        img + row * kNtK + 4 * ((c0 + 1) ^ sw));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 hh, mm, ll;
+      x6_split(e < 4 ? u0[e] : u1[e - 4], hh, mm, ll);
+      v[0][e] = hh;
+      v[1][e] = mm;
+      v[2][e] = ll;
+    }
+  };
+  stage(0, lds);
+  for (int kc = 0; kc < nk; ++kc) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x6_barrier();
+    if (kc + 1 < nk) stage(kc + 1, lds + ((kc + 1) & 1) * 2 * kNtImg);
+    const DGMC_LDS float* buf = lds + (kc & 1) * 2 * kNtImg;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      x6_bf16x8 x[3], w[3];
+      frag(buf, ra, st, x);
+      frag(buf + kNtImg, rb, st, w);
+      acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acs, 0, 0, 0);
+      acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acs, 0, 0, 0);
+      acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acs, 0, 0, 0);
+      acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], acs, 0, 0, 0);
+      acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], acs, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0], acc, 0, 0, 0);
+    }
+  }
+  // acc: Y^T block - lane column i = row m, rows (r & 3) + 8 (r >> 2) + 4 h
+  // = column n.
+  const int m = m0 + wm * 32 + i;
+  if (m < M) {
+    float* yrow = Y + (size_t)m * Nn + n0 + wn * 32 + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(yrow + 8 * q) = make_float4(
+          acc[4 * q] + acs[4 * q], acc[4 * q + 1] + acs[4 * q + 1],
+          acc[4 * q + 2] + acs[4 * q + 2], acc[4 * q + 3] + acs[4 * q + 3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host wrappers
 // ---------------------------------------------------------------------------
 at::Tensor split3(const at::Tensor& x) {
@@ -1098,6 +1208,36 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                      (int)C, part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return slot_fold_parts(part, it[1], S, Kin, C);
+}
+
+at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt) {
+  const int64_t np = (int64_t)parts.size();
+  TORCH_CHECK(np >= 1 && np <= 4, "dense_nt_x6: 1..4 parts");
+  const int64_t M = parts[0].size(0);
+  NtParts A{};
+  for (int64_t j = 0; j < np; ++j) {
+    const at::Tensor& p = parts[j];
+    TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat &&
+                    p.is_contiguous() && p.dim() == 2 && p.size(0) == M &&
+                    p.size(1) == 128 && aligned16(p.data_ptr()),
+                "dense_nt_x6: parts contiguous fp32 [M, 128]");
+    A.p[j] = p.data_ptr<float>();
+  }
+  TORCH_CHECK(bt.is_cuda() && bt.scalar_type() == at::kFloat &&
+                  bt.is_contiguous() && bt.dim() == 2 &&
+                  bt.size(1) == 128 * np && bt.size(0) % kNtT == 0 &&
+                  aligned16(bt.data_ptr()),
+              "dense_nt_x6: Bt fp32 [Nn % 64, 128 * parts]");
+  const int64_t Nn = bt.size(0), K = bt.size(1);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bt.device());
+  at::Tensor Y = at::empty({M, Nn}, bt.options());
+  if (M == 0) return Y;
+  const int64_t tiles = ((M + kNtT - 1) / kNtT) * (Nn / kNtT);
+  hipLaunchKernelGGL(dense_nt_x6_kernel, dim3((unsigned)tiles), dim3(256), 0,
+                     stream(), A, (int)M, bt.data_ptr<float>(), (int)K,
+                     (int)Nn, Y.data_ptr<float>());
+  DGMC_CHECK_LAUNCH();
+  return Y;
 }
 
 }  // namespace dgmc

@@ -660,6 +660,17 @@ def _seg01(M, device):
     return t
 
 
+# The folded projection's NT products on bf16x6 (fp32 parts split in the
+# kernel's registers; error vs fp64 below the exact-f32 MFMA kernel's:
+# tests/test_slot_gemm_x6.py) or on the exact-f32 MFMA kernel.
+NT_X6 = os.environ.get('DGMC_AMD_X6_NT', '1') == '1'
+
+
+def _nt(ops):
+    from . import slot_gemm
+    return ops.dense_nt_x6 if (NT_X6 and slot_gemm.X6) else ops.dense_nt_f32
+
+
 class _CatMatmulF32(torch.autograd.Function):
     """fp32 ``[X_0 | X_1 | ...] @ W`` (``W = w_t [128 n, 128]``) on the
     LDS-DMA MFMA GEMM reading psi_2's feature parts in place
@@ -672,7 +683,7 @@ class _CatMatmulF32(torch.autograd.Function):
     def forward(ctx, w_t, loop, *parts):
         from ..runtime.cache import cached
         ops = _backend.ops()
-        out = ops.dense_nt_f32(list(parts), w_t.detach().t().contiguous())
+        out = _nt(ops)(list(parts), w_t.detach().t().contiguous())
         ctx.loop, ctx.np = loop, len(parts)
         # The backward's B operand (w_t itself, k-contiguous): one copy per
         # forward scope, shared by the consensus loop's uses (was a clone
@@ -693,7 +704,7 @@ class _CatMatmulF32(torch.autograd.Function):
         ctx.parts = tuple(kept) if kept else None
         ops = _backend.ops()
         g = g.float().contiguous()
-        gx = ops.dense_nt_f32([g], wc)                          # [M, 128 n]
+        gx = _nt(ops)([g], wc)                                  # [M, 128 n]
         grads = tuple(gx[:, 128 * i:128 * (i + 1)]
                       if ctx.needs_input_grad[2 + i] else None
                       for i in range(ctx.np))

@@ -423,3 +423,24 @@ def test_dense_x6_linear_gradients_flow(monkeypatch):
                                atol=1e-2, rtol=1e-4)
     torch.testing.assert_close(lin.bias.grad, go.sum(0), atol=1e-2,
                                rtol=1e-4)
+
+
+@pytest.mark.parametrize('M,parts,Nn', [(10944, 3, 128), (10944, 1, 384),
+                                        (1000, 2, 64), (33, 4, 128)])
+def test_dense_nt_x6_error_not_above_exact_f32(M, parts, Nn):
+    """The folded projection's NT GEMM on bf16x6 (fp32 parts read in place,
+    split in registers): max error vs fp64 <= the exact-f32 MFMA kernel's;
+    rows past M untouched-safe (M not a multiple of the tile)."""
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(M + parts)
+    ps = [torch.randn(M, 128, device=DEV, generator=g) for _ in range(parts)]
+    bt = torch.randn(Nn, 128 * parts, device=DEV, generator=g) / 12
+    ref = torch.cat(ps, 1).double() @ bt.double().t()
+    y6 = ops.dense_nt_x6(ps, bt)
+    assert y6.shape == (M, Nn)
+    e6 = float((y6.double() - ref).abs().max())
+    if Nn % 64 == 0 and M >= 64:
+        y32 = ops.dense_nt_f32(ps, bt)
+        e32 = float((y32.double() - ref).abs().max())
+        assert e6 <= e32 * 1.0001 + 1e-7, (e6, e32)
+    assert e6 < 1e-5 * float(ref.abs().max())
