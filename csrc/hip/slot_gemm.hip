@@ -1226,6 +1226,93 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_kernel(
   }
 }
 
+// Entry-table rowmap, RPL rows per lane group: the table loads of all RPL
+// rows are issued together, then all their gathers (RPL independent
+// latency chains per wave instead of one).  XCD-local row groups as above.
+template <int LPR, int RPL>
+__global__ __launch_bounds__(256) void sg_spmm_rowmap_ell_kernel(
+    const int* __restrict__ col, const float* __restrict__ val,
+    const int4* __restrict__ ell, const int* __restrict__ seg, int S,
+    const float* __restrict__ g, float* __restrict__ out,
+    __bf16* __restrict__ out3, int P, int C) {
+  constexpr int RPB = 256 / LPR;
+  const int r0 = sg_xcd_unit(seg, S, blockIdx.x % kNumXcd,
+                             blockIdx.x / kNumXcd, RPB * RPL);
+  if (r0 < 0) return;
+  const int lane = threadIdx.x % LPR;
+  const int pend = min(P, seg[S]);
+  int pr[RPL];
+  int4 ec[RPL], ev[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    pr[q] = r0 + q * RPB + threadIdx.x / LPR;
+    ec[q] = make_int4(0, 0, 0, 0);
+    ev[q] = make_int4(0, 0, 0, 0);
+    if (pr[q] < pend) {
+      ec[q] = ell[2 * pr[q]];
+      ev[q] = ell[2 * pr[q] + 1];
+    }
+  }
+  for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
+    float4 v[RPL][3];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int n = pr[q] < pend && ec[q].w <= 3 ? ec[q].w : 0;
+      const int cs[3] = {ec[q].x, ec[q].y, ec[q].z};
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        v[q][u] = u < n ? ld4(g + (size_t)cs[u] * C + c0)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      if (pr[q] >= pend) continue;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int n = ec[q].w;
+      if (n <= 3) {
+        const int vs[3] = {ev[q].x, ev[q].y, ev[q].z};
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+          if (u < n) {
+            const float w = __int_as_float(vs[u]);
+            acc.x = fmaf(w, v[q][u].x, acc.x);
+            acc.y = fmaf(w, v[q][u].y, acc.y);
+            acc.z = fmaf(w, v[q][u].z, acc.z);
+            acc.w = fmaf(w, v[q][u].w, acc.w);
+          }
+      } else {          // long row: walk col / val (entry order)
+        for (int e = ev[q].w; e < ev[q].w + n; ++e) {
+          const float w = val[e];
+          const float4 x = ld4(g + (size_t)col[e] * C + c0);
+          acc.x = fmaf(w, x.x, acc.x);
+          acc.y = fmaf(w, x.y, acc.y);
+          acc.z = fmaf(w, x.z, acc.z);
+          acc.w = fmaf(w, x.w, acc.w);
+        }
+      }
+      if (out3 != nullptr) {
+        sg_bf16x4 h, m, l;
+        sg_split4(acc, h, m, l);
+        const size_t o = (size_t)pr[q] * C + c0, plane = (size_t)P * C;
+        *reinterpret_cast<sg_bf16x4*>(out3 + o) = h;
+        *reinterpret_cast<sg_bf16x4*>(out3 + o + plane) = m;
+        *reinterpret_cast<sg_bf16x4*>(out3 + o + 2 * plane) = l;
+      } else {
+        *reinterpret_cast<float4*>(out + (size_t)pr[q] * C + c0) = acc;
+      }
+    }
+  }
+}
+
+static int rowmap_rpl() {     // DGMC_ROWMAP_RPL: rows per lane group (1: off)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGMC_ROWMAP_RPL");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
+}
+
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
                             const at::Tensor& val, const at::Tensor& cinv,
                             const at::Tensor& g,
@@ -1267,6 +1354,28 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
   }
   const bool xl = segp != nullptr;      // XCD-local row groups (above)
   const int lanes = (int)(C / 4);
+  const int rpl = rowmap_rpl();
+  if (el != nullptr && xl && (rpl == 2 || rpl == 4) && lanes <= 64) {
+    auto go2 = [&](auto lpr, auto rtag) {
+      constexpr int L = decltype(lpr)::value, RP = decltype(rtag)::value;
+      constexpr int RPB = 256 / L;
+      const int64_t blocks = (P / (RPB * RP) / kNumXcd + S + 1) * kNumXcd;
+      hipLaunchKernelGGL((sg_spmm_rowmap_ell_kernel<L, RP>), dim3(blocks),
+                         dim3(256), 0, stream(), col.data_ptr<int>(),
+                         val.data_ptr<float>(), el, segp, S,
+                         g.data_ptr<float>(), op, op3, (int)P, (int)C);
+    };
+    auto pick = [&](auto rtag) {
+      if (lanes <= 8) go2(std::integral_constant<int, 8>(), rtag);
+      else if (lanes <= 16) go2(std::integral_constant<int, 16>(), rtag);
+      else if (lanes <= 32) go2(std::integral_constant<int, 32>(), rtag);
+      else go2(std::integral_constant<int, 64>(), rtag);
+    };
+    if (rpl == 4) pick(std::integral_constant<int, 4>());
+    else pick(std::integral_constant<int, 2>());
+    DGMC_CHECK_LAUNCH();
+    return out;
+  }
   auto go = [&](auto lpr) {
     constexpr int L = decltype(lpr)::value;
     constexpr int RPB = 256 / L;
