@@ -18,7 +18,16 @@
 namespace dgmc {
 
 namespace {
-constexpr int kMaxColBlocks = 256;   // partial rows folded by the 2nd kernel
+// Partial rows folded by the 2nd kernel (DGMC_COLSUM_MAXBLOCKS; keep in sync
+// with ops/gemm.py::col_partial_rows).  1024: a [11k, 128] gradient gets one
+// 16-row pass per block instead of ~6 sequential passes at 1 wave per SIMD.
+int max_col_blocks() {
+  static const int v = [] {
+    const char* e = getenv("DGMC_COLSUM_MAXBLOCKS");
+    return e ? atoi(e) : 1024;
+  }();
+  return v;
+}
 }  // namespace
 
 // NOTE (MI355X): a single-kernel "last block folds" reduction needs a
@@ -145,7 +154,7 @@ void dispatch_colsum(const at::Tensor& grad, const void* out, void* g,
 
 // Keep in sync with ops/gemm.py::col_partial_rows.
 static int colsum_blocks(int rows) {
-  return std::max(1, std::min((rows + 15) / 16, kMaxColBlocks));
+  return std::max(1, std::min((rows + 15) / 16, max_col_blocks()));
 }
 
 // Optional caller-owned partial buffer [blocks, C] fp32 (a loop-gradient

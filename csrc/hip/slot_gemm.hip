@@ -1732,7 +1732,19 @@ __global__ __launch_bounds__(256) void sg_fold_kernel(
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= per) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int g = ib[s]; g < ib[s + 1]; ++g) {
+  const int ge = ib[s + 1];
+  int g = ib[s];
+  // (eight partial loads in flight; the sum keeps item order)
+  for (; g + 8 <= ge; g += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ld4(part + (size_t)(g + u) * per + i);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+    }
+  }
+  for (; g < ge; ++g) {
     const float4 v = ld4(part + (size_t)g * per + i);
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }

@@ -217,10 +217,13 @@ class _MixedMatmul(torch.autograd.Function):
         return gx, gw, None, gb, None
 
 
+_COL_MAX_BLOCKS = int(os.environ.get('DGMC_COLSUM_MAXBLOCKS', '1024'))
+
+
 def col_partial_rows(rows):
     """Per-block partial rows of the HIP column reductions (keep in sync
     with csrc/hip/elementwise.hip::colsum_blocks)."""
-    return max(1, min((rows + 15) // 16, 256))
+    return max(1, min((rows + 15) // 16, _COL_MAX_BLOCKS))
 
 
 def loop_col_sum(loop, name, idx, src):
