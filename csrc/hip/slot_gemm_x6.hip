@@ -617,20 +617,26 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     const int chunk = (col0 + cb) / 8 + (gp >> 1);
     return row * 128 + 8 * (chunk ^ wx_swz(row)) + 4 * (gp & 1);
   };
-  int offG[2][2], offX[2][2];
+  // Wave tile of the 128 x 128 output: 64 x 64 (NA = NB = 2) on planes; with
+  // fp32 dY (column reads + splits) 32 dY columns x all 128 X columns
+  // (NA = 1, NB = 4), so no two waves read and split the same dY columns.
+  constexpr int NA = (GF32 && !XF32) ? 1 : 2, NB = 4 / NA;
+  const int cbase = NA == 1 ? 32 * wave : wn * 64;
+  const int ibase = NA == 1 ? 0 : wm * 64;
+  int offG[NA][2], offX[NB][2];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int rr = 0; rr < 2; ++rr) {
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      offG[a][rr] = tr_off(wn * 64 + a * 32, 4 * rr);
-      offX[a][rr] = tr_off(wm * 64 + a * 32, 4 * rr);
-    }
+    for (int a = 0; a < NA; ++a) offG[a][rr] = tr_off(cbase + a * 32, 4 * rr);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) offX[b][rr] = tr_off(ibase + b * 32, 4 * rr);
+  }
 
-  x6_f32x16 acc[2][2], acs[2][2];
+  x6_f32x16 acc[NA][NB], acs[NA][NB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
 
@@ -648,24 +654,26 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     return __builtin_bit_cast(x6_bf16x8, both);
   };
   auto compute = [&](const DGMC_LDS __bf16* buf) {
-    x6_bf16x8 gv[3][2], xv[3][2];
+    x6_bf16x8 gv[3][NA], xv[3][NB];
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < 3; ++p) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+      for (int a = 0; a < NA; ++a)
         if (!GF32)
           gv[p][a] = frag(buf + (3 + p) * kWXPlane, offG[a][0], offG[a][1]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
         if (!XF32)
-          xv[p][a] = frag(buf + p * kWXPlane, offX[a][0], offX[a][1]);
-      }
+          xv[p][b] = frag(buf + p * kWXPlane, offX[b][0], offX[b][1]);
+    }
     if (XF32) {
-      // B operand X: lane l -> column i = wm 64 + 32 b + l % 32, rows
+      // B operand X: lane l -> column i = ibase + 32 b + l % 32, rows
       // 8 (l / 32) + j, j < 8.
       const DGMC_LDS float* xf = reinterpret_cast<const DGMC_LDS float*>(buf);
       const int hl = lane >> 5;
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int c = wm * 64 + b * 32 + (lane & 31);
+      for (int b = 0; b < NB; ++b) {
+        const int c = ibase + b * 32 + (lane & 31);
         const int pc = 4 * ((c >> 2) ^ (8 * hl)) + (c & 3);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -678,14 +686,14 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
       }
     }
     if (GF32) {
-      // A operand dY^T: lane l -> column c = wn 64 + 32 a + l % 32, rows
+      // A operand dY^T: lane l -> column c = cbase + 32 a + l % 32, rows
       // 8 (l / 32) + j, j < 8.
       const DGMC_LDS float* gf =
           reinterpret_cast<const DGMC_LDS float*>(buf + XREG);
       const int hl = lane >> 5;
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int c = wn * 64 + a * 32 + (lane & 31);
+      for (int a = 0; a < NA; ++a) {
+        const int c = cbase + a * 32 + (lane & 31);
         const int pc = 4 * ((c >> 2) ^ (8 * hl)) + (c & 3);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -698,9 +706,9 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
       }
     }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < NA; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < NB; ++b) {
         x6_f32x16 sm = acs[a][b];
         sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[2][a], xv[0][b], sm, 0, 0, 0);
         sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gv[0][a], xv[2][b], sm, 0, 0, 0);
@@ -732,16 +740,16 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     compute(ring + (q % kWXNst) * STG);
     x6_barrier();
   }
-  // acc[a][b]: rows c = wn 64 + 32 a + 8 qd + 4 h + e, column i = wm 64 +
+  // acc[a][b]: rows c = cbase + 32 a + 8 qd + 4 h + e, column i = ibase +
   // 32 b + l32 (the dW^T layout of slot_wgrad2_kernel).
   const int l32 = lane & 31, h = lane >> 5;
   float* outp = part + (size_t)item * Kin * C;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      float* row = outp + (size_t)(i0 + wm * 64 + b * 32 + l32) * C + n0 +
-                   wn * 64 + a * 32 + 4 * h;
+    for (int b = 0; b < NB; ++b) {
+      float* row = outp + (size_t)(i0 + ibase + b * 32 + l32) * C + n0 +
+                   cbase + a * 32 + 4 * h;
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd)
         *reinterpret_cast<float4*>(row + 8 * qd) = make_float4(
