@@ -365,16 +365,22 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
 
   // Fragment offsets: row (block base + i), logical quad 2 s + h at physical
   // quad (2 s + h) ^ swz(i) (block bases are multiples of 32: swz of i).
+  // Wave tiles: 64 x 64 on A planes; with fp32 A (fragments split in
+  // registers) 32 rows x all 128 columns (FA = 4 W blocks, FB = 1 row
+  // block), so no two waves read and split the same A rows.
+  constexpr int FA = AF32 ? 4 : 2, FB = AF32 ? 1 : 2;
+  const int xbase = AF32 ? 32 * wave : wm * 64;
+  const int wbase = AF32 ? 0 : wn * 64;
   const int i = lane & 31, h = lane >> 5;
   const int fs = x6_qswz(i);
-  const int offX = (wm * 64 + i) * kXBK;
-  const int offW = (wn * 64 + i) * kXBK;
+  const int offX = (xbase + i) * kXBK;
+  const int offW = (wbase + i) * kXBK;
 
-  x6_f32x16 acc[2][2], acs[2][2];
+  x6_f32x16 acc[FA][FB], acs[FA][FB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < FA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < FB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
 
@@ -382,26 +388,28 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     if (dbg & 1) return;
     const DGMC_LDS __bf16* la = buf;
     const DGMC_LDS __bf16* lb = buf + AREG;
-    x6_bf16x8 w[2][3][2], x[2][3][2];
+    x6_bf16x8 w[2][3][FA], x[2][3][FB];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       const int qo = 8 * ((2 * st + h) ^ fs);
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < 3; ++p) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
+        for (int a = 0; a < FA; ++a)
           w[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
               lb + p * kXBPlane + offW + a * 32 * kXBK + qo);
+#pragma unroll
+        for (int b = 0; b < FB; ++b)
           if (!AF32)
-            x[st][p][a] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
-                la + p * kXAPlane + offX + a * 32 * kXBK + qo);
-        }
+            x[st][p][b] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
+                la + p * kXAPlane + offX + b * 32 * kXBK + qo);
+      }
       if (AF32) {
         // 8 consecutive k of row r: logical chunks 4 st + 2 h, + 1.
         const DGMC_LDS float* lf = reinterpret_cast<const DGMC_LDS float*>(la);
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int r = wm * 64 + a * 32 + i;
+        for (int a = 0; a < FB; ++a) {
+          const int r = xbase + a * 32 + i;
           const int sw = (r >> 1) & 7, c0 = 4 * st + 2 * h;
           const x6_f32x4 u0 = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
               lf + r * kXBK + 4 * (c0 ^ sw));
@@ -421,9 +429,9 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
 #pragma unroll
     for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < FA; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < FB; ++b) {
           x6_f32x16 sm = acs[a][b];
           sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][2][a], x[st][0][b], sm, 0, 0, 0);
           sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[st][0][a], x[st][2][b], sm, 0, 0, 0);
@@ -436,12 +444,12 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
         }
   };
   auto epilogue = [&](int j) {
-    const int m0 = row_tile(j) * kXBM + wm * 64 + i;
-    const int n0 = col_tile(j) * kX6BN + wn * 64 + 4 * h;
+    const int m0 = row_tile(j) * kXBM + xbase + i;
+    const int n0 = col_tile(j) * kX6BN + wbase + 4 * h;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < FA; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < FB; ++b) {
         float* yrow = Y + (size_t)(m0 + 32 * b) * Nn + n0 + 32 * a;
         const bool store = m0 + 32 * b < m_lim;    // (dense: rows past M)
 #pragma unroll

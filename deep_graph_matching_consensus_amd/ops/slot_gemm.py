@@ -53,9 +53,10 @@ F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
 ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
 # bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging).
 F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
-# (only for in <= 128: tools/bench_slot_gemm_x6.py, 128->128 43.4 -> 39.5 us,
-# but 256->256 117 -> 120 and 1024->256 360 -> 369 us)
-F32X_KMAX = int(os.environ.get('DGMC_AMD_X6_F32X_KMAX', '128'))
+# (tools/bench_slot_gemm_x6.py with the 32 x 128 wave tiles of the fp32-A
+# kernel: 128->128 42.9 -> 38.0 us, 256->256 115 -> 113, 1024->256 351 -> 346
+# vs bf16 planes; the 64 x 64 tiles were slower than planes beyond K = 128)
+F32X_KMAX = int(os.environ.get('DGMC_AMD_X6_F32X_KMAX', '4096'))
 # ... and the weight gradient reads fp32 X rows too (with F32DY: no operand
 # planes of X at all - no split pass, no plane output of the producing SpMM).
 # Off: measured slower (PascalVOC 5.57 -> 5.66 ms: both operands' column
