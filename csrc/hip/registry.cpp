@@ -265,7 +265,8 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
 at::Tensor slot_weight_t(const at::Tensor& weight,
                          const c10::optional<at::Tensor>& root);
 at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt);
-at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt);
+at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt,
+                       const c10::optional<at::Tensor>& b3);
 at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
                            at::TensorList gs, const at::Tensor& seg01);
 at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
@@ -501,7 +502,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm_x6(Tensor a3, Tensor src, Tensor seg, Tensor b3, bool gather, "
       "Tensor? tiles=None) -> Tensor");
   m.def("dense_nt_f32(Tensor[] parts, Tensor bt) -> Tensor");
-  m.def("dense_nt_x6(Tensor[] parts, Tensor bt) -> Tensor");
+  m.def("dense_nt_x6(Tensor[] parts, Tensor bt, Tensor? b3=None) -> Tensor");
   m.def(
       "dense_wgrad_f32(Tensor[] xparts, int nparts, Tensor[] gs, Tensor "
       "seg01) -> Tensor");

@@ -779,9 +779,10 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
 // stages of fp32 row images ([64][32] floats, 16-byte chunks XOR-swizzled by
 // row bits 1-3: conflict-free ds_read_b128), each fragment split into its
 // three bf16 terms in registers.  Rows past M are clamped on load and not
-// stored.  tools/micro/bench_dense_nt.py: [10944, 128] x [128, 384] 24.1 ->
-// 15.6 us vs the exact-f32 kernel, [10944, 384] x [384, 128] 18.7 -> 18.1 us
-// (a four-stage ring, three chunks in flight, changed nothing: 18.8 us).
+// stored.  tools/micro/bench_dense_nt.py: [10944, 128] x [128, 384] 24.4 ->
+// 14.9 us vs the exact-f32 kernel, [10944, 384] x [384, 128] 18.9 -> 15.1 us
+// with B as pre-split planes (18.4 us splitting B in registers too; a
+// four-stage ring, three chunks in flight, changed nothing).
 // ---------------------------------------------------------------------------
 struct NtParts {
   const float* p[4];
@@ -791,23 +792,39 @@ constexpr int kNtT = 64;                    // tile rows / columns
 constexpr int kNtK = 32;                    // k per chunk
 constexpr int kNtImg = kNtT * kNtK;         // floats per operand image
 
+// B3: Bt given as bf16 planes [3][Nn][K] (split once per forward scope by the
+// caller): only the A rows are split in registers.
+template <bool B3>
 __global__ __launch_bounds__(256, 4) void dense_nt_x6_kernel(
-    NtParts A, int M, const float* __restrict__ bt, int K, int Nn,
-    float* __restrict__ Y) {
-  __shared__ __attribute__((aligned(16))) float lds_[2 * 2 * kNtImg];
+    NtParts A, int M, const float* __restrict__ bt,
+    const __bf16* __restrict__ b3, int K, int Nn, float* __restrict__ Y) {
+  constexpr int BIMG = B3 ? 3 * kNtT * kNtK / 2 : kNtImg;   // floats
+  constexpr int STG = kNtImg + BIMG;
+  __shared__ __attribute__((aligned(16))) float lds_[2 * STG];
   DGMC_LDS float* lds = (DGMC_LDS float*)lds_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
   const int ntn = Nn / kNtT, nk = K / kNtK;
   const int m0 = (blockIdx.x / ntn) * kNtT, n0 = (blockIdx.x % ntn) * kNtT;
-  // Staging: wave w fills rows 16 w + 8 e + L / 8 (e < 2) of both images;
-  // lane L holds physical chunk L % 8 = logical (L % 8) ^ ((row >> 1) & 7).
+  // Staging: wave w fills rows 16 w + 8 e + L / 8 (e < 2) of the fp32
+  // images; lane L holds physical chunk L % 8 = logical (L % 8) ^ ((row >> 1)
+  // & 7).  B3: DMA t = 3 w + e (e < 3) fills plane t / 4, rows 16 (t % 4) +
+  // L / 4, lane L holding physical quad L % 4 = logical (L % 4) ^ swz(row).
   int srow[2], sq[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     srow[e] = 16 * wave + 8 * e + (lane >> 3);
     sq[e] = 4 * ((lane & 7) ^ ((srow[e] >> 1) & 7));
   }
+  int bpl[3], brw[3], bqd[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int t = 3 * wave + e;
+    bpl[e] = t >> 2;
+    brw[e] = 16 * (t & 3) + (lane >> 2);
+    bqd[e] = 8 * ((lane & 3) ^ x6_qswz(brw[e]));
+  }
+  const int64_t bplane = (int64_t)Nn * K;
   auto stage = [&](int kc, DGMC_LDS float* buf) {
     const int k0 = kc * kNtK;
     const float* part = A.p[k0 >> 7];
@@ -819,14 +836,25 @@ __global__ __launch_bounds__(256, 4) void dense_nt_x6_kernel(
                                                sq[e]),
                reinterpret_cast<DGMC_LDS __bf16*>(
                    buf + (16 * wave + 8 * e) * kNtK));
-      x6_dma16(reinterpret_cast<const __bf16*>(
-                   bt + (size_t)(n0 + srow[e]) * K + k0 + sq[e]),
-               reinterpret_cast<DGMC_LDS __bf16*>(
-                   buf + kNtImg + (16 * wave + 8 * e) * kNtK));
+      if (!B3)
+        x6_dma16(reinterpret_cast<const __bf16*>(
+                     bt + (size_t)(n0 + srow[e]) * K + k0 + sq[e]),
+                 reinterpret_cast<DGMC_LDS __bf16*>(
+                     buf + kNtImg + (16 * wave + 8 * e) * kNtK));
+    }
+    if (B3) {
+      DGMC_LDS __bf16* bb =
+          reinterpret_cast<DGMC_LDS __bf16*>(buf + kNtImg);
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        x6_dma16(b3 + bpl[e] * bplane + (size_t)(n0 + brw[e]) * K + k0 +
+                     bqd[e],
+                 bb + bpl[e] * kNtT * kNtK + (brw[e] - (lane >> 2)) * kNtK);
     }
   };
   const int i = lane & 31, h = lane >> 5;
   const int ra = wm * 32 + i, rb = wn * 32 + i;   // A (m) / Bt (n) rows
+  const int fs = x6_qswz(i);
   x6_f32x16 acc, acs;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = acs[r] = 0.f;
@@ -850,13 +878,23 @@ __global__ __launch_bounds__(256, 4) void dense_nt_x6_kernel(
   for (int kc = 0; kc < nk; ++kc) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     x6_barrier();
-    if (kc + 1 < nk) stage(kc + 1, lds + ((kc + 1) & 1) * 2 * kNtImg);
-    const DGMC_LDS float* buf = lds + (kc & 1) * 2 * kNtImg;
+    if (kc + 1 < nk) stage(kc + 1, lds + ((kc + 1) & 1) * STG);
+    const DGMC_LDS float* buf = lds + (kc & 1) * STG;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       x6_bf16x8 x[3], w[3];
       frag(buf, ra, st, x);
-      frag(buf + kNtImg, rb, st, w);
+      if (B3) {
+        const DGMC_LDS __bf16* lb =
+            reinterpret_cast<const DGMC_LDS __bf16*>(buf + kNtImg);
+        const int qo = 8 * ((2 * st + h) ^ fs);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          w[p] = *reinterpret_cast<const DGMC_LDS x6_bf16x8*>(
+              lb + p * kNtT * kNtK + rb * kNtK + qo);
+      } else {
+        frag(buf + kNtImg, rb, st, w);
+      }
       acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], acs, 0, 0, 0);
       acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], acs, 0, 0, 0);
       acs = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], acs, 0, 0, 0);
@@ -1226,7 +1264,8 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   return slot_fold_parts(part, it[1], S, Kin, C);
 }
 
-at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt) {
+at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt,
+                       const c10::optional<at::Tensor>& b3) {
   const int64_t np = (int64_t)parts.size();
   TORCH_CHECK(np >= 1 && np <= 4, "dense_nt_x6: 1..4 parts");
   const int64_t M = parts[0].size(0);
@@ -1248,10 +1287,20 @@ at::Tensor dense_nt_x6(at::TensorList parts, const at::Tensor& bt) {
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(bt.device());
   at::Tensor Y = at::empty({M, Nn}, bt.options());
   if (M == 0) return Y;
+  const bool planes = b3.has_value() && b3->defined();
+  if (planes)
+    TORCH_CHECK(b3->scalar_type() == at::kBFloat16 && b3->is_contiguous() &&
+                    b3->dim() == 3 && b3->size(0) == 3 && b3->size(1) == Nn &&
+                    b3->size(2) == K,
+                "dense_nt_x6: Bt planes bf16 [3, Nn, K]");
   const int64_t tiles = ((M + kNtT - 1) / kNtT) * (Nn / kNtT);
-  hipLaunchKernelGGL(dense_nt_x6_kernel, dim3((unsigned)tiles), dim3(256), 0,
-                     stream(), A, (int)M, bt.data_ptr<float>(), (int)K,
-                     (int)Nn, Y.data_ptr<float>());
+  hipLaunchKernelGGL(planes ? dense_nt_x6_kernel<true>
+                            : dense_nt_x6_kernel<false>,
+                     dim3((unsigned)tiles), dim3(256), 0, stream(), A, (int)M,
+                     bt.data_ptr<float>(),
+                     planes ? reinterpret_cast<const __bf16*>(b3->data_ptr())
+                            : nullptr,
+                     (int)K, (int)Nn, Y.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
   return Y;
 }

@@ -666,9 +666,17 @@ def _seg01(M, device):
 NT_X6 = os.environ.get('DGMC_AMD_X6_NT', '1') == '1'
 
 
-def _nt(ops):
+def _nt_x6():
     from . import slot_gemm
-    return ops.dense_nt_x6 if (NT_X6 and slot_gemm.X6) else ops.dense_nt_f32
+    return NT_X6 and slot_gemm.X6
+
+
+def _nt(ops, parts, bt, b3=None):
+    """``[parts] @ bt^T``; ``b3``: bf16x6 planes of ``bt`` (split once per
+    forward scope), used by the bf16x6 kernel."""
+    if _nt_x6():
+        return ops.dense_nt_x6(parts, bt, b3)
+    return ops.dense_nt_f32(parts, bt)
 
 
 class _CatMatmulF32(torch.autograd.Function):
@@ -683,17 +691,22 @@ class _CatMatmulF32(torch.autograd.Function):
     def forward(ctx, w_t, loop, *parts):
         from ..runtime.cache import cached
         ops = _backend.ops()
-        out = _nt(ops)(list(parts), w_t.detach().t().contiguous())
+        # Both B operands (w_t^T for the forward, w_t itself for the input
+        # gradient, k-contiguous) and their bf16x6 planes: built once per
+        # forward scope, shared by the consensus loop's uses.
+        key = ('cat_f32_w', w_t.data_ptr(), w_t._version, tuple(w_t.shape),
+               tuple(w_t.stride()))
+        bt = cached(key + ('t', ), lambda: w_t.detach().t().contiguous())
+        wc = cached(key, lambda: w_t.detach().contiguous())
+        x6 = _nt_x6()
+        bt3 = cached(key + ('t3', ), lambda: ops.split3(bt)) if x6 else None
+        wc3 = cached(key + ('3', ), lambda: ops.split3(wc)) if x6 else None
+        out = _nt(ops, list(parts), bt, bt3)
         ctx.loop, ctx.np = loop, len(parts)
-        # The backward's B operand (w_t itself, k-contiguous): one copy per
-        # forward scope, shared by the consensus loop's uses (was a clone
-        # per use in the backward).
-        wc = cached(('cat_f32_w', w_t.data_ptr(), w_t._version,
-                     tuple(w_t.shape), tuple(w_t.stride())),
-                    lambda: w_t.detach().contiguous())
         # The parts go through save_for_backward (autograd's version check
         # catches an in-place write to a part before the weight gradient).
         keep = tuple(parts) if ctx.needs_input_grad[0] else ()
+        ctx.wc3 = wc3
         ctx.save_for_backward(w_t, wc, *keep)
         ctx.idx = loop.register() if loop is not None else None
         return out
@@ -704,7 +717,8 @@ class _CatMatmulF32(torch.autograd.Function):
         ctx.parts = tuple(kept) if kept else None
         ops = _backend.ops()
         g = g.float().contiguous()
-        gx = _nt(ops)([g], wc)                                  # [M, 128 n]
+        gx = _nt(ops, [g], wc, ctx.wc3)                         # [M, 128 n]
+        ctx.wc3 = None
         grads = tuple(gx[:, 128 * i:128 * (i + 1)]
                       if ctx.needs_input_grad[2 + i] else None
                       for i in range(ctx.np))

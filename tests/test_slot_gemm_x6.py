@@ -438,6 +438,8 @@ def test_dense_nt_x6_error_not_above_exact_f32(M, parts, Nn):
     ref = torch.cat(ps, 1).double() @ bt.double().t()
     y6 = ops.dense_nt_x6(ps, bt)
     assert y6.shape == (M, Nn)
+    # pre-split B planes: the same products, bit for bit
+    assert torch.equal(ops.dense_nt_x6(ps, bt, ops.split3(bt)), y6)
     e6 = float((y6.double() - ref).abs().max())
     if Nn % 64 == 0 and M >= 64:
         y32 = ops.dense_nt_f32(ps, bt)

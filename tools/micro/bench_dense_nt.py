@@ -31,9 +31,12 @@ def main():
     for M, parts, Nn in ((10944, 3, 128), (10944, 1, 384)):
         ps = [torch.randn(M, 128, device='cuda') for _ in range(parts)]
         bt = torch.randn(Nn, 128 * parts, device='cuda')
+        b3 = ops.split3(bt)
         print(json.dumps({'M': M, 'K': 128 * parts, 'N': Nn,
                           'f32_us': timeit(lambda: ops.dense_nt_f32(ps, bt)),
-                          'x6_us': timeit(lambda: ops.dense_nt_x6(ps, bt))}))
+                          'x6_us': timeit(lambda: ops.dense_nt_x6(ps, bt)),
+                          'x6_b3_us': timeit(lambda: ops.dense_nt_x6(ps, bt,
+                                                                     b3))}))
 
 
 if __name__ == '__main__':
