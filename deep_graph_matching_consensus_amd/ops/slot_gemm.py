@@ -47,15 +47,19 @@ X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
 # (+0.03 ms per PascalVOC step for the extra fold); PIECES_ALWAYS=1 pieces
 # regardless (tests compare a one-rank RCCL run bit-for-bit with that).
 PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
+PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
+PIECE_BYTES = 8 << 20
 # bf16x6 backward on fp32 dY_c (split inside the dX / dW kernels' LDS
 # staging) instead of the rowmap SpMM writing three bf16 planes.
 F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
+# Rowmap SpMM entries from a per-step inline (col, val) table.
 ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
-# bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging).
+# bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging) for
+# in <= F32X_KMAX (tools/bench_slot_gemm_x6.py with the 32 x 128 wave tiles
+# of the fp32-A kernel: 128->128 42.9 -> 38.0 us, 256->256 115 -> 113,
+# 1024->256 351 -> 346 vs bf16 planes; the earlier 64 x 64 tiles were slower
+# than planes beyond K = 128).
 F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
-# (tools/bench_slot_gemm_x6.py with the 32 x 128 wave tiles of the fp32-A
-# kernel: 128->128 42.9 -> 38.0 us, 256->256 115 -> 113, 1024->256 351 -> 346
-# vs bf16 planes; the 64 x 64 tiles were slower than planes beyond K = 128)
 F32X_KMAX = int(os.environ.get('DGMC_AMD_X6_F32X_KMAX', '4096'))
 # ... and the weight gradient reads fp32 X rows too (with F32DY: no operand
 # planes of X at all - no split pass, no plane output of the producing SpMM).
@@ -65,9 +69,9 @@ F32X_WGRAD = os.environ.get('DGMC_AMD_X6_F32X_WGRAD', '0') == '1'
 
 
 def _x_planes_free():
+    """No bf16 planes of X are needed anywhere (forward and weight
+    gradient both read fp32 X)."""
     return F32X and F32DY and F32X_WGRAD
-PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
-PIECE_BYTES = 8 << 20
 
 
 class CompactPlan(object):

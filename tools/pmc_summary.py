@@ -1,7 +1,9 @@
 """Per-(kernel, grid) averages of a rocprofv3 ``--pmc`` run's
 ``counter_collection.csv`` (one line per kernel and grid size).
 
-    python tools/pmc_summary.py <counter_collection.csv> [name-filter, e.g. dgmc::] > out
+    python tools/pmc_summary.py <counter_collection.csv> [filter] > out
+
+(filter: a kernel-name substring, e.g. ``dgmc::``.)
 """
 import collections
 import csv
