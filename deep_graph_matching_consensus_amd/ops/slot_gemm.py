@@ -162,11 +162,14 @@ def _x6_rounds(tiles):
     items are sized for (more items: better balance, more partial bytes
     for the fold)."""
     if tiles == 1:
-        return 1
+        return X6_WGRAD_ROUNDS_ONE
     return 2 if tiles <= 4 else X6_WGRAD_ROUNDS_BIG
 
 
 X6_WGRAD_ROUNDS_BIG = int(os.environ.get('DGMC_AMD_X6_WGRAD_ROUNDS', '6'))
+# (single-tile shapes, psi_2's 10-use gradient: 1 / 2 / 3 rounds measured
+# 5.637 / 5.658 / 5.68 ms per PascalVOC step)
+X6_WGRAD_ROUNDS_ONE = int(os.environ.get('DGMC_AMD_X6_WGRAD_ROUNDS_ONE', '1'))
 
 
 def weight_grad_x6(x3s, dy3s, plan, cin, cout):
