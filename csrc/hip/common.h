@@ -163,6 +163,27 @@ __host__ __device__ inline bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 
+// Diagnostic knobs (kernel ablations, relaxed top-k margins, forced split
+// counts) exist only in the diagnostic library (`tools/build_native.py
+// --diag` -> _C_hip_diag.so, compiled with -DDGMC_DIAG, loaded when
+// DGMC_AMD_DIAG=1).  The production library never reads the environment
+// for them: it always uses `dflt`, so no stray variable can skip MFMAs or
+// shrink a proven error margin.
+#ifdef DGMC_DIAG
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+inline int diag_env_int(const char* name, int dflt) {
+#ifdef DGMC_DIAG
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
+
 }  // namespace dgmc
 
 // Dispatch over the floating types our kernels accept (f32, bf16, f16).

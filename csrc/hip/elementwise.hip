@@ -18,16 +18,12 @@
 namespace dgmc {
 
 namespace {
-// Partial rows folded by the 2nd kernel (DGMC_COLSUM_MAXBLOCKS; keep in sync
-// with ops/gemm.py::col_partial_rows).  1024: a [11k, 128] gradient gets one
-// 16-row pass per block instead of ~6 sequential passes at 1 wave per SIMD.
-int max_col_blocks() {
-  static const int v = [] {
-    const char* e = getenv("DGMC_COLSUM_MAXBLOCKS");
-    return e ? atoi(e) : 1024;
-  }();
-  return v;
-}
+// Partial rows folded by the 2nd kernel (keep in sync with
+// ops/gemm.py::col_partial_rows, which sizes the callers' partial buffers).
+// 1024: a [11k, 128] gradient gets one 16-row pass per block instead of ~6
+// sequential passes at 1 wave per SIMD.
+constexpr int kMaxColBlocks = 1024;
+int max_col_blocks() { return kMaxColBlocks; }
 }  // namespace
 
 // NOTE (MI355X): a single-kernel "last block folds" reduction needs a

@@ -1304,12 +1304,10 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_ell_kernel(
   }
 }
 
-static int rowmap_rpl() {     // DGMC_ROWMAP_RPL: rows per lane group (1: off)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DGMC_ROWMAP_RPL");
-    v = e ? atoi(e) : 2;
-  }
+// Rows per lane group of the ELL rowmap SpMM (2; DGMC_ROWMAP_RPL=1 in the
+// diagnostic build restores one row per group).
+static int rowmap_rpl() {
+  static const int v = diag_env_int("DGMC_ROWMAP_RPL", 2);
   return v;
 }
 

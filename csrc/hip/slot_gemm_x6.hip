@@ -195,46 +195,15 @@ __device__ __forceinline__ int x6_qswz(int r) {
   return (((r >> 2) & 1) ^ b4) | ((((r >> 3) & 1) ^ b4) << 1);
 }
 
-// XCD-local 256-row units of the compact row space (as slot_gemm.hip's
-// sg_xcd_unit): slot segments list their rows in source-node order, so the
-// x-th eighth of every segment covers about the x-th eighth of the nodes.
-// Returns the first row of XCD x's i-th unit (-1 past the end) and, in
-// *total, XCD x's unit count.  Wave-wide (lane s holds slot s).
-__device__ __forceinline__ int x6_xcd_unit(const int* __restrict__ seg, int S,
-                                           int x, int i, int* total) {
-  const int lane = threadIdx.x & 63;
-  const int sv = lane <= S ? seg[lane] : 0;
-  const int sn = __shfl_down(sv, 1);
-  int lo = 0, cnt = 0;
-  if (lane < S) {
-    const int q = (sn - sv) / kXBM;
-    lo = q * x / kNumXcd;
-    cnt = q * (x + 1) / kNumXcd - lo;
-  }
-  int incl = cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  *total = __shfl(incl, S - 1);
-  const unsigned long long hit = __ballot(lane < S && incl > i);
-  if (hit == 0ull) return -1;
-  const int sl = __ffsll((long long)hit) - 1;
-  const int base = __shfl(sv, sl), first = __shfl(lo, sl),
-            before = __shfl(incl - cnt, sl);
-  return base + (first + i - before) * kXBM;
-}
-
-// XL (forward, K <= 256): workgroup b works on XCD b % 8's node eighth of
-// every slot, so the X rows it gathers (<= 1 / 8 of X) stay in that XCD's
-// L2 (grid = a multiple of 8, dispatched round-robin over the XCDs).
+// (An XCD-local tile order - workgroup b on XCD b % 8's node eighth of every
+// slot - measured slower: 128->128 50.5 vs 44.3 us, 256->256 130 vs 111 us,
+// profiles/bench_slot_gemm_x6_xl_r4.json; removed in round 5.)
 // AF32 (fp32 A: the input gradient's dY_c, or the forward's gathered X):
 // the A operand is staged
 // as fp32 row images ([256][32] floats, 16-byte chunks XOR-swizzled by row
 // bits 1-3 - conflict-free ds_read_b128) and split into the three bf16
 // terms in registers: dY_c is stored at 4 instead of 6 bytes per element.
-template <bool GATHER, bool XL, bool AF32 = false>
+template <bool GATHER, bool AF32 = false>
 __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
     const __bf16* __restrict__ A, int64_t a_plane, const int* __restrict__ src,
     const int* __restrict__ seg, int S, const __bf16* __restrict__ B,
@@ -255,11 +224,9 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   const int segv = lane <= S ? seg[lane] : 0x7fffffff;
   int nrt = tiles != nullptr ? tiles[tcap]
                               : __builtin_amdgcn_readlane(segv, S) / kXBM;
-  const int xcd = blockIdx.x % kNumXcd;
-  if (XL) x6_xcd_unit(seg, S, xcd, 0, &nrt);     // this XCD's unit count
   const int U = nrt * ntn;
-  const int G = XL ? gridDim.x / kNumXcd : gridDim.x;
-  const int u0 = XL ? blockIdx.x / kNumXcd : xcd_remap(blockIdx.x, G);
+  const int G = gridDim.x;
+  const int u0 = xcd_remap(blockIdx.x, G);
   if (u0 >= U) return;
   const int my_tiles = (U - u0 + G - 1) / G;
   const int total = my_tiles * nk;
@@ -268,10 +235,6 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   };
   auto row_tile = [&](int j) {          // j-th tile of this workgroup
     const int q = (u0 + j * G) / ntn;
-    if (XL) {
-      int dummy;
-      return x6_xcd_unit(seg, S, xcd, q, &dummy) / kXBM;
-    }
     return tiles != nullptr ? tiles[q] : q;
   };
   auto col_tile = [&](int j) { return (u0 + j * G) % ntn; };
@@ -340,7 +303,7 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
       set_tile(j);
       idx_dma(j + 1);
     }
-    if (dbg & 2) return;
+    if (kDiagBuild && (dbg & 2)) return;
     DGMC_LDS __bf16* buf = ring + (it & 1) * STG;
     const int k0 = kc * kXBK;
     if (AF32) {
@@ -385,7 +348,7 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
       for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
 
   auto compute = [&](const DGMC_LDS __bf16* buf) {
-    if (dbg & 1) return;
+    if (kDiagBuild && (dbg & 1)) return;
     const DGMC_LDS __bf16* la = buf;
     const DGMC_LDS __bf16* lb = buf + AREG;
     x6_bf16x8 w[2][3][FA], x[2][3][FB];
@@ -967,27 +930,10 @@ at::Tensor slot_weight_x3(const at::Tensor& weight,
   return img;
 }
 
-// Largest K of the XCD-local forward mapping (DGMC_X6_XL_KMAX; default 0 =
-// off: measured SLOWER on the headline plan - 128->128 50.5 vs 44.3 us,
-// 256->256 130 vs 111 us, 1024->256 equal; profiles/bench_slot_gemm_x6_xl_r4
-// .json.  The slot-segment order already keeps a W_s image hot in L2).
-static int x6_xl_kmax() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DGMC_X6_XL_KMAX");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-// DGMC_X6_DEBUG (diagnostic ablations, never set in production runs):
-// bit 0 skips the MFMAs, bit 1 the operand DMAs.
+// DGMC_X6_DEBUG (diagnostic build only): bit 0 skips the MFMAs, bit 1 the
+// operand DMAs.
 static int x6_debug() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DGMC_X6_DEBUG");
-    v = e ? atoi(e) : 0;
-  }
+  static const int v = diag_env_int("DGMC_X6_DEBUG", 0);
   return v;
 }
 
@@ -1033,16 +979,11 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   const __bf16* ap = reinterpret_cast<const __bf16*>(a3.data_ptr());
   const __bf16* bp = reinterpret_cast<const __bf16*>(b3.data_ptr());
   const int* tl = listed ? tiles->data_ptr<int>() : nullptr;
-  // XCD-local forward tiles where the gathered X (and the weights) fit the
-  // XCDs' L2s (K <= 256); the 1024-wide psi_1 layer streams.
-  const bool xl = gather && !af32 && !listed && K <= x6_xl_kmax() &&
-                  blocks >= 64;
-  auto kern = af32 ? (gather ? slot_gemm_x6_kernel<true, false, true>
-                             : slot_gemm_x6_kernel<false, false, true>)
-              : gather ? (xl ? slot_gemm_x6_kernel<true, true>
-                             : slot_gemm_x6_kernel<true, false>)
+  auto kern = af32 ? (gather ? slot_gemm_x6_kernel<true, true>
+                             : slot_gemm_x6_kernel<false, true>)
+              : gather ? slot_gemm_x6_kernel<true, false>
                        : slot_gemm_x6_kernel<false, false>;
-  const int64_t grid = xl ? blocks / kNumXcd * kNumXcd : blocks;
+  const int64_t grid = blocks;
   const size_t lds = af32 ? (size_t)2 * (2 * kXBM * kXBK + 3 * kXBPlane) * 2 +
                                 2 * kXBM * 4
                           : kXLds;

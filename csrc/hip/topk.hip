@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll 4
-    for (int s = 0; s < ((dbg & 2) ? 0 : CP / 8); ++s) {
+    for (int s = 0; s < ((kDiagBuild && (dbg & 2)) ? 0 : CP / 8); ++s) {
       const float4 a = *reinterpret_cast<const float4*>(aRow + 8 * s);
       const float4 bb = *reinterpret_cast<const float4*>(bRow + 8 * s);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bb.x, acc, 0, 0, 0);
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void topk_dot_kernel(
     if (t + 1 < ntiles) store_tile(sB, pre);
 
     const int j = t * kTile + lane;
-    const bool col_ok = j < Nt && !(dbg & 1);
+    const bool col_ok = j < Nt && !(kDiagBuild && (dbg & 1));
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int row = wave * 16 + q;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if (!(dbg & 2)) {
+    if (!(kDiagBuild && (dbg & 2))) {
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const bf16x8 vh = *reinterpret_cast<const DGMC_LDS bf16x8*>(bh + 16 * ks);
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     }
     if (t + 1 < ntiles) store_tile((t + 1) & 1, pre);
 
-    const bool col_ok = j0 + hl < j_end && !(dbg & 1);
+    const bool col_ok = j0 + hl < j_end && !(kDiagBuild && (dbg & 1));
     // One wave vote for the whole tile first: once the lists have filled,
     // most tiles hold no candidate beating any row's k-th score, and the
     // 16 per-row votes below are skipped.
@@ -429,11 +429,11 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 // multiple of 8 channels) and broadcast to the lanes' chains.
 // ---------------------------------------------------------------------------
 constexpr float kTopkTau = 1.0f / 8192.0f;
-// DGMC_TOPK_TAU_LOG2 (diagnostics): tau = 2^-value.
+// DGMC_TOPK_TAU_LOG2 (diagnostic build only): tau = 2^-value.
 static float topk_tau() {
   static const float v = [] {
-    const char* e = getenv("DGMC_TOPK_TAU_LOG2");
-    return e ? ldexpf(1.0f, -atoi(e)) : kTopkTau;
+    const int e = diag_env_int("DGMC_TOPK_TAU_LOG2", 0);
+    return e > 0 ? ldexpf(1.0f, -e) : kTopkTau;
   }();
   return v;
 }
@@ -573,11 +573,8 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
   // pass's insertion work grows ~K2 ln(Nt / K2); a row whose K2-th
   // candidate still clears the margin is recomputed exhaustively, so K2
   // only trades filter time against (rare) fallbacks.  DGMC_TOPK_K2
-  // overrides (diagnostics).
-  static const int k2_env = [] {
-    const char* e = getenv("DGMC_TOPK_K2");
-    return e ? atoi(e) : 0;
-  }();
+  // overrides (diagnostic build only).
+  static const int k2_env = diag_env_int("DGMC_TOPK_K2", 0);
   int K2 = k2_env > 0 ? k2_env : std::max<int>(16, (int)k + 6);
   K2 = std::min(std::min(32, Nt), std::max<int>(K2, (int)k));
   at::Tensor cv;
@@ -604,12 +601,9 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
 }
 
 // (The kernels' dbg argument - 1 skip selection, 2 skip MFMA - is an
-// ablation knob: DGMC_TOPK_DEBUG, never set in production runs.)
+// ablation knob: DGMC_TOPK_DEBUG, diagnostic build only.)
 static int topk_debug() {
-  static const int v = [] {
-    const char* e = getenv("DGMC_TOPK_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = diag_env_int("DGMC_TOPK_DEBUG", 0);
   return v;
 }
 
@@ -646,10 +640,8 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
   const int row_blocks = (Ns + 32 * W - 1) / (32 * W);
   int S = x3_splits((int64_t)row_blocks * B, Nt, W == 8 ? 1 : 2);
   {
-    static const int s_env = [] {     // DGMC_TOPK_SPLITS: diagnostics only
-      const char* e = getenv("DGMC_TOPK_SPLITS");
-      return e ? atoi(e) : 0;
-    }();
+    // DGMC_TOPK_SPLITS: diagnostic build only
+    static const int s_env = diag_env_int("DGMC_TOPK_SPLITS", 0);
     if (s_env > 0) S = s_env;
   }
   int span = (Nt + S - 1) / S;

@@ -24,14 +24,25 @@ _STATE = {'hip': None, 'host': None}
 
 
 def _find(name):
-    hits = sorted(glob.glob(osp.join(_PKG_DIR, name + '*.so')))
+    hits = sorted(glob.glob(osp.join(_PKG_DIR, name + '.so')) +
+                  glob.glob(osp.join(_PKG_DIR, name + '.*.so')))
     return hits[0] if hits else None
+
+
+def diag_requested():
+    """``DGMC_AMD_DIAG=1``: load the diagnostic HIP library
+    (``tools/build_native.py --diag``), whose kernel ablation knobs read the
+    environment.  Never for measurements of record."""
+    return os.environ.get('DGMC_AMD_DIAG', '0') == '1'
 
 
 def _load(kind):
     if _STATE[kind] is not None:
         return _STATE[kind]
-    path = _find('_C_' + kind)
+    name = '_C_' + kind
+    if kind == 'hip' and diag_requested():
+        name += '_diag'
+    path = _find(name)
     ok = False
     if path is not None:
         try:

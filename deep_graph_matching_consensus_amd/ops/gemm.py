@@ -217,7 +217,8 @@ class _MixedMatmul(torch.autograd.Function):
         return gx, gw, None, gb, None
 
 
-_COL_MAX_BLOCKS = int(os.environ.get('DGMC_COLSUM_MAXBLOCKS', '1024'))
+# (= csrc/hip/elementwise.hip::kMaxColBlocks)
+_COL_MAX_BLOCKS = 1024
 
 
 def col_partial_rows(rows):

@@ -1546,21 +1546,38 @@ def test_fold_weights_kernel():
     assert torch.equal(wnt, w.t().contiguous().bfloat16())
 
 
-@pytest.mark.parametrize('slot_gemm', [True, False])
-def test_dgmc_fp32_headline_widths_vs_reference_mode(slot_gemm, monkeypatch):
+# Every alternative kernel path still behind a switch (each measured slower
+# or kept as an exact-f32 fallback, docs/performance.md) is exercised here
+# against the reference expression: (module, attribute, value).
+_SWITCHES = [None, ('slot_gemm', 'ENABLED', False),
+             ('slot_gemm', 'X6', False), ('slot_gemm', 'F32DY', False),
+             ('slot_gemm', 'F32X', False), ('slot_gemm', 'ROWMAP_ELL', False),
+             ('slot_gemm', 'F32X_WGRAD', True), ('dense', 'NT_X6', False),
+             ('dense', 'FUSE_STEPS', False)]
+
+
+@pytest.mark.parametrize('switch', _SWITCHES,
+                         ids=lambda s: 'default' if s is None else
+                         '{}.{}={}'.format(*s))
+def test_dgmc_fp32_headline_widths_vs_reference_mode(switch, monkeypatch):
     """fp32 at the flagship's layer widths (psi_1 in/out multiples of 128,
     psi_2 128 -> 128 with cat=True): the step runs the fp32 slot GEMMs,
     the folded projection on the dense fp32 GEMM, the fused pair-step and
     objective kernels; outputs, loss and every parameter gradient match the
     reference-mode expression (``/root/reference/dgmc/models/dgmc.py:
     163-244``, fp32) to fp32 tolerance (loss 1e-5 relative, gradients 1e-4
-    relative to their largest entry).  ``slot_gemm=False``: the
-    ``DGMC_AMD_SLOT_GEMM=0`` alternative (GEMM over all slots + SpMM)."""
+    relative to their largest entry).  ``switch``: one alternative path
+    (e.g. ``slot_gemm.ENABLED=False``: GEMM over all slots + SpMM;
+    ``slot_gemm.X6=False``: the exact-f32 MFMA kernels)."""
     from deep_graph_matching_consensus_amd.datasets import (
         GraphStore, DevicePairLoader, make_keypoint_datasets)
     from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.ops import dense as dense_mod
     from deep_graph_matching_consensus_amd.ops import slot_gemm as sg
-    monkeypatch.setattr(sg, 'ENABLED', slot_gemm)
+    if switch is not None:
+        mod = {'slot_gemm': sg, 'dense': dense_mod}[switch[0]]
+        assert hasattr(mod, switch[1])
+        monkeypatch.setattr(mod, switch[1], switch[2])
     groups = make_keypoint_datasets(graphs=8, feature_dim=256, seed=0)
     store = GraphStore(groups, DEV)
     batch = next(iter(DevicePairLoader(store, batch_size=32, seed=0)))

@@ -9,6 +9,11 @@ kernels are written for CDNA4 directly, so we drive ``hipcc`` ourselves:
 Outputs (loaded with ``torch.ops.load_library``):
   deep_graph_matching_consensus_amd/_C_hip.so   gfx950 kernels + op registry
   deep_graph_matching_consensus_amd/_C_host.so  host C++ runtime (OpenMP)
+
+``--diag`` builds ``_C_hip_diag.so`` instead (``-DDGMC_DIAG``: the kernel
+ablation / margin / split knobs of ``csrc/hip/common.h::diag_env_int`` read
+the environment); it is loaded only when ``DGMC_AMD_DIAG=1``.  The
+production library ignores those variables.
 """
 import argparse
 import glob
@@ -38,17 +43,19 @@ def _ninja_escape(p):
     return p.replace('$', '$$').replace(' ', '$ ').replace(':', '$:')
 
 
-def write_ninja(debug=False):
+def write_ninja(debug=False, diag=False):
     inc, lib, abi = _torch_paths()
-    os.makedirs(BUILD, exist_ok=True)
+    build_dir = BUILD + '_diag' if diag else BUILD
+    os.makedirs(build_dir, exist_ok=True)
     incs = ' '.join('-isystem ' + p for p in inc)
     common = ('-fPIC -std=c++17 -D_GLIBCXX_USE_CXX11_ABI={} '
               '-D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 {}').format(abi, incs)
     opt = '-O0 -g' if debug else '-O3'
     hipcc = osp.join(ROCM, 'bin', 'hipcc')
     hip_flags = ('{} {} -x hip --offload-arch={} -fno-gpu-rdc '
-                 '-munsafe-fp-atomics -I{}'.format(
-                     opt, common, ARCH, osp.join(ROOT, 'csrc', 'hip')))
+                 '-munsafe-fp-atomics -I{}{}'.format(
+                     opt, common, ARCH, osp.join(ROOT, 'csrc', 'hip'),
+                     ' -DDGMC_DIAG=1' if diag else ''))
     host_flags = '{} {} -fopenmp -Wall -Wno-unused-function -I{}'.format(
         opt, common, osp.join(ROOT, 'csrc', 'host'))
     libs_hip = ('-L{0} -Wl,-rpath,{0} -lc10 -ltorch -ltorch_cpu -lc10_hip '
@@ -80,17 +87,17 @@ def write_ninja(debug=False):
                      glob.glob(osp.join(ROOT, 'csrc', 'hip', '*.cpp')))
     objs = []
     for src in hip_src:
-        obj = osp.join(BUILD, 'hip', osp.basename(src) + '.o')
+        obj = osp.join(build_dir, 'hip', osp.basename(src) + '.o')
         lines.append('build {}: hipcc {}'.format(_ninja_escape(obj),
                                                  _ninja_escape(src)))
         objs.append(obj)
-    out = osp.join(PKG, '_C_hip.so')
+    out = osp.join(PKG, '_C_hip_diag.so' if diag else '_C_hip.so')
     lines.append('build {}: link_hip {}'.format(
         _ninja_escape(out), ' '.join(_ninja_escape(o) for o in objs)))
     targets.append(out)
 
     host_src = sorted(glob.glob(osp.join(ROOT, 'csrc', 'host', '*.cpp')))
-    if host_src:
+    if host_src and not diag:
         objs = []
         for src in host_src:
             obj = osp.join(BUILD, 'host', osp.basename(src) + '.o')
@@ -102,29 +109,31 @@ def write_ninja(debug=False):
             _ninja_escape(out), ' '.join(_ninja_escape(o) for o in objs)))
         targets.append(out)
     lines.append('default ' + ' '.join(_ninja_escape(t) for t in targets))
-    with open(osp.join(BUILD, 'build.ninja'), 'w') as f:
+    with open(osp.join(build_dir, 'build.ninja'), 'w') as f:
         f.write('\n'.join(lines) + '\n')
     return targets
 
 
-def build(jobs=None, debug=False, verbose=False):
+def build(jobs=None, debug=False, verbose=False, diag=False):
     """Incremental ninja build (gcc-style depfiles track every included
     header; ninja also rebuilds an object whose command line changed), then
     a dry run that must report nothing left to do, and a manifest
     (``build/native/manifest.json``: sha256 of every source and library) of
     what the libraries were built from."""
-    targets = write_ninja(debug)
+    targets = write_ninja(debug, diag)
+    build_dir = BUILD + '_diag' if diag else BUILD
     jobs = jobs or min(16, os.cpu_count() or 4)
-    cmd = ['ninja', '-C', BUILD, '-j', str(jobs)]
+    cmd = ['ninja', '-C', build_dir, '-j', str(jobs)]
     if verbose:
         cmd.append('-v')
     subprocess.check_call(cmd)
-    dry = subprocess.run(['ninja', '-C', BUILD, '-n'], check=True,
+    dry = subprocess.run(['ninja', '-C', build_dir, '-n'], check=True,
                          capture_output=True, text=True).stdout
     if 'no work to do' not in dry:
         raise RuntimeError('native build not up to date after ninja:\n' +
                            dry)
-    _write_manifest(targets)
+    if not diag:
+        _write_manifest(targets)
     return targets
 
 
@@ -150,6 +159,7 @@ def _write_manifest(targets):
 
 def clean():
     shutil.rmtree(BUILD, ignore_errors=True)
+    shutil.rmtree(BUILD + '_diag', ignore_errors=True)
     for so in glob.glob(osp.join(PKG, '_C_*.so')):
         os.remove(so)
 
@@ -160,11 +170,13 @@ def main(argv=None):
     p.add_argument('--debug', action='store_true')
     p.add_argument('-j', '--jobs', type=int, default=None)
     p.add_argument('-v', '--verbose', action='store_true')
+    p.add_argument('--diag', action='store_true',
+                   help='diagnostic library _C_hip_diag.so (-DDGMC_DIAG)')
     args = p.parse_args(argv)
     if args.clean:
         clean()
         return 0
-    for t in build(args.jobs, args.debug, args.verbose):
+    for t in build(args.jobs, args.debug, args.verbose, args.diag):
         print('built', osp.relpath(t, ROOT))
     return 0
 

@@ -2,9 +2,10 @@
 C = 256): times mode 2 (default exact: filter + re-score), mode 0 (filter
 only, k list) and the filter with a 16-candidate list; run it under
 DGMC_TOPK_DEBUG=1 (selection skipped) / 2 (MFMA skipped) to split the
-filter kernel's time.
+filter kernel's time.  The knob exists only in the diagnostic library:
 
-    DGMC_TOPK_DEBUG=1 python tools/micro/topk_ablation.py
+    python tools/build_native.py --diag
+    DGMC_AMD_DIAG=1 DGMC_TOPK_DEBUG=1 python tools/micro/topk_ablation.py
 """
 import json
 import os
@@ -21,7 +22,8 @@ ops = _backend.ops()
 torch.manual_seed(0)
 hs = torch.randn(1, 19388, 256, device='cuda')
 ht = torch.randn(1, 19572, 256, device='cuda')
-out = {'debug': os.environ.get('DGMC_TOPK_DEBUG', '0')}
+out = {'debug': os.environ.get('DGMC_TOPK_DEBUG', '0'),
+       'diag_lib': _backend.diag_requested()}
 for name, k, mode in (('exact_k10', 10, 2), ('x3_k10', 10, 0),
                       ('x3_k16', 16, 0)):
     for _ in range(2):
