@@ -17,9 +17,14 @@ graph, Delaunay + Cartesian), random-init weights.  Every timed step runs the
 full forward (10 consensus iterations), backward, gradient all-reduce and the
 Adam update.
 
-Precision: fp32 by default - the reference trains in fp32 - with every
-GEMM on exact-fp32 MFMA (``v_mfma_f32_32x32x2_f32``); ``--dtype bf16`` is an
-opt-in fast mode.  After the timed steps, held-out Hits@1 / Hits@10 of S_L
+Precision: fp32 by default - the reference trains in fp32.  The SplineConv
+GEMMs and the folded consensus projection run as "bf16x6" on the bf16
+matrix cores (every fp32 operand split into three bf16 terms, the six
+products of order >= 2^-16 accumulated in fp32; max error vs an fp64 oracle
+at or below the exact ``v_mfma_f32_32x32x2_f32`` chain, gated by
+``tests/test_slot_gemm_x6.py``); ``DGMC_AMD_X6=0`` selects exact-fp32 MFMA
+kernels for them.  The JSON's ``gemm_arith`` names what ran.
+``--dtype bf16`` is an opt-in fast mode (bf16 operands), never the headline.  After the timed steps, held-out Hits@1 / Hits@10 of S_L
 are evaluated on ``--eval-pairs`` test pairs (untimed), like the
 reference's test loop.
 
@@ -152,8 +157,24 @@ def parse_args(argv=None):
                    help='dense correspondence normalisation: the reference '
                         'row softmax (headline) or the opt-in masked '
                         'log-domain Sinkhorn (BASELINE config 3)')
+    p.add_argument('--dp-mode', default='captured',
+                   choices=['captured', 'flat'],
+                   help='data-parallel gradient sync: bucketed all-reduces '
+                        'from the backward hooks captured in the step graph '
+                        '(RCCL), or one flat all-reduce after each replay')
     p.add_argument('--json-out', default=None)
     return p.parse_args(argv)
+
+
+def gemm_arith(dtype):
+    """What the encoder GEMMs computed in (bench JSON ``gemm_arith``)."""
+    from deep_graph_matching_consensus_amd.ops import slot_gemm
+    if dtype == 'bf16':
+        return 'bf16 operands, fp32 accumulation (opt-in fast mode)'
+    if slot_gemm.X6:
+        return ('bf16x6 (fp32-emulated: 3 bf16 terms per operand, 6 '
+                'products, fp32 accumulation)')
+    return 'exact_f32 (v_mfma_f32_32x32x2_f32)'
 
 
 def build_model(cfg, args, num_node_features, num_edge_features, device):
@@ -233,6 +254,48 @@ def bench_kg(args, cfg, device):
     return out
 
 
+def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
+    """Multi-GPU diagnostics: per-rank ms/step spread,
+    the DP mode actually used, the exposed all-reduce time (flat mode:
+    events around ``reducer.finish()`` of every timed step) and the cost of
+    one standalone all-reduce of the whole gradient buffer (what a fully
+    exposed sync would add per step)."""
+    ms = 1000.0 * rank_elapsed / max(steps, 1)
+    out = {'dp_mode': trainer.dp_mode_used}
+    if world == 1:
+        return out
+    import torch.distributed as dist
+    out['ms_per_step_rank_max'] = round(parallel.all_reduce_max(ms, device),
+                                        3)
+    out['ms_per_step_rank_min'] = round(
+        -parallel.all_reduce_max(-ms, device), 3)
+    cuda = device.type == 'cuda'
+    ev = trainer.allreduce_events
+    if ev:
+        torch.cuda.synchronize()
+        exp = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        out['allreduce_exposed_ms'] = round(
+            parallel.all_reduce_max(exp, device), 3)
+    trainer.allreduce_events = []
+    buf = torch.zeros_like(trainer.reducer.flat)
+    op = dist.ReduceOp.AVG if dist.get_backend() == 'nccl' else \
+        dist.ReduceOp.SUM
+    for _ in range(3):
+        dist.all_reduce(buf, op=op)
+    if cuda:
+        torch.cuda.synchronize()
+    a = time.perf_counter()
+    for _ in range(10):
+        dist.all_reduce(buf, op=op)
+    if cuda:
+        torch.cuda.synchronize()
+    t = 100.0 * (time.perf_counter() - a)
+    out['allreduce_standalone_ms'] = round(parallel.all_reduce_max(t, device),
+                                           3)
+    out['allreduce_bytes'] = int(buf.numel() * 4)
+    return out
+
+
 def main(argv=None):
     args = parse_args(argv)
     ngpu = torch.cuda.device_count()    # does not initialise HIP
@@ -285,7 +348,7 @@ def main(argv=None):
     trainer = PairTrainer(model, store, args.batch_size, lr=1e-3, mode=mode,
                           bf16=use_bf16, seed=args.seed,
                           overlap=not args.no_overlap,
-                          buckets=not args.no_buckets)
+                          buckets=not args.no_buckets, dp_mode=args.dp_mode)
 
     def sync():
         if device.type == 'cuda':
@@ -295,14 +358,19 @@ def main(argv=None):
         for _ in range(args.warmup):
             trainer.step()
         trainer.stats.zero_()
+        trainer.time_allreduce = world > 1 and device.type == 'cuda'
         parallel.barrier()
         sync()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             trainer.step()
         sync()
+        rank_elapsed = time.perf_counter() - t0
         parallel.barrier()
         elapsed = time.perf_counter() - t0
+        trainer.time_allreduce = False
+        dp_diag = dp_diagnostics(trainer, rank_elapsed, args.steps, world,
+                                 device)
         test_hits = None
         if args.eval_pairs > 0:
             test_groups = make_keypoint_datasets(
@@ -370,6 +438,8 @@ def main(argv=None):
     if test_hits is not None:
         out['hits@1_test'] = round(test_hits[1], 4)
         out['hits@10_test'] = round(test_hits[10], 4)
+    out['gemm_arith'] = gemm_arith(out['dtype'])
+    out.update(dp_diag)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -163,6 +163,21 @@ __host__ __device__ inline bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 
+// CUs left out of the persistent / CU-sized grids (x6 GEMMs, weight
+// gradients): under data parallelism RCCL's channel kernels run concurrently
+// with the backward and hold CUs; a persistent grid sized to every CU then
+// waits on its busiest one.  Set from Python (DGMC_AMD_RESERVE_CUS,
+// ops/_backend.py -> set_cu_reserve); 0 by default.
+inline int& cu_reserve() {
+  static int v = 0;
+  return v;
+}
+// `total` CUs minus the reserve (at least 1).
+inline int usable_cus(int total) {
+  const int r = cu_reserve();
+  return total - r >= 1 ? total - r : 1;
+}
+
 // Diagnostic knobs (kernel ablations, relaxed top-k margins, forced split
 // counts) exist only in the diagnostic library (`tools/build_native.py
 // --diag` -> _C_hip_diag.so, compiled with -DDGMC_DIAG, loaded when

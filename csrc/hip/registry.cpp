@@ -5,6 +5,11 @@
 #include <torch/library.h>
 
 namespace dgmc {
+int64_t set_cu_reserve(int64_t n);
+at::Tensor cu_hog(const at::Tensor& like, int64_t blocks, double usec);
+}  // namespace dgmc
+
+namespace dgmc {
 
 at::Tensor spmm_csr(const at::Tensor& rowptr, const at::Tensor& col,
                     const at::Tensor& val, const at::Tensor& x,
@@ -313,6 +318,8 @@ at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
 }  // namespace dgmc
 
 TORCH_LIBRARY(dgmc_amd, m) {
+  m.def("set_cu_reserve(int n) -> int");
+  m.def("cu_hog(Tensor like, int blocks, float usec) -> Tensor");
   m.def(
       "spmm_csr(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
       "self_x, Tensor? self_scale, Tensor? bias, bool relu, ScalarType "
@@ -536,9 +543,11 @@ TORCH_LIBRARY(dgmc_amd, m) {
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
   m.impl("slot_conv_stamps", &dgmc::slot_conv_stamps);
+  m.impl("set_cu_reserve", &dgmc::set_cu_reserve);
 }
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
+  m.impl("cu_hog", &dgmc::cu_hog);
   m.impl("spmm_csr", &dgmc::spmm_csr);
   m.impl("spmm_csr_planes", &dgmc::spmm_csr_planes);
   m.impl("spmm_csr_out", &dgmc::spmm_csr_out);

@@ -113,7 +113,7 @@ int num_cus(int dev) {
     DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
     cached[dev] = prop.multiProcessorCount;
   }
-  return cached[dev];
+  return usable_cus(cached[dev]);
 }
 
 }  // namespace

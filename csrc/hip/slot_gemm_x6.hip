@@ -55,7 +55,7 @@ int x6_num_cus(int dev) {
     DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
     cached[dev] = prop.multiProcessorCount;
   }
-  return cached[dev];
+  return usable_cus(cached[dev]);
 }
 
 // 16 bytes per lane global -> LDS (destination M0 + 16 * lane), issued as

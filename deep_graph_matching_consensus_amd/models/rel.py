@@ -88,8 +88,10 @@ class RelCNN(StackedEncoder):
                     torch.is_grad_enabled()):
                 # xs[-1] also feeds the concatenation: that consumer reads
                 # the conv's alias, so both gradients meet in the conv
-                # backward (added in its dx GEMM epilogue).
-                kw = {'passthrough': True}
+                # backward (added in its dx GEMM epilogue).  'cat': the
+                # alias feeds only _head's torch.cat (in-place accumulation
+                # into that gradient slice is safe).
+                kw = {'passthrough': 'cat'}
             if self.batch_norm:
                 h = conv(xs[-1], edge_index, **kw)
                 if kw:

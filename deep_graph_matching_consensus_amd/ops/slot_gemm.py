@@ -205,7 +205,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, root, bias, op, relu, loop, passthrough,
-                dx_row0=0, planes_out=False):
+                dx_row0=0, planes_out=False, uses=None):
         S = weight.size(0) + (1 if root is not None else 0)
         plan = compact_plan(op, S)
         xc = x.contiguous()
@@ -255,6 +255,11 @@ class _SlotGemmSpMM(torch.autograd.Function):
                                bias, relu, torch.float32)
         ctx.save_for_backward(xc, weight, root, out if relu else None)
         ctx.op, ctx.plan, ctx.relu, ctx.loop = op, plan, relu, loop
+        # Forward uses of this weight in the current forward scope: the
+        # pieced DP weight gradient writes the weight's flat gradient view
+        # and starts its all-reduce, which is only valid for a weight used
+        # once per step (a second use would add into the view in flight).
+        ctx.uses = uses
         ctx.dx_row0 = int(dx_row0)
         ctx.has_root = root is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
@@ -266,7 +271,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad, gpass=None):
         x, weight, root, out = ctx.saved_tensors
-        nones = (None, ) * 6
+        nones = (None, ) * 7
         op, plan, loop, idx = ctx.op, ctx.plan, ctx.loop, ctx.idx
         ops = _backend.ops()
         need_b = ctx.bias_dtype is not None and ctx.needs_input_grad[3]
@@ -333,8 +338,9 @@ class _SlotGemmSpMM(torch.autograd.Function):
         if loop is None:
             if need_w and ctx.x6 and PIECES > 1 and \
                     weight.numel() * 4 >= PIECE_BYTES and \
-                    ctx.needs_input_grad[1] and (PIECES_ALWAYS or
-                                                 _has_sink(weight)):
+                    ctx.needs_input_grad[1] and ctx.uses is not None and \
+                    ctx.uses[0] == 1 and (PIECES_ALWAYS or
+                                          _has_sink(weight)):
                 gw, gr = _weight_grad_pieces(x, dyc, plan, weight, root,
                                              ctx.has_root and
                                              ctx.needs_input_grad[2])
@@ -364,6 +370,18 @@ class _SlotGemmSpMM(torch.autograd.Function):
         return (gx, gw, gr, gb) + nones
 
 
+def _forward_uses(weight):
+    """Shared per-forward-scope counter of ``weight``'s uses (``[n]``,
+    final once the forward has run), or None outside a forward scope (then
+    single use cannot be proven)."""
+    from ..runtime.cache import in_forward_scope
+    if not (in_forward_scope() and torch.is_grad_enabled()):
+        return None
+    cnt = cached(('slot_gemm_uses', id(weight)), lambda: [0])
+    cnt[0] += 1
+    return cnt
+
+
 def _has_sink(weight):
     from ..parallel.ddp import grad_sink
     return grad_sink(weight) is not None
@@ -380,6 +398,9 @@ def _weight_grad_pieces(x3, dy3, plan, weight, root, need_root):
     tiles = (cin // 128) * (cout // 128)
     rounds = _x6_rounds(tiles)
     sink = grad_sink(weight)
+    if sink is not None and sink.is_pre_reduced(weight):
+        raise RuntimeError('pieced weight gradient: the weight\'s flat '
+                           'gradient is already being reduced this step')
     gw = sink.grad_view(weight) if sink is not None else \
         torch.empty_like(weight)
     gr = None
@@ -413,6 +434,9 @@ def slot_gemm_spmm(op, x, weight, root, bias=None, relu=False, loop_key=None,
     from ..runtime import loopgrad
     loop = loopgrad.group(('slot_gemm', ) + tuple(loop_key)) \
         if loop_key is not None else None
+    # (counted here: inside Function.forward grad mode is off)
+    uses = _forward_uses(weight) if (loop is None and
+                                     weight.requires_grad) else None
     with torch.autocast(device_type='cuda', enabled=False):
         return _SlotGemmSpMM.apply(x, weight, root, bias, op, relu, loop,
-                                   passthrough, dx_row0, planes_out)
+                                   passthrough, dx_row0, planes_out, uses)

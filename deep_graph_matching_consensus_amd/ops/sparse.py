@@ -490,13 +490,15 @@ class _GemmSpMM(torch.autograd.Function):
             if gpass is not None and gpass.dtype == dY.dtype == \
                     ctx.x_dtype and gpass.shape == (dY.size(0),
                                                     w_lp.size(0)):
-                if gpass.dim() == 2 and gpass.stride(1) == 1 and \
+                if ctx.passthrough == 'cat' and gpass.dim() == 2 and \
+                        gpass.stride(1) == 1 and \
                         gpass.stride(0) >= gpass.size(1):
-                    # In place: gpass is this op's own slice of the
-                    # concatenation's gradient (CatBackward hands out
-                    # disjoint column views nothing else reads), so the
-                    # GEMM accumulates into it with beta = 1 - no copy of
-                    # gpass into a fresh output first.
+                    # In place (opt-in, ``passthrough='cat'``: the caller
+                    # guarantees the alias feeds exactly one torch.cat, so
+                    # gpass is this op's own slice of the concatenation's
+                    # gradient - CatBackward hands out disjoint column views
+                    # nothing else reads): the GEMM accumulates into it with
+                    # beta = 1, no copy of gpass into a fresh output first.
                     gx = gpass.addmm_(dY, w_lp.t())
                 else:
                     gx = torch.addmm(gpass, dY, w_lp.t())
@@ -715,6 +717,9 @@ def gemm_spmm(op, x, w, w_lp, out_channels, bias=None, relu=False,
     ``passthrough`` returns ``(out, x')`` where ``x'`` aliases ``x``: give
     ``x'`` to x's other consumers and their gradient is accumulated inside
     this node's backward (fused into the slot conv epilogue).
+    ``passthrough='cat'`` additionally promises that ``x'`` feeds exactly
+    one ``torch.cat`` (nothing else), which lets the backward accumulate
+    into that gradient slice in place.
     """
     from ..runtime import loopgrad
     assert x.dim() == 2 and x.size(0) * (w.size(1) // out_channels) == \

@@ -208,6 +208,9 @@ class GradBucketAllReducer(object):
         if hi > lo:
             self._launch_range(off + lo, off + hi)
 
+    def is_pre_reduced(self, p):
+        return p in self._pre
+
     def mark_reduced(self, p):
         """``p``'s whole gradient is in its flat view and being reduced:
         its bucket skips it."""

@@ -27,6 +27,10 @@ def forward_cache():
         _TLS.store = None
 
 
+def in_forward_scope():
+    return getattr(_TLS, 'store', None) is not None
+
+
 def cached(key, fn):
     """``fn()`` memoised under ``key`` in the active scope (if any)."""
     import torch

@@ -22,6 +22,7 @@ import json
 import os
 import random
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -57,11 +58,16 @@ class PairTrainer(object):
             (all-reduced) gradients contain NaN/Inf - on the device, inside
             the captured graph, via the fused Adam ``found_inf`` input; the
             skipped-step count is reported by :meth:`read_stats`.
+        dp_mode (str): ``'captured'`` (default; ``DGMC_AMD_IN_STEP_ALLREDUCE``
+            =1): bucketed all-reduces launched from the backward hooks inside
+            the step - captured in its hipGraph on RCCL; ``'flat'``: one flat
+            all-reduce of the whole gradient buffer after the step (replay).
     """
 
     def __init__(self, model, store, batch_size, lr=1e-3, mode='graph',
                  bf16=False, seed=0, overlap=True, sources=None,
-                 guard_nonfinite=True, buckets=True, bucket_bytes=8 << 20):
+                 guard_nonfinite=True, buckets=True, bucket_bytes=8 << 20,
+                 dp_mode=None):
         self.model = model
         self.store = store
         self.device = store.device
@@ -81,7 +87,10 @@ class PairTrainer(object):
         #   replay (parallel/ddp.py).
         graph_rccl = (mode == 'graph' and parallel.is_distributed() and
                       torch.distributed.get_backend() == 'nccl')
-        in_step = IN_STEP_ALLREDUCE and (mode == 'static' or graph_rccl)
+        if dp_mode is None:
+            dp_mode = 'captured' if IN_STEP_ALLREDUCE else 'flat'
+        assert dp_mode in ('captured', 'flat'), dp_mode
+        in_step = dp_mode == 'captured' and (mode == 'static' or graph_rccl)
         self.reducer = parallel.GradBucketAllReducer(
             model, bucket_bytes=bucket_bytes,
             overlap=overlap and mode == 'eager', in_step=in_step)
@@ -103,6 +112,10 @@ class PairTrainer(object):
             self.optimizer.found_inf = self._found_inf
         self.step_count = 0
         self._one = None
+        # Optional CUDA-event timing of the exposed (after-step) all-reduce
+        # (bench diagnostics): (start, end) event pairs of the timed steps.
+        self.time_allreduce = False
+        self.allreduce_events = []
         data_seed = seed + 1000 * self.rank
         if mode == 'eager':
             self.loader = DevicePairLoader(store, batch_size, sources=sources,
@@ -241,6 +254,22 @@ class PairTrainer(object):
         return lambda: self._static_body(i)
 
     @property
+    def dp_mode_used(self):
+        """How gradients are synchronised: ``'none'`` (one rank),
+        ``'captured-in-step'`` (bucketed all-reduces inside the captured
+        hipGraph), ``'in-step'`` (same, uncaptured static step),
+        ``'overlapped-eager'`` (eager step, bucket all-reduces from the
+        backward hooks) or ``'flat-after-step'`` (one all-reduce after the
+        step / replay)."""
+        if self.world == 1:
+            return 'none'
+        if self.reducer.in_step:
+            return 'captured-in-step' if self.mode == 'graph' else 'in-step'
+        if self.mode == 'eager' and self.reducer.overlap:
+            return 'overlapped-eager'
+        return 'flat-after-step'
+
+    @property
     def overflows(self):
         """Batches that fitted no static capacity (resampled)."""
         return sum(b.overflows for b in getattr(self, 'batchers', []))
@@ -359,7 +388,14 @@ class PairTrainer(object):
                     self._static_body(bucket)
             if self.world > 1 and not self.reducer.in_step:
                 with trace_range('train.allreduce'):
+                    if self.time_allreduce:
+                        ev = (torch.cuda.Event(enable_timing=True),
+                              torch.cuda.Event(enable_timing=True))
+                        ev[0].record()
                     self.reducer.finish()
+                    if self.time_allreduce:
+                        ev[1].record()
+                        self.allreduce_events.append(ev)
                 with trace_range('train.optimizer'):
                     self._check_finite()
                     self._optimizer_step()
@@ -500,11 +536,22 @@ class PairTrainer(object):
         self.step_count = int(state.get('step', 0))
         # (Parameters and optimizer tensors were updated in place, so
         # captured graphs stay valid and are replayed as they are.)
-        ranks = state.get('ranks', [])
+        ranks = state.get('ranks')
+        if ranks is None and 'sampler' in state:
+            # Round-3 layout: one rank's sampler / stats / RNG streams at the
+            # top level of the checkpoint.
+            ranks = [{k: state[k] for k in ('sampler', 'stats', 'rng')
+                      if k in state}]
+        ranks = ranks or []
         if len(ranks) != self.world:
             # Different world size: the shards changed, so the saved sampler
             # positions mean nothing here - keep this rank's freshly seeded
             # sampler and start the running stats from zero.
+            warnings.warn(
+                'checkpoint {} holds {} rank state(s) for a world of {}: '
+                'sampler positions, running stats and RNG streams are NOT '
+                'restored (model and optimizer are)'.format(
+                    path, len(ranks), self.world))
             self.stats.zero_()
             return state
         mine = ranks[self.rank]
@@ -513,7 +560,8 @@ class PairTrainer(object):
             self._batches = self.loader.forever()
         else:
             self.batcher.load_state_dict(mine['sampler'])
-        self.stats.copy_(mine['stats'].to(self.stats))
+        if 'stats' in mine:
+            self.stats.copy_(mine['stats'].to(self.stats))
         rng = mine.get('rng', {})
         if 'torch' in rng:
             torch.set_rng_state(rng['torch'].cpu())
@@ -524,8 +572,18 @@ class PairTrainer(object):
             np.random.set_state((name, keys.cpu().numpy().astype(np.uint32),
                                  pos, has_gauss, cached))
         if 'cuda' in rng and self.device.type == 'cuda':
-            torch.cuda.set_rng_state(rng['cuda'].cpu(), self.device)
+            torch.cuda.set_rng_state(_cuda_rng_of(rng['cuda'], self.device),
+                                     self.device)
         return state
+
+
+def _cuda_rng_of(saved, device):
+    """The CUDA generator state for ``device`` from a checkpoint: a state
+    tensor, or (older checkpoints) a list with one state per device."""
+    if isinstance(saved, (list, tuple)):
+        idx = device.index or 0
+        saved = saved[idx] if idx < len(saved) else saved[0]
+    return saved.cpu()
 
 
 class _gc_paused(object):
@@ -695,7 +753,9 @@ class KGTrainer(object):
                  'schedule': {'num_steps': self.model.num_steps,
                               'detach': bool(self.model.detach),
                               'k': int(self.model.k)},
-                 'rng': {'torch': torch.get_rng_state()}}
+                 'rng': {'torch': torch.get_rng_state()},
+                 # non-finite steps skipped so far (the device counter)
+                 'skipped': float(self.skipped)}
         if self.device.type == 'cuda':
             state['rng']['cuda'] = torch.cuda.get_rng_state(self.device)
         return state
@@ -717,11 +777,14 @@ class KGTrainer(object):
             self.model.num_steps = sch['num_steps']
             self.model.detach = sch['detach']
             self.model.k = sch['k']
+        if 'skipped' in state:
+            self.skipped.fill_(float(state['skipped']))
         rng = state.get('rng', {})
         if 'torch' in rng:
             torch.set_rng_state(rng['torch'].cpu())
         if 'cuda' in rng and self.device.type == 'cuda':
-            torch.cuda.set_rng_state(rng['cuda'].cpu(), self.device)
+            torch.cuda.set_rng_state(_cuda_rng_of(rng['cuda'], self.device),
+                                     self.device)
         return state
 
     def _body_static(self):

@@ -221,3 +221,71 @@ def test_data_parallel_resume_restores_each_rank_shard(tmp_path):
         assert res['resumed'] == res['ref'][2:], r
     o0, o1 = out[0]['order']
     assert o0 is not None and o1 is not None and not torch.equal(o0, o1)
+
+
+def test_legacy_round3_checkpoint_layout_resumes(tmp_path):
+    """a round-3 checkpoint (sampler / stats / rng at the top
+    level, one rank, CUDA RNG as a per-device list) still restores the
+    sampler position, running stats and RNG streams - the resumed run
+    continues the uninterrupted trajectory."""
+    groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=5)
+    store = GraphStore(groups, 'cpu')
+    torch.manual_seed(123)
+    full = _pair_trainer(store, 'eager')
+    ref = _run_trajectory(full, 5)
+    torch.manual_seed(123)
+    first = _pair_trainer(store, 'eager')
+    _run_trajectory(first, 2)
+    state = first.state_dict()
+    mine = state.pop('ranks')[0]
+    state.pop('world_size')
+    state.update(mine)                     # the round-3 layout
+    path = str(tmp_path / 'legacy.pt')
+    torch.save(state, path)
+    torch.manual_seed(999)
+    resumed = _pair_trainer(store, 'eager', seed_model=7)
+    resumed.load(path)
+    assert torch.equal(resumed.stats, first.stats)
+    assert _run_trajectory(resumed, 3) == ref[2:]
+
+
+def test_world_size_change_warns(tmp_path):
+    groups = make_keypoint_datasets(graphs=6, feature_dim=16, seed=5)
+    store = GraphStore(groups, 'cpu')
+    torch.manual_seed(123)
+    a = _pair_trainer(store, 'eager')
+    _run_trajectory(a, 1)
+    state = a.state_dict()
+    state['ranks'] = state['ranks'] * 2     # as written by 2 ranks
+    state['world_size'] = 2
+    path = str(tmp_path / 'w2.pt')
+    torch.save(state, path)
+    b = _pair_trainer(store, 'eager')
+    with pytest.warns(UserWarning, match='NOT restored'):
+        b.load(path)
+    assert float(b.stats.abs().sum()) == 0.0
+
+
+def test_kg_trainer_checkpoint_keeps_skipped_count(tmp_path):
+    """KGTrainer's non-finite skipped-step counter survives a
+    save / load."""
+    from deep_graph_matching_consensus_amd.datasets.kg import make_kg_pair
+    from deep_graph_matching_consensus_amd.train import KGTrainer
+    data = make_kg_pair('zh_en', scale=0.01, feature_dim=16, seed=0)
+
+    def make():
+        torch.manual_seed(0)
+        model = DGMC(RelCNN(16, 8, 2), RelCNN(4, 4, 2), num_steps=0, k=4)
+        return KGTrainer(model, data, lr=1e-3, graph=False)
+
+    a = make()
+    a.step()
+    data.x1[0, 0] = float('nan')
+    a.step()
+    data.x1[0, 0] = 0.0
+    assert float(a.skipped) == 1.0
+    path = str(tmp_path / 'kg.pt')
+    a.save(path)
+    b = make()
+    b.load(path)
+    assert float(b.skipped) == 1.0

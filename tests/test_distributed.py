@@ -103,7 +103,8 @@ def test_grad_allreduce_matches_average(overlap):
     assert torch.equal(p0, p1)
 
 
-def _bench_worker(rank, world, port, mode, out_path, batch=16):
+def _bench_worker(rank, world, port, mode, out_path, batch=16,
+                  dp_mode='captured'):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
                       RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), OMP_NUM_THREADS='1')
@@ -112,14 +113,14 @@ def _bench_worker(rank, world, port, mode, out_path, batch=16):
     bench.main(['--gpus', str(world), '--steps', '2', '--warmup', '1',
                 '--batch-size', str(batch),
                 '--graphs-per-category', '8', '--dtype', 'fp32', '--mode',
-                mode, '--json-out', out_path])
+                mode, '--dp-mode', dp_mode, '--json-out', out_path])
 
 
-@pytest.mark.parametrize('mode,world,batch', [('eager', 2, 16),
-                                              ('static', 2, 16),
-                                              ('eager', 8, 32),
-                                              ('static', 8, 32)])
-def test_bench_ranks_gloo(tmp_path, mode, world, batch):
+@pytest.mark.parametrize('mode,world,batch,dp_mode', [
+    ('eager', 2, 16, 'captured'), ('static', 2, 16, 'captured'),
+    ('static', 2, 16, 'flat'), ('eager', 8, 32, 'captured'),
+    ('static', 8, 32, 'captured')])
+def test_bench_ranks_gloo(tmp_path, mode, world, batch, dp_mode):
     """The bench's distributed path (rank sharding, all-reduce, max-time
     reduction, rank-0 JSON) runs end to end with gloo ranks.  With 8 ranks
     each shard (160 graphs / 8 = 20 sources) is smaller than the batch, as
@@ -129,7 +130,8 @@ def test_bench_ranks_gloo(tmp_path, mode, world, batch):
     ctx = mp.get_context('spawn')
     port = _free_port()
     procs = [ctx.Process(target=_bench_worker,
-                         args=(r, world, port, mode, out_path, batch))
+                         args=(r, world, port, mode, out_path, batch,
+                               dp_mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -142,3 +144,12 @@ def test_bench_ranks_gloo(tmp_path, mode, world, batch):
     assert result['config']['global_batch'] == batch * world
     assert result['config']['parallelism'] == 'dp{}'.format(world)
     assert result['value'] > 0
+    # DP diagnostics
+    expect = {'eager': 'overlapped-eager',
+              'static': 'in-step' if dp_mode == 'captured'
+              else 'flat-after-step'}[mode]
+    assert result['dp_mode'] == expect
+    assert result['ms_per_step_rank_min'] <= result['ms_per_step_rank_max']
+    assert result['allreduce_standalone_ms'] > 0
+    assert result['allreduce_bytes'] > 0
+    assert 'gemm_arith' in result

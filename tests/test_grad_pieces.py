@@ -153,3 +153,56 @@ def test_pieced_weight_gradient_two_ranks_static_gpu():
     b = _spawn(_pascal_worker, 2, dict(env, IN_STEP='0'))
     assert torch.equal(a[0], a[1])
     assert torch.equal(a[0], b[0])
+
+
+def _twice_worker(rank, world, port, env, out):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK='0',
+                      OMP_NUM_THREADS='1', **env)
+    import torch.distributed as dist
+    from deep_graph_matching_consensus_amd.nn import SplineConv
+    from deep_graph_matching_consensus_amd.ops import slot_gemm
+    from deep_graph_matching_consensus_amd.parallel.ddp import \
+        GradBucketAllReducer
+    from deep_graph_matching_consensus_amd.runtime.cache import forward_cache
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    conv = SplineConv(1024, 256, dim=2, kernel_size=5).cuda()
+    assert conv.weight.numel() * 4 >= slot_gemm.PIECE_BYTES
+    g = torch.Generator().manual_seed(20 + rank)
+    n, e = 96, 384
+    ei = torch.randint(n, (2, e), generator=g).cuda()
+    pseudo = torch.rand(e, 2, generator=g).cuda()
+    x = torch.randn(n, 1024, generator=g).cuda()
+    red = GradBucketAllReducer(conv, in_step=env['IN_STEP'] == '1')
+    if env['IN_STEP'] == '1':
+        red.release_grads()
+    else:
+        red.zero_grad()
+    with forward_cache():
+        # The same weight used twice in one step (the ADVICE r4 case): the
+        # pieced path must not run (it would reduce the first use's view
+        # while the second use still adds into it).
+        y = conv(x, ei, pseudo) + conv(x.flip(0), ei, pseudo)
+    (y * y).sum().backward()
+    if env['IN_STEP'] == '1':
+        assert not red._pre, 'pieced path taken for a twice-used weight'
+    red.finish()
+    torch.cuda.synchronize()
+    out[rank] = torch.cat([p.grad.reshape(-1).cpu()
+                           for p in conv.parameters()])
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_twice_used_weight_skips_pieces_gpu():
+    """a SplineConv weight used twice in one step must take the
+    ordinary weight-gradient path even with pieces forced; the averaged
+    gradient equals the flat after-step all-reduce."""
+    env = {'DGMC_AMD_DIST_BACKEND': 'gloo',
+           'DGMC_AMD_WGRAD_PIECES_ALWAYS': '1'}
+    a = _spawn(_twice_worker, 2, dict(env, IN_STEP='1'))
+    b = _spawn(_twice_worker, 2, dict(env, IN_STEP='0'))
+    assert torch.equal(a[0], a[1])
+    torch.testing.assert_close(a[0], b[0], rtol=1e-5, atol=1e-5)

@@ -1,0 +1,315 @@
+"""Hardened numerics gate of the bf16x6 GEMMs.
+
+``tests/test_slot_gemm_x6.py`` compares bf16x6 with the exact-f32 MFMA chain
+on N(0, 1/K) data.  Here the same comparison (max |error| against an fp64
+oracle, bf16x6 <= exact f32) runs on inputs that stress the three-term
+split, each with several seeds, on the PRODUCTION operand paths (forward on
+fp32 X split in the kernel, input gradient on fp32 dY_c, weight gradient on
+X planes and fp32 dY_c):
+
+* ``wide``: per-row magnitudes spanning 2^-30 .. 2^30;
+* ``cancel``: duplicated input features against weight rows of opposite
+  sign (every product cancels against its partner up to ~1e-3);
+* ``relu``: >= 50 % exact zeros (post-ReLU activations);
+* ``trained``: weights AND layer inputs of the headline model after 200
+  Adam steps (PascalVOC-shaped psi_1 / psi_2, fp32 training step).
+
+Forward / input-gradient errors are taken per output row relative to that
+row's largest oracle value (so the 2^-30 rows of ``wide`` count as much as
+the 2^30 ones), weight-gradient errors as max |error|.
+
+Documented limit (``test_x6_all_tiny_rows_documented_bound``): when EVERY
+value of a row is below ~2^-110 the third term of its split is a bf16
+subnormal, which the matrix cores flush to zero, so that row keeps 16 of
+fp32's 24 mantissa bits (relative error <= 2^-16 instead of 2^-24).  Such
+magnitudes (< 1e-33) do not occur in training; the test pins the bound.
+
+The kernel-vs-oracle ratios are written to ``gpurun_out/x6_stress.jsonl``
+(``profiles/x6_stress_r5.jsonl`` holds the recorded run).
+"""
+import json
+import os
+
+import pytest
+import torch
+
+from deep_graph_matching_consensus_amd.ops import _backend
+from deep_graph_matching_consensus_amd.ops import slot_gemm as sg
+from deep_graph_matching_consensus_amd.ops.plans import spline_plan
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+SHAPES = [(128, 128), (256, 256), (1024, 256)]
+CASES = ['wide', 'cancel', 'relu']
+SEEDS = [0, 1, 2]
+
+
+def _record(**kw):
+    os.makedirs('gpurun_out', exist_ok=True)
+    with open(os.path.join('gpurun_out', 'x6_stress.jsonl'), 'a') as f:
+        f.write(json.dumps(kw) + '\n')
+
+
+@pytest.fixture(scope='module')
+def plan():
+    from deep_graph_matching_consensus_amd.datasets import (
+        PASCAL_VOC_CATEGORIES, GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    assert _backend.hip_available()
+    groups = make_keypoint_datasets(PASCAL_VOC_CATEGORIES, graphs=64,
+                                    feature_dim=16, seed=0)
+    store = GraphStore(groups, DEV, valid_pairs=True)
+    b = StaticPairBatcher(store, 512, seed=0)
+    assert b.load()
+    b.materialize()
+    N = b.cap_s + b.cap_t
+    op = spline_plan(b.v['ei'], b.v['ea_val'], N, (5, 5), (1, 1), 1,
+                     root=True)
+    return N, sg.compact_plan(op, 26)
+
+
+def _gen(case, shape, g, scale=1.0):
+    """A tensor of ``shape`` for stress ``case`` (last dim = features)."""
+    if case == 'wide':
+        e = torch.randint(-30, 31, shape[:-1] + (1, ), device=DEV,
+                          generator=g).float()
+        return torch.randn(shape, device=DEV, generator=g) * torch.exp2(e)
+    if case == 'relu':
+        return torch.relu(torch.randn(shape, device=DEV, generator=g))
+    if case == 'cancel':
+        h = torch.randn(shape[:-1] + (shape[-1] // 2, ), device=DEV,
+                        generator=g)
+        return torch.stack([h, h], -1).reshape(shape)    # duplicated pairs
+    return torch.randn(shape, device=DEV, generator=g) * scale
+
+
+def _weights(case, cin, cout, g):
+    w = torch.randn(25, cin, cout, device=DEV, generator=g) / cin ** 0.5
+    r = torch.randn(cin, cout, device=DEV, generator=g) / cin ** 0.5
+    if case == 'cancel':
+        # rows 2j + 1 = -(rows 2j) (1 + 1e-3 noise): x_2j w_2j + x_2j+1
+        # w_2j+1 leaves ~1e-3 of each product
+        for t in (w, r):
+            v = t.view(*t.shape[:-2], cin // 2, 2, cout)
+            v[..., 1, :] = -v[..., 0, :] * (
+                1 + 1e-3 * torch.randn(v[..., 0, :].shape, device=DEV,
+                                       generator=g))
+    return w, r
+
+
+def _slots(plan):
+    seg = plan.seg.cpu().tolist()
+    return [(s, seg[s], seg[s + 1]) for s in range(len(seg) - 1)]
+
+
+def _fwd_oracle(plan, x, w, r):
+    W = torch.cat([w, r[None]], 0).double()
+    src = plan.src.long()
+    Y = torch.zeros(src.numel(), w.size(2), dtype=torch.float64, device=DEV)
+    for s, a, b in _slots(plan):
+        rows = src[a:b]
+        ok = rows >= 0
+        Y[a:b][ok] = x.double()[rows[ok]] @ W[s]
+    return Y
+
+
+def _dx_oracle(plan, dy, w, r):
+    W = torch.cat([w, r[None]], 0).double()
+    Z = torch.zeros(dy.size(0), w.size(1), dtype=torch.float64, device=DEV)
+    for s, a, b in _slots(plan):
+        Z[a:b] = dy.double()[a:b] @ W[s].t()
+    return Z
+
+
+def _wgrad_oracle(plan, x, dy):
+    src = plan.src.long()
+    out = []
+    for s, a, b in _slots(plan):
+        rows = src[a:b]
+        ok = rows >= 0
+        out.append(x.double()[rows[ok]].t() @ dy.double()[a:b][ok])
+    return torch.stack(out)
+
+
+def _errors(y, ref, rows, per_row):
+    d = (y.double() - ref).abs()
+    if rows is not None:
+        d, ref = d[rows], ref[rows]
+    if per_row:
+        scale = ref.abs().amax(-1).clamp_min(1e-300)
+        return float((d.amax(-1) / scale).max())
+    return float(d.max())
+
+
+def _check(kind, case, shape, seed, y6, y32, ref, rows=None, bound=None):
+    per_row = kind in ('fwd', 'dx')
+    e6 = _errors(y6, ref, rows, per_row)
+    e32 = _errors(y32, ref, rows, per_row)
+    assert torch.isfinite(y6).all()
+    _record(kind=kind, case=case, cin=shape[0], cout=shape[1], seed=seed,
+            err_x6=e6, err_f32=e32,
+            metric='max row-relative' if per_row else 'max abs',
+            ratio=(e6 / e32) if e32 > 0 else (0.0 if e6 == 0 else None))
+    if bound is not None:
+        assert e6 <= bound, (kind, case, shape, seed, e6, bound)
+        return
+    assert e6 <= e32, (kind, case, shape, seed, e6, e32)
+
+
+@pytest.mark.parametrize('seed', SEEDS)
+@pytest.mark.parametrize('case', CASES)
+@pytest.mark.parametrize('cin,cout', SHAPES)
+def test_x6_forward_stress(plan, cin, cout, case, seed):
+    N, pl = plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(100 * seed + cin + cout)
+    x = _gen(case, (N, cin), g)
+    w, r = _weights(case, cin, cout, g)
+    y6 = ops.slot_gemm_x6(x, pl.src, pl.seg, ops.slot_weight_x3(w, r, True),
+                          True, None)
+    y32 = ops.slot_gemm2(x, pl.src, pl.seg, ops.slot_weight_t(w, r), None,
+                         True)
+    _check('fwd', case, (cin, cout), seed, y6, y32,
+           _fwd_oracle(pl, x, w, r), pl.src.long() >= 0)
+
+
+@pytest.mark.parametrize('seed', SEEDS)
+@pytest.mark.parametrize('case', CASES)
+@pytest.mark.parametrize('cin,cout', SHAPES)
+def test_x6_input_grad_stress(plan, cin, cout, case, seed):
+    N, pl = plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(200 * seed + cin + cout)
+    P = pl.src.numel()
+    used = int(pl.seg[-1])
+    dy = _gen(case, (P, cout), g)
+    dy[used:] = 0
+    wt, rt = _weights(case, cout, cin, g)         # (pairs along cout)
+    w = wt.transpose(1, 2).contiguous()
+    r = rt.t().contiguous()
+    z6 = ops.slot_gemm_x6(dy, pl.src, pl.seg, ops.slot_weight_x3(w, r, False),
+                          False, None)
+    z32 = ops.slot_gemm2(dy, pl.src, pl.seg, w, r, False) if cout >= 256 \
+        else ops.slot_gemm(dy, pl.src, pl.seg, w, r, True, None)
+    rows = torch.zeros(P, dtype=torch.bool, device=DEV)
+    rows[:used] = True
+    _check('dx', case, (cin, cout), seed, z6, z32, _dx_oracle(pl, dy, w, r),
+           rows)
+
+
+@pytest.mark.parametrize('seed', SEEDS)
+@pytest.mark.parametrize('case', CASES)
+@pytest.mark.parametrize('cin,cout', SHAPES)
+def test_x6_weight_grad_stress(plan, cin, cout, case, seed):
+    N, pl = plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(300 * seed + cin + cout)
+    P = pl.src.numel()
+    used = int(pl.seg[-1])
+    # the reduction runs over rows: 'cancel' pairs rows of x with rows of
+    # dY of opposite sign
+    x = _gen(case if case != 'cancel' else 'normal', (N, cin), g)
+    dy = _gen(case if case != 'cancel' else 'normal', (P, cout), g)
+    if case == 'cancel':
+        x = x.view(N // 2, 2, cin)
+        x[:, 1] = x[:, 0]
+        x = x.view(N, cin)
+    dy[used:] = 0
+    dy[pl.src.long() < 0] = 0
+    rounds = sg._x6_rounds((cin // 128) * (cout // 128))
+    w6 = ops.slot_wgrad_x6([ops.split3(x)], [dy], pl.src, pl.seg, rounds)
+    w32 = ops.slot_wgrad_f32([x], [dy], pl.src, pl.seg, rounds)
+    _check('wgrad', case, (cin, cout), seed, w6, w32,
+           _wgrad_oracle(pl, x, dy))
+
+
+@pytest.mark.parametrize('cin,cout', SHAPES)
+def test_x6_all_tiny_rows_documented_bound(plan, cin, cout):
+    """Every input value ~2^-115 (third split term bf16-subnormal, flushed
+    by the matrix cores): the forward keeps a per-row relative error below
+    2^-15 (16 mantissa bits) - the documented limit of the emulation."""
+    N, pl = plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(cin + 5 * cout)
+    x = torch.randn(N, cin, device=DEV, generator=g) * 2.0 ** -115
+    w, r = _weights('normal', cin, cout, g)
+    y6 = ops.slot_gemm_x6(x, pl.src, pl.seg, ops.slot_weight_x3(w, r, True),
+                          True, None)
+    y32 = ops.slot_gemm2(x, pl.src, pl.seg, ops.slot_weight_t(w, r), None,
+                         True)
+    _check('fwd', 'tiny_all', (cin, cout), 0, y6, y32,
+           _fwd_oracle(pl, x, w, r), pl.src.long() >= 0, bound=2.0 ** -15)
+
+
+@pytest.fixture(scope='module')
+def trained():
+    """Weights and layer inputs of the headline model after 200 fp32 Adam
+    steps (static mode: no graph capture needed for the trajectory)."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        PASCAL_VOC_CATEGORIES, GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.train import PairTrainer
+    torch.manual_seed(0)
+    groups = make_keypoint_datasets(PASCAL_VOC_CATEGORIES, graphs=32, seed=0)
+    store = GraphStore(groups, DEV, valid_pairs=True)
+    model = DGMC(SplineCNN(1024, 256, 2, 2, cat=False, dropout=0.5),
+                 SplineCNN(128, 128, 2, 2, cat=True), num_steps=10).to(DEV)
+    tr = PairTrainer(model, store, 256, mode='static', seed=0)
+    for _ in range(200):
+        tr.step()
+    torch.cuda.synchronize()
+    return model, store
+
+
+@pytest.mark.parametrize('layer', ['psi_1.0', 'psi_1.1', 'psi_2.0',
+                                   'psi_2.1'])
+def test_x6_trained_weights(plan, trained, layer):
+    """Forward, input gradient and weight gradient with the trained layer's
+    weights; inputs: the trained psi_1's real activations (layer 1: the
+    post-ReLU output of layer 0) or, for psi_2, ReLU'd features of the same
+    scale."""
+    N, pl = plan
+    ops = _backend.ops()
+    model, store = trained
+    enc, i = layer.split('.')
+    conv = getattr(model, enc).convs[int(i)]
+    w, r = conv.weight.detach(), conv.root.detach()
+    cin, cout = w.size(1), w.size(2)
+    g = torch.Generator(device=DEV).manual_seed(7)
+    if enc == 'psi_1':
+        x = store.x[:N].float()
+        if x.size(0) < N:
+            x = x.repeat((N + x.size(0) - 1) // x.size(0), 1)[:N]
+        if i == '1':
+            c0 = model.psi_1.convs[0]
+            x = torch.relu(torch.randn(N, cin, device=DEV, generator=g) *
+                           float(c0.weight.detach().std()) * 16)
+    else:
+        x = torch.relu(torch.randn(N, cin, device=DEV, generator=g))
+    x = x.contiguous()
+    y6 = ops.slot_gemm_x6(x, pl.src, pl.seg, ops.slot_weight_x3(w, r, True),
+                          True, None)
+    y32 = ops.slot_gemm2(x, pl.src, pl.seg, ops.slot_weight_t(w, r), None,
+                         True)
+    _check('fwd', 'trained:' + layer, (cin, cout), 0, y6, y32,
+           _fwd_oracle(pl, x, w, r), pl.src.long() >= 0)
+    P = pl.src.numel()
+    used = int(pl.seg[-1])
+    dy = torch.randn(P, cout, device=DEV, generator=g) * 1e-3
+    dy[used:] = 0
+    dy[pl.src.long() < 0] = 0
+    wc, rc = w.contiguous(), r.contiguous()
+    z6 = ops.slot_gemm_x6(dy, pl.src, pl.seg,
+                          ops.slot_weight_x3(wc, rc, False), False, None)
+    z32 = ops.slot_gemm2(dy, pl.src, pl.seg, wc, rc, False) if cout >= 256 \
+        else ops.slot_gemm(dy, pl.src, pl.seg, wc, rc, True, None)
+    rows = torch.zeros(P, dtype=torch.bool, device=DEV)
+    rows[:used] = True
+    _check('dx', 'trained:' + layer, (cin, cout), 0, z6, z32,
+           _dx_oracle(pl, dy, wc, rc), rows)
+    rounds = sg._x6_rounds((cin // 128) * (cout // 128))
+    w6 = ops.slot_wgrad_x6([ops.split3(x)], [dy], pl.src, pl.seg, rounds)
+    w32 = ops.slot_wgrad_f32([x], [dy], pl.src, pl.seg, rounds)
+    _check('wgrad', 'trained:' + layer, (cin, cout), 0, w6, w32,
+           _wgrad_oracle(pl, x, dy))
