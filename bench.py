@@ -20,12 +20,16 @@ Adam update.
 Precision: fp32 by default - the reference trains in fp32.  The SplineConv
 GEMMs and the folded consensus projection run as "bf16x6" on the bf16
 matrix cores (every fp32 operand split into three bf16 terms, the six
-products of order >= 2^-16 accumulated in fp32; max error vs an fp64 oracle
-at or below the exact ``v_mfma_f32_32x32x2_f32`` chain, gated by
-``tests/test_slot_gemm_x6.py``); ``DGMC_AMD_X6=0`` selects exact-fp32 MFMA
-kernels for them.  The JSON's ``gemm_arith`` names what ran.
-``--dtype bf16`` is an opt-in fast mode (bf16 operands), never the headline.  After the timed steps, held-out Hits@1 / Hits@10 of S_L
-are evaluated on ``--eval-pairs`` test pairs (untimed), like the
+products of order >= 2^-16 accumulated in fp32); ``DGMC_AMD_X6=0`` selects
+exact-fp32 MFMA kernels (``v_mfma_f32_32x32x2_f32``) for them.  Measured
+against fp64 (``tests/test_slot_gemm_x6.py``, ``tests/test_x6_stress.py``):
+forward and input-gradient errors at or below the exact chain's on every
+headline shape and stress input; see docs/performance.md for the weight
+gradient and the documented subnormal limit.  The RelConv / Linear node
+GEMMs of the DBP15K config are exact fp32.  The JSON's ``gemm_arith``
+names what ran.  ``--dtype bf16`` is an opt-in fast mode (bf16 operands),
+never the headline.  After the timed steps, held-out Hits@1 / Hits@10 of
+S_L are evaluated on ``--eval-pairs`` test pairs (untimed), like the
 reference's test loop.
 
 Rank 0 prints ONE JSON line.  ``--impl reference`` measures the eager
@@ -261,7 +265,8 @@ def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
     one standalone all-reduce of the whole gradient buffer (what a fully
     exposed sync would add per step)."""
     ms = 1000.0 * rank_elapsed / max(steps, 1)
-    out = {'dp_mode': trainer.dp_mode_used}
+    out = {'dp_mode': trainer.dp_mode_used,
+           'reserved_cus': int(getattr(trainer, 'reserved_cus', 0))}
     if world == 1:
         return out
     import torch.distributed as dist

@@ -1,0 +1,300 @@
+// Exact-fp32 NT GEMM over column chunks read in place, with an optional bias
+// / ReLU epilogue:
+//
+//   Y[M, Nn] = act([A_0 | A_1 | ...] Bt^T + bias),   Bt [Nn, K] k-contiguous
+//
+// The A operand is a list of fp32 row-major parts (any row stride, any
+// width that is a multiple of 4) - the concatenation is never formed.  Each
+// part is consumed in 128-wide chunks; a chunk's columns past the part's
+// width, and the matching Bt columns, read a zero page instead of memory,
+// so no part or weight needs padding (e.g. the 300-wide DBP15K features
+// and the 1068-wide [x | h1 | h2 | h3] of RelCNN's final Linear,
+// /root/reference/dgmc/models/rel.py:90-92, read in place).
+//
+// Uses: RelConv's stacked node map x [W1 | W2 | Wr]^T (rel.py:28-31) and
+// the encoders' final Linear on the concatenated features (rel.py:92,
+// spline.py:53) - the fp32 node GEMMs that ran on hipBLASLt.
+//
+// Kernel: v_mfma_f32_32x32x2_f32 (a k-ordered fmaf chain - exact fp32),
+// 128x128 tiles of 4 waves (64x64 each) or 64x64 tiles for skinny outputs,
+// k consumed 32 at a time through two LDS stages filled by
+// global_load_lds_dwordx4 (XOR-swizzled [row][32] images read as
+// ds_read_b128, conflict-free), persistent grid of up to 2 workgroups per
+// CU walking tiles in an XCD-aware order.  Rows past M are clamped on load
+// and not stored.
+#include "common.h"
+
+namespace dgmc {
+
+namespace {
+
+typedef float gf_f32x16 __attribute__((ext_vector_type(16)));
+typedef float gf_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGfBK = 32;           // k per staged chunk
+constexpr int kGfMaxChunks = 24;    // 128-wide chunks (K <= 3072)
+
+// A zero page for the DMAs of columns past a part's width.
+__device__ __attribute__((aligned(16))) float g_gf_zero[4] = {0.f, 0.f, 0.f,
+                                                             0.f};
+
+struct GfChunks {
+  const float* a[kGfMaxChunks];   // chunk start (part base + 128 j)
+  int lda[kGfMaxChunks];
+  int width[kGfMaxChunks];        // valid columns (<= 128)
+  int boff[kGfMaxChunks];         // first Bt column of the chunk
+  int n;
+};
+
+__device__ __forceinline__ void gf_dma16(const float* g, DGMC_LDS float* l) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :: "v"(g), "s"(m0) : "memory", "m0");
+}
+
+__device__ __forceinline__ void gf_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MB, int NB>
+__global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
+    GfChunks A, int M, const float* __restrict__ bt, int ldb, int Nn,
+    const float* __restrict__ bias, int relu, float* __restrict__ Y,
+    int ldy) {
+  constexpr int TM = 64 * MB, TN = 64 * NB;
+  __shared__ __attribute__((aligned(16))) float sA0_[TM * kGfBK];
+  __shared__ __attribute__((aligned(16))) float sA1_[TM * kGfBK];
+  __shared__ __attribute__((aligned(16))) float sB0_[TN * kGfBK];
+  __shared__ __attribute__((aligned(16))) float sB1_[TN * kGfBK];
+  DGMC_LDS float* sA0 = (DGMC_LDS float*)sA0_;
+  DGMC_LDS float* sA1 = (DGMC_LDS float*)sA1_;
+  DGMC_LDS float* sB0 = (DGMC_LDS float*)sB0_;
+  DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave & 1, wm = wave >> 1;
+  const int ntn = Nn / TN, nk = A.n * (128 / kGfBK);
+  const int U = ((M + TM - 1) / TM) * ntn;
+  const int G = gridDim.x;
+  int u = xcd_remap(blockIdx.x, G);
+  if (u >= U) return;
+
+  // Staging: wave w's A pieces j < 2 MB cover rows 16 MB w + 8 j + lane / 8,
+  // its B pieces j < 2 NB rows 16 NB w + 8 j + lane / 8; lane L loads the
+  // 4 floats of physical chunk L % 8 = logical (L % 8) ^ ((row >> 1) & 7).
+  const int prow = lane >> 3;
+  auto swz = [&](int row) { return 4 * ((lane & 7) ^ ((row >> 1) & 7)); };
+  int arow[2 * MB];
+  int brow0;
+  auto tile_ptrs = [&](int uu) {
+    const int m0 = (uu / ntn) * TM, n0 = (uu % ntn) * TN;
+#pragma unroll
+    for (int j = 0; j < 2 * MB; ++j)
+      arow[j] = min(m0 + 16 * MB * wave + 8 * j + prow, M - 1);
+    brow0 = n0 + 16 * NB * wave + prow;
+  };
+  const float* zero = g_gf_zero;
+  auto stage = [&](int kc, DGMC_LDS float* da, DGMC_LDS float* db) {
+    const int c = kc >> 2;                 // 128-wide chunk
+    const int kp = (kc & 3) * kGfBK;       // offset inside it
+    const float* ap = A.a[c];
+    const int lda = A.lda[c], wid = A.width[c], bo = A.boff[c];
+#pragma unroll
+    for (int j = 0; j < 2 * MB; ++j) {
+      const int row = 16 * MB * wave + 8 * j + prow;
+      const int k = kp + swz(row);
+      gf_dma16(k < wid ? ap + (size_t)arow[j] * lda + k : zero,
+               da + (16 * MB * wave + 8 * j) * kGfBK);
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * NB; ++j) {
+      const int row = 16 * NB * wave + 8 * j + prow;
+      const int k = kp + swz(row);
+      gf_dma16(k < wid ? bt + (size_t)(brow0 + 8 * j) * ldb + bo + k : zero,
+               db + (16 * NB * wave + 8 * j) * kGfBK);
+    }
+  };
+  const int i = lane & 31, h = lane >> 5, sw = (i >> 1) & 7;
+  int qoff[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) qoff[g] = 4 * ((2 * g + h) ^ sw);
+  const int offN = (wn * 32 * NB + i) * kGfBK;
+  const int offM = (wm * 32 * MB + i) * kGfBK;
+  gf_f32x16 acc[NB][MB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      gf_f32x4 fa[NB], fb[MB];
+#pragma unroll
+      for (int a = 0; a < NB; ++a)
+        fa[a] = *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+            lb + offN + a * 32 * kGfBK + qoff[g]);
+#pragma unroll
+      for (int b = 0; b < MB; ++b)
+        fb[b] = *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+            la + offM + b * 32 * kGfBK + qoff[g]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                fa[a][t], fb[b][t], acc[a][b], 0, 0, 0);
+    }
+  };
+  // acc[a][b]: accumulator of Y^T block (n block a, m block b): lane i is
+  // row m0 + 32 b + i, registers 4 q + r columns n0 + 32 a + 8 q + 4 h + r.
+  auto epilogue = [&](int uu) {
+    const int m0 = (uu / ntn) * TM + wm * 32 * MB + i;
+    const int n0 = (uu % ntn) * TN + wn * 32 * NB + 4 * h;
+#pragma unroll
+    for (int a = 0; a < NB; ++a) {
+      float4 bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bv[q] = bias ? *reinterpret_cast<const float4*>(bias + n0 + 32 * a +
+                                                        8 * q)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        const int m = m0 + 32 * b;
+        float* yrow = Y + (size_t)m * ldy + n0 + 32 * a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 v = make_float4(acc[a][b][4 * q] + bv[q].x,
+                                 acc[a][b][4 * q + 1] + bv[q].y,
+                                 acc[a][b][4 * q + 2] + bv[q].z,
+                                 acc[a][b][4 * q + 3] + bv[q].w);
+          if (relu) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+          }
+          if (m < M) *reinterpret_cast<float4*>(yrow + 8 * q) = v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][4 * q + r] = 0.f;
+        }
+      }
+    }
+  };
+  tile_ptrs(u);
+  stage(0, sA0, sB0);
+  int kc = 0;
+  auto step = [&](DGMC_LDS float* ca, DGMC_LDS float* cb, DGMC_LDS float* na,
+                  DGMC_LDS float* nbuf) -> bool {
+    const bool last_chunk = kc + 1 == nk;
+    const int tu = last_chunk ? u + G : u;
+    const int tkc = last_chunk ? 0 : kc + 1;
+    const bool more = tu < U;
+    if (more) {
+      if (last_chunk) tile_ptrs(tu);
+      stage(tkc, na, nbuf);
+      // (this wave's 2 (MB + NB) pieces of the next chunk stay in flight)
+      if constexpr (MB + NB == 4)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    gf_barrier();
+    compute(ca, cb);
+    if (last_chunk) epilogue(u);
+    gf_barrier();
+    u = tu;
+    kc = tkc;
+    return more;
+  };
+  while (step(sA0, sB0, sA1, sB1) && step(sA1, sB1, sA0, sB0)) {
+  }
+}
+
+int gf_num_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    hipDeviceProp_t prop;
+    DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
+    cached[dev] = prop.multiProcessorCount;
+  }
+  return usable_cus(cached[dev]);
+}
+
+}  // namespace
+
+// Y = act([parts] bt^T + bias).  parts: fp32 [M, K_p] views (unit column
+// stride, 16-byte aligned rows, K_p % 4 == 0); bt: fp32 [Nn, sum K_p] with
+// unit column stride (Nn % 64 == 0); out: optional [M, Nn] view to write.
+at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
+                       const c10::optional<at::Tensor>& bias, bool relu,
+                       const c10::optional<at::Tensor>& out) {
+  TORCH_CHECK(parts.size() >= 1, "gemm_nt_f32: at least one part");
+  const int64_t M = parts[0].size(0);
+  GfChunks A{};
+  int64_t K = 0;
+  for (const at::Tensor& p : parts) {
+    TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat &&
+                    p.dim() == 2 && p.size(0) == M && p.stride(1) == 1 &&
+                    p.size(1) % 4 == 0 && p.stride(0) % 4 == 0 &&
+                    aligned16(p.data_ptr()),
+                "gemm_nt_f32: parts fp32 [M, K_p % 4] with 16-byte rows");
+    for (int64_t c0 = 0; c0 < p.size(1); c0 += 128) {
+      TORCH_CHECK(A.n < kGfMaxChunks, "gemm_nt_f32: K too large");
+      A.a[A.n] = p.data_ptr<float>() + c0;
+      A.lda[A.n] = (int)p.stride(0);
+      A.width[A.n] = (int)std::min<int64_t>(128, p.size(1) - c0);
+      A.boff[A.n] = (int)(K + c0);
+      ++A.n;
+    }
+    K += p.size(1);
+  }
+  TORCH_CHECK(bt.is_cuda() && bt.scalar_type() == at::kFloat &&
+                  bt.dim() == 2 && bt.size(1) == K && bt.stride(1) == 1 &&
+                  bt.stride(0) % 4 == 0 && aligned16(bt.data_ptr()) &&
+                  bt.size(0) % 64 == 0,
+              "gemm_nt_f32: Bt fp32 [Nn % 64, K] with 16-byte rows");
+  const int64_t Nn = bt.size(0);
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
+                    bias->numel() == Nn && aligned16(bias->data_ptr()),
+                "gemm_nt_f32: fp32 bias [Nn]");
+    bp = bias->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(bt.device());
+  at::Tensor Y;
+  if (out.has_value() && out->defined()) {
+    Y = *out;
+    TORCH_CHECK(Y.scalar_type() == at::kFloat && Y.dim() == 2 &&
+                    Y.size(0) == M && Y.size(1) == Nn && Y.stride(1) == 1 &&
+                    Y.stride(0) % 4 == 0 && aligned16(Y.data_ptr()),
+                "gemm_nt_f32: out fp32 [M, Nn] with 16-byte rows");
+  } else {
+    Y = at::empty({M, Nn}, bt.options());
+  }
+  if (M == 0 || Nn == 0) return Y;
+  const int cus = gf_num_cus(bt.device().index());
+  const int64_t big = ((M + 127) / 128) * (Nn / 128);
+  const bool small = big < cus || Nn % 128 != 0;
+  const int64_t tiles = small ? ((M + 63) / 64) * (Nn / 64) : big;
+  const int64_t blocks = std::min<int64_t>(tiles, 2 * (int64_t)cus);
+  auto kern = small ? gemm_nt_f32_kernel<1, 1> : gemm_nt_f32_kernel<2, 2>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream(), A,
+                     (int)M, bt.data_ptr<float>(), (int)bt.stride(0),
+                     (int)Nn, bp, relu ? 1 : 0, Y.data_ptr<float>(),
+                     (int)Y.stride(0));
+  DGMC_CHECK_LAUNCH();
+  return Y;
+}
+
+}  // namespace dgmc

@@ -5,6 +5,33 @@
 #include <torch/library.h>
 
 namespace dgmc {
+void relconv_fwd(const at::Tensor& ptr, const at::Tensor& col,
+                 const at::Tensor& split, const at::Tensor& hub,
+                 const at::Tensor& xa, const c10::optional<at::Tensor>& xb,
+                 const at::Tensor& w1, const at::Tensor& w2,
+                 const at::Tensor& wr, const at::Tensor& bias, bool relu,
+                 at::Tensor out, const c10::optional<at::Tensor>& xcopy,
+                 const c10::optional<at::Tensor>& feat,
+                 const c10::optional<at::Tensor>& fold,
+                 const c10::optional<at::Tensor>& pq);
+void relconv_bwd(const at::Tensor& ptr, const at::Tensor& col,
+                 const at::Tensor& w, const at::Tensor& split,
+                 const at::Tensor& hub, const at::Tensor& g,
+                 const at::Tensor& xa, const c10::optional<at::Tensor>& xb,
+                 const at::Tensor& w1, const at::Tensor& w2,
+                 const at::Tensor& wr, const c10::optional<at::Tensor>& dadd,
+                 at::Tensor dout, int64_t row0, bool mask, at::Tensor part,
+                 bool part_acc);
+void rel_proj_bwd(const at::Tensor& dpq, const at::Tensor& feat,
+                  const at::Tensor& fold, at::Tensor dfeat, at::Tensor part,
+                  bool part_acc);
+void rel_fold(at::TensorList parts, at::TensorList outs);
+at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
+                       const c10::optional<at::Tensor>& bias, bool relu,
+                       const c10::optional<at::Tensor>& out);
+std::tuple<at::Tensor, at::Tensor> fold_weights_bwd(const at::Tensor& w1,
+                                                    const at::Tensor& wf,
+                                                    const at::Tensor& g);
 int64_t set_cu_reserve(int64_t n);
 at::Tensor cu_hog(const at::Tensor& like, int64_t blocks, double usec);
 }  // namespace dgmc
@@ -319,6 +346,24 @@ at::Tensor sinkhorn_bwd(const at::Tensor& G, const at::Tensor& S_hat,
 
 TORCH_LIBRARY(dgmc_amd, m) {
   m.def("set_cu_reserve(int n) -> int");
+  m.def(
+      "relconv_fwd(Tensor ptr, Tensor col, Tensor split, Tensor hub, Tensor "
+      "xa, Tensor? xb, Tensor w1, Tensor w2, Tensor wr, Tensor bias, bool "
+      "relu, Tensor(a!) out, Tensor(b!)? xcopy, Tensor? feat, Tensor? fold, "
+      "Tensor(c!)? pq) -> ()");
+  m.def(
+      "relconv_bwd(Tensor ptr, Tensor col, Tensor w, Tensor split, Tensor "
+      "hub, Tensor g, Tensor xa, Tensor? xb, Tensor w1, Tensor w2, Tensor wr, "
+      "Tensor? dadd, Tensor(a!) dout, int row0, bool mask, Tensor(b!) part, "
+      "bool part_acc) -> ()");
+  m.def("rel_fold(Tensor[] parts, Tensor(a!)[] outs) -> ()");
+  m.def(
+      "gemm_nt_f32(Tensor[] parts, Tensor bt, Tensor? bias=None, bool "
+      "relu=False, Tensor(a!)? out=None) -> Tensor");
+  m.def("fold_weights_bwd(Tensor w1, Tensor wf, Tensor g) -> (Tensor, Tensor)");
+  m.def(
+      "rel_proj_bwd(Tensor dpq, Tensor feat, Tensor fold, Tensor(a!) dfeat, "
+      "Tensor(b!) part, bool part_acc) -> ()");
   m.def("cu_hog(Tensor like, int blocks, float usec) -> Tensor");
   m.def(
       "spmm_csr(Tensor rowptr, Tensor col, Tensor val, Tensor x, Tensor? "
@@ -548,6 +593,12 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CompositeExplicitAutograd, m) {
 
 TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("cu_hog", &dgmc::cu_hog);
+  m.impl("relconv_fwd", &dgmc::relconv_fwd);
+  m.impl("relconv_bwd", &dgmc::relconv_bwd);
+  m.impl("rel_proj_bwd", &dgmc::rel_proj_bwd);
+  m.impl("fold_weights_bwd", &dgmc::fold_weights_bwd);
+  m.impl("rel_fold", &dgmc::rel_fold);
+  m.impl("gemm_nt_f32", &dgmc::gemm_nt_f32);
   m.impl("spmm_csr", &dgmc::spmm_csr);
   m.impl("spmm_csr_planes", &dgmc::spmm_csr_planes);
   m.impl("spmm_csr_out", &dgmc::spmm_csr_out);

@@ -35,6 +35,7 @@ from ..nn.inits import reset
 from ..ops import _backend
 from ..ops import dense as dense_ops
 from ..ops.gemm import mixed_matmul
+from ..ops import relconv as relconv_ops
 from ..ops import sparse_corr
 from ..ops.plans import _IdentityCache
 from ..runtime import loopgrad
@@ -480,24 +481,45 @@ class DGMC(torch.nn.Module):
             # the dense path: [P; Q] = feat (W1 W_f)^T on psi_2's joint
             # features (b_f cancels in P_i - Q_idx) - one node GEMM per step
             # instead of three (final Linear, P, Q), forward and backward.
-            fold_w = None
+            fold_w = rel = None
             if steps > 0 and cand is not None and pair is not None and \
                     self._fusable(self.psi_2) and self._foldable() and \
                     lay_s.identity and lay_t.identity:
-                fold_w = _FoldProduct.apply(self.mlp[0].weight,
-                                            self.psi_2.final.weight,
-                                            self.psi_2.final.bias)[0]
+                # RelCNN psi_2 of the DBP15K config: the whole encoder +
+                # folded projection as fused HIP kernels (ops/relconv.py).
+                if relconv_ops.supported(self.psi_2, self.psi_2.final,
+                                         self.mlp[0]):
+                    rel = relconv_ops.rel_plan(pair.edge_index,
+                                               lay_s.num_nodes +
+                                               lay_t.num_nodes)
+                if rel is None:
+                    fold_w = _FoldProduct.apply(self.mlp[0].weight,
+                                                self.psi_2.final.weight,
+                                                self.psi_2.final.bias)[0]
             # The consensus kernel also emits softmax(S_hat') - the next
             # step's S and finally S_L (dgmc.py:205,225) - and runs its
             # backward: no separate softmax kernels nor gradient add.
-            fused_soft = fold_w is not None and sparse_corr.soft_fusable(
-                k, self.mlp[0].weight.size(0))
+            fused_soft = (fold_w is not None or rel is not None) and \
+                sparse_corr.soft_fusable(k, self.mlp[0].weight.size(0))
             for step in range(steps):
                 if step > 0 and not fused_soft:
                     S = S_hat.softmax(dim=-1)
                 r_s = r_all[step]
                 r_t = sparse_corr.sparse_transport(
                     S, lay_s.to_dense(r_s), S_idx, N_t, cand)
+                if rel is not None:
+                    PQ = relconv_ops.psi2_fold(
+                        self.psi_2, self.mlp[0].weight, rel, r_s,
+                        r_t.reshape(-1, r_t.size(-1)),
+                        (id(self.psi_2), rel.N))
+                    res = sparse_corr.consensus_update_pq(
+                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand,
+                        with_prob=fused_soft)
+                    if fused_soft:
+                        S_hat, S = res
+                    else:
+                        S_hat = res
+                    continue
                 if fold_w is not None:
                     _, _, feat = refine(r_s, lay_t.to_sparse(r_t),
                                         features=True)

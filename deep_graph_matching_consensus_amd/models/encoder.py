@@ -20,7 +20,7 @@ import contextlib
 import torch
 from torch.nn import Linear
 
-from ..ops.gemm import linear
+from ..ops.gemm import linear, linear_parts
 
 
 class CatParts(object):
@@ -66,6 +66,14 @@ class StackedEncoder(torch.nn.Module):
         if not self.lin or getattr(self, '_features_only', False):
             return x
         return linear(x, self.final.weight, self.final.bias)
+
+    def _head_project(self, xs):
+        """``_project(_head(xs))``; with ``cat`` and the final Linear the
+        layer features are read in place by one GEMM (no concatenation)."""
+        if self.cat and self.lin and not getattr(self, '_features_only',
+                                                 False):
+            return linear_parts(xs, self.final.weight, self.final.bias)
+        return self._project(self._head(xs))
 
     @contextlib.contextmanager
     def features_only(self):

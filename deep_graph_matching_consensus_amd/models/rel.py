@@ -45,9 +45,11 @@ class RelConv(torch.nn.Module):
         plan = relational_plan(edge_index, x.size(0))
         dtype = compute_dtype(x)
         w = self.stacked_weight()
-        w_lp = cached(('rel_w_lp', id(self), dtype),
-                      lambda: w.detach().to(
-                          dtype, memory_format=torch.contiguous_format))
+        # (fp32: the GEMM reads the stacked weight in place - no copy)
+        w_lp = w if dtype == w.dtype else cached(
+            ('rel_w_lp', id(self), dtype),
+            lambda: w.detach().to(dtype,
+                                  memory_format=torch.contiguous_format))
         # root.bias enters through the root slot (coefficient 1) = output bias.
         return gemm_spmm(plan, x, w, w_lp, self.out_channels,
                          bias=self.root.bias, relu=(act == 'relu'),
@@ -102,7 +104,7 @@ class RelCNN(StackedEncoder):
                 if kw:
                     h, xs[-1] = h
             xs.append(F.dropout(h, p=self.dropout, training=self.training))
-        return self._project(self._head(xs))
+        return self._head_project(xs)
 
     def __repr__(self):
         return ('{}({}, {}, num_layers={}, batch_norm={}, cat={}, lin={}, '

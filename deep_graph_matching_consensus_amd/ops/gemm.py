@@ -61,6 +61,88 @@ def dense_x6(x, w, bias=None):
     return ops.dense_gemm_x6(x, w3, b)
 
 
+def _rows16(t):
+    return (t.dim() == 2 and t.dtype == torch.float32 and t.stride(1) == 1
+            and t.size(1) % 4 == 0 and t.stride(0) % 4 == 0 and
+            t.data_ptr() % 16 == 0)
+
+
+def nt_f32_supported(parts, bt):
+    """``[parts] @ bt^T`` on the exact-f32 chunked GEMM
+    (``csrc/hip/gemm_f32.hip``): fp32 device operands with 16-byte rows,
+    output width a multiple of 64, K <= 3072."""
+    if not (parts and _backend.use_hip(parts[0]) and _rows16(bt) and
+            bt.size(0) % 64 == 0):
+        return False
+    M = parts[0].size(0)
+    chunks = 0
+    for p in parts:
+        if not (_rows16(p) and p.size(0) == M):
+            return False
+        chunks += (p.size(1) + 127) // 128
+    return (chunks <= 24 and bt.size(1) == sum(p.size(1) for p in parts)
+            and M > 0)
+
+
+def nt_f32(parts, bt, bias=None, relu=False, out=None):
+    """``act([parts] @ bt^T + bias)`` (fp32, no autograd; parts read in
+    place, never concatenated)."""
+    b = None
+    if bias is not None:
+        b = bias.detach()
+        if not b.is_contiguous():
+            b = b.contiguous()
+    return _backend.ops().gemm_nt_f32(list(parts), bt, b, relu, out)
+
+
+class _LinearParts(torch.autograd.Function):
+    """``torch.cat(parts, -1) @ W^T + b`` without the concatenation: the
+    exact-f32 chunked GEMM reads the parts in place (forward); backward by
+    per-part library products (the training-phase path)."""
+
+    @staticmethod
+    def forward(ctx, weight, bias, *parts):
+        w = weight.detach()
+        out = nt_f32(parts, w, bias)
+        ctx.widths = [p.size(1) for p in parts]
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(weight, *parts)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        weight, *parts = ctx.saved_tensors
+        g = g.contiguous()
+        grads, off = [], 0
+        for i, w in enumerate(ctx.widths):
+            grads.append(g @ weight[:, off:off + w]
+                         if ctx.needs_input_grad[2 + i] else None)
+            off += w
+        gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gw = torch.cat([matmul_tn_fp32(g, p.contiguous())
+                            for p in parts], 1)
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            gb = _col_sum(g)
+        return (gw, gb) + tuple(grads)
+
+
+def linear_parts(parts, weight, bias=None):
+    """``F.linear(torch.cat(parts, -1), weight, bias)``; on the GPU (fp32)
+    the parts are read in place by one exact-f32 GEMM (no concatenation)."""
+    parts = list(parts)
+    ok = nt_f32_supported(parts, weight) and (
+        bias is None or (bias.dtype == torch.float32 and
+                         bias.is_contiguous() and bias.data_ptr() % 16 == 0))
+    if not ok:
+        return linear(torch.cat(parts, -1), weight, bias)
+    if torch.is_grad_enabled() and (
+            weight.requires_grad or any(p.requires_grad for p in parts) or
+            (bias is not None and bias.requires_grad)):
+        return _LinearParts.apply(weight, bias, *parts)
+    return nt_f32(parts, weight, bias)
+
+
 def _split_factor(m, n, k):
     elems = m * n
     if elems >= (4 << 20) or k < 2048:

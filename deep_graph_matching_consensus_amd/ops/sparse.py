@@ -313,9 +313,13 @@ class _GemmSpMM(torch.autograd.Function):
                 xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
                 relu, xc.dtype, None)
         else:
-            from .gemm import dense_x6, dense_x6_supported
+            from .gemm import (dense_x6, dense_x6_supported, nt_f32,
+                               nt_f32_supported)
             if dense_x6_supported(xc, w_lp):
                 y = dense_x6(xc, w_lp).view(-1, C)      # fp32 as bf16x6
+            elif nt_f32_supported([xc], w_lp.t()):
+                # exact-f32 MFMA GEMM, x read in place (csrc/hip/gemm_f32.hip)
+                y = nt_f32([xc], w_lp.t()).view(-1, C)
             else:
                 y = (xc @ w_lp).view(-1, C)
             out_dtype = y.dtype if y.dtype in (torch.bfloat16,

@@ -38,6 +38,12 @@ from .runtime.tuning import tuned_gemms, use_tuned_gemms
 # with the backward (DGMC_AMD_IN_STEP_ALLREDUCE=0: one flat all-reduce after
 # the step).
 IN_STEP_ALLREDUCE = os.environ.get('DGMC_AMD_IN_STEP_ALLREDUCE', '1') == '1'
+# CUs the persistent GEMM grids leave to RCCL's channel kernels under data
+# parallelism (DGMC_AMD_RESERVE_CUS overrides; single-GPU runs reserve none).
+# tools/bench_cu_reserve.py (profiles/cu_reserve_r5.json): 8 CUs held by a
+# concurrent kernel stretch psi_1's 1024 -> 256 bf16x6 forward from 400 to
+# 615 us; with the grid sized to 256 - 8 CUs it runs 405 us.
+DP_RESERVE_CUS = 16
 
 
 class PairTrainer(object):
@@ -97,6 +103,12 @@ class PairTrainer(object):
         cuda = self.device.type == 'cuda'
         if cuda:
             use_tuned_gemms()     # measured GEMM solutions (runtime/tuning.py)
+        self.reserved_cus = 0
+        if cuda and self.world > 1:
+            from .ops import _backend
+            env = os.environ.get('DGMC_AMD_RESERVE_CUS')
+            self.reserved_cus = int(env) if env else DP_RESERVE_CUS
+            _backend.set_cu_reserve(self.reserved_cus)
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda,
                                           capturable=mode == 'graph')

@@ -1,0 +1,70 @@
+"""Exact-fp32 chunked NT GEMM (csrc/hip/gemm_f32.hip): parts read in place
+(arbitrary widths % 4, row strides), zero-page tails, bias / ReLU epilogue,
+strided output - against fp64, error at most that of torch's fp32 GEMM
+(x2) on the same inputs.  Shapes of the DBP15K psi_1 node GEMMs
+(/root/reference/dgmc/models/rel.py:28-31,92)."""
+import pytest
+import torch
+
+from deep_graph_matching_consensus_amd.ops import _backend
+from deep_graph_matching_consensus_amd.ops import gemm
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.mark.parametrize('M,widths,Nn,bias,relu', [
+    (19388 + 19572, [300], 768, False, False),     # RelConv layer 0 map
+    (39000, [256], 768, False, False),             # layers 1, 2
+    (39000, [300, 256, 256, 256], 256, True, False),   # final Linear
+    (1000, [4, 132, 64], 64, True, True),          # tails, skinny tiles
+    (77, [128], 128, False, True)])
+def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu):
+    g = torch.Generator(device=DEV).manual_seed(M + Nn)
+    # parts as column slices of one wider buffer (strided rows)
+    K = sum(widths)
+    buf = torch.randn(M, K + 8, device=DEV, generator=g)
+    parts, off = [], 0
+    for w in widths:
+        parts.append(buf[:, off:off + w])
+        off += w
+    wt = torch.randn(Nn, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(Nn, device=DEV, generator=g) if bias else None
+    assert gemm.nt_f32_supported(parts, wt)
+    y = gemm.nt_f32(parts, wt, b, relu)
+    x = torch.cat(parts, 1)
+    ref = x.double() @ wt.double().t()
+    y32 = x @ wt.t()
+    if bias:
+        ref = ref + b.double()
+        y32 = y32 + b
+    if relu:
+        ref, y32 = ref.clamp(min=0), y32.clamp(min=0)
+    e = float((y.double() - ref).abs().max())
+    e32 = float((y32.double() - ref).abs().max())
+    assert e <= 2 * e32 + 1e-7, (e, e32)
+
+
+def test_gemm_nt_f32_out_view_and_linear_parts():
+    """``out=`` writes a column slice of a larger buffer; linear_parts (the
+    RelCNN head) equals F.linear on the concatenation, gradients included."""
+    g = torch.Generator(device=DEV).manual_seed(1)
+    a = torch.randn(500, 300, device=DEV, generator=g)
+    w = torch.randn(128, 300, device=DEV, generator=g) / 17
+    big = torch.full((500, 256), 7.0, device=DEV)
+    _backend.ops().gemm_nt_f32([a], w, None, False, big[:, 64:192])
+    torch.testing.assert_close(big[:, 64:192], a @ w.t(), rtol=1e-5,
+                               atol=1e-5)
+    assert bool((big[:, :64] == 7).all() and (big[:, 192:] == 7).all())
+    lin = torch.nn.Linear(300 + 256, 256).to(DEV)
+    h = torch.randn(500, 256, device=DEV, generator=g, requires_grad=True)
+    a.requires_grad_()
+    y = gemm.linear_parts([a, h], lin.weight, lin.bias)
+    ref = torch.nn.functional.linear(torch.cat([a, h], 1), lin.weight,
+                                     lin.bias)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    go = torch.randn_like(y)
+    g1 = torch.autograd.grad(y, [a, h, lin.weight, lin.bias], go)
+    g2 = torch.autograd.grad(ref, [a, h, lin.weight, lin.bias], go)
+    for u, v in zip(g1, g2):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-4)

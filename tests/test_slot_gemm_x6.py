@@ -446,3 +446,30 @@ def test_dense_nt_x6_error_not_above_exact_f32(M, parts, Nn):
         e32 = float((y32.double() - ref).abs().max())
         assert e6 <= e32 * 1.0001 + 1e-7, (e6, e32)
     assert e6 < 1e-5 * float(ref.abs().max())
+
+
+def test_cu_reserve_keeps_results_and_hog_exits(headline_plan):
+    """``set_cu_reserve``: the persistent x6 forward on CUs - 16 gives the
+    same bits (each tile is computed by one workgroup either way); the
+    ``cu_hog`` micro-benchmark kernel (tools/bench_cu_reserve.py) runs on
+    its own, holds one CU per block and exits on its wall-clock bound."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(N, 256, device=DEV, generator=g)
+    w = torch.randn(25, 256, 256, device=DEV, generator=g) / 16
+    r = torch.randn(256, 256, device=DEV, generator=g) / 16
+    wt3 = ops.slot_weight_x3(w, r, True)
+    rows = plan.src.long() >= 0
+    y0 = ops.slot_gemm_x6(x, plan.src, plan.seg, wt3, True, None)
+    prev = _backend.set_cu_reserve(16)
+    try:
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            done = ops.cu_hog(x, 8, 200.0)
+        y1 = ops.slot_gemm_x6(x, plan.src, plan.seg, wt3, True, None)
+        torch.cuda.synchronize()
+    finally:
+        _backend.set_cu_reserve(prev)
+    assert torch.equal(y0[rows], y1[rows])
+    assert done.tolist() == [1] * 8
