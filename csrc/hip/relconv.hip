@@ -172,100 +172,129 @@ __device__ __forceinline__ void rc_entry(const RcPlan& pl,
   }
 }
 
-// Regular rows: lane group `grp` (8 lanes, lane q holds channels 4q..4q+3)
-// sums the two lists of local rows la and lb as ONE entry stream, 8 entries
-// in flight per lane, each list summed in order.  acc[0..1]: row a's lists,
-// acc[2..3]: row b's.  Hub rows (va / vb false) are skipped.
-template <bool WEIGHTED>
-__device__ __forceinline__ void rc_gather_rows(const RcPlan& pl,
+// Balanced (merge-path) gather of the tile's 128 segments (row lr, list
+// l: segment 2 lr + l): the tile's contiguous entry range is cut into 32
+// equal chunks, one per lane group (8 lanes, lane q holds channels
+// 4q..4q+3); a group walks its chunk in order with 8 loads in flight per
+// lane and writes every segment that starts and ends inside it straight
+// to sA (MEAN: divided by the segment's entry count), while the partial
+// sums of segments crossing a chunk border go to LDS and are added in
+// chunk order by the group where the segment starts.  Long rows (hub
+// entities) are spread over several groups; no group walks more than
+// ceil(n / 32) entries.  Empty segments keep the zeros written up front.
+struct RcFlat {
+  float* P;    // [32][2][32] border partials: slot 0 head, slot 1 tail
+  int* PS;     // [32][2] their segments (-1: none)
+  int* PO;     // [32] 1: the tail segment started in this chunk (owner)
+};
+
+__device__ __forceinline__ int rc_seg_end(const RcTileLists& s, int seg) {
+  return (seg & 1) ? s.ptr[(seg >> 1) + 1] : s.split[seg >> 1];
+}
+__device__ __forceinline__ int rc_seg_begin(const RcTileLists& s, int seg) {
+  return (seg & 1) ? s.split[seg >> 1] : s.ptr[seg >> 1];
+}
+
+template <bool WEIGHTED, bool MEAN>
+__device__ __forceinline__ void rc_gather_flat(const RcPlan& pl,
                                                const RcTileLists& s,
-                                               const RcRows& src, int la,
-                                               int lb, bool va, bool vb,
-                                               int q, float4 acc[4]) {
-  const int e0 = s.ptr[0];
-  const int pa = s.ptr[la], sa = s.split[la];
-  const int pb = s.ptr[lb], sb = s.split[lb];
-  const int La = va ? s.ptr[la + 1] - pa : 0;
-  const int Lb = vb ? s.ptr[lb + 1] - pb : 0;
-#pragma unroll
-  for (int u = 0; u < 4; ++u) acc[u] = f4_zero();
-  const int T = La + Lb;
-  for (int t0 = 0; t0 < T; t0 += 8) {
-    int seg[8], j[8];
-    float wt[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int t = t0 + u;
-      const bool inA = t < La;
-      const int e = inA ? pa + t : pb + (t - La);
-      seg[u] = t < T ? (inA ? (e < sa ? 0 : 1) : (e < sb ? 2 : 3)) : -1;
-      j[u] = 0;
-      wt[u] = 0.f;
-      if (t < T) rc_entry<WEIGHTED>(pl, s, e0, e, j[u], wt[u]);
+                                               const RcRows& src, float* sA,
+                                               int pitch, const RcFlat& fl) {
+  const int tid = threadIdx.x, q = tid & 7, g = tid >> 3;   // 32 groups
+  const int E0 = s.ptr[0], E1 = s.ptr[kRcRows];
+  const int n = E1 - E0;
+  const int L = (n + 31) >> 5;
+  const int c0 = E0 + min(n, g * L), c1 = E0 + min(n, (g + 1) * L);
+  if (q == 0) {
+    fl.PS[2 * g] = -1;
+    fl.PS[2 * g + 1] = -1;
+    fl.PO[g] = 0;
+  }
+  auto put = [&](int seg, const float4& acc) {
+    float4 v = acc;
+    if (MEAN) {
+      const float cnt =
+          (float)max(rc_seg_end(s, seg) - rc_seg_begin(s, seg), 1);
+      v = f4_div(acc, cnt);
     }
-    float4 v[8];
+    lds_put4(sA + (seg >> 1) * pitch + (seg & 1) * kRcK + 4 * q, v);
+  };
+  if (c0 < c1) {
+    // first segment whose end is past c0 (segment ends are non-decreasing)
+    int lo = 0, hi = 2 * kRcRows - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (rc_seg_end(s, mid) > c0) hi = mid; else lo = mid + 1;
+    }
+    int seg = lo;
+    int send = rc_seg_end(s, seg);
+    bool started = rc_seg_begin(s, seg) >= c0;
+    float4 acc = f4_zero();
+    for (int e0 = c0; e0 < c1; e0 += 8) {
+      int j[8];
+      float wt[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = seg[u] >= 0 ? f4_ld(src.row(j[u]) + 4 * q) : f4_zero();
+      for (int u = 0; u < 8; ++u) {
+        j[u] = 0;
+        wt[u] = 0.f;
+        if (e0 + u < c1) rc_entry<WEIGHTED>(pl, s, E0, e0 + u, j[u], wt[u]);
+      }
+      float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 8; ++u)
+        v[u] = e0 + u < c1 ? f4_ld(src.row(j[u]) + 4 * q) : f4_zero();
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (seg[u] == g) {
-          if (WEIGHTED)
-            f4_fma(acc[g], wt[u], v[u]);
-          else
-            f4_add(acc[g], v[u]);
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u;
+        if (e >= c1) break;
+        while (e >= send) {            // segment(s) ending before e
+          if (started) {
+            put(seg, acc);
+          } else {
+            float* p = fl.P + (2 * g) * kRcK + 4 * q;   // head partial
+            p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
+            if (q == 0) fl.PS[2 * g] = seg;
+          }
+          acc = f4_zero();
+          ++seg;
+          send = rc_seg_end(s, seg);
+          started = true;
         }
+        if (WEIGHTED)
+          f4_fma(acc, wt[u], v[u]);
+        else
+          f4_add(acc, v[u]);
+      }
+    }
+    // the segment current at c1
+    if (send <= c1) {
+      if (started) {
+        put(seg, acc);
+      } else {
+        float* p = fl.P + (2 * g) * kRcK + 4 * q;
+        p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
+        if (q == 0) fl.PS[2 * g] = seg;
+      }
+    } else {
+      float* p = fl.P + (2 * g + 1) * kRcK + 4 * q;     // tail partial
+      p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
+      if (q == 0) {
+        fl.PS[2 * g + 1] = seg;
+        fl.PO[g] = started ? 1 : 0;
       }
     }
   }
-}
-
-// A hub row by the whole wave: group g takes entries g, g + 8, ... of the
-// row's joint list (8 in flight per lane); the 8 group partials are summed
-// by an xor butterfly over the group bits; lanes of group 0 return them.
-template <bool WEIGHTED>
-__device__ __forceinline__ void rc_gather_hub(const RcPlan& pl,
-                                              const RcTileLists& s,
-                                              const RcRows& src, int lr,
-                                              int grp, int q, float4& acc0,
-                                              float4& acc1) {
-  const int e0 = s.ptr[0];
-  const int p0 = s.ptr[lr], sp = s.split[lr], p1 = s.ptr[lr + 1];
-  acc0 = f4_zero();
-  acc1 = f4_zero();
-  for (int b = p0 + grp; b < p1; b += 64) {
-    int j[8];
-    float wt[8];
-    bool ok[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = b + 8 * u;
-      ok[u] = e < p1;
-      j[u] = 0;
-      wt[u] = 0.f;
-      if (ok[u]) rc_entry<WEIGHTED>(pl, s, e0, e, j[u], wt[u]);
-    }
-    float4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = ok[u] ? f4_ld(src.row(j[u]) + 4 * q) : f4_zero();
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (!ok[u]) continue;
-      float4& a = (b + 8 * u) < sp ? acc0 : acc1;
-      if (WEIGHTED)
-        f4_fma(a, wt[u], v[u]);
-      else
-        f4_add(a, v[u]);
-    }
-  }
-#pragma unroll
-  for (int m = 8; m < 64; m <<= 1) {
-    const float4 o0 = f4_xor(acc0, m), o1 = f4_xor(acc1, m);
-    f4_add(acc0, o0);
-    f4_add(acc1, o1);
+  __syncthreads();
+  // owners complete their border segments in chunk order
+  if (fl.PO[g]) {
+    const int seg = fl.PS[2 * g + 1];
+    float4 acc = f4_ld(fl.P + (2 * g + 1) * kRcK + 4 * q);
+    int h = g + 1;
+    for (; h < 32 && fl.PS[2 * h + 1] == seg && fl.PO[h] == 0; ++h)
+      f4_add(acc, f4_ld(fl.P + (2 * h + 1) * kRcK + 4 * q));
+    if (h < 32 && fl.PS[2 * h] == seg)
+      f4_add(acc, f4_ld(fl.P + (2 * h) * kRcK + 4 * q));
+    put(seg, acc);
   }
 }
 
@@ -289,7 +318,8 @@ __device__ __forceinline__ void rc_stage_w(const float* const w[3],
 // Forward.  LDS: sA [64][kRcP] (PROJ: sF [64][kRcFP]), sW [32][kRcP] (PROJ:
 // then the fold [32][kRcFP]), lists.
 // ---------------------------------------------------------------------------
-constexpr int kRcListLds = (kRcRows + 1 + 2 * kRcRows + kRcCap) * 4;
+constexpr int kRcListLds = (kRcRows + 1 + 2 * kRcRows + kRcCap) * 4 +
+                           (64 * kRcK + 64 + 32) * 4;   // + RcFlat
 constexpr int kRcFwdLds = (kRcRows * kRcP + kRcC * kRcP) * 4 + kRcListLds;
 constexpr int kRcFwdProjLds =
     (kRcRows * kRcFP + 32 * kRcFP) * 4 + kRcListLds;
@@ -303,6 +333,9 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
   int* lists = reinterpret_cast<int*>(sW + (PROJ ? 32 * kRcFP : kRcC * kRcP));
   const RcTileLists s{lists, lists + kRcRows + 1, lists + 2 * kRcRows + 1,
                       lists + 3 * kRcRows + 1, nullptr};
+  float* flp = reinterpret_cast<float*>(lists + 3 * kRcRows + 1 + kRcCap);
+  const RcFlat fl{flp, reinterpret_cast<int*>(flp + 64 * kRcK),
+                  reinterpret_cast<int*>(flp + 64 * kRcK) + 64};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * kRcRows;
   const int q = lane & 7, grp = lane >> 3;
@@ -312,25 +345,15 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
   const float4 xa = ra < pl.N ? f4_ld(a.x.row(ra) + 4 * q) : f4_zero();
   const float4 xb = rb < pl.N ? f4_ld(a.x.row(rb) + 4 * q) : f4_zero();
   rc_stage_w<true>(a.w, sW);
-  rc_stage_lists<false>(pl, r0, s);
-  const bool va = ra < pl.N && !s.hub[la];
-  const bool vb = rb < pl.N && !s.hub[lb];
-  float4 acc[4];
-  rc_gather_rows<false>(pl, s, a.x, la, lb, va, vb, q, acc);
   {
-    const float n0 = (float)max(s.split[la] - s.ptr[la], 1);
-    const float n1 = (float)max(s.ptr[la + 1] - s.split[la], 1);
-    const float n2 = (float)max(s.split[lb] - s.ptr[lb], 1);
-    const float n3 = (float)max(s.ptr[lb + 1] - s.split[lb], 1);
     const int P = PROJ ? kRcFP : kRcP;
-    if (va) {
-      lds_put4(sA + la * P + 4 * q, f4_div(acc[0], n0));
-      lds_put4(sA + la * P + kRcK + 4 * q, f4_div(acc[1], n1));
-    }
-    if (vb) {
-      lds_put4(sA + lb * P + 4 * q, f4_div(acc[2], n2));
-      lds_put4(sA + lb * P + kRcK + 4 * q, f4_div(acc[3], n3));
-    }
+    for (int t = tid; t < kRcRows * 16; t += 256)       // mean parts := 0
+      lds_put4(sA + (t >> 4) * P + (t & 15) * 4, f4_zero());
+  }
+  rc_stage_lists<false>(pl, r0, s);
+  {
+    const int P = PROJ ? kRcFP : kRcP;
+    rc_gather_flat<false, true>(pl, s, a.x, sA, P, fl);
     lds_put4(sA + la * P + 2 * kRcK + 4 * q, xa);
     lds_put4(sA + lb * P + 2 * kRcK + 4 * q, xb);
     if (a.xcopy) {
@@ -338,24 +361,6 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
         *reinterpret_cast<float4*>(a.xcopy + (size_t)ra * a.ldxc + 4 * q) = xa;
       if (rb < pl.N)
         *reinterpret_cast<float4*>(a.xcopy + (size_t)rb * a.ldxc + 4 * q) = xb;
-    }
-  }
-  // hub rows of this wave's 16 (whole wave each)
-  unsigned long long hm =
-      __ballot(lane < 16 && r0 + wave * 16 + lane < pl.N &&
-               s.hub[wave * 16 + (lane & 15)]);
-  while (hm) {
-    const int l = __builtin_ctzll(hm);
-    hm &= hm - 1;
-    const int lr = wave * 16 + l;
-    float4 h0, h1;
-    rc_gather_hub<false>(pl, s, a.x, lr, grp, q, h0, h1);
-    if (grp == 0) {
-      const int P = PROJ ? kRcFP : kRcP;
-      const float n0 = (float)max(s.split[lr] - s.ptr[lr], 1);
-      const float n1 = (float)max(s.ptr[lr + 1] - s.split[lr], 1);
-      lds_put4(sA + lr * P + 4 * q, f4_div(h0, n0));
-      lds_put4(sA + lr * P + kRcK + 4 * q, f4_div(h1, n1));
     }
   }
   __syncthreads();
@@ -446,6 +451,9 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
   int* lists = reinterpret_cast<int*>(sWt + kRcCap);
   const RcTileLists s{lists, lists + kRcRows + 1, lists + 2 * kRcRows + 1,
                       lists + 3 * kRcRows + 1, sWt};
+  float* flp = reinterpret_cast<float*>(lists + 3 * kRcRows + 1 + kRcCap);
+  const RcFlat fl{flp, reinterpret_cast<int*>(flp + 64 * kRcK),
+                  reinterpret_cast<int*>(flp + 64 * kRcK) + 64};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool pacc = a.part_acc != 0;
   const int r0 = blockIdx.x * kRcRows;
@@ -467,34 +475,15 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
   const float4 xa = ra < pl.N ? f4_ld(a.x.row(ra) + 4 * q) : f4_zero();
   const float4 xb = rb < pl.N ? f4_ld(a.x.row(rb) + 4 * q) : f4_zero();
   rc_stage_w<false>(a.w, sW);
+  for (int t = tid; t < kRcRows * 16; t += 256)         // t_in / t_out := 0
+    lds_put4(sG + (t >> 4) * kRcP + (t & 15) * 4, f4_zero());
   rc_stage_lists<true>(pl, r0, s);
   const RcRows gsrc{a.g, a.g, 0, a.ldg, a.ldg};
-  const bool va = ra < pl.N && !s.hub[la];
-  const bool vb = rb < pl.N && !s.hub[lb];
-  float4 acc[4];
-  rc_gather_rows<true>(pl, s, gsrc, la, lb, va, vb, q, acc);
-  lds_put4(sG + la * kRcP + 4 * q, acc[0]);
-  lds_put4(sG + la * kRcP + kRcC + 4 * q, acc[1]);
+  rc_gather_flat<true, false>(pl, s, gsrc, sG, kRcP, fl);
   lds_put4(sG + la * kRcP + 2 * kRcC + 4 * q, ga);
-  lds_put4(sG + lb * kRcP + 4 * q, acc[2]);
-  lds_put4(sG + lb * kRcP + kRcC + 4 * q, acc[3]);
   lds_put4(sG + lb * kRcP + 2 * kRcC + 4 * q, gb);
   *reinterpret_cast<float4*>(sX + la * kRcXP + 4 * q) = xa;
   *reinterpret_cast<float4*>(sX + lb * kRcXP + 4 * q) = xb;
-  unsigned long long hm =
-      __ballot(lane < 16 && r0 + wave * 16 + lane < pl.N &&
-               s.hub[wave * 16 + (lane & 15)]);
-  while (hm) {
-    const int l = __builtin_ctzll(hm);
-    hm &= hm - 1;
-    const int lr = wave * 16 + l;
-    float4 h0, h1;
-    rc_gather_hub<true>(pl, s, gsrc, lr, grp, q, h0, h1);
-    if (grp == 0) {
-      lds_put4(sG + lr * kRcP + 4 * q, h0);
-      lds_put4(sG + lr * kRcP + kRcC + 4 * q, h1);
-    }
-  }
   __syncthreads();
   const int i = lane & 15, kk = lane >> 4;
   // dx[16 rows][32] = G W_stack

@@ -641,6 +641,17 @@ class KGTrainer(object):
                  guard_nonfinite=True):
         self.model = model
         self.data = data
+        if data.x1.dim() == 2 and data.x1.shape[1:] == data.x2.shape[1:] \
+                and data.x1.dtype == data.x2.dtype and \
+                not (data.x1._base is not None and
+                     data.x1._base is data.x2._base):
+            # Both graphs' features in ONE buffer (x1 / x2 become row views
+            # of it): the model's joint encoding reads it in place - no
+            # concatenation per step (models/dgmc.py::_cat_rows); in-place
+            # writes to data.x1 / x2 still reach a captured step.
+            joint = torch.cat([data.x1, data.x2], 0)
+            data.x1 = joint[:data.x1.size(0)]
+            data.x2 = joint[data.x1.size(0):]
         self.device = data.x1.device
         cuda = self.device.type == 'cuda'
         self.graph = graph and cuda

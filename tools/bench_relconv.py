@@ -38,9 +38,13 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument('--reps', type=int, default=50)
     p.add_argument('--json', default=None)
+    p.add_argument('--hub-sweep', type=int, nargs='*', default=[],
+                   help='also time fwd / bwd with these hub thresholds')
+    p.add_argument('--scale', type=float, default=1.0)
+    p.add_argument('--no-gemm', action='store_true')
     args = p.parse_args()
     dev = torch.device('cuda')
-    d = make_kg_pair('zh_en', seed=0)
+    d = make_kg_pair('zh_en', seed=0, scale=args.scale)
     n_s, n_t = d.x1.size(0), d.x2.size(0)
     N = n_s + n_t
     ei = torch.cat([d.edge_index1, d.edge_index2 + n_s], 1).to(dev)
@@ -78,6 +82,27 @@ def main():
         dfeat[:, 32:64], 0, True, part, True), args.reps)
     res['fold_us'] = timeit(lambda: ops.rel_fold(
         [part, part, part, partf], outs), args.reps)
+    for T in args.hub_sweep:
+        pt = rc.RelPlan(ei, N, hub_threshold=T)
+        fa2, ba2 = pt.fwd_args(), pt.bwd_args()
+        res['hub%d_rows' % T] = int(pt.hub.sum())
+        res['hub%d_fwd_us' % T] = timeit(lambda: ops.relconv_fwd(
+            *fa2, feat[:, 32:64], None, *w, b, True, feat[:, 64:96], None,
+            None, None, None), args.reps)
+        res['hub%d_bwd_us' % T] = timeit(lambda: ops.relconv_bwd(
+            *ba2, dfeat[:, 64:96], feat[:, 32:64], None, *w,
+            dfeat[:, 32:64], dfeat[:, 32:64], 0, True, part, True),
+            args.reps)
+    # node GEMMs of psi_1 (exact-f32 chunked kernel vs torch / hipBLASLt)
+    tiny = torch.zeros(1, device=dev)
+    res['launch_floor_us'] = timeit(lambda: tiny.add_(1), args.reps)
+    for K, Nn in (() if args.no_gemm else
+                  ((300, 768), (256, 768), (1068, 256))):
+        xg = torch.randn(N, K, device=dev)
+        wg = torch.randn(Nn, K, device=dev)
+        res['gemm_%dx%d_us' % (K, Nn)] = timeit(
+            lambda: ops.gemm_nt_f32([xg], wg, None, False, None), 10)
+        res['torch_%dx%d_us' % (K, Nn)] = timeit(lambda: xg @ wg.t(), 10)
     r_s = torch.randn(n_s, 32, device=dev)
     r_t = torch.randn(n_t, 32, device=dev, requires_grad=True)
 
