@@ -20,12 +20,14 @@
 // rounded differently.)  Lists: one joint CSR per direction (forward: row i =
 // in-neighbours then out-neighbours; backward: out-list then in-list with the
 // per-entry weights), so a tile's entries are one contiguous range, staged
-// into LDS in one coalesced round.  A workgroup owns a 64-row tile; each of
-// its 4 waves gathers 16 rows - 8-lane groups (one 16-byte vector per lane
-// per row), two rows per group, 8 loads in flight per lane - and rows with
-// long lists (knowledge-graph hub entities) are gathered by the whole wave
-// afterwards (entries split over the 8 groups, butterfly-summed), so no
-// group walks a hub alone and no extra workgroups are needed.  Then the
+// into LDS in one coalesced round.  A workgroup owns a 64-row tile; the
+// tile's contiguous entry range is cut into 32 equal chunks gathered by
+// 8-lane groups (one 16-byte vector per lane and entry, 16 loads in flight
+// per lane), partial sums of segments crossing chunk borders completed in
+// chunk order (merge-path balance: knowledge-graph hub rows are spread over
+// several groups, no group walks more than ceil(entries / 32)).  All loads
+// that do not depend on the lists are issued in one round at kernel start,
+// so a tile costs ~2 + entries / 512 memory round trips.  Then the
 // tile is multiplied on v_mfma_f32_16x16x4_f32 (exact fp32 products) and the
 // epilogue adds the bias / ReLU, the fused consensus projection, or the
 // masked gradient adds.  Deterministic: fixed summation orders, no atomics;
@@ -45,16 +47,18 @@ constexpr int kRcFP = 130;        // pitch of [row][128] projection tiles
 constexpr int kRcDP = 34;         // pitch of [row][32] dPQ tiles
 constexpr int kRcFT = 144;        // pitch of the [row][128] feat tile (bwd)
 constexpr int kRcCap = 1024;      // tile entries staged in LDS (rest: global)
+constexpr int kRcU = 16;          // gather loads in flight per lane (max)
 constexpr int kRcPart = 3 * kRcC * kRcK + kRcC;   // dW_stack + db per tile
 constexpr int kRcPartPer = (kRcPart + 255) / 256; // per thread
 
 typedef float rc_f32x4 __attribute__((ext_vector_type(4)));
+typedef float rc_f32x2 __attribute__((ext_vector_type(2)));
 
 // Joint lists of one direction: row i's entries [ptr[i], ptr[i+1]), the
 // second list starting at split[i]; w: per-entry weights (backward only).
 struct RcPlan {
   const int* ptr;
-  const int* col;
+  const int* col;     // packed: column | (2 (row % 64) + list) << 24
   const int* split;
   const float* w;
   const unsigned char* hub;   // 1: gathered by the whole wave
@@ -67,8 +71,10 @@ struct RcRows {
   const float* a;
   const float* b;
   int split, lda, ldb;
+  // (32-bit offsets: the host checks rows * ld < 2^31)
   __device__ __forceinline__ const float* row(int j) const {
-    return j < split ? a + (size_t)j * lda : b + (size_t)(j - split) * ldb;
+    const bool first = j < split;
+    return (first ? a : b) + (first ? j * lda : (j - split) * ldb);
   }
 };
 
@@ -114,68 +120,105 @@ __device__ __forceinline__ void f4_fma(float4& a, float s, const float4& b) {
   a.z = fmaf(s, b.z, a.z); a.w = fmaf(s, b.w, a.w);
 }
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0, 0, 0, 0); }
-__device__ __forceinline__ float4 f4_div(const float4& a, float n) {
-  return make_float4(a.x / n, a.y / n, a.z / n, a.w / n);
+// Loads are issued unconditionally (from clamped, in-bounds addresses) and
+// zeroed afterwards by a select: `cond ? load : 0` compiles to a divergent
+// branch whose other side writes the load's registers, which forces a wait
+// for that load on the spot - one memory round trip per load instead of one
+// per round of independent loads.
+__device__ __forceinline__ float4 f4_keep(bool keep, const float4& v) {
+  return keep ? v : f4_zero();
+}
+__device__ __forceinline__ float4 f4_scale(const float4& a, float s) {
+  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
 }
 __device__ __forceinline__ float4 f4_xor(const float4& a, int m) {
   return make_float4(__shfl_xor(a.x, m), __shfl_xor(a.y, m),
                      __shfl_xor(a.z, m), __shfl_xor(a.w, m));
 }
 
-__device__ __forceinline__ void lds_put4(float* p, const float4& v) {
+__device__ __forceinline__ void lds_put4(DGMC_LDS float* p, const float4& v) {
   // (8-byte aligned rows: pitch 98)
-  reinterpret_cast<float2*>(p)[0] = make_float2(v.x, v.y);
-  reinterpret_cast<float2*>(p)[1] = make_float2(v.z, v.w);
+  reinterpret_cast<DGMC_LDS rc_f32x2*>(p)[0] = rc_f32x2{v.x, v.y};
+  reinterpret_cast<DGMC_LDS rc_f32x2*>(p)[1] = rc_f32x2{v.z, v.w};
+}
+__device__ __forceinline__ void lds_put4a(DGMC_LDS float* p,
+                                          const float4& v) {   // 16-byte
+  *reinterpret_cast<DGMC_LDS rc_f32x4*>(p) = rc_f32x4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ float4 lds_get4(const DGMC_LDS float* p) {
+  const rc_f32x2 a = reinterpret_cast<const DGMC_LDS rc_f32x2*>(p)[0];
+  const rc_f32x2 b = reinterpret_cast<const DGMC_LDS rc_f32x2*>(p)[1];
+  return make_float4(a.x, a.y, b.x, b.y);
 }
 
-// Per-tile list staging: row pointers / splits / hub flags of the tile's
-// 64 rows and its entries (up to kRcCap) in LDS.
+// Per-tile list staging: row pointers / splits of the tile's 64 rows and
+// its entries (up to kRcCap) in LDS.  Every stage issues all of its global
+// loads before its first LDS store (constant, unrolled trip counts), so a
+// stage costs one memory round trip rather than one per loop iteration: the
+// row heads are loaded with the kernel's other independent loads
+// (rc_load_heads), the entries in one unrolled round after them.
 struct RcTileLists {
-  int* ptr;     // [65] absolute entry indices
-  int* split;   // [64]
-  int* hub;     // [64]
-  int* col;     // [kRcCap]
-  float* w;     // [kRcCap] (weighted plans)
+  DGMC_LDS int* ptr;     // [65] absolute entry indices
+  DGMC_LDS int* split;   // [64] (padding rows: ptr[N], so segment ends stay sorted)
+  DGMC_LDS float* inv;   // [128] 1 / max(segment entries, 1)
+  DGMC_LDS int* col;     // [kRcCap] packed entries: column | tile segment << 24
+  DGMC_LDS float* w;     // [kRcCap] (weighted plans)
 };
+constexpr int kRcListInts =    // (padded to 16 bytes: the partials follow)
+    (kRcRows + 1 + kRcRows + 2 * kRcRows + kRcCap + 3) & ~3;
+constexpr int kRcColMask = (1 << 24) - 1;
+
+__device__ __forceinline__ RcTileLists rc_lists(DGMC_LDS int* l, DGMC_LDS float* w) {
+  return RcTileLists{l, l + kRcRows + 1, reinterpret_cast<DGMC_LDS float*>(l) +
+                     2 * kRcRows + 1, l + 4 * kRcRows + 1, w};
+}
+
+__device__ __forceinline__ void rc_load_heads(const RcPlan& pl, int r0,
+                                              int& hp, int& hs) {
+  const int tid = threadIdx.x;
+  hp = pl.ptr[min(r0 + min(tid, kRcRows), pl.N)];
+  hs = pl.split[min(r0 + min(tid, kRcRows - 1), pl.N - 1)];
+}
 
 template <bool WEIGHTED>
 __device__ __forceinline__ void rc_stage_lists(const RcPlan& pl, int r0,
-                                               const RcTileLists& s) {
+                                               const RcTileLists& s, int hp,
+                                               int hs) {
+  static_assert(kRcCap == 4 * 256, "four entries per thread");
   const int tid = threadIdx.x;
-  if (tid <= kRcRows) s.ptr[tid] = pl.ptr[min(r0 + tid, pl.N)];
-  if (tid < kRcRows) {
-    const int r = r0 + tid;
-    s.split[tid] = r < pl.N ? pl.split[r] : 0;
-    s.hub[tid] = r < pl.N ? (int)pl.hub[r] : 0;
-  }
+  if (tid <= kRcRows) s.ptr[tid] = hp;
+  if (tid < kRcRows) s.split[tid] = r0 + tid < pl.N ? hs : hp;
   __syncthreads();
+  if (tid < 2 * kRcRows) {
+    const int lr = tid >> 1;
+    const int b = (tid & 1) ? s.split[lr] : s.ptr[lr];
+    const int e = (tid & 1) ? s.ptr[lr + 1] : s.split[lr];
+    s.inv[tid] = 1.f / (float)max(e - b, 1);
+  }
   const int e0 = s.ptr[0], n = min(s.ptr[kRcRows] - e0, kRcCap);
-  for (int t = tid; t < n; t += 256) {
-    s.col[t] = pl.col[e0 + t];
-    if (WEIGHTED) s.w[t] = pl.w[e0 + t];
+  int cv[4];
+  float wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {      // (the lists end with a dummy entry)
+    const int t = e0 + max(min(tid + 256 * u, n - 1), 0);
+    cv[u] = pl.col[t];
+    wv[u] = WEIGHTED ? pl.w[t] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = tid + 256 * u;
+    if (t < n) {
+      s.col[t] = cv[u];
+      if (WEIGHTED) s.w[t] = wv[u];
+    }
   }
   __syncthreads();
-}
-
-// Entry e (absolute) of the tile: from LDS, or global past the cap.
-template <bool WEIGHTED>
-__device__ __forceinline__ void rc_entry(const RcPlan& pl,
-                                         const RcTileLists& s, int e0, int e,
-                                         int& j, float& w) {
-  const int rel = e - e0;
-  if (rel < kRcCap) {
-    j = s.col[rel];
-    if (WEIGHTED) w = s.w[rel];
-  } else {
-    j = pl.col[e];
-    if (WEIGHTED) w = pl.w[e];
-  }
 }
 
 // Balanced (merge-path) gather of the tile's 128 segments (row lr, list
 // l: segment 2 lr + l): the tile's contiguous entry range is cut into 32
 // equal chunks, one per lane group (8 lanes, lane q holds channels
-// 4q..4q+3); a group walks its chunk in order with 8 loads in flight per
+// 4q..4q+3); a group walks its chunk in order with kRcU loads in flight per
 // lane and writes every segment that starts and ends inside it straight
 // to sA (MEAN: divided by the segment's entry count), while the partial
 // sums of segments crossing a chunk border go to LDS and are added in
@@ -183,9 +226,9 @@ __device__ __forceinline__ void rc_entry(const RcPlan& pl,
 // entities) are spread over several groups; no group walks more than
 // ceil(n / 32) entries.  Empty segments keep the zeros written up front.
 struct RcFlat {
-  float* P;    // [32][2][32] border partials: slot 0 head, slot 1 tail
-  int* PS;     // [32][2] their segments (-1: none)
-  int* PO;     // [32] 1: the tail segment started in this chunk (owner)
+  DGMC_LDS float* P;    // [32][2][32] border partials: slot 0 head, slot 1 tail
+  DGMC_LDS int* PS;     // [32][2] their segments (-1: none)
+  DGMC_LDS int* PO;     // [32] 1: the tail segment started in this chunk (owner)
 };
 
 __device__ __forceinline__ int rc_seg_end(const RcTileLists& s, int seg) {
@@ -195,10 +238,90 @@ __device__ __forceinline__ int rc_seg_begin(const RcTileLists& s, int seg) {
   return (seg & 1) ? s.split[seg >> 1] : s.ptr[seg >> 1];
 }
 
-template <bool WEIGHTED, bool MEAN>
+// First segment whose end is past e (segment ends are non-decreasing):
+// the non-empty segment holding entry e; 7 unrolled, branch-free steps.
+__device__ __forceinline__ int rc_seg_of(const RcTileLists& s, int e) {
+  int lo = 0;
+#pragma unroll
+  for (int st = kRcRows; st > 0; st >>= 1)
+    lo += rc_seg_end(s, lo + st - 1) <= e ? st : 0;
+  return lo;
+}
+
+// One 8-lane group's walk over its chunk [c0, c1): running segment `seg`
+// (started inside the chunk or not), its partial sum `acc`.
+template <bool WEIGHTED, bool MEAN, bool TWO>
+struct RcWalk {
+  const RcPlan& pl;
+  const RcTileLists& s;
+  const RcRows& src;
+  DGMC_LDS float* sA;
+  int pitch;
+  const RcFlat& fl;
+  int q, g, E0, c1;
+  bool fits;
+  int seg;
+  bool started;
+  float4 acc;
+
+  __device__ __forceinline__ const float* row(int j) const {
+    return TWO ? src.row(j) : src.a + (unsigned)(j * src.lda);
+  }
+  // The finished segment: its sum (MEAN: scaled by 1 / count) into the
+  // tile, or - it began in an earlier chunk - the head partial.  (One code
+  // path; divergent groups of a wave flush in the same instructions.)
+  __device__ __forceinline__ void flush() {
+    const float sc = (MEAN && started) ? s.inv[seg] : 1.f;
+    DGMC_LDS float* p = started ? sA + (seg >> 1) * pitch + (seg & 1) * kRcK + 4 * q
+                       : fl.P + (2 * g) * kRcK + 4 * q;
+    lds_put4(p, f4_scale(acc, sc));
+    if (!started && q == 0) fl.PS[2 * g] = seg;
+  }
+  // U entries from e0 (FULL: all before c1), U loads in flight per lane.
+  template <int U, bool FULL>
+  __device__ __forceinline__ void batch(int e0) {
+    int pk[U];
+    float wt[U];
+    if (fits) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = (FULL ? e0 + u : min(e0 + u, c1 - 1)) - E0;
+        pk[u] = s.col[e];
+        wt[u] = WEIGHTED ? s.w[e] : 1.f;
+      }
+    } else {                         // > kRcCap entries: lists from global
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = FULL ? e0 + u : min(e0 + u, c1 - 1);
+        pk[u] = pl.col[e];
+        wt[u] = WEIGHTED ? pl.w[e] : 1.f;
+      }
+    }
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = f4_ld(row(pk[u] & kRcColMask) + 4 * q);
+    // Entries past c1 (clamped duplicates) add 0 and keep the segment; a
+    // segment change (the packed tile segment of the entry - empty segments
+    // never appear and keep their zeros) flushes the running sum.
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool live = FULL || e0 + u < c1;
+      const int sg = live ? (pk[u] >> 24) : seg;
+      if (sg != seg) {
+        flush();
+        acc = f4_zero();
+        seg = sg;
+        started = true;
+      }
+      f4_fma(acc, live ? wt[u] : 0.f, v[u]);     // (fma by 1: exact add)
+    }
+  }
+};
+
+template <bool WEIGHTED, bool MEAN, bool TWO, int U>
 __device__ __forceinline__ void rc_gather_flat(const RcPlan& pl,
                                                const RcTileLists& s,
-                                               const RcRows& src, float* sA,
+                                               const RcRows& src, DGMC_LDS float* sA,
                                                int pitch, const RcFlat& fl) {
   const int tid = threadIdx.x, q = tid & 7, g = tid >> 3;   // 32 groups
   const int E0 = s.ptr[0], E1 = s.ptr[kRcRows];
@@ -210,77 +333,23 @@ __device__ __forceinline__ void rc_gather_flat(const RcPlan& pl,
     fl.PS[2 * g + 1] = -1;
     fl.PO[g] = 0;
   }
-  auto put = [&](int seg, const float4& acc) {
-    float4 v = acc;
-    if (MEAN) {
-      const float cnt =
-          (float)max(rc_seg_end(s, seg) - rc_seg_begin(s, seg), 1);
-      v = f4_div(acc, cnt);
-    }
-    lds_put4(sA + (seg >> 1) * pitch + (seg & 1) * kRcK + 4 * q, v);
-  };
   if (c0 < c1) {
-    // first segment whose end is past c0 (segment ends are non-decreasing)
-    int lo = 0, hi = 2 * kRcRows - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (rc_seg_end(s, mid) > c0) hi = mid; else lo = mid + 1;
-    }
-    int seg = lo;
-    int send = rc_seg_end(s, seg);
-    bool started = rc_seg_begin(s, seg) >= c0;
-    float4 acc = f4_zero();
-    for (int e0 = c0; e0 < c1; e0 += 8) {
-      int j[8];
-      float wt[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        j[u] = 0;
-        wt[u] = 0.f;
-        if (e0 + u < c1) rc_entry<WEIGHTED>(pl, s, E0, e0 + u, j[u], wt[u]);
-      }
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        v[u] = e0 + u < c1 ? f4_ld(src.row(j[u]) + 4 * q) : f4_zero();
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u;
-        if (e >= c1) break;
-        while (e >= send) {            // segment(s) ending before e
-          if (started) {
-            put(seg, acc);
-          } else {
-            float* p = fl.P + (2 * g) * kRcK + 4 * q;   // head partial
-            p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
-            if (q == 0) fl.PS[2 * g] = seg;
-          }
-          acc = f4_zero();
-          ++seg;
-          send = rc_seg_end(s, seg);
-          started = true;
-        }
-        if (WEIGHTED)
-          f4_fma(acc, wt[u], v[u]);
-        else
-          f4_add(acc, v[u]);
-      }
-    }
+    const int seg = rc_seg_of(s, c0);
+    RcWalk<WEIGHTED, MEAN, TWO> w{pl, s, src, sA, pitch, fl, q, g, E0, c1,
+                                  n <= kRcCap, seg,
+                                  rc_seg_begin(s, seg) >= c0, f4_zero()};
+    int e0 = c0;
+    for (; e0 + U <= c1; e0 += U) w.template batch<U, true>(e0);
+    for (; e0 < c1; e0 += U / 2) w.template batch<U / 2, false>(e0);
     // the segment current at c1
-    if (send <= c1) {
-      if (started) {
-        put(seg, acc);
-      } else {
-        float* p = fl.P + (2 * g) * kRcK + 4 * q;
-        p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
-        if (q == 0) fl.PS[2 * g] = seg;
-      }
+    if (rc_seg_end(s, w.seg) <= c1) {
+      w.flush();
     } else {
-      float* p = fl.P + (2 * g + 1) * kRcK + 4 * q;     // tail partial
-      p[0] = acc.x; p[1] = acc.y; p[2] = acc.z; p[3] = acc.w;
+      DGMC_LDS float* p = fl.P + (2 * g + 1) * kRcK + 4 * q;     // tail partial
+      lds_put4(p, w.acc);
       if (q == 0) {
-        fl.PS[2 * g + 1] = seg;
-        fl.PO[g] = started ? 1 : 0;
+        fl.PS[2 * g + 1] = w.seg;
+        fl.PO[g] = w.started ? 1 : 0;
       }
     }
   }
@@ -288,29 +357,52 @@ __device__ __forceinline__ void rc_gather_flat(const RcPlan& pl,
   // owners complete their border segments in chunk order
   if (fl.PO[g]) {
     const int seg = fl.PS[2 * g + 1];
-    float4 acc = f4_ld(fl.P + (2 * g + 1) * kRcK + 4 * q);
+    float4 acc = lds_get4(fl.P + (2 * g + 1) * kRcK + 4 * q);
     int h = g + 1;
     for (; h < 32 && fl.PS[2 * h + 1] == seg && fl.PO[h] == 0; ++h)
-      f4_add(acc, f4_ld(fl.P + (2 * h + 1) * kRcK + 4 * q));
+      f4_add(acc, lds_get4(fl.P + (2 * h + 1) * kRcK + 4 * q));
     if (h < 32 && fl.PS[2 * h] == seg)
-      f4_add(acc, f4_ld(fl.P + (2 * h) * kRcK + 4 * q));
-    put(seg, acc);
+      f4_add(acc, lds_get4(fl.P + (2 * h) * kRcK + 4 * q));
+    const float4 v = MEAN ? f4_scale(acc, s.inv[seg]) : acc;
+    lds_put4(sA + (seg >> 1) * pitch + (seg & 1) * kRcK + 4 * q, v);
   }
 }
 
-// Stage the three [C][K] weights.  FWD: sW[c][s * K + k] = W_s[c][k]
-// (pitch kRcP); else (backward) sW[k][s * C + c] = W_s[c][k].
+// The three [C][K] weights: loaded into registers with the other
+// independent loads (rc_load_w), stored afterwards (rc_store_w).  FWD:
+// sW[c][s * K + k] = W_s[c][k] (pitch kRcP); else (backward)
+// sW[k][s * C + c] = W_s[c][k].
+__device__ __forceinline__ void rc_load_w(const float* const w[3],
+                                          float4 (&v)[3]) {
+  static_assert(kRcC * kRcK == 4 * 256, "one vector per thread and weight");
+#pragma unroll
+  for (int u = 0; u < 3; ++u) v[u] = f4_ld(w[u] + 4 * threadIdx.x);
+}
+
 template <bool FWD>
-__device__ __forceinline__ void rc_stage_w(const float* const w[3],
-                                           float* sW) {
-  for (int t = threadIdx.x; t < 3 * kRcC * kRcK; t += blockDim.x) {
-    const int s = t / (kRcC * kRcK), r = t % (kRcC * kRcK);
-    const int c = r / kRcK, k = r % kRcK;
-    const float v = w[s][r];
-    if (FWD)
-      sW[c * kRcP + s * kRcK + k] = v;
-    else
-      sW[k * kRcP + s * kRcC + c] = v;
+__device__ __forceinline__ void rc_store_w(const float4 (&v)[3], DGMC_LDS float* sW) {
+  const int r = 4 * threadIdx.x, c = r / kRcK, k = r % kRcK;
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    if (FWD) {
+      lds_put4(sW + c * kRcP + u * kRcK + k, v[u]);
+    } else {
+      DGMC_LDS float* p = sW + k * kRcP + u * kRcC + c;
+      p[0] = v[u].x;
+      p[kRcP] = v[u].y;
+      p[2 * kRcP] = v[u].z;
+      p[3 * kRcP] = v[u].w;
+    }
+  }
+}
+
+// zero the first `vecs` 4-float vectors of each of the 64 rows of an LDS tile
+template <int VECS>
+__device__ __forceinline__ void rc_zero_rows(DGMC_LDS float* sA, int pitch) {
+#pragma unroll
+  for (int u = 0; u < kRcRows * VECS / 256; ++u) {
+    const int t = threadIdx.x + 256 * u;
+    lds_put4(sA + (t / VECS) * pitch + (t % VECS) * 4, f4_zero());
   }
 }
 
@@ -318,42 +410,55 @@ __device__ __forceinline__ void rc_stage_w(const float* const w[3],
 // Forward.  LDS: sA [64][kRcP] (PROJ: sF [64][kRcFP]), sW [32][kRcP] (PROJ:
 // then the fold [32][kRcFP]), lists.
 // ---------------------------------------------------------------------------
-constexpr int kRcListLds = (kRcRows + 1 + 2 * kRcRows + kRcCap) * 4 +
+constexpr int kRcListLds = kRcListInts * 4 +
                            (64 * kRcK + 64 + 32) * 4;   // + RcFlat
 constexpr int kRcFwdLds = (kRcRows * kRcP + kRcC * kRcP) * 4 + kRcListLds;
 constexpr int kRcFwdProjLds =
     (kRcRows * kRcFP + 32 * kRcFP) * 4 + kRcListLds;
 
-template <bool PROJ>
+template <bool PROJ, bool TWO>
 __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
                                                           RcFwd a) {
   extern __shared__ __attribute__((aligned(16))) float rc_smem[];
-  float* sA = rc_smem;                            // [64][kRcP] / [64][kRcFP]
-  float* sW = sA + kRcRows * (PROJ ? kRcFP : kRcP);
-  int* lists = reinterpret_cast<int*>(sW + (PROJ ? 32 * kRcFP : kRcC * kRcP));
-  const RcTileLists s{lists, lists + kRcRows + 1, lists + 2 * kRcRows + 1,
-                      lists + 3 * kRcRows + 1, nullptr};
-  float* flp = reinterpret_cast<float*>(lists + 3 * kRcRows + 1 + kRcCap);
-  const RcFlat fl{flp, reinterpret_cast<int*>(flp + 64 * kRcK),
-                  reinterpret_cast<int*>(flp + 64 * kRcK) + 64};
+  DGMC_LDS float* sA = (DGMC_LDS float*)rc_smem;                            // [64][kRcP] / [64][kRcFP]
+  DGMC_LDS float* sW = sA + kRcRows * (PROJ ? kRcFP : kRcP);
+  DGMC_LDS int* lists = reinterpret_cast<DGMC_LDS int*>(sW + (PROJ ? 32 * kRcFP : kRcC * kRcP));
+  const RcTileLists s = rc_lists(lists, nullptr);
+  DGMC_LDS float* flp = reinterpret_cast<DGMC_LDS float*>(lists + kRcListInts);
+  const RcFlat fl{flp, reinterpret_cast<DGMC_LDS int*>(flp + 64 * kRcK),
+                  reinterpret_cast<DGMC_LDS int*>(flp + 64 * kRcK) + 64};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * kRcRows;
   const int q = lane & 7, grp = lane >> 3;
   const int la = wave * 16 + grp, lb = la + 8;
   const int ra = r0 + la, rb = r0 + lb;
-  // self rows first (independent of the lists)
-  const float4 xa = ra < pl.N ? f4_ld(a.x.row(ra) + 4 * q) : f4_zero();
-  const float4 xb = rb < pl.N ? f4_ld(a.x.row(rb) + 4 * q) : f4_zero();
-  rc_stage_w<true>(a.w, sW);
-  {
-    const int P = PROJ ? kRcFP : kRcP;
-    for (int t = tid; t < kRcRows * 16; t += 256)       // mean parts := 0
-      lds_put4(sA + (t >> 4) * P + (t & 15) * 4, f4_zero());
+  // round 1: every load that does not depend on the lists
+  const int rl = pl.N - 1;
+  const float4 xa = f4_keep(ra < pl.N, f4_ld(a.x.row(min(ra, rl)) + 4 * q));
+  const float4 xb = f4_keep(rb < pl.N, f4_ld(a.x.row(min(rb, rl)) + 4 * q));
+  float4 wv[3];
+  rc_load_w(a.w, wv);
+  int hp, hs;
+  rc_load_heads(pl, r0, hp, hs);
+  float4 fr[6], fo[4];     // PROJ: this lane's share of feat[:, 0:96], fold
+  if (PROJ) {
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int t = lane + 64 * u;            // 16 rows x 24 vectors
+      const int r = r0 + wave * 16 + t / 24;
+      fr[u] = f4_keep(r < pl.N, f4_ld(a.feat + (size_t)min(r, rl) * a.ldf +
+                                      (t % 24) * 4));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) fo[u] = f4_ld(a.fold + 4 * (tid + 256 * u));
   }
-  rc_stage_lists<false>(pl, r0, s);
+  rc_store_w<true>(wv, sW);
+  rc_zero_rows<16>(sA, PROJ ? kRcFP : kRcP);       // mean parts := 0
+  rc_stage_lists<false>(pl, r0, s, hp, hs);
   {
     const int P = PROJ ? kRcFP : kRcP;
-    rc_gather_flat<false, true>(pl, s, a.x, sA, P, fl);
+    rc_gather_flat<false, true, TWO, PROJ ? 8 : kRcU>(pl, s, a.x, sA, P,
+                                                            fl);
     lds_put4(sA + la * P + 2 * kRcK + 4 * q, xa);
     lds_put4(sA + lb * P + 2 * kRcK + 4 * q, xb);
     if (a.xcopy) {
@@ -368,7 +473,7 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
   const int i = lane & 15, kk = lane >> 4;
   const int P = PROJ ? kRcFP : kRcP;
   rc_f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-  const float* arow = sA + (wave * 16 + i) * P + kk;
+  const DGMC_LDS float* arow = sA + (wave * 16 + i) * P + kk;
 #pragma unroll 8
   for (int k0 = 0; k0 < 3 * kRcK; k0 += 4) {
     const float av = arow[k0];
@@ -377,20 +482,15 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
     o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(
         av, sW[(16 + i) * kRcP + k0 + kk], o1, 0, 0, 0);
   }
-  float4 fr[6];            // PROJ: this lane's share of feat[:, 0:96]
   if (PROJ) {
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int t = lane + 64 * u;            // 16 rows x 24 vectors
-      const int r = r0 + wave * 16 + t / 24;
-      fr[u] = r < pl.N ? f4_ld(a.feat + (size_t)r * a.ldf + (t % 24) * 4)
-                       : f4_zero();
-    }
     __syncthreads();        // sA / sW are reused below
-    for (int t = tid; t < 32 * 128; t += 256)
-      sW[(t >> 7) * kRcFP + (t & 127)] = a.fold[t];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = 4 * (tid + 256 * u);
+      lds_put4(sW + (t >> 7) * kRcFP + (t & 127), fo[u]);
+    }
   }
-  float* sF = sA;
+  DGMC_LDS float* sF = sA;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int c = 16 * h + i;
@@ -409,13 +509,13 @@ __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     const int t = lane + 64 * u;
-    float* p = sF + (wave * 16 + t / 24) * kRcFP + (t % 24) * 4;
+    DGMC_LDS float* p = sF + (wave * 16 + t / 24) * kRcFP + (t % 24) * 4;
     p[0] = fr[u].x; p[1] = fr[u].y; p[2] = fr[u].z; p[3] = fr[u].w;
   }
   __syncthreads();
   // pq[16 rows][32] = [feat[:, 0:96] | out] fold^T
   rc_f32x4 p0 = {0.f, 0.f, 0.f, 0.f}, p1 = {0.f, 0.f, 0.f, 0.f};
-  const float* frow = sF + (wave * 16 + i) * kRcFP + kk;
+  const DGMC_LDS float* frow = sF + (wave * 16 + i) * kRcFP + kk;
 #pragma unroll 8
   for (int k0 = 0; k0 < 128; k0 += 4) {
     const float av = frow[k0];
@@ -444,16 +544,15 @@ constexpr int kRcBwdLds =
 __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
                                                           RcBwd a) {
   extern __shared__ __attribute__((aligned(16))) float rc_smem[];
-  float* sG = rc_smem;                       // [64][kRcP]
-  float* sW = sG + kRcRows * kRcP;           // [32 k][kRcP] (3C wide)
-  float* sX = sW + kRcK * kRcP;              // [64][kRcXP]
-  float* sWt = sX + kRcRows * kRcXP;         // [kRcCap] entry weights
-  int* lists = reinterpret_cast<int*>(sWt + kRcCap);
-  const RcTileLists s{lists, lists + kRcRows + 1, lists + 2 * kRcRows + 1,
-                      lists + 3 * kRcRows + 1, sWt};
-  float* flp = reinterpret_cast<float*>(lists + 3 * kRcRows + 1 + kRcCap);
-  const RcFlat fl{flp, reinterpret_cast<int*>(flp + 64 * kRcK),
-                  reinterpret_cast<int*>(flp + 64 * kRcK) + 64};
+  DGMC_LDS float* sG = (DGMC_LDS float*)rc_smem;                       // [64][kRcP]
+  DGMC_LDS float* sW = sG + kRcRows * kRcP;           // [32 k][kRcP] (3C wide)
+  DGMC_LDS float* sX = sW + kRcK * kRcP;              // [64][kRcXP]
+  DGMC_LDS float* sWt = sX + kRcRows * kRcXP;         // [kRcCap] entry weights
+  DGMC_LDS int* lists = reinterpret_cast<DGMC_LDS int*>(sWt + kRcCap);
+  const RcTileLists s = rc_lists(lists, sWt);
+  DGMC_LDS float* flp = reinterpret_cast<DGMC_LDS float*>(lists + kRcListInts);
+  const RcFlat fl{flp, reinterpret_cast<DGMC_LDS int*>(flp + 64 * kRcK),
+                  reinterpret_cast<DGMC_LDS int*>(flp + 64 * kRcK) + 64};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool pacc = a.part_acc != 0;
   const int r0 = blockIdx.x * kRcRows;
@@ -463,33 +562,38 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
 #pragma unroll
   for (int u = 0; u < kRcPartPer; ++u) {
     const int t = tid + 256 * u;
-    old[u] = (pacc && t < kRcPart) ? part[t] : 0.f;
+    const float v = part[min(t, kRcPart - 1)];
+    old[u] = (pacc && t < kRcPart) ? v : 0.f;
   }
   const int q = lane & 7, grp = lane >> 3;
   const int la = wave * 16 + grp, lb = la + 8;
   const int ra = r0 + la, rb = r0 + lb;
-  const float4 ga = ra < pl.N ? f4_ld(a.g + (size_t)ra * a.ldg + 4 * q)
-                              : f4_zero();
-  const float4 gb = rb < pl.N ? f4_ld(a.g + (size_t)rb * a.ldg + 4 * q)
-                              : f4_zero();
-  const float4 xa = ra < pl.N ? f4_ld(a.x.row(ra) + 4 * q) : f4_zero();
-  const float4 xb = rb < pl.N ? f4_ld(a.x.row(rb) + 4 * q) : f4_zero();
-  rc_stage_w<false>(a.w, sW);
-  for (int t = tid; t < kRcRows * 16; t += 256)         // t_in / t_out := 0
-    lds_put4(sG + (t >> 4) * kRcP + (t & 15) * 4, f4_zero());
-  rc_stage_lists<true>(pl, r0, s);
+  const int rl = pl.N - 1;
+  const float4 ga = f4_keep(
+      ra < pl.N, f4_ld(a.g + (size_t)min(ra, rl) * a.ldg + 4 * q));
+  const float4 gb = f4_keep(
+      rb < pl.N, f4_ld(a.g + (size_t)min(rb, rl) * a.ldg + 4 * q));
+  const float4 xa = f4_keep(ra < pl.N, f4_ld(a.x.row(min(ra, rl)) + 4 * q));
+  const float4 xb = f4_keep(rb < pl.N, f4_ld(a.x.row(min(rb, rl)) + 4 * q));
+  float4 wv[3];
+  rc_load_w(a.w, wv);
+  int hp, hs;
+  rc_load_heads(pl, r0, hp, hs);
+  rc_store_w<false>(wv, sW);
+  rc_zero_rows<16>(sG, kRcP);                            // t_in / t_out := 0
+  rc_stage_lists<true>(pl, r0, s, hp, hs);
   const RcRows gsrc{a.g, a.g, 0, a.ldg, a.ldg};
-  rc_gather_flat<true, false>(pl, s, gsrc, sG, kRcP, fl);
+  rc_gather_flat<true, false, false, 12>(pl, s, gsrc, sG, kRcP, fl);
   lds_put4(sG + la * kRcP + 2 * kRcC + 4 * q, ga);
   lds_put4(sG + lb * kRcP + 2 * kRcC + 4 * q, gb);
-  *reinterpret_cast<float4*>(sX + la * kRcXP + 4 * q) = xa;
-  *reinterpret_cast<float4*>(sX + lb * kRcXP + 4 * q) = xb;
+  lds_put4a(sX + la * kRcXP + 4 * q, xa);
+  lds_put4a(sX + lb * kRcXP + 4 * q, xb);
   __syncthreads();
   const int i = lane & 15, kk = lane >> 4;
   // dx[16 rows][32] = G W_stack
   {
     rc_f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};
-    const float* grow = sG + (wave * 16 + i) * kRcP + kk;
+    const DGMC_LDS float* grow = sG + (wave * 16 + i) * kRcP + kk;
 #pragma unroll 8
     for (int k0 = 0; k0 < 3 * kRcC; k0 += 4) {
       const float av = grow[k0];
@@ -498,16 +602,16 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
       o1 = __builtin_amdgcn_mfma_f32_16x16x4f32(
           av, sW[(16 + i) * kRcP + k0 + kk], o1, 0, 0, 0);
     }
-    float dv[2][4];
+    float dv[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if (a.dadd) {                                  // (uniform)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int r = r0 + wave * 16 + kk * 4 + rr;
-        dv[h][rr] = (a.dadd && r < pl.N)
-                        ? a.dadd[(size_t)r * a.ldadd + 16 * h + i]
-                        : 0.f;
-      }
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = min(r0 + wave * 16 + kk * 4 + rr, rl);
+          dv[h][rr] = a.dadd[(size_t)r * a.ldadd + 16 * h + i];
+        }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = 16 * h + i;
@@ -543,7 +647,7 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
   if (tid < kRcC)
     for (int j = 0; j < kRcRows; ++j) dbias += sG[j * kRcP + 2 * kRcC + tid];
   __syncthreads();
-  float* sP = sG;                           // [kRcPart] staging
+  DGMC_LDS float* sP = sG;                           // [kRcPart] staging
 #pragma unroll
   for (int bb = 0; bb < 3; ++bb) {
     const int blk = 3 * wave + bb, mb = blk >> 1, nb = blk & 1;
@@ -563,63 +667,64 @@ __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
 // ---------------------------------------------------------------------------
 // Projection backward: dfeat = dPQ fold (the last 32 columns masked by
 // feat > 0: they are the last layer's g'), dfold partial += dPQ^T feat.
-// LDS: sD [64][kRcDP], sFo [128 k][kRcDP] (fold^T), sF [64][kRcFT].
+// LDS: sD [64][kRcDP], sFo [32][kRcFT] (fold), sF [64][kRcFT].
 // ---------------------------------------------------------------------------
 constexpr int kRcPbLds =
-    (kRcRows * kRcDP + 128 * kRcDP + kRcRows * kRcFT) * 4;
+    (kRcRows * kRcDP + 32 * kRcFT + kRcRows * kRcFT) * 4;
 
 __global__ __launch_bounds__(256) void rel_proj_bwd_kernel(
     const float* __restrict__ dpq, const float* __restrict__ feat, int ldf,
     const float* __restrict__ fold, float* __restrict__ dfeat, int lddf,
     float* __restrict__ part, int part_acc, int N) {
   extern __shared__ __attribute__((aligned(16))) float rc_smem[];
-  float* sD = rc_smem;
-  float* sFo = sD + kRcRows * kRcDP;
-  float* sF = sFo + 128 * kRcDP;
+  DGMC_LDS float* sD = (DGMC_LDS float*)rc_smem;
+  DGMC_LDS float* sFo = sD + kRcRows * kRcDP;
+  DGMC_LDS float* sF = sFo + 32 * kRcFT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * kRcRows;
   float* pp = part + (size_t)blockIdx.x * (32 * 128);
   float old[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) old[u] = part_acc ? pp[tid + 256 * u] : 0.f;
+  for (int u = 0; u < 16; ++u) {
+    const float v = pp[tid + 256 * u];
+    old[u] = part_acc ? v : 0.f;
+  }
   float4 dv[2], fv[8], wv[4];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = tid + 256 * u, r = r0 + (t >> 3);
-    dv[u] = r < N ? f4_ld(dpq + (size_t)r * 32 + (t & 7) * 4) : f4_zero();
+    dv[u] = f4_keep(r < N,
+                    f4_ld(dpq + (size_t)min(r, N - 1) * 32 + (t & 7) * 4));
   }
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int t = tid + 256 * u, r = r0 + (t >> 5);
-    fv[u] = r < N ? f4_ld(feat + (size_t)r * ldf + (t & 31) * 4) : f4_zero();
+    fv[u] = f4_keep(r < N,
+                    f4_ld(feat + (size_t)min(r, N - 1) * ldf + (t & 31) * 4));
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) wv[u] = f4_ld(fold + 4 * (tid + 256 * u));
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int t = tid + 256 * u;
-    float* p = sD + (t >> 3) * kRcDP + (t & 7) * 4;
+    DGMC_LDS float* p = sD + (t >> 3) * kRcDP + (t & 7) * 4;
     p[0] = dv[u].x; p[1] = dv[u].y; p[2] = dv[u].z; p[3] = dv[u].w;
   }
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int t = tid + 256 * u;
-    *reinterpret_cast<float4*>(sF + (t >> 5) * kRcFT + (t & 31) * 4) = fv[u];
+    lds_put4a(sF + (t >> 5) * kRcFT + (t & 31) * 4, fv[u]);
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int t = 4 * (tid + 256 * u);       // fold[c'][k .. k + 3]
-    const int c = t >> 7, k = t & 127;
-    sFo[k * kRcDP + c] = wv[u].x;
-    sFo[(k + 1) * kRcDP + c] = wv[u].y;
-    sFo[(k + 2) * kRcDP + c] = wv[u].z;
-    sFo[(k + 3) * kRcDP + c] = wv[u].w;
+    lds_put4a(sFo + (t >> 7) * kRcFT + (t & 127), wv[u]);
   }
   __syncthreads();
   const int i = lane & 15, kk = lane >> 4;
   // dfeat[16 rows of wave][128] = dPQ fold: 8 column blocks, K = 32
   {
-    const float* drow = sD + (wave * 16 + i) * kRcDP + kk;
+    const DGMC_LDS float* drow = sD + (wave * 16 + i) * kRcDP + kk;
     float a8[8];
 #pragma unroll
     for (int s = 0; s < 8; ++s) a8[s] = drow[4 * s];
@@ -629,7 +734,7 @@ __global__ __launch_bounds__(256) void rel_proj_bwd_kernel(
 #pragma unroll
       for (int s = 0; s < 8; ++s)
         o = __builtin_amdgcn_mfma_f32_16x16x4f32(
-            a8[s], sFo[(nb * 16 + i) * kRcDP + 4 * s + kk], o, 0, 0, 0);
+            a8[s], sFo[(4 * s + kk) * kRcFT + nb * 16 + i], o, 0, 0, 0);
       const int c = nb * 16 + i;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -653,7 +758,7 @@ __global__ __launch_bounds__(256) void rel_proj_bwd_kernel(
           sF[(j0 + kk) * kRcFT + nb * 16 + i], d[bb], 0, 0, 0);
   }
   __syncthreads();
-  float* sP = sF;                           // [32][128] staging
+  DGMC_LDS float* sP = sF;                           // [32][128] staging
 #pragma unroll
   for (int bb = 0; bb < 4; ++bb) {
     const int blk = 4 * wave + bb, mb = blk >> 3, nb = blk & 7;
@@ -712,6 +817,7 @@ __global__ __launch_bounds__(256) void fold_weights_bwd_kernel(
     if (t >= R * Kin) return;
     const int r = t / Kin, m = t % Kin;
     float s = 0.f;
+#pragma unroll 8
     for (int k = 0; k < K; k += 4) {
       const float4 a = f4_ld(g + (size_t)r * K + k);
       const float4 b = f4_ld(wf + (size_t)m * K + k);
@@ -725,6 +831,7 @@ __global__ __launch_bounds__(256) void fold_weights_bwd_kernel(
   if (t >= Kin * K) return;
   const int m = t / K, k = t % K;
   float s = 0.f;
+#pragma unroll 16
   for (int r = 0; r < R; ++r) s = fmaf(w1[r * Kin + m], g[(size_t)r * K + k], s);
   gwf[t] = s;
 }
@@ -742,6 +849,9 @@ RcPlan make_plan(const at::Tensor& ptr, const at::Tensor& col,
   for (const at::Tensor* t : {&ptr, &col, &split, &hub})
     TORCH_CHECK(t->is_cuda() && t->is_contiguous(), "rel plan: contiguous "
                 "device tensors");
+  TORCH_CHECK(N > 0 && N < (1 << 24) && col.numel() > 0,
+              "rel plan: 1 .. 2^24 - 1 rows and a trailing dummy list entry "
+              "(ops/relconv.py RelPlan)");
   const float* wp = nullptr;
   if (w.has_value() && w->defined()) {
     TORCH_CHECK(w->scalar_type() == at::kFloat && w->is_contiguous() &&
@@ -756,6 +866,8 @@ RcPlan make_plan(const at::Tensor& ptr, const at::Tensor& col,
 
 void check_rows(const at::Tensor& t, int64_t rows, int64_t cols,
                 const char* what) {
+  TORCH_CHECK(rows * std::max<int64_t>(t.stride(0), cols) < (int64_t(1) << 31),
+              what, ": rows * row stride must stay below 2^31");
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.dim() == 2 &&
                   t.size(0) == rows && t.size(1) == cols && t.stride(1) == 1 &&
                   t.stride(0) % 4 == 0 && aligned16(t.data_ptr()),
@@ -842,7 +954,11 @@ void relconv_fwd(const at::Tensor& ptr, const at::Tensor& col,
   }
   const int n_tiles = (int)((N + kRcRows - 1) / kRcRows);
   if (n_tiles == 0) return;
-  auto kern = proj ? relconv_fwd_kernel<true> : relconv_fwd_kernel<false>;
+  const bool two = xb.has_value() && xb->defined();   // [x_s; x_t] split
+  auto kern = proj ? (two ? relconv_fwd_kernel<true, true>
+                          : relconv_fwd_kernel<true, false>)
+                   : (two ? relconv_fwd_kernel<false, true>
+                          : relconv_fwd_kernel<false, false>);
   const int lds = proj ? kRcFwdProjLds : kRcFwdLds;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),

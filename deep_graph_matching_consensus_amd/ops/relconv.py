@@ -65,18 +65,31 @@ class RelPlan(object):
         cols_f = torch.cat([src, dst])
         perm = torch.argsort(rows_f, stable=True)
         self.col_f = cols_f[perm].int().contiguous()
+        seg_f = rows_f[perm] % (2 * ROWS)      # segment inside the row tile
         rows_b = torch.cat([src * 2, dst * 2 + 1])
         cols_b = torch.cat([dst, src])
         perm = torch.argsort(rows_b, stable=True)
         col_b = cols_b[perm]
+        seg_b = rows_b[perm] % (2 * ROWS)
         inv_in = 1.0 / deg_in.clamp(min=1).float()
         inv_out = 1.0 / deg_out.clamp(min=1).float()
         first = torch.cat([torch.ones(E, dtype=torch.bool, device=dev),
                            torch.zeros(E, dtype=torch.bool, device=dev)])
         # (list 0 of the backward: out-neighbours, weight 1 / deg_in)
-        self.w_b = torch.where(first[perm], inv_in[col_b],
-                               inv_out[col_b]).contiguous()
-        self.col_b = col_b.int().contiguous()
+        w_b = torch.where(first[perm], inv_in[col_b], inv_out[col_b])
+        # one trailing dummy entry: the kernels' clamped (branch-free) list
+        # loads stay in bounds for edgeless tiles and graphs
+        pad_i = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.col_f = torch.cat([self.col_f, pad_i])
+        self.col_b = torch.cat([col_b.int(), pad_i])
+        self.w_b = torch.cat([w_b, torch.zeros(1, device=dev)])
+        # kernel lists: column | tile segment (2 (row % 64) + list) << 24, so
+        # a gathering lane sees segment changes without a search
+        assert N < (1 << 24), 'RelPlan: at most 2^24 - 1 rows'
+        self.pk_f = torch.cat([(self.col_f[:-1].long() | (seg_f << 24)).int(),
+                               pad_i])
+        self.pk_b = torch.cat([(self.col_b[:-1].long() | (seg_b << 24)).int(),
+                               pad_i])
         self.ptr = ptr.int().contiguous()
         self.split_f = (ptr[:-1] + deg_in).int().contiguous()
         self.split_b = (ptr[:-1] + deg_out).int().contiguous()
@@ -84,10 +97,10 @@ class RelPlan(object):
         self.n_tiles = (N + ROWS - 1) // ROWS
 
     def fwd_args(self):
-        return (self.ptr, self.col_f, self.split_f, self.hub)
+        return (self.ptr, self.pk_f, self.split_f, self.hub)
 
     def bwd_args(self):
-        return (self.ptr, self.col_b, self.w_b, self.split_b, self.hub)
+        return (self.ptr, self.pk_b, self.w_b, self.split_b, self.hub)
 
 
 def rel_plan(edge_index, N):

@@ -46,6 +46,13 @@ def test_rel_plan_lists_and_hubs_cpu():
     assert torch.equal(p.w_b[s2:b], inv_out[src[dst == i]])
     hub = (deg_in + deg_out) > 8
     assert torch.equal(p.hub.bool(), hub) and int(hub.sum()) > 0
+    # packed kernel lists: column | (2 (row % 64) + list) << 24
+    for pk, col, split in ((p.pk_f, p.col_f, p.split_f),
+                           (p.pk_b, p.col_b, p.split_b)):
+        assert torch.equal(pk & ((1 << 24) - 1), col)
+        row = torch.repeat_interleave(torch.arange(N), deg_in + deg_out)
+        lst = (torch.arange(row.numel()) >= split.long()[row]).long()
+        assert torch.equal((pk[:-1] >> 24).long(), 2 * (row % 64) + lst)
 
 
 def _model(seed=0):

@@ -19,7 +19,8 @@ def main():
         name = r['Kernel_Name']
         if filt not in name:
             continue
-        key = (name.split('(')[0], r['Grid_Size'])
+        base = name.replace('(anonymous namespace)::', '')
+        key = (base.split('(')[0], r['Grid_Size'])
         sums[key][r['Counter_Name']] += float(r['Counter_Value'])
         disp[key].add(r['Dispatch_Id'])
     for key in sorted(sums):
