@@ -338,21 +338,29 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     for (int r = 0; r < 16; ++r) {
       if (!any) break;
       const float v = col_ok ? acc[r] : -INFINITY;
-      unsigned long long mask = __ballot(v > thr[r]);
-      while (mask) {
-        const int src = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const int sh = src & 32;
-        const float cv = lane_f(v, src);
-        if (!(cv > lane_f(thr[r], src))) continue;
-        const bool mine = hb == sh && hl < k;
-        const int pos = __popcll(__ballot(mine && lv[r] >= cv));
+      const unsigned long long mask = __ballot(v > thr[r]);
+      // One candidate of each half-wave per round (the halves hold
+      // different rows): max(hits_lo, hits_hi) rounds, not their sum.
+      unsigned lo = (unsigned)mask, hi = (unsigned)(mask >> 32);
+      while (lo | hi) {
+        const int slo = lo ? __builtin_ctz(lo) : 0;
+        const int shi = hi ? __builtin_ctz(hi) : 0;
+        const bool has = hb ? hi != 0u : lo != 0u;
+        lo &= lo - 1u;
+        hi &= hi - 1u;
+        const float cv0 = lane_f(v, slo), cv1 = lane_f(v, 32 + shi);
+        const float cv = hb ? cv1 : cv0;
+        const int src = hb ? shi : slo;
+        const bool mine = has && hl < k && cv > thr[r];
+        const unsigned long long bm = __ballot(mine && lv[r] >= cv);
+        const int pos =
+            hb ? __popc((unsigned)(bm >> 32)) : __popc((unsigned)bm);
         // shift the tail of the half's list down one lane (DPP wave_shr:1;
         // lane hl > pos >= 0 always reads a lane of its own half)
         const float pv = shr1(lv[r]);
         const int pi = shr1(li[r]);
         if (mine && hl > pos) { lv[r] = pv; li[r] = pi; }
-        if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + (src & 31); }
+        if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + src; }
         const float t_lo_half = lane_f(lv[r], k - 1);
         const float t_hi_half = lane_f(lv[r], 32 + k - 1);
         thr[r] = hb ? t_hi_half : t_lo_half;
