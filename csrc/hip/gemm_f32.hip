@@ -5,7 +5,7 @@
 //
 // The A operand is a list of fp32 row-major parts (any row stride, any
 // width that is a multiple of 4) - the concatenation is never formed.  Each
-// part is consumed in 128-wide chunks; a chunk's columns past the part's
+// part is consumed in 32-wide steps; a step's columns past the part's
 // width, and the matching Bt columns, read a zero page instead of memory,
 // so no part or weight needs padding (e.g. the 300-wide DBP15K features
 // and the 1068-wide [x | h1 | h2 | h3] of RelCNN's final Linear,
@@ -16,8 +16,9 @@
 // spline.py:53) - the fp32 node GEMMs that ran on hipBLASLt.
 //
 // Kernel: v_mfma_f32_32x32x2_f32 (a k-ordered fmaf chain - exact fp32),
-// 128x128 tiles of 4 waves (64x64 each) or 64x64 tiles for skinny outputs,
-// k consumed 32 at a time through two LDS stages filled by
+// 128x128, 128x64 or 64x64 tiles of 4 waves (picked for whole rounds of
+// tiles on the chip), k consumed in 32-wide steps (a part's last step only as
+// wide as needed) through two LDS stages filled by
 // global_load_lds_dwordx4 (XOR-swizzled [row][32] images read as
 // ds_read_b128, conflict-free), persistent grid of up to 2 workgroups per
 // CU walking tiles in an XCD-aware order.  Rows past M are clamped on load
@@ -31,18 +32,20 @@ namespace {
 typedef float gf_f32x16 __attribute__((ext_vector_type(16)));
 typedef float gf_f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGfBK = 32;           // k per staged chunk
-constexpr int kGfMaxChunks = 24;    // 128-wide chunks (K <= 3072)
+constexpr int kGfBK = 32;           // k per staged step
+constexpr int kGfMaxSteps = 96;     // 32-wide k steps (K <= 3072)
 
 // A zero page for the DMAs of columns past a part's width.
 __device__ __attribute__((aligned(16))) float g_gf_zero[4] = {0.f, 0.f, 0.f,
                                                              0.f};
 
-struct GfChunks {
-  const float* a[kGfMaxChunks];   // chunk start (part base + 128 j)
-  int lda[kGfMaxChunks];
-  int width[kGfMaxChunks];        // valid columns (<= 128)
-  int boff[kGfMaxChunks];         // first Bt column of the chunk
+// The k range as 32-wide steps over the parts (a part's last step may be
+// narrower: its missing columns read the zero page).
+struct GfSteps {
+  const float* a[kGfMaxSteps];    // step start (part base + 32 j)
+  int lda[kGfMaxSteps];
+  int width[kGfMaxSteps];         // valid columns (<= 32)
+  int boff[kGfMaxSteps];          // first Bt column of the step
   int n;
 };
 
@@ -63,7 +66,7 @@ __device__ __forceinline__ void gf_barrier() {
 
 template <int MB, int NB>
 __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
-    GfChunks A, int M, const float* __restrict__ bt, int ldb, int Nn,
+    GfSteps A, int M, const float* __restrict__ bt, int ldb, int Nn,
     const float* __restrict__ bias, int relu, float* __restrict__ Y,
     int ldy) {
   constexpr int TM = 64 * MB, TN = 64 * NB;
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
   DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
-  const int ntn = Nn / TN, nk = A.n * (128 / kGfBK);
+  const int ntn = Nn / TN, nk = A.n;
   const int U = ((M + TM - 1) / TM) * ntn;
   const int G = gridDim.x;
   int u = xcd_remap(blockIdx.x, G);
@@ -99,21 +102,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
   };
   const float* zero = g_gf_zero;
   auto stage = [&](int kc, DGMC_LDS float* da, DGMC_LDS float* db) {
-    const int c = kc >> 2;                 // 128-wide chunk
-    const int kp = (kc & 3) * kGfBK;       // offset inside it
-    const float* ap = A.a[c];
-    const int lda = A.lda[c], wid = A.width[c], bo = A.boff[c];
+    const float* ap = A.a[kc];
+    const int lda = A.lda[kc], wid = A.width[kc], bo = A.boff[kc];
 #pragma unroll
     for (int j = 0; j < 2 * MB; ++j) {
       const int row = 16 * MB * wave + 8 * j + prow;
-      const int k = kp + swz(row);
+      const int k = swz(row);
       gf_dma16(k < wid ? ap + (size_t)arow[j] * lda + k : zero,
                da + (16 * MB * wave + 8 * j) * kGfBK);
     }
 #pragma unroll
     for (int j = 0; j < 2 * NB; ++j) {
       const int row = 16 * NB * wave + 8 * j + prow;
-      const int k = kp + swz(row);
+      const int k = swz(row);
       gf_dma16(k < wid ? bt + (size_t)(brow0 + 8 * j) * ldb + bo + k : zero,
                db + (16 * NB * wave + 8 * j) * kGfBK);
     }
@@ -202,6 +203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
       // (this wave's 2 (MB + NB) pieces of the next chunk stay in flight)
       if constexpr (MB + NB == 4)
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr (MB + NB == 3)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
@@ -240,7 +243,7 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& out) {
   TORCH_CHECK(parts.size() >= 1, "gemm_nt_f32: at least one part");
   const int64_t M = parts[0].size(0);
-  GfChunks A{};
+  GfSteps A{};
   int64_t K = 0;
   for (const at::Tensor& p : parts) {
     TORCH_CHECK(p.is_cuda() && p.scalar_type() == at::kFloat &&
@@ -248,11 +251,11 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                     p.size(1) % 4 == 0 && p.stride(0) % 4 == 0 &&
                     aligned16(p.data_ptr()),
                 "gemm_nt_f32: parts fp32 [M, K_p % 4] with 16-byte rows");
-    for (int64_t c0 = 0; c0 < p.size(1); c0 += 128) {
-      TORCH_CHECK(A.n < kGfMaxChunks, "gemm_nt_f32: K too large");
+    for (int64_t c0 = 0; c0 < p.size(1); c0 += kGfBK) {
+      TORCH_CHECK(A.n < kGfMaxSteps, "gemm_nt_f32: K too large");
       A.a[A.n] = p.data_ptr<float>() + c0;
       A.lda[A.n] = (int)p.stride(0);
-      A.width[A.n] = (int)std::min<int64_t>(128, p.size(1) - c0);
+      A.width[A.n] = (int)std::min<int64_t>(kGfBK, p.size(1) - c0);
       A.boff[A.n] = (int)(K + c0);
       ++A.n;
     }
@@ -284,11 +287,32 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   }
   if (M == 0 || Nn == 0) return Y;
   const int cus = gf_num_cus(bt.device().index());
-  const int64_t big = ((M + 127) / 128) * (Nn / 128);
-  const bool small = big < cus || Nn % 128 != 0;
-  const int64_t tiles = small ? ((M + 63) / 64) * (Nn / 64) : big;
+  // Tile shape: the fewest tile-time units on 2 blocks per CU - whole
+  // rounds of 2 * CUs tiles, each costing its MFMA work with the smaller
+  // tiles' lower operand reuse (measured ~1.12x / ~1.3x per MAC).
+  struct Cfg { int mb, nb; double eff; };
+  const Cfg cfgs[3] = {{2, 2, 1.0}, {2, 1, 1.12}, {1, 1, 1.3}};
+  int pick = -1;
+  double best = 0.0;
+  int64_t tiles = 0;
+  const int forced = diag_env_int("DGMC_GEMM_F32_CFG", 0);   // diag build
+  for (int c = 0; c < 3; ++c) {
+    const int TM = 64 * cfgs[c].mb, TN = 64 * cfgs[c].nb;
+    if (Nn % TN != 0) continue;
+    const int64_t t = ((M + TM - 1) / TM) * (Nn / TN);
+    const int64_t rounds = (t + 2 * cus - 1) / (2 * cus);
+    const double cost = (double)rounds * cfgs[c].mb * cfgs[c].nb * cfgs[c].eff;
+    if (forced ? c == forced - 1 : (pick < 0 || cost < best - 1e-9)) {
+      pick = c;
+      best = cost;
+      tiles = t;
+    }
+  }
+  TORCH_CHECK(pick >= 0, "gemm_nt_f32: no tile shape for Nn = ", Nn);
   const int64_t blocks = std::min<int64_t>(tiles, 2 * (int64_t)cus);
-  auto kern = small ? gemm_nt_f32_kernel<1, 1> : gemm_nt_f32_kernel<2, 2>;
+  auto kern = pick == 0 ? gemm_nt_f32_kernel<2, 2>
+                        : pick == 1 ? gemm_nt_f32_kernel<2, 1>
+                                    : gemm_nt_f32_kernel<1, 1>;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream(), A,
                      (int)M, bt.data_ptr<float>(), (int)bt.stride(0),
                      (int)Nn, bp, relu ? 1 : 0, Y.data_ptr<float>(),

@@ -116,7 +116,8 @@ sparse_consensus_bwd(
     const c10::optional<at::Tensor>& pbeg,
     const c10::optional<at::Tensor>& pend,
     const c10::optional<at::Tensor>& prob,
-    const c10::optional<at::Tensor>& gS);
+    const c10::optional<at::Tensor>& gS,
+    const c10::optional<at::Tensor>& dpq);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
     const at::Tensor& rowptr, int64_t nnz, int64_t T);
 void spmm_split_out(const at::Tensor& rowptr, const at::Tensor& col,
@@ -512,8 +513,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "sparse_consensus_bwd(Tensor rowptr, Tensor col, Tensor colptr, Tensor "
       "row_of, Tensor perm, Tensor grad, Tensor P, Tensor Q, Tensor b1, Tensor "
       "w2, Tensor? pptr=None, Tensor? prow=None, Tensor? pbeg=None, Tensor? "
-      "pend=None, Tensor? prob=None, Tensor? gS=None) -> (Tensor, Tensor, "
-      "Tensor, Tensor)");
+      "pend=None, Tensor? prob=None, Tensor? gS=None, Tensor(a!)? dpq=None) "
+      "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "sparse_consensus_fwd_prob(Tensor rowptr, Tensor col, Tensor S_hat, "
       "Tensor P, Tensor Q, Tensor b1, Tensor w2, Tensor b2, int k) -> (Tensor, "

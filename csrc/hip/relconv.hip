@@ -420,9 +420,11 @@ template <bool PROJ, bool TWO>
 __global__ __launch_bounds__(256) void relconv_fwd_kernel(RcPlan pl,
                                                           RcFwd a) {
   extern __shared__ __attribute__((aligned(16))) float rc_smem[];
-  DGMC_LDS float* sA = (DGMC_LDS float*)rc_smem;                            // [64][kRcP] / [64][kRcFP]
+  // sA [64][kRcP] / [64][kRcFP]
+  DGMC_LDS float* sA = (DGMC_LDS float*)rc_smem;
   DGMC_LDS float* sW = sA + kRcRows * (PROJ ? kRcFP : kRcP);
-  DGMC_LDS int* lists = reinterpret_cast<DGMC_LDS int*>(sW + (PROJ ? 32 * kRcFP : kRcC * kRcP));
+  DGMC_LDS int* lists = reinterpret_cast<DGMC_LDS int*>(
+      sW + (PROJ ? 32 * kRcFP : kRcC * kRcP));
   const RcTileLists s = rc_lists(lists, nullptr);
   DGMC_LDS float* flp = reinterpret_cast<DGMC_LDS float*>(lists + kRcListInts);
   const RcFlat fl{flp, reinterpret_cast<DGMC_LDS int*>(flp + 64 * kRcK),
@@ -544,7 +546,7 @@ constexpr int kRcBwdLds =
 __global__ __launch_bounds__(256) void relconv_bwd_kernel(RcPlan pl,
                                                           RcBwd a) {
   extern __shared__ __attribute__((aligned(16))) float rc_smem[];
-  DGMC_LDS float* sG = (DGMC_LDS float*)rc_smem;                       // [64][kRcP]
+  DGMC_LDS float* sG = (DGMC_LDS float*)rc_smem;   // [64][kRcP]
   DGMC_LDS float* sW = sG + kRcRows * kRcP;           // [32 k][kRcP] (3C wide)
   DGMC_LDS float* sX = sW + kRcK * kRcP;              // [64][kRcXP]
   DGMC_LDS float* sWt = sX + kRcRows * kRcXP;         // [kRcCap] entry weights

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_kernel(
     const float* __restrict__ G, const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, float* __restrict__ dP,
-    float* __restrict__ dw2_part, int rows, int R) {
+    float* __restrict__ dw2_part, int rows, int R, int ldp) {
   __shared__ float red[kSpWaves][kMaxChanPerLane * kWave];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int blk = blockIdx.x;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_kernel(
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < kSpWaves; ++w) s += red[w][c];
-    dw2_part[(size_t)blk * R + c] = s;
+    dw2_part[(size_t)blk * ldp + c] = s;
   }
 }
 
@@ -329,15 +329,19 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
     const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ b1,
     const float* __restrict__ w2, float* __restrict__ dP,
-    float* __restrict__ dw2_part, int rows, int R) {
+    float* __restrict__ dw2_part, int ldp, int rows, int R) {
   constexpr int NG = kWave / G;
   __shared__ float4 red[kSpWaves][G];
+  __shared__ float4 redb[kSpWaves][G];
+  __shared__ float redg[kSpWaves];
   const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   const int g = lane / G, gl = lane % G, c = gl * 4;
   const bool cok = c < R;
   const float4 bb = cok ? ld4(b1 + c) : make_float4(0, 0, 0, 0);
   const float4 wv = cok ? ld4(w2 + c) : make_float4(0, 0, 0, 0);
   float dw[4] = {0.f, 0.f, 0.f, 0.f};
+  float db[4] = {0.f, 0.f, 0.f, 0.f};   // b1 gradient: sum of dP rows
+  float gsum = 0.f;                      // b2 gradient: sum of the entries' g
   for (int r = blockIdx.x * kSpWaves + wave; r < rows;
        r += gridDim.x * kSpWaves) {
     float pv[4] = {0.f, 0.f, 0.f, 0.f}, dp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -364,6 +368,7 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
       if constexpr (SOFT) gv = __shfl(gt, (g + NG * j) & (kWave - 1));
       if (p >= p1 || !cok) continue;
       if constexpr (!SOFT) gv = Gr[p];
+      if (gl == 0) gsum += gv;
       const float4 q4 = ld4(Q + (size_t)col[p] * R + c);
       const float q[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
@@ -379,25 +384,43 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_rows_g_kernel(
     for (int off = G; off < kWave; off <<= 1)
 #pragma unroll
       for (int k = 0; k < 4; ++k) dp[k] += __shfl_xor(dp[k], off);
-    if (g == 0 && cok)
-      *reinterpret_cast<float4*>(dP + (size_t)r * R + c) =
+    if (g == 0 && cok) {
+      const float4 d =
           make_float4(dp[0] * wv.x, dp[1] * wv.y, dp[2] * wv.z, dp[3] * wv.w);
+      *reinterpret_cast<float4*>(dP + (size_t)r * R + c) = d;
+      db[0] += d.x; db[1] += d.y; db[2] += d.z; db[3] += d.w;
+    }
   }
 #pragma unroll
   for (int off = G; off < kWave; off <<= 1)
 #pragma unroll
     for (int k = 0; k < 4; ++k) dw[k] += __shfl_xor(dw[k], off);
-  if (g == 0) red[wave][gl] = make_float4(dw[0], dw[1], dw[2], dw[3]);
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) gsum += __shfl_xor(gsum, off);
+  if (g == 0) {
+    red[wave][gl] = make_float4(dw[0], dw[1], dw[2], dw[3]);
+    redb[wave][gl] = make_float4(db[0], db[1], db[2], db[3]);
+  }
+  if (lane == 0) redg[wave] = gsum;
   __syncthreads();
+  // block partial row: [dw2 (R) | db1 (R) | db2, 0, 0, 0]
+  float* prow = dw2_part + (size_t)blockIdx.x * ldp;
   if (threadIdx.x < G && threadIdx.x * 4 < R) {
-    float4 s = red[0][threadIdx.x];
+    float4 s = red[0][threadIdx.x], sb = redb[0][threadIdx.x];
 #pragma unroll
     for (int w = 1; w < kSpWaves; ++w) {
-      const float4 t = red[w][threadIdx.x];
+      const float4 t = red[w][threadIdx.x], tb = redb[w][threadIdx.x];
       s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+      sb.x += tb.x; sb.y += tb.y; sb.z += tb.z; sb.w += tb.w;
     }
-    *reinterpret_cast<float4*>(dw2_part + (size_t)blockIdx.x * R +
-                               threadIdx.x * 4) = s;
+    *reinterpret_cast<float4*>(prow + threadIdx.x * 4) = s;
+    *reinterpret_cast<float4*>(prow + R + threadIdx.x * 4) = sb;
+  }
+  if (threadIdx.x == 0) {
+    float t = redg[0];
+#pragma unroll
+    for (int w = 1; w < kSpWaves; ++w) t += redg[w];
+    *reinterpret_cast<float4*>(prow + 2 * R) = make_float4(t, 0.f, 0.f, 0.f);
   }
 }
 
@@ -613,7 +636,8 @@ sparse_consensus_bwd(
     const c10::optional<at::Tensor>& pbeg,
     const c10::optional<at::Tensor>& pend,
     const c10::optional<at::Tensor>& prob,
-    const c10::optional<at::Tensor>& gS) {
+    const c10::optional<at::Tensor>& gS,
+    const c10::optional<at::Tensor>& dpq) {
   check_f32_2d(P, "P");
   check_f32_2d(Q, "Q");
   const bool pieces = pptr.has_value() && pptr->defined() &&
@@ -630,9 +654,22 @@ sparse_consensus_bwd(
   TORCH_CHECK(G.numel() == col.numel() && perm.numel() == col.numel() &&
                   row_of.numel() == col.numel(),
               "sparse_consensus_bwd: entry arrays");
-  at::Tensor dP = at::empty_like(P), dQ = at::empty_like(Q);
+  at::Tensor dP, dQ;
+  if (dpq.has_value() && dpq->defined()) {   // [dP; dQ] in one buffer
+    TORCH_CHECK(dpq->scalar_type() == at::kFloat && dpq->is_contiguous() &&
+                    dpq->dim() == 2 && dpq->size(0) == rows + cols &&
+                    dpq->size(1) == R,
+                "sparse_consensus_bwd: dpq fp32 contiguous [rows + cols, R]");
+    dP = dpq->narrow(0, 0, rows);
+    dQ = dpq->narrow(0, rows, cols);
+  } else {
+    dP = at::empty_like(P);
+    dQ = at::empty_like(Q);
+  }
   const int nb = std::max(1, std::min(sp_blocks(rows), 1024));
-  at::Tensor dw2 = at::empty({nb, R}, P.options());
+  // per-block partials [dw2 (R) | db1 (R) | db2, 0, 0, 0]
+  const int ldp = 2 * R + 4;
+  at::Tensor dw2 = at::empty({nb, ldp}, P.options());
   const int Gl = group_lanes(R, {P.data_ptr(), Q.data_ptr(), b1.data_ptr(),
                                  w2.data_ptr()});
   const bool soft = prob.has_value() && prob->defined() && gS.has_value() &&
@@ -653,7 +690,7 @@ sparse_consensus_bwd(
         G.data_ptr<float>(), prob->data_ptr<float>(), gS->data_ptr<float>(),
         Gt.data_ptr<float>(), P.data_ptr<float>(), Q.data_ptr<float>(),
         b1.data_ptr<float>(), w2.data_ptr<float>(), dP.data_ptr<float>(),
-        dw2.data_ptr<float>(), (int)rows, R));
+        dw2.data_ptr<float>(), ldp, (int)rows, R));
     DGMC_CHECK_LAUNCH();
   } else if (rows > 0 && Gl > 0) {
     DGMC_GROUP_DISPATCH(Gl, hipLaunchKernelGGL(
@@ -662,7 +699,7 @@ sparse_consensus_bwd(
         G.data_ptr<float>(), (const float*)nullptr, (const float*)nullptr,
         (float*)nullptr, P.data_ptr<float>(), Q.data_ptr<float>(),
         b1.data_ptr<float>(), w2.data_ptr<float>(), dP.data_ptr<float>(),
-        dw2.data_ptr<float>(), (int)rows, R));
+        dw2.data_ptr<float>(), ldp, (int)rows, R));
     DGMC_CHECK_LAUNCH();
   } else if (rows > 0) {
     hipLaunchKernelGGL(sparse_consensus_bwd_rows_kernel, dim3(nb), dim3(256),
@@ -671,8 +708,12 @@ sparse_consensus_bwd(
                        P.data_ptr<float>(), Q.data_ptr<float>(),
                        b1.data_ptr<float>(), w2.data_ptr<float>(),
                        dP.data_ptr<float>(), dw2.data_ptr<float>(), (int)rows,
-                       R);
+                       R, ldp);
     DGMC_CHECK_LAUNCH();
+    // (wide-R fallback: the bias partials by library reductions, block 0)
+    dw2.narrow(1, R, R + 4).zero_();
+    dw2.select(0, 0).narrow(0, R, R).copy_(dP.sum(0));
+    dw2.select(0, 0).narrow(0, 2 * R, 1).copy_(G.sum().view({1}));
   } else {
     dw2.zero_();
   }

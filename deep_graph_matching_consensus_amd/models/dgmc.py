@@ -513,7 +513,7 @@ class DGMC(torch.nn.Module):
                         r_t.reshape(-1, r_t.size(-1)),
                         (id(self.psi_2), rel.N))
                     res = sparse_corr.consensus_update_pq(
-                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand,
+                        S_hat, PQ, pair.n_s, self.mlp, cand,
                         with_prob=fused_soft)
                     if fused_soft:
                         S_hat, S = res
@@ -529,7 +529,7 @@ class DGMC(torch.nn.Module):
                                       loop_key=('sparse_fold',
                                                 id(self.mlp[0].weight)))
                     res = sparse_corr.consensus_update_pq(
-                        S_hat, PQ[:pair.n_s], PQ[pair.n_s:], self.mlp, cand,
+                        S_hat, PQ, pair.n_s, self.mlp, cand,
                         with_prob=fused_soft)
                     if fused_soft:
                         S_hat, S = res

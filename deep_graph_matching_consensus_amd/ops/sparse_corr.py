@@ -35,7 +35,7 @@ import torch.nn.functional as F
 
 from . import _backend
 from . import reference as ref
-from .gemm import _col_sum, loop_col_sum, loop_col_total
+from .gemm import _col_sum
 from ..runtime import loopgrad
 from .sparse import SparseOperator, piece_plan
 
@@ -194,17 +194,21 @@ def sparse_transport(S, r_s, S_idx, N_t, cand=None):
 
 # ---------------------------------------------------------------------------
 class _SparseConsensus(torch.autograd.Function):
-    """Inside a loop scope the MLP's b1 / w2 / b2 gradients of the
-    consensus steps are deposited as per-use partials and folded once by
-    the last use (runtime/loopgrad.py): no per-step reductions and no
-    AccumulateGrad adds.  ``soft_k > 0`` (uniform rows of ``soft_k``
-    candidates) also returns the row softmax of the update - the next
-    step's ``S`` - from the same kernel; its backward (softmax backward +
-    the pass-through add) runs inside the consensus backward kernel."""
+    """Consensus update from the joint node projections ``PQ = [P; Q]``
+    (``P = PQ[:n_s]``, ``Q = PQ[n_s:]``): the backward writes ``[dP; dQ]``
+    into one buffer (no slice-backward zero fills, copies and adds), and its
+    row kernel also emits the per-block partials of the MLP's b1 / w2 / b2
+    gradients.  Inside a loop scope those partials are kept per use and
+    folded once by the last use (runtime/loopgrad.py): no per-step
+    reductions and no AccumulateGrad adds.  ``soft_k > 0`` (uniform rows of
+    ``soft_k`` candidates) also returns the row softmax of the update - the
+    next step's ``S`` - from the same kernel; its backward (softmax backward
+    + the pass-through add) runs inside the consensus backward kernel."""
 
     @staticmethod
-    def forward(ctx, S_hat, P, Q, b1, w2, b2, cand, loop=None, soft_k=0):
+    def forward(ctx, S_hat, PQ, n_s, b1, w2, b2, cand, loop=None, soft_k=0):
         ctx.cand = cand
+        ctx.n_s = n_s
         ctx.meta = (b1.dtype, w2.dtype, b2.dtype, b2.shape)
         ctx.loop = loop
         ctx.idx = loop.register() if loop is not None else None
@@ -213,54 +217,54 @@ class _SparseConsensus(torch.autograd.Function):
         b1f = b1.float().contiguous()
         w2f = w2.float().contiguous().view(-1)
         b2f = b2.float().contiguous().view(-1)
+        P, Q = PQ[:n_s], PQ[n_s:]
         if soft_k:
             out, prob = _backend.ops().sparse_consensus_fwd_prob(
                 cand.rowptr, cand.col, S_hat, P, Q, b1f, w2f, b2f,
                 int(soft_k))
-            ctx.save_for_backward(P, Q, b1, w2, prob)
+            ctx.save_for_backward(PQ, b1, w2, prob)
             return out, prob
-        ctx.save_for_backward(P, Q, b1, w2)
+        ctx.save_for_backward(PQ, b1, w2)
         return _backend.ops().sparse_consensus_fwd(
             cand.rowptr, cand.col, S_hat, P, Q, b1f, w2f, b2f)
 
     @staticmethod
     def backward(ctx, g, gS=None):
         if ctx.soft:
-            P, Q, b1, w2, prob = ctx.saved_tensors
+            PQ, b1, w2, prob = ctx.saved_tensors
         else:
-            P, Q, b1, w2 = ctx.saved_tensors
+            PQ, b1, w2 = ctx.saved_tensors
             prob = None
-        cand = ctx.cand
+        cand, n_s = ctx.cand, ctx.n_s
+        P, Q = PQ[:n_s], PQ[n_s:]
         if g is None:
             g = torch.zeros(cand.col.numel(), dtype=torch.float32,
-                            device=P.device)
+                            device=PQ.device)
         g = g.contiguous().float()
         soft = prob is not None and gS is not None
-        dP, dQ, dw2_part, g = _backend.ops().sparse_consensus_bwd(
+        dPQ = torch.empty_like(PQ)
+        _, _, part, g = _backend.ops().sparse_consensus_bwd(
             cand.rowptr, cand.col, cand.colptr, cand.row_of, cand.perm32, g,
             P, Q, b1.float().contiguous(), w2.float().contiguous().view(-1),
             *cand.col_pieces, prob if soft else None,
-            gS.contiguous().float() if soft else None)
+            gS.contiguous().float() if soft else None, dPQ)
         b1_dt, w2_dt, b2_dt, b2_shape = ctx.meta
+        R = PQ.size(1)
         nones = (None, None, None)
+
+        def split(tot):     # [dw2 | db1 | db2, 0, 0, 0]
+            return (tot[R:2 * R].to(b1_dt), tot[:R].view_as(w2).to(w2_dt),
+                    tot[2 * R].view(b2_shape).to(b2_dt))
         loop = ctx.loop
         if loop is None:
-            db1 = dP.sum(0).to(b1_dt)
-            dw2 = dw2_part.sum(0).view_as(w2).to(w2_dt)
-            db2 = g.sum().view(b2_shape).to(b2_dt)
-            return (g, dP, dQ, db1, dw2, db2) + nones
-        idx = ctx.idx
-        loop_col_sum(loop, 'b1', idx, dP)
-        loop.keep('w2', idx, dw2_part)
-        g4 = g.view(-1, 4) if g.numel() % 4 == 0 else g.view(-1, 1)
-        loop_col_sum(loop, 'b2', idx, g4)
+            db1, dw2, db2 = split(_col_sum(part))
+            return (g, dPQ, None, db1, dw2, db2) + nones
+        loop.keep('part', ctx.idx, part)
         db1 = dw2 = db2 = None
         if loop.arrive():
-            db1 = loop_col_total(loop, 'b1').to(b1_dt)
-            dw2 = _col_sum(loop.kept('w2')).view_as(w2).to(w2_dt)
-            db2 = loop_col_total(loop, 'b2').sum().view(b2_shape).to(b2_dt)
+            db1, dw2, db2 = split(_col_sum(loop.kept('part')))
             loop.release()
-        return (g, dP, dQ, db1, dw2, db2) + nones
+        return (g, dPQ, None, db1, dw2, db2) + nones
 
 
 def soft_fusable(k, R):
@@ -274,16 +278,16 @@ def soft_fusable(k, R):
     return 1 <= k <= min(64, 8 * (64 // G))
 
 
-def consensus_update_pq(S_hat, P, Q, mlp, cand, with_prob=False):
-    """``S_hat + relu(P_i + b1 - Q_idx) . w2 + b2`` from node-level
-    projections ``P [B * N_s, R]``, ``Q [B * N_t, R]`` (the folded form
-    ``P = o_s W1^T`` with psi_2's final Linear inside, models/dgmc.py).
+def consensus_update_pq(S_hat, PQ, n_s, mlp, cand, with_prob=False):
+    """``S_hat + relu(P_i + b1 - Q_idx) . w2 + b2`` from the joint node-level
+    projections ``PQ = [P; Q]``: ``P = PQ[:n_s]`` (``[B * N_s, R]``), ``Q =
+    PQ[n_s:]`` (``[B * N_t, R]``) - the folded form ``P = o_s W1^T`` with
+    psi_2's final Linear inside, models/dgmc.py.
     ``with_prob``: returns ``(S_hat', softmax(S_hat'))`` from one kernel."""
     B, N_s, k = S_hat.shape
     lin1, lin2 = mlp[0], mlp[2]
     res = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
-                                 P.float().contiguous(),
-                                 Q.float().contiguous(), lin1.bias,
+                                 PQ.float().contiguous(), n_s, lin1.bias,
                                  lin2.weight, lin2.bias, cand,
                                  _consensus_loop(lin1),
                                  k if with_prob else 0)
@@ -305,10 +309,10 @@ def consensus_update(S_hat, o_s, o_t, S_idx, mlp, cand=None):
     R = o_s.size(-1)
     lin1, lin2 = mlp[0], mlp[2]
     if cand is not None and _backend.use_hip(S_hat) and R <= 512:
-        P = F.linear(o_s.reshape(-1, R).float(), lin1.weight.float())
-        Q = F.linear(o_t.reshape(-1, R).float(), lin1.weight.float())
+        PQ = F.linear(torch.cat([o_s.reshape(-1, R), o_t.reshape(-1, R)]
+                                ).float(), lin1.weight.float())
         out = _SparseConsensus.apply(S_hat.reshape(-1).float().contiguous(),
-                                     P.contiguous(), Q.contiguous(),
+                                     PQ.contiguous(), B * N_s,
                                      lin1.bias, lin2.weight, lin2.bias, cand,
                                      _consensus_loop(lin1))
         return out.view(B, N_s, k)
