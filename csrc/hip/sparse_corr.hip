@@ -448,30 +448,31 @@ __global__ __launch_bounds__(256) void sparse_consensus_bwd_cols_piece_kernel(
   const float4 q = ld4(Q + (size_t)j * R + c), bb = ld4(b1 + c);
   const float qb[4] = {bb.x - q.x, bb.y - q.y, bb.z - q.z, bb.w - q.w};
   float dq[4] = {0.f, 0.f, 0.f, 0.f};
-  int e = beg;
-  for (; e + 2 <= end; e += 2) {
-    float gv[2];
-    float4 pr[2];
+  // 8 entries per round (indices clamped, out-of-piece entries add 0): two
+  // dependent load rounds per 8 entries instead of per 2
+  for (int e = beg; e < end; e += 8) {
+    int pi[8], ri[8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      gv[u] = Gr[perm[e + u]];
-      pr[u] = ld4(P + (size_t)row_of[e + u] * R + c);
+    for (int u = 0; u < 8; ++u) {
+      const int eu = min(e + u, end - 1);
+      pi[u] = perm[eu];
+      ri[u] = row_of[eu];
+    }
+    float gv[8];
+    float4 pr[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      gv[u] = Gr[pi[u]];
+      pr[u] = ld4(P + (size_t)ri[u] * R + c);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (pr[u].x + qb[0] > 0.f) dq[0] += gv[u];
-      if (pr[u].y + qb[1] > 0.f) dq[1] += gv[u];
-      if (pr[u].z + qb[2] > 0.f) dq[2] += gv[u];
-      if (pr[u].w + qb[3] > 0.f) dq[3] += gv[u];
+    for (int u = 0; u < 8; ++u) {
+      const float g = e + u < end ? gv[u] : 0.f;
+      if (pr[u].x + qb[0] > 0.f) dq[0] += g;
+      if (pr[u].y + qb[1] > 0.f) dq[1] += g;
+      if (pr[u].z + qb[2] > 0.f) dq[2] += g;
+      if (pr[u].w + qb[3] > 0.f) dq[3] += g;
     }
-  }
-  if (e < end) {
-    const float gv = Gr[perm[e]];
-    const float4 pr = ld4(P + (size_t)row_of[e] * R + c);
-    if (pr.x + qb[0] > 0.f) dq[0] += gv;
-    if (pr.y + qb[1] > 0.f) dq[1] += gv;
-    if (pr.z + qb[2] > 0.f) dq[2] += gv;
-    if (pr.w + qb[3] > 0.f) dq[3] += gv;
   }
   if (single) {
     const float4 w = ld4(w2 + c);

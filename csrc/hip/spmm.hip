@@ -70,17 +70,22 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     if (p < p1) {
       // Remainder (< UNROLL entries) as ONE predicated batch: its gathers
       // are in flight together instead of one latency round each.
+      // (clamped unconditional loads, zeroed by selects: a predicated load
+      // would wait for its own round trip)
       float v[UNROLL][VEC];
       float w[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        w[u] = 0.f;
+        const int pe = min(p + u, p1 - 1);
+        w[u] = val[pe];
+        load_vec<TIn, VEC>(x + (size_t)col[pe] * C + c0, v[u]);
+      }
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) v[u][k] = 0.f;
-        if (p + u < p1) {
-          w[u] = val[p + u];
-          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, v[u]);
-        }
+      for (int u = 0; u < UNROLL; ++u) {
+        const bool ok = p + u < p1;
+        w[u] = ok ? w[u] : 0.f;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) v[u][k] = ok ? v[u][k] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u)
@@ -420,36 +425,32 @@ __global__ __launch_bounds__(256) void spmm_piece_kernel(
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-    int p = beg;
-    for (; p + 4 <= end; p += 4) {
-      float xv[4][VEC];
-      float w[4];
+    // 8 entries per round, indices clamped and out-of-piece entries zeroed
+    // by selects (a predicated load would wait for its own round trip)
+    for (int p = beg; p < end; p += 8) {
+      int ci[8], vi[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = p + u;
-        w[u] = val[perm != nullptr ? perm[e] : e];
-        load_vec<TIn, VEC>(x + (size_t)col[e] * C + c0, xv[u]);
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(p + u, end - 1);
+        ci[u] = col[e];
+        vi[u] = perm != nullptr ? perm[e] : e;
+      }
+      float xv[8][VEC];
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        w[u] = val[vi[u]];
+        load_vec<TIn, VEC>(x + (size_t)ci[u] * C + c0, xv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u) {
+        const bool ok = p + u < end;
+        w[u] = ok ? w[u] : 0.f;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
-    }
-    if (p < end) {   // remainder: one predicated batch of gathers
-      float xv[4][VEC];
-      float w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        w[u] = 0.f;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) xv[u][k] = 0.f;
-        if (p + u < end) {
-          w[u] = val[perm != nullptr ? perm[p + u] : p + u];
-          load_vec<TIn, VEC>(x + (size_t)col[p + u] * C + c0, xv[u]);
-        }
+        for (int k = 0; k < VEC; ++k) xv[u][k] = ok ? xv[u][k] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w[u], xv[u][k], acc[k]);
     }
@@ -589,7 +590,22 @@ __global__ __launch_bounds__(256) void spmm_piece_fold_kernel(
   float acc[VEC];
 #pragma unroll
   for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-  for (int q = q0; q < q1; ++q) {
+  // (hub rows have tens of pieces: 8 partial loads in flight, summed in
+  // piece order)
+  int q = q0;
+  for (; q + 8 <= q1; q += 8) {
+    float pv[8][VEC];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < VEC; k += 4)
+        load_vec<float, 4>(part + (size_t)(q + u) * C + c0 + k, pv[u] + k);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] += pv[u][k];
+  }
+  for (; q < q1; ++q) {
     float pv[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; k += 4)

@@ -59,7 +59,8 @@ def parse(asm_text):
             bodies[cur] = []
             continue
         if cur is not None:
-            if line.strip().startswith('s_endpgm'):
+            # (a kernel may hold several s_endpgm: early exits)
+            if line.startswith('.Lfunc_end'):
                 cur = None
                 continue
             bodies[cur].append(line.strip())
