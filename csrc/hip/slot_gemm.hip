@@ -1243,26 +1243,23 @@ __global__ __launch_bounds__(256) void sg_spmm_rowmap_ell_kernel(
   const int pend = min(P, seg[S]);
   int pr[RPL];
   int4 ec[RPL], ev[RPL];
+  // (table rows clamped, not predicated: a predicated load waits for its
+  // own round trip; rows past pend are skipped below)
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     pr[q] = r0 + q * RPB + threadIdx.x / LPR;
-    ec[q] = make_int4(0, 0, 0, 0);
-    ev[q] = make_int4(0, 0, 0, 0);
-    if (pr[q] < pend) {
-      ec[q] = ell[2 * pr[q]];
-      ev[q] = ell[2 * pr[q] + 1];
-    }
+    const int pc = max(min(pr[q], pend - 1), 0);
+    ec[q] = ell[2 * pc];
+    ev[q] = ell[2 * pc + 1];
   }
   for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
     float4 v[RPL][3];
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
-      const int n = pr[q] < pend && ec[q].w <= 3 ? ec[q].w : 0;
+      // unused table slots hold column 0: every gather is in bounds
       const int cs[3] = {ec[q].x, ec[q].y, ec[q].z};
 #pragma unroll
-      for (int u = 0; u < 3; ++u)
-        v[q][u] = u < n ? ld4(g + (size_t)cs[u] * C + c0)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < 3; ++u) v[q][u] = ld4(g + (size_t)cs[u] * C + c0);
     }
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
