@@ -222,8 +222,11 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
   const int ntn = Nn / kX6BN, nk = K / kXBK;
   // Segment starts in lane registers: slot(m) = #{1 <= s < S: seg[s] <= m}.
   const int segv = lane <= S ? seg[lane] : 0x7fffffff;
-  int nrt = tiles != nullptr ? tiles[tcap]
-                              : __builtin_amdgcn_readlane(segv, S) / kXBM;
+  // (read here on every path: the compiler then waits for segv's load once,
+  // before the DMA pipeline, instead of inside it - a vmcnt(0) there would
+  // drain every DMA in flight at each tile start)
+  const int seg_end = __builtin_amdgcn_readlane(segv, S);
+  int nrt = tiles != nullptr ? tiles[tcap] : seg_end / kXBM;
   const int U = nrt * ntn;
   const int G = gridDim.x;
   const int u0 = xcd_remap(blockIdx.x, G);
