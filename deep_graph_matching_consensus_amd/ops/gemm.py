@@ -241,8 +241,17 @@ class _MixedMatmul(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, w_lp, bias, loop):
         xc = x if x.dtype == w_lp.dtype else x.to(w_lp.dtype)
+        # w = weight.t() of an fp32 [out, in] parameter: the exact-f32
+        # chunked NT kernel reads the weight in place (GIN / MLP / encoder
+        # Linears, /root/reference/dgmc/models/gin.py:49, mlp.py:35)
+        wt = w_lp.t() if w_lp.dim() == 2 else None
         if dense_x6_supported(xc, w_lp):
             out = dense_x6(xc, w_lp, bias)
+        elif wt is not None and xc.dtype == torch.float32 and \
+                wt.is_contiguous() and nt_f32_supported([xc], wt) and \
+                (bias is None or (bias.dtype == torch.float32 and
+                                  bias.is_contiguous())):
+            out = nt_f32([xc], wt, bias)
         elif bias is not None:
             # Bias in the GEMM epilogue (hipBLASLt), cast once per forward.
             b_lp = bias if bias.dtype == w_lp.dtype else cached(
@@ -269,7 +278,12 @@ class _MixedMatmul(torch.autograd.Function):
             g = g.to(w_lp.dtype)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = (g @ w_lp.t()).to(ctx.x_dtype)
+            if g.dtype == torch.float32 and w_lp.dim() == 2 and \
+                    w_lp.is_contiguous() and nt_f32_supported([g], w_lp):
+                # dX = g W: NT with Bt = W^T = w_lp ([in, out] contiguous)
+                gx = nt_f32([g], w_lp).to(ctx.x_dtype)
+            else:
+                gx = (g @ w_lp.t()).to(ctx.x_dtype)
         need_w = ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[3]
         loop = ctx.loop

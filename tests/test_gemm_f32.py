@@ -68,3 +68,28 @@ def test_gemm_nt_f32_out_view_and_linear_parts():
     g2 = torch.autograd.grad(ref, [a, h, lin.weight, lin.bias], go)
     for u, v in zip(g1, g2):
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize('M,cin,cout,bias', [(2000, 128, 256, True),
+                                             (777, 64, 64, False),
+                                             (4096, 300, 128, True)])
+def test_linear_fp32_on_native_nt_gemm(M, cin, cout, bias):
+    """``ops.gemm.linear`` (GIN / MLP / encoder Linears, /root/reference/
+    dgmc/models/gin.py:49, mlp.py:35): fp32 forward on the exact-f32 NT
+    kernel, gradients equal F.linear's to fp32 tolerance."""
+    g = torch.Generator(device=DEV).manual_seed(M + cin)
+    lin = torch.nn.Linear(cin, cout, bias=bias).to(DEV)
+    x = torch.randn(M, cin, device=DEV, generator=g, requires_grad=True)
+    wt = lin.weight.detach().t().t()
+    assert gemm.nt_f32_supported([x.detach()], wt.contiguous())
+    y = gemm.linear(x, lin.weight, lin.bias)
+    ref = torch.nn.functional.linear(x, lin.weight, lin.bias)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    go = torch.randn_like(y)
+    leaves = [x, lin.weight] + ([lin.bias] if bias else [])
+    g1 = torch.autograd.grad(y, leaves, go)
+    g2 = torch.autograd.grad(ref, leaves, go)
+    # (weight gradients sum M products: fp32 order noise scales with |dW|)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=1e-4,
+                                   atol=1e-5 * max(1.0, float(b.abs().max())))
