@@ -294,7 +294,9 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
                         bool gather, const c10::optional<at::Tensor>& tiles);
 at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                          const at::Tensor& src, const at::Tensor& seg,
-                         int64_t rounds);
+                         int64_t rounds, const c10::optional<at::Tensor>& ell,
+                         const c10::optional<at::Tensor>& ecol,
+                         const c10::optional<at::Tensor>& evl);
 at::Tensor slot_weight_t(const at::Tensor& weight,
                          const c10::optional<at::Tensor>& root);
 at::Tensor dense_nt_f32(at::TensorList parts, const at::Tensor& bt);
@@ -549,7 +551,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("dense_gemm_x6(Tensor x, Tensor b3, Tensor? bias) -> Tensor");
   m.def(
       "slot_wgrad_x6(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
-      "rounds) -> Tensor");
+      "rounds, Tensor? ell=None, Tensor? ecol=None, Tensor? evl=None) -> "
+      "Tensor");
   m.def("slot_weight_x3(Tensor weight, Tensor? root, bool transpose) -> Tensor");
   m.def(
       "slot_gemm_x6(Tensor a3, Tensor src, Tensor seg, Tensor b3, bool gather, "

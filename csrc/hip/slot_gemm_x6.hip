@@ -502,12 +502,32 @@ __device__ __forceinline__ int wx_swz(int r) {
 constexpr int kWXStageF = 3 * kWXPlane + 2 * kWXPlane;   // X planes + fp32 dY
 constexpr int kWXStageFF = 2 * kWXPlane + 2 * kWXPlane;  // fp32 X + fp32 dY
 
-template <bool GF32, bool XF32 = false>
+// GG (with GF32, bf16 X planes): dY_c is never formed.  U.g[u] is the
+// node-level output gradient g'_u [N, C] and the compact rows are built in
+// the staging from the rowmap entry table (slot_gemm.hip::
+// sg_rowmap_ell_kernel, 32 bytes per row: {c0, c1, c2, n}, {v0, v1, v2, e0}):
+// dY_c[p] = sum_{e < n} v_e g'[c_e] (rows with n > 3 walk ecol / evl from
+// e0), the same fmaf chain in the same entry order as the rowmap SpMM, so
+// the result is bit-identical to the dY_c path.  Per step the 16 rows' table
+// (512 B) is DMA'd into LDS ahead; each thread gathers its row's two 16-byte
+// column chunks of up to three g' rows into registers before a step's MFMAs
+// and combines and stores them into the ring after them.
+// Measured (tools/bench_wgrad_gather.py, profiles/wgrad_gather_r5.json):
+// psi_2's 10-use 128 -> 128 gradient 500 us vs 533 us for the rowmap SpMMs
+// plus the dY_c kernel, psi_1's 256 -> 256 / 1024 -> 256 slower (180 vs
+// 157, 588 vs 471 us: every 128-column X tile re-gathers the rows); two
+// register sets (loads flying across two steps) measured 540 us.  Not on
+// the training path: the input gradient still needs dY_c (docs/
+// performance.md, "dY_c in the consumers").
+template <bool GF32, bool XF32 = false, bool GG = false>
 __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     X6Uses U, int nu, int64_t xplane, int64_t gplane,
     const int* __restrict__ src, const int* __restrict__ seg,
-    const int* __restrict__ items, int Kin, int C, float* __restrict__ part) {
+    const int* __restrict__ items, int Kin, int C, float* __restrict__ part,
+    const int* __restrict__ ell, const int* __restrict__ ecol,
+    const float* __restrict__ evl) {
   static_assert(GF32 || !XF32, "fp32 X only with fp32 dY");
+  static_assert(!GG || (GF32 && !XF32), "gathered dY: fp32 dY, X planes");
   constexpr int STG = XF32 ? kWXStageFF : GF32 ? kWXStageF : kWXStage;
   constexpr int XREG = XF32 ? 2 * kWXPlane : 3 * kWXPlane;   // X image size
   extern __shared__ __attribute__((aligned(16))) char wx_smem[];
@@ -695,6 +715,110 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
       }
   };
 
+  if (GG) {
+    DGMC_LDS int* tab = sidx + kWXMaxRows;          // [3][16 rows][8]
+    auto prow = [&](int q) {                        // first compact row of q
+      return pb + ((qb + q) / nu - c0) * kWXRows;
+    };
+    auto tab_dma = [&](int q) {                     // waves 0, 1: 512 B
+      if (wave < 2)
+        x6_dma4(ell + (size_t)prow(q) * 8 + 64 * wave + lane,
+                tab + (q % 3) * 128 + 64 * wave);
+    };
+    const int gr = tid >> 4, gl = tid & 15;         // row, column chunk
+    const int gsw = 8 * ((gr >> 3) & 1);
+    auto gbase = [&](int q) {
+      const int qq = qb + q, u = qq - (qq / nu) * nu;
+      return reinterpret_cast<const float*>(U.g[u]) + n0 + 4 * gl;
+    };
+    float4 gv[3][2];
+    auto gather = [&](int q) {                      // issue step q's gathers
+      const float* g = gbase(q);
+      const DGMC_LDS int* t = tab + (q % 3) * 128 + 8 * gr;
+      // (unused entries hold column 0: every load is in bounds)
+      const int cs[3] = {t[0], t[1], t[2]};
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          gv[e][h2] = *reinterpret_cast<const float4*>(
+              g + (size_t)cs[e] * C + 64 * h2);
+    };
+    auto combine = [&](int q) {                     // dY rows into the ring
+      const DGMC_LDS int* t = tab + (q % 3) * 128 + 8 * gr;
+      const int n = t[3];
+      float4 acc[2] = {make_float4(0.f, 0.f, 0.f, 0.f),
+                       make_float4(0.f, 0.f, 0.f, 0.f)};
+      if (n <= 3) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const float w = __int_as_float(t[4 + e]);
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2)
+            if (e < n) {
+              acc[h2].x = fmaf(w, gv[e][h2].x, acc[h2].x);
+              acc[h2].y = fmaf(w, gv[e][h2].y, acc[h2].y);
+              acc[h2].z = fmaf(w, gv[e][h2].z, acc[h2].z);
+              acc[h2].w = fmaf(w, gv[e][h2].w, acc[h2].w);
+            }
+        }
+      } else {                     // long row: walk (col, val) in entry order
+        const float* g = gbase(q);
+        const int e0 = t[7];
+        for (int e = e0; e < e0 + n; ++e) {
+          const float w = evl[e];
+          const float* gr0 = g + (size_t)ecol[e] * C;
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const float4 x = *reinterpret_cast<const float4*>(gr0 + 64 * h2);
+            acc[h2].x = fmaf(w, x.x, acc[h2].x);
+            acc[h2].y = fmaf(w, x.y, acc[h2].y);
+            acc[h2].z = fmaf(w, x.z, acc[h2].z);
+            acc[h2].w = fmaf(w, x.w, acc[h2].w);
+          }
+        }
+      }
+      DGMC_LDS float* dg = reinterpret_cast<DGMC_LDS float*>(
+          ring + (q % kWXNst) * STG + XREG);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int pc = (gl + 16 * h2) ^ gsw;
+        *reinterpret_cast<DGMC_LDS x6_f32x4*>(dg + gr * 128 + 4 * pc) =
+            x6_f32x4{acc[h2].x, acc[h2].y, acc[h2].z, acc[h2].w};
+      }
+    };
+    auto stage_x = [&](int q) {                     // X planes of step q
+      const int qq = qb + q;
+      const int ch = qq / nu - c0, u = qq - (qq / nu) * nu;
+      const __bf16* xr = U.x[u] + (size_t)sidx[ch * kWXRows + srow] * Kin +
+                         i0 + 8 * schunk;
+      DGMC_LDS __bf16* d = ring + (q % kWXNst) * STG + 4 * wave * 128;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) x6_dma16(xr + p * xplane, d + p * kWXPlane);
+    };
+    // Iteration q: X of q + 2 and the table of q + 3 DMA'd and q + 2's rows
+    // gathered (registers) before step q's MFMAs, combined into the ring
+    // after them; q = -2, -1 only fill the first two steps.
+    tab_dma(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x6_barrier();
+    for (int q = -2; q < total; ++q) {
+      const bool nxt = q + 2 < total;
+      if (nxt) {
+        gather(q + 2);
+        stage_x(q + 2);
+      }
+      if (q + 3 < total) tab_dma(q + 3);
+      if (q >= 0) {
+        x6_barrier();
+        compute(ring + (q % kWXNst) * STG);
+      }
+      if (nxt) combine(q + 2);
+      // (X of q + 2 and the table of q + 3 landed: visible after the barrier)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      x6_barrier();
+    }
+  } else {
   const int pro = total < kWXNst - 1 ? total : kWXNst - 1;
   for (int q = 0; q < pro; ++q) stage(q, ring + (q % kWXNst) * STG);
   for (int q = 0; q < total; ++q) {
@@ -713,6 +837,7 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
     x6_barrier();
     compute(ring + (q % kWXNst) * STG);
     x6_barrier();
+  }
   }
   // acc[a][b]: rows c = cbase + 32 a + 8 qd + 4 h + e, column i = ibase +
   // 32 b + l32 (the dW^T layout of slot_wgrad2_kernel).
@@ -1137,7 +1262,12 @@ at::Tensor slot_fold_parts(const at::Tensor& part, const at::Tensor& ib,
 // workgroups the items are sized for (as slot_wgrad_f32).
 at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                          const at::Tensor& src, const at::Tensor& seg,
-                         int64_t rounds) {
+                         int64_t rounds, const c10::optional<at::Tensor>& ell,
+                         const c10::optional<at::Tensor>& ecol,
+                         const c10::optional<at::Tensor>& evl) {
+  // ell given: gs are node-level fp32 output gradients [N_g, out], and the
+  // compact dY rows are gathered in the kernel (GG above).
+  const bool gg = ell.has_value() && ell->defined();
   const int64_t nu = (int64_t)xs.size();
   TORCH_CHECK(nu >= 1 && nu <= kWXMaxU && (int64_t)gs.size() == nu,
               "slot_wgrad_x6: 1 <= uses <= 16, one dY per X");
@@ -1146,6 +1276,8 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const bool gf32 = gs[0].scalar_type() == at::kFloat;
   const bool xf32 = xs[0].scalar_type() == at::kFloat;
   TORCH_CHECK(gf32 || !xf32, "slot_wgrad_x6: fp32 X needs fp32 dY");
+  TORCH_CHECK(!gg || (gf32 && !xf32),
+              "slot_wgrad_x6: gathered dY needs fp32 g' and X planes");
   const int64_t N = xf32 ? xs[0].size(0) : xs[0].size(1);
   const int64_t Kin = xf32 ? xs[0].size(1) : xs[0].size(2);
   const int64_t C = gf32 ? gs[0].size(1) : gs[0].size(2);
@@ -1168,7 +1300,12 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
                       x.size(1) == N && x.size(2) == Kin,
                   "slot_wgrad_x6: X_u bf16 planes [3, N, in]");
     }
-    if (gf32) {
+    if (gg) {
+      TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous() &&
+                      g.dim() == 2 && g.size(0) == gs[0].size(0) &&
+                      g.size(1) == C && aligned16(g.data_ptr()),
+                  "slot_wgrad_x6: g'_u fp32 [N_g, out] (all uses alike)");
+    } else if (gf32) {
       TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous() &&
                       g.dim() == 2 && g.size(0) == P && g.size(1) == C &&
                       aligned16(g.data_ptr()),
@@ -1192,18 +1329,34 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const int64_t per = Kin * C;
   at::Tensor part =
       at::empty({G_cap, per}, xs[0].options().dtype(at::kFloat));
-  auto kern = xf32 ? slot_wgrad_x6_kernel<true, true>
+  const int *ep = nullptr, *cp = nullptr;
+  const float* vp = nullptr;
+  if (gg) {
+    // entry table [P_cap, 8] of the same compact plan; long rows' (col, val)
+    TORCH_CHECK(ell->scalar_type() == at::kInt && ell->is_contiguous() &&
+                    ell->numel() == 8 * P && ecol.has_value() &&
+                    evl.has_value() && ecol->scalar_type() == at::kInt &&
+                    evl->scalar_type() == at::kFloat &&
+                    ecol->is_contiguous() && evl->is_contiguous() &&
+                    ecol->numel() == evl->numel(),
+                "slot_wgrad_x6: int32 entry table [P_cap, 8] + col / val");
+    ep = ell->data_ptr<int>();
+    cp = ecol->data_ptr<int>();
+    vp = evl->data_ptr<float>();
+  }
+  auto kern = gg ? slot_wgrad_x6_kernel<true, false, true>
+              : xf32 ? slot_wgrad_x6_kernel<true, true>
               : gf32 ? slot_wgrad_x6_kernel<true> : slot_wgrad_x6_kernel<false>;
   const size_t lds =
       (size_t)kWXNst * (xf32 ? kWXStageFF : gf32 ? kWXStageF : kWXStage) * 2 +
-      kWXMaxRows * 4;
+      kWXMaxRows * 4 + (gg ? 3 * 128 * 4 : 0);
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, dim3(G_cap * tiles), dim3(256), lds, stream(), U,
                      (int)nu, N * Kin, P * C, src.data_ptr<int>(),
                      seg.data_ptr<int>(), it[0].data_ptr<int>(), (int)Kin,
-                     (int)C, part.data_ptr<float>());
+                     (int)C, part.data_ptr<float>(), ep, cp, vp);
   DGMC_CHECK_LAUNCH();
   return slot_fold_parts(part, it[1], S, Kin, C);
 }

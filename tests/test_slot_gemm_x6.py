@@ -36,6 +36,7 @@ def headline_plan():
     op = spline_plan(b.v['ei'], b.v['ea_val'], N, (5, 5), (1, 1), 1,
                      root=True)
     plan = sg.compact_plan(op, 26)
+    plan.test_op = op
     return N, plan
 
 
@@ -193,6 +194,34 @@ def test_x6_weight_grad_fp32_dy_equals_planes(headline_plan, cin, cout,
     # fp32 X rows as well (split in the kernel)
     wff = ops.slot_wgrad_x6(xf, dys, plan.src, plan.seg, rounds)
     assert torch.equal(wff, wp), float((wff - wp).abs().max())
+
+
+@pytest.mark.parametrize('cin,cout,uses', [(128, 128, 10), (256, 256, 1),
+                                           (1024, 256, 1)])
+def test_x6_weight_grad_gathered_dy_equals_rowmap(headline_plan, cin, cout,
+                                                  uses):
+    """dY_c rows built inside the weight gradient's staging from the node
+    gradient g' and the rowmap entry table (no dY_c tensor) give bit-for-bit
+    the result on the rowmap SpMM's dY_c (same fmaf chains, same order)."""
+    N, plan = headline_plan
+    ops = _backend.ops()
+    At = plan.test_op.t()
+    ell = sg.rowmap_ranges(plan, At)
+    assert ell.numel() == 8 * plan.src.numel()
+    g = torch.Generator(device=DEV).manual_seed(29 + cin)
+    xs = [ops.split3(torch.randn(N, cin, device=DEV, generator=g))
+          for _ in range(uses)]
+    gs = [torch.randn(N, cout, device=DEV, generator=g) for _ in range(uses)]
+    dys = [ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, gu,
+                                plan.seg, ell, False) for gu in gs]
+    rounds = 1 if cin == 128 else (2 if cin == 256 else 6)
+    wd = ops.slot_wgrad_x6(xs, dys, plan.src, plan.seg, rounds)
+    wg = ops.slot_wgrad_x6(xs, gs, plan.src, plan.seg, rounds, ell, At.col,
+                           At.val)
+    assert torch.equal(wg, wd), float((wg - wd).abs().max())
+    # rows with more than three entries take the (col, val) walk
+    n = ell.view(-1, 8)[:, 3]
+    assert int((n > 3).sum()) > 0
 
 
 def test_x6_f32dy_training_step_matches_planes(monkeypatch):
