@@ -178,6 +178,8 @@ constexpr int kXAPlane = kXBM * kXBK;            // 8192 bf16 (16 KB)
 constexpr int kXBPlane = kX6BN * kXBK;           // 4096 bf16 (8 KB)
 constexpr int kXStage = 3 * kXAPlane + 3 * kXBPlane;   // bf16 per stage
 constexpr size_t kXLds = (size_t)2 * kXStage * 2 + 2 * kXBM * 4;
+constexpr int kXEpiPitch = 32;       // floats per row of the epilogue transpose
+constexpr size_t kXEpiBytes = (size_t)8 * 32 * kXEpiPitch * 4;   // 8 waves
 
 __device__ __forceinline__ void x6_dma4(const int* g, DGMC_LDS int* l) {
   const unsigned m0 =
@@ -409,7 +411,59 @@ __global__ __launch_bounds__(kXThreads, 1) void slot_gemm_x6_kernel(
               w[st][0][a], x[st][0][b], acc[a][b], 0, 0, 0);
         }
   };
+  // fp32-A kernels (32 x 128 wave tiles): the tile leaves through a
+  // wave-private LDS transpose, so each store instruction writes 8 whole
+  // 128-byte row segments instead of 32 rows x 32 bytes (4x fewer write
+  // requests; the values and their order of summation are unchanged).
+  // 16-byte chunk c of row r sits at chunk c ^ (r & 7): the column writes
+  // (ds_write_b128: 8-lane groups = 8 rows of one chunk, 32 banks) and the
+  // row reads (ds_read_b128: 16-lane groups over 4 rows x 4 chunks, 64
+  // banks) are both bank-conflict free.
+  DGMC_LDS float* epi = (DGMC_LDS float*)(x6_smem + (size_t)2 * STG * 2 +
+                                          2 * kXBM * 4) +
+                        wave * 32 * kXEpiPitch;
+  auto epilogue_t = [&](int j) {
+    const int rb = row_tile(j) * kXBM + xbase;      // the wave's first row
+    const int cb = col_tile(j) * kX6BN;
+    const int rr = lane >> 3, cc = 4 * (lane & 7);
+#pragma unroll
+    for (int a = 0; a < FA; ++a) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bias != nullptr)
+          bv = *reinterpret_cast<const float4*>(bias + cb + 32 * a + 8 * q +
+                                                4 * h);
+        *reinterpret_cast<DGMC_LDS x6_f32x4*>(
+            epi + i * kXEpiPitch + 4 * ((2 * q + h) ^ (i & 7))) =
+            x6_f32x4{
+            acc[a][0][4 * q] + acs[a][0][4 * q] + bv.x,
+            acc[a][0][4 * q + 1] + acs[a][0][4 * q + 1] + bv.y,
+            acc[a][0][4 * q + 2] + acs[a][0][4 * q + 2] + bv.z,
+            acc[a][0][4 * q + 3] + acs[a][0][4 * q + 3] + bv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[a][0][4 * q + r] = acs[a][0][4 * q + r] = 0.f;
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = 8 * k + rr;
+        const x6_f32x4 v = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+            epi + r * kXEpiPitch + 4 * ((lane & 7) ^ (r & 7)));
+        if (rb + r < m_lim)
+          *reinterpret_cast<float4*>(Y + (size_t)(rb + r) * Nn + cb +
+                                     32 * a + cc) =
+              make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
   auto epilogue = [&](int j) {
+    if (AF32) {
+      epilogue_t(j);
+      return;
+    }
     const int m0 = row_tile(j) * kXBM + xbase + i;
     const int n0 = col_tile(j) * kX6BN + wbase + 4 * h;
 #pragma unroll
@@ -1113,7 +1167,7 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
                        : slot_gemm_x6_kernel<false, false>;
   const int64_t grid = blocks;
   const size_t lds = af32 ? (size_t)2 * (2 * kXBM * kXBK + 3 * kXBPlane) * 2 +
-                                2 * kXBM * 4
+                                2 * kXBM * 4 + kXEpiBytes
                           : kXLds;
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
