@@ -894,22 +894,37 @@ __global__ __launch_bounds__(256, 2) void slot_wgrad_x6_kernel(
   }
   }
   // acc[a][b]: rows c = cbase + 32 a + 8 qd + 4 h + e, column i = ibase +
-  // 32 b + l32 (the dW^T layout of slot_wgrad2_kernel).
+  // 32 b + l32 (the dW^T layout of slot_wgrad2_kernel).  Each 32 x 32 block
+  // leaves through a wave-private transpose in the (now idle) ring - the
+  // swizzled image of the slot GEMM's epilogue - so a store instruction
+  // writes 8 whole 128-byte row segments instead of 32 rows x 32 bytes.
   const int l32 = lane & 31, h = lane >> 5;
   float* outp = part + (size_t)item * Kin * C;
+  DGMC_LDS float* epi = (DGMC_LDS float*)ring + wave * 32 * kXEpiPitch;
+  const int rr = lane >> 3, cc = 4 * (lane & 7);
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      float* row = outp + (size_t)(i0 + ibase + b * 32 + l32) * C + n0 +
-                   cbase + a * 32 + 4 * h;
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int qd = 0; qd < 4; ++qd)
-        *reinterpret_cast<float4*>(row + 8 * qd) = make_float4(
-            acc[a][b][4 * qd] + acs[a][b][4 * qd],
-            acc[a][b][4 * qd + 1] + acs[a][b][4 * qd + 1],
-            acc[a][b][4 * qd + 2] + acs[a][b][4 * qd + 2],
-            acc[a][b][4 * qd + 3] + acs[a][b][4 * qd + 3]);
+        *reinterpret_cast<DGMC_LDS x6_f32x4*>(
+            epi + l32 * kXEpiPitch + 4 * ((2 * qd + h) ^ (l32 & 7))) =
+            x6_f32x4{acc[a][b][4 * qd] + acs[a][b][4 * qd],
+                     acc[a][b][4 * qd + 1] + acs[a][b][4 * qd + 1],
+                     acc[a][b][4 * qd + 2] + acs[a][b][4 * qd + 2],
+                     acc[a][b][4 * qd + 3] + acs[a][b][4 * qd + 3]};
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = 8 * k + rr;
+        const x6_f32x4 v = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+            epi + r * kXEpiPitch + 4 * ((lane & 7) ^ (r & 7)));
+        *reinterpret_cast<float4*>(outp + (size_t)(i0 + ibase + b * 32 + r) *
+                                              C + n0 + cbase + a * 32 + cc) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
 }
 
@@ -1049,15 +1064,29 @@ __global__ __launch_bounds__(256, 4) void dense_nt_x6_kernel(
     }
   }
   // acc: Y^T block - lane column i = row m, rows (r & 3) + 8 (r >> 2) + 4 h
-  // = column n.
-  const int m = m0 + wm * 32 + i;
-  if (m < M) {
-    float* yrow = Y + (size_t)m * Nn + n0 + wn * 32 + 4 * h;
+  // = column n.  Out through a wave-private swizzled transpose in the ring
+  // (after a barrier: other waves may still read the last chunk), 8 whole
+  // 128-byte row segments per store instruction.
+  x6_barrier();
+  DGMC_LDS float* epi = lds + wave * 32 * 32;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      *reinterpret_cast<float4*>(yrow + 8 * q) = make_float4(
-          acc[4 * q] + acs[4 * q], acc[4 * q + 1] + acs[4 * q + 1],
-          acc[4 * q + 2] + acs[4 * q + 2], acc[4 * q + 3] + acs[4 * q + 3]);
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<DGMC_LDS x6_f32x4*>(
+        epi + i * 32 + 4 * ((2 * q + h) ^ (i & 7))) =
+        x6_f32x4{acc[4 * q] + acs[4 * q], acc[4 * q + 1] + acs[4 * q + 1],
+                 acc[4 * q + 2] + acs[4 * q + 2],
+                 acc[4 * q + 3] + acs[4 * q + 3]};
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 8 * k + (lane >> 3);
+    const x6_f32x4 v = *reinterpret_cast<const DGMC_LDS x6_f32x4*>(
+        epi + r * 32 + 4 * ((lane & 7) ^ (r & 7)));
+    const int m = m0 + wm * 32 + r;
+    if (m < M)
+      *reinterpret_cast<float4*>(Y + (size_t)m * Nn + n0 + wn * 32 +
+                                 4 * (lane & 7)) =
+          make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
