@@ -34,6 +34,7 @@ typedef float gf_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kGfBK = 32;           // k per staged step
 constexpr int kGfMaxSteps = 96;     // 32-wide k steps (K <= 3072)
+constexpr size_t kGfEpiBytes = 4 * 32 * 32 * 4;   // epilogue transpose
 
 // A zero page for the DMAs of columns past a part's width.
 __device__ __attribute__((aligned(16))) float g_gf_zero[4] = {0.f, 0.f, 0.f,
@@ -156,21 +157,26 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
   };
   // acc[a][b]: accumulator of Y^T block (n block a, m block b): lane i is
   // row m0 + 32 b + i, registers 4 q + r columns n0 + 32 a + 8 q + 4 h + r.
+  // Each 32 x 32 block leaves through a wave-private LDS transpose (16-byte
+  // chunk c of row r at c ^ (r & 7): conflict-free ds_write_b128 columns and
+  // ds_read_b128 rows), so a store instruction writes 8 whole 128-byte row
+  // segments instead of 32 rows x 32 bytes.
+  extern __shared__ __attribute__((aligned(16))) float gf_epi_[];  // [4][32][32]
+  DGMC_LDS float* epi = (DGMC_LDS float*)gf_epi_ + wave * 32 * 32;
   auto epilogue = [&](int uu) {
-    const int m0 = (uu / ntn) * TM + wm * 32 * MB + i;
-    const int n0 = (uu % ntn) * TN + wn * 32 * NB + 4 * h;
+    const int mb = (uu / ntn) * TM + wm * 32 * MB;
+    const int nb = (uu % ntn) * TN + wn * 32 * NB;
 #pragma unroll
     for (int a = 0; a < NB; ++a) {
       float4 bv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        bv[q] = bias ? *reinterpret_cast<const float4*>(bias + n0 + 32 * a +
-                                                        8 * q)
+        bv[q] = bias ? *reinterpret_cast<const float4*>(bias + nb + 4 * h +
+                                                        32 * a + 8 * q)
                      : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
-        const int m = m0 + 32 * b;
-        float* yrow = Y + (size_t)m * ldy + n0 + 32 * a;
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float4 v = make_float4(acc[a][b][4 * q] + bv[q].x,
@@ -181,9 +187,23 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f);
             v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
           }
-          if (m < M) *reinterpret_cast<float4*>(yrow + 8 * q) = v;
+          *reinterpret_cast<DGMC_LDS gf_f32x4*>(
+              epi + i * 32 + 4 * ((2 * q + h) ^ (i & 7))) =
+              gf_f32x4{v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[a][b][4 * q + r] = 0.f;
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = 8 * k + (lane >> 3);
+          const gf_f32x4 v = *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+              epi + r * 32 + 4 * ((lane & 7) ^ (r & 7)));
+          const int m = mb + 32 * b + r;
+          if (m < M)
+            *reinterpret_cast<float4*>(Y + (size_t)m * ldy + nb + 32 * a +
+                                       4 * (lane & 7)) =
+                make_float4(v[0], v[1], v[2], v[3]);
         }
       }
     }
@@ -313,7 +333,11 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   auto kern = pick == 0 ? gemm_nt_f32_kernel<2, 2>
                         : pick == 1 ? gemm_nt_f32_kernel<2, 1>
                                     : gemm_nt_f32_kernel<1, 1>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream(), A,
+  DGMC_CHECK_HIP(hipFuncSetAttribute(
+      reinterpret_cast<const void*>(kern),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGfEpiBytes));
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), kGfEpiBytes,
+                     stream(), A,
                      (int)M, bt.data_ptr<float>(), (int)bt.stride(0),
                      (int)Nn, bp, relu ? 1 : 0, Y.data_ptr<float>(),
                      (int)Y.stride(0));
