@@ -25,9 +25,11 @@ exact-fp32 MFMA kernels (``v_mfma_f32_32x32x2_f32``) for them.  Measured
 against fp64 (``tests/test_slot_gemm_x6.py``, ``tests/test_x6_stress.py``):
 forward and input-gradient errors at or below the exact chain's on every
 headline shape and stress input; see docs/performance.md for the weight
-gradient and the documented subnormal limit.  The RelConv / Linear node
-GEMMs of the DBP15K config are exact fp32.  The JSON's ``gemm_arith``
-names what ran.  ``--dtype bf16`` is an opt-in fast mode (bf16 operands),
+gradient and the documented subnormal limit.  The DBP15K config's node
+GEMMs (RelConv's stacked maps, the final Linears) run bf16x6 as well
+(``tests/test_gemm_f32.py``: error at or below the exact chain's); its
+fused RelConv aggregation and the top-k re-score stay exact fp32.  The
+JSON's ``gemm_arith`` names what ran.  ``--dtype bf16`` is an opt-in fast mode (bf16 operands),
 never the headline.  After the timed steps, held-out Hits@1 / Hits@10 of
 S_L are evaluated on ``--eval-pairs`` test pairs (untimed), like the
 reference's test loop.
@@ -181,6 +183,17 @@ def gemm_arith(dtype):
     return 'exact_f32 (v_mfma_f32_32x32x2_f32)'
 
 
+def kg_gemm_arith():
+    """DBP15K config: the stacked node maps and final Linears on the
+    chunked NT GEMM (bf16x6 unless DGMC_AMD_X6=0); RelConv's fused
+    aggregation kernels and the top-k re-score are exact fp32."""
+    from deep_graph_matching_consensus_amd.ops import gemm
+    if gemm.NT_X6:
+        return ('bf16x6 node GEMMs (fp32-emulated); RelConv aggregation and '
+                'top-k selection exact fp32')
+    return 'exact_f32 (v_mfma_f32_32x32x2_f32 / 16x16x4_f32)'
+
+
 def build_model(cfg, args, num_node_features, num_edge_features, device):
     psi_1 = SplineCNN(num_node_features, 256, num_edge_features, 2,
                       cat=False, dropout=0.5)
@@ -254,6 +267,7 @@ def bench_kg(args, cfg, device):
                    'impl': args.impl, 'hipgraph': trainer.graph},
         'hits@1_test': round(hits1, 4), 'hits@10_test': round(hits10, 4),
         'loss': round(float(trainer.last_loss), 4),
+        'gemm_arith': kg_gemm_arith(),
     }
     return out
 

@@ -65,7 +65,30 @@ __device__ __forceinline__ void gf_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int MB, int NB>
+typedef __bf16 gf_bf16x8 __attribute__((ext_vector_type(8)));
+
+// fp32 -> three bf16 terms hi + mid + lo (slot_gemm_x6.hip's split)
+__device__ __forceinline__ void gf_split8(const gf_f32x4 u0, const gf_f32x4 u1,
+                                          gf_bf16x8 (&v)[3]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float x = e < 4 ? u0[e] : u1[e - 4];
+    const __bf16 hh = (__bf16)x;
+    const float r1 = x - (float)hh;
+    const __bf16 mm = (__bf16)r1;
+    v[0][e] = hh;
+    v[1][e] = mm;
+    v[2][e] = (__bf16)(r1 - (float)mm);
+  }
+}
+
+// X6: the same tiles, staging and epilogue with the products on the bf16
+// matrix cores as bf16x6 (slot_gemm_x6.hip: each fp32 operand split into
+// three bf16 terms in registers, six v_mfma_f32_32x32x16_bf16 per 16-deep
+// step into a large- and a small-term accumulator; max error below the
+// exact-f32 chain's, tests/test_gemm_f32.py) - 2.7x fewer matrix-core
+// cycles than v_mfma_f32_32x32x2_f32.
+template <int MB, int NB, bool X6 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
     GfSteps A, int M, const float* __restrict__ bt, int ldb, int Nn,
     const float* __restrict__ bias, int relu, float* __restrict__ Y,
@@ -126,14 +149,53 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
   for (int g = 0; g < 4; ++g) qoff[g] = 4 * ((2 * g + h) ^ sw);
   const int offN = (wn * 32 * NB + i) * kGfBK;
   const int offM = (wm * 32 * MB + i) * kGfBK;
-  gf_f32x16 acc[NB][MB];
+  gf_f32x16 acc[NB][MB], acs[NB][MB];
 #pragma unroll
   for (int a = 0; a < NB; ++a)
 #pragma unroll
     for (int b = 0; b < MB; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+    if (X6) {
+      // 16-deep step st: lane (i, h) supplies k = 16 st + 8 h .. + 7, the
+      // logical chunks 4 st + 2 h and + 1 of its row image
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        gf_bf16x8 w[NB][3], x[MB][3];
+        const int c0 = 4 * st + 2 * h;
+        const int o0 = 4 * (c0 ^ sw), o1 = 4 * ((c0 + 1) ^ sw);
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+          gf_split8(*reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                        lb + offN + a * 32 * kGfBK + o0),
+                    *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                        lb + offN + a * 32 * kGfBK + o1),
+                    w[a]);
+#pragma unroll
+        for (int b = 0; b < MB; ++b)
+          gf_split8(*reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                        la + offM + b * 32 * kGfBK + o0),
+                    *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                        la + offM + b * 32 * kGfBK + o1),
+                    x[b]);
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            gf_f32x16 sm = acs[a][b];
+            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[a][2], x[b][0], sm, 0, 0, 0);
+            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[a][0], x[b][2], sm, 0, 0, 0);
+            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[a][1], x[b][1], sm, 0, 0, 0);
+            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[a][1], x[b][0], sm, 0, 0, 0);
+            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[a][0], x[b][1], sm, 0, 0, 0);
+            acs[a][b] = sm;
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                w[a][0], x[b][0], acc[a][b], 0, 0, 0);
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       gf_f32x4 fa[NB], fb[MB];
@@ -179,10 +241,20 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          float4 v = make_float4(acc[a][b][4 * q] + bv[q].x,
-                                 acc[a][b][4 * q + 1] + bv[q].y,
-                                 acc[a][b][4 * q + 2] + bv[q].z,
-                                 acc[a][b][4 * q + 3] + bv[q].w);
+          float4 v;
+          if (X6)
+            v = make_float4(acc[a][b][4 * q] + acs[a][b][4 * q] + bv[q].x,
+                            acc[a][b][4 * q + 1] + acs[a][b][4 * q + 1] +
+                                bv[q].y,
+                            acc[a][b][4 * q + 2] + acs[a][b][4 * q + 2] +
+                                bv[q].z,
+                            acc[a][b][4 * q + 3] + acs[a][b][4 * q + 3] +
+                                bv[q].w);
+          else
+            v = make_float4(acc[a][b][4 * q] + bv[q].x,
+                            acc[a][b][4 * q + 1] + bv[q].y,
+                            acc[a][b][4 * q + 2] + bv[q].z,
+                            acc[a][b][4 * q + 3] + bv[q].w);
           if (relu) {
             v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f);
             v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
@@ -191,7 +263,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
               epi + i * 32 + 4 * ((2 * q + h) ^ (i & 7))) =
               gf_f32x4{v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[a][b][4 * q + r] = 0.f;
+          for (int r = 0; r < 4; ++r)
+            acc[a][b][4 * q + r] = acs[a][b][4 * q + r] = 0.f;
         }
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -260,7 +333,7 @@ int gf_num_cus(int dev) {
 // unit column stride (Nn % 64 == 0); out: optional [M, Nn] view to write.
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
-                       const c10::optional<at::Tensor>& out) {
+                       const c10::optional<at::Tensor>& out, bool x6) {
   TORCH_CHECK(parts.size() >= 1, "gemm_nt_f32: at least one part");
   const int64_t M = parts[0].size(0);
   GfSteps A{};
@@ -310,8 +383,13 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   // Tile shape: the fewest tile-time units on 2 blocks per CU - whole
   // rounds of 2 * CUs tiles, each costing its MFMA work with the smaller
   // tiles' lower operand reuse (measured ~1.12x / ~1.3x per MAC).
+  // bf16x6 (2.7x fewer matrix-core cycles) is bound by the operand
+  // traffic: 128x64 tiles cost no more per MAC than 128x128 there
+  // (tools/micro/bench_nt_f32_cfg.py, DBP15K final Linear 1068 -> 256:
+  // 237 / 229 / 215 / 226 us for the picks / 128x128 / 128x64 / 64x64).
   struct Cfg { int mb, nb; double eff; };
-  const Cfg cfgs[3] = {{2, 2, 1.0}, {2, 1, 1.12}, {1, 1, 1.3}};
+  const Cfg cfgs[3] = {{2, 2, 1.0}, {2, 1, x6 ? 1.0 : 1.12},
+                       {1, 1, 1.3}};
   int pick = -1;
   double best = 0.0;
   int64_t tiles = 0;
@@ -330,9 +408,12 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   }
   TORCH_CHECK(pick >= 0, "gemm_nt_f32: no tile shape for Nn = ", Nn);
   const int64_t blocks = std::min<int64_t>(tiles, 2 * (int64_t)cus);
-  auto kern = pick == 0 ? gemm_nt_f32_kernel<2, 2>
-                        : pick == 1 ? gemm_nt_f32_kernel<2, 1>
-                                    : gemm_nt_f32_kernel<1, 1>;
+  auto kern = x6 ? (pick == 0 ? gemm_nt_f32_kernel<2, 2, true>
+                              : pick == 1 ? gemm_nt_f32_kernel<2, 1, true>
+                                          : gemm_nt_f32_kernel<1, 1, true>)
+                 : (pick == 0 ? gemm_nt_f32_kernel<2, 2>
+                              : pick == 1 ? gemm_nt_f32_kernel<2, 1>
+                                          : gemm_nt_f32_kernel<1, 1>);
   DGMC_CHECK_HIP(hipFuncSetAttribute(
       reinterpret_cast<const void*>(kern),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGfEpiBytes));

@@ -28,7 +28,7 @@ void rel_proj_bwd(const at::Tensor& dpq, const at::Tensor& feat,
 void rel_fold(at::TensorList parts, at::TensorList outs);
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
-                       const c10::optional<at::Tensor>& out);
+                       const c10::optional<at::Tensor>& out, bool x6);
 std::tuple<at::Tensor, at::Tensor> fold_weights_bwd(const at::Tensor& w1,
                                                     const at::Tensor& wf,
                                                     const at::Tensor& g);
@@ -362,7 +362,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("rel_fold(Tensor[] parts, Tensor(a!)[] outs) -> ()");
   m.def(
       "gemm_nt_f32(Tensor[] parts, Tensor bt, Tensor? bias=None, bool "
-      "relu=False, Tensor(a!)? out=None) -> Tensor");
+      "relu=False, Tensor(a!)? out=None, bool x6=False) -> Tensor");
   m.def("fold_weights_bwd(Tensor w1, Tensor wf, Tensor g) -> (Tensor, Tensor)");
   m.def(
       "rel_proj_bwd(Tensor dpq, Tensor feat, Tensor fold, Tensor(a!) dfeat, "

@@ -84,15 +84,24 @@ def nt_f32_supported(parts, bt):
             and M > 0)
 
 
-def nt_f32(parts, bt, bias=None, relu=False, out=None):
+# fp32 products of the chunked NT GEMM on the bf16 matrix cores as bf16x6
+# (three bf16 terms per operand, six products, two fp32 accumulators; error
+# below the exact-f32 MFMA chain's, tests/test_gemm_f32.py) - the same
+# switch as ops/slot_gemm.py::X6 (DGMC_AMD_X6=0: exact-f32 kernels).
+NT_X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
+
+
+def nt_f32(parts, bt, bias=None, relu=False, out=None, x6=None):
     """``act([parts] @ bt^T + bias)`` (fp32, no autograd; parts read in
-    place, never concatenated)."""
+    place, never concatenated).  ``x6``: bf16x6 products (default
+    :data:`NT_X6`) or the exact-f32 chain."""
     b = None
     if bias is not None:
         b = bias.detach()
         if not b.is_contiguous():
             b = b.contiguous()
-    return _backend.ops().gemm_nt_f32(list(parts), bt, b, relu, out)
+    return _backend.ops().gemm_nt_f32(list(parts), bt, b, relu, out,
+                                      NT_X6 if x6 is None else bool(x6))
 
 
 class _LinearParts(torch.autograd.Function):

@@ -13,13 +13,17 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
+@pytest.mark.parametrize('x6', [False, True])
 @pytest.mark.parametrize('M,widths,Nn,bias,relu', [
     (19388 + 19572, [300], 768, False, False),     # RelConv layer 0 map
     (39000, [256], 768, False, False),             # layers 1, 2
     (39000, [300, 256, 256, 256], 256, True, False),   # final Linear
     (1000, [4, 132, 64], 64, True, True),          # tails, skinny tiles
     (77, [128], 128, False, True)])
-def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu):
+def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu, x6):
+    """Exact-f32 chain and bf16x6 (x6=True, the default arithmetic): max
+    error against fp64 at most twice torch's fp32 GEMM's; bf16x6 also at
+    most the exact-f32 kernel's."""
     g = torch.Generator(device=DEV).manual_seed(M + Nn)
     # parts as column slices of one wider buffer (strided rows)
     K = sum(widths)
@@ -31,7 +35,7 @@ def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu):
     wt = torch.randn(Nn, K, device=DEV, generator=g) / K ** 0.5
     b = torch.randn(Nn, device=DEV, generator=g) if bias else None
     assert gemm.nt_f32_supported(parts, wt)
-    y = gemm.nt_f32(parts, wt, b, relu)
+    y = gemm.nt_f32(parts, wt, b, relu, x6=x6)
     x = torch.cat(parts, 1)
     ref = x.double() @ wt.double().t()
     y32 = x @ wt.t()
@@ -43,6 +47,10 @@ def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu):
     e = float((y.double() - ref).abs().max())
     e32 = float((y32.double() - ref).abs().max())
     assert e <= 2 * e32 + 1e-7, (e, e32)
+    if x6:
+        ye = gemm.nt_f32(parts, wt, b, relu, x6=False)
+        ee = float((ye.double() - ref).abs().max())
+        assert e <= ee, (e, ee)
 
 
 def test_gemm_nt_f32_out_view_and_linear_parts():
