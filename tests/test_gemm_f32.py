@@ -101,3 +101,32 @@ def test_linear_fp32_on_native_nt_gemm(M, cin, cout, bias):
     for a, b in zip(g1, g2):
         torch.testing.assert_close(a, b, rtol=1e-4,
                                    atol=1e-5 * max(1.0, float(b.abs().max())))
+
+
+@pytest.mark.parametrize('seed', [0, 1, 2])
+@pytest.mark.parametrize('case', ['wide', 'cancel', 'relu'])
+def test_gemm_nt_x6_stress_vs_exact(case, seed):
+    """The bf16x6 chunked GEMM on the inputs of tests/test_x6_stress.py's
+    gate (DBP15K map shape, 300 -> 256): per-row error relative to the row's
+    largest fp64 value, at most the exact-f32 chain's."""
+    g = torch.Generator(device=DEV).manual_seed(100 + seed)
+    M, K, Nn = 4096, 300, 256
+    x = torch.randn(M, K, device=DEV, generator=g)
+    w = torch.randn(Nn, K, device=DEV, generator=g) / K ** 0.5
+    if case == 'wide':
+        e = torch.randint(-30, 31, (M, 1), device=DEV, generator=g)
+        x = x * torch.pow(2.0, e.float())
+    elif case == 'cancel':
+        h = K // 2
+        x[:, h:2 * h] = x[:, :h]
+        w[:, h:2 * h] = -w[:, :h] * (1 + 1e-3 * torch.randn(
+            Nn, h, device=DEV, generator=g))
+    else:
+        x = torch.relu(x - 0.2)
+    ref = x.double() @ w.double().t()
+    scale = ref.abs().amax(1, keepdim=True).clamp_min(1e-300)
+    errs = []
+    for x6 in (True, False):
+        y = gemm.nt_f32([x], w, None, False, x6=x6)
+        errs.append(float(((y.double() - ref).abs() / scale).amax()))
+    assert errs[0] <= errs[1], errs
