@@ -29,10 +29,10 @@ gradient and the documented subnormal limit.  The DBP15K config's node
 GEMMs (RelConv's stacked maps, the final Linears) run bf16x6 as well
 (``tests/test_gemm_f32.py``: error at or below the exact chain's); its
 fused RelConv aggregation and the top-k re-score stay exact fp32.  The
-JSON's ``gemm_arith`` names what ran.  ``--dtype bf16`` is an opt-in fast mode (bf16 operands),
-never the headline.  After the timed steps, held-out Hits@1 / Hits@10 of
-S_L are evaluated on ``--eval-pairs`` test pairs (untimed), like the
-reference's test loop.
+JSON's ``gemm_arith`` names what ran.  ``--dtype bf16`` is an opt-in fast
+mode (bf16 operands), never the headline.  After the timed steps,
+held-out Hits@1 / Hits@10 of S_L are evaluated on ``--eval-pairs`` test
+pairs (untimed), like the reference's test loop.
 
 Rank 0 prints ONE JSON line.  ``--impl reference`` measures the eager
 PyTorch expression of the reference algorithm (fp32, oracle ops, reference

@@ -287,10 +287,13 @@ class _MixedMatmul(torch.autograd.Function):
             g = g.to(w_lp.dtype)
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            if g.dtype == torch.float32 and w_lp.dim() == 2 and \
-                    w_lp.is_contiguous() and nt_f32_supported([g], w_lp):
-                # dX = g W: NT with Bt = W^T = w_lp ([in, out] contiguous)
-                gx = nt_f32([g], w_lp).to(ctx.x_dtype)
+            # dX = g W: NT with Bt = W^T = w_lp ([in, out]); a transposed
+            # view (linear's weight.t()) is made contiguous (<= 1 MB copy)
+            wb = w_lp if (w_lp.dim() != 2 or w_lp.is_contiguous() or
+                          w_lp.numel() > (1 << 18)) else w_lp.contiguous()
+            if g.dtype == torch.float32 and wb.dim() == 2 and \
+                    wb.is_contiguous() and nt_f32_supported([g], wb):
+                gx = nt_f32([g], wb).to(ctx.x_dtype)
             else:
                 gx = (g @ w_lp.t()).to(ctx.x_dtype)
         need_w = ctx.needs_input_grad[1]
