@@ -808,8 +808,9 @@ __global__ __launch_bounds__(256) void rel_fold_kernel(RcFold f, int rows,
 
 // Backward of the folded projection fold = W1 W_f (models/dgmc.py): from
 // its gradient g [R, K]: gw1 = g W_f^T [R, Kin], gwf = W1^T g [Kin, K].
-// One output per thread over the staged (L1 / L2-resident) operands,
-// k-ordered fmaf chains.
+// One output per thread over the staged (L1 / L2-resident) operands, four
+// interleaved fmaf chains (k mod 4) summed in a fixed order: four times
+// the latency-bound chain's throughput at R = 128, K = 384 (PascalVOC).
 __global__ __launch_bounds__(256) void fold_weights_bwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ wf,
     const float* __restrict__ g, float* __restrict__ gw1,
@@ -818,24 +819,29 @@ __global__ __launch_bounds__(256) void fold_weights_bwd_kernel(
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= R * Kin) return;
     const int r = t / Kin, m = t % Kin;
-    float s = 0.f;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll 8
     for (int k = 0; k < K; k += 4) {
       const float4 a = f4_ld(g + (size_t)r * K + k);
       const float4 b = f4_ld(wf + (size_t)m * K + k);
-      s = fmaf(a.x, b.x, s); s = fmaf(a.y, b.y, s);
-      s = fmaf(a.z, b.z, s); s = fmaf(a.w, b.w, s);
+      s0 = fmaf(a.x, b.x, s0); s1 = fmaf(a.y, b.y, s1);
+      s2 = fmaf(a.z, b.z, s2); s3 = fmaf(a.w, b.w, s3);
     }
-    gw1[t] = s;
+    gw1[t] = (s0 + s1) + (s2 + s3);
     return;
   }
   const int t = (blockIdx.x - nb1) * 256 + threadIdx.x;
   if (t >= Kin * K) return;
   const int m = t / K, k = t % K;
-  float s = 0.f;
-#pragma unroll 16
-  for (int r = 0; r < R; ++r) s = fmaf(w1[r * Kin + m], g[(size_t)r * K + k], s);
-  gwf[t] = s;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = 0;
+#pragma unroll 4
+  for (; r + 4 <= R; r += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      s[u] = fmaf(w1[(r + u) * Kin + m], g[(size_t)(r + u) * K + k], s[u]);
+  for (; r < R; ++r) s[0] = fmaf(w1[r * Kin + m], g[(size_t)r * K + k], s[0]);
+  gwf[t] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 RcPlan make_plan(const at::Tensor& ptr, const at::Tensor& col,

@@ -107,10 +107,19 @@ class _FoldProduct(torch.autograd.Function):
         if g is None:
             return None, None, None
         g = g.float()
-        gw1 = (g @ wf.float().t()).to(w1.dtype) \
-            if ctx.needs_input_grad[0] else None
-        gwf = (w1.float().t() @ g).to(wf.dtype) \
-            if ctx.needs_input_grad[1] else None
+        if _backend.use_hip(w1) and w1.dtype == wf.dtype == torch.float32 \
+                and wf.size(1) % 4 == 0:
+            # both products in one launch (relconv.hip::fold_weights_bwd:
+            # k-ordered fp32 chains, no library GEMM in the step)
+            gw1, gwf = _backend.ops().fold_weights_bwd(
+                w1.contiguous(), wf.contiguous(), g.contiguous())
+            gw1 = gw1 if ctx.needs_input_grad[0] else None
+            gwf = gwf if ctx.needs_input_grad[1] else None
+        else:
+            gw1 = (g @ wf.float().t()).to(w1.dtype) \
+                if ctx.needs_input_grad[0] else None
+            gwf = (w1.float().t() @ g).to(wf.dtype) \
+                if ctx.needs_input_grad[1] else None
         gbf = None
         if ctx.bf_like is not None and ctx.needs_input_grad[2]:
             gbf = g.new_zeros(ctx.bf_like[0], dtype=ctx.bf_like[1])
