@@ -136,6 +136,71 @@ __global__ __launch_bounds__(256) void nll_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Sparse NLL (+ Hits@1) over top-k candidate lists (reference dgmc.py:
+// 258-266: val = S.__val__[y0][S.__idx__[y0] == y1]; nll = -log(val + eps)).
+// Every candidate slot of row y0_g holding target y1_g contributes (a
+// ground truth missing from the candidates contributes nothing, duplicates
+// count per slot); 'mean' divides by the number of contributing slots.
+//   aux = [hits, correct, ground truths]  (correct: the row's first maximal
+//   candidate is y1_g).  One workgroup, fixed-order reduction.
+// The backward writes dval[y0_g, c] = -grad / ((val + eps) div) with atomics
+// only where two ground truths name the same (row, target): identical
+// addends, so the sum does not depend on their order (deterministic).  This
+// replaces the ATen chain of advanced-indexing gathers and the sort-based
+// index_put backward (~25 launches per DBP15K step).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kLossThreads) void sparse_nll_fwd_kernel(
+    const float* __restrict__ val, const int64_t* __restrict__ idx,
+    const int64_t* __restrict__ y0, const int64_t* __restrict__ y1,
+    const bool* __restrict__ mask, float* __restrict__ loss,
+    float* __restrict__ aux, int G, int K, float eps, int mean) {
+  __shared__ float red[kLossThreads / kWave];
+  float acc = 0.f, hits = 0.f, cor = 0.f, cnt = 0.f;
+  for (int g = threadIdx.x; g < G; g += kLossThreads) {
+    if (mask != nullptr && !mask[g]) continue;
+    const size_t o = (size_t)y0[g] * K;
+    const int64_t t = y1[g];
+    float best = -INFINITY;
+    int64_t pred = -1;
+    for (int c = 0; c < K; ++c) {
+      const float v = val[o + c];
+      const int64_t j = idx[o + c];
+      if (j == t) { acc += -__logf(v + eps); hits += 1.f; }
+      if (v > best || pred < 0) { best = v; pred = j; }
+    }
+    cor += pred == t ? 1.f : 0.f;
+    cnt += 1.f;
+  }
+  acc = block_sum(acc, red);
+  hits = block_sum(hits, red);
+  cor = block_sum(cor, red);
+  cnt = block_sum(cnt, red);
+  if (threadIdx.x == 0) {
+    loss[0] = mean ? acc / fmaxf(hits, 1.f) : acc;
+    aux[0] = hits;
+    aux[1] = cor;
+    aux[2] = cnt;
+  }
+}
+
+__global__ __launch_bounds__(256) void sparse_nll_bwd_kernel(
+    const float* __restrict__ grad, const float* __restrict__ val,
+    const int64_t* __restrict__ idx, const int64_t* __restrict__ y0,
+    const int64_t* __restrict__ y1, const bool* __restrict__ mask,
+    const float* __restrict__ aux, float* __restrict__ dval, int G, int K,
+    float eps, int mean) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  if (mask != nullptr && !mask[g]) return;
+  const float div = mean ? fmaxf(aux[0], 1.f) : 1.f;
+  const size_t o = (size_t)y0[g] * K;
+  const int64_t t = y1[g];
+  for (int c = 0; c < K; ++c)
+    if (idx[o + c] == t)
+      atomicAdd(dval + o + c, -grad[0] / ((val[o + c] + eps) * div));
+}
+
+// ---------------------------------------------------------------------------
 // Fused masked row softmax + NLL + Hits@1 of the dense correspondences, for
 // the training objective (DGMC.loss / DGMC.acc, dgmc.py:246-288, on
 // masked_softmax(S_hat), dgmc.py:15-19,165,181).  Ground truth of packed row
@@ -441,6 +506,72 @@ at::Tensor nll_bwd(const at::Tensor& grad, const at::Tensor& S,
                      (int)S.size(1), (float)eps, mean ? 1 : 0);
   DGMC_CHECK_LAUNCH();
   return dS;
+}
+
+static void check_sparse_nll_args(const at::Tensor& val,
+                                  const at::Tensor& idx, const at::Tensor& y0,
+                                  const at::Tensor& y1,
+                                  const c10::optional<at::Tensor>& mask) {
+  TORCH_CHECK(val.is_cuda() && val.scalar_type() == at::kFloat &&
+                  val.is_contiguous() && val.dim() == 2,
+              "sparse_nll: contiguous fp32 [rows, k] candidate values");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.is_contiguous() &&
+                  idx.sizes() == val.sizes(),
+              "sparse_nll: int64 [rows, k] candidate indices like val");
+  TORCH_CHECK(y0.scalar_type() == at::kLong && y1.scalar_type() == at::kLong &&
+                  y0.is_contiguous() && y1.is_contiguous() &&
+                  y0.numel() == y1.numel(),
+              "sparse_nll: int64 contiguous y0 / y1 of equal length");
+  if (mask.has_value() && mask->defined())
+    TORCH_CHECK(mask->scalar_type() == at::kBool && mask->is_contiguous() &&
+                    mask->numel() == y0.numel(),
+                "sparse_nll: bool mask per ground truth");
+}
+
+std::tuple<at::Tensor, at::Tensor> sparse_nll_fwd(
+    const at::Tensor& val, const at::Tensor& idx, const at::Tensor& y0,
+    const at::Tensor& y1, const c10::optional<at::Tensor>& mask, double eps,
+    bool mean) {
+  check_sparse_nll_args(val, idx, y0, y1, mask);
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(val.device());
+  at::Tensor loss = at::empty({}, val.options());
+  at::Tensor aux = at::empty({3}, val.options());
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  hipLaunchKernelGGL(sparse_nll_fwd_kernel, dim3(1), dim3(kLossThreads), 0,
+                     stream(), val.data_ptr<float>(), idx.data_ptr<int64_t>(),
+                     y0.data_ptr<int64_t>(), y1.data_ptr<int64_t>(), mp,
+                     loss.data_ptr<float>(), aux.data_ptr<float>(),
+                     (int)y0.numel(), (int)val.size(1), (float)eps,
+                     mean ? 1 : 0);
+  DGMC_CHECK_LAUNCH();
+  return {loss, aux};
+}
+
+at::Tensor sparse_nll_bwd(const at::Tensor& grad, const at::Tensor& val,
+                          const at::Tensor& idx, const at::Tensor& y0,
+                          const at::Tensor& y1,
+                          const c10::optional<at::Tensor>& mask,
+                          const at::Tensor& aux, double eps, bool mean) {
+  check_sparse_nll_args(val, idx, y0, y1, mask);
+  TORCH_CHECK(grad.numel() == 1 && grad.scalar_type() == at::kFloat &&
+                  aux.numel() == 3 && aux.scalar_type() == at::kFloat,
+              "sparse_nll_bwd: scalar fp32 grad, [3] aux");
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(val.device());
+  at::Tensor dval = at::zeros_like(val);
+  const int G = y0.numel();
+  if (G == 0) return dval;
+  const bool* mp = (mask.has_value() && mask->defined())
+                       ? mask->data_ptr<bool>() : nullptr;
+  at::Tensor g = grad.contiguous();
+  hipLaunchKernelGGL(sparse_nll_bwd_kernel, dim3((G + 255) / 256), dim3(256),
+                     0, stream(), g.data_ptr<float>(), val.data_ptr<float>(),
+                     idx.data_ptr<int64_t>(), y0.data_ptr<int64_t>(),
+                     y1.data_ptr<int64_t>(), mp, aux.data_ptr<float>(),
+                     dval.data_ptr<float>(), G, (int)val.size(1), (float)eps,
+                     mean ? 1 : 0);
+  DGMC_CHECK_LAUNCH();
+  return dval;
 }
 
 void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,

@@ -173,6 +173,15 @@ at::Tensor nll_bwd(const at::Tensor& grad, const at::Tensor& S,
                    const at::Tensor& y0, const at::Tensor& y1,
                    const c10::optional<at::Tensor>& mask, const at::Tensor& aux,
                    double eps, bool mean);
+std::tuple<at::Tensor, at::Tensor> sparse_nll_fwd(
+    const at::Tensor& val, const at::Tensor& idx, const at::Tensor& y0,
+    const at::Tensor& y1, const c10::optional<at::Tensor>& mask, double eps,
+    bool mean);
+at::Tensor sparse_nll_bwd(const at::Tensor& grad, const at::Tensor& val,
+                          const at::Tensor& idx, const at::Tensor& y0,
+                          const at::Tensor& y1,
+                          const c10::optional<at::Tensor>& mask,
+                          const at::Tensor& aux, double eps, bool mean);
 void nonfinite_flag(const at::Tensor& x, at::Tensor found_inf,
                     const c10::optional<at::Tensor>& counter);
 at::Tensor slot_conv_stamps();
@@ -429,6 +438,12 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "nll_bwd(Tensor grad, Tensor S, Tensor y0, Tensor y1, Tensor? mask, "
       "Tensor aux, float eps, bool mean) -> Tensor");
   m.def(
+      "sparse_nll_fwd(Tensor val, Tensor idx, Tensor y0, Tensor y1, Tensor? "
+      "mask, float eps, bool mean) -> (Tensor, Tensor)");
+  m.def(
+      "sparse_nll_bwd(Tensor grad, Tensor val, Tensor idx, Tensor y0, Tensor "
+      "y1, Tensor? mask, Tensor aux, float eps, bool mean) -> Tensor");
+  m.def(
       "nonfinite_flag(Tensor x, Tensor(a!) found_inf, Tensor(b!)? counter=None)"
       " -> ()");
   m.def(
@@ -626,6 +641,8 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("masked_softmax_packed_bwd", &dgmc::masked_softmax_packed_bwd);
   m.impl("nll_fwd", &dgmc::nll_fwd);
   m.impl("nll_bwd", &dgmc::nll_bwd);
+  m.impl("sparse_nll_fwd", &dgmc::sparse_nll_fwd);
+  m.impl("sparse_nll_bwd", &dgmc::sparse_nll_bwd);
   m.impl("nonfinite_flag", &dgmc::nonfinite_flag);
   m.impl("assemble_slot_plan", &dgmc::assemble_slot_plan);
   m.impl("slot_conv", &dgmc::slot_conv);

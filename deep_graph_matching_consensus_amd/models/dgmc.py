@@ -77,6 +77,32 @@ class _PackedNLL(torch.autograd.Function):
         return dS, None, None, None, None, None
 
 
+class _SparseNLL(torch.autograd.Function):
+    """NLL of the ground truths over top-k candidate lists (+ Hits@1 and
+    ground-truth counts), HIP: ``csrc/hip/loss.hip::sparse_nll_*``
+    (reference ``dgmc.py:258-266``)."""
+
+    @staticmethod
+    def forward(ctx, val, idx, y0, y1, mask, mean):
+        loss, aux = _backend.ops().sparse_nll_fwd(val, idx, y0, y1, mask,
+                                                  EPS, mean)
+        ctx.save_for_backward(val, idx, y0, y1, mask, aux)
+        ctx.mean = mean
+        ctx.mark_non_differentiable(aux)
+        ctx.set_materialize_grads(False)
+        return loss, aux
+
+    @staticmethod
+    def backward(ctx, grad, grad_aux):
+        if grad is None:
+            return (None, ) * 6
+        val, idx, y0, y1, mask, aux = ctx.saved_tensors
+        dval = _backend.ops().sparse_nll_bwd(grad.float().contiguous(), val,
+                                             idx, y0, y1, mask, aux, EPS,
+                                             ctx.mean)
+        return dval, None, None, None, None, None
+
+
 class _FoldProduct(torch.autograd.Function):
     """``W1 @ W_f`` in fp32 (the folded consensus projection; ``b_f`` rides
     along with an exact zero gradient)."""
@@ -699,6 +725,10 @@ class DGMC(torch.nn.Module):
         if self._fused_nll_ok(S, y, reduction, mask):
             return _PackedNLL.apply(S, y[0].contiguous(), y[1].contiguous(),
                                     mask, reduction == 'mean', False)[0]
+        if self._fused_sparse_nll_ok(S, y, reduction, mask):
+            return _SparseNLL.apply(S.__val__, S.__idx__, y[0].contiguous(),
+                                    y[1].contiguous(), mask,
+                                    reduction == 'mean')[0]
         if not S.is_sparse:
             nll = -torch.log(S[y[0], y[1]] + EPS)
             weight = mask
@@ -727,6 +757,18 @@ class DGMC(torch.nn.Module):
                 (mask is None or mask.dtype == torch.bool) and
                 not is_reference_mode() and _backend.use_hip(S))
 
+    @staticmethod
+    def _fused_sparse_nll_ok(S, y, reduction, mask):
+        if not (S.is_sparse and reduction != 'none'):
+            return False
+        val, idx = getattr(S, '__val__', None), getattr(S, '__idx__', None)
+        return (val is not None and idx is not None and val.dim() == 2 and
+                val.dtype == torch.float32 and val.is_contiguous() and
+                idx.dtype == torch.long and idx.is_contiguous() and
+                idx.shape == val.shape and y.dtype == torch.long and
+                (mask is None or mask.dtype == torch.bool) and
+                not is_reference_mode() and _backend.use_hip(val))
+
     def loss_stats(self, S, y, mask=None):
         """``(loss (mean), ground-truth count, correct top-1 count)`` as device
         tensors - :meth:`loss` and :meth:`correct` in one pass (one fused
@@ -735,6 +777,11 @@ class DGMC(torch.nn.Module):
             loss, aux = _PackedNLL.apply(S, y[0].contiguous(),
                                          y[1].contiguous(), mask, True, True)
             return loss, aux[0], aux[1]
+        if self._fused_sparse_nll_ok(S, y, 'mean', mask):
+            loss, aux = _SparseNLL.apply(S.__val__, S.__idx__,
+                                         y[0].contiguous(), y[1].contiguous(),
+                                         mask, True)
+            return loss, aux[2], aux[1]
         loss = self.loss(S, y, mask=mask)
         count = (torch.full((), y.size(1), dtype=torch.float32,
                             device=S.device) if mask is None else

@@ -877,6 +877,65 @@ def test_fused_nll_and_hits(masked, reduction):
     assert int(cor) == int(((pred == y[1]) & m).sum())
 
 
+def _sparse_S(val, idx, Nt):
+    rows, k = val.shape
+    row = torch.arange(rows, device=val.device).view(-1, 1).expand(-1, k)
+    S = torch.sparse_coo_tensor(torch.stack([row.reshape(-1),
+                                             idx.reshape(-1)]),
+                                val.reshape(-1), (rows, Nt),
+                                requires_grad=val.requires_grad)
+    S.__idx__, S.__val__ = idx, val
+    return S
+
+
+@pytest.mark.parametrize('masked', [False, True])
+@pytest.mark.parametrize('reduction', ['mean', 'sum'])
+def test_fused_sparse_nll_and_hits(masked, reduction):
+    """Native sparse NLL (loss.hip::sparse_nll_*) against the reference
+    expression (dgmc.py:258-266): ground truths outside the candidates,
+    duplicated ground truths (same row and target, same row other target),
+    ties in the candidate values, and the ground-truth mask."""
+    from deep_graph_matching_consensus_amd.models import DGMC, MLP
+    g = torch.Generator(device='cpu').manual_seed(3)
+    rows, Nt, k, G = 901, 4000, 12, 600
+    idx = torch.stack([torch.randperm(Nt, generator=g)[:k]
+                       for _ in range(rows)]).to(DEV)
+    val = torch.randn(rows, k, generator=g).to(DEV).softmax(-1)
+    val[5, 3] = val[5, 7] = val[5].max()        # tie: first slot wins
+    val = val.requires_grad_()
+    y0 = torch.randperm(rows, generator=g)[:G].to(DEV)
+    slot = torch.randint(0, k, (G, ), generator=g).to(DEV)
+    y1 = idx[y0, slot]
+    y1[::7] = torch.randint(0, Nt, (y1[::7].numel(), ), generator=g).to(DEV)
+    y0 = torch.cat([y0, y0[:20], y0[20:30]])     # duplicated ground truths
+    y1 = torch.cat([y1, y1[:20], idx[y0[20:30], (slot[20:30] + 1) % k]])
+    y0[-1] = 5
+    y1[-1] = idx[5, 7]
+    y = torch.stack([y0, y1])
+    mask = (torch.rand(y.size(1), generator=g) > 0.3).to(DEV) \
+        if masked else None
+    model = DGMC(MLP(4, 4, 1), MLP(4, 4, 1), num_steps=1)
+    S = _sparse_S(val, idx, Nt)
+    assert model._fused_sparse_nll_ok(S, y, reduction, mask)
+    loss = model.loss(S, y, reduction=reduction, mask=mask)
+    with reference_mode():
+        loss2 = model.loss(S, y, reduction=reduction, mask=mask)
+    assert torch.allclose(loss, loss2, rtol=1e-5, atol=1e-6)
+    ga = torch.autograd.grad(loss, val)[0]
+    gb = torch.autograd.grad(loss2, val)[0]
+    assert torch.allclose(ga, gb, rtol=1e-5, atol=1e-7)
+    assert torch.equal(ga, torch.autograd.grad(
+        model.loss(S, y, reduction=reduction, mask=mask), val)[0])
+    l3, cnt, cor = model.loss_stats(S, y, mask)
+    m = mask if masked else torch.ones(y.size(1), dtype=torch.bool,
+                                       device=DEV)
+    assert int(cnt) == int(m.sum())
+    pred = idx[y[0], val.detach()[y[0]].argmax(-1)]
+    assert int(cor) == int(((pred == y[1]) & m).sum())
+    if reduction == 'mean':
+        assert torch.allclose(l3, loss2, rtol=1e-5, atol=1e-6)
+
+
 def test_nonfinite_flag():
     x = torch.randn(1000003, device=DEV)
     flag = torch.full((), 7.0, device=DEV)
