@@ -142,26 +142,31 @@ __global__ __launch_bounds__(256) void nll_bwd_kernel(
 // ground truth missing from the candidates contributes nothing, duplicates
 // count per slot); 'mean' divides by the number of contributing slots.
 //   aux = [hits, correct, ground truths]  (correct: the row's first maximal
-//   candidate is y1_g).  One workgroup, fixed-order reduction.
+//   candidate is y1_g).  Per-block partials + a one-wave fold (fixed order).
 // The backward writes dval[y0_g, c] = -grad / ((val + eps) div) with atomics
 // only where two ground truths name the same (row, target): identical
 // addends, so the sum does not depend on their order (deterministic).  This
 // replaces the ATen chain of advanced-indexing gathers and the sort-based
 // index_put backward (~25 launches per DBP15K step).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kLossThreads) void sparse_nll_fwd_kernel(
+constexpr int kSnllMaxBlocks = 256;
+
+// Stage 1: one ground truth per thread; per-block partials
+// part[block] = {sum nll, hits, correct, ground truths}.
+__global__ __launch_bounds__(256) void sparse_nll_part_kernel(
     const float* __restrict__ val, const int64_t* __restrict__ idx,
     const int64_t* __restrict__ y0, const int64_t* __restrict__ y1,
-    const bool* __restrict__ mask, float* __restrict__ loss,
-    float* __restrict__ aux, int G, int K, float eps, int mean) {
-  __shared__ float red[kLossThreads / kWave];
+    const bool* __restrict__ mask, float4* __restrict__ part, int G, int K,
+    float eps) {
+  __shared__ float4 red[4];
   float acc = 0.f, hits = 0.f, cor = 0.f, cnt = 0.f;
-  for (int g = threadIdx.x; g < G; g += kLossThreads) {
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < G; g += gridDim.x * 256) {
     if (mask != nullptr && !mask[g]) continue;
     const size_t o = (size_t)y0[g] * K;
     const int64_t t = y1[g];
     float best = -INFINITY;
     int64_t pred = -1;
+#pragma unroll 4
     for (int c = 0; c < K; ++c) {
       const float v = val[o + c];
       const int64_t j = idx[o + c];
@@ -171,15 +176,41 @@ __global__ __launch_bounds__(kLossThreads) void sparse_nll_fwd_kernel(
     cor += pred == t ? 1.f : 0.f;
     cnt += 1.f;
   }
-  acc = block_sum(acc, red);
-  hits = block_sum(hits, red);
-  cor = block_sum(cor, red);
-  cnt = block_sum(cnt, red);
+  acc = wave_sum(acc);
+  hits = wave_sum(hits);
+  cor = wave_sum(cor);
+  cnt = wave_sum(cnt);
+  const int wave = threadIdx.x / kWave;
+  if (threadIdx.x % kWave == 0) red[wave] = make_float4(acc, hits, cor, cnt);
+  __syncthreads();
   if (threadIdx.x == 0) {
-    loss[0] = mean ? acc / fmaxf(hits, 1.f) : acc;
-    aux[0] = hits;
-    aux[1] = cor;
-    aux[2] = cnt;
+    float4 t = red[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      t.x += red[w].x; t.y += red[w].y; t.z += red[w].z; t.w += red[w].w;
+    }
+    part[blockIdx.x] = t;
+  }
+}
+
+// Stage 2 (one wave, fixed order): loss and aux = [hits, correct, count].
+__global__ __launch_bounds__(64) void sparse_nll_fold_kernel(
+    const float4* __restrict__ part, int nparts, float* __restrict__ loss,
+    float* __restrict__ aux, int mean) {
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = threadIdx.x; b < nparts; b += kWave) {
+    const float4 q = part[b];
+    t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+  }
+  t.x = wave_sum(t.x);
+  t.y = wave_sum(t.y);
+  t.z = wave_sum(t.z);
+  t.w = wave_sum(t.w);
+  if (threadIdx.x == 0) {
+    loss[0] = mean ? t.x / fmaxf(t.y, 1.f) : t.x;
+    aux[0] = t.y;
+    aux[1] = t.z;
+    aux[2] = t.w;
   }
 }
 
@@ -538,11 +569,17 @@ std::tuple<at::Tensor, at::Tensor> sparse_nll_fwd(
   at::Tensor aux = at::empty({3}, val.options());
   const bool* mp = (mask.has_value() && mask->defined())
                        ? mask->data_ptr<bool>() : nullptr;
-  hipLaunchKernelGGL(sparse_nll_fwd_kernel, dim3(1), dim3(kLossThreads), 0,
-                     stream(), val.data_ptr<float>(), idx.data_ptr<int64_t>(),
-                     y0.data_ptr<int64_t>(), y1.data_ptr<int64_t>(), mp,
-                     loss.data_ptr<float>(), aux.data_ptr<float>(),
-                     (int)y0.numel(), (int)val.size(1), (float)eps,
+  const int G = y0.numel();
+  const int nb = std::max(1, std::min(kSnllMaxBlocks, (G + 255) / 256));
+  at::Tensor part = at::empty({nb, 4}, val.options());
+  float4* pp = reinterpret_cast<float4*>(part.data_ptr<float>());
+  hipLaunchKernelGGL(sparse_nll_part_kernel, dim3(nb), dim3(256), 0, stream(),
+                     val.data_ptr<float>(), idx.data_ptr<int64_t>(),
+                     y0.data_ptr<int64_t>(), y1.data_ptr<int64_t>(), mp, pp,
+                     G, (int)val.size(1), (float)eps);
+  DGMC_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sparse_nll_fold_kernel, dim3(1), dim3(64), 0, stream(),
+                     pp, nb, loss.data_ptr<float>(), aux.data_ptr<float>(),
                      mean ? 1 : 0);
   DGMC_CHECK_LAUNCH();
   return {loss, aux};

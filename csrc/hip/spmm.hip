@@ -325,11 +325,47 @@ void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
 // reads entry values through a permutation, so a CSC walk over the CSR
 // values (val[perm[e]]) needs no gathered copy of them.
 // ---------------------------------------------------------------------------
+// Piece pointers: pptr[r] = sum_{r' < r} max(1, ceil(count_r' / T)), one
+// 1024-thread workgroup (contiguous row ranges per thread, LDS scan of the
+// thread totals) - one launch instead of an ATen count / divide / clamp /
+// cumsum / copy chain.
+constexpr int kPpThreads = 1024;
+__global__ __launch_bounds__(kPpThreads) void piece_ptr_kernel(
+    const int* __restrict__ rowptr, int R, int T, int* __restrict__ pptr) {
+  __shared__ int tot[kPpThreads];
+  const int per = (R + kPpThreads - 1) / kPpThreads;
+  const int r0 = min(R, (int)threadIdx.x * per), r1 = min(R, r0 + per);
+  int s = 0;
+  for (int r = r0; r < r1; ++r)
+    s += max(1, (rowptr[r + 1] - rowptr[r] + T - 1) / T);
+  tot[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < kPpThreads; d <<= 1) {     // inclusive Hillis-Steele
+    const int v = threadIdx.x >= d ? tot[threadIdx.x - d] : 0;
+    __syncthreads();
+    tot[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = threadIdx.x > 0 ? tot[threadIdx.x - 1] : 0;
+  for (int r = r0; r < r1; ++r) {
+    pptr[r] = run;
+    run += max(1, (rowptr[r + 1] - rowptr[r] + T - 1) / T);
+  }
+  if (threadIdx.x == kPpThreads - 1) pptr[R] = tot[kPpThreads - 1];
+}
+
+// One thread per row (its pieces) and per piece slot (slots past pptr[R]
+// are marked unused: prow = R, empty range).
 __global__ __launch_bounds__(256) void piece_plan_fill_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ pptr, int R,
-    int T, int* __restrict__ prow, int* __restrict__ pbeg,
+    int T, int P, int* __restrict__ prow, int* __restrict__ pbeg,
     int* __restrict__ pend) {
   const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < P && r >= pptr[R]) {
+    prow[r] = R;
+    pbeg[r] = 0;
+    pend[r] = 0;
+  }
   if (r >= R) return;
   const int q0 = pptr[r], np = pptr[r + 1] - q0;
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
@@ -353,21 +389,21 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
   const int64_t R = rowptr.numel() - 1;
   const int64_t P = R + nnz / T + 1;
   TORCH_CHECK(P < INT32_MAX, "piece_plan: size");
-  at::Tensor counts = rowptr.slice(0, 1) - rowptr.slice(0, 0, R);
-  at::Tensor npc = at::clamp_min(at::floor_divide(counts + (int)(T - 1), T), 1);
-  at::Tensor pptr = at::zeros({R + 1}, rowptr.options());
-  if (R > 0) pptr.slice(0, 1).copy_(at::cumsum(npc, 0, at::kInt));
-  at::Tensor prow = at::full({P}, (int)R, rowptr.options());
-  at::Tensor pbeg = at::zeros({P}, rowptr.options());
-  at::Tensor pend = at::zeros({P}, rowptr.options());
-  if (R > 0) {
-    hipLaunchKernelGGL(piece_plan_fill_kernel, dim3((unsigned)((R + 255) / 256)),
-                       dim3(256), 0, stream(), rowptr.data_ptr<int>(),
-                       pptr.data_ptr<int>(), (int)R, (int)T,
-                       prow.data_ptr<int>(), pbeg.data_ptr<int>(),
-                       pend.data_ptr<int>());
-    DGMC_CHECK_LAUNCH();
-  }
+  at::Tensor pptr = at::empty({R + 1}, rowptr.options());
+  at::Tensor prow = at::empty({P}, rowptr.options());
+  at::Tensor pbeg = at::empty({P}, rowptr.options());
+  at::Tensor pend = at::empty({P}, rowptr.options());
+  hipLaunchKernelGGL(piece_ptr_kernel, dim3(1), dim3(kPpThreads), 0, stream(),
+                     rowptr.data_ptr<int>(), (int)R, (int)T,
+                     pptr.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
+  const int64_t m = std::max<int64_t>(R, P);
+  hipLaunchKernelGGL(piece_plan_fill_kernel, dim3((unsigned)((m + 255) / 256)),
+                     dim3(256), 0, stream(), rowptr.data_ptr<int>(),
+                     pptr.data_ptr<int>(), (int)R, (int)T, (int)P,
+                     prow.data_ptr<int>(), pbeg.data_ptr<int>(),
+                     pend.data_ptr<int>());
+  DGMC_CHECK_LAUNCH();
   return {pptr, prow, pbeg, pend};
 }
 

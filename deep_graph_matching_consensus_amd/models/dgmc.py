@@ -579,9 +579,17 @@ class DGMC(torch.nn.Module):
                                   S_hat.softmax(dim=-1))
             S_idx = lay_s.to_sparse(S_idx)
 
-        row = torch.arange(x_s.size(0), device=device).view(-1, 1)
-        row = row.expand(-1, k)
-        idx = torch.stack([row.reshape(-1), S_idx.reshape(-1)], dim=0)
+        # COO row indices are a function of (N_s, k) only: built once and
+        # kept (one stack kernel per forward instead of arange + copy + cat).
+        key = (x_s.size(0), k, str(device))
+        row = self.__dict__.setdefault('_coo_rows', {}).get(key)
+        if row is None:
+            row = torch.arange(x_s.size(0), device=device).view(-1, 1)
+            row = row.expand(-1, k).reshape(-1)
+            if not (device.type == 'cuda' and
+                    torch.cuda.is_current_stream_capturing()):
+                self._coo_rows[key] = row   # (never a graph-pool tensor)
+        idx = torch.stack([row, S_idx.reshape(-1)], dim=0)
         size = torch.Size([x_s.size(0), N_t])
         out = []
         for val in (S_0, S_L):

@@ -151,12 +151,13 @@ def test_spmm_split_static_operator(C, dtype):
 
 def test_piece_plan_hip_matches_torch():
     from deep_graph_matching_consensus_amd.ops.sparse import piece_plan
-    op = _skewed_op(300, 257, DEV)
-    for T in (1, 16, 64):
-        a = piece_plan(op.rowptr, op.nnz, T)
-        b = piece_plan(op.rowptr.cpu(), op.nnz, T)
-        for x, y in zip(a, b):
-            assert torch.equal(x.cpu(), y)
+    # (20011 rows: several rows per scan thread, a partial last thread)
+    for op in (_skewed_op(300, 257, DEV), _skewed_op(20011, 257, DEV)):
+        for T in (1, 16, 64):
+            a = piece_plan(op.rowptr, op.nnz, T)
+            b = piece_plan(op.rowptr.cpu(), op.nnz, T)
+            for x, y in zip(a, b):
+                assert torch.equal(x.cpu(), y)
 
 
 def test_spmm_pieces_self_term_and_perm():
