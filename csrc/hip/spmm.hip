@@ -325,56 +325,86 @@ void spmm_csr_out(const at::Tensor& rowptr, const at::Tensor& col,
 // reads entry values through a permutation, so a CSC walk over the CSR
 // values (val[perm[e]]) needs no gathered copy of them.
 // ---------------------------------------------------------------------------
-// Piece pointers: pptr[r] = sum_{r' < r} max(1, ceil(count_r' / T)), one
-// 1024-thread workgroup (contiguous row ranges per thread, LDS scan of the
-// thread totals) - one launch instead of an ATen count / divide / clamp /
-// cumsum / copy chain.
-constexpr int kPpThreads = 1024;
-__global__ __launch_bounds__(kPpThreads) void piece_ptr_kernel(
-    const int* __restrict__ rowptr, int R, int T, int* __restrict__ pptr) {
-  __shared__ int tot[kPpThreads];
-  const int per = (R + kPpThreads - 1) / kPpThreads;
-  const int r0 = min(R, (int)threadIdx.x * per), r1 = min(R, r0 + per);
-  int s = 0;
-  for (int r = r0; r < r1; ++r)
-    s += max(1, (rowptr[r + 1] - rowptr[r] + T - 1) / T);
-  tot[threadIdx.x] = s;
-  __syncthreads();
-  for (int d = 1; d < kPpThreads; d <<= 1) {     // inclusive Hillis-Steele
-    const int v = threadIdx.x >= d ? tot[threadIdx.x - d] : 0;
-    __syncthreads();
-    tot[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int run = threadIdx.x > 0 ? tot[threadIdx.x - 1] : 0;
-  for (int r = r0; r < r1; ++r) {
-    pptr[r] = run;
-    run += max(1, (rowptr[r + 1] - rowptr[r] + T - 1) / T);
-  }
-  if (threadIdx.x == kPpThreads - 1) pptr[R] = tot[kPpThreads - 1];
+// Piece plan in two fully parallel launches (instead of an ATen count /
+// divide / clamp / cumsum / copy / fill chain in front of a fill kernel):
+//   piece_count  one row per thread, per-block totals of the piece counts
+//                max(1, ceil(count / T));
+//   piece_fill   every block sums the totals of the blocks before it (and
+//                all of them: the number of used slots), scans its own rows
+//                (wave shuffles + LDS), writes pptr and its rows' pieces, and
+//                marks the piece slots past the total unused (prow = R).
+__device__ __forceinline__ int piece_count(const int* __restrict__ rowptr,
+                                           int r, int R, int T) {
+  return r < R ? max(1, (rowptr[r + 1] - rowptr[r] + T - 1) / T) : 0;
 }
 
-// One thread per row (its pieces) and per piece slot (slots past pptr[R]
-// are marked unused: prow = R, empty range).
+__global__ __launch_bounds__(256) void piece_count_kernel(
+    const int* __restrict__ rowptr, int R, int T, int* __restrict__ part) {
+  __shared__ int red[4];
+  const int c = piece_count(rowptr, blockIdx.x * 256 + threadIdx.x, R, T);
+  int v = c;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
 __global__ __launch_bounds__(256) void piece_plan_fill_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ pptr, int R,
-    int T, int P, int* __restrict__ prow, int* __restrict__ pbeg,
-    int* __restrict__ pend) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r < P && r >= pptr[R]) {
+    const int* __restrict__ rowptr, const int* __restrict__ part, int nb,
+    int R, int T, int P, int* __restrict__ pptr, int* __restrict__ prow,
+    int* __restrict__ pbeg, int* __restrict__ pend) {
+  __shared__ int red[3][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x;
+  int before = 0, all = 0;                 // block totals (fixed order)
+  for (int q = tid; q < nb; q += 256) {
+    const int v = part[q];
+    before += q < b ? v : 0;
+    all += v;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    before += __shfl_xor(before, d);
+    all += __shfl_xor(all, d);
+  }
+  const int r = b * 256 + tid;
+  const int c = piece_count(rowptr, r, R, T);
+  int inc = c;                             // wave-inclusive scan
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(inc, d);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) red[0][wave] = inc;
+  if (lane == 0) {
+    red[1][wave] = before;
+    red[2][wave] = all;
+  }
+  __syncthreads();
+  int base = 0, total = 0, woff = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    base += red[1][w];
+    total += red[2][w];
+    woff += w < wave ? red[0][w] : 0;
+  }
+  if (b == 0 && tid == 0) pptr[R] = total;
+  if (r < P && r >= total) {
     prow[r] = R;
     pbeg[r] = 0;
     pend[r] = 0;
   }
   if (r >= R) return;
-  const int q0 = pptr[r], np = pptr[r + 1] - q0;
+  const int q0 = base + woff + inc - c, np = c;
+  pptr[r] = q0;
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
   const int code = np == 1 ? r : ~r;
   for (int q = 0; q < np; ++q) {
-    const int b = e0 + q * T;
+    const int e = e0 + q * T;
     prow[q0 + q] = code;
-    pbeg[q0 + q] = b;
-    pend[q0 + q] = min(e1, b + T);
+    pbeg[q0 + q] = e;
+    pend[q0 + q] = min(e1, e + T);
   }
 }
 
@@ -393,16 +423,20 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> piece_plan(
   at::Tensor prow = at::empty({P}, rowptr.options());
   at::Tensor pbeg = at::empty({P}, rowptr.options());
   at::Tensor pend = at::empty({P}, rowptr.options());
-  hipLaunchKernelGGL(piece_ptr_kernel, dim3(1), dim3(kPpThreads), 0, stream(),
-                     rowptr.data_ptr<int>(), (int)R, (int)T,
-                     pptr.data_ptr<int>());
-  DGMC_CHECK_LAUNCH();
+  const int64_t nb = (R + 255) / 256;
+  at::Tensor part = at::empty({std::max<int64_t>(nb, 1)}, rowptr.options());
+  if (nb > 0) {
+    hipLaunchKernelGGL(piece_count_kernel, dim3((unsigned)nb), dim3(256), 0,
+                       stream(), rowptr.data_ptr<int>(), (int)R, (int)T,
+                       part.data_ptr<int>());
+    DGMC_CHECK_LAUNCH();
+  }
   const int64_t m = std::max<int64_t>(R, P);
   hipLaunchKernelGGL(piece_plan_fill_kernel, dim3((unsigned)((m + 255) / 256)),
                      dim3(256), 0, stream(), rowptr.data_ptr<int>(),
-                     pptr.data_ptr<int>(), (int)R, (int)T, (int)P,
-                     prow.data_ptr<int>(), pbeg.data_ptr<int>(),
-                     pend.data_ptr<int>());
+                     part.data_ptr<int>(), (int)nb, (int)R, (int)T, (int)P,
+                     pptr.data_ptr<int>(), prow.data_ptr<int>(),
+                     pbeg.data_ptr<int>(), pend.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
   return {pptr, prow, pbeg, pend};
 }
