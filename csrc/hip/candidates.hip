@@ -16,7 +16,6 @@
 
 #include <ATen/hip/HIPGeneratorImpl.h>
 #include <ATen/hip/detail/UnpackRaw.cuh>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <mutex>
 
@@ -114,15 +113,153 @@ __global__ __launch_bounds__(256) void csc_finish_kernel(
   if (i < n) row_of[i] = perm[i] / k;
 }
 
+// Stable LSD radix sort of (key, value) int32 pairs, 8-bit digits, for the
+// candidate CSC (a few hundred thousand entries: rocprim merge-sorts that
+// size in ~18 launches).  Per pass two launches over tiles of kRsTile
+// items (4 waves, each a contiguous quarter, 32 items per lane loaded into
+// registers up front - one memory round trip):
+//   rs_hist     per-wave digit counts (64-item groups: the lanes with the
+//               same digit found by 8 ballots; the digit's highest lane adds
+//               the group's count) -> [tiles][4 waves][256];
+//   rs_scatter  every tile derives its waves' digit offsets from the whole
+//               (small) count table, then writes every item at its digit's
+//               running position in the wave + its rank among the group's
+//               lanes with that digit: tile, wave, group, lane order -
+//               stable.
+constexpr int kRsBins = 256;
+constexpr int kRsPer = 32;                       // items per lane
+constexpr int kRsWave = 64 * kRsPer;             // items per wave
+constexpr int kRsTile = 4 * kRsWave;             // items per tile (8192)
+constexpr int kRsChunk = 32;                     // count rows per load round
+
+__device__ __forceinline__ unsigned long long rs_match(int d) {
+  unsigned long long m = ~0ull;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const unsigned long long v = __ballot((d >> b) & 1);
+    m &= ((d >> b) & 1) ? v : ~v;
+  }
+  return m;
+}
+
+// Digit counts of this wave's quarter into cnt[256] (LDS, zeroed).
+__device__ __forceinline__ void rs_count(const int* kr, int64_t i0, int64_t n,
+                                         int shift, int* cnt) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < kRsPer; ++q) {
+    const bool ok = i0 + 64 * q < n;
+    const int d = ok ? (kr[q] >> shift) & (kRsBins - 1) : -1;
+    const unsigned long long m = rs_match(d) & __ballot(ok);
+    if (ok && (m >> lane) == 1ull) cnt[d] += __popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void rs_hist_kernel(
+    const int* __restrict__ keys, int64_t n, int shift,
+    int* __restrict__ hist, int tiles) {
+  __shared__ int cnt[4][kRsBins];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = blockIdx.x;
+  for (int d = lane; d < kRsBins; d += 64) cnt[wave][d] = 0;
+  const int64_t i0 = (int64_t)t * kRsTile + wave * kRsWave + lane;
+  int kr[kRsPer];
+#pragma unroll
+  for (int q = 0; q < kRsPer; ++q) {
+    const int64_t i = i0 + 64 * q;
+    kr[q] = keys[i < n ? i : 0];
+  }
+  __builtin_amdgcn_wave_barrier();
+  rs_count(kr, i0, n, shift, &cnt[wave][0]);
+  __builtin_amdgcn_wave_barrier();
+  // per (digit, tile, wave) counts: digit-major rows of 4 * tiles
+  for (int d = lane; d < kRsBins; d += 64)
+    hist[((int64_t)4 * t + wave) * kRsBins + d] = cnt[wave][d];
+}
+
+__global__ __launch_bounds__(256) void rs_scatter_kernel(
+    const int* __restrict__ keys, const int* __restrict__ vals, int64_t n,
+    int shift, const int* __restrict__ offs, int tiles,
+    int* __restrict__ keys_out, int* __restrict__ vals_out) {
+  __shared__ int cnt[4][kRsBins];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int t = blockIdx.x;
+  const int64_t i0 = (int64_t)t * kRsTile + wave * kRsWave + lane;
+  int kr[kRsPer], vr[kRsPer];
+#pragma unroll
+  for (int q = 0; q < kRsPer; ++q) {
+    const int64_t i = i0 + 64 * q;
+    kr[q] = keys[i < n ? i : 0];
+    vr[q] = vals[i < n ? i : 0];
+  }
+  {
+    // Start of digit d = tid in each of this tile's 4 waves, from the whole
+    // [tiles][4][256] count table (coalesced rows, 32 loads in flight): the
+    // digit's total (scanned over digits), the counts of the rows before
+    // this tile, and this tile's own 4 counts.
+    __shared__ int wtot[4];
+    const int d = tid, R4 = 4 * tiles, r0 = 4 * t;
+    int tot = 0, pre = 0, own[4] = {0, 0, 0, 0};
+    for (int q0 = 0; q0 < R4; q0 += kRsChunk) {
+      int c[kRsChunk];
+#pragma unroll
+      for (int q = 0; q < kRsChunk; ++q)    // (clamped, unconditional)
+        c[q] = offs[(int64_t)min(q0 + q, R4 - 1) * kRsBins + d];
+#pragma unroll
+      for (int q = 0; q < kRsChunk; ++q) {
+        const int r = q0 + q;
+        const int v = r < R4 ? c[q] : 0;
+        tot += v;
+        pre += r < r0 ? v : 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) own[w] += r == r0 + w ? v : 0;
+      }
+    }
+    int inc = tot;                                 // scan over digits
+#pragma unroll
+    for (int e = 1; e < 64; e <<= 1) {
+      const int v = __shfl_up(inc, e);
+      if (lane >= e) inc += v;
+    }
+    if (lane == 63) wtot[wave] = inc;
+    __syncthreads();
+    int run = inc - tot + pre;
+    for (int w = 0; w < wave; ++w) run += wtot[w];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      cnt[w][d] = run;
+      run += own[w];
+    }
+    __syncthreads();
+  }
+  int* cur = &cnt[wave][0];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int q = 0; q < kRsPer; ++q) {
+    const bool ok = i0 + 64 * q < n;
+    const int d = ok ? (kr[q] >> shift) & (kRsBins - 1) : -1;
+    const unsigned long long m = rs_match(d) & __ballot(ok);
+    const int pos = ok ? cur[d] + __popcll(m & lt) : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      keys_out[pos] = kr[q];
+      vals_out[pos] = vr[q];
+      if ((m >> lane) == 1ull) cur[d] = pos + 1;   // digit's last lane
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace
 
 // S_idx [B, N_s, k] int64 (targets local to each pair's N_t block) ->
 // (col int32 [nnz] global targets, rowptr int32 [B N_s + 1], colptr int32
 // [B N_t + 1], perm int32 [nnz] CSC -> CSR entry map (stable: row order
-// inside a column), row_of int32 [nnz]).  Prep + rocprim's stable radix
-// sort (default configuration: it merge-sorts up to 1 M keys; forcing
-// onesweep faulted inside the captured step) + finish, instead of an argsort
-// + histogram + scan chain.
+// inside a column), row_of int32 [nnz]).  Prep + the stable LSD radix sort
+// above (3 launches per 8-bit digit: 2 digits up to 65536 columns; rocprim's
+// default merge-sorts this size in ~18 launches, and forcing its onesweep
+// faulted inside the captured step) + finish.
 std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
   TORCH_CHECK(S_idx.is_cuda() && S_idx.scalar_type() == at::kLong &&
                   S_idx.is_contiguous() && S_idx.dim() == 3,
@@ -145,17 +282,30 @@ std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
   DGMC_CHECK_LAUNCH();
   unsigned bits = 1;
   while (bits < 31 && (int64_t(1) << bits) < C) ++bits;
-  size_t tmp_bytes = 0;
-  DGMC_CHECK_HIP(rocprim::radix_sort_pairs(
-      nullptr, tmp_bytes, col.data_ptr<int>(), keys.data_ptr<int>(),
-      iota.data_ptr<int>(), perm.data_ptr<int>(), (size_t)n, 0, bits,
-      stream()));
-  at::Tensor tmp = at::empty({(int64_t)std::max<size_t>(tmp_bytes, 1)},
-                             S_idx.options().dtype(at::kByte));
-  DGMC_CHECK_HIP(rocprim::radix_sort_pairs(
-      tmp.data_ptr(), tmp_bytes, col.data_ptr<int>(), keys.data_ptr<int>(),
-      iota.data_ptr<int>(), perm.data_ptr<int>(), (size_t)n, 0, bits,
-      stream()));
+  const int passes = (int)((bits + 7) / 8);
+  const int tiles = (int)((n + kRsTile - 1) / kRsTile);
+  at::Tensor hist = at::empty({(int64_t)kRsBins * 4 * std::max(tiles, 1)},
+                              i32);
+  at::Tensor k2 = at::empty({n}, i32), v2 = at::empty({n}, i32);
+  // ping-pong so the last pass lands in keys / perm
+  const int* ki = col.data_ptr<int>();
+  const int* vi = iota.data_ptr<int>();
+  for (int p = 0; p < passes && n > 0; ++p) {
+    const bool last = p == passes - 1;
+    const bool odd = ((passes - 1 - p) & 1) != 0;
+    int* ko = last ? keys.data_ptr<int>()
+                   : (odd ? k2.data_ptr<int>() : keys.data_ptr<int>());
+    int* vo = last ? perm.data_ptr<int>()
+                   : (odd ? v2.data_ptr<int>() : perm.data_ptr<int>());
+    hipLaunchKernelGGL(rs_hist_kernel, dim3(tiles), dim3(256), 0, stream(), ki,
+                       n, 8 * p, hist.data_ptr<int>(), tiles);
+    DGMC_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rs_scatter_kernel, dim3(tiles), dim3(256), 0, stream(),
+                       ki, vi, n, 8 * p, hist.data_ptr<int>(), tiles, ko, vo);
+    DGMC_CHECK_LAUNCH();
+    ki = ko;
+    vi = vo;
+  }
   hipLaunchKernelGGL(csc_finish_kernel, dim3((unsigned)((n + 256) / 256)),
                      dim3(256), 0, stream(), keys.data_ptr<int>(),
                      perm.data_ptr<int>(), n, (int)k, C,

@@ -55,3 +55,33 @@ def test_cli_presets_list_and_er_train(capsys):
     out = capsys.readouterr().out
     for name in ('er', 'willow', 'pascal', 'pascal_pf', 'dbp15k'):
         assert name in out
+
+
+def test_cli_info_reports_build_state(capsys, tmp_path):
+    import json
+    from deep_graph_matching_consensus_amd import cli
+    assert cli.main(['info', '--json']) == 0
+    rep = json.loads(capsys.readouterr().out)
+    for key in ('torch', 'gpu', 'libraries', 'ops', 'build', 'switches'):
+        assert key in rep
+    assert rep['libraries']['host']['loaded']
+    # build_status against a synthetic tree: one edited, one new source
+    src = tmp_path / 'csrc' / 'hip'
+    src.mkdir(parents=True)
+    (src / 'a.hip').write_text('a')
+    (src / 'b.hip').write_text('b')
+    (tmp_path / 'lib.so').write_text('x')
+    man = {'arch': 'gfx950',
+           'sources': {'csrc/hip/a.hip': cli._sha256(str(src / 'a.hip')),
+                       'csrc/hip/b.hip': 'old'},
+           'libraries': {'lib.so': cli._sha256(str(tmp_path / 'lib.so'))}}
+    (tmp_path / 'build' / 'native').mkdir(parents=True)
+    (tmp_path / 'build' / 'native' / 'manifest.json').write_text(
+        json.dumps(man))
+    (src / 'c.hip').write_text('c')
+    st = cli.build_status(str(tmp_path))
+    assert st['manifest'] and st['arch'] == 'gfx950'
+    assert st['stale_sources'] == ['csrc/hip/b.hip', 'csrc/hip/c.hip']
+    assert st['changed_libs'] == []
+    (tmp_path / 'lib.so').write_text('y')
+    assert cli.build_status(str(tmp_path))['changed_libs'] == ['lib.so']
