@@ -472,19 +472,35 @@ __global__ __launch_bounds__(256) void row_sqnorm_max_kernel(
         fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// Exact chain of topk_dot_kernel for one target row (a: LDS, zero-padded).
+// Exact chain of topk_dot_kernel for one target row (a: LDS, zero-padded;
+// C % 4 == 0).  The target row is fetched 64 channels at a time as 16
+// independent 16-byte loads (clamped, zeroed past C) before that chunk's
+// FMAs - the chain itself (k = 8s + t, then 8s + 4 + t) is unchanged.
 __device__ __forceinline__ float exact_dot(const DGMC_LDS float* a,
                                            const float* __restrict__ b,
                                            int C, int C8) {
   float acc = 0.f;
-  for (int s = 0; s < C8; s += 8) {
-    float bv[8];
+  for (int s0 = 0; s0 < C8; s0 += 64) {
+    float4 v[16];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bv[e] = s + e < C ? b[s + e] : 0.f;
+    for (int q = 0; q < 16; ++q) {
+      const int e = s0 + 4 * q;
+      const float4 t =
+          *reinterpret_cast<const float4*>(b + min(e, C - 4));
+      v[q] = e < C ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      acc = __builtin_fmaf(a[s + t], bv[t], acc);
-      acc = __builtin_fmaf(a[s + 4 + t], bv[4 + t], acc);
+    for (int u = 0; u < 8; ++u) {
+      const int s = s0 + 8 * u;
+      if (s >= C8) break;
+      const float bv[8] = {v[2 * u].x,     v[2 * u].y,     v[2 * u].z,
+                           v[2 * u].w,     v[2 * u + 1].x, v[2 * u + 1].y,
+                           v[2 * u + 1].z, v[2 * u + 1].w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc = __builtin_fmaf(a[s + t], bv[t], acc);
+        acc = __builtin_fmaf(a[s + 4 + t], bv[4 + t], acc);
+      }
     }
   }
   return acc;
@@ -572,6 +588,105 @@ __global__ __launch_bounds__(kRefRows * 64) void topk_refine_kernel(
   if (lane < k) orow[lane] = li;
 }
 
+// Exhaustive exact scan of one row by the whole wave (lanes 0..k-1 keep the
+// list, as in topk_dot_kernel) - the fallback of both refine kernels.
+__device__ __forceinline__ void refine_exhaustive(
+    const DGMC_LDS float* a, const float* __restrict__ tb,
+    int64_t* __restrict__ orow, int Nt, int C, int C8, int k) {
+  const int lane = threadIdx.x & 63;
+  float lv = -INFINITY;
+  int li = 0;
+  for (int j0 = 0; j0 < Nt; j0 += 64) {
+    const int j = j0 + lane;
+    const float v =
+        j < Nt ? exact_dot(a, tb + (size_t)j * C, C, C8) : -INFINITY;
+    float thr = __shfl(lv, k - 1);
+    unsigned long long mask = __ballot(j < Nt && v > thr);
+    while (mask) {
+      const int src = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const float nv = __shfl(v, src);
+      if (!(nv > thr)) continue;
+      const int pos = __popcll(__ballot(lane < k && lv >= nv));
+      const float pv = __shfl_up(lv, 1);
+      const int pi = __shfl_up(li, 1);
+      if (lane > pos && lane < k) { lv = pv; li = pi; }
+      if (lane == pos) { lv = nv; li = j0 + src; }
+      thr = __shfl(lv, k - 1);
+    }
+  }
+  if (lane < k) orow[lane] = li;
+}
+
+// K2 <= 16: four rows per wave (lane group r = lane / 16 re-scores row r's
+// candidates, lane c of the group candidate c) - the same exact chains,
+// margins, ranks and fallback as topk_refine_kernel, a quarter of the waves.
+constexpr int kRef4Waves = 4;
+__global__ __launch_bounds__(kRef4Waves * 64) void topk_refine4_kernel(
+    const float* __restrict__ h_s, const float* __restrict__ h_t,
+    const int64_t* __restrict__ cand_i, const float* __restrict__ cand_v,
+    const float* __restrict__ nmax_part, int nparts, int64_t* __restrict__ out,
+    int* __restrict__ n_overflow, int Ns, int Nt, int C, int k, int K2,
+    float tau) {
+  __shared__ __attribute__((aligned(16))) float sa[kRef4Waves][4][264];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, c = lane & 15;
+  const int64_t g0 = ((int64_t)blockIdx.x * kRef4Waves + wave) * 4;
+  const int b = blockIdx.y;
+  if (g0 >= Ns) return;                  // wave-uniform; no block barrier
+  const int64_t g = g0 + grp;
+  const bool row_ok = g < Ns;
+  const int C8 = (C + 7) & ~7;
+  DGMC_LDS float* a = (DGMC_LDS float*)sa[wave][grp];
+  float sq = 0.f;
+  {
+    const float* arow = h_s + ((size_t)b * Ns + (row_ok ? g : g0)) * C;
+    for (int e = c; e < C8; e += 16) {
+      const float v = e < C ? arow[e] : 0.f;
+      a[e] = v;
+      sq += v * v;
+    }
+  }
+#pragma unroll
+  for (int d = 8; d >= 1; d >>= 1) sq += __shfl_xor(sq, d);   // group sum
+  float bm = 0.f;
+  for (int p = lane; p < nparts; p += 64)
+    bm = fmaxf(bm, nmax_part[(size_t)b * nparts + p]);
+  bm = wave_max(bm);
+  const float E = tau * sqrtf(sq * bm) * (1.0f + 1.0f / 1024.0f);
+  const size_t o = (size_t)b * Ns + (row_ok ? g : g0);
+  const bool has = row_ok && c < K2;
+  const int ci = has ? (int)cand_i[o * K2 + c] : 0;
+  const float cv = has ? cand_v[o * K2 + c] : -INFINITY;
+  const int base = grp * 16;
+  const float Tk = __shfl(cv, base + k - 1);
+  const float lim = Tk - 2.0f * E;
+  const bool keep = has && cv >= lim;
+  const unsigned gmask = (unsigned)(__ballot(keep) >> base) & 0xffffu;
+  const bool overflow = row_ok &&
+      ((K2 < Nt && __shfl(cv, base + K2 - 1) >= lim) || __popc(gmask) < k);
+  __builtin_amdgcn_wave_barrier();
+  const float* tb = h_t + (size_t)b * Nt * C;
+  const float ev = keep && !overflow
+                       ? exact_dot(a, tb + (size_t)ci * C, C, C8) : -INFINITY;
+  int rank = 0;
+  for (int l = 0; l < 16; ++l) {
+    const float ov = __shfl(ev, base + l);
+    const int oj = __shfl(ci, base + l);
+    const bool ok = ((gmask >> l) & 1u) != 0;
+    rank += ok && (ov > ev || (ov == ev && oj < ci));
+  }
+  if (keep && !overflow && rank < k) out[o * k + rank] = ci;
+  // Incomplete lists: each such row by the whole wave, in row order.
+  const unsigned long long ovm = __ballot(overflow && c == 0);
+  for (int r = 0; r < 4; ++r) {
+    if (!((ovm >> (16 * r)) & 1ull)) continue;
+    if (lane == 0) atomicAdd(n_overflow, 1);
+    refine_exhaustive((DGMC_LDS float*)sa[wave][r], tb,
+                      out + ((size_t)b * Ns + g0 + r) * k, Nt, C, C8, k);
+  }
+}
+
 static at::Tensor topk_dot_refined(const at::Tensor& h_s,
                                    const at::Tensor& h_t, int64_t k,
                                    at::Tensor* n_overflow) {
@@ -597,6 +712,18 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
                      stream(), h_t.data_ptr<float>(), Nt, C,
                      part.data_ptr<float>());
   DGMC_CHECK_LAUNCH();
+  if (K2 <= 16) {
+    hipLaunchKernelGGL(topk_refine4_kernel,
+                       dim3((Ns + 4 * kRef4Waves - 1) / (4 * kRef4Waves), B),
+                       dim3(kRef4Waves * 64), 0, stream(),
+                       h_s.data_ptr<float>(), h_t.data_ptr<float>(),
+                       ci.data_ptr<int64_t>(), cv.data_ptr<float>(),
+                       part.data_ptr<float>(), nparts,
+                       out.data_ptr<int64_t>(), cnt.data_ptr<int>(), Ns, Nt, C,
+                       (int)k, K2, topk_tau());
+    DGMC_CHECK_LAUNCH();
+    return out;
+  }
   hipLaunchKernelGGL(topk_refine_kernel,
                      dim3((Ns + kRefRows - 1) / kRefRows, B),
                      dim3(kRefRows * 64), 0, stream(), h_s.data_ptr<float>(),
