@@ -275,9 +275,10 @@ def bench_kg(args, cfg, device):
 def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
     """Multi-GPU diagnostics: per-rank ms/step spread,
     the DP mode actually used, the exposed all-reduce time (flat mode:
-    events around ``reducer.finish()`` of every timed step) and the cost of
+    events around ``reducer.finish()`` of every timed step), the cost of
     one standalone all-reduce of the whole gradient buffer (what a fully
-    exposed sync would add per step)."""
+    exposed sync would add per step) and whether the parameters are still
+    bit-identical across ranks (``params_in_sync``)."""
     ms = 1000.0 * rank_elapsed / max(steps, 1)
     out = {'dp_mode': trainer.dp_mode_used,
            'reserved_cus': int(getattr(trainer, 'reserved_cus', 0))}
@@ -312,6 +313,18 @@ def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
     out['allreduce_standalone_ms'] = round(parallel.all_reduce_max(t, device),
                                            3)
     out['allreduce_bytes'] = int(buf.numel() * 4)
+    # Data-parallel correctness after the timed steps: every rank applied the
+    # same averaged gradients, so the parameters must be bit-identical across
+    # ranks.  Per-parameter fp64 sums, max and min over ranks.
+    with torch.no_grad():
+        sums = torch.stack([p.detach().double().sum()
+                            for p in trainer.model.parameters()])
+        hi, lo = sums.clone(), -sums
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+        diff = float((hi + lo).abs().max()) if sums.numel() else 0.0
+    out['params_max_rank_diff'] = diff
+    out['params_in_sync'] = diff == 0.0
     return out
 
 

@@ -157,12 +157,14 @@ __global__ __launch_bounds__(256) void sparse_nll_part_kernel(
     const float* __restrict__ val, const int64_t* __restrict__ idx,
     const int64_t* __restrict__ y0, const int64_t* __restrict__ y1,
     const bool* __restrict__ mask, float4* __restrict__ part, int G, int K,
-    float eps) {
+    int64_t R, float eps) {
   __shared__ float4 red[4];
   float acc = 0.f, hits = 0.f, cor = 0.f, cnt = 0.f;
   for (int g = blockIdx.x * 256 + threadIdx.x; g < G; g += gridDim.x * 256) {
     if (mask != nullptr && !mask[g]) continue;
-    const size_t o = (size_t)y0[g] * K;
+    const int64_t r = y0[g];
+    if (r < 0 || r >= R) continue;       // (invalid source row: ignored)
+    const size_t o = (size_t)r * K;
     const int64_t t = y1[g];
     float best = -INFINITY;
     int64_t pred = -1;
@@ -219,12 +221,14 @@ __global__ __launch_bounds__(256) void sparse_nll_bwd_kernel(
     const int64_t* __restrict__ idx, const int64_t* __restrict__ y0,
     const int64_t* __restrict__ y1, const bool* __restrict__ mask,
     const float* __restrict__ aux, float* __restrict__ dval, int G, int K,
-    float eps, int mean) {
+    int64_t R, float eps, int mean) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= G) return;
   if (mask != nullptr && !mask[g]) return;
+  const int64_t r = y0[g];
+  if (r < 0 || r >= R) return;
   const float div = mean ? fmaxf(aux[0], 1.f) : 1.f;
-  const size_t o = (size_t)y0[g] * K;
+  const size_t o = (size_t)r * K;
   const int64_t t = y1[g];
   for (int c = 0; c < K; ++c)
     if (idx[o + c] == t)
@@ -576,7 +580,7 @@ std::tuple<at::Tensor, at::Tensor> sparse_nll_fwd(
   hipLaunchKernelGGL(sparse_nll_part_kernel, dim3(nb), dim3(256), 0, stream(),
                      val.data_ptr<float>(), idx.data_ptr<int64_t>(),
                      y0.data_ptr<int64_t>(), y1.data_ptr<int64_t>(), mp, pp,
-                     G, (int)val.size(1), (float)eps);
+                     G, (int)val.size(1), val.size(0), (float)eps);
   DGMC_CHECK_LAUNCH();
   hipLaunchKernelGGL(sparse_nll_fold_kernel, dim3(1), dim3(64), 0, stream(),
                      pp, nb, loss.data_ptr<float>(), aux.data_ptr<float>(),
@@ -605,8 +609,8 @@ at::Tensor sparse_nll_bwd(const at::Tensor& grad, const at::Tensor& val,
                      0, stream(), g.data_ptr<float>(), val.data_ptr<float>(),
                      idx.data_ptr<int64_t>(), y0.data_ptr<int64_t>(),
                      y1.data_ptr<int64_t>(), mp, aux.data_ptr<float>(),
-                     dval.data_ptr<float>(), G, (int)val.size(1), (float)eps,
-                     mean ? 1 : 0);
+                     dval.data_ptr<float>(), G, (int)val.size(1),
+                     val.size(0), (float)eps, mean ? 1 : 0);
   DGMC_CHECK_LAUNCH();
   return dval;
 }

@@ -153,3 +153,5 @@ def test_bench_ranks_gloo(tmp_path, mode, world, batch, dp_mode):
     assert result['allreduce_standalone_ms'] > 0
     assert result['allreduce_bytes'] > 0
     assert 'gemm_arith' in result
+    # every rank applied the same averaged update: bit-identical parameters
+    assert result['params_in_sync'], result['params_max_rank_diff']
