@@ -414,6 +414,35 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   }
 }
 
+// The same merge with one wave per row (S * k <= 64): lane l holds
+// candidate l, its rank from uniform-lane reads of the others (same
+// comparisons, same output).
+__global__ __launch_bounds__(256) void topk_merge_wave_kernel(
+    const float* __restrict__ part_v, const int* __restrict__ part_i,
+    int64_t* __restrict__ out, float* __restrict__ out_v, int64_t rows, int S,
+    int k, int Nt) {
+  const int n = S * k;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;                     // wave-uniform
+  const float* v = part_v + row * n;
+  const int* ix = part_i + row * n;
+  const bool on = lane < n;
+  const float mv = on ? v[lane] : 0.f;
+  const int mj = on ? ix[lane] : 0;
+  int rank = 0;
+  for (int e = 0; e < n; ++e) {
+    const float ov = __int_as_float(
+        __builtin_amdgcn_readlane(__float_as_int(mv), e));
+    const int oj = __builtin_amdgcn_readlane(mj, e);
+    rank += (ov > mv) || (ov == mv && oj < mj);
+  }
+  if (on && rank < k) {
+    out[row * k + rank] = mj < Nt ? mj : 0;
+    if (out_v) out_v[row * k + rank] = mj < Nt ? mv : -INFINITY;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Exact fp32 top-k at split-bf16 speed: filter + exact re-score.
 //
@@ -821,7 +850,14 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
     default: launch(topk_x3_kernel<16, 8>); break;
   }
   DGMC_CHECK_LAUNCH();
-  if (S > 1) {
+  if (S > 1 && S * k <= 64) {
+    const int64_t rows = (int64_t)B * Ns;
+    hipLaunchKernelGGL(topk_merge_wave_kernel,
+                       dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                       stream(), pv.data_ptr<float>(), pi.data_ptr<int>(),
+                       out.data_ptr<int64_t>(), out_v, rows, S, (int)k, Nt);
+    DGMC_CHECK_LAUNCH();
+  } else if (S > 1) {
     const int64_t rows = (int64_t)B * Ns;
     const int64_t n = rows * S * k;
     hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)((n + 255) / 256)),
