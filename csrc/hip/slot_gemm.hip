@@ -131,35 +131,53 @@ __global__ __launch_bounds__(256) void sg_mark_kernel(
 }
 
 // One block per slot: rank[j*S+k] = rank of j among the used sources of slot
-// k (-1 if unused); cnt[k] = used count.  Ballot prefix sums (0/1 values).
+// k (-1 if unused); cnt[k] = used count.  Rounds of 1024 x 16 sources: each
+// thread loads its 16 consecutive marks in one round (clamped addresses),
+// then a shuffle scan per wave and the 16 wave totals through LDS - two
+// barriers per round instead of four per 1024 sources.
+constexpr int kSgScanPer = 16;
 __global__ __launch_bounds__(1024) void sg_scan_kernel(
     const int* __restrict__ mark, int Nsrc, int S, int* __restrict__ rank,
     int* __restrict__ cnt) {
   __shared__ int wtot[16];
-  __shared__ int base_sh;
   const int k = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
             wave = tid >> 6;
-  if (tid == 0) base_sh = 0;
-  __syncthreads();
-  for (int j0 = 0; j0 < Nsrc; j0 += 1024) {
-    const int j = j0 + tid;
-    const int v = j < Nsrc ? (mark[(size_t)j * S + k] != 0) : 0;
-    const unsigned long long m = __ballot(v);
-    const int below = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wtot[wave] = __popcll(m);
-    __syncthreads();
-    int off = base_sh;
-    for (int w = 0; w < wave; ++w) off += wtot[w];
-    if (j < Nsrc) rank[(size_t)j * S + k] = v ? off + below : -1;
-    __syncthreads();
-    if (tid == 0) {
-      int t = 0;
-      for (int w = 0; w < 16; ++w) t += wtot[w];
-      base_sh += t;
+  int base = 0;
+  for (int j0 = 0; j0 < Nsrc; j0 += 1024 * kSgScanPer) {
+    const int jt = j0 + tid * kSgScanPer;
+    int v[kSgScanPer];
+    int s = 0;
+#pragma unroll
+    for (int e = 0; e < kSgScanPer; ++e) {
+      const int j = min(jt + e, Nsrc - 1);
+      const int m = mark[(size_t)j * S + k];
+      v[e] = (jt + e < Nsrc && m != 0) ? 1 : 0;
+      s += v[e];
     }
+    int inc = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) wtot[wave] = inc;
     __syncthreads();
+    int off = base + inc - s, all = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const int t = wtot[w];
+      off += w < wave ? t : 0;
+      all += t;
+    }
+#pragma unroll
+    for (int e = 0; e < kSgScanPer; ++e) {
+      if (jt + e < Nsrc) rank[(size_t)(jt + e) * S + k] = v[e] ? off : -1;
+      off += v[e];
+    }
+    base += all;
+    __syncthreads();                     // wtot reused next round
   }
-  if (tid == 0) cnt[k] = base_sh;
+  if (tid == 0) cnt[k] = base;
 }
 
 // posmap / src / cinv over the column space, col_c over the entries, seg.

@@ -73,8 +73,8 @@ def test_slot_gemm_spmm_matches_fp64(cin, cout, relu):
         assert _rel(a, bb) < 1e-5, name
 
 
-def test_compact_plan_layout():
-    n, e = 500, 2000
+@pytest.mark.parametrize('n,e', [(500, 2000), (20000, 60000)])
+def test_compact_plan_layout(n, e):
     ei, pseudo = _graph(n, e, seed=3)
     op = spline_plan(ei, pseudo, n, (5, 5), (1, 1), 1, root=True)
     S = 26
@@ -96,6 +96,11 @@ def test_compact_plan_layout():
     k = used % S
     p = pm[used].cpu()
     assert ((p >= seg[k.cpu()]) & (p < seg[k.cpu() + 1])).all()
+    # ... in ascending source order (20000 sources: several scan rounds)
+    src, cnt = plan.src.long().cpu(), plan.counts.long().cpu()
+    for s_ in range(S):
+        rows = src[int(seg[s_]):int(seg[s_]) + int(cnt[s_])]
+        assert bool((rows[1:] > rows[:-1]).all())
 
 
 def test_loop_weight_grad_equals_per_use():
