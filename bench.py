@@ -60,19 +60,26 @@ def launch_ranks(argv=None):
     """One process per GPU.  Runs BEFORE torch (or anything else) touches
     the GPU: a plain ``python bench.py --gpus N`` starts N ranks through
     ``torch.distributed.run`` as a CHILD process (never an exec) and returns
-    its exit code; under a launcher it checks ``WORLD_SIZE == N``.  Returns
-    None when this process should run the benchmark itself."""
+    its exit code; under a launcher it checks ``WORLD_SIZE == N`` and, for
+    N > 1, turns this rank into a :func:`supervise` process whose GPU work
+    runs in a child.  Returns None when this process should run the
+    benchmark itself."""
     argv = sys.argv[1:] if argv is None else list(argv)
     n = _gpus_arg(argv)
     if n < 1:
         sys.stderr.write('bench.py: --gpus must be >= 1\n')
         return 2
+    if os.environ.get(WORKER_ENV) == '1':
+        return None
     if 'WORLD_SIZE' in os.environ:
         world = int(os.environ['WORLD_SIZE'])
         if world != n:
             sys.stderr.write('bench.py: --gpus {} but the launcher started '
                              'WORLD_SIZE={} ranks\n'.format(n, world))
             return 2
+        if world > 1 and os.environ.get('DGMC_AMD_BENCH_SUPERVISE',
+                                        '1') == '1':
+            return supervise(argv)
         return None
     if n == 1:
         return None
@@ -86,6 +93,194 @@ def launch_ranks(argv=None):
            '--nproc-per-node', str(n), '--master-addr', '127.0.0.1',
            '--master-port', str(port), osp.abspath(__file__)] + argv
     return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------
+# Multi-GPU first-run insurance.  Under ``torch.distributed.run`` every rank
+# process becomes a SUPERVISOR that never touches the GPU (it imports torch
+# for a CPU-only gloo group, no HIP call): the benchmark itself runs in a
+# child process per rank, on a fresh RCCL rendezvous port per attempt.  If
+# any rank's child fails, hangs past its wall budget or (rank 0) prints no
+# JSON line, every supervisor kills its child's process group and all start
+# the next, more conservative data-parallel mode together:
+#   1. graph mode, bucketed all-reduces captured in the step's hipGraph;
+#   2. graph mode, one flat all-reduce after each replay;
+#   3. static (uncaptured) steps with one flat all-reduce after each step.
+# Rank 0 prints the successful attempt's JSON line with ``dp_attempts``
+# ([{mode, rc, reason, wall_s}]) appended.  Each attempt is a new child,
+# never a re-exec.
+WORKER_ENV = 'DGMC_AMD_BENCH_WORKER'
+ATTEMPT_ENV = 'DGMC_AMD_BENCH_ATTEMPT'
+DONE_MARK = '#dgmc-bench-done'
+DP_LADDER = [
+    ('graph-captured', []),
+    ('graph-flat', ['--dp-mode', 'flat']),
+    ('static-flat', ['--mode', 'static', '--dp-mode', 'flat']),
+]
+
+
+def dp_ladder(argv):
+    """Attempts for ``argv``: the ladder from the user's own choice down
+    (an explicit ``--mode static``/``eager`` or ``--dp-mode flat`` skips
+    the rungs above it)."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument('--mode', default=None)
+    p.add_argument('--dp-mode', default='captured')
+    p.add_argument('--no-graph', action='store_true')
+    a = p.parse_known_args(argv)[0]
+    if a.mode == 'eager':
+        return [('eager', [])]
+    start = 0
+    if a.mode == 'static' or a.no_graph:
+        start = 2
+    elif a.dp_mode == 'flat':
+        start = 1
+    return DP_LADDER[start:]
+
+
+def attempt_budgets(total_s, n_attempts, used_s, index, cap_s=240.0,
+                    reserve_s=100.0, floor_s=60.0):
+    """Wall budget of attempt ``index`` (0-based): what is left of
+    ``total_s`` minus ``reserve_s`` for each later attempt, at most
+    ``cap_s`` and at least ``floor_s``."""
+    left = total_s - used_s - reserve_s * (n_attempts - index - 1)
+    return max(floor_s, min(cap_s, left))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _run_child(cmd, env, budget_s, grace_s=30.0):
+    """Run one rank's benchmark child; stdout lines are forwarded to stderr
+    (JSON lines are kept).  Returns ``(rc, json_lines, done, reason)``;
+    a child past ``budget_s`` (or still alive ``grace_s`` after it printed
+    the done mark) is killed with its whole process group."""
+    import signal
+    import threading
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE,
+                            stderr=None, start_new_session=True,
+                            universal_newlines=True, bufsize=1)
+    lines, done = [], threading.Event()
+
+    def pump():
+        for ln in proc.stdout:
+            if ln.startswith('{'):
+                lines.append(ln.strip())
+            elif ln.startswith(DONE_MARK):
+                done.set()
+            else:
+                sys.stderr.write(ln)
+        proc.stdout.close()
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    t0 = time.monotonic()
+    reason = ''
+    while proc.poll() is None:
+        now = time.monotonic() - t0
+        if now > budget_s:
+            reason = 'timeout after {:.0f} s'.format(now)
+            break
+        if done.is_set() and not reason:
+            reason = 'done'
+            done_t = now
+        if reason == 'done' and now - done_t > grace_s:
+            reason = 'hung in teardown after its result'
+            break
+        time.sleep(0.2)
+    if proc.poll() is None:
+        for sig, wait in ((signal.SIGTERM, 10), (signal.SIGKILL, 30)):
+            try:
+                os.killpg(proc.pid, sig)
+            except OSError:
+                pass
+            try:
+                proc.wait(timeout=wait)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+    th.join(timeout=10)
+    rc = proc.returncode
+    if reason in ('', 'done'):
+        reason = 'ok' if rc == 0 else 'exit code {}'.format(rc)
+    return rc, lines, done.is_set(), reason
+
+
+def supervise(argv, total_s=None):
+    """Supervisor rank under ``torch.distributed.run`` (see above)."""
+    import datetime
+    import torch.distributed as dist
+    if total_s is None:
+        total_s = float(os.environ.get('DGMC_AMD_BENCH_BUDGET_S', '560'))
+    cap_s = float(os.environ.get('DGMC_AMD_BENCH_ATTEMPT_S', '240'))
+    rank = int(os.environ['RANK'])
+    world = int(os.environ['WORLD_SIZE'])
+    # CPU-only group of the supervisors (no HIP call in this process).
+    dist.init_process_group(
+        'gloo', timeout=datetime.timedelta(seconds=total_s + 300))
+    ladder = dp_ladder(argv)
+    t_start = time.monotonic()
+    record, result = [], None
+    for i, (name, extra) in enumerate(ladder):
+        budget = attempt_budgets(total_s, len(ladder),
+                                 time.monotonic() - t_start, i, cap_s=cap_s,
+                                 floor_s=min(60.0, cap_s))
+        port = [_free_port() if rank == 0 else 0]
+        dist.broadcast_object_list(port, src=0)
+        env = dict(os.environ)
+        env.update({WORKER_ENV: '1', ATTEMPT_ENV: str(i),
+                    'MASTER_PORT': str(port[0]),
+                    'MASTER_ADDR': env.get('MASTER_ADDR', '127.0.0.1')})
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+        # RCCL collectives of a bench child give up well inside the budget.
+        env.setdefault('DGMC_AMD_DIST_TIMEOUT', '90')
+        # The child's rank 0 hosts its own store on the new port.
+        for k in ('TORCHELASTIC_USE_AGENT_STORE',):
+            env.pop(k, None)
+        cmd = [sys.executable, '-u', osp.abspath(__file__)] + list(argv) + \
+            list(extra)
+        t0 = time.monotonic()
+        rc, lines, done, reason = _run_child(cmd, env, budget)
+        wall = time.monotonic() - t0
+        got = rank != 0 or bool(lines)
+        if rank == 0 and not lines and rc == 0:
+            reason = 'no JSON line'
+        # Rank 0's JSON line is the measurement (printed after the last
+        # collective of the timed region); the attempt succeeds when it
+        # exists and no rank failed before finishing its work.
+        fine = int(got and (rc == 0 or done))
+        flags = [None] * world
+        dist.all_gather_object(flags, (fine, rc, reason, round(wall, 1)))
+        record.append({'mode': name, 'budget_s': round(budget, 1),
+                       'rc': [f[1] for f in flags],
+                       'reason': sorted({f[2] for f in flags}),
+                       'wall_s': max(f[3] for f in flags)})
+        if all(f[0] for f in flags):
+            if rank == 0:
+                result = json.loads(lines[-1])
+            break
+    ok = result is not None if rank == 0 else True
+    if rank == 0:
+        if result is None:
+            result = {'metric': 'graph-pairs/sec training', 'value': None,
+                      'n_gpus': world, 'error': 'every data-parallel '
+                      'attempt failed'}
+        result['dp_attempts'] = record
+        line = json.dumps(result)
+        print(line, flush=True)
+        jp = argparse.ArgumentParser(add_help=False)
+        jp.add_argument('--json-out', default=None)
+        json_out = jp.parse_known_args(argv)[0].json_out
+        if json_out:
+            with open(json_out, 'w') as f:
+                f.write(line + '\n')
+    done_all = [None] * world
+    dist.all_gather_object(done_all, ok)
+    dist.destroy_process_group()
+    return 0 if all(done_all) else 1
 
 
 if __name__ == '__main__':
@@ -154,6 +349,10 @@ def parse_args(argv=None):
                    help='execution mode (default: graph on GPU, else eager)')
     p.add_argument('--kg-scale', type=float, default=1.0,
                    help='size multiplier of the DBP15K-shaped KG pair')
+    p.add_argument('--kg-phase', default='both',
+                   choices=['both', 'phase1', 'phase2'],
+                   help='DBP15K schedule phases to time (dbp15k.py:64-69); '
+                        'one phase alone for profiling')
     p.add_argument('--eval-pairs', type=int, default=1000,
                    help='held-out Hits@1/@10 on this many test pairs per '
                         'evaluation, outside the timed region (reference '
@@ -223,9 +422,11 @@ def bench_kg(args, cfg, device):
             torch.cuda.synchronize()
 
     times = {}
+    phases = [('phase1', (0, False)), ('phase2', (args.num_steps, True))]
+    if args.kg_phase != 'both':
+        phases = [ph for ph in phases if ph[0] == args.kg_phase]
     with reference_mode(reference):
-        for phase, (steps, detach) in [('phase1', (0, False)),
-                                       ('phase2', (args.num_steps, True))]:
+        for phase, (steps, detach) in phases:
             model.num_steps, model.detach = steps, detach
             for _ in range(args.warmup):
                 trainer.step()
@@ -236,7 +437,8 @@ def bench_kg(args, cfg, device):
             sync()
             times[phase] = (time.perf_counter() - t0) / max(args.steps, 1)
         hits1, hits10 = trainer.evaluate()
-    ms2 = 1000.0 * times['phase2']
+    main_phase = 'phase2' if 'phase2' in times else 'phase1'
+    ms2 = 1000.0 * times[main_phase]
     baseline = None
     if osp.exists(BASELINE_FILE) and not reference:
         with open(BASELINE_FILE) as f:
@@ -244,17 +446,19 @@ def bench_kg(args, cfg, device):
     out = {
         'metric': 'DBP15K-shaped KG alignment training steps/sec '
                   '(refinement phase, full graph)',
-        'value': round(1.0 / times['phase2'], 3),
+        'value': round(1.0 / times[main_phase], 3),
         'unit': 'steps/s',
         'n_gpus': 1,
         'steps': args.steps,
         'warmup': args.warmup,
         'ms_per_step': round(ms2, 3),
-        'ms_per_step_phase1': round(1000.0 * times['phase1'], 3),
+        'ms_per_step_phase1': round(1000.0 * times['phase1'], 3)
+        if 'phase1' in times else None,
+        'timed_phase': main_phase,
         'higher_is_better': True,
         'scaling': 'strong',
-        'vs_baseline': round((1.0 / times['phase2']) / baseline, 3)
-        if baseline else None,
+        'vs_baseline': round((1.0 / times[main_phase]) / baseline, 3)
+        if baseline and main_phase == 'phase2' else None,
         'dtype': 'fp32',
         'data': 'synthetic DBP15K-shaped {} KG pair ({} / {} entities, {} / '
                 '{} triples, {} train / {} test alignments), random-init '
@@ -282,6 +486,8 @@ def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
     ms = 1000.0 * rank_elapsed / max(steps, 1)
     out = {'dp_mode': trainer.dp_mode_used,
            'reserved_cus': int(getattr(trainer, 'reserved_cus', 0))}
+    if getattr(trainer, 'dp_checks', None):
+        out['dp_checks'] = trainer.dp_checks
     if world == 1:
         return out
     import torch.distributed as dist
@@ -328,8 +534,39 @@ def dp_diagnostics(trainer, rank_elapsed, steps, world, device):
     return out
 
 
+def _inject(where):
+    """Fault injection for the supervisor tests:
+    ``DGMC_AMD_BENCH_INJECT=<kind>:<attempt>:<rank>`` with kind ``crash``
+    (raise), ``hang`` (sleep forever) or ``nojson`` (rank 0 exits 0 without
+    its line), applied at ``where`` = ``start`` (before the warm-up)."""
+    spec = os.environ.get('DGMC_AMD_BENCH_INJECT')
+    if not spec:
+        return None
+    kind, attempt, rank = spec.split(':')
+    if os.environ.get(ATTEMPT_ENV, '0') != attempt or \
+            os.environ.get('RANK', '0') != rank:
+        return None
+    if kind == 'crash' and where == 'start':
+        raise RuntimeError('injected failure (DGMC_AMD_BENCH_INJECT)')
+    if kind == 'hang' and where == 'start':
+        while True:
+            time.sleep(60)
+    return kind
+
+
+def _finish_worker():
+    """Tell a supervising parent this rank's measurement is complete (it
+    then tolerates a teardown that hangs)."""
+    if os.environ.get(WORKER_ENV) == '1':
+        print(DONE_MARK, flush=True)
+
+
 def main(argv=None):
     args = parse_args(argv)
+    if args.gpus > 1:
+        # Collectives of a multi-rank bench give up well inside the
+        # driver's run limit (a hang must end in an error, not silence).
+        os.environ.setdefault('DGMC_AMD_DIST_TIMEOUT', '120')
     ngpu = torch.cuda.device_count()    # does not initialise HIP
     if ngpu and args.gpus > ngpu:
         sys.stderr.write('bench.py: --gpus {} but only {} GPU(s) visible\n'
@@ -386,6 +623,7 @@ def main(argv=None):
         if device.type == 'cuda':
             torch.cuda.synchronize()
 
+    injected = _inject('start')
     with reference_mode(reference):
         for _ in range(args.warmup):
             trainer.step()
@@ -472,12 +710,13 @@ def main(argv=None):
         out['hits@10_test'] = round(test_hits[10], 4)
     out['gemm_arith'] = gemm_arith(out['dtype'])
     out.update(dp_diag)
-    if rank == 0:
+    if rank == 0 and injected != 'nojson':
         line = json.dumps(out)
         print(line, flush=True)
-        if args.json_out:
+        if args.json_out and os.environ.get(WORKER_ENV) != '1':
             with open(args.json_out, 'w') as f:
                 f.write(line + '\n')
+    _finish_worker()
     parallel.shutdown()
     return 0
 

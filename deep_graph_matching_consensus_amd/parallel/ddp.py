@@ -116,6 +116,11 @@ class GradBucketAllReducer(object):
             self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad)
                            for p in self.params]
         self._pre = set()          # params whose gradient was pre-reduced
+        # Optional record of the collectives each step issues: a list with
+        # one [(lo, hi), ...] list per step (started by release_grads /
+        # zero_grad) - checked across captured size-bucket graphs and ranks
+        # (train.py::PairTrainer._check_collective_sequence).
+        self.seq_log = None
         if self.in_step:
             me = weakref.ref(self)
             for p in self.params:
@@ -130,6 +135,8 @@ class GradBucketAllReducer(object):
             p.grad = self.flat[off:off + n].view_as(p)
 
     def zero_grad(self):
+        if self.seq_log is not None:
+            self.seq_log.append([])
         self.flat.zero_()
         self.attach_grads()
 
@@ -140,6 +147,8 @@ class GradBucketAllReducer(object):
         the freshly computed gradient tensor as ``p.grad`` (no copy) instead
         of adding it into a zeroed view of the flat buffer - which costs a
         zero-fill of the whole buffer plus one add kernel per parameter."""
+        if self.seq_log is not None:
+            self.seq_log.append([])
         for p in self.params:
             p.grad = None
 
@@ -234,6 +243,8 @@ class GradBucketAllReducer(object):
             self._launch_range(*run)
 
     def _launch_range(self, lo, hi):
+        if self.seq_log is not None and self.seq_log:
+            self.seq_log[-1].append((int(lo), int(hi)))
         buf = self.flat[lo:hi]
         if dist.get_backend(self.group) == 'nccl':
             work = dist.all_reduce(buf, op=dist.ReduceOp.AVG,
@@ -305,3 +316,52 @@ class GradBucketAllReducer(object):
         # Parameters that did not receive a gradient this step keep a
         # consistent (averaged) zero; reset counters for the next step.
         self._reset_counts()
+
+
+def captured_allreduce_preflight(device, sizes, group=None, reps=2):
+    """Capture ONE ``all_reduce(AVG)`` of each size in ``sizes`` (elements)
+    into a hipGraph on the real communicator, replay it ``reps`` times and
+    compare with the uncaptured result - before the training step, whose
+    gradient buckets are captured the same way, is.  Ranks agree on the
+    outcome through an uncaptured ``all_reduce(MIN)``; returns ``(ok,
+    reason)`` (``ok`` identical on every rank).  RCCL only."""
+    ok, reason = True, 'ok'
+    try:
+        gen = torch.Generator().manual_seed(1234 + dist.get_rank(group))
+        for n in sizes:
+            x = torch.randn(int(n), generator=gen).to(device)
+            ref = x.clone()
+            dist.all_reduce(ref, op=dist.ReduceOp.AVG, group=group)
+            buf = x.clone()
+            torch.cuda.synchronize(device)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, capture_error_mode='thread_local'):
+                work = dist.all_reduce(buf, op=dist.ReduceOp.AVG,
+                                       group=group, async_op=True)
+                work.wait()
+            for _ in range(reps):
+                buf.copy_(x)
+                graph.replay()
+                torch.cuda.synchronize(device)
+                if not torch.allclose(buf, ref, rtol=1e-5, atol=1e-6):
+                    ok, reason = False, 'captured all_reduce of {} elements ' \
+                        'differs from the uncaptured one'.format(n)
+                    break
+            del graph
+            if not ok:
+                break
+    except Exception as e:       # capture refused / RCCL error
+        ok, reason = False, '{}: {}'.format(type(e).__name__, e)[:300]
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    agreed = bool(flag.item())
+    if ok and not agreed:
+        reason = 'failed on another rank'
+    return agreed, reason
+
+
+def sequence_digest(seq):
+    """Stable 63-bit digest of a collective sequence ``[(lo, hi), ...]``."""
+    import hashlib
+    h = hashlib.sha256(repr([tuple(map(int, r)) for r in seq]).encode())
+    return int.from_bytes(h.digest()[:8], 'little') & ((1 << 63) - 1)

@@ -44,6 +44,9 @@ IN_STEP_ALLREDUCE = os.environ.get('DGMC_AMD_IN_STEP_ALLREDUCE', '1') == '1'
 # concurrent kernel stretch psi_1's 1024 -> 256 bf16x6 forward from 400 to
 # 615 us; with the grid sized to 256 - 8 CUs it runs 405 us.
 DP_RESERVE_CUS = 16
+# Captured all-reduce pre-flight before the first step capture
+# (DGMC_AMD_DP_PREFLIGHT=0 skips it).
+PREFLIGHT = os.environ.get('DGMC_AMD_DP_PREFLIGHT', '1') == '1'
 
 
 class PairTrainer(object):
@@ -97,6 +100,23 @@ class PairTrainer(object):
             dp_mode = 'captured' if IN_STEP_ALLREDUCE else 'flat'
         assert dp_mode in ('captured', 'flat'), dp_mode
         in_step = dp_mode == 'captured' and (mode == 'static' or graph_rccl)
+        # First-run insurance for captured collectives: one bucket-sized and
+        # one piece-sized all-reduce captured + replayed on the real
+        # communicator before anything else is; every rank falls back to
+        # the flat after-replay all-reduce together if any rank fails.
+        self.dp_checks = {}
+        if in_step and graph_rccl and PREFLIGHT:
+            from .ops.slot_gemm import PIECES
+            piece = max(p.numel() for p in model.parameters()) // \
+                max(PIECES, 1)
+            ok, why = parallel.captured_allreduce_preflight(
+                self.device, [bucket_bytes // 4, piece])
+            self.dp_checks['preflight'] = why
+            if not ok:
+                warnings.warn('captured all-reduce pre-flight failed ({}): '
+                              'using one flat all-reduce after each '
+                              'replay'.format(why))
+                in_step = False
         self.reducer = parallel.GradBucketAllReducer(
             model, bucket_bytes=bucket_bytes,
             overlap=overlap and mode == 'eager', in_step=in_step)
@@ -348,6 +368,8 @@ class PairTrainer(object):
         warm-up iterations before each capture run real steps; their effect
         on the model, optimizer, RNG and sampler is undone afterwards."""
         snap = self._snapshot()
+        check = self.reducer.in_step and self.reducer.distributed
+        seqs = []
         for i, b in enumerate(self.batchers):
             for _ in range(10000):
                 s, t = self.batcher.next_ids()
@@ -355,13 +377,65 @@ class PairTrainer(object):
                     break
             else:
                 raise RuntimeError('no batch fits bucket {}'.format(b))
-            self._graphs[i].capture()
+            if check:
+                self.reducer.seq_log = []
+            try:
+                self._graphs[i].capture()
+            finally:
+                if check:
+                    seqs.append(self.reducer.seq_log)
+                    self.reducer.seq_log = None
         self._captured = True
         self._restore(snap)
+        if check:
+            self._check_collective_sequence(seqs)
         # The capture phase leaves large autograd graphs behind: collect them
         # now, not in the middle of a replayed step (steps pause the cyclic
         # collector themselves, see step()).
         gc.collect()
+
+    def _check_collective_sequence(self, runs_per_bucket):
+        """Ranks replay DIFFERENT size-bucket graphs in the same step, so
+        every captured graph must issue the same ordered (offset, length)
+        all-reduces, on every rank.  ``runs_per_bucket``: per bucket, the
+        collective lists of its warm-up runs and its captured run.  Checked
+        here (bucket vs bucket) and across ranks (digest all-gather); every
+        rank raises together on a mismatch (the bench supervisor then
+        retries with the flat after-replay all-reduce)."""
+        import torch.distributed as dist
+        from .parallel.ddp import sequence_digest
+        problems = []
+        ref = None
+        for i, runs in enumerate(runs_per_bucket):
+            if not runs or not runs[-1]:
+                problems.append('bucket {}: no collective captured'.format(i))
+                continue
+            if any(r != runs[-1] for r in runs):
+                problems.append('bucket {}: warm-up and captured runs '
+                                'differ'.format(i))
+            if ref is None:
+                ref = runs[-1]
+            elif runs[-1] != ref:
+                problems.append('bucket {}: sequence differs from bucket '
+                                '0'.format(i))
+        digest = sequence_digest(ref or [])
+        mine = torch.tensor([digest, len(problems)], dtype=torch.int64,
+                            device=self.device)
+        every = [torch.zeros_like(mine) for _ in range(self.world)]
+        dist.all_gather(every, mine)
+        every = [tuple(int(v) for v in t.tolist()) for t in every]
+        if len({d for d, _ in every}) != 1:
+            problems.append('sequence digests differ across ranks')
+        bad = any(n for _, n in every) or problems
+        self.dp_checks.update({
+            'collective_sequence': 'identical' if not bad else 'MISMATCH',
+            'collectives_per_step': len(ref or []),
+            'bucket_graphs': len(runs_per_bucket),
+            'sequence_digest': '{:016x}'.format(digest)})
+        if bad:
+            raise RuntimeError('captured collective sequence check failed: '
+                               '{}'.format('; '.join(problems) or
+                                           'on another rank'))
 
     def step(self):
         """One training step (data, forward, backward, all-reduce, Adam).
