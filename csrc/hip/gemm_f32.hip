@@ -92,7 +92,7 @@ template <int MB, int NB, bool X6 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
     GfSteps A, int M, const float* __restrict__ bt, int ldb, int Nn,
     const float* __restrict__ bias, int relu, float* __restrict__ Y,
-    int ldy) {
+    int ldy, int accumulate) {
   constexpr int TM = 64 * MB, TN = 64 * NB;
   __shared__ __attribute__((aligned(16))) float sA0_[TM * kGfBK];
   __shared__ __attribute__((aligned(16))) float sA1_[TM * kGfBK];
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
   DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
-  const int ntn = Nn / TN, nk = A.n;
+  const int ntn = (Nn + TN - 1) / TN, nk = A.n;
   const int U = ((M + TM - 1) / TM) * ntn;
   const int G = gridDim.x;
   int u = xcd_remap(blockIdx.x, G);
@@ -139,7 +139,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
     for (int j = 0; j < 2 * NB; ++j) {
       const int row = 16 * NB * wave + 8 * j + prow;
       const int k = swz(row);
-      gf_dma16(k < wid ? bt + (size_t)(brow0 + 8 * j) * ldb + bo + k : zero,
+      gf_dma16(k < wid && brow0 + 8 * j < Nn
+                   ? bt + (size_t)(brow0 + 8 * j) * ldb + bo + k
+                   : zero,
                db + (16 * NB * wave + 8 * j) * kGfBK);
     }
   };
@@ -233,9 +235,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
       float4 bv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        bv[q] = bias ? *reinterpret_cast<const float4*>(bias + nb + 4 * h +
-                                                        32 * a + 8 * q)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[q] = bias && nb + 4 * h + 32 * a + 8 * q < Nn
+                    ? *reinterpret_cast<const float4*>(bias + nb + 4 * h +
+                                                       32 * a + 8 * q)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int b = 0; b < MB; ++b) {
         asm volatile("" ::: "memory");
@@ -273,10 +276,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
           const gf_f32x4 v = *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
               epi + r * 32 + 4 * ((lane & 7) ^ (r & 7)));
           const int m = mb + 32 * b + r;
-          if (m < M)
-            *reinterpret_cast<float4*>(Y + (size_t)m * ldy + nb + 32 * a +
-                                       4 * (lane & 7)) =
-                make_float4(v[0], v[1], v[2], v[3]);
+          const int n = nb + 32 * a + 4 * (lane & 7);
+          if (m < M && n < Nn) {
+            float4* y = reinterpret_cast<float4*>(Y + (size_t)m * ldy + n);
+            float4 o = make_float4(v[0], v[1], v[2], v[3]);
+            if (accumulate) {
+              const float4 p = *y;       // beta = 1 (e.g. a cat gradient)
+              o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+            }
+            *y = o;
+          }
         }
       }
     }
@@ -330,10 +339,13 @@ int gf_num_cus(int dev) {
 
 // Y = act([parts] bt^T + bias).  parts: fp32 [M, K_p] views (unit column
 // stride, 16-byte aligned rows, K_p % 4 == 0); bt: fp32 [Nn, sum K_p] with
-// unit column stride (Nn % 64 == 0); out: optional [M, Nn] view to write.
+// unit column stride (Nn % 4 == 0; a partial last tile column block is
+// masked); out: optional [M, Nn] view to write, or to add into
+// (accumulate: beta = 1).
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
-                       const c10::optional<at::Tensor>& out, bool x6) {
+                       const c10::optional<at::Tensor>& out, bool x6,
+                       bool accumulate) {
   TORCH_CHECK(parts.size() >= 1, "gemm_nt_f32: at least one part");
   const int64_t M = parts[0].size(0);
   GfSteps A{};
@@ -357,8 +369,8 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   TORCH_CHECK(bt.is_cuda() && bt.scalar_type() == at::kFloat &&
                   bt.dim() == 2 && bt.size(1) == K && bt.stride(1) == 1 &&
                   bt.stride(0) % 4 == 0 && aligned16(bt.data_ptr()) &&
-                  bt.size(0) % 64 == 0,
-              "gemm_nt_f32: Bt fp32 [Nn % 64, K] with 16-byte rows");
+                  bt.size(0) % 4 == 0,
+              "gemm_nt_f32: Bt fp32 [Nn % 4, K] with 16-byte rows");
   const int64_t Nn = bt.size(0);
   const float* bp = nullptr;
   if (bias.has_value() && bias->defined()) {
@@ -376,6 +388,7 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                     Y.stride(0) % 4 == 0 && aligned16(Y.data_ptr()),
                 "gemm_nt_f32: out fp32 [M, Nn] with 16-byte rows");
   } else {
+    TORCH_CHECK(!accumulate, "gemm_nt_f32: accumulate needs out");
     Y = at::empty({M, Nn}, bt.options());
   }
   if (M == 0 || Nn == 0) return Y;
@@ -396,10 +409,13 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   const int forced = diag_env_int("DGMC_GEMM_F32_CFG", 0);   // diag build
   for (int c = 0; c < 3; ++c) {
     const int TM = 64 * cfgs[c].mb, TN = 64 * cfgs[c].nb;
-    if (Nn % TN != 0) continue;
-    const int64_t t = ((M + TM - 1) / TM) * (Nn / TN);
+    // (a tile column block past Nn is masked: its share of wasted MACs
+    // counts against the shape)
+    const int64_t tn = (Nn + TN - 1) / TN;
+    const int64_t t = ((M + TM - 1) / TM) * tn;
     const int64_t rounds = (t + 2 * cus - 1) / (2 * cus);
-    const double cost = (double)rounds * cfgs[c].mb * cfgs[c].nb * cfgs[c].eff;
+    const double cost = (double)rounds * cfgs[c].mb * cfgs[c].nb *
+                        cfgs[c].eff * ((double)(tn * TN) / (double)Nn);
     if (forced ? c == forced - 1 : (pick < 0 || cost < best - 1e-9)) {
       pick = c;
       best = cost;
@@ -421,7 +437,7 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                      stream(), A,
                      (int)M, bt.data_ptr<float>(), (int)bt.stride(0),
                      (int)Nn, bp, relu ? 1 : 0, Y.data_ptr<float>(),
-                     (int)Y.stride(0));
+                     (int)Y.stride(0), accumulate ? 1 : 0);
   DGMC_CHECK_LAUNCH();
   return Y;
 }

@@ -28,7 +28,11 @@ void rel_proj_bwd(const at::Tensor& dpq, const at::Tensor& feat,
 void rel_fold(at::TensorList parts, at::TensorList outs);
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
-                       const c10::optional<at::Tensor>& out, bool x6);
+                       const c10::optional<at::Tensor>& out, bool x6,
+                       bool accumulate);
+at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
+                       const c10::optional<at::Tensor>& out, bool accumulate,
+                       bool x6, int64_t splits);
 std::tuple<at::Tensor, at::Tensor> fold_weights_bwd(const at::Tensor& w1,
                                                     const at::Tensor& wf,
                                                     const at::Tensor& g);
@@ -371,7 +375,11 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def("rel_fold(Tensor[] parts, Tensor(a!)[] outs) -> ()");
   m.def(
       "gemm_nt_f32(Tensor[] parts, Tensor bt, Tensor? bias=None, bool "
-      "relu=False, Tensor(a!)? out=None, bool x6=False) -> Tensor");
+      "relu=False, Tensor(a!)? out=None, bool x6=False, bool accumulate="
+      "False) -> Tensor");
+  m.def(
+      "gemm_tn_f32(Tensor[] a_parts, Tensor[] b_parts, Tensor(a!)? out=None, "
+      "bool accumulate=False, bool x6=True, int splits=0) -> Tensor");
   m.def("fold_weights_bwd(Tensor w1, Tensor wf, Tensor g) -> (Tensor, Tensor)");
   m.def(
       "rel_proj_bwd(Tensor dpq, Tensor feat, Tensor fold, Tensor(a!) dfeat, "
@@ -618,6 +626,7 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("fold_weights_bwd", &dgmc::fold_weights_bwd);
   m.impl("rel_fold", &dgmc::rel_fold);
   m.impl("gemm_nt_f32", &dgmc::gemm_nt_f32);
+  m.impl("gemm_tn_f32", &dgmc::gemm_tn_f32);
   m.impl("spmm_csr", &dgmc::spmm_csr);
   m.impl("spmm_csr_planes", &dgmc::spmm_csr_planes);
   m.impl("spmm_csr_out", &dgmc::spmm_csr_out);

@@ -68,11 +68,11 @@ def _rows16(t):
 
 
 def nt_f32_supported(parts, bt):
-    """``[parts] @ bt^T`` on the exact-f32 chunked GEMM
-    (``csrc/hip/gemm_f32.hip``): fp32 device operands with 16-byte rows,
-    output width a multiple of 64, K <= 3072."""
+    """``[parts] @ bt^T`` on the chunked NT GEMM (``csrc/hip/gemm_f32.hip``):
+    fp32 device operands with 16-byte rows, output width a multiple of 4
+    (a partial last tile column block is masked), K <= 3072."""
     if not (parts and _backend.use_hip(parts[0]) and _rows16(bt) and
-            bt.size(0) % 64 == 0):
+            bt.size(0) % 4 == 0):
         return False
     M = parts[0].size(0)
     chunks = 0
@@ -91,23 +91,53 @@ def nt_f32_supported(parts, bt):
 NT_X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
 
 
-def nt_f32(parts, bt, bias=None, relu=False, out=None, x6=None):
+def nt_f32(parts, bt, bias=None, relu=False, out=None, x6=None,
+           accumulate=False):
     """``act([parts] @ bt^T + bias)`` (fp32, no autograd; parts read in
     place, never concatenated).  ``x6``: bf16x6 products (default
-    :data:`NT_X6`) or the exact-f32 chain."""
+    :data:`NT_X6`) or the exact-f32 chain.  ``accumulate``: add the product
+    into ``out`` (beta = 1) instead of overwriting it."""
     b = None
     if bias is not None:
         b = bias.detach()
         if not b.is_contiguous():
             b = b.contiguous()
     return _backend.ops().gemm_nt_f32(list(parts), bt, b, relu, out,
-                                      NT_X6 if x6 is None else bool(x6))
+                                      NT_X6 if x6 is None else bool(x6),
+                                      bool(accumulate))
+
+
+def _tn_part_ok(t, K):
+    return (t.dim() == 2 and t.size(0) == K and t.dtype == torch.float32 and
+            t.is_cuda and t.stride(1) == 1 and t.size(1) % 4 == 0 and
+            (t.stride(0) % 4 == 0 or K <= 1) and t.data_ptr() % 16 == 0)
+
+
+def tn_f32_supported(a_parts, b_parts):
+    """``[a_parts]^T [b_parts]`` on the split-K TN GEMM
+    (``csrc/hip/gemm_tn.hip``): fp32 device parts ``[K, w]`` with 16-byte
+    rows, widths multiples of 4, at most 8 parts per operand."""
+    if not (a_parts and b_parts and len(a_parts) <= 8 and len(b_parts) <= 8
+            and _backend.use_hip(a_parts[0])):
+        return False
+    K = a_parts[0].size(0)
+    return all(_tn_part_ok(t, K) for t in list(a_parts) + list(b_parts))
+
+
+def tn_f32(a_parts, b_parts, out=None, accumulate=False, x6=None):
+    """``[a_parts]^T [b_parts]`` (fp32 ``[M, N]``; written, or added into
+    ``out``).  bf16x6 products unless ``x6=False`` / ``DGMC_AMD_X6=0``."""
+    return _backend.ops().gemm_tn_f32(list(a_parts), list(b_parts), out,
+                                      bool(accumulate),
+                                      NT_X6 if x6 is None else bool(x6), 0)
 
 
 class _LinearParts(torch.autograd.Function):
     """``torch.cat(parts, -1) @ W^T + b`` without the concatenation: the
-    exact-f32 chunked GEMM reads the parts in place (forward); backward by
-    per-part library products (the training-phase path)."""
+    chunked NT GEMM (bf16x6 unless ``DGMC_AMD_X6=0``) reads the parts in
+    place.  Backward on the same kernels: the input gradients of the parts
+    that need one are ONE NT product ``g W[:, lo:hi]`` (handed out as column
+    slices), the weight gradient ONE split-K TN product ``g^T [parts]``."""
 
     @staticmethod
     def forward(ctx, weight, bias, *parts):
@@ -122,15 +152,29 @@ class _LinearParts(torch.autograd.Function):
     def backward(ctx, g):
         weight, *parts = ctx.saved_tensors
         g = g.contiguous()
-        grads, off = [], 0
-        for i, w in enumerate(ctx.widths):
-            grads.append(g @ weight[:, off:off + w]
-                         if ctx.needs_input_grad[2 + i] else None)
-            off += w
+        need = [ctx.needs_input_grad[2 + i] for i in range(len(parts))]
+        grads = [None] * len(parts)
+        offs = [0]
+        for w in ctx.widths:
+            offs.append(offs[-1] + w)
+        if any(need):
+            lo = offs[need.index(True)]
+            hi = offs[len(need) - need[::-1].index(True)]
+            wt = weight.detach().t().contiguous()        # [in, out]
+            if nt_f32_supported([g], wt[lo:hi]):
+                dx = nt_f32([g], wt[lo:hi])
+            else:
+                dx = g @ weight[:, lo:hi]
+            for i, w in enumerate(ctx.widths):
+                if need[i]:
+                    grads[i] = dx[:, offs[i] - lo:offs[i] - lo + w]
         gw = gb = None
         if ctx.needs_input_grad[0]:
-            gw = torch.cat([matmul_tn_fp32(g, p.contiguous())
-                            for p in parts], 1)
+            if tn_f32_supported([g], parts):
+                gw = tn_f32([g], parts)
+            else:
+                gw = torch.cat([matmul_tn_fp32(g, p.contiguous())
+                                for p in parts], 1)
         if ctx.has_bias and ctx.needs_input_grad[1]:
             gb = _col_sum(g)
         return (gw, gb) + tuple(grads)
@@ -138,7 +182,8 @@ class _LinearParts(torch.autograd.Function):
 
 def linear_parts(parts, weight, bias=None):
     """``F.linear(torch.cat(parts, -1), weight, bias)``; on the GPU (fp32)
-    the parts are read in place by one exact-f32 GEMM (no concatenation)."""
+    the parts are read in place by one chunked NT GEMM (bf16x6 unless
+    ``DGMC_AMD_X6=0``; no concatenation)."""
     parts = list(parts)
     ok = nt_f32_supported(parts, weight) and (
         bias is None or (bias.dtype == torch.float32 and
@@ -198,6 +243,10 @@ def matmul_tn_fp32(a, b, out=None, accumulate=False):
         from .dense import _seg01
         res = _backend.ops().dense_wgrad_f32([a], 1, [b],
                                              _seg01(K, a.device))
+    elif tn_f32_supported([a], [b]):
+        # fp32, any width: the split-K TN MFMA kernel (csrc/hip/gemm_tn.hip;
+        # the deterministic fold writes / adds ``out`` directly).
+        return tn_f32([a], [b], out=out, accumulate=accumulate)
     elif not a.is_cuda:
         res = a.float().t() @ b.float()
     else:

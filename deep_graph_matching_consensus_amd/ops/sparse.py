@@ -490,6 +490,25 @@ class _GemmSpMM(torch.autograd.Function):
         dY = dy.view(xc.size(0), -1)
         # 3. dx (unfused path) and dW.  A passthrough consumer's gradient
         #    enters the GEMM epilogue (beta = 1): no separate add kernel.
+        if ctx.needs_input_grad[0] and gx is None and hip and \
+                dY.dtype == torch.float32 and ctx.x_dtype == torch.float32:
+            # fp32 (RelConv's stacked map, ψ₁ of the DBP15K config): dx =
+            # dY [N, 3C] @ W_stacked [3C, K] on the chunked NT GEMM; a
+            # passthrough consumer's gradient is accumulated in place by its
+            # epilogue (beta = 1, ``passthrough='cat'``) - no library GEMM.
+            from .gemm import nt_f32, nt_f32_supported
+            bt = w_lp.contiguous()                   # [K, 3C]
+            if nt_f32_supported([dY], bt):
+                if ctx.passthrough == 'cat' and gpass is not None and \
+                        gpass.dtype == torch.float32 and \
+                        gpass.shape == (dY.size(0), bt.size(0)) and \
+                        gpass.dim() == 2 and gpass.stride(1) == 1 and \
+                        gpass.stride(0) % 4 == 0 and \
+                        gpass.data_ptr() % 16 == 0:
+                    gx = nt_f32([dY], bt, out=gpass, accumulate=True)
+                    gpass = None
+                else:
+                    gx = nt_f32([dY], bt)
         if ctx.needs_input_grad[0] and gx is None:
             if gpass is not None and gpass.dtype == dY.dtype == \
                     ctx.x_dtype and gpass.shape == (dY.size(0),
