@@ -14,13 +14,14 @@
 // past their last column.
 //
 // Kernel: 128 x 128 output tiles of 4 waves (64 x 64 each, 2 x 2 MFMA blocks
-// of 32 x 32), the K range of the grid split into equal 32-row-aligned
+// of 32 x 32), the K range of the grid split into equal 16-row-aligned
 // chunks so that tiles x splits fills two workgroups per CU.  Each step
-// stages 32 rows of both operand column blocks as k-major fp32 images
-// ([32][128] floats, 16 KB each) by global_load_lds_dwordx4 into one of two
-// LDS stages; the MFMA operand of lane (i, h) is column i of rows 8 h .. + 7
-// (bf16x6) or row 2 s + h (exact f32): 32 consecutive floats per half wave,
-// conflict-free ds_read_b32.
+// stages 16 rows of both operand column blocks as k-major fp32 images
+// ([16][128] floats, 8 KB each) by global_load_lds_dwordx4 into a ring of
+// four LDS stages (three steps in flight while one is multiplied: HBM
+// latency is hidden at two workgroups per CU); the MFMA operand of lane
+// (i, h) is column i of rows 8 h .. + 7 (bf16x6) or row 2 s + h (exact f32):
+// 32 consecutive floats per half wave, conflict-free ds_read_b32.
 //
 // Arithmetic: bf16x6 (each fp32 operand split into three bf16 terms in
 // registers, six v_mfma_f32_32x32x16_bf16 per 16-deep step into a large-
@@ -41,7 +42,8 @@ typedef float tn_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kTnT = 128;               // tile rows / columns
-constexpr int kTnK = 32;                // k rows per staged step
+constexpr int kTnK = 16;                // k rows per staged step
+constexpr int kTnNst = 4;               // LDS ring stages
 constexpr int kTnImg = kTnK * kTnT;     // floats per operand image
 constexpr int kTnTile = kTnT * kTnT;    // floats per partial tile
 constexpr int kTnMaxParts = 8;
@@ -86,18 +88,25 @@ __device__ __forceinline__ const float* tn_col(const TnParts& P, int c,
   return r;
 }
 
+// Wait until at most N of this thread's DMAs are outstanding (N: 4 per
+// younger stage in flight).
+__device__ __forceinline__ void tn_wait_stages(int younger) {
+  switch (younger) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+  }
+}
+
 template <bool X6>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     TnParts A, TnParts B, int K, int kchunk, int tiles_n, int tiles,
     float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sA0_[kTnImg];
-  __shared__ __attribute__((aligned(16))) float sA1_[kTnImg];
-  __shared__ __attribute__((aligned(16))) float sB0_[kTnImg];
-  __shared__ __attribute__((aligned(16))) float sB1_[kTnImg];
-  DGMC_LDS float* sA0 = (DGMC_LDS float*)sA0_;
-  DGMC_LDS float* sA1 = (DGMC_LDS float*)sA1_;
-  DGMC_LDS float* sB0 = (DGMC_LDS float*)sB0_;
-  DGMC_LDS float* sB1 = (DGMC_LDS float*)sB1_;
+  __shared__ __attribute__((aligned(16))) float sA_[kTnNst * kTnImg];
+  __shared__ __attribute__((aligned(16))) float sB_[kTnNst * kTnImg];
+  DGMC_LDS float* sA = (DGMC_LDS float*)sA_;
+  DGMC_LDS float* sB = (DGMC_LDS float*)sB_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   // consecutive logical blocks = the tiles of one k chunk: they share its
@@ -109,24 +118,26 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
   const int k1 = min(K, k0 + kchunk);
   const int nsteps = k1 > k0 ? (k1 - k0 + kTnK - 1) / kTnK : 0;
 
-  // Staging: wave w's DMA j covers rows 8 w + 2 j (lanes 0-31) and + 1
+  // Staging: wave w's DMA j covers rows 4 w + 2 j (lanes 0-31) and + 1
   // (lanes 32-63), 16-byte chunk lane % 32 of the 128 columns.
   const int cc = 4 * (lane & 31);
   int lda, ldb;
   const float* acol = tn_col(A, tm * kTnT + cc, lda);
   const float* bcol = tn_col(B, tn * kTnT + cc, ldb);
-  const int rbase = 8 * wave + (lane >> 5);
+  const int rbase = 4 * wave + (lane >> 5);
   const float* zero = g_tn_zero;
-  auto stage = [&](int s, DGMC_LDS float* da, DGMC_LDS float* db) {
+  auto stage = [&](int s) {
     const int kb = k0 + s * kTnK;
+    DGMC_LDS float* da = sA + (s % kTnNst) * kTnImg;
+    DGMC_LDS float* db = sB + (s % kTnNst) * kTnImg;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 2; ++j) {
       const int row = kb + rbase + 2 * j;
       const bool in = row < k1;
       tn_dma16(in && acol ? acol + (size_t)row * lda : zero,
-               da + (8 * wave + 2 * j) * kTnT);
+               da + (4 * wave + 2 * j) * kTnT);
       tn_dma16(in && bcol ? bcol + (size_t)row * ldb : zero,
-               db + (8 * wave + 2 * j) * kTnT);
+               db + (4 * wave + 2 * j) * kTnT);
     }
   };
 
@@ -141,44 +152,42 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
   const int am = wm * 64 + i, bn = wn * 64 + i;
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
     if (X6) {
+      // one 16-deep step: lane (i, h) supplies rows 8 h .. 8 h + 7
+      tn_bf16x8 av[2][3], bv[2][3];
+      const int kr = 8 * h;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        tn_bf16x8 av[2][3], bv[2][3];
-        const int kr = 16 * st + 8 * h;
+      for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-#pragma unroll
-          for (int a = 0; a < 2; ++a) {
-            __bf16 hh, mm, ll;
-            split3_bf16(la[(kr + j) * kTnT + am + 32 * a], hh, mm, ll);
-            av[a][0][j] = hh;
-            av[a][1][j] = mm;
-            av[a][2][j] = ll;
-          }
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            __bf16 hh, mm, ll;
-            split3_bf16(lb[(kr + j) * kTnT + bn + 32 * b], hh, mm, ll);
-            bv[b][0][j] = hh;
-            bv[b][1][j] = mm;
-            bv[b][2][j] = ll;
-          }
+        for (int a = 0; a < 2; ++a) {
+          __bf16 hh, mm, ll;
+          split3_bf16(la[(kr + j) * kTnT + am + 32 * a], hh, mm, ll);
+          av[a][0][j] = hh;
+          av[a][1][j] = mm;
+          av[a][2][j] = ll;
         }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            tn_f32x16 sm = acs[a][b];
-            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][2], bv[b][0], sm, 0, 0, 0);
-            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][2], sm, 0, 0, 0);
-            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][1], sm, 0, 0, 0);
-            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][0], sm, 0, 0, 0);
-            sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][1], sm, 0, 0, 0);
-            acs[a][b] = sm;
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                av[a][0], bv[b][0], acc[a][b], 0, 0, 0);
-          }
+        for (int b = 0; b < 2; ++b) {
+          __bf16 hh, mm, ll;
+          split3_bf16(lb[(kr + j) * kTnT + bn + 32 * b], hh, mm, ll);
+          bv[b][0][j] = hh;
+          bv[b][1][j] = mm;
+          bv[b][2][j] = ll;
+        }
       }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          tn_f32x16 sm = acs[a][b];
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][2], bv[b][0], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][2], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][1], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][0], sm, 0, 0, 0);
+          sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][1], sm, 0, 0, 0);
+          acs[a][b] = sm;
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              av[a][0], bv[b][0], acc[a][b], 0, 0, 0);
+        }
       return;
     }
 #pragma unroll
@@ -198,19 +207,16 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     }
   };
 
-  if (nsteps > 0) stage(0, sA0, sB0);
+  // kTnNst-stage ring: kTnNst - 1 steps in flight while one is multiplied;
+  // the stage refilled at step s was consumed at step s - 1 (its trailing
+  // barrier orders the refill after every wave's reads).
+  const int pro = min(nsteps, kTnNst - 1);
+  for (int s = 0; s < pro; ++s) stage(s);
   for (int s = 0; s < nsteps; ++s) {
-    DGMC_LDS float* ca = (s & 1) ? sA1 : sA0;
-    DGMC_LDS float* cb = (s & 1) ? sB1 : sB0;
-    if (s + 1 < nsteps) {
-      stage(s + 1, (s & 1) ? sA0 : sA1, (s & 1) ? sB0 : sB1);
-      // (this thread's 8 DMAs of the next step stay in flight)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (s + kTnNst - 1 < nsteps) stage(s + kTnNst - 1);
+    tn_wait_stages(min(kTnNst - 1, nsteps - 1 - s));
     tn_barrier();
-    compute(ca, cb);
+    compute(sA + (s % kTnNst) * kTnImg, sB + (s % kTnNst) * kTnImg);
     tn_barrier();
   }
 
@@ -339,7 +345,7 @@ at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
   const int64_t cus = tn_num_cus(a_parts[0].device().index());
   if (splits <= 0)
     splits = std::max<int64_t>(1, (2 * cus + tiles - 1) / tiles);
-  // equal chunks of whole 32-row steps
+  // equal chunks of whole 16-row steps
   const int64_t steps = std::max<int64_t>(1, (K + kTnK - 1) / kTnK);
   splits = std::min(splits, steps);
   const int64_t kchunk = ((steps + splits - 1) / splits) * kTnK;

@@ -95,7 +95,7 @@ at::Tensor train_candidates(const at::Tensor& topk, int64_t n_t, int64_t kr,
                             const at::Tensor& gt_row,
                             const at::Tensor& gt_col);
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
-                    int64_t mode);
+                    int64_t mode, const c10::optional<at::Tensor>& warm);
 std::vector<at::Tensor> topk_dot_refined_stats(const at::Tensor& h_s,
                                                const at::Tensor& h_t,
                                                int64_t k);
@@ -418,7 +418,9 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "w2, Tensor ptr_s, Tensor ptr_t, Tensor(a!)? dpq_out=None, Tensor(b!)? "
       "part=None, bool accumulate=False) -> (Tensor, Tensor, Tensor, "
       "Tensor)");
-  m.def("topk_dot(Tensor h_s, Tensor h_t, int k, int mode=2) -> Tensor");
+  m.def(
+      "topk_dot(Tensor h_s, Tensor h_t, int k, int mode=2, Tensor(a!)? "
+      "warm=None) -> Tensor");
   m.def("topk_dot_refined_stats(Tensor h_s, Tensor h_t, int k) -> Tensor[]");
   m.def("train_candidates(Tensor topk, int n_t, int kr, Tensor gt_row, "
         "Tensor gt_col) -> Tensor");

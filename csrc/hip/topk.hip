@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     const __bf16* __restrict__ t_lo,
     float* __restrict__ part_v, int* __restrict__ part_i,
     int64_t* __restrict__ out, float* __restrict__ out_v, int Ns, int Nt,
-    int C, int k, int span, int dbg) {
+    int C, int k, int span, int dbg, const float* __restrict__ warm) {
   constexpr int CP = NKS * 16;              // padded channels
   constexpr int BP = CP + 8;                // LDS row pitch (bf16)
   constexpr int TILE = kX3Tile * BP;        // one hi or lo tile (bf16)
@@ -288,15 +288,28 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
 
   float lv[16];
   int li[16];
-  const int init_i = part_v ? Nt + split * 64 + hl : 0;   // unique sentinels
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { lv[r] = -INFINITY; li[r] = init_i; }
-
+  const int init_i = Nt + split * 64 + hl;    // unique sentinels (>= Nt)
   // k-th value of each row's list, kept per half-wave (lanes of half h hold
   // their row's threshold) - no readlane per candidate test.
   float thr[16];
+  // Warm start (topk_warm_kernel): each list starts FULL of sentinel
+  // entries valued just below a proven lower bound of the row's k-th
+  // approximate score, so only targets that can still make the final list
+  // are ever inserted.  Every member of the row's true top-k (by
+  // approximate score) lies strictly above the start value and evicts the
+  // sentinels; the selected lists are the same as from an empty start.
 #pragma unroll
-  for (int r = 0; r < 16; ++r) thr[r] = -INFINITY;
+  for (int r = 0; r < 16; ++r) {
+    float t0 = -INFINITY;
+    const int row = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (warm && row < Ns) {
+      const float w = warm[(size_t)b * Ns + row];
+      t0 = w > -INFINITY ? nextafterf(w, -INFINITY) : -INFINITY;  // NaN too
+    }
+    lv[r] = t0;
+    li[r] = init_i;
+    thr[r] = t0;
+  }
 
   const int ntiles = (j_end - j_begin + kX3Tile - 1) / kX3Tile;
   u32x4 pre[2 * PRE];
@@ -380,8 +393,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
         part_v[o] = lv[r];
         part_i[o] = li[r];
       } else {
-        out[g * k + hl] = (int64_t)li[r];
-        if (out_v) out_v[g * k + hl] = lv[r];
+        // (a sentinel can only survive a warm start whose bound did not
+        // hold: it leaves as index 0 with value -inf, which the exact
+        // re-score treats as a short list - the exhaustive fallback)
+        const bool real = li[r] < Nt;
+        out[g * k + hl] = real ? (int64_t)li[r] : 0;
+        if (out_v) out_v[g * k + hl] = real ? lv[r] : -INFINITY;
       }
     }
   }
@@ -476,7 +493,8 @@ static float topk_tau() {
 }
 
 static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
-                              int64_t k, at::Tensor* vals = nullptr);
+                              int64_t k, at::Tensor* vals = nullptr,
+                              const at::Tensor* warm = nullptr);
 constexpr int kRefRows = 4;      // rows (waves) per block
 
 // Per-block partial maxima of |h_t[b, j]|^2 (any summation order: the value
@@ -716,9 +734,76 @@ __global__ __launch_bounds__(kRef4Waves * 64) void topk_refine4_kernel(
   }
 }
 
+// Warm start of the filter from an earlier candidate list `prev` (row
+// stride ld, e.g. the previous training step's filter output): per row,
+// the K2 <= 16 listed targets are re-scored with the exact chain and
+//   warm_i = min_j s_j - E_i    (E_i: the refine kernels' bound on
+//                                |approximate - exact| score),
+// a lower bound of the row's K2-th approximate score - K2 distinct targets
+// have an approximate score >= min_j s_j - E_i.  Rows whose list is not K2
+// distinct in-range indices (or any non-finite score) get -inf (cold).
+// Four rows per wave, lane c of group r re-scores row r's candidate c.
+__global__ __launch_bounds__(kRef4Waves * 64) void topk_warm_kernel(
+    const float* __restrict__ h_s, const float* __restrict__ h_t,
+    const int64_t* __restrict__ prev, int ld,
+    const float* __restrict__ nmax_part, int nparts,
+    float* __restrict__ warm, int Ns, int Nt, int C, int K2, float tau) {
+  __shared__ __attribute__((aligned(16))) float sa[kRef4Waves][4][264];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, c = lane & 15;
+  const int64_t g0 = ((int64_t)blockIdx.x * kRef4Waves + wave) * 4;
+  const int b = blockIdx.y;
+  if (g0 >= Ns) return;                  // wave-uniform; no block barrier
+  const int64_t g = g0 + grp;
+  const bool row_ok = g < Ns;
+  const int C8 = (C + 7) & ~7;
+  DGMC_LDS float* a = (DGMC_LDS float*)sa[wave][grp];
+  float sq = 0.f;
+  {
+    const float* arow = h_s + ((size_t)b * Ns + (row_ok ? g : g0)) * C;
+    for (int e = c; e < C8; e += 16) {
+      const float v = e < C ? arow[e] : 0.f;
+      a[e] = v;
+      sq += v * v;
+    }
+  }
+#pragma unroll
+  for (int d = 8; d >= 1; d >>= 1) sq += __shfl_xor(sq, d);   // group sum
+  float bm = 0.f;
+  for (int p = lane; p < nparts; p += 64)
+    bm = fmaxf(bm, nmax_part[(size_t)b * nparts + p]);
+  bm = wave_max(bm);
+  const float E = tau * sqrtf(sq * bm) * (1.0f + 1.0f / 1024.0f);
+  const size_t o = (size_t)b * Ns + (row_ok ? g : g0);
+  const bool has = c < K2;
+  const int64_t cl = has ? prev[o * ld + c] : 0;
+  bool ok = !has || (cl >= 0 && cl < Nt);
+  const int ci = ok ? (int)cl : -1 - c;     // (invalid: unique, never used)
+  // distinct: no earlier lane of the group holds the same index
+  const int base = grp * 16;
+  for (int l = 0; l < 16; ++l) {
+    const int oj = __shfl(ci, base + l);
+    if (has && l < c && oj == ci) ok = false;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const float* tb = h_t + (size_t)b * Nt * C;
+  float s = has && ok ? exact_dot(a, tb + (size_t)ci * C, C, C8) : INFINITY;
+  if (!has) s = INFINITY;
+  if (!(s == s)) ok = false;             // NaN
+  float m = ok ? s : -INFINITY;
+#pragma unroll
+  for (int d = 8; d >= 1; d >>= 1) m = fminf(m, __shfl_xor(m, d));
+  const bool all_ok = (unsigned)(__ballot(!ok) >> base & 0xffffu) == 0u;
+  if (row_ok && c == 0) {
+    const float t = m - E;
+    warm[o] = all_ok && t - t == 0.f ? t : -INFINITY;     // finite only
+  }
+}
+
 static at::Tensor topk_dot_refined(const at::Tensor& h_s,
                                    const at::Tensor& h_t, int64_t k,
-                                   at::Tensor* n_overflow) {
+                                   at::Tensor* n_overflow,
+                                   const at::Tensor* warm_state = nullptr) {
   const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
   const int Nt = h_t.size(1);
   // Candidates kept by the filter pass: k + 6 (>= 16), at most 32.  The
@@ -729,18 +814,36 @@ static at::Tensor topk_dot_refined(const at::Tensor& h_s,
   static const int k2_env = diag_env_int("DGMC_TOPK_K2", 0);
   int K2 = k2_env > 0 ? k2_env : std::max<int>(16, (int)k + 6);
   K2 = std::min(std::min(32, Nt), std::max<int>(K2, (int)k));
-  at::Tensor cv;
-  at::Tensor ci = topk_dot_x3(h_s, h_t, K2, &cv);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
   at::Tensor cnt = at::zeros({1}, h_s.options().dtype(at::kInt));
   if (n_overflow) *n_overflow = cnt;
-  if (B == 0 || Ns == 0) return out;
   const int nparts = (Nt + 255) / 256;
   at::Tensor part = at::empty({B, nparts}, h_s.options());
-  hipLaunchKernelGGL(row_sqnorm_max_kernel, dim3(nparts, B), dim3(256), 0,
-                     stream(), h_t.data_ptr<float>(), Nt, C,
-                     part.data_ptr<float>());
-  DGMC_CHECK_LAUNCH();
+  if (B > 0 && Nt > 0) {
+    hipLaunchKernelGGL(row_sqnorm_max_kernel, dim3(nparts, B), dim3(256), 0,
+                       stream(), h_t.data_ptr<float>(), Nt, C,
+                       part.data_ptr<float>());
+    DGMC_CHECK_LAUNCH();
+  }
+  at::Tensor warm;
+  const bool use_warm = warm_state != nullptr && K2 <= 16 && B > 0 && Ns > 0;
+  if (use_warm) {
+    warm = at::empty({B, Ns}, h_s.options());
+    hipLaunchKernelGGL(topk_warm_kernel,
+                       dim3((Ns + 4 * kRef4Waves - 1) / (4 * kRef4Waves), B),
+                       dim3(kRef4Waves * 64), 0, stream(),
+                       h_s.data_ptr<float>(), h_t.data_ptr<float>(),
+                       warm_state->data_ptr<int64_t>(),
+                       (int)warm_state->size(2), part.data_ptr<float>(),
+                       nparts, warm.data_ptr<float>(), Ns, Nt, C, K2,
+                       topk_tau());
+    DGMC_CHECK_LAUNCH();
+  }
+  at::Tensor cv;
+  at::Tensor ci = topk_dot_x3(h_s, h_t, K2, &cv, use_warm ? &warm : nullptr);
+  if (warm_state != nullptr && B > 0 && Ns > 0)
+    warm_state->narrow(2, 0, K2).copy_(ci);       // the next call's start
+  if (B == 0 || Ns == 0) return out;
   if (K2 <= 16) {
     hipLaunchKernelGGL(topk_refine4_kernel,
                        dim3((Ns + 4 * kRef4Waves - 1) / (4 * kRef4Waves), B),
@@ -790,7 +893,8 @@ static int x3_splits(int64_t row_blocks, int Nt, int per_cu) {
 }
 
 static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
-                              int64_t k, at::Tensor* vals) {
+                              int64_t k, at::Tensor* vals,
+                              const at::Tensor* warm) {
   const int B = h_s.size(0), Ns = h_s.size(1), C = h_s.size(2);
   const int Nt = h_t.size(1);
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
@@ -841,7 +945,8 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
                        S > 1 ? pv.data_ptr<float>() : nullptr,
                        S > 1 ? pi.data_ptr<int>() : nullptr,
                        out.data_ptr<int64_t>(), out_v, Ns, Nt, C, (int)k,
-                       span, topk_debug());
+                       span, topk_debug(),
+                       warm ? warm->data_ptr<float>() : nullptr);
   };
   switch (NKS) {
     case 4: launch(topk_x3_kernel<4, 4>); break;
@@ -873,7 +978,7 @@ static at::Tensor topk_dot_x3(const at::Tensor& h_s, const at::Tensor& h_t,
 // 2 (default): exact - the split-bf16 filter + exact re-score above, with
 // the brute-force kernel where the filter does not apply (k > 32).
 at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
-                    int64_t mode) {
+                    int64_t mode, const c10::optional<at::Tensor>& warm) {
   TORCH_CHECK(h_s.is_cuda() && h_t.is_cuda() && h_s.dim() == 3 &&
                   h_t.dim() == 3 && h_s.scalar_type() == at::kFloat &&
                   h_t.scalar_type() == at::kFloat && h_s.is_contiguous() &&
@@ -886,7 +991,20 @@ at::Tensor topk_dot(const at::Tensor& h_s, const at::Tensor& h_t, int64_t k,
   TORCH_CHECK(k >= 1 && k <= 64 && k <= Nt, "topk_dot: need 1 <= k <= min(64, N_t)");
   TORCH_CHECK(C % 4 == 0 && C <= 256, "topk_dot: C % 4 == 0 and C <= 256");
   if (mode == 0 && k <= 32) return topk_dot_x3(h_s, h_t, k);
-  if (mode == 2 && k <= 16) return topk_dot_refined(h_s, h_t, k, nullptr);
+  if (mode == 2 && k <= 16) {
+    const at::Tensor* ws = nullptr;
+    if (warm.has_value() && warm->defined()) {
+      // int64 [B, N_s, >= K2] candidate state (any content: entries that are
+      // not K2 distinct in-range indices only disable the warm start)
+      TORCH_CHECK(warm->is_cuda() && warm->scalar_type() == at::kLong &&
+                      warm->dim() == 3 && warm->size(0) == B &&
+                      warm->size(1) == Ns && warm->size(2) >= 32 &&
+                      warm->is_contiguous(),
+                  "topk_dot: warm state int64 [B, N_s, 32]");
+      ws = &*warm;
+    }
+    return topk_dot_refined(h_s, h_t, k, nullptr, ws);
+  }
   at::Tensor out = at::empty({B, Ns, k}, h_s.options().dtype(at::kLong));
   if (B == 0 || Ns == 0) return out;
   const int CT = (C + 63) / 64;

@@ -24,6 +24,7 @@ What differs is the execution plan (MI355X-first):
   the encoders' GEMMs drop to bf16);
 * all random indicators of the L steps are drawn with one ``randn`` call.
 """
+import collections
 import contextlib
 import os
 
@@ -51,6 +52,8 @@ FOLD_PROJECTION = os.environ.get('DGMC_AMD_FOLD_PROJECTION', '1') == '1'
 SINKHORN_FUSED = os.environ.get('DGMC_AMD_SINKHORN_FUSED', '1') == '1'
 
 EPS = 1e-8
+# Cached sparse-output COO row index tensors (one per (N_s, k, device)).
+COO_ROWS_CACHE = 4
 _PAIR_CACHE = _IdentityCache(max_entries=8)
 
 
@@ -133,12 +136,13 @@ class _FoldProduct(torch.autograd.Function):
         if g is None:
             return None, None, None
         g = g.float()
+        w1c, wfc, gc = w1.contiguous(), wf.contiguous(), g.contiguous()
         if _backend.use_hip(w1) and w1.dtype == wf.dtype == torch.float32 \
-                and wf.size(1) % 4 == 0:
+                and wf.size(1) % 4 == 0 and all(
+                    t.data_ptr() % 16 == 0 for t in (w1c, wfc, gc)):
             # both products in one launch (relconv.hip::fold_weights_bwd:
             # k-ordered fp32 chains, no library GEMM in the step)
-            gw1, gwf = _backend.ops().fold_weights_bwd(
-                w1.contiguous(), wf.contiguous(), g.contiguous())
+            gw1, gwf = _backend.ops().fold_weights_bwd(w1c, wfc, gc)
             gw1 = gw1 if ctx.needs_input_grad[0] else None
             gwf = gwf if ctx.needs_input_grad[1] else None
         else:
@@ -274,8 +278,33 @@ class DGMC(torch.nn.Module):
     # Sparse helpers
     # ------------------------------------------------------------------
     def __top_k__(self, x_s, x_t):  # pragma: no cover
-        r"""Memory-efficient top-k correspondence computation."""
-        return sparse_corr.top_k(x_s, x_t, self.k)
+        r"""Memory-efficient top-k correspondence computation.
+
+        The GPU filter starts from this model's previous candidate lists of
+        the same shape (a persistent warm-start state): the selected indices
+        do not depend on it, only the filter's insertion work does
+        (``csrc/hip/topk.hip::topk_warm_kernel``)."""
+        return sparse_corr.top_k(x_s, x_t, self.k,
+                                 warm=self._topk_warm_state(x_s, x_t))
+
+    def _topk_warm_state(self, x_s, x_t):
+        """Persistent int64 ``[B, N_s, 32]`` candidate state of the top-k
+        filter for this shape (-1: cold); allocated outside any capture."""
+        if not (_backend.use_hip(x_s) and x_s.dim() == 3):
+            return None
+        key = (tuple(x_s.shape[:2]), x_t.size(1), str(x_s.device))
+        cache = self.__dict__.setdefault('_topk_warm',
+                                         collections.OrderedDict())
+        st = cache.get(key)
+        if st is None:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            st = cache[key] = torch.full(
+                (x_s.size(0), x_s.size(1), 32), -1, dtype=torch.long,
+                device=x_s.device)
+            while len(cache) > 2:
+                cache.popitem(last=False)
+        return st
 
     @staticmethod
     def _include_gt(S_idx, dense_rows, y):
@@ -581,14 +610,22 @@ class DGMC(torch.nn.Module):
 
         # COO row indices are a function of (N_s, k) only: built once and
         # kept (one stack kernel per forward instead of arange + copy + cat).
+        # A small LRU: variable-size batches (eager sparse training) must
+        # not keep one [N_s * k] tensor per distinct node count alive.
         key = (x_s.size(0), k, str(device))
-        row = self.__dict__.setdefault('_coo_rows', {}).get(key)
-        if row is None:
+        cache = self.__dict__.setdefault('_coo_rows',
+                                         collections.OrderedDict())
+        row = cache.get(key)
+        if row is not None:
+            cache.move_to_end(key)
+        else:
             row = torch.arange(x_s.size(0), device=device).view(-1, 1)
             row = row.expand(-1, k).reshape(-1)
             if not (device.type == 'cuda' and
                     torch.cuda.is_current_stream_capturing()):
-                self._coo_rows[key] = row   # (never a graph-pool tensor)
+                cache[key] = row            # (never a graph-pool tensor)
+                while len(cache) > COO_ROWS_CACHE:
+                    cache.popitem(last=False)
         idx = torch.stack([row, S_idx.reshape(-1)], dim=0)
         size = torch.Size([x_s.size(0), N_t])
         out = []

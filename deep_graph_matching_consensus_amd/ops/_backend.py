@@ -52,17 +52,14 @@ def _load(kind):
             _STATE[kind + '_error'] = str(e)
     _STATE[kind] = ok
     _STATE[kind + '_path'] = path
-    if ok and kind == 'hip':
-        n = int(os.environ.get('DGMC_AMD_RESERVE_CUS', '0') or 0)
-        if n:
-            torch.ops.dgmc_amd.set_cu_reserve(n)
     return ok
 
 
 def set_cu_reserve(n):
     """CUs the persistent / CU-sized HIP grids leave free (e.g. for RCCL
     channel kernels running concurrently under data parallelism); returns
-    the previous value.  Default ``DGMC_AMD_RESERVE_CUS`` (0)."""
+    the previous value (default 0; the data-parallel reducer sets it only
+    while its all-reduces are in flight, parallel/ddp.py)."""
     _load('hip')
     return int(torch.ops.dgmc_amd.set_cu_reserve(int(n)))
 

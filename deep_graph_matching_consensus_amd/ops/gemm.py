@@ -308,7 +308,8 @@ class _MixedMatmul(torch.autograd.Function):
         elif wt is not None and xc.dtype == torch.float32 and \
                 wt.is_contiguous() and nt_f32_supported([xc], wt) and \
                 (bias is None or (bias.dtype == torch.float32 and
-                                  bias.is_contiguous())):
+                                  bias.is_contiguous() and
+                                  bias.data_ptr() % 16 == 0)):
             out = nt_f32([xc], wt, bias)
         elif bias is not None:
             # Bias in the GEMM epilogue (hipBLASLt), cast once per forward.

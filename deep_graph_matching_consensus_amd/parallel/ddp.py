@@ -67,8 +67,14 @@ class GradBucketAllReducer(object):
     """
 
     def __init__(self, module, bucket_bytes=8 << 20, overlap=True,
-                 process_group=None, in_step=False):
+                 process_group=None, in_step=False, reserve_cus=0):
         self.module = module
+        # CUs the persistent HIP grids leave to RCCL's kernels - only while
+        # this step's all-reduces are in flight (from the first launch to
+        # finish(); in a captured step the grids of the kernels captured in
+        # that window are sized so).  Forward and Adam get every CU.
+        self.reserve_cus = int(reserve_cus)
+        self._reserve_prev = None
         self.group = process_group
         self.params = [p for p in module.parameters() if p.requires_grad]
         self.distributed = is_distributed()
@@ -245,6 +251,10 @@ class GradBucketAllReducer(object):
     def _launch_range(self, lo, hi):
         if self.seq_log is not None and self.seq_log:
             self.seq_log[-1].append((int(lo), int(hi)))
+        if self.reserve_cus and self._reserve_prev is None and \
+                self.flat.is_cuda:
+            from ..ops import _backend
+            self._reserve_prev = _backend.set_cu_reserve(self.reserve_cus)
         buf = self.flat[lo:hi]
         if dist.get_backend(self.group) == 'nccl':
             work = dist.all_reduce(buf, op=dist.ReduceOp.AVG,
@@ -313,6 +323,10 @@ class GradBucketAllReducer(object):
             work.wait()
             if buf is not None:
                 buf.div_(self.world)
+        if self._reserve_prev is not None:
+            from ..ops import _backend
+            _backend.set_cu_reserve(self._reserve_prev)
+            self._reserve_prev = None
         # Parameters that did not receive a gradient this step keep a
         # consistent (averaged) zero; reset counters for the next step.
         self._reset_counts()

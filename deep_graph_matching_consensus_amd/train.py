@@ -39,11 +39,12 @@ from .runtime.tuning import tuned_gemms, use_tuned_gemms
 # the step).
 IN_STEP_ALLREDUCE = os.environ.get('DGMC_AMD_IN_STEP_ALLREDUCE', '1') == '1'
 # CUs the persistent GEMM grids leave to RCCL's channel kernels under data
-# parallelism (DGMC_AMD_RESERVE_CUS overrides; single-GPU runs reserve none).
-# tools/bench_cu_reserve.py (profiles/cu_reserve_r5.json): 8 CUs held by a
-# concurrent kernel stretch psi_1's 1024 -> 256 bf16x6 forward from 400 to
-# 615 us; with the grid sized to 256 - 8 CUs it runs 405 us.
-DP_RESERVE_CUS = 16
+# parallelism, applied only while the step's all-reduces are in flight
+# (parallel/ddp.py; DGMC_AMD_RESERVE_CUS overrides; single-GPU runs reserve
+# none).  tools/bench_cu_reserve.py (profiles/cu_reserve_r5.json): 8 CUs
+# held by a concurrent kernel stretch psi_1's 1024 -> 256 bf16x6 forward
+# from 400 to 615 us; with the grid sized to 256 - 8 CUs it runs 405 us.
+DP_RESERVE_CUS = 8
 # Captured all-reduce pre-flight before the first step capture
 # (DGMC_AMD_DP_PREFLIGHT=0 skips it).
 PREFLIGHT = os.environ.get('DGMC_AMD_DP_PREFLIGHT', '1') == '1'
@@ -117,18 +118,17 @@ class PairTrainer(object):
                               'using one flat all-reduce after each '
                               'replay'.format(why))
                 in_step = False
-        self.reducer = parallel.GradBucketAllReducer(
-            model, bucket_bytes=bucket_bytes,
-            overlap=overlap and mode == 'eager', in_step=in_step)
         cuda = self.device.type == 'cuda'
-        if cuda:
-            use_tuned_gemms()     # measured GEMM solutions (runtime/tuning.py)
         self.reserved_cus = 0
         if cuda and self.world > 1:
-            from .ops import _backend
             env = os.environ.get('DGMC_AMD_RESERVE_CUS')
             self.reserved_cus = int(env) if env else DP_RESERVE_CUS
-            _backend.set_cu_reserve(self.reserved_cus)
+        self.reducer = parallel.GradBucketAllReducer(
+            model, bucket_bytes=bucket_bytes,
+            overlap=overlap and mode == 'eager', in_step=in_step,
+            reserve_cus=self.reserved_cus)
+        if cuda:
+            use_tuned_gemms()     # measured GEMM solutions (runtime/tuning.py)
         self.optimizer = torch.optim.Adam(model.parameters(), lr=lr,
                                           fused=cuda,
                                           capturable=mode == 'graph')

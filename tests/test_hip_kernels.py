@@ -380,6 +380,51 @@ def test_topk_exact_refined_equals_brute_force(case, k):
         assert int(n_over) == 0      # the margin covers random inputs
 
 
+@pytest.mark.parametrize('case', ['random', 'hub', 'clustered'])
+def test_topk_warm_start_same_output(case):
+    """The filter's warm start (a persistent candidate state re-scored into
+    per-row lower bounds of the threshold, ``topk_warm_kernel``) never
+    changes the selection: cold state, the previous call's state on the
+    same or on perturbed embeddings (training steps), the WORST targets as
+    the state (weak bounds), and garbage states (duplicates, out-of-range
+    indices) all give the brute-force exact indices."""
+    if case == 'random':
+        torch.manual_seed(1)
+        h_s = torch.randn(2, 700, 256, device=DEV)
+        h_t = torch.randn(2, 1500, 256, device=DEV)
+    elif case == 'hub':
+        h_s, h_t = _hub_case(1, 2000, 3000, 256, seed=3)
+    else:
+        g = torch.Generator().manual_seed(5)
+        cent = torch.randn(5, 64, generator=g)
+        h_t = (cent[torch.randint(0, 5, (2500, ), generator=g)] +
+               1e-6 * torch.randn(2500, 64, generator=g))[None].to(DEV)
+        h_s = torch.randn(1, 900, 64, generator=g).to(DEV)
+    B, Ns, _ = h_s.shape
+    Nt = h_t.size(1)
+    state = torch.full((B, Ns, 32), -1, dtype=torch.long, device=DEV)
+    want = sparse_corr.top_k(h_s, h_t, 10, brute_force=True)
+    assert torch.equal(sparse_corr.top_k(h_s, h_t, 10, warm=state), want)
+    assert bool((state[..., :16] >= 0).all())         # kept for next call
+    assert torch.equal(sparse_corr.top_k(h_s, h_t, 10, warm=state), want)
+    # a "training step": perturbed embeddings, previous state
+    g = torch.Generator(device=DEV).manual_seed(9)
+    h_s2 = h_s + 0.05 * torch.randn(h_s.shape, device=DEV, generator=g)
+    h_t2 = h_t + 0.05 * torch.randn(h_t.shape, device=DEV, generator=g)
+    want2 = sparse_corr.top_k(h_s2, h_t2, 10, brute_force=True)
+    assert torch.equal(sparse_corr.top_k(h_s2, h_t2, 10, warm=state), want2)
+    # weak bounds: the 16 worst targets of every row
+    worst = sparse_corr.top_k(-h_s2, h_t2, 16, brute_force=True)
+    state[..., :16] = worst
+    assert torch.equal(sparse_corr.top_k(h_s2, h_t2, 10, warm=state), want2)
+    # garbage: duplicates, negative and out-of-range indices
+    bad = torch.randint(0, 4, (B, Ns, 32), device=DEV)
+    bad[:, ::3, 5] = Nt + 7
+    bad[:, 1::3, 2] = -5
+    state.copy_(bad)
+    assert torch.equal(sparse_corr.top_k(h_s2, h_t2, 10, warm=state), want2)
+
+
 @pytest.mark.parametrize('exact', [True, False])
 def test_topk_nonfinite_rows_give_valid_indices(exact):
     """Rows (or targets) holding NaN / Inf still produce k in-range indices
