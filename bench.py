@@ -112,6 +112,8 @@ def launch_ranks(argv=None):
 WORKER_ENV = 'DGMC_AMD_BENCH_WORKER'
 ATTEMPT_ENV = 'DGMC_AMD_BENCH_ATTEMPT'
 DONE_MARK = '#dgmc-bench-done'
+# Wall budget of all attempts together: inside the driver's 600 s run limit.
+BENCH_BUDGET_S = 560.0
 DP_LADDER = [
     ('graph-captured', []),
     ('graph-flat', ['--dp-mode', 'flat']),
@@ -214,7 +216,7 @@ def supervise(argv, total_s=None):
     import datetime
     import torch.distributed as dist
     if total_s is None:
-        total_s = float(os.environ.get('DGMC_AMD_BENCH_BUDGET_S', '560'))
+        total_s = BENCH_BUDGET_S
     cap_s = float(os.environ.get('DGMC_AMD_BENCH_ATTEMPT_S', '240'))
     rank = int(os.environ['RANK'])
     world = int(os.environ['WORLD_SIZE'])

@@ -42,9 +42,7 @@ typedef float tn_f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kTnT = 128;               // tile rows / columns
-constexpr int kTnK = 16;                // k rows per staged step
-constexpr int kTnNst = 4;               // LDS ring stages
-constexpr int kTnImg = kTnK * kTnT;     // floats per operand image
+constexpr int kTnAlign = 32;            // split chunks: multiples of this
 constexpr int kTnTile = kTnT * kTnT;    // floats per partial tile
 constexpr int kTnMaxParts = 8;
 
@@ -88,23 +86,36 @@ __device__ __forceinline__ const float* tn_col(const TnParts& P, int c,
   return r;
 }
 
-// Wait until at most N of this thread's DMAs are outstanding (N: 4 per
-// younger stage in flight).
+template <int N>
+__device__ __forceinline__ void tn_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+// Wait until at most `younger` stages' DMAs (D per stage and thread) are
+// outstanding.
+template <int D>
 __device__ __forceinline__ void tn_wait_stages(int younger) {
   switch (younger) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 0: tn_vmcnt<0>(); break;
+    case 1: tn_vmcnt<D>(); break;
+    case 2: tn_vmcnt<2 * D>(); break;
+    case 3: tn_vmcnt<3 * D>(); break;
+    case 4: tn_vmcnt<4 * D>(); break;
+    default: tn_vmcnt<5 * D>(); break;
   }
 }
 
-template <bool X6>
+// KR rows per staged step, NST stages in the LDS ring (NST - 1 steps in
+// flight while one is multiplied).
+template <bool X6, int KR, int NST>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     TnParts A, TnParts B, int K, int kchunk, int tiles_n, int tiles,
     float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sA_[kTnNst * kTnImg];
-  __shared__ __attribute__((aligned(16))) float sB_[kTnNst * kTnImg];
+  static_assert(KR % 16 == 0 && NST >= 2 && NST <= 6, "tn config");
+  constexpr int IMG = KR * kTnT;              // floats per operand image
+  constexpr int DJ = KR / 8;                  // DMAs per operand, thread
+  __shared__ __attribute__((aligned(16))) float sA_[NST * IMG];
+  __shared__ __attribute__((aligned(16))) float sB_[NST * IMG];
   DGMC_LDS float* sA = (DGMC_LDS float*)sA_;
   DGMC_LDS float* sB = (DGMC_LDS float*)sB_;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -116,28 +127,29 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int k0 = split * kchunk;
   const int k1 = min(K, k0 + kchunk);
-  const int nsteps = k1 > k0 ? (k1 - k0 + kTnK - 1) / kTnK : 0;
+  const int nsteps = k1 > k0 ? (k1 - k0 + KR - 1) / KR : 0;
 
-  // Staging: wave w's DMA j covers rows 4 w + 2 j (lanes 0-31) and + 1
-  // (lanes 32-63), 16-byte chunk lane % 32 of the 128 columns.
+  // Staging: wave w's DMA j covers rows (KR / 4) w + 2 j (lanes 0-31) and
+  // + 1 (lanes 32-63), 16-byte chunk lane % 32 of the 128 columns.
   const int cc = 4 * (lane & 31);
   int lda, ldb;
   const float* acol = tn_col(A, tm * kTnT + cc, lda);
   const float* bcol = tn_col(B, tn * kTnT + cc, ldb);
-  const int rbase = 4 * wave + (lane >> 5);
+  const int wrow = (KR / 4) * wave;
+  const int rbase = wrow + (lane >> 5);
   const float* zero = g_tn_zero;
   auto stage = [&](int s) {
-    const int kb = k0 + s * kTnK;
-    DGMC_LDS float* da = sA + (s % kTnNst) * kTnImg;
-    DGMC_LDS float* db = sB + (s % kTnNst) * kTnImg;
+    const int kb = k0 + s * KR;
+    DGMC_LDS float* da = sA + (s % NST) * IMG;
+    DGMC_LDS float* db = sB + (s % NST) * IMG;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < DJ; ++j) {
       const int row = kb + rbase + 2 * j;
       const bool in = row < k1;
       tn_dma16(in && acol ? acol + (size_t)row * lda : zero,
-               da + (4 * wave + 2 * j) * kTnT);
+               da + (wrow + 2 * j) * kTnT);
       tn_dma16(in && bcol ? bcol + (size_t)row * ldb : zero,
-               db + (4 * wave + 2 * j) * kTnT);
+               db + (wrow + 2 * j) * kTnT);
     }
   };
 
@@ -152,9 +164,11 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
   const int am = wm * 64 + i, bn = wn * 64 + i;
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
     if (X6) {
+#pragma unroll
+     for (int st = 0; st < KR / 16; ++st) {
       // one 16-deep step: lane (i, h) supplies rows 8 h .. 8 h + 7
       tn_bf16x8 av[2][3], bv[2][3];
-      const int kr = 8 * h;
+      const int kr = 16 * st + 8 * h;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
 #pragma unroll
@@ -188,10 +202,11 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               av[a][0], bv[b][0], acc[a][b], 0, 0, 0);
         }
+     }
       return;
     }
 #pragma unroll
-    for (int s = 0; s < kTnK / 2; ++s) {
+    for (int s = 0; s < KR / 2; ++s) {
       const int kk = 2 * s + h;
       float av[2], bv[2];
 #pragma unroll
@@ -207,16 +222,16 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     }
   };
 
-  // kTnNst-stage ring: kTnNst - 1 steps in flight while one is multiplied;
-  // the stage refilled at step s was consumed at step s - 1 (its trailing
+  // NST-stage ring: NST - 1 steps in flight while one is multiplied; the
+  // stage refilled at step s was consumed at step s - 1 (its trailing
   // barrier orders the refill after every wave's reads).
-  const int pro = min(nsteps, kTnNst - 1);
+  const int pro = min(nsteps, NST - 1);
   for (int s = 0; s < pro; ++s) stage(s);
   for (int s = 0; s < nsteps; ++s) {
-    if (s + kTnNst - 1 < nsteps) stage(s + kTnNst - 1);
-    tn_wait_stages(min(kTnNst - 1, nsteps - 1 - s));
+    if (s + NST - 1 < nsteps) stage(s + NST - 1);
+    tn_wait_stages<2 * DJ>(min(NST - 1, nsteps - 1 - s));
     tn_barrier();
-    compute(sA + (s % kTnNst) * kTnImg, sB + (s % kTnNst) * kTnImg);
+    compute(sA + (s % NST) * IMG, sB + (s % NST) * IMG);
     tn_barrier();
   }
 
@@ -319,7 +334,7 @@ int tn_num_cus(int dev) {
 // `accumulate`).  splits <= 0: chosen to fill two workgroups per CU.
 at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
                        const c10::optional<at::Tensor>& out, bool accumulate,
-                       bool x6, int64_t splits) {
+                       bool x6, int64_t splits, int64_t cfg) {
   TORCH_CHECK(!a_parts.empty(), "gemm_tn_f32: A parts");
   const int64_t K = a_parts[0].size(0);
   int64_t M = 0, N = 0;
@@ -345,14 +360,25 @@ at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
   const int64_t cus = tn_num_cus(a_parts[0].device().index());
   if (splits <= 0)
     splits = std::max<int64_t>(1, (2 * cus + tiles - 1) / tiles);
-  // equal chunks of whole 16-row steps
-  const int64_t steps = std::max<int64_t>(1, (K + kTnK - 1) / kTnK);
+  // equal chunks of whole 32-row steps
+  const int64_t steps = std::max<int64_t>(1, (K + kTnAlign - 1) / kTnAlign);
   splits = std::min(splits, steps);
-  const int64_t kchunk = ((steps + splits - 1) / splits) * kTnK;
+  const int64_t kchunk = ((steps + splits - 1) / splits) * kTnAlign;
   splits = std::max<int64_t>(1, (K + kchunk - 1) / kchunk);
   at::Tensor part = at::empty({splits * tiles * kTnTile},
                               a_parts[0].options());
-  auto kern = x6 ? gemm_tn_kernel<true> : gemm_tn_kernel<false>;
+  // cfg (measurement hook, tools/bench_gemm_tn.py): 0 = default
+  // (32-row steps, 2 stages), 1 = 16 x 4, 2 = 32 x 3 (1 workgroup per CU).
+  using KernT = void (*)(TnParts, TnParts, int, int, int, int, float*);
+  KernT kern;
+  switch (cfg) {
+    case 1: kern = x6 ? gemm_tn_kernel<true, 16, 4>
+                      : gemm_tn_kernel<false, 16, 4>; break;
+    case 2: kern = x6 ? gemm_tn_kernel<true, 32, 3>
+                      : gemm_tn_kernel<false, 32, 3>; break;
+    default: kern = x6 ? gemm_tn_kernel<true, 32, 2>
+                       : gemm_tn_kernel<false, 32, 2>; break;
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)(splits * tiles)), dim3(256), 0,
                      stream(), A, B, (int)K, (int)kchunk, (int)tiles_n,
                      (int)tiles, part.data_ptr<float>());

@@ -32,7 +32,7 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        bool accumulate);
 at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
                        const c10::optional<at::Tensor>& out, bool accumulate,
-                       bool x6, int64_t splits);
+                       bool x6, int64_t splits, int64_t cfg);
 std::tuple<at::Tensor, at::Tensor> fold_weights_bwd(const at::Tensor& w1,
                                                     const at::Tensor& wf,
                                                     const at::Tensor& g);
@@ -295,9 +295,6 @@ at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
 at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
                       const at::Tensor& seg, const at::Tensor& bt,
                       const c10::optional<at::Tensor>& broot, bool gather);
-at::Tensor dense_weight_x3(const at::Tensor& w, int64_t Kp);
-at::Tensor dense_gemm_x6(const at::Tensor& x, const at::Tensor& b3,
-                         const c10::optional<at::Tensor>& bias);
 at::Tensor split3(const at::Tensor& x);
 at::Tensor slot_weight_x3(const at::Tensor& weight,
                           const c10::optional<at::Tensor>& root,
@@ -379,7 +376,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "False) -> Tensor");
   m.def(
       "gemm_tn_f32(Tensor[] a_parts, Tensor[] b_parts, Tensor(a!)? out=None, "
-      "bool accumulate=False, bool x6=True, int splits=0) -> Tensor");
+      "bool accumulate=False, bool x6=True, int splits=0, int cfg=0) -> "
+      "Tensor");
   m.def("fold_weights_bwd(Tensor w1, Tensor wf, Tensor g) -> (Tensor, Tensor)");
   m.def(
       "rel_proj_bwd(Tensor dpq, Tensor feat, Tensor fold, Tensor(a!) dfeat, "
@@ -572,8 +570,6 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "broot, bool gather) -> Tensor");
   m.def("slot_weight_t(Tensor weight, Tensor? root) -> Tensor");
   m.def("split3(Tensor x) -> Tensor");
-  m.def("dense_weight_x3(Tensor w, int Kp) -> Tensor");
-  m.def("dense_gemm_x6(Tensor x, Tensor b3, Tensor? bias) -> Tensor");
   m.def(
       "slot_wgrad_x6(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
       "rounds, Tensor? ell=None, Tensor? ecol=None, Tensor? evl=None) -> "
@@ -692,8 +688,6 @@ TORCH_LIBRARY_IMPL(dgmc_amd, CUDA, m) {
   m.impl("slot_dx_tiles", &dgmc::slot_dx_tiles);
   m.impl("slot_weight_t", &dgmc::slot_weight_t);
   m.impl("split3", &dgmc::split3);
-  m.impl("dense_weight_x3", &dgmc::dense_weight_x3);
-  m.impl("dense_gemm_x6", &dgmc::dense_gemm_x6);
   m.impl("slot_wgrad_x6", &dgmc::slot_wgrad_x6);
   m.impl("slot_weight_x3", &dgmc::slot_weight_x3);
   m.impl("slot_gemm_x6", &dgmc::slot_gemm_x6);

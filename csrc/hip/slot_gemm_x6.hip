@@ -1211,129 +1211,6 @@ at::Tensor slot_gemm_x6(const at::Tensor& a3, const at::Tensor& src,
   return Y;
 }
 
-// ---------------------------------------------------------------------------
-// Dense fp32 GEMM on the same kernel (one "slot", no gather):
-//   Y[M, N] = X[M, K] W[K, N] (+ bias)
-// X split into zero-padded planes [3][Mp][Kp] (Mp % 256, Kp % 128), W into
-// [3][1][N][Kp] images (built once per forward scope by the caller).  Used
-// for the fp32 node GEMMs outside the slot convs (RelConv's stacked
-// [lin1 | lin2 | root] maps, encoder projections).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void split3_pad_kernel(
-    const float* __restrict__ x, int64_t M, int K, int64_t lda, int64_t Mp,
-    int Kp, __bf16* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int vpr = Kp / 4;
-  const int64_t r = t / vpr;
-  if (r >= Mp) return;
-  const int c = (int)(t - r * vpr) * 4;
-  x6_bf16x4 h, m, l;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float f = (r < M && c + e < K) ? x[r * lda + c + e] : 0.f;
-    __bf16 he, me, le;
-    x6_split(f, he, me, le);
-    h[e] = he;
-    m[e] = me;
-    l[e] = le;
-  }
-  const int64_t plane = Mp * Kp;
-  __bf16* o = out + r * Kp + c;
-  *reinterpret_cast<x6_bf16x4*>(o) = h;
-  *reinterpret_cast<x6_bf16x4*>(o + plane) = m;
-  *reinterpret_cast<x6_bf16x4*>(o + 2 * plane) = l;
-}
-
-__global__ __launch_bounds__(256) void dense_weight_x3_kernel(
-    const float* __restrict__ w, int64_t ldk, int64_t ldn, int K, int N,
-    int Kp, __bf16* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)N * Kp) return;
-  const int n = (int)(t / Kp), k = (int)(t - (int64_t)n * Kp);
-  const float f = k < K ? w[k * ldk + n * ldn] : 0.f;
-  __bf16 h, m, l;
-  x6_split(f, h, m, l);
-  const int64_t plane = (int64_t)N * Kp;
-  out[t] = h;
-  out[t + plane] = m;
-  out[t + 2 * plane] = l;
-}
-
-__global__ void dense_seg_kernel(int* seg, int Mp) {
-  if (threadIdx.x == 0) {
-    seg[0] = 0;
-    seg[1] = Mp;
-  }
-}
-
-at::Tensor dense_weight_x3(const at::Tensor& w, int64_t Kp) {
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 2,
-              "dense_weight_x3: fp32 W [K, N]");
-  const int64_t K = w.size(0), N = w.size(1);
-  TORCH_CHECK(Kp >= K && Kp % 128 == 0 && N % kX6BN == 0,
-              "dense_weight_x3: Kp >= K, Kp % 128, N % 128");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(w.device());
-  at::Tensor out = at::empty({3, 1, N, Kp}, w.options().dtype(at::kBFloat16));
-  const int64_t n = N * Kp;
-  hipLaunchKernelGGL(dense_weight_x3_kernel, dim3((unsigned)((n + 255) / 256)),
-                     dim3(256), 0, stream(), w.data_ptr<float>(), w.stride(0),
-                     w.stride(1), (int)K, (int)N, (int)Kp,
-                     reinterpret_cast<__bf16*>(out.data_ptr()));
-  DGMC_CHECK_LAUNCH();
-  return out;
-}
-
-at::Tensor dense_gemm_x6(const at::Tensor& x, const at::Tensor& b3,
-                         const c10::optional<at::Tensor>& bias) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 2 &&
-                  x.stride(1) == 1,
-              "dense_gemm_x6: fp32 X [M, K] with unit column stride");
-  TORCH_CHECK(b3.scalar_type() == at::kBFloat16 && b3.is_contiguous() &&
-                  b3.dim() == 4 && b3.size(0) == 3 && b3.size(1) == 1,
-              "dense_gemm_x6: B planes [3, 1, N, Kp]");
-  const int64_t M = x.size(0), K = x.size(1);
-  const int64_t N = b3.size(2), Kp = b3.size(3);
-  TORCH_CHECK(Kp >= K && Kp % 128 == 0 && N % kX6BN == 0,
-              "dense_gemm_x6: Kp >= K, Kp % 128, N % 128");
-  const float* bp = nullptr;
-  if (bias.has_value() && bias->defined()) {
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() &&
-                    bias->numel() == N && aligned16(bias->data_ptr()),
-                "dense_gemm_x6: fp32 bias [N]");
-    bp = bias->data_ptr<float>();
-  }
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int64_t Mp = (M + kXBM - 1) / kXBM * kXBM;
-  at::Tensor Y = at::empty({M, N}, x.options());     // rows >= M not stored
-  if (M == 0) return Y;
-  at::Tensor a3 = at::empty({3, Mp, Kp}, x.options().dtype(at::kBFloat16));
-  const int64_t n = Mp * (Kp / 4);
-  hipLaunchKernelGGL(split3_pad_kernel, dim3((unsigned)((n + 255) / 256)),
-                     dim3(256), 0, stream(), x.data_ptr<float>(), M, (int)K,
-                     x.stride(0), Mp, (int)Kp,
-                     reinterpret_cast<__bf16*>(a3.data_ptr()));
-  DGMC_CHECK_LAUNCH();
-  at::Tensor seg = at::empty({2}, x.options().dtype(at::kInt));
-  hipLaunchKernelGGL(dense_seg_kernel, dim3(1), dim3(64), 0, stream(),
-                     seg.data_ptr<int>(), (int)Mp);
-  DGMC_CHECK_LAUNCH();
-  const int64_t tiles_max = (Mp / kXBM) * (N / kX6BN);
-  const int64_t blocks = std::min<int64_t>(
-      tiles_max, (int64_t)x6_num_cus(x.device().index()));
-  auto kern = slot_gemm_x6_kernel<false, false>;
-  DGMC_CHECK_HIP(hipFuncSetAttribute(
-      reinterpret_cast<const void*>(kern),
-      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kXLds));
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kXThreads), kXLds, stream(),
-                     reinterpret_cast<const __bf16*>(a3.data_ptr()), Mp * Kp,
-                     nullptr, seg.data_ptr<int>(), 1,
-                     reinterpret_cast<const __bf16*>(b3.data_ptr()), N * Kp,
-                     (int)Kp, (int)N, nullptr, (int)(Mp / kXBM),
-                     Y.data_ptr<float>(), bp, (int)M, x6_debug());
-  DGMC_CHECK_LAUNCH();
-  return Y;
-}
-
 std::vector<at::Tensor> slot_wgrad_items(const at::Tensor& seg, int64_t nu,
                                          int64_t target, int64_t qcap,
                                          int64_t G_cap, int64_t rows);

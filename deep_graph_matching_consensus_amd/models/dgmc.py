@@ -26,7 +26,6 @@ What differs is the execution plan (MI355X-first):
 """
 import collections
 import contextlib
-import os
 
 import torch
 from torch.nn import Linear, ReLU, Sequential
@@ -45,11 +44,11 @@ from ..runtime.profiling import mark, trace_range
 from ..runtime.mode import is_reference_mode
 from .encoder import CatParts, StackedEncoder
 
-# DGMC_AMD_FOLD_PROJECTION=0 keeps psi_2's final Linear as its own GEMM.
-FOLD_PROJECTION = os.environ.get('DGMC_AMD_FOLD_PROJECTION', '1') == '1'
-# DGMC_AMD_SINKHORN_FUSED=0 runs the Sinkhorn consensus loop unfused
+# FOLD_PROJECTION = False keeps psi_2's final Linear as its own GEMM (tests).
+FOLD_PROJECTION = True
+# SINKHORN_FUSED = False runs the Sinkhorn consensus loop unfused
 # (separate normalisation kernel + batched-GEMM transport).
-SINKHORN_FUSED = os.environ.get('DGMC_AMD_SINKHORN_FUSED', '1') == '1'
+SINKHORN_FUSED = True
 
 EPS = 1e-8
 # Cached sparse-output COO row index tensors (one per (N_s, k, device)).

@@ -22,7 +22,6 @@ per pair entry.  The reference materialises ``D [B, N_s, N_t, R]`` (25 MiB
 per step for PascalVOC shapes); the backward recomputes the ReLU from
 ``P``/``Q``.  Masks come from per-pair node counts.
 """
-import os
 
 import torch
 
@@ -34,8 +33,8 @@ from ..runtime import loopgrad
 # Largest padded graph the per-pair HIP kernels handle (LDS-resident tiles).
 MAX_PAIR_NODES = 64
 # Consensus update of step l fused with the softmax transport of step l + 1
-# (one per-pair kernel each way); DGMC_AMD_FUSE_STEPS=0 keeps them apart.
-FUSE_STEPS = os.environ.get('DGMC_AMD_FUSE_STEPS', '1') == '1'
+# (one per-pair kernel each way); FUSE_STEPS = False keeps them apart (tests).
+FUSE_STEPS = True
 
 
 def _hip_ok(x, N_s, N_t):
@@ -663,7 +662,7 @@ def _seg01(M, device):
 # The folded projection's NT products on bf16x6 (fp32 parts split in the
 # kernel's registers; error vs fp64 below the exact-f32 MFMA kernel's:
 # tests/test_slot_gemm_x6.py) or on the exact-f32 MFMA kernel.
-NT_X6 = os.environ.get('DGMC_AMD_X6_NT', '1') == '1'
+NT_X6 = True
 
 
 def _nt_x6():

@@ -24,43 +24,6 @@ from . import _backend
 from ..runtime import loopgrad
 from ..runtime.cache import cached
 
-# fp32 node GEMMs (RelConv's stacked maps, encoder projections) as bf16x6 on
-# the matrix cores (csrc/hip/slot_gemm_x6.hip::dense_gemm_x6: three bf16
-# terms per operand, six products, two fp32 accumulators - error below the
-# exact fp32 MFMA chain).  Opt-in (DGMC_AMD_X6_DENSE=1): measured slower
-# than hipBLASLt fp32 on these shapes - DBP15K refinement step 6.75 ->
-# 6.99 ms (the [39k, 256] x [256, 768] maps: 142 us + 32 us operand split
-# vs ~140 us), PascalVOC neutral.
-X6_DENSE = os.environ.get('DGMC_AMD_X6_DENSE', '0') == '1'
-X6_DENSE_MIN_ROWS = 4096
-
-
-def dense_x6_supported(x, w):
-    """``x [M, K] @ w [K, N]`` in fp32 on the bf16x6 dense kernel."""
-    return (X6_DENSE and _backend.use_hip(x) and x.dtype == torch.float32
-            and w.dtype == torch.float32 and x.dim() == 2 and w.dim() == 2
-            and x.stride(1) == 1 and x.size(0) >= X6_DENSE_MIN_ROWS and
-            x.size(1) >= 64 and w.size(1) % 128 == 0)
-
-
-def dense_x6(x, w, bias=None):
-    """``x @ w (+ bias)`` (fp32 in, fp32 out) via bf16x6; the weight's bf16
-    planes are built once per forward scope."""
-    ops = _backend.ops()
-    K = w.size(0)
-    Kp = (K + 127) // 128 * 128
-    wd = w.detach()
-    w3 = cached(('dense_w3', wd.data_ptr(), wd._version, tuple(wd.shape),
-                 tuple(wd.stride()), Kp),
-                lambda: ops.dense_weight_x3(wd, Kp))
-    b = None
-    if bias is not None:
-        b = bias.detach()
-        if b.dtype != torch.float32 or not b.is_contiguous():
-            b = b.float().contiguous()
-    return ops.dense_gemm_x6(x, w3, b)
-
-
 def _rows16(t):
     return (t.dim() == 2 and t.dtype == torch.float32 and t.stride(1) == 1
             and t.size(1) % 4 == 0 and t.stride(0) % 4 == 0 and
@@ -124,12 +87,14 @@ def tn_f32_supported(a_parts, b_parts):
     return all(_tn_part_ok(t, K) for t in list(a_parts) + list(b_parts))
 
 
-def tn_f32(a_parts, b_parts, out=None, accumulate=False, x6=None):
+def tn_f32(a_parts, b_parts, out=None, accumulate=False, x6=None, cfg=0):
     """``[a_parts]^T [b_parts]`` (fp32 ``[M, N]``; written, or added into
-    ``out``).  bf16x6 products unless ``x6=False`` / ``DGMC_AMD_X6=0``."""
+    ``out``).  bf16x6 products unless ``x6=False`` / ``DGMC_AMD_X6=0``.
+    ``cfg``: kernel staging variant (measurement hook; 0 = default)."""
     return _backend.ops().gemm_tn_f32(list(a_parts), list(b_parts), out,
                                       bool(accumulate),
-                                      NT_X6 if x6 is None else bool(x6), 0)
+                                      NT_X6 if x6 is None else bool(x6), 0,
+                                      int(cfg))
 
 
 class _LinearParts(torch.autograd.Function):
@@ -303,9 +268,7 @@ class _MixedMatmul(torch.autograd.Function):
         # chunked NT kernel reads the weight in place (GIN / MLP / encoder
         # Linears, /root/reference/dgmc/models/gin.py:49, mlp.py:35)
         wt = w_lp.t() if w_lp.dim() == 2 else None
-        if dense_x6_supported(xc, w_lp):
-            out = dense_x6(xc, w_lp, bias)
-        elif wt is not None and xc.dtype == torch.float32 and \
+        if wt is not None and xc.dtype == torch.float32 and \
                 wt.is_contiguous() and nt_f32_supported([xc], wt) and \
                 (bias is None or (bias.dtype == torch.float32 and
                                   bias.is_contiguous() and

@@ -33,7 +33,7 @@ from .gemm import col_partial_rows, loop_col_total
 BM = 128                      # compact tile unit (slot_gemm.hip)
 SEG = 256                     # slot segment alignment (256-row x6 tiles)
 MAX_USES = 16                 # pointer table of slot_wgrad_f32
-ENABLED = os.environ.get('DGMC_AMD_SLOT_GEMM', '1') == '1'
+ENABLED = True                # (tests compare against the GEMM + SpMM path)
 # fp32 products on the bf16 matrix cores ("bf16x6", csrc/hip/slot_gemm_x6.hip):
 # every operand split into three bf16 terms, six products, two fp32
 # accumulators - max error vs fp64 BELOW the exact-f32 MFMA kernels on every
@@ -46,32 +46,25 @@ X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
 # waiting for the last launch.  Without a reducer one launch is cheaper
 # (+0.03 ms per PascalVOC step for the extra fold); PIECES_ALWAYS=1 pieces
 # regardless (tests compare a one-rank RCCL run bit-for-bit with that).
-PIECES = int(os.environ.get('DGMC_AMD_WGRAD_PIECES', '2'))
+PIECES = 2
 PIECES_ALWAYS = os.environ.get('DGMC_AMD_WGRAD_PIECES_ALWAYS', '0') == '1'
 PIECE_BYTES = 8 << 20
 # bf16x6 backward on fp32 dY_c (split inside the dX / dW kernels' LDS
 # staging) instead of the rowmap SpMM writing three bf16 planes.
-F32DY = os.environ.get('DGMC_AMD_X6_F32DY', '1') == '1'
+F32DY = True
 # Rowmap SpMM entries from a per-step inline (col, val) table.
-ROWMAP_ELL = os.environ.get('DGMC_AMD_ROWMAP_ELL', '1') == '1'
+ROWMAP_ELL = True
 # bf16x6 forward on fp32 X (gathered rows split in the GEMM's staging) for
 # in <= F32X_KMAX (tools/bench_slot_gemm_x6.py with the 32 x 128 wave tiles
 # of the fp32-A kernel: 128->128 42.9 -> 38.0 us, 256->256 115 -> 113,
 # 1024->256 351 -> 346 vs bf16 planes; the earlier 64 x 64 tiles were slower
 # than planes beyond K = 128).
-F32X = os.environ.get('DGMC_AMD_X6_F32X', '1') == '1'
-F32X_KMAX = int(os.environ.get('DGMC_AMD_X6_F32X_KMAX', '4096'))
-# ... and the weight gradient reads fp32 X rows too (with F32DY: no operand
-# planes of X at all - no split pass, no plane output of the producing SpMM).
-# Off: measured slower (PascalVOC 5.57 -> 5.66 ms: both operands' column
-# reads + splits cost more than the 1/3 of X traffic they save).
-F32X_WGRAD = os.environ.get('DGMC_AMD_X6_F32X_WGRAD', '0') == '1'
-
-
-def _x_planes_free():
-    """No bf16 planes of X are needed anywhere (forward and weight
-    gradient both read fp32 X)."""
-    return F32X and F32DY and F32X_WGRAD
+F32X = True
+F32X_KMAX = 4096
+# (The weight gradient keeps reading bf16 planes of X: an fp32-X weight
+# gradient measured slower - PascalVOC 5.57 -> 5.66 ms, both operands'
+# column reads + splits cost more than the 1/3 of X traffic they save - and
+# was removed in round 6.)
 
 
 class CompactPlan(object):
@@ -166,10 +159,10 @@ def _x6_rounds(tiles):
     return 2 if tiles <= 4 else X6_WGRAD_ROUNDS_BIG
 
 
-X6_WGRAD_ROUNDS_BIG = int(os.environ.get('DGMC_AMD_X6_WGRAD_ROUNDS', '6'))
+X6_WGRAD_ROUNDS_BIG = 6
 # (single-tile shapes, psi_2's 10-use gradient: 1 / 2 / 3 rounds measured
 # 5.637 / 5.658 / 5.68 ms per PascalVOC step)
-X6_WGRAD_ROUNDS_ONE = int(os.environ.get('DGMC_AMD_X6_WGRAD_ROUNDS_ONE', '1'))
+X6_WGRAD_ROUNDS_ONE = 1
 
 
 def weight_grad_x6(x3s, dy3s, plan, cin, cout):
@@ -221,18 +214,17 @@ class _SlotGemmSpMM(torch.autograd.Function):
             planes = pl[0] if (pl is not None and pl[1] == x._version and
                                tuple(pl[0].shape) == (3, ) + tuple(x.shape)) \
                 else None
-            if F32X and (x.size(1) <= F32X_KMAX or _x_planes_free()):
+            if F32X and x.size(1) <= F32X_KMAX:
                 if xc.data_ptr() % 16 != 0:
                     xc = xc.clone()          # (16-byte row DMA)
                 # The GEMM gathers fp32 X rows and splits them in its LDS
-                # staging (4 instead of 6 bytes per gathered element); with
-                # the fp32-X weight gradient no X planes are formed at all.
+                # staging (4 instead of 6 bytes per gathered element); the
+                # weight gradient reads X's planes.
                 Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True, None)
-                if not _x_planes_free():
-                    if planes is None and (ctx.needs_input_grad[1] or (
-                            root is not None and ctx.needs_input_grad[2])):
-                        planes = ops.split3(xc)
-                    xc = planes
+                if planes is None and (ctx.needs_input_grad[1] or (
+                        root is not None and ctx.needs_input_grad[2])):
+                    planes = ops.split3(xc)
+                xc = planes
             else:
                 xc = planes if planes is not None else ops.split3(xc)
                 Y = ops.slot_gemm_x6(xc, plan.src, plan.seg, wt3, True,
@@ -244,7 +236,7 @@ class _SlotGemmSpMM(torch.autograd.Function):
                 weight.detach().contiguous(),
                 root.detach().contiguous() if root is not None else None))
             Y = ops.slot_gemm2(xc, plan.src, plan.seg, wt, None, True)
-        if X6 and planes_out and not _x_planes_free():
+        if X6 and planes_out:
             # The consumer is another bf16x6 slot conv: the SpMM also
             # writes its operand planes (no split pass there).
             out, planes = ops.spmm_csr_planes(op.rowptr, plan.col_c, op.val,

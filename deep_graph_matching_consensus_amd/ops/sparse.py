@@ -18,7 +18,6 @@ atomics anywhere (the reference's torch_scatter / spline_weighting backward
 use atomicAdd).  Plans are built once per batch and reused by every layer and
 every consensus step.
 """
-import os
 
 import torch
 
@@ -313,12 +312,10 @@ class _GemmSpMM(torch.autograd.Function):
                 xc.contiguous(), *slot_tile_plan(op, S), S, img, False, bias,
                 relu, xc.dtype, None)
         else:
-            from .gemm import (dense_x6, dense_x6_supported, nt_f32,
-                               nt_f32_supported)
-            if dense_x6_supported(xc, w_lp):
-                y = dense_x6(xc, w_lp).view(-1, C)      # fp32 as bf16x6
-            elif nt_f32_supported([xc], w_lp.t()):
-                # exact-f32 MFMA GEMM, x read in place (csrc/hip/gemm_f32.hip)
+            from .gemm import nt_f32, nt_f32_supported
+            if nt_f32_supported([xc], w_lp.t()):
+                # chunked NT MFMA GEMM (bf16x6 unless DGMC_AMD_X6=0), x read
+                # in place (csrc/hip/gemm_f32.hip)
                 y = nt_f32([xc], w_lp.t()).view(-1, C)
             else:
                 y = (xc @ w_lp).view(-1, C)
@@ -574,8 +571,8 @@ def _add_pass(gx, gpass):
 # backward: the transposed slot conv (ReLU mask, g', bias partials and dx in
 # one kernel) + the slot weight gradient from the kept (x, g') pairs of every
 # use (csrc/hip/slot_wgrad.hip; no dY stack).  Measured on MI355X:
-# docs/performance.md.  DGMC_AMD_SLOT_CONV=0 selects GEMM + SpMM.
-SLOT_CONV = os.environ.get('DGMC_AMD_SLOT_CONV', '1') != '0'
+# docs/performance.md.  SLOT_CONV = False selects GEMM + SpMM (tests).
+SLOT_CONV = True
 _SLOT_C = 128
 _SLOT_MAX_S = 62    # one wave lane per slot offset (csrc/hip/slot_conv.hip)
 _SLOT_ERR = {}

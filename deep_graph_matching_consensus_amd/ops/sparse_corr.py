@@ -11,8 +11,8 @@
   a proven error margin of the k-th is re-scored with the exact fp32 chain,
   and rows whose margin is not covered are recomputed exhaustively
   (``csrc/hip/topk.hip::topk_refine_kernel``) - indices identical to the
-  brute-force exact-f32 MFMA kernel.  ``DGMC_AMD_TOPK_EXACT=0`` (or
-  ``exact=False``) returns the unrefined split-bf16 selection.
+  brute-force exact-f32 MFMA kernel.  ``exact=False`` returns the unrefined
+  split-bf16 selection.
 * :class:`CandidateGraph`  - the candidate set ``S_idx [B, N_s, k]`` as a CSR
   matrix over flattened source rows (global target columns ``b*N_t + idx``)
   plus its transpose, built once per forward.
@@ -28,7 +28,6 @@
 The reference quirks are kept: no masking of padded targets or rows in the
 sparse path (``dgmc.py:202,223``).
 """
-import os
 
 import torch
 import torch.nn.functional as F
@@ -40,14 +39,14 @@ from ..runtime import loopgrad
 from .sparse import SparseOperator, piece_plan
 
 
-TOPK_EXACT = os.environ.get('DGMC_AMD_TOPK_EXACT', '1') == '1'
+TOPK_EXACT = True
 
 
 def top_k(h_s, h_t, k, exact=None, brute_force=False, warm=None):
     """``[B, N_s, k]`` int64 indices of the k best targets per source row
     (best first, ties to the lower index).
 
-    ``exact`` (default ``DGMC_AMD_TOPK_EXACT``, on): exact fp32 selection
+    ``exact`` (default :data:`TOPK_EXACT`, on): exact fp32 selection
     (filter + exact re-score on the GPU); ``exact=False``: split-bf16
     scores (~2^-16 relative error - near-ties can rank differently).
     ``brute_force``: the exact-f32 MFMA kernel over every target (the test

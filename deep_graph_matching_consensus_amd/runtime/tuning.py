@@ -38,7 +38,7 @@ def use_tuned_gemms(path=None):
         return False
     if not torch.cuda.is_available():
         return False
-    path = path or os.environ.get('DGMC_AMD_TUNED_FILE') or TUNED_FILE
+    path = path or TUNED_FILE
     if not osp.exists(path):
         return False
     if _STATE.get('path') == path:

@@ -120,7 +120,8 @@ class PairTrainer(object):
                 in_step = False
         cuda = self.device.type == 'cuda'
         self.reserved_cus = 0
-        if cuda and self.world > 1:
+        if self.world > 1:
+            # (recorded on any device; only HIP grids are resized)
             env = os.environ.get('DGMC_AMD_RESERVE_CUS')
             self.reserved_cus = int(env) if env else DP_RESERVE_CUS
         self.reducer = parallel.GradBucketAllReducer(

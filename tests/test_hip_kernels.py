@@ -1657,7 +1657,7 @@ def test_fold_weights_kernel():
 _SWITCHES = [None, ('slot_gemm', 'ENABLED', False),
              ('slot_gemm', 'X6', False), ('slot_gemm', 'F32DY', False),
              ('slot_gemm', 'F32X', False), ('slot_gemm', 'ROWMAP_ELL', False),
-             ('slot_gemm', 'F32X_WGRAD', True), ('dense', 'NT_X6', False),
+             ('dense', 'NT_X6', False),
              ('dense', 'FUSE_STEPS', False)]
 
 

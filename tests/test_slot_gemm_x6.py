@@ -238,7 +238,6 @@ def test_x6_f32dy_training_step_matches_planes(monkeypatch):
     for flag in (False, True):
         monkeypatch.setattr(sg, 'F32DY', flag)
         monkeypatch.setattr(sg, 'F32X', flag)
-        monkeypatch.setattr(sg, 'F32X_WGRAD', flag)
         conv.zero_grad()
         x.grad = None
         conv(x, ei, ea).square().sum().backward()
@@ -374,11 +373,10 @@ def test_rowmap_entry_table_equals_ranges(headline_plan):
 
 
 def test_spmm_planes_feed_next_conv(monkeypatch):
-    """Plane path (``F32X_WGRAD=0``): a non-last fp32 SplineConv's
+    """Plane path: a non-last fp32 SplineConv's
     aggregation also writes the bf16x6 planes of its output (== split3 of
     it, bitwise); the next conv consumes them instead of splitting, with an
     identical result."""
-    monkeypatch.setattr(sg, 'F32X_WGRAD', False)
     from deep_graph_matching_consensus_amd.datasets import (
         GraphStore, DevicePairLoader, make_keypoint_datasets)
     from deep_graph_matching_consensus_amd.nn.conv import SplineConv
@@ -401,57 +399,6 @@ def test_spmm_planes_feed_next_conv(monkeypatch):
     with torch.no_grad():
         h.add_(0)             # an in-place write bumps the version: stale
     assert h._dgmc_x6[1] != h._version
-
-
-@pytest.mark.parametrize('M,K,N,bias', [(39000, 256, 768, False),
-                                        (19388, 300, 768, False),
-                                        (39000, 1068, 256, True),
-                                        (10944, 256, 256, True)])
-def test_dense_x6_error_not_above_fp32(M, K, N, bias, monkeypatch):
-    """The dense bf16x6 GEMM (RelConv stacked maps, encoder projections;
-    K padded to 128, rows to 256) against fp64: error <= torch's fp32 GEMM
-    on the same inputs (strided weight view as the callers pass it)."""
-    from deep_graph_matching_consensus_amd.ops import gemm
-    monkeypatch.setattr(gemm, 'X6_DENSE', True)
-    g = torch.Generator(device=DEV).manual_seed(M + K)
-    x = torch.randn(M, K, device=DEV, generator=g)
-    wt = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
-    w = wt.t()                                   # [K, N] view, as linear()
-    b = torch.randn(N, device=DEV, generator=g) if bias else None
-    assert gemm.dense_x6_supported(x, w)
-    y6 = gemm.dense_x6(x, w, b)
-    ref = x.double() @ w.double()
-    y32 = x @ w
-    if bias:
-        ref = ref + b.double()
-        y32 = y32 + b
-    assert y6.shape == (M, N) and y6.is_contiguous()
-    e6 = float((y6.double() - ref).abs().max())
-    e32 = float((y32.double() - ref).abs().max())
-    assert e6 <= e32, (e6, e32)
-
-
-def test_dense_x6_linear_gradients_flow(monkeypatch):
-    """``ops.gemm.linear`` on the dense bf16x6 forward: the output is a
-    plain tensor of the op, and the input, weight and bias gradients reach
-    their leaves (equal to the fp32 expressions)."""
-    from deep_graph_matching_consensus_amd.ops import gemm
-    monkeypatch.setattr(gemm, 'X6_DENSE', True)
-    g = torch.Generator(device=DEV).manual_seed(5)
-    x = torch.randn(8192, 256, device=DEV, generator=g, requires_grad=True)
-    lin = torch.nn.Linear(256, 256).to(DEV)
-    assert gemm.dense_x6_supported(x.detach(), lin.weight.t())
-    y = gemm.linear(x, lin.weight, lin.bias)
-    assert y.grad_fn is not None and not y._is_view()
-    go = torch.randn(y.shape, device=DEV, generator=g)
-    y.backward(go)
-    torch.testing.assert_close(y, x @ lin.weight.t() + lin.bias, atol=1e-4,
-                               rtol=1e-5)
-    torch.testing.assert_close(x.grad, go @ lin.weight, atol=1e-3, rtol=1e-4)
-    torch.testing.assert_close(lin.weight.grad, go.t() @ x.detach(),
-                               atol=1e-2, rtol=1e-4)
-    torch.testing.assert_close(lin.bias.grad, go.sum(0), atol=1e-2,
-                               rtol=1e-4)
 
 
 @pytest.mark.parametrize('M,parts,Nn', [(10944, 3, 128), (10944, 1, 384),

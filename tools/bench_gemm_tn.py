@@ -41,10 +41,15 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument('--reps', type=int, default=50)
     p.add_argument('--json', default=None)
+    p.add_argument('--cfgs', type=int, nargs='+', default=[0, 1, 2])
+    p.add_argument('--only', default=None, help='one shape name')
+    p.add_argument('--no-torch', action='store_true')
     args = p.parse_args()
     dev = torch.device('cuda')
     out = {}
     for name, K, wa, wb in SHAPES:
+        if args.only and name != args.only:
+            continue
         g = torch.Generator(device=dev).manual_seed(0)
         a = [torch.randn(K, w, device=dev, generator=g) for w in wa]
         b = [torch.randn(K, w, device=dev, generator=g) for w in wb]
@@ -53,10 +58,16 @@ def main():
         flop = 2.0 * K * M * N
         row = {'K': K, 'M': M, 'N': N}
         for x6 in (True, False):
-            us = timeit(lambda: gemm.tn_f32(a, b, x6=x6), args.reps)
-            row['tn_x6' if x6 else 'tn_f32'] = round(us, 1)
-        row['torch_fp32_us'] = round(timeit(lambda: A.t() @ B, args.reps), 1)
-        if gemm._dense_tn_f32_ok(A, B):
+            for cfg in args.cfgs:
+                us = timeit(lambda: gemm.tn_f32(a, b, x6=x6, cfg=cfg),
+                            args.reps)
+                row['tn_{}_cfg{}'.format('x6' if x6 else 'f32', cfg)] = \
+                    round(us, 1)
+        row['tn_x6'] = row['tn_x6_cfg0']
+        if not args.no_torch:
+            row['torch_fp32_us'] = round(timeit(lambda: A.t() @ B,
+                                                args.reps), 1)
+        if gemm._dense_tn_f32_ok(A, B) and not args.no_torch:
             from deep_graph_matching_consensus_amd.ops.dense import _seg01
             seg = _seg01(K, dev)
             row['dense_wgrad_f32_us'] = round(timeit(
