@@ -215,25 +215,28 @@ def matmul_tn_fp32(a, b, out=None, accumulate=False):
     elif not a.is_cuda:
         res = a.float().t() @ b.float()
     else:
+        # (low-precision inputs accumulate into fp32; fp32 / fp64 - the
+        # reference-mode oracle - stay in their own dtype)
+        low = a.dtype in (torch.bfloat16, torch.float16)
         s = _split_factor(M, N, K)
         if s == 1:
-            res = torch.mm(a.t(), b, out_dtype=torch.float32) \
-                if a.dtype != torch.float32 else a.t() @ b
+            res = torch.mm(a.t(), b, out_dtype=torch.float32) if low \
+                else a.t() @ b
         else:
             k = K // s
             main = k * s
             a3 = a[:main].view(s, k, M).transpose(1, 2)
             b3 = b[:main].view(s, k, N)
-            if a.dtype == torch.float32:
+            if not low:
                 part = torch.bmm(a3, b3)
             else:
                 part = torch.bmm(a3, b3, out_dtype=torch.float32)
             if main < K:   # fold the remainder rows into the first split
                 tail = torch.mm(a[main:].t(), b[main:],
-                                out_dtype=torch.float32) \
-                    if a.dtype != torch.float32 else a[main:].t() @ b[main:]
+                                out_dtype=torch.float32) if low \
+                    else a[main:].t() @ b[main:]
                 part[0].add_(tail)
-            if _backend.hip_available():
+            if _backend.hip_available() and part.dtype == torch.float32:
                 if out is None:
                     out = torch.empty((M, N), dtype=torch.float32,
                                       device=a.device)

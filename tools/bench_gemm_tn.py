@@ -63,7 +63,7 @@ def main():
                             args.reps)
                 row['tn_{}_cfg{}'.format('x6' if x6 else 'f32', cfg)] = \
                     round(us, 1)
-        row['tn_x6'] = row['tn_x6_cfg0']
+        row['tn_x6'] = row['tn_x6_cfg{}'.format(args.cfgs[0])]
         if not args.no_torch:
             row['torch_fp32_us'] = round(timeit(lambda: A.t() @ B,
                                                 args.reps), 1)
