@@ -177,6 +177,20 @@ inline int usable_cus(int total) {
   const int r = cu_reserve();
   return total - r >= 1 ? total - r : 1;
 }
+// The device's CU count, reserve ignored.  Work DECOMPOSITIONS that fix a
+// summation order (split-K chunks, weight-gradient items) are sized from
+// this, so results never depend on the reserve; only persistent grid sizes
+// use usable_cus().
+inline int device_cus(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    hipDeviceProp_t prop;
+    DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
+    cached[dev] = prop.multiProcessorCount;
+  }
+  return cached[dev];
+}
 
 // Diagnostic knobs (kernel ablations, relaxed top-k margins, forced split
 // counts) exist only in the diagnostic library (`tools/build_native.py

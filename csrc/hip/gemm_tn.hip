@@ -317,16 +317,6 @@ TnParts tn_parts(at::TensorList parts, int64_t K, const char* what,
   return P;
 }
 
-int tn_num_cus(int dev) {
-  static int cached[64] = {0};
-  if (dev < 0 || dev >= 64) dev = 0;
-  if (cached[dev] == 0) {
-    hipDeviceProp_t prop;
-    DGMC_CHECK_HIP(hipGetDeviceProperties(&prop, dev));
-    cached[dev] = prop.multiProcessorCount;
-  }
-  return usable_cus(cached[dev]);
-}
 
 }  // namespace
 
@@ -357,7 +347,9 @@ at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
   if (M == 0 || N == 0) return C;
   const int64_t tiles_n = (N + kTnT - 1) / kTnT;
   const int64_t tiles = ((M + kTnT - 1) / kTnT) * tiles_n;
-  const int64_t cus = tn_num_cus(a_parts[0].device().index());
+  // (the split count fixes the summation order: sized from the physical
+  // CU count, never the DP reserve)
+  const int64_t cus = device_cus(a_parts[0].device().index());
   if (splits <= 0)
     splits = std::max<int64_t>(1, (2 * cus + tiles - 1) / tiles);
   // equal chunks of whole 32-row steps

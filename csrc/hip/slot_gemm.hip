@@ -1825,7 +1825,7 @@ at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
   // capped so an item's rows fit the LDS index buffer.
   const int64_t tiles = (Kin / kSgBM) * (C / kSgBN);
   const int64_t target = std::max<int64_t>(
-      1, rounds * 2 * (int64_t)num_cus(src.device().index()) / tiles);
+      1, rounds * 2 * (int64_t)device_cus(src.device().index()) / tiles);
   const int64_t qcap = (kW2MaxRows / kW2Rows - 2) * nu;
   const int64_t G_cap = target + (P / kW2Rows * nu + qcap - 1) / qcap + S;
   auto i32 = src.options();
@@ -1894,7 +1894,7 @@ at::Tensor dense_wgrad_f32(at::TensorList xparts, int64_t nparts,
   // One round of resident workgroups: the outputs are small (<= 512 x 512)
   // and every item writes a full partial tile set for the fold.
   const int64_t target = std::max<int64_t>(
-      2, 2 * (int64_t)num_cus(seg01.device().index()) / tiles);
+      2, 2 * (int64_t)device_cus(seg01.device().index()) / tiles);
   const int64_t qcap = (kW2MaxRows / kW2Rows - 2) * nu;
   const int64_t G_cap = target + (M / kW2Rows * nu + qcap - 1) / qcap + 1;
   auto i32 = seg01.options();

@@ -1282,7 +1282,7 @@ at::Tensor slot_wgrad_x6(at::TensorList xs, at::TensorList gs,
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   const int64_t tiles = (Kin / 128) * (C / 128);
   const int64_t target = std::max<int64_t>(
-      1, rounds * 2 * (int64_t)x6_num_cus(src.device().index()) / tiles);
+      1, rounds * 2 * (int64_t)device_cus(src.device().index()) / tiles);
   const int64_t qcap = (kWXMaxRows / kWXRows - 2) * nu;
   const int64_t G_cap = target + (P / kWXRows * nu + qcap - 1) / qcap + S;
   auto it = slot_wgrad_items(seg, nu, target, qcap, G_cap, kWXRows);
