@@ -347,51 +347,37 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) hit |= col_ok && acc[r] > thr[r];
     const bool any = __ballot(hit) != 0ull;
-    // One insertion per half-wave and call: candidate = the lowest pending
-    // lane of the half's mask; an empty mask (or a candidate no longer
-    // above the updated threshold) changes nothing.
-    auto insert_one = [&](int r, float v, unsigned& lo, unsigned& hi) {
-      const int slo = lo ? __builtin_ctz(lo) : 0;
-      const int shi = hi ? __builtin_ctz(hi) : 0;
-      const bool has = hb ? hi != 0u : lo != 0u;
-      lo &= lo - 1u;
-      hi &= hi - 1u;
-      const float cv0 = lane_f(v, slo), cv1 = lane_f(v, 32 + shi);
-      const float cv = hb ? cv1 : cv0;
-      const int src = hb ? shi : slo;
-      const bool mine = has && hl < k && cv > thr[r];
-      const unsigned long long bm = __ballot(mine && lv[r] >= cv);
-      const int pos =
-          hb ? __popc((unsigned)(bm >> 32)) : __popc((unsigned)bm);
-      // shift the tail of the half's list down one lane (DPP wave_shr:1;
-      // lane hl > pos >= 0 always reads a lane of its own half)
-      const float pv = shr1(lv[r]);
-      const int pi = shr1(li[r]);
-      if (mine && hl > pos) { lv[r] = pv; li[r] = pi; }
-      if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + src; }
-      const float t_lo_half = lane_f(lv[r], k - 1);
-      const float t_hi_half = lane_f(lv[r], 32 + k - 1);
-      thr[r] = hb ? t_hi_half : t_lo_half;
-    };
-    // Two rows (accumulator registers r, r + 1) at a time: their insertion
-    // chains are independent, so each round issues both straight-line (a
-    // pair member without pending candidates runs as a no-op) and the
-    // chains' cross-lane latencies overlap.  Same insertions in the same
-    // order per row as one row at a time.
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
+    for (int r = 0; r < 16; ++r) {
       if (!any) break;
-      const float v0 = col_ok ? acc[r] : -INFINITY;
-      const float v1 = col_ok ? acc[r + 1] : -INFINITY;
-      const unsigned long long m0 = __ballot(v0 > thr[r]);
-      const unsigned long long m1 = __ballot(v1 > thr[r + 1]);
+      const float v = col_ok ? acc[r] : -INFINITY;
+      const unsigned long long mask = __ballot(v > thr[r]);
       // One candidate of each half-wave per round (the halves hold
       // different rows): max(hits_lo, hits_hi) rounds, not their sum.
-      unsigned lo0 = (unsigned)m0, hi0 = (unsigned)(m0 >> 32);
-      unsigned lo1 = (unsigned)m1, hi1 = (unsigned)(m1 >> 32);
-      while (lo0 | hi0 | lo1 | hi1) {
-        insert_one(r, v0, lo0, hi0);
-        insert_one(r + 1, v1, lo1, hi1);
+      // (Interleaving two rows' rounds measured slower: 1.27 -> 1.39 ms.)
+      unsigned lo = (unsigned)mask, hi = (unsigned)(mask >> 32);
+      while (lo | hi) {
+        const int slo = lo ? __builtin_ctz(lo) : 0;
+        const int shi = hi ? __builtin_ctz(hi) : 0;
+        const bool has = hb ? hi != 0u : lo != 0u;
+        lo &= lo - 1u;
+        hi &= hi - 1u;
+        const float cv0 = lane_f(v, slo), cv1 = lane_f(v, 32 + shi);
+        const float cv = hb ? cv1 : cv0;
+        const int src = hb ? shi : slo;
+        const bool mine = has && hl < k && cv > thr[r];
+        const unsigned long long bm = __ballot(mine && lv[r] >= cv);
+        const int pos =
+            hb ? __popc((unsigned)(bm >> 32)) : __popc((unsigned)bm);
+        // shift the tail of the half's list down one lane (DPP wave_shr:1;
+        // lane hl > pos >= 0 always reads a lane of its own half)
+        const float pv = shr1(lv[r]);
+        const int pi = shr1(li[r]);
+        if (mine && hl > pos) { lv[r] = pv; li[r] = pi; }
+        if (mine && hl == pos) { lv[r] = cv; li[r] = j0 + src; }
+        const float t_lo_half = lane_f(lv[r], k - 1);
+        const float t_hi_half = lane_f(lv[r], 32 + k - 1);
+        thr[r] = hb ? t_hi_half : t_lo_half;
       }
     }
     __syncthreads();

@@ -49,6 +49,10 @@ def test_gemm_tn_vs_fp64(K, wa, wb, x6):
         ye = gemm.tn_f32(a, b, x6=False)
         ee = float((ye.double() - ref).abs().max())
         assert e <= 1.5 * ee + 1e-6, (e, ee)
+        # every staging variant: the same products per element, in the same
+        # k order - bit-identical results
+        for cfg in (1, 2, 3):
+            assert torch.equal(gemm.tn_f32(a, b, x6=True, cfg=cfg), y), cfg
 
 
 def test_gemm_tn_accumulate_into_strided_out_and_determinism():
