@@ -88,7 +88,7 @@ __device__ __forceinline__ void gf_split8(const gf_f32x4 u0, const gf_f32x4 u1,
 // step into a large- and a small-term accumulator; max error below the
 // exact-f32 chain's, tests/test_gemm_f32.py) - 2.7x fewer matrix-core
 // cycles than v_mfma_f32_32x32x2_f32.
-template <int MB, int NB, bool X6 = false>
+template <int MB, int NB, bool X6 = false, bool SCHED = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
     GfSteps A, int M, const float* __restrict__ bt, int ldb, int Nn,
     const float* __restrict__ bias, int relu, float* __restrict__ Y,
@@ -158,7 +158,67 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_f32_kernel(
     for (int b = 0; b < MB; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
+  // SCHED (bf16x6): each fragment is split right before its first MFMA
+  // and overlaps the previous block's MFMAs (regions fenced by
+  // sched_barrier): w0 x0 | MFMA(0,0) + the next fragment | ... | the last
+  // block's MFMAs + the next 16-deep step's w0 x0.
+  auto wsplit = [&](const DGMC_LDS float* lb, int st, int a,
+                    gf_bf16x8 (&v)[3]) {
+    const int c0 = 4 * st + 2 * h;
+    gf_split8(*reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                  lb + offN + a * 32 * kGfBK + 4 * (c0 ^ sw)),
+              *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                  lb + offN + a * 32 * kGfBK + 4 * ((c0 + 1) ^ sw)),
+              v);
+  };
+  auto xsplit = [&](const DGMC_LDS float* la, int st, int b,
+                    gf_bf16x8 (&v)[3]) {
+    const int c0 = 4 * st + 2 * h;
+    gf_split8(*reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                  la + offM + b * 32 * kGfBK + 4 * (c0 ^ sw)),
+              *reinterpret_cast<const DGMC_LDS gf_f32x4*>(
+                  la + offM + b * 32 * kGfBK + 4 * ((c0 + 1) ^ sw)),
+              v);
+  };
+  auto mfma6 = [&](int a, int b, const gf_bf16x8 (&w)[3],
+                   const gf_bf16x8 (&x)[3]) {
+    gf_f32x16 sm = acs[a][b];
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], sm, 0, 0, 0);
+    acs[a][b] = sm;
+    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0],
+                                                        acc[a][b], 0, 0, 0);
+  };
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+    if (X6 && SCHED) {
+      gf_bf16x8 w[NB][3], x[MB][3];
+      wsplit(lb, 0, 0, w[0]);
+      xsplit(la, 0, 0, x[0]);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int a = 0; a < NB; ++a)
+#pragma unroll
+          for (int b = 0; b < MB; ++b) {
+            __builtin_amdgcn_sched_barrier(0);
+            mfma6(a, b, w[a], x[b]);
+            // the next fragment in consumption order
+            if (a == 0 && b + 1 < MB) {
+              xsplit(la, st, b + 1, x[b + 1]);
+            } else if (b == MB - 1 && a + 1 < NB) {
+              wsplit(lb, st, a + 1, w[a + 1]);
+            } else if (a == NB - 1 && b == MB - 1 && st == 0) {
+              wsplit(lb, 1, 0, w[0]);
+              xsplit(la, 1, 0, x[0]);
+            }
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if (X6) {
       // 16-deep step st: lane (i, h) supplies k = 16 st + 8 h .. + 7, the
       // logical chunks 4 st + 2 h and + 1 of its row image
@@ -345,7 +405,7 @@ int gf_num_cus(int dev) {
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
                        const c10::optional<at::Tensor>& out, bool x6,
-                       bool accumulate) {
+                       bool accumulate, int64_t sched) {
   TORCH_CHECK(parts.size() >= 1, "gemm_nt_f32: at least one part");
   const int64_t M = parts[0].size(0);
   GfSteps A{};
@@ -424,9 +484,14 @@ at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
   }
   TORCH_CHECK(pick >= 0, "gemm_nt_f32: no tile shape for Nn = ", Nn);
   const int64_t blocks = std::min<int64_t>(tiles, 2 * (int64_t)cus);
-  auto kern = x6 ? (pick == 0 ? gemm_nt_f32_kernel<2, 2, true>
-                              : pick == 1 ? gemm_nt_f32_kernel<2, 1, true>
-                                          : gemm_nt_f32_kernel<1, 1, true>)
+  // sched (measurement hook): bf16x6 with the fragment splits scheduled
+  // against the previous block's MFMAs.
+  auto kern = x6 ? (sched ? (pick == 0 ? gemm_nt_f32_kernel<2, 2, true, true>
+                             : pick == 1 ? gemm_nt_f32_kernel<2, 1, true, true>
+                                         : gemm_nt_f32_kernel<1, 1, true, true>)
+                          : (pick == 0 ? gemm_nt_f32_kernel<2, 2, true>
+                             : pick == 1 ? gemm_nt_f32_kernel<2, 1, true>
+                                         : gemm_nt_f32_kernel<1, 1, true>))
                  : (pick == 0 ? gemm_nt_f32_kernel<2, 2>
                               : pick == 1 ? gemm_nt_f32_kernel<2, 1>
                                           : gemm_nt_f32_kernel<1, 1>);

@@ -65,8 +65,14 @@ __device__ __forceinline__ void tn_dma16(const float* g, DGMC_LDS float* l) {
       :: "v"(g), "s"(m0) : "memory", "m0");
 }
 
+// Barrier that also drains this wave's LDS operations: the MFMAs that
+// consume a fragment may be scheduled after the barrier (they touch no
+// memory), and with them the wait for the fragment's ds_read - which could
+// then still be in flight when another wave overwrites the image after the
+// barrier (observed as rare result differences of the cooperative-split
+// kernel, whose plane images are rewritten right after it).
 __device__ __forceinline__ void tn_barrier() {
-  asm volatile("" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -107,7 +113,7 @@ __device__ __forceinline__ void tn_wait_stages(int younger) {
 
 // KR rows per staged step, NST stages in the LDS ring (NST - 1 steps in
 // flight while one is multiplied).
-template <bool X6, int KR, int NST>
+template <bool X6, int KR, int NST, bool SCHED = false>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
     TnParts A, TnParts B, int K, int kchunk, int tiles_n, int tiles,
     float* __restrict__ part) {
@@ -162,7 +168,58 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
   const int am = wm * 64 + i, bn = wn * 64 + i;
+  // SCHED: the splits of each 32 x 32 block's fragments are placed right
+  // before their first MFMA and overlap the previous block's MFMAs
+  // (scheduling regions fenced by sched_barrier): a0 b0 | MFMA(0,0) + b1 |
+  // MFMA(0,1) + a1 | MFMA(1,0) MFMA(1,1) + the next 16 rows' a0 b0 | ...
+  auto ld_split = [&](const DGMC_LDS float* img, int kr, int col,
+                      tn_bf16x8 (&v)[3]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __bf16 hh, mm, ll;
+      split3_bf16(img[(kr + j) * kTnT + col], hh, mm, ll);
+      v[0][j] = hh;
+      v[1][j] = mm;
+      v[2][j] = ll;
+    }
+  };
+  auto mfma6 = [&](int a, int b, const tn_bf16x8 (&av)[3],
+                   const tn_bf16x8 (&bv)[3]) {
+    tn_f32x16 sm = acs[a][b];
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], sm, 0, 0, 0);
+    sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], sm, 0, 0, 0);
+    acs[a][b] = sm;
+    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0],
+                                                        acc[a][b], 0, 0, 0);
+  };
   auto compute = [&](const DGMC_LDS float* la, const DGMC_LDS float* lb) {
+    if (X6 && SCHED) {
+      tn_bf16x8 a0[3], a1[3], b0[3], b1[3];
+      ld_split(la, 8 * h, am, a0);
+      ld_split(lb, 8 * h, bn, b0);
+#pragma unroll
+      for (int st = 0; st < KR / 16; ++st) {
+        const int kr = 16 * st + 8 * h;
+        __builtin_amdgcn_sched_barrier(0);
+        mfma6(0, 0, a0, b0);
+        ld_split(lb, kr, bn + 32, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma6(0, 1, a0, b1);
+        ld_split(la, kr, am + 32, a1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma6(1, 0, a1, b0);
+        mfma6(1, 1, a1, b1);
+        if (st + 1 < KR / 16) {
+          ld_split(la, kr + 16, am, a0);
+          ld_split(lb, kr + 16, bn, b0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     if (X6) {
 #pragma unroll
      for (int st = 0; st < KR / 16; ++st) {
@@ -257,168 +314,6 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(
         *reinterpret_cast<float4*>(out + (((a * 2 + b) * 4 + q) * 64 + lane) *
                                              4) = v;
       }
-}
-
-// ---------------------------------------------------------------------------
-// bf16x6 with a COOPERATIVE split (cfg 3): every staged fp32 element is split
-// into its three bf16 terms ONCE per workgroup (each of the 256 threads
-// splits one column's 8 rows of A and of B per 16-row step) into bf16 plane
-// images [plane][column][16 k] (32 B per column, the two 16-byte halves
-// XOR-swizzled, tc_swz), read as MFMA
-// fragments by one ds_read_b128 per plane.  In the per-wave split above
-// every element is split by the two waves that use it and each fragment
-// needs eight ds_read_b32; here the split VALU work per MFMA halves.
-// Per step: wait for the step's DMA, barrier, refill the ring, split,
-// barrier, MFMAs.  fp32 ring of kTcNst stages (48 KB) + single plane
-// buffer (24 KB): two workgroups per CU.
-// ---------------------------------------------------------------------------
-constexpr int kTcKR = 16;                    // rows per step
-constexpr int kTcNst = 3;                    // fp32 ring stages
-constexpr int kTcImg = kTcKR * kTnT;         // floats per operand image
-constexpr int kTcPlane = kTnT * kTcKR;       // bf16 per plane image
-
-// Half swizzle of column c's 32-byte plane record: bit 2 ^ bit 4 of c.
-// Conflict-free both for the split's ds_write_b128 (8 consecutive columns
-// per lane group: bit 2 alternates) and for the fragment ds_read_b128
-// (lane groups {0-3, 12-15, 20-27} / {4-11, 16-19, 28-31}: the 16 records'
-// 16-byte halves land on 16 distinct 4-bank groups).
-__device__ __forceinline__ int tc_swz(int c) { return ((c >> 2) ^ (c >> 4)) & 1; }
-
-__global__ __launch_bounds__(256, 2) void gemm_tn_x6c_kernel(
-    TnParts A, TnParts B, int K, int kchunk, int tiles_n, int tiles,
-    float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sA_[kTcNst * kTcImg];
-  __shared__ __attribute__((aligned(16))) float sB_[kTcNst * kTcImg];
-  __shared__ __attribute__((aligned(16))) __bf16 pA_[3 * kTcPlane];
-  __shared__ __attribute__((aligned(16))) __bf16 pB_[3 * kTcPlane];
-  DGMC_LDS float* sA = (DGMC_LDS float*)sA_;
-  DGMC_LDS float* sB = (DGMC_LDS float*)sB_;
-  DGMC_LDS __bf16* pA = (DGMC_LDS __bf16*)pA_;
-  DGMC_LDS __bf16* pB = (DGMC_LDS __bf16*)pB_;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wg / tiles, tile = wg - split * tiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int k0 = split * kchunk;
-  const int k1 = min(K, k0 + kchunk);
-  const int nsteps = k1 > k0 ? (k1 - k0 + kTcKR - 1) / kTcKR : 0;
-
-  // DMA staging as gemm_tn_kernel<.., 16, ..>: wave w's DMA j covers rows
-  // 4 w + 2 j (+ 1 for lanes 32-63), 16-byte chunk lane % 32.
-  const int cc = 4 * (lane & 31);
-  int lda, ldb;
-  const float* acol = tn_col(A, tm * kTnT + cc, lda);
-  const float* bcol = tn_col(B, tn * kTnT + cc, ldb);
-  const int wrow = 4 * wave;
-  const int rbase = wrow + (lane >> 5);
-  const float* zero = g_tn_zero;
-  auto stage = [&](int s) {
-    const int kb = k0 + s * kTcKR;
-    DGMC_LDS float* da = sA + (s % kTcNst) * kTcImg;
-    DGMC_LDS float* db = sB + (s % kTcNst) * kTcImg;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = kb + rbase + 2 * j;
-      const bool in = row < k1;
-      tn_dma16(in && acol ? acol + (size_t)row * lda : zero,
-               da + (wrow + 2 * j) * kTnT);
-      tn_dma16(in && bcol ? bcol + (size_t)row * ldb : zero,
-               db + (wrow + 2 * j) * kTnT);
-    }
-  };
-  // Split role: column sc, rows 8 sh .. 8 sh + 7 of both images.
-  const int sc = tid & 127, sh = tid >> 7;
-  const int swz_w = 16 * (sh ^ tc_swz(sc));               // bytes
-  auto split_step = [&](int s) {
-    const DGMC_LDS float* la = sA + (s % kTcNst) * kTcImg;
-    const DGMC_LDS float* lb = sB + (s % kTcNst) * kTcImg;
-    tn_bf16x8 va[3], vb[3];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      __bf16 hh, mm, ll;
-      split3_bf16(la[(8 * sh + j) * kTnT + sc], hh, mm, ll);
-      va[0][j] = hh; va[1][j] = mm; va[2][j] = ll;
-      split3_bf16(lb[(8 * sh + j) * kTnT + sc], hh, mm, ll);
-      vb[0][j] = hh; vb[1][j] = mm; vb[2][j] = ll;
-    }
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      *reinterpret_cast<DGMC_LDS tn_bf16x8*>(
-          reinterpret_cast<DGMC_LDS char*>(pA + p * kTcPlane) + sc * 32 +
-          swz_w) = va[p];
-      *reinterpret_cast<DGMC_LDS tn_bf16x8*>(
-          reinterpret_cast<DGMC_LDS char*>(pB + p * kTcPlane) + sc * 32 +
-          swz_w) = vb[p];
-    }
-  };
-
-  const int i = lane & 31, h = lane >> 5;
-  tn_f32x16 acc[2][2], acs[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = acs[a][b][r] = 0.f;
-  auto frag = [&](const DGMC_LDS __bf16* plane, int c) {
-    const int off = c * 32 + 16 * (h ^ tc_swz(c));
-    return *reinterpret_cast<const DGMC_LDS tn_bf16x8*>(
-        reinterpret_cast<const DGMC_LDS char*>(plane) + off);
-  };
-  auto compute = [&]() {
-    tn_bf16x8 av[2][3], bv[2][3];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        av[a][p] = frag(pA + p * kTcPlane, wm * 64 + 32 * a + i);
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        bv[b][p] = frag(pB + p * kTcPlane, wn * 64 + 32 * b + i);
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        tn_f32x16 sm = acs[a][b];
-        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][2], bv[b][0], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][2], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][1], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][1], bv[b][0], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[a][0], bv[b][1], sm, 0, 0, 0);
-        acs[a][b] = sm;
-        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            av[a][0], bv[b][0], acc[a][b], 0, 0, 0);
-      }
-  };
-
-  const int pro = min(nsteps, kTcNst - 1);
-  for (int s = 0; s < pro; ++s) stage(s);
-  for (int s = 0; s < nsteps; ++s) {
-    // (stages issued after s: at most kTcNst - 2, 4 DMAs each)
-    tn_wait_stages<4>(min(kTcNst - 2, nsteps - 1 - s));
-    tn_barrier();     // step s landed; every wave done with the planes
-    if (s + kTcNst - 1 < nsteps) stage(s + kTcNst - 1);   // slot of s - 1
-    split_step(s);
-    tn_barrier();
-    compute();
-  }
-
-  float* out = part + ((size_t)split * tiles + tile) * kTnTile + wave * 4096;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<float4*>(out + (((a * 2 + b) * 4 + q) * 64 + lane) *
-                                             4) =
-            make_float4(acc[a][b][4 * q] + acs[a][b][4 * q],
-                        acc[a][b][4 * q + 1] + acs[a][b][4 * q + 1],
-                        acc[a][b][4 * q + 2] + acs[a][b][4 * q + 2],
-                        acc[a][b][4 * q + 3] + acs[a][b][4 * q + 3]);
 }
 
 // C[m, n] (+)= sum over splits (in order) of the partial tiles.
@@ -521,8 +416,12 @@ at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
   splits = std::max<int64_t>(1, (K + kchunk - 1) / kchunk);
   at::Tensor part = at::empty({splits * tiles * kTnTile},
                               a_parts[0].options());
-  // cfg (measurement hook, tools/bench_gemm_tn.py): 0 = default
-  // (32-row steps, 2 stages), 1 = 16 x 4, 2 = 32 x 3 (1 workgroup per CU).
+  // cfg (measurement hook, tools/bench_gemm_tn.py; profiles/
+  // bench_gemm_tn_r6_*.json): 0 = default (32-row steps, 2 stages, bf16x6
+  // splits scheduled against the previous block's MFMAs), 1 = 16 x 4,
+  // 2 = 32 x 3 (one workgroup per CU), 4 = 32 x 2 unscheduled.  (A
+  // cooperative split - each element split once per workgroup into LDS
+  // bf16 planes - measured no faster: LDS waits replaced the split VALU.)
   using KernT = void (*)(TnParts, TnParts, int, int, int, int, float*);
   KernT kern;
   switch (cfg) {
@@ -530,9 +429,9 @@ at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
                       : gemm_tn_kernel<false, 16, 4>; break;
     case 2: kern = x6 ? gemm_tn_kernel<true, 32, 3>
                       : gemm_tn_kernel<false, 32, 3>; break;
-    case 3: kern = x6 ? gemm_tn_x6c_kernel : gemm_tn_kernel<false, 32, 2>;
-      break;
-    default: kern = x6 ? gemm_tn_kernel<true, 32, 2>
+    case 4: kern = x6 ? gemm_tn_kernel<true, 32, 2>
+                      : gemm_tn_kernel<false, 32, 2>; break;
+    default: kern = x6 ? gemm_tn_kernel<true, 32, 2, true>
                        : gemm_tn_kernel<false, 32, 2>; break;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)(splits * tiles)), dim3(256), 0,

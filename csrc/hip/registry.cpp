@@ -29,7 +29,7 @@ void rel_fold(at::TensorList parts, at::TensorList outs);
 at::Tensor gemm_nt_f32(at::TensorList parts, const at::Tensor& bt,
                        const c10::optional<at::Tensor>& bias, bool relu,
                        const c10::optional<at::Tensor>& out, bool x6,
-                       bool accumulate);
+                       bool accumulate, int64_t sched);
 at::Tensor gemm_tn_f32(at::TensorList a_parts, at::TensorList b_parts,
                        const c10::optional<at::Tensor>& out, bool accumulate,
                        bool x6, int64_t splits, int64_t cfg);
@@ -373,7 +373,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "gemm_nt_f32(Tensor[] parts, Tensor bt, Tensor? bias=None, bool "
       "relu=False, Tensor(a!)? out=None, bool x6=False, bool accumulate="
-      "False) -> Tensor");
+      "False, int sched=0) -> Tensor");
   m.def(
       "gemm_tn_f32(Tensor[] a_parts, Tensor[] b_parts, Tensor(a!)? out=None, "
       "bool accumulate=False, bool x6=True, int splits=0, int cfg=0) -> "

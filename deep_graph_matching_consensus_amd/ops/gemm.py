@@ -52,10 +52,14 @@ def nt_f32_supported(parts, bt):
 # below the exact-f32 MFMA chain's, tests/test_gemm_f32.py) - the same
 # switch as ops/slot_gemm.py::X6 (DGMC_AMD_X6=0: exact-f32 kernels).
 NT_X6 = os.environ.get('DGMC_AMD_X6', '1') == '1'
+# bf16x6 NT kernel with the fragment splits scheduled against the previous
+# block's MFMAs (csrc/hip/gemm_f32.hip, SCHED; tools/bench_gemm_nt.py: 2-10 %
+# faster on the DBP15K psi_1 shapes, bit-identical).
+NT_SCHED = 1
 
 
 def nt_f32(parts, bt, bias=None, relu=False, out=None, x6=None,
-           accumulate=False):
+           accumulate=False, sched=None):
     """``act([parts] @ bt^T + bias)`` (fp32, no autograd; parts read in
     place, never concatenated).  ``x6``: bf16x6 products (default
     :data:`NT_X6`) or the exact-f32 chain.  ``accumulate``: add the product
@@ -67,7 +71,9 @@ def nt_f32(parts, bt, bias=None, relu=False, out=None, x6=None,
             b = b.contiguous()
     return _backend.ops().gemm_nt_f32(list(parts), bt, b, relu, out,
                                       NT_X6 if x6 is None else bool(x6),
-                                      bool(accumulate))
+                                      bool(accumulate),
+                                      NT_SCHED if sched is None else
+                                      int(sched))
 
 
 def _tn_part_ok(t, K):

@@ -51,6 +51,9 @@ def test_gemm_nt_f32_vs_fp64(M, widths, Nn, bias, relu, x6):
         ye = gemm.nt_f32(parts, wt, b, relu, x6=False)
         ee = float((ye.double() - ref).abs().max())
         assert e <= ee, (e, ee)
+        # the scheduled-split variant: same products, same order
+        assert torch.equal(gemm.nt_f32(parts, wt, b, relu, x6=True, sched=1),
+                           y)
 
 
 def test_gemm_nt_f32_out_view_and_linear_parts():

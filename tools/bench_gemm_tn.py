@@ -41,7 +41,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument('--reps', type=int, default=50)
     p.add_argument('--json', default=None)
-    p.add_argument('--cfgs', type=int, nargs='+', default=[0, 1, 2])
+    p.add_argument('--cfgs', type=int, nargs='+', default=[0, 4])
     p.add_argument('--only', default=None, help='one shape name')
     p.add_argument('--no-torch', action='store_true')
     args = p.parse_args()

@@ -74,12 +74,15 @@ def write_ninja(debug=False, diag=False):
         '  command = g++ {} -MD -MF $out.d -c $in -o $out'.format(host_flags),
         '  depfile = $out.d', '  deps = gcc',
         '  description = CXX $in',
+        # (linked to a temporary name and renamed: a snapshot of the tree
+        # taken during a build never sees a half-written library)
         'rule link_hip',
         '  command = {} -shared -fPIC --offload-arch={} -fno-gpu-rdc $in -o '
-        '$out {}'.format(hipcc, ARCH, libs_hip),
+        '$out.tmp {} && mv -f $out.tmp $out'.format(hipcc, ARCH, libs_hip),
         '  description = LINK $out',
         'rule link_host',
-        '  command = g++ -shared -fPIC $in -o $out {}'.format(libs_host),
+        '  command = g++ -shared -fPIC $in -o $out.tmp {} && mv -f $out.tmp '
+        '$out'.format(libs_host),
         '  description = LINK $out',
     ]
     targets = []
