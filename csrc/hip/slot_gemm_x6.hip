@@ -154,6 +154,50 @@ __global__ __launch_bounds__(256) void weight_x3_kernel(
   *reinterpret_cast<x6_bf16x4*>(o + 2 * plane) = l;
 }
 
+// TRANS images through a 64 x 64 LDS tile: W_s rows read as whole 256-byte
+// segments (the per-element kernel above reads 4 floats 4 rows apart per
+// thread - one 4-byte access per 1-KB row for psi_1's 1024 x 256 slots).
+// grid (in / 64, out / 64, S); 256 threads.
+__global__ __launch_bounds__(256) void weight_x3_t_kernel(
+    const float* __restrict__ weight, const float* __restrict__ root, int nw,
+    int in, int out, __bf16* __restrict__ img, int64_t plane) {
+  __shared__ float tile[64][65];
+  const int s = blockIdx.z;
+  if (s == nw && root == nullptr) return;
+  const float* w = s < nw ? weight + (size_t)s * in * out : root;
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, t = threadIdx.x;
+  const int r = t >> 4, c4 = 4 * (t & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kk = r + 16 * i;
+    const float4 v = *reinterpret_cast<const float4*>(
+        w + (size_t)(k0 + kk) * out + n0 + c4);
+    tile[kk][c4] = v.x;
+    tile[kk][c4 + 1] = v.y;
+    tile[kk][c4 + 2] = v.z;
+    tile[kk][c4 + 3] = v.w;
+  }
+  __syncthreads();
+  // image row n = n0 + t / 4, 16 consecutive k = k0 + 16 (t % 4) ..
+  const int n = t >> 2, kq = 16 * (t & 3);
+  __bf16* o = img + ((size_t)s * out + n0 + n) * in + k0 + kq;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    x6_bf16x4 hv, mv, lv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      __bf16 he, me, le;
+      x6_split(tile[kq + 4 * g + e][n], he, me, le);
+      hv[e] = he;
+      mv[e] = me;
+      lv[e] = le;
+    }
+    *reinterpret_cast<x6_bf16x4*>(o + 4 * g) = hv;
+    *reinterpret_cast<x6_bf16x4*>(o + 4 * g + plane) = mv;
+    *reinterpret_cast<x6_bf16x4*>(o + 4 * g + 2 * plane) = lv;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // The GEMM.  A planes [3][*][K] (plane stride a_plane), B planes
 // [3][S][Nn][K] (plane stride b_plane).  tiles (optional): 256-row tile list
@@ -1132,6 +1176,17 @@ at::Tensor slot_weight_x3(const at::Tensor& weight,
   const int64_t n = S * Nn * (K / 4);
   if (n == 0) return img;
   const float* rp = has_root ? root->data_ptr<float>() : nullptr;
+  if (transpose && in % 64 == 0 && out % 64 == 0) {
+    hipLaunchKernelGGL(weight_x3_t_kernel,
+                       dim3((unsigned)(in / 64), (unsigned)(out / 64),
+                            (unsigned)S),
+                       dim3(256), 0, stream(), weight.data_ptr<float>(), rp,
+                       (int)nw, (int)in, (int)out,
+                       reinterpret_cast<__bf16*>(img.data_ptr()),
+                       S * Nn * K);
+    DGMC_CHECK_LAUNCH();
+    return img;
+  }
   auto kern = transpose ? weight_x3_kernel<true> : weight_x3_kernel<false>;
   hipLaunchKernelGGL(kern, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      stream(), weight.data_ptr<float>(), rp, (int)nw, (int)in,

@@ -401,6 +401,25 @@ def test_spmm_planes_feed_next_conv(monkeypatch):
     assert h._dgmc_x6[1] != h._version
 
 
+@pytest.mark.parametrize('cin,cout', [(1024, 256), (256, 256), (128, 128),
+                                       (300, 68)])
+def test_slot_weight_x3_images_equal_split3(cin, cout):
+    """Weight images of the slot GEMMs (forward: transposed, through the
+    64 x 64 LDS tile kernel where in / out allow it; dX: as stored) are
+    exactly the three-term split of the (transposed) fp32 weights."""
+    ops = _backend.ops()
+    g = torch.Generator(device=DEV).manual_seed(cin + cout)
+    w = torch.randn(25, cin, cout, device=DEV, generator=g)
+    r = torch.randn(cin, cout, device=DEV, generator=g)
+    full = torch.cat([w, r[None]], 0)                   # [S, in, out]
+    img_t = ops.slot_weight_x3(w, r, True)
+    ref_t = ops.split3(full.transpose(1, 2).contiguous().view(-1, cin))
+    assert torch.equal(img_t, ref_t.view(3, 26, cout, cin))
+    img = ops.slot_weight_x3(w, r, False)
+    ref = ops.split3(full.contiguous().view(-1, cout))
+    assert torch.equal(img, ref.view(3, 26, cin, cout))
+
+
 @pytest.mark.parametrize('M,parts,Nn', [(10944, 3, 128), (10944, 1, 384),
                                         (1000, 2, 64), (33, 4, 128)])
 def test_dense_nt_x6_error_not_above_exact_f32(M, parts, Nn):
