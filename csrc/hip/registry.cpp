@@ -289,7 +289,7 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
                      const at::Tensor& seg, const at::Tensor& weight,
                      const c10::optional<at::Tensor>& root, bool trans_w,
                      const c10::optional<at::Tensor>& tiles);
-at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
+at::Tensor slot_dx_tiles(const at::Tensor& src, const at::Tensor& seg,
                          int64_t N, int64_t row0, int64_t P_cap,
                          int64_t unit);
 at::Tensor slot_gemm2(const at::Tensor& X, const at::Tensor& src,
@@ -327,7 +327,9 @@ at::Tensor slot_rowmap_ranges(const at::Tensor& rowptr,
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t N, int64_t S,
                            const c10::optional<at::Tensor>& add,
-                           int64_t row0);
+                           int64_t row0,
+                           const c10::optional<at::Tensor>& relu_out,
+                           const c10::optional<at::Tensor>& part);
 at::Tensor slot_wgrad_f32(at::TensorList xs, at::TensorList gs,
                           const at::Tensor& src, const at::Tensor& seg,
                           int64_t rounds);
@@ -563,7 +565,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "slot_gemm(Tensor X, Tensor src, Tensor seg, Tensor weight, Tensor? "
       "root, bool trans_w, Tensor? tiles=None) -> Tensor");
   m.def(
-      "slot_dx_tiles(Tensor posmap, Tensor seg, int N, int row0, int P_cap, "
+      "slot_dx_tiles(Tensor src, Tensor seg, int N, int row0, int P_cap, "
       "int unit=128) -> Tensor");
   m.def(
       "slot_gemm2(Tensor X, Tensor src, Tensor seg, Tensor bt, Tensor? "
@@ -592,7 +594,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
         "-> Tensor");
   m.def(
       "slot_gather_sum(Tensor posmap, Tensor Z, int N, int S, Tensor? add, "
-      "int row0=0) -> Tensor");
+      "int row0=0, Tensor? relu_out=None, Tensor(a!)? part=None) -> Tensor");
   m.def(
       "slot_wgrad_f32(Tensor[] xs, Tensor[] gs, Tensor src, Tensor seg, int "
       "rounds) -> Tensor");

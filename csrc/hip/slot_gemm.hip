@@ -180,22 +180,36 @@ __global__ __launch_bounds__(1024) void sg_scan_kernel(
   if (tid == 0) cnt[k] = base;
 }
 
-// posmap / src / cinv over the column space, col_c over the entries, seg.
+// posmap / src / cinv over the column space, col_c over the entries, seg;
+// src / cinv of the compact rows no source fills (segment padding, rows past
+// the last segment) are set to -1 here as well (no separate fill launches).
 __global__ __launch_bounds__(256) void sg_fill_kernel(
     const int* __restrict__ rank, const int* __restrict__ cnt, int Nsrc,
     int S, const int* __restrict__ rowptr, int R, const int* __restrict__ col,
-    int cap, int* __restrict__ posmap, int* __restrict__ src,
+    int cap, int P_cap, int* __restrict__ posmap, int* __restrict__ src,
     int* __restrict__ cinv, int* __restrict__ col_c, int* __restrict__ seg) {
-  __shared__ int sseg[kSgMaxS + 1];
+  __shared__ int sseg[kSgMaxS + 1], scnt[kSgMaxS];
   if (threadIdx.x == 0) {
     int run = 0;
     for (int k = 0; k < S; ++k) {
       sseg[k] = run;
+      scnt[k] = cnt[k];
       run += (cnt[k] + kSgSeg - 1) / kSgSeg * kSgSeg;
     }
     sseg[S] = run;
   }
   __syncthreads();
+  {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p < P_cap) {
+      int k = 0;
+      while (k < S && sseg[k + 1] <= p) ++k;
+      if (k == S || p >= sseg[k] + scnt[k]) {
+        src[p] = -1;
+        cinv[p] = -1;
+      }
+    }
+  }
   if (blockIdx.x == 0)
     for (int k = threadIdx.x; k <= S; k += 256) seg[k] = sseg[k];
   const int ncols = Nsrc * S;
@@ -241,8 +255,8 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
   at::Tensor rank = at::empty({ncols}, i32);
   at::Tensor cnt = at::empty({S}, i32);
   at::Tensor posmap = at::empty({ncols}, i32);
-  at::Tensor src = at::full({P_cap}, -1, i32);
-  at::Tensor cinv = at::full({P_cap}, -1, i32);
+  at::Tensor src = at::empty({P_cap}, i32);     // (padding: sg_fill_kernel)
+  at::Tensor cinv = at::empty({P_cap}, i32);
   at::Tensor col_c = at::empty({cap}, i32);
   at::Tensor seg = at::empty({S + 1}, i32);
   if (cap > 0) {
@@ -256,11 +270,12 @@ std::vector<at::Tensor> slot_compact_plan(const at::Tensor& rowptr,
                      mark.data_ptr<int>(), (int)Nsrc, (int)S,
                      rank.data_ptr<int>(), cnt.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
-  const int64_t span = std::max<int64_t>(ncols, cap);
+  const int64_t span = std::max<int64_t>(std::max<int64_t>(ncols, cap), P_cap);
   hipLaunchKernelGGL(sg_fill_kernel, dim3((span + 255) / 256), dim3(256), 0,
                      stream(), rank.data_ptr<int>(), cnt.data_ptr<int>(),
                      (int)Nsrc, (int)S, rowptr.data_ptr<int>(), R,
-                     col.data_ptr<int>(), cap, posmap.data_ptr<int>(),
+                     col.data_ptr<int>(), cap, (int)P_cap,
+                     posmap.data_ptr<int>(),
                      src.data_ptr<int>(), cinv.data_ptr<int>(),
                      col_c.data_ptr<int>(), seg.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
@@ -491,57 +506,91 @@ at::Tensor slot_gemm(const at::Tensor& X, const at::Tensor& src,
   return Y;
 }
 
-// Row tiles of the dX pass that hold sources j >= row0 (slot segments list
-// their sources in ascending j): lane k finds slot k's first such compact
-// row through posmap, the tiles from its row tile to the segment end are
-// listed in slot order; out[tcap] = count.
-__global__ __launch_bounds__(64) void sg_dx_tiles_kernel(
-    const int* __restrict__ posmap, const int* __restrict__ seg, int N, int S,
+// Row tiles of the dX pass that hold sources j >= row0.  Slot k's compact
+// rows list its used sources in ascending j, then padding (src -1), so its
+// first row with src >= row0 is found by a 64-ary search of src over the
+// segment - one probe per lane and round, <= 3 rounds up to 262k rows -
+// instead of a serial walk over the sources.  One wave per slot; the tiles
+// from that row's tile to the segment end are listed in slot order;
+// out[tcap] = count.
+__global__ __launch_bounds__(1024) void sg_dx_tiles_kernel(
+    const int* __restrict__ src, const int* __restrict__ seg, int S,
     int row0, int tcap, int unit, int* __restrict__ out) {
-  const int k = threadIdx.x;
-  int first = 0, last = 0;
-  if (k < S) {
-    int p = seg[k + 1];
-    for (int j = row0; j < N; ++j) {
-      const int q = posmap[(size_t)j * S + k];
-      if (q >= 0) {
-        p = q;
-        break;
+  __shared__ int sfirst[kSgMaxS], scnt[kSgMaxS], sbase[kSgMaxS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < S; k += 16) {
+    const int a = seg[k], b = seg[k + 1];
+    // first p in [a, b] with p == b, src[p] >= row0 or src[p] < 0
+    // (monotone over the segment)
+    int lo = a, hi = b;
+    while (lo < hi) {
+      const int step = (hi - lo + 63) / 64;
+      const int q = lo + lane * step;
+      bool ok = true;
+      if (q < hi) {
+        const int v = src[q];
+        ok = v >= row0 || v < 0;
+      }
+      const unsigned long long m = __ballot(ok);
+      if (m == 0ull) {
+        lo += 63 * step + 1;
+        continue;
+      }
+      const int f = __ffsll((long long)m) - 1;
+      if (f == 0) {
+        hi = lo;
+      } else {
+        hi = min(lo + f * step, hi);
+        lo = lo + (f - 1) * step + 1;
       }
     }
-    first = p / unit;
-    last = seg[k + 1] / unit;
+    // a padding row: no used source >= row0 in this slot
+    const int p = (lo < b && src[lo] < 0) ? b : lo;
+    int first = p / unit;
+    const int last = b / unit;
     if (first > last) first = last;
+    if (lane == 0) {
+      sfirst[k] = first;
+      scnt[k] = last - first;
+    }
   }
-  const int n = last - first;
-  int incl = n;
+  __syncthreads();
+  if (wave == 0) {
+    const int n = lane < S ? scnt[lane] : 0;
+    int incl = n;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o);
-    if (k >= o) incl += v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane < S) sbase[lane] = incl - n;
+    if (lane == 63) out[tcap] = min(incl, tcap);
   }
-  const int base = incl - n;
-  for (int t = 0; t < n && base + t < tcap; ++t) out[base + t] = first + t;
-  if (k == 63) out[tcap] = min(incl, tcap);
+  __syncthreads();
+  for (int k = 0; k < S; ++k) {
+    const int base = sbase[k], first = sfirst[k];
+    for (int t = threadIdx.x; t < scnt[k] && base + t < tcap; t += 1024)
+      out[base + t] = first + t;
+  }
 }
 
-at::Tensor slot_dx_tiles(const at::Tensor& posmap, const at::Tensor& seg,
+at::Tensor slot_dx_tiles(const at::Tensor& src, const at::Tensor& seg,
                          int64_t N, int64_t row0, int64_t P_cap,
                          int64_t unit) {
-  TORCH_CHECK(posmap.is_cuda() && posmap.scalar_type() == at::kInt &&
-                  seg.scalar_type() == at::kInt,
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kInt &&
+                  seg.scalar_type() == at::kInt && src.is_contiguous(),
               "slot_dx_tiles: int32 plan");
   const int64_t S = seg.numel() - 1;
-  TORCH_CHECK(S <= 64 && posmap.numel() == N * S && (unit == 128 ||
+  TORCH_CHECK(S <= kSgMaxS && src.numel() == P_cap && (unit == 128 ||
               unit == 256) && P_cap % unit == 0,
-              "slot_dx_tiles: plan shapes, unit 128 / 256");
-  const c10::hip::HIPGuardMasqueradingAsCUDA guard(posmap.device());
+              "slot_dx_tiles: plan shapes (src [P_cap]), unit 128 / 256");
+  (void)N;
+  const c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
   const int64_t tcap = P_cap / unit;
-  at::Tensor out = at::empty({tcap + 1}, posmap.options());
-  hipLaunchKernelGGL(sg_dx_tiles_kernel, dim3(1), dim3(64), 0, stream(),
-                     posmap.data_ptr<int>(), seg.data_ptr<int>(), (int)N,
-                     (int)S, (int)row0, (int)tcap, (int)unit,
-                     out.data_ptr<int>());
+  at::Tensor out = at::empty({tcap + 1}, src.options());
+  hipLaunchKernelGGL(sg_dx_tiles_kernel, dim3(1), dim3(1024), 0, stream(),
+                     src.data_ptr<int>(), seg.data_ptr<int>(), (int)S,
+                     (int)row0, (int)tcap, (int)unit, out.data_ptr<int>());
   DGMC_CHECK_LAUNCH();
   return out;
 }
@@ -1415,60 +1464,100 @@ at::Tensor slot_spmm_rowmap(const at::Tensor& rowptr, const at::Tensor& col,
 // ---------------------------------------------------------------------------
 // Per-node gather-sum over slots: out[j, :] = add[j, :] + sum_k Z[posmap[j*S
 // + k], :]  (slot order fixed: deterministic).  dX of the slot GEMM.
+//
+// RB (fused ReLU / bias backward of the PRODUCING layer, whose output the
+// gathered gradient belongs to): out = (relu_out > 0) ? sum : 0, and the
+// bias gradient's column partials of 16-row blocks go to part[blk].  A
+// block is 16 lane groups, one row each; the masked rows are stashed in LDS
+// and summed in elementwise.hip::colsum_kernel<float, ..., LPR, true>'s
+// order (its lane group q accumulates rows q, q + R, ... from 0 with
+// R = 256 / LPR, then the groups are added in q order), so the partials
+// are bit-identical to relu_bias_bwd on the unfused output.
 // ---------------------------------------------------------------------------
-template <int LPR>
-__global__ __launch_bounds__(256) void sg_gather_sum_kernel(
+template <int LPR, bool RB>
+__global__ __launch_bounds__(RB ? 16 * LPR : 256) void sg_gather_sum_kernel(
     const int* __restrict__ posmap, const float* __restrict__ Z,
     const float* __restrict__ add, int lda, float* __restrict__ out, int N,
-    int S, int C, int row0) {
-  constexpr int RPB = 256 / LPR;
-  const int blk = xcd_remap(blockIdx.x, gridDim.x);
-  const int j = blk * RPB + threadIdx.x / LPR;
+    int S, int C, int row0, const float* __restrict__ relu_out,
+    float* __restrict__ part) {
+  constexpr int RPB = RB ? 16 : 256 / LPR;      // rows per block
+  const int blk = RB ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int q = threadIdx.x / LPR;
+  const int j = blk * RPB + q;
   const int lane = threadIdx.x % LPR;
-  if (j >= N) return;
-  if (j < row0) {          // rows nobody reads the gradient of: zeros
+  __shared__ float stash[RB ? 16 * 4 * LPR : 1];     // [16][C] masked rows
+  if (RB && (j >= N || j < row0)) {     // (zero rows of the partials)
+    for (int c0 = lane * 4; c0 < C; c0 += LPR * 4)
+      *reinterpret_cast<float4*>(stash + q * C + c0) =
+          make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (j < N && j < row0) {   // rows nobody reads the gradient of: zeros
     for (int c0 = lane * 4; c0 < C; c0 += LPR * 4)
       *reinterpret_cast<float4*>(out + (size_t)j * C + c0) =
           make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  // The row's S posmap entries are loaded once, lane-parallel (lane l of
-  // the group holds entries l, l + LPR, ...), and broadcast by shuffles;
-  // the Z rows are then gathered eight slots at a time, branch-free (unused
-  // slots read row 0 and are not added), so a node's gathers are in flight
-  // together instead of one dependent (posmap, Z) round per slot.
-  constexpr int NP = (kSgMaxS + LPR - 1) / LPR;
-  const int* pm = posmap + (size_t)j * S;
-  int pl[NP];
+  } else if (j < N) {
+    // The row's S posmap entries are loaded once, lane-parallel (lane l of
+    // the group holds entries l, l + LPR, ...), and broadcast by shuffles;
+    // the Z rows are then gathered eight slots at a time, branch-free
+    // (unused slots read row 0 and are not added), so a node's gathers are
+    // in flight together instead of one dependent (posmap, Z) round per slot.
+    constexpr int NP = (kSgMaxS + LPR - 1) / LPR;
+    const int* pm = posmap + (size_t)j * S;
+    int pl[NP];
 #pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const int k = q * LPR + lane;
-    const int v = pm[k < S ? k : 0];       // (clamped: never past the row)
-    pl[q] = k < S ? v : -1;
-  }
-  for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
-    float4 acc = add ? ld4(add + (size_t)j * lda + c0)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k0 = 0; k0 < kSgMaxS; k0 += 8) {
-      if (k0 >= S) break;
-      int p[8];
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = k0 + u;
-        p[u] = __shfl(pl[k / LPR], k % LPR, LPR);
-        p[u] = k < S ? p[u] : -1;
-        v[u] = ld4(Z + (size_t)(p[u] < 0 ? 0 : p[u]) * C + c0);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (p[u] >= 0) {          // slot order: the same sums as before
-          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z;
-          acc.w += v[u].w;
-        }
+    for (int u = 0; u < NP; ++u) {
+      const int k = u * LPR + lane;
+      const int v = pm[k < S ? k : 0];       // (clamped: never past the row)
+      pl[u] = k < S ? v : -1;
     }
-    *reinterpret_cast<float4*>(out + (size_t)j * C + c0) = acc;
+    for (int c0 = lane * 4; c0 < C; c0 += LPR * 4) {
+      float4 acc = add ? ld4(add + (size_t)j * lda + c0)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k0 = 0; k0 < kSgMaxS; k0 += 8) {
+        if (k0 >= S) break;
+        int p[8];
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int k = k0 + u;
+          p[u] = __shfl(pl[k / LPR], k % LPR, LPR);
+          p[u] = k < S ? p[u] : -1;
+          v[u] = ld4(Z + (size_t)(p[u] < 0 ? 0 : p[u]) * C + c0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (p[u] >= 0) {          // slot order: the same sums as before
+            acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z;
+            acc.w += v[u].w;
+          }
+      }
+      if (RB) {
+        const float4 m = ld4(relu_out + (size_t)j * C + c0);
+        acc.x = m.x > 0.f ? acc.x : 0.f;
+        acc.y = m.y > 0.f ? acc.y : 0.f;
+        acc.z = m.z > 0.f ? acc.z : 0.f;
+        acc.w = m.w > 0.f ? acc.w : 0.f;
+        *reinterpret_cast<float4*>(stash + q * C + c0) = acc;
+      }
+      *reinterpret_cast<float4*>(out + (size_t)j * C + c0) = acc;
+    }
+  }
+  if (RB) {
+    // (stash: the masked rows, 0 for rows < row0 - relu_bias_bwd sums
+    // those zeros)
+    __syncthreads();
+    constexpr int R = 256 / LPR;              // colsum's lane groups
+    for (int c = threadIdx.x; c < C; c += 16 * LPR) {
+      float s = 0.f;
+      for (int g = 0; g < R; ++g) {
+        float a = 0.f;
+        for (int r = g; r < 16; r += R)
+          if (blk * 16 + r < N) a += stash[r * C + c];
+        s += a;
+      }
+      part[(size_t)blk * C + c] = s;
+    }
   }
 }
 
@@ -1515,7 +1604,9 @@ at::Tensor slot_rowmap_ell(const at::Tensor& rowptr, const at::Tensor& col,
 at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
                            int64_t N, int64_t S,
                            const c10::optional<at::Tensor>& add,
-                           int64_t row0) {
+                           int64_t row0,
+                           const c10::optional<at::Tensor>& relu_out,
+                           const c10::optional<at::Tensor>& part) {
   TORCH_CHECK(Z.is_cuda() && Z.scalar_type() == at::kFloat &&
                   Z.is_contiguous() && Z.dim() == 2 && Z.size(1) % 4 == 0 &&
                   aligned16(Z.data_ptr()),
@@ -1533,17 +1624,43 @@ at::Tensor slot_gather_sum(const at::Tensor& posmap, const at::Tensor& Z,
     ap = add->data_ptr<float>();
     lda = add->stride(0);
   }
+  const bool rb = relu_out.has_value() && relu_out->defined();
+  if (rb) {
+    // (16-row partial blocks = relu_bias_bwd's blocks for these N)
+    TORCH_CHECK(relu_out->scalar_type() == at::kFloat &&
+                    relu_out->is_contiguous() && relu_out->size(0) == N &&
+                    relu_out->size(1) == C && aligned16(relu_out->data_ptr()),
+                "slot_gather_sum: relu_out contiguous fp32 [N, C]");
+    TORCH_CHECK(N >= 256 && N <= 16 * 1024 && C >= 64 && C <= 256,
+                "slot_gather_sum: fused ReLU / bias backward needs 256 <= N "
+                "<= 16384, 64 <= C <= 256");
+    TORCH_CHECK(part.has_value() && part->defined() &&
+                    part->scalar_type() == at::kFloat && part->is_contiguous() &&
+                    part->numel() == (N + 15) / 16 * C,
+                "slot_gather_sum: part fp32 [ceil(N / 16), C]");
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(Z.device());
   at::Tensor out = at::empty({N, C}, Z.options());
   if (N == 0) return out;
   const int lanes = (int)(C / 4);
+  const float* rp = rb ? relu_out->data_ptr<float>() : nullptr;
+  float* pp = rb ? part->data_ptr<float>() : nullptr;
   auto go = [&](auto lpr) {
     constexpr int L = decltype(lpr)::value;
+    if (rb) {
+      hipLaunchKernelGGL((sg_gather_sum_kernel<L, true>),
+                         dim3((unsigned)((N + 15) / 16)), dim3(16 * L), 0,
+                         stream(), posmap.data_ptr<int>(), Z.data_ptr<float>(),
+                         ap, (int)lda, out.data_ptr<float>(), (int)N, (int)S,
+                         (int)C, (int)row0, rp, pp);
+      return;
+    }
     const int64_t blocks = (N + 256 / L - 1) / (256 / L);
-    hipLaunchKernelGGL(sg_gather_sum_kernel<L>, dim3(blocks), dim3(256), 0,
-                       stream(), posmap.data_ptr<int>(), Z.data_ptr<float>(),
-                       ap, (int)lda, out.data_ptr<float>(), (int)N, (int)S,
-                       (int)C, (int)row0);
+    hipLaunchKernelGGL((sg_gather_sum_kernel<L, false>), dim3(blocks),
+                       dim3(256), 0, stream(), posmap.data_ptr<int>(),
+                       Z.data_ptr<float>(), ap, (int)lda,
+                       out.data_ptr<float>(), (int)N, (int)S, (int)C,
+                       (int)row0, nullptr, nullptr);
   };
   if (lanes <= 8) go(std::integral_constant<int, 8>());
   else if (lanes <= 16) go(std::integral_constant<int, 16>());

@@ -23,6 +23,7 @@ loop) the weight gradient of all uses is ONE launch over the kept ``(X_u,
 dY_c,u)`` pairs.
 """
 import os
+import weakref
 
 import torch
 
@@ -88,7 +89,7 @@ def dx_tiles(plan, row0, unit=BM):
     t = cache.get((row0, unit))
     if t is None:
         t = cache[(row0, unit)] = _backend.ops().slot_dx_tiles(
-            plan.posmap, plan.seg, plan.N, row0, plan.P_cap, unit)
+            plan.src, plan.seg, plan.N, row0, plan.P_cap, unit)
     return t
 
 
@@ -256,6 +257,18 @@ class _SlotGemmSpMM(torch.autograd.Function):
         ctx.has_root = root is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.idx = loop.register() if loop is not None else None
+        # Fused ReLU / bias backward: the NEXT slot conv's gather-sum (the
+        # dX producing this output's gradient) applies this layer's ReLU mask
+        # and deposits its bias-gradient partials into this use's loop slot
+        # (bit-identical to relu_bias_bwd; csrc/hip/slot_gemm.hip
+        # sg_gather_sum_kernel<RB>).  ``out`` carries the hand-off record,
+        # the consumer keeps the record of its input.
+        ctx.rb = None
+        if RB_FUSE and relu and loop is not None and ctx.x6:
+            ctx.rb = _ReluBiasHandoff(out, loop, ctx.idx, ctx.bias_dtype
+                                      is not None and ctx.needs_input_grad[3])
+            out._dgmc_rb = ctx.rb
+        ctx.in_rb = getattr(x, '_dgmc_rb', None)
         if passthrough:
             return out, x.view_as(x)
         return out
@@ -270,12 +283,21 @@ class _SlotGemmSpMM(torch.autograd.Function):
         if grad.stride(-1) != 1 or grad.stride(0) < grad.size(1) or \
                 grad.dtype != torch.float32:
             grad = grad.float().contiguous()
-        part = loop.slot('b', idx, (col_partial_rows(grad.size(0)),
-                                    grad.size(1)), torch.float32,
-                         grad.device) if (loop is not None and need_b) \
-            else None
-        g, db = ops.relu_bias_bwd(grad, out if ctx.relu else grad, ctx.relu,
-                                  torch.float32, None, False, part)
+        rb = ctx.rb
+        if rb is not None and rb.accepts(grad):
+            # ReLU mask applied and bias partials deposited by the consumer's
+            # gather-sum
+            g, db = grad, None
+        else:
+            part = loop.slot('b', idx, (col_partial_rows(grad.size(0)),
+                                        grad.size(1)), torch.float32,
+                             grad.device) if (loop is not None and need_b) \
+                else None
+            g, db = ops.relu_bias_bwd(grad, out if ctx.relu else grad,
+                                      ctx.relu, torch.float32, None, False,
+                                      part)
+        if rb is not None:
+            rb.g = None
         At = op.t()
         dyc = ops.slot_spmm_rowmap(At.rowptr, At.col, At.val, plan.cinv, g,
                                     plan.seg, rowmap_ranges(plan, At),
@@ -293,8 +315,16 @@ class _SlotGemmSpMM(torch.autograd.Function):
                             and gpass.stride(1) == 1 and
                             gpass.stride(0) % 4 == 0 and
                             gpass.data_ptr() % 16 == 0) else None
-            gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add,
-                                     row0)
+            rb = ctx.in_rb
+            if rb is not None and (gpass is None or add is not None):
+                fused = rb.fuse_args(plan.N, Z.size(1), Z.device)
+                if fused is not None:
+                    gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S,
+                                             add, row0, *fused)
+                    rb.hand(gx)
+            if gx is None:
+                gx = ops.slot_gather_sum(plan.posmap, Z, plan.N, plan.S, add,
+                                         row0)
             if gpass is not None and add is None:
                 gx = gx + gpass
         elif ctx.needs_input_grad[0]:
@@ -360,6 +390,46 @@ class _SlotGemmSpMM(torch.autograd.Function):
             if ctx.has_root and ctx.needs_input_grad[2]:
                 gr = dW[nw]
         return (gx, gw, gr, gb) + nones
+
+
+# Fused ReLU / bias backward of a slot conv into the next slot conv's
+# gather-sum (PascalVOC: psi_2 layer 0's relu_bias_bwd, 10 launches a step).
+RB_FUSE = True
+
+
+class _ReluBiasHandoff(object):
+    """Hand-off record between a ReLU slot conv (producer) and the slot conv
+    that consumes its output: the consumer's dX gather-sum writes the masked
+    gradient ``g`` and the producer's bias partials; the producer's backward
+    takes ``g`` as is only if autograd hands it over unchanged (same tensor,
+    same version - no other consumer's gradient was added), and otherwise
+    recomputes both (the ReLU mask is idempotent and the partials are
+    overwritten, so the fallback stays exact)."""
+
+    def __init__(self, out, loop, idx, need_b):
+        self.out = weakref.ref(out)
+        self.loop, self.idx, self.need_b = loop, idx, need_b
+        self.g = None
+        self.gv = None
+
+    def fuse_args(self, N, C, device):
+        out = self.out()
+        if out is None or self.g is not None or out.dtype != torch.float32 \
+                or not out.is_contiguous() or tuple(out.shape) != (N, C) or \
+                out.data_ptr() % 16 != 0 or not (256 <= N <= 16384) or \
+                not (64 <= C <= 256):
+            return None
+        shape = (col_partial_rows(N), C)
+        part = self.loop.slot('b', self.idx, shape, torch.float32, device) \
+            if self.need_b else torch.empty(shape, device=device)
+        return out, part
+
+    def hand(self, g):
+        self.g, self.gv = g, g._version
+
+    def accepts(self, grad):
+        return self.g is not None and grad is self.g and \
+            grad._version == self.gv
 
 
 def _forward_uses(weight):

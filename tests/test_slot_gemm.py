@@ -101,6 +101,24 @@ def test_compact_plan_layout(n, e):
     for s_ in range(S):
         rows = src[int(seg[s_]):int(seg[s_]) + int(cnt[s_])]
         assert bool((rows[1:] > rows[:-1]).all())
+    # Rows no used column maps to (segment padding, the tail) hold -1.
+    free = torch.ones(plan.P_cap, dtype=torch.bool)
+    free[p] = False
+    assert (src[free] == -1).all() and (plan.cinv.cpu()[free] == -1).all()
+    # dX row-tile lists: slot k's tiles from the tile of its first source
+    # >= row0 to its segment end, in slot order (count at [tcap]).
+    for row0 in (0, 1, n // 3, n - 1, n):
+        for unit in (128, 256):
+            got = sg.dx_tiles(plan, row0, unit).cpu()
+            ref = []
+            for s_ in range(S):
+                a, b = int(seg[s_]), int(seg[s_ + 1])
+                hit = (src[a:a + int(cnt[s_])] >= row0).nonzero()
+                first = (a + int(hit[0])) // unit if hit.numel() else b // unit
+                ref += list(range(min(first, b // unit), b // unit))
+            tcap = plan.P_cap // unit
+            assert int(got[tcap]) == min(len(ref), tcap)
+            assert got[:min(len(ref), tcap)].tolist() == ref[:tcap]
 
 
 def test_loop_weight_grad_equals_per_use():
@@ -122,6 +140,46 @@ def test_loop_weight_grad_equals_per_use():
 
     for a, bb in zip(run(True), run(False)):
         assert _rel(a, bb) < 1e-6
+
+
+@pytest.mark.parametrize('n,cat', [(600, True), (2000, False)])
+def test_relu_bias_handoff_bit_identical(n, cat):
+    """Layer 0's ReLU mask and bias partials applied by layer 1's dX
+    gather-sum (RB_FUSE) give bit-identical gradients to the unfused
+    relu_bias_bwd, inside the consensus loop (3 uses)."""
+    if not sg.X6:
+        pytest.skip('bf16x6 path only')
+    e, C = 4 * n, 128
+    ei, pseudo = _graph(n, e, seed=13)
+    op = spline_plan(ei, pseudo, n, (5, 5), (1, 1), 1, root=True)
+    p0 = [t.requires_grad_() for t in _params(C, C, seed=3)]
+    p1 = [t.requires_grad_() for t in _params(C, C, seed=6)]
+    xs = [torch.randn(n, C, device=DEV) for _ in range(3)]
+    gs = [torch.randn(n, 3 * C if cat else C, device=DEV) for _ in range(3)]
+
+    def run(fuse):
+        sg.RB_FUSE = fuse
+        try:
+            with loopgrad.loop_scope(True):
+                loss = 0
+                for x, g in zip(xs, gs):
+                    x = x.clone().requires_grad_()
+                    h0 = sg.slot_gemm_spmm(op, x, *p0, relu=True,
+                                           loop_key=('l0', ), passthrough=cat)
+                    if cat:
+                        h0, x = h0
+                    h1 = sg.slot_gemm_spmm(op, h0, *p1, relu=True,
+                                           loop_key=('l1', ), passthrough=cat)
+                    if cat:
+                        h1, h0 = h1
+                        h1 = torch.cat([x, h0, h1], 1)
+                    loss = loss + (h1 * g).sum()
+                return torch.autograd.grad(loss, p0 + p1)
+        finally:
+            sg.RB_FUSE = True
+
+    for a, b in zip(run(True), run(False)):
+        assert torch.equal(a, b)
 
 
 def test_passthrough_gradient_added():
