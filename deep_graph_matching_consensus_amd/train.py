@@ -41,9 +41,15 @@ IN_STEP_ALLREDUCE = os.environ.get('DGMC_AMD_IN_STEP_ALLREDUCE', '1') == '1'
 # CUs the persistent GEMM grids leave to RCCL's channel kernels under data
 # parallelism, applied only while the step's all-reduces are in flight
 # (parallel/ddp.py; DGMC_AMD_RESERVE_CUS overrides; single-GPU runs reserve
-# none).  tools/bench_cu_reserve.py (profiles/cu_reserve_r5.json): 8 CUs
-# held by a concurrent kernel stretch psi_1's 1024 -> 256 bf16x6 forward
-# from 400 to 615 us; with the grid sized to 256 - 8 CUs it runs 405 us.
+# none).  tools/bench_cu_reserve.py (profiles/cu_reserve_r6.json, psi_1's
+# 1024 -> 256 bf16x6 forward / input gradient, persistent grids): a
+# concurrent kernel holding h CUs stretches them 400 -> 611-623 / 419 ->
+# 602-635 us whenever the reserve r < h, and costs nothing beyond the lost
+# CUs once r >= h (dX 440 / 455 us at r = 8 / 32); the weight gradient's
+# item grid is insensitive (469-540 us either way).  8 covers an RCCL
+# all-reduce on up to 8 channel workgroups at ~5 % on the backward's
+# persistent kernels; DGMC_AMD_RESERVE_CUS raises it where RCCL runs more
+# channels (untested on multi-GPU hardware by us).
 DP_RESERVE_CUS = 8
 # Captured all-reduce pre-flight before the first step capture
 # (DGMC_AMD_DP_PREFLIGHT=0 skips it).

@@ -8,6 +8,9 @@ kernel that occupies ``--hog`` CUs for the whole measurement
 the grids sized to all CUs (reserve 0) and to ``CUs - reserve``.
 
     python tools/bench_cu_reserve.py [--hog 8 16] [--reserve 8 16] [--json f]
+
+(round 6: the input-gradient kernel added - the reserve is applied only
+from the step's first gradient all-reduce launch to its end.)
 """
 import argparse
 import json
@@ -77,9 +80,14 @@ def main():
     dy = torch.randn(P, cout, device=dev)
     x3 = ops.split3(x)
     wt3 = ops.slot_weight_x3(w, r, True)
+    w3 = ops.slot_weight_x3(w, r, False)
     kernels = {
         'fwd_1024x256': lambda: ops.slot_gemm_x6(x, plan.src, plan.seg, wt3,
                                                  True, None),
+        # the input gradient (persistent like the forward; runs in the
+        # backward next to the gradient all-reduces)
+        'dx_1024x256': lambda: ops.slot_gemm_x6(dy, plan.src, plan.seg, w3,
+                                                False, None),
         'wgrad_1024x256': lambda: ops.slot_wgrad_x6(
             [x3], [dy], plan.src, plan.seg, sg._x6_rounds(16)),
     }
