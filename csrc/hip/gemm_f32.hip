@@ -60,7 +60,10 @@ __device__ __forceinline__ void gf_dma16(const float* g, DGMC_LDS float* l) {
 }
 
 __device__ __forceinline__ void gf_barrier() {
-  asm volatile("" ::: "memory");
+  // (drain this wave's LDS reads first: gfx950 barriers do not wait for
+  // them, and their consumers - MFMAs, no memory operands - may be
+  // scheduled past the barrier while another wave's DMA refills the stage)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

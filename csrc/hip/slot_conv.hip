@@ -470,7 +470,8 @@ static_assert(kScC * kScAP <= 3 * kScATile, "xt must fit the A tiles");
 // access of one slot step may be scheduled across the barrier into another
 // (s_barrier alone is not a memory operation to the optimiser).
 __device__ __forceinline__ void sc_raw_barrier() {
-  asm volatile("" ::: "memory");
+  // (drains this wave's LDS reads: see slot_gemm_x6.hip::x6_barrier)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

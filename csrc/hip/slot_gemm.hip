@@ -640,7 +640,8 @@ __device__ __forceinline__ void sg_dma16(const float* g, DGMC_LDS float* l) {
 // would serialise the next chunk's LDS-DMA with this chunk's MFMAs); the
 // empty asm statements keep the compiler from moving memory ops across it.
 __device__ __forceinline__ void sg_raw_barrier() {
-  asm volatile("" ::: "memory");
+  // (drains this wave's LDS reads: see slot_gemm_x6.hip::x6_barrier)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

@@ -74,7 +74,10 @@ __device__ __forceinline__ void x6_dma16(const __bf16* g, DGMC_LDS __bf16* l) {
 // s_barrier without __syncthreads' fence (which would drain vmcnt and
 // serialise the next chunk's DMA with this chunk's MFMAs).
 __device__ __forceinline__ void x6_barrier() {
-  asm volatile("" ::: "memory");
+  // (drain this wave's LDS reads first: gfx950 barriers do not wait for
+  // them, and their consumers - MFMAs, no memory operands - may be
+  // scheduled past the barrier while another wave's DMA refills the stage)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
