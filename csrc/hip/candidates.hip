@@ -178,10 +178,50 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(
     hist[((int64_t)4 * t + wave) * kRsBins + d] = cnt[wave][d];
 }
 
+// Large inputs (more than kRsScanTiles tiles): the per-digit exclusive
+// prefixes of the [4 tiles][256] count table, column by column (block =
+// digit, 256-row chunks scanned by wave shuffles + LDS with a running carry),
+// and each digit's total - so every scatter block reads only its own four
+// count rows instead of the whole table (O(tiles) instead of O(tiles^2)
+// count traffic per pass).
+constexpr int kRsScanTiles = 256;
+
+__global__ __launch_bounds__(256) void rs_scan_kernel(
+    const int* __restrict__ hist, int R4, int* __restrict__ pre,
+    int* __restrict__ tot) {
+  __shared__ int wsum[4];
+  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63,
+            wave = tid >> 6;
+  int carry = 0;
+  for (int r0 = 0; r0 < R4; r0 += 256) {
+    const int r = r0 + tid;
+    const int v = r < R4 ? hist[(int64_t)r * kRsBins + d] : 0;
+    int inc = v;
+#pragma unroll
+    for (int e = 1; e < 64; e <<= 1) {
+      const int t = __shfl_up(inc, e);
+      if (lane >= e) inc += t;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int base = carry, all = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      base += w < wave ? wsum[w] : 0;
+      all += wsum[w];
+    }
+    if (r < R4) pre[(int64_t)r * kRsBins + d] = base + inc - v;
+    carry += all;
+    __syncthreads();                       // wsum reused
+  }
+  if (tid == 0) tot[d] = carry;
+}
+
 __global__ __launch_bounds__(256) void rs_scatter_kernel(
     const int* __restrict__ keys, const int* __restrict__ vals, int64_t n,
     int shift, const int* __restrict__ offs, int tiles,
-    int* __restrict__ keys_out, int* __restrict__ vals_out) {
+    int* __restrict__ keys_out, int* __restrict__ vals_out,
+    const int* __restrict__ spre, const int* __restrict__ stot) {
   __shared__ int cnt[4][kRsBins];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int t = blockIdx.x;
@@ -193,7 +233,27 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(
     kr[q] = keys[i < n ? i : 0];
     vr[q] = vals[i < n ? i : 0];
   }
-  {
+  if (spre != nullptr) {
+    // scanned table: digit totals scanned over digits, plus this tile's
+    // four exclusive prefixes
+    __shared__ int wtot2[4];
+    const int d = tid, r0 = 4 * t;
+    const int tt = stot[d];
+    int inc = tt;
+#pragma unroll
+    for (int e = 1; e < 64; e <<= 1) {
+      const int v = __shfl_up(inc, e);
+      if (lane >= e) inc += v;
+    }
+    if (lane == 63) wtot2[wave] = inc;
+    __syncthreads();
+    int run = inc - tt;
+    for (int w = 0; w < wave; ++w) run += wtot2[w];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      cnt[w][d] = run + spre[(int64_t)(r0 + w) * kRsBins + d];
+    __syncthreads();
+  } else {
     // Start of digit d = tid in each of this tile's 4 waves, from the whole
     // [tiles][4][256] count table (coalesced rows, 32 loads in flight): the
     // digit's total (scanned over digits), the counts of the rows before
@@ -287,6 +347,13 @@ std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
   at::Tensor hist = at::empty({(int64_t)kRsBins * 4 * std::max(tiles, 1)},
                               i32);
   at::Tensor k2 = at::empty({n}, i32), v2 = at::empty({n}, i32);
+  // (large inputs: a scanned count table, see rs_scan_kernel)
+  const bool scan = tiles > kRsScanTiles;
+  at::Tensor pre, tot;
+  if (scan) {
+    pre = at::empty({(int64_t)kRsBins * 4 * tiles}, i32);
+    tot = at::empty({kRsBins}, i32);
+  }
   // ping-pong so the last pass lands in keys / perm
   const int* ki = col.data_ptr<int>();
   const int* vi = iota.data_ptr<int>();
@@ -300,8 +367,16 @@ std::vector<at::Tensor> candidate_csc(const at::Tensor& S_idx, int64_t n_t) {
     hipLaunchKernelGGL(rs_hist_kernel, dim3(tiles), dim3(256), 0, stream(), ki,
                        n, 8 * p, hist.data_ptr<int>(), tiles);
     DGMC_CHECK_LAUNCH();
+    if (scan) {
+      hipLaunchKernelGGL(rs_scan_kernel, dim3(kRsBins), dim3(256), 0,
+                         stream(), hist.data_ptr<int>(), 4 * tiles,
+                         pre.data_ptr<int>(), tot.data_ptr<int>());
+      DGMC_CHECK_LAUNCH();
+    }
     hipLaunchKernelGGL(rs_scatter_kernel, dim3(tiles), dim3(256), 0, stream(),
-                       ki, vi, n, 8 * p, hist.data_ptr<int>(), tiles, ko, vo);
+                       ki, vi, n, 8 * p, hist.data_ptr<int>(), tiles, ko, vo,
+                       scan ? pre.data_ptr<int>() : nullptr,
+                       scan ? tot.data_ptr<int>() : nullptr);
     DGMC_CHECK_LAUNCH();
     ki = ko;
     vi = vo;

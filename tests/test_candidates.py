@@ -94,10 +94,12 @@ def test_train_candidates_fresh_negatives_and_graph_replay():
     assert torch.equal(first[..., :10], topk)
 
 
-# (DBP15K size: 2 radix digits; 140k columns: 3 digits; a partial tile)
+# (DBP15K size: 2 radix digits; 140k columns: 3 digits; a partial tile;
+# 2.4M entries: more than 256 tiles, the scanned count table)
 @pytest.mark.parametrize('B,N_s,N_t,k', [(1, 1937, 1960, 20), (4, 50, 70, 7),
                                          (1, 19388, 19572, 10),
-                                         (2, 3000, 70000, 5), (1, 3, 5, 2)])
+                                         (2, 3000, 70000, 5), (1, 3, 5, 2),
+                                         (1, 200000, 60000, 12)])
 def test_candidate_csc_matches_stable_argsort(B, N_s, N_t, k):
     g = torch.Generator().manual_seed(B)
     # Skewed targets (a few hubs), like top-k of random-init embeddings.
