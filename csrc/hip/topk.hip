@@ -210,6 +210,32 @@ __global__ __launch_bounds__(256) void split_bf16_kernel(
   *reinterpret_cast<bf16x4*>(lo + r * CP + c) = vl;
 }
 
+// Bitonic sort of (v, ix) over the 32 lanes of each half-wave into (value
+// desc, index asc) order, from stage k2 = k2_0 (2: a full sort; 32: only the
+// final merge of a bitonic sequence).
+__device__ __forceinline__ void x3_bitonic32(float& v, int& ix, int hl,
+                                             int k2_0) {
+#pragma unroll
+  for (int k2 = 2; k2 <= 32; k2 <<= 1) {
+    if (k2 < k2_0) continue;
+#pragma unroll
+    for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
+      const float pv = __shfl_xor(v, jj);
+      const int pix = __shfl_xor(ix, jj);
+      const bool better = v > pv || (v == pv && ix < pix);
+      const bool desc = (hl & k2) == 0, lower = (hl & jj) == 0;
+      if ((lower == desc) != better) {
+        v = pv;
+        ix = pix;
+      }
+    }
+  }
+}
+
+// Tiles (from the first) whose lists are updated by sort + merge instead of
+// insertion rounds (the rounds win once few scores of a tile still enter).
+constexpr int kX3MergeTiles = 4;
+
 template <int NKS, int W>
 __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     const float* __restrict__ h_s, const __bf16* __restrict__ t_hi,
@@ -352,20 +378,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
       const bool ok = col_ok && acc[r] > -INFINITY;
       float v = ok ? acc[r] : -INFINITY;
       int ix = ok ? j0 + hl : init_i;
-#pragma unroll
-      for (int k2 = 2; k2 <= 32; k2 <<= 1) {
-#pragma unroll
-        for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
-          const float pv = __shfl_xor(v, jj);
-          const int pix = __shfl_xor(ix, jj);
-          const bool better = v > pv || (v == pv && ix < pix);
-          const bool desc = (hl & k2) == 0, lower = (hl & jj) == 0;
-          if ((lower == desc) != better) {
-            v = pv;
-            ix = pix;
-          }
-        }
-      }
+      x3_bitonic32(v, ix, hl, 2);
       lv[r] = v;
       li[r] = ix;
       const float t_lo_half = lane_f(v, k - 1);
@@ -377,7 +390,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     t_first = 1;
   }
 
-  for (int t = t_first; t < ntiles; ++t) {
+  auto step = [&](int t, auto merge_tag) {
+    constexpr bool MERGE = decltype(merge_tag)::value;
     const int j0 = j_begin + t * kX3Tile;
     if (t + 1 < ntiles) load_tile(j0 + kX3Tile, pre);
     const DGMC_LDS __bf16* bh = sB + (t & 1) * 2 * TILE + hl * BP + 8 * h;
@@ -398,6 +412,42 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
     if (t + 1 < ntiles) store_tile((t + 1) & 1, pre);
 
     const bool col_ok = j0 + hl < j_end && !(kDiagBuild && (dbg & 1));
+    if constexpr (MERGE) {
+      // Early tiles still put about half their scores into the lists: sort
+      // the tile's 32 scores per row-half (bitonic, value desc, index asc)
+      // and merge them with the sorted 32-entry list (lanes >= k hold the
+      // runners-up of the earlier tiles): the better of list[i] and
+      // new[31 - i] gives the top 32 as a bitonic sequence, five more steps
+      // sort it.  Every entry stays distinct - the tile's sentinels
+      // (masked / non-finite scores) get indices of their own, >= Nt and
+      // unique per (split, tile, lane) - so the split merge can rank them.
+      const int sent = Nt + 64 * (split + (int)gridDim.y * t) + hl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool ok = col_ok && acc[r] > -INFINITY;
+        float v = ok ? acc[r] : -INFINITY;
+        int ix = ok ? j0 + hl : sent;
+        x3_bitonic32(v, ix, hl, 2);
+        // reversed new list against the current list
+        const float rv = __shfl(v, (lane & 32) + 31 - hl);
+        const int rix = __shfl(ix, (lane & 32) + 31 - hl);
+        float a = lv[r];
+        int ai = li[r];
+        if (rv > a || (rv == a && rix < ai)) {
+          a = rv;
+          ai = rix;
+        }
+        x3_bitonic32(a, ai, hl, 32);
+        lv[r] = a;
+        li[r] = ai;
+        const float t_lo_half = lane_f(a, k - 1);
+        const float t_hi_half = lane_f(a, 32 + k - 1);
+        thr[r] = hb ? t_hi_half : t_lo_half;
+        __builtin_amdgcn_sched_barrier(0);   // (one row at a time)
+      }
+      __syncthreads();
+      return;
+    }
     // One wave vote for the whole tile first: once the lists have filled,
     // most tiles hold no candidate beating any row's k-th score, and the
     // 16 per-row votes below are skipped.
@@ -439,7 +489,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
       }
     }
     __syncthreads();
-  }
+  };
+  // (two loops: the merge tiles' register use stays out of the main loop)
+  int t = t_first;
+  if (t_first == 1)
+    for (; t < min(kX3MergeTiles, ntiles); ++t) step(t, std::true_type());
+  for (; t < ntiles; ++t) step(t, std::false_type());
 
   if (hl < k) {
 #pragma unroll

@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# (Round-6 A/B of the top-k first-tile sort: TK_AB_NOSORT was a temporary
+# host hook of that build, removed after the measurement.)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
