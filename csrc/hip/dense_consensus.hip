@@ -23,6 +23,8 @@
 //   * sizes LDS dynamically from the padded pair tile (Ns, Nt <= 64).
 #include "common.h"
 
+#include <type_traits>
+
 namespace dgmc {
 
 constexpr int kMaxN = 64;      // max padded nodes per graph of a pair
@@ -941,6 +943,25 @@ template <> struct StepIO<float> {
   }
 };
 
+// Four fp32 values as their bf16x6 operand planes (common.h split3_bf16,
+// the same split as slot_gemm_x6.hip's split3): p -> planes 0 / 1 / 2 at
+// p, p + ps, p + 2 ps.
+__device__ __forceinline__ void store_planes4(__bf16* p, size_t ps,
+                                              ps_f32x4 a) {
+  ps_bf16x4 h, m, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __bf16 he, me, le;
+    split3_bf16(a[e], he, me, le);
+    h[e] = he;
+    m[e] = me;
+    l[e] = le;
+  }
+  *reinterpret_cast<ps_bf16x4*>(p) = h;
+  *reinterpret_cast<ps_bf16x4*>(p + ps) = m;
+  *reinterpret_cast<ps_bf16x4*>(p + 2 * ps) = l;
+}
+
 // One operand block staged by stage_blocks: rows [0, rows) of a packed
 // [*, R] block (storage T) into an fp32 LDS tile of pitch `pitch`,
 // optionally copied verbatim to `copy` (same row layout).
@@ -999,16 +1020,21 @@ __device__ __forceinline__ void stage_blocks(const StageBlk<T> (&blk)[NB]) {
         if (bk.copy)
           *reinterpret_cast<typename IO::vec*>(bk.copy + (size_t)qq * VN) =
               v[u];
+
       }
     }
   }
 }
 
 // Static-batch padding rows spread over the whole grid in 16-byte pieces:
-// rows [z0, z1) of zdst zeroed and rows [c0, c1) of csrc copied to cdst.
+// rows [z0, z1) of zdst zeroed and rows [c0, c1) of csrc copied to cdst
+// (fp32 only: also as bf16x6 planes at pz / pc, rows laid out like zdst /
+// cdst, plane stride ps).
 template <int R, typename T>
 __device__ __forceinline__ void pad_rows(T* zdst, int z0, int z1, T* cdst,
-                                         const T* csrc, int c0, int c1) {
+                                         const T* csrc, int c0, int c1,
+                                         __bf16* pz = nullptr,
+                                         __bf16* pc = nullptr, size_t ps = 0) {
   using V = typename StepIO<T>::vec;
   constexpr int VN = StepIO<T>::VN;
   constexpr int V8 = R / VN;
@@ -1017,11 +1043,16 @@ __device__ __forceinline__ void pad_rows(T* zdst, int z0, int z1, T* cdst,
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nz + nc;
        e += stride) {
     if (e < nz) {
-      *reinterpret_cast<V*>(zdst + (size_t)z0 * R + (size_t)e * VN) = V{};
+      const size_t off = (size_t)z0 * R + (size_t)e * VN;
+      *reinterpret_cast<V*>(zdst + off) = V{};
+      if constexpr (VN == 4)
+        if (pz) store_planes4(pz + off, ps, V{});
     } else {
       const size_t off = (size_t)c0 * R + (size_t)(e - nz) * VN;
-      *reinterpret_cast<V*>(cdst + off) =
-          *reinterpret_cast<const V*>(csrc + off);
+      const V v = *reinterpret_cast<const V*>(csrc + off);
+      *reinterpret_cast<V*>(cdst + off) = v;
+      if constexpr (VN == 4)
+        if (pc) store_planes4(pc + off, ps, v);
     }
   }
 }
@@ -1046,7 +1077,8 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
     const T* __restrict__ r_s, const int* __restrict__ ptr_s,
     const int* __restrict__ ptr_t, float* __restrict__ S_new,
     float* __restrict__ S_prob, T* __restrict__ rs_copy,
-    T* __restrict__ rt_out, int Ns, int Nt, int rows_s, int rows_t) {
+    T* __restrict__ rt_out, __bf16* __restrict__ planes, int Ns, int Nt,
+    int rows_s, int rows_t) {
   using G = StepGeom<R>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   DGMC_LDS float* sP = (DGMC_LDS float*)smem_raw;
@@ -1075,6 +1107,11 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
     bias2 = b2[0];
   }
   T* rsc = rs_copy ? rs_copy + (size_t)s0 * R : nullptr;
+  // bf16x6 planes of the joint [r_s; r_t] (psi_2's operand; fp32 only, with
+  // rs_copy): plane stride ps, r_t rows from row rows_s.  Written after the
+  // last global load of the workgroup (vmcnt counts stores too: stores
+  // issued during the staging would stall its load waits).
+  const size_t ps = (size_t)(rows_s + rows_t) * R;
   if constexpr (CONS && TRANS) {
     const StageBlk<T> blk[3] = {{P + (size_t)s0 * R, sP, nullptr, ns, G::PP},
                              {Q + (size_t)t0 * R, sQ, nullptr, nt, G::PP},
@@ -1094,9 +1131,10 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
     if (e < NN) sS[e] = pre[u];
   }
   for (int e = tid + kPrefetch * kThreads; e < NN; e += kThreads) sS[e] = Sh[e];
+  __bf16* plt = (planes && rs_copy) ? planes + (size_t)rows_s * R : nullptr;
   if constexpr (TRANS)
     pad_rows<R, T>(rt_out, ptr_t[gridDim.x], rows_t, rs_copy, r_s,
-                   ptr_s[gridDim.x], rows_s);
+                   ptr_s[gridDim.x], rows_s, plt, plt ? planes : nullptr, ps);
   __syncthreads();
 
   // 1. consensus update of the valid block: 4 lanes per (i, j) entry.
@@ -1163,6 +1201,21 @@ __global__ __launch_bounds__(kThreads) void pair_step_fwd_kernel(
     }
     StepIO<T>::store4(rt + (size_t)j0 * R + 4 * cq, a0);
     if (has1) StepIO<T>::store4(rt + (size_t)j1 * R + 4 * cq, a1);
+    if constexpr (std::is_same<T, float>::value) {
+      if (plt) {
+        __bf16* pj = plt + (size_t)t0 * R + 4 * cq;
+        store_planes4(pj + (size_t)j0 * R, ps, a0);
+        if (has1) store_planes4(pj + (size_t)j1 * R, ps, a1);
+      }
+    }
+  }
+  // the pair's r_s rows as planes, from their fp32 LDS image
+  if constexpr (std::is_same<T, float>::value) {
+    if (plt) {
+      __bf16* pr = planes + (size_t)s0 * R;
+      for (int q = tid; q < ns * (R / 4); q += kThreads)
+        store_planes4(pr + (size_t)q * 4, ps, lds4(sR + q * 4));
+    }
   }
 }
 
@@ -1464,6 +1517,7 @@ struct StepFwdArgs {
   void *rs_copy, *rt_out;
   int B, Ns, Nt, rows_s, rows_t;
   bool f32 = false;            // node-level storage fp32 (else bf16)
+  __bf16* planes = nullptr;    // joint's bf16x6 planes (fp32, with rs_copy)
 };
 
 struct StepBwdArgs {
@@ -1489,8 +1543,9 @@ static void step_fwd_launch(const StepFwdArgs& a) {
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(kThreads), lds, stream(), a.S_hat,
                      (const E*)a.P, (const E*)a.Q, a.b1, a.w2, a.b2,
                      (const E*)a.r_s, a.ptr_s, a.ptr_t, a.S_new, a.S_prob,
-                     (E*)a.rs_copy, (E*)a.rt_out, a.Ns, a.Nt, a.rows_s,
-                     a.rows_t);
+                     (E*)a.rs_copy, (E*)a.rt_out,
+                     std::is_same<E, float>::value ? a.planes : nullptr, a.Ns,
+                     a.Nt, a.rows_s, a.rows_t);
   DGMC_CHECK_LAUNCH();
 }
 
@@ -1567,10 +1622,37 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
   return out;
 }
 
+at::Tensor split3(const at::Tensor& x);   // slot_gemm_x6.hip
+
+// Optional bf16x6 planes output of the joint [r_s; r_t] ([3, rows, R] bf16,
+// fp32 joint only); nullptr when absent.
+static __bf16* joint_planes(const c10::optional<at::Tensor>& planes,
+                            const at::Tensor& joint) {
+  if (!planes.has_value() || !planes->defined()) return nullptr;
+  const at::Tensor& p = *planes;
+  TORCH_CHECK(joint.scalar_type() == at::kFloat &&
+                  p.scalar_type() == at::kBFloat16 && p.is_contiguous() &&
+                  p.dim() == 3 && p.size(0) == 3 &&
+                  p.size(1) == joint.size(0) && p.size(2) == joint.size(1) &&
+                  aligned16(p.data_ptr()) && p.device() == joint.device(),
+              "joint planes: bf16 [3, rows_s + rows_t, R] of an fp32 joint");
+  return reinterpret_cast<__bf16*>(p.data_ptr());
+}
+
+// (planes filled from the finished joint: the paths without the step kernel)
+static void joint_planes_fill(const c10::optional<at::Tensor>& planes,
+                              const at::Tensor& joint) {
+  if (joint_planes(planes, joint) != nullptr && joint.numel() > 0)
+    planes->copy_(split3(joint));
+}
+
 // r_s: packed [sum N_s, R]; returns (S [B, Ns, Nt], r_t packed [rows_t, R]).
+// `planes` (with joint_out, fp32): also written with the joint's bf16x6
+// operand planes (psi_2's first slot GEMM reads them; no split pass).
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out) {
+    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out,
+    const c10::optional<at::Tensor>& planes) {
   check_pair_tensor(S_hat, "S_hat");
   check_packed(r_s, "r_s");
   const c10::hip::HIPGuardMasqueradingAsCUDA guard(S_hat.device());
@@ -1589,8 +1671,13 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
   } else {
     r_t = at::empty({rows_t, R}, r_s.options());
   }
+  TORCH_CHECK(joint_out || !planes.has_value() || !planes->defined(),
+              "dense_softmax_transport: planes need joint_out");
   if (B == 0) {
-    if (joint_out) joint.narrow(0, 0, rows_s).copy_(r_s);
+    if (joint_out) {
+      joint.narrow(0, 0, rows_s).copy_(r_s);
+      joint_planes_fill(planes, joint);
+    }
     return {S, joint_out ? joint : r_t};
   }
   if (fast_step_ok(R, {&r_s})) {
@@ -1600,6 +1687,7 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
                   joint_out ? vp(joint) : nullptr, vp(r_t), B, Ns,
                   Nt, (int)rows_s, (int)rows_t};
     a.f32 = r_s.scalar_type() == at::kFloat;
+    if (joint_out) a.planes = joint_planes(planes, joint);
     step_fwd<false, true>(R, a);
     return {S, joint_out ? joint : r_t};
   }
@@ -1618,6 +1706,7 @@ std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
                        (int)rows_s, vec);
   });
   DGMC_CHECK_LAUNCH();
+  if (joint_out) joint_planes_fill(planes, joint);
   return {S, joint_out ? joint : r_t};
 }
 
@@ -1825,7 +1914,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
     const at::Tensor& S_hat, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
     const at::Tensor& r_s, const at::Tensor& ptr_s, const at::Tensor& ptr_t,
-    int64_t rows_t) {
+    int64_t rows_t, const c10::optional<at::Tensor>& planes) {
   check_pair_tensor(S_hat, "S_hat");
   check_packed(P, "P");
   check_packed(Q, "Q");
@@ -1850,6 +1939,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
   if (B == 0) {
     joint.narrow(0, 0, rows_s).copy_(r_s);
     joint.narrow(0, rows_s, rows_t).zero_();
+    joint_planes_fill(planes, joint);
     return {S_new, S_prob, joint};
   }
   const int vec_pq = (rows_vec_ok(P) && rows_vec_ok(Q)) ? 1 : 0;
@@ -1867,6 +1957,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
                   vp(joint.narrow(0, rows_s, rows_t)), B, Ns, Nt, (int)rows_s,
                   (int)rows_t};
     a.f32 = P.scalar_type() == at::kFloat;
+    a.planes = joint_planes(planes, joint);
     step_fwd<true, true>(R, a);
     return {S_new, S_prob, joint};
   }
@@ -1888,6 +1979,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
                      (int)rows_s, (int)rows_t, vec_pq, vec_r);
   });
   DGMC_CHECK_LAUNCH();
+  joint_planes_fill(planes, joint);
   return {S_new, S_prob, joint};
 }
 

@@ -73,7 +73,8 @@ at::Tensor dense_masked_softmax_bwd(const at::Tensor& S, const at::Tensor& G,
                                     const at::Tensor& n_t);
 std::tuple<at::Tensor, at::Tensor> dense_softmax_transport(
     const at::Tensor& S_hat, const at::Tensor& r_s, const at::Tensor& ptr_s,
-    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out);
+    const at::Tensor& ptr_t, int64_t rows_t, bool joint_out,
+    const c10::optional<at::Tensor>& planes);
 at::Tensor dense_softmax_transport_bwd(const at::Tensor& S,
                                        const at::Tensor& r_s,
                                        const at::Tensor& g,
@@ -240,7 +241,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> dense_consensus_transport(
     const at::Tensor& S_hat, const at::Tensor& P, const at::Tensor& Q,
     const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
     const at::Tensor& r_s, const at::Tensor& ptr_s, const at::Tensor& ptr_t,
-    int64_t rows_t);
+    int64_t rows_t, const c10::optional<at::Tensor>& planes);
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor>
 dense_transport_consensus_bwd(const at::Tensor& S_prob, const at::Tensor& r_s,
                               const at::Tensor& g_t,
@@ -406,7 +407,8 @@ TORCH_LIBRARY(dgmc_amd, m) {
       "-> Tensor");
   m.def(
       "dense_softmax_transport(Tensor S_hat, Tensor r_s, Tensor ptr_s, Tensor "
-      "ptr_t, int rows_t, bool joint_out=False) -> (Tensor, Tensor)");
+      "ptr_t, int rows_t, bool joint_out=False, Tensor(a!)? planes=None) -> "
+      "(Tensor, Tensor)");
   m.def(
       "dense_softmax_transport_bwd(Tensor S, Tensor r_s, Tensor grad, Tensor "
       "ptr_s, Tensor ptr_t, Tensor? addend=None) -> Tensor");
@@ -491,7 +493,7 @@ TORCH_LIBRARY(dgmc_amd, m) {
   m.def(
       "dense_consensus_transport(Tensor S_hat, Tensor P, Tensor Q, Tensor b1, "
       "Tensor w2, Tensor b2, Tensor r_s, Tensor ptr_s, Tensor ptr_t, int "
-      "rows_t) -> (Tensor, Tensor, Tensor)");
+      "rows_t, Tensor(a!)? planes=None) -> (Tensor, Tensor, Tensor)");
   m.def(
       "dense_transport_consensus_bwd(Tensor S, Tensor r_s, Tensor g_t, "
       "Tensor? addend, Tensor P, Tensor Q, Tensor b1, Tensor w2, Tensor "

@@ -477,6 +477,11 @@ class DGMC(torch.nn.Module):
                 # backward); the fold's weight gradient flows through the
                 # tiny W1 W_f product once per step.
                 fold = self._dense_fold(steps) if joint else None
+                # psi_2's first conv on the bf16x6 slot path: the transport
+                # kernels also write the joint's operand planes.
+                planes = joint and steps > 0 and hasattr(
+                    self.psi_2, 'takes_x6_planes') and \
+                    self.psi_2.takes_x6_planes(r_all[0])
                 pending = None    # (joint, S_hat) from a fused step boundary
                 for step in range(steps):
                     mark('dgmc.consensus_step')
@@ -492,12 +497,13 @@ class DGMC(torch.nn.Module):
                         # update reads it through the transport's alias, so
                         # both gradients meet in the transport backward.
                         r_joint, S_hat = dense_ops.softmax_transport_joint(
-                            S_hat, r_s, lay_s, lay_t, passthrough=True)
+                            S_hat, r_s, lay_s, lay_t, passthrough=True,
+                            planes=planes)
                         o_s, o_t, o = refine(None, None, r_joint,
                                              features=fold is not None)
                     elif joint:
                         r_joint = dense_ops.softmax_transport_joint(
-                            S_hat, r_s, lay_s, lay_t)
+                            S_hat, r_s, lay_s, lay_t, planes=planes)
                         o_s, o_t, o = refine(None, None, r_joint,
                                              features=fold is not None)
                     else:
@@ -510,7 +516,7 @@ class DGMC(torch.nn.Module):
                                               step + 1 < steps) else None
                     res = dense_ops.consensus_update(
                         S_hat, o_s, o_t, self.mlp, lay_s, lay_t, o_joint=o,
-                        w1_fold=fold, next_r_s=nxt)
+                        w1_fold=fold, next_r_s=nxt, planes=planes)
                     if isinstance(res, tuple):
                         pending = res
                     else:

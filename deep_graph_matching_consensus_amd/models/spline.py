@@ -10,6 +10,7 @@ import torch.nn.functional as F
 from torch.nn import ModuleList
 
 from ..nn.conv import SplineConv
+from ..ops import _backend, slot_gemm
 from .encoder import StackedEncoder
 
 
@@ -32,6 +33,16 @@ class SplineCNN(StackedEncoder):
             conv.reset_parameters()
         if self.lin:
             self.final.reset_parameters()
+
+    def takes_x6_planes(self, x):
+        """Whether the first conv reads ``x`` (fp32) on the bf16x6 slot path:
+        a producer may then hand it the operand planes as well (attached as
+        ``x._dgmc_x6``; ops/slot_gemm.py)."""
+        conv = self.convs[0] if len(self.convs) else None
+        return (conv is not None and slot_gemm.X6 and
+                slot_gemm.ENABLED and x.dtype == torch.float32 and
+                conv.in_channels % 128 == 0 and conv.out_channels % 128 == 0
+                and _backend.use_hip(x))
 
     def forward(self, x, edge_index, edge_attr, *args):
         xs = [x]

@@ -330,10 +330,13 @@ class _SoftmaxTransportJoint(torch.autograd.Function):
     backward kernel instead of by a separate autograd add."""
 
     @staticmethod
-    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t, passthrough=False):
+    def forward(ctx, S_hat, r_s, ptr_s, ptr_t, rows_t, passthrough=False,
+                planes=False):
+        r_s = r_s.contiguous()
+        pl = _joint_planes(r_s, rows_t) if planes else None
         S, joint = _backend.ops().dense_softmax_transport(
-            S_hat.float().contiguous(), r_s.contiguous(), ptr_s, ptr_t,
-            rows_t, True)
+            S_hat.float().contiguous(), r_s, ptr_s, ptr_t, rows_t, True, pl)
+        _attach_planes(joint, pl)
         ctx.save_for_backward(S, r_s, ptr_s, ptr_t)
         ctx.dtype = S_hat.dtype
         ctx.n_s = r_s.size(0)
@@ -354,7 +357,23 @@ class _SoftmaxTransportJoint(torch.autograd.Function):
         g = g.to(ctx.dtype)
         if gpass is not None and add is None:
             g = g + gpass
-        return g, None, None, None, None, None
+        return g, None, None, None, None, None, None
+
+
+def _joint_planes(r_s, rows_t):
+    """bf16x6 planes buffer ``[3, rows_s + rows_t, R]`` for the joint
+    ``[r_s; r_t]`` (written by the transport kernel), or None when the joint
+    is not fp32."""
+    if r_s.dtype != torch.float32 or r_s.size(1) % 4 != 0:
+        return None
+    return torch.empty((3, r_s.size(0) + rows_t, r_s.size(1)),
+                       dtype=torch.bfloat16, device=r_s.device)
+
+
+def _attach_planes(joint, planes):
+    # (the record psi_2's first slot conv checks: shape and version of x)
+    if planes is not None:
+        joint._dgmc_x6 = (planes, joint._version)
 
 
 def transport_joint_supported(S_hat, lay_s, lay_t):
@@ -362,13 +381,16 @@ def transport_joint_supported(S_hat, lay_s, lay_t):
     return _hip_ok(S_hat, N_s, N_t)
 
 
-def softmax_transport_joint(S_hat, r_s, lay_s, lay_t, passthrough=False):
+def softmax_transport_joint(S_hat, r_s, lay_s, lay_t, passthrough=False,
+                            planes=False):
     r"""``[r_s; masked_softmax(S_hat)^T r_s]`` as one packed
     ``[sum N_s + sum N_t, R]`` tensor (differentiable w.r.t. ``S_hat``).
     ``passthrough`` returns ``(joint, S_hat')`` with ``S_hat'`` an alias of
-    ``S_hat`` whose gradient is summed inside this op's backward kernel."""
+    ``S_hat`` whose gradient is summed inside this op's backward kernel.
+    ``planes``: the consumer is a bf16x6 slot conv - the kernel also writes
+    the joint's operand planes (fp32; attached to ``joint``)."""
     return _SoftmaxTransportJoint.apply(S_hat, r_s, lay_s.ptr, lay_t.ptr,
-                                        lay_t.num_nodes, passthrough)
+                                        lay_t.num_nodes, passthrough, planes)
 
 
 def softmax_transport(S_hat, r_s, lay_s, lay_t):
@@ -444,12 +466,15 @@ class _ConsensusTransport(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, S_hat, PQ, split, b1, w2, b2, r_s, ptr_s, ptr_t, rows_t,
-                loop):
+                loop, planes=False):
         P, Q = PQ[:split], PQ[split:]
+        r_s = r_s.contiguous()
+        pl = _joint_planes(r_s, rows_t) if planes else None
         S_new, S_prob, joint = _backend.ops().dense_consensus_transport(
             S_hat.float().contiguous(), P, Q, b1.float().contiguous(),
             w2.float().contiguous().view(-1), b2.float().contiguous().view(-1),
-            r_s.contiguous(), ptr_s, ptr_t, rows_t)
+            r_s, ptr_s, ptr_t, rows_t, pl)
+        _attach_planes(joint, pl)
         ctx.save_for_backward(S_prob, r_s, P, Q, b1, w2, ptr_s, ptr_t)
         ctx.meta = (S_hat.dtype, b1.dtype, w2.dtype, b2.dtype, b2.shape)
         ctx.n_s = r_s.size(0)
@@ -485,7 +510,7 @@ class _ConsensusTransport(torch.autograd.Function):
             dw2 = dw2.view_as(w2).to(w2_dt)
             db2 = db2.view(b2_shape).to(b2_dt)
         return (G.to(s_dt), dPQ, None, db1, dw2, db2, None, None, None, None,
-                None)
+                None, None)
 
 
 def _loop_part(loop, B, R, device):
@@ -767,7 +792,7 @@ def cat_matmul_f32(parts, w_t, key, total):
 
 
 def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
-                     w1_fold=None, next_r_s=None):
+                     w1_fold=None, next_r_s=None, planes=False):
     r"""``S_hat + mask * mlp(o_s[:, :, None] - o_t[:, None])`` for packed
     ``o_s [sum N_s, R]`` / ``o_t [sum N_t, R]``.  ``o_joint`` may pass the
     concatenation ``[o_s; o_t]`` (fused encoder output) to compute both
@@ -775,6 +800,8 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
     Lin(R, 1))`` (``dgmc.py:74-78``).  ``w1_fold = (W^T, lp_cache, key)``
     replaces ``W1^T`` by a folded ``[K, R]`` map applied to ``o_joint``
     (the encoder's pre-projection features; see ``DGMC._forward``).
+    ``next_r_s`` / ``planes``: see :class:`_ConsensusTransport` /
+    :func:`softmax_transport_joint`.
     """
     lin1, lin2 = mlp[0], mlp[2]
     B, N_s, N_t = S_hat.shape
@@ -803,7 +830,7 @@ def consensus_update(S_hat, o_s, o_t, mlp, lay_s, lay_t, o_joint=None,
             return _ConsensusTransport.apply(
                 S_hat, PQ, lay_s.num_nodes, lin1.bias, lin2.weight,
                 lin2.bias, next_r_s, lay_s.ptr, lay_t.ptr,
-                lay_t.num_nodes, loop)
+                lay_t.num_nodes, loop, planes)
         return _ConsensusUpdate.apply(S_hat, PQ, lay_s.num_nodes, lin1.bias,
                                       lin2.weight, lin2.bias, lay_s.ptr,
                                       lay_t.ptr, loop)

@@ -1606,6 +1606,91 @@ def test_step_kernels_split_vs_fp32(R, Ns, Nt, B):
     torch.testing.assert_close(g, ref['gS'], atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize('R', [32, 128, 48])
+@pytest.mark.parametrize('Ns,Nt,B', [(19, 23, 37), (9, 9, 300)])
+def test_step_joint_planes_equal_split3(R, Ns, Nt, B):
+    """The joint [r_s; r_t]'s bf16x6 planes written by the transport kernels
+    (psi_2's slot-conv operand) == split3 of the joint, every row (incl. the
+    static-batch padding rows; R = 48: the generic kernels' fill path)."""
+    ops = _backend.ops()
+    d = _step_problem(R, Ns, Nt, B, torch.float32)
+    rows = d['rows_s'] + d['rows_t']
+
+    def fresh():
+        return torch.full((3, rows, R), float('nan'), dtype=torch.bfloat16,
+                          device=DEV)
+    pl = fresh()
+    _, _, joint = ops.dense_consensus_transport(
+        d['S_hat'], d['P'], d['Q'], d['b1'], d['w2'], d['b2'], d['r_s'],
+        d['ps'], d['pt'], d['rows_t'], pl)
+    _, _, ref = ops.dense_consensus_transport(
+        d['S_hat'], d['P'], d['Q'], d['b1'], d['w2'], d['b2'], d['r_s'],
+        d['ps'], d['pt'], d['rows_t'])
+    assert torch.equal(joint, ref)
+    assert torch.equal(pl, ops.split3(joint))
+    pl = fresh()
+    _, joint = ops.dense_softmax_transport(d['S_hat'], d['r_s'], d['ps'],
+                                           d['pt'], d['rows_t'], True, pl)
+    assert torch.equal(pl, ops.split3(joint))
+
+
+def test_joint_planes_model_bit_identical(monkeypatch):
+    """fp32 DGMC (dense, SplineCNN psi_2): psi_2's first conv reading the
+    transport kernels' planes gives bit-identical loss and gradients to the
+    split pass."""
+    from deep_graph_matching_consensus_amd.datasets import (
+        GraphStore, make_keypoint_datasets)
+    from deep_graph_matching_consensus_amd.datasets.static_batch import \
+        StaticPairBatcher
+    from deep_graph_matching_consensus_amd.models import DGMC, SplineCNN
+    from deep_graph_matching_consensus_amd.ops import slot_gemm
+    groups = make_keypoint_datasets(graphs=16, feature_dim=32, seed=6)
+    store = GraphStore(groups, torch.device(DEV))
+    batcher = StaticPairBatcher(store, 48, seed=4)
+    torch.manual_seed(0)
+    model = DGMC(SplineCNN(32, 128, 2, 2, cat=False),
+                 SplineCNN(128, 128, 2, 2, cat=False), num_steps=4).to(DEV)
+    assert batcher.load()
+    batch = batcher.materialize()
+    assert model.psi_2.takes_x6_planes(batch.x_s.new_zeros(1, 128))
+    split_calls = []
+    real_split = _backend.ops().split3
+
+    class _Spy(object):
+        def __getattr__(self, name):
+            if name == 'split3':
+                def f(*a):
+                    split_calls.append(tuple(a[0].shape))
+                    return real_split(*a)
+                return f
+            return getattr(torch.ops.dgmc_amd, name)
+
+    def run():
+        torch.manual_seed(1)
+        loss, count, correct = model.objective(
+            batch.x_s, batch.edge_index_s, batch.edge_attr_s,
+            batch.x_s_batch, batch.x_t, batch.edge_index_t,
+            batch.edge_attr_t, batch.x_t_batch, batch.y, batch.y_mask)
+        return loss.detach(), torch.autograd.grad(
+            loss, list(model.parameters()), allow_unused=True)
+    orig = _backend.ops
+    monkeypatch.setattr(_backend, 'ops', lambda: _Spy())
+    l1, g1 = run()
+    n1 = len(split_calls)
+    monkeypatch.setattr(SplineCNN, 'takes_x6_planes', lambda self, x: False)
+    l0, g0 = run()
+    n0 = len(split_calls) - n1
+    monkeypatch.setattr(_backend, 'ops', orig)
+    if slot_gemm.F32X:
+        assert n0 - n1 == 4, (n0, n1)   # one split per psi_2 call saved
+    assert torch.equal(l1, l0)
+    for a, b in zip(g1, g0):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize('U,N,K', [(10, 1000, 384), (3, 77, 128),
                                    (17, 300, 256)])
 def test_dense_wgrad_matches_fp32(U, N, K):
