@@ -467,6 +467,27 @@ def test_topk_dot_split_merge(Ns, Nt):
     assert (a == b).float().mean().item() > 0.99
 
 
+@pytest.mark.parametrize('B,Ns,Nt,C', [(1, 3000, 9000, 256),
+                                        (2, 1000, 4000, 128),
+                                        (1, 4900, 6001, 256),
+                                        (3, 300, 2000, 64)])
+def test_topk_split_shapes(B, Ns, Nt, C):
+    """The filter on split target ranges of several shapes (batches, C =
+    64 / 128 / 256, row blocks that do not fill the chip): exact selection
+    == brute force, the split-bf16 one within its score tolerance."""
+    torch.manual_seed(B + Ns)
+    h_s = torch.randn(B, Ns, C, device=DEV)
+    h_t = torch.randn(B, Nt, C, device=DEV)
+    want = sparse_corr.top_k(h_s, h_t, 10, brute_force=True)
+    assert torch.equal(sparse_corr.top_k(h_s, h_t, 10), want)
+    got = sparse_corr.top_k(h_s, h_t, 10, exact=False)
+    assert (got >= 0).all() and (got < Nt).all()
+    scores = h_s @ h_t.transpose(-1, -2)
+    torch.testing.assert_close(torch.gather(scores, -1, got),
+                               torch.gather(scores, -1, want), atol=4e-3,
+                               rtol=0)
+
+
 def test_dgmc_dense_hip_vs_reference_mode():
     from deep_graph_matching_consensus_amd.datasets import (
         GraphStore, DevicePairLoader, make_keypoint_datasets)
