@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
-# Top-k insertion rounds by the sorted-prefix test (no ballot / popcount)
-# vs the ballot form (TK_AB_OLD=1, a temporary host hook): tests + A/B.
+# Top-k A/B through a temporary host hook (TK_AB_OLD=1: the previous
+# kernel); first use: sorted-prefix insertion test, second: tile pre-check
+# only in warm mode.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
