@@ -234,7 +234,10 @@ __device__ __forceinline__ void x3_bitonic32(float& v, int& ix, int hl,
 
 // Tiles (from the first) whose lists are updated by sort + merge instead of
 // insertion rounds (the rounds win once few scores of a tile still enter).
-constexpr int kX3MergeTiles = 4;
+// Same-box sweeps (tools/gpu_r6_ac.sh, gpu_r6_aj.sh): 4 with the first
+// insertion rounds; 2 since the rounds got cheaper (1.12-1.14 ms against
+// 1.15 at 4, 1.14 at 1, 1.14 at 3, 1.18 at 6).
+constexpr int kX3MergeTiles = 2;
 
 template <int NKS, int W>
 __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
