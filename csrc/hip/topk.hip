@@ -178,8 +178,10 @@ __device__ __forceinline__ float lane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-__device__ __forceinline__ int shr1(int v) {   // v of lane - 1 (DPP)
-  return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+// v of lane - 1 (DPP wave_shr:1); lane 0's result is undefined (no "old"
+// operand to materialise: the callers never use it).
+__device__ __forceinline__ int shr1(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, false);
 }
 __device__ __forceinline__ float shr1(float v) {
   return __int_as_float(shr1(__float_as_int(v)));
@@ -260,6 +262,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
   const int tid = threadIdx.x, wave = tid / kWave, lane = tid % kWave;
   const int h = lane >> 5, hl = lane & 31, hb = lane & 32;
   const bool in_list = hl < k;
+  // the list lanes of both halves as a ballot mask
+  const unsigned long long in_mask =
+      (((1ull << k) - 1ull) << 32) | ((1ull << k) - 1ull);
   const int row0 = blockIdx.x * (32 * W) + wave * 32;
   const int j_begin = split * span;
   const int j_end = min(Nt, j_begin + span);
@@ -500,7 +505,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
           hi ^= 1u << s1;
         }
         const float cv = hb ? cv1 : cv0;
-        const unsigned long long bm = __ballot(in_list && lv[r] >= cv);
+        // (list lanes masked in scalar: a ballot of a compound condition
+        // is materialised through a VGPR first)
+        const unsigned long long bm = __ballot(lv[r] >= cv) & in_mask;
         const int pos =
             hb ? __popc((unsigned)(bm >> 32)) : __popc((unsigned)bm);
         // shift the tail of the half's list down one lane (DPP wave_shr:1;
