@@ -482,15 +482,16 @@ __global__ __launch_bounds__(64 * W, 8 / W) void topk_x3_kernel(
       // One candidate of each half-wave per round (the halves hold
       // different rows): max(hits_lo, hits_hi) rounds, not their sum.
       // (Interleaving two rows' rounds measured slower: 1.27 -> 1.39 ms.)
+      // Scalar picks; an exhausted half proposes -inf, which its whole
+      // list outranks (no insertion).  No threshold test per round: a
+      // candidate that no longer beats the k-th entry ranks at pos = k and
+      // changes nothing, so the threshold is re-read once per row, after
+      // its rounds.  Branch-free list update (selects, no exec-mask
+      // branches).  ~20 vector instructions a round against ~40 before
+      // (hipcc -S; same-box filter 1.277 -> 1.196 ms, tools/gpu_r6_af.sh,
+      // then 1.12 -> 1.08 ms for the ballot mask and DPP form,
+      // tools/gpu_r6_ah.sh).
       unsigned lo = (unsigned)mask, hi = (unsigned)(mask >> 32);
-      // One round per candidate of each half (scalar picks; an exhausted
-      // half proposes -inf, which its whole list outranks: no insertion).
-      // No threshold test per round: a candidate that no longer beats the
-      // k-th entry ranks at pos = k and changes nothing, so the threshold
-      // is re-read once per row, after its rounds.  The list update is
-      // branch-free (selects, no exec-mask branches): ~22 instead of ~40
-      // vector instructions a round (hipcc -S), filter 1.277 -> 1.196 ms
-      // (same box, tools/gpu_r6_af.sh).
       while (lo | hi) {
         float cv0 = -INFINITY, cv1 = -INFINITY;
         int s0 = 0, s1 = 0;
