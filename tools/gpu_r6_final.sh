@@ -4,7 +4,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r6final; mkdir -p $O
+O=gpurun_out/${R6FINAL_DIR:-r6final}; mkdir -p $O
 run() {  # run <name> <timeout> cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name ($(date +%T))"
