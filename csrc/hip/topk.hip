@@ -212,6 +212,17 @@ __global__ __launch_bounds__(256) void split_bf16_kernel(
   *reinterpret_cast<bf16x4*>(lo + r * CP + c) = vl;
 }
 
+// Lane l ^ jj's value (jj = 1, 2, 4, 8 or 16, a constant after unrolling):
+// DPP within the 16-lane row for 1, 2 (quad_perm) and 8 (row_ror:8), the
+// LDS crossbar (ds_bpermute) otherwise.  (Same-box A/B, tools/gpu_r6_ah.sh:
+// cold filter 1.077 -> 1.066 ms.)
+__device__ __forceinline__ int xor_lane(int v, int jj) {
+  if (jj == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false);
+  if (jj == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false);
+  if (jj == 8) return __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false);
+  return __shfl_xor(v, jj);
+}
+
 // Bitonic sort of (v, ix) over the 32 lanes of each half-wave into (value
 // desc, index asc) order, from stage k2 = k2_0 (2: a full sort; 32: only the
 // final merge of a bitonic sequence).
@@ -222,8 +233,8 @@ __device__ __forceinline__ void x3_bitonic32(float& v, int& ix, int hl,
     if (k2 < k2_0) continue;
 #pragma unroll
     for (int jj = k2 >> 1; jj > 0; jj >>= 1) {
-      const float pv = __shfl_xor(v, jj);
-      const int pix = __shfl_xor(ix, jj);
+      const float pv = __int_as_float(xor_lane(__float_as_int(v), jj));
+      const int pix = xor_lane(ix, jj);
       const bool better = v > pv || (v == pv && ix < pix);
       const bool desc = (hl & k2) == 0, lower = (hl & jj) == 0;
       if ((lower == desc) != better) {

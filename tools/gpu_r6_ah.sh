@@ -2,7 +2,8 @@
 # Top-k A/B through a temporary host hook (TK_AB_OLD=1: the previous
 # kernel); first use: sorted-prefix insertion test, second: tile pre-check
 # only in warm mode, third: column mask applied to the votes once a tile,
-# fourth: DPP shifts without an "old" operand + ballot masked in scalar.
+# fourth: DPP shifts without an "old" operand + ballot masked in scalar,
+# fifth: bitonic partner exchanges by DPP for lane distances 1, 2, 8.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
